@@ -1,0 +1,153 @@
+/*
+ * statecatcher.h — C ABI of libstatecatcher_hip.so, the MI355X (gfx950) hot path of the
+ * stateful recurrent ASR step (LucyRNN scan fwd/bwd, decay scan, CTC alpha-beta, greedy
+ * CTC decode).
+ *
+ * Every entry point takes plain device pointers, element counts/strides (in ELEMENTS, as the
+ * reference's Triton launches do) and a hipStream_t passed as void*.  No torch types cross
+ * this boundary.  All calls are asynchronous on `stream` and never synchronise the host.
+ *
+ * Return value: 0 on success; SC_EINVAL (-1) for an invalid argument (message in
+ * sc_last_error()); a positive hipError_t if the launch failed.
+ *
+ * Reference interfaces replaced (paths under speechcatcher-asr/statecatcher):
+ *   sc_lucy_scan_fwd  <- lucyrnn_triton.py:179-244 `rnn_forward_unfused_rmsnorm`,
+ *                        launched at lucyrnn_triton.py:61-73 with grid (B, D)
+ *   sc_lucy_scan_bwd  <- (absent in the reference) adjoint of the above
+ *   sc_decay_scan_fwd <- lucyrnn_triton.py:158-177 `fused_decay_scan`, launched at
+ *                        lucyrnn.py:147-151; generalised with an optional initial state
+ *   sc_decay_scan_bwd <- (absent) adjoint of the above
+ *   sc_ctc_*          <- ATen ctc_loss behind nn.CTCLoss(blank=0, zero_infinity=True),
+ *                        train.py:142 / model.py:68-71
+ *   sc_ctc_greedy_decode <- decoder.py:3-30 `ctc_greedy_decoder`
+ */
+#ifndef STATECATCHER_H
+#define STATECATCHER_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SC_EINVAL (-1)
+
+/* element types of floating tensors crossing the ABI */
+#define SC_F32 0
+#define SC_BF16 1
+#define SC_F16 2
+
+/* ABI version; bumped on any signature change */
+int sc_abi_version(void);
+
+/* Message for the last SC_EINVAL / launch failure on this thread ("" if none). */
+const char* sc_last_error(void);
+
+/* ---------------------------------------------------------------- LucyRNN scan ---------- */
+
+/* Time steps per checkpointed super-chunk (state saved at each super-chunk start). */
+int sc_lucy_scan_chunk(void);
+
+/* Floats needed for the forward->backward state checkpoint: B * ceil(T/chunk) * 2 * D. */
+int64_t sc_lucy_scan_ckpt_numel(int B, int T, int D);
+
+/*
+ * Forward scan.  Mirrors rnn_forward_unfused_rmsnorm(gates_ptr, h0_ptr, s0_ptr, out_ptr,
+ * s_out_ptr, B, T, D, stride_g_bt, stride_g_td, stride_g_cd, stride_o_bt, stride_o_bd)
+ * (lucyrnn_triton.py:180-194).
+ *   gates  [B,T,7,D] of gates_dtype, d-stride 1, gate order r,z,k,v,h_pre,decay,alpha
+ *   h0,s0  [B,D] fp32 contiguous (read exactly as contiguous; the caller must not pass the
+ *          strided out[:, -1] view the reference passes — SURVEY F3)
+ *   out    [B,T,D] of gates_dtype, d-stride 1 (strides stride_o_bt, stride_o_bd)
+ *   s_out  [B,D] fp32 contiguous: state after the last step
+ *   ckpt   NULL, or sc_lucy_scan_ckpt_numel() floats: (s,h) at every super-chunk start,
+ *          consumed by sc_lucy_scan_bwd (training)
+ * State arithmetic is fp32 for every gates_dtype.
+ */
+int sc_lucy_scan_fwd(const void* gates, int gates_dtype, const float* h0, const float* s0,
+                     void* out, float* s_out, int B, int T, int D,
+                     int64_t stride_g_bt, int64_t stride_g_td, int64_t stride_g_cd,
+                     int64_t stride_o_bt, int64_t stride_o_bd, float* ckpt, void* stream);
+
+/*
+ * Backward scan.  Inputs: the forward's gates and ckpt, dout = dL/d out (same dtype as gates,
+ * strides stride_d_bt/stride_d_bd), ds_last = dL/d s_out (fp32 [B,D], may be NULL = zero).
+ * Outputs: dgates (gates_dtype, strides stride_dg_*), dh0, ds0 (fp32 [B,D]).
+ */
+int sc_lucy_scan_bwd(const void* gates, int gates_dtype, const float* ckpt,
+                     const void* dout, const float* ds_last,
+                     void* dgates, float* dh0, float* ds0, int B, int T, int D,
+                     int64_t stride_g_bt, int64_t stride_g_td, int64_t stride_g_cd,
+                     int64_t stride_d_bt, int64_t stride_d_bd,
+                     int64_t stride_dg_bt, int64_t stride_dg_td, int64_t stride_dg_cd,
+                     void* stream);
+
+/* ---------------------------------------------------------------- decay scan ------------ */
+
+/*
+ * s_t = decay_t * s_{t-1} + kv_t with s_{-1} = init (init NULL -> 0, as fused_decay_scan).
+ * Mirrors fused_decay_scan(kv_ptr, decay_ptr, output_ptr, B, T, D, stride_b, stride_t,
+ * stride_d) (lucyrnn_triton.py:159-163); kv, decay and out share the strides, stride_d == 1.
+ * init: fp32 [B,D] contiguous or NULL.  Accumulation fp32 (lucyrnn_triton.py:171).
+ */
+int sc_decay_scan_fwd(const void* kv, const void* decay, void* out, int dtype,
+                      const float* init, int B, int T, int D,
+                      int64_t stride_b, int64_t stride_t, int64_t stride_d, void* stream);
+
+/*
+ * Adjoint: g_t = dout_t + decay_{t+1} g_{t+1};  dkv_t = g_t;  ddecay_t = g_t * s_{t-1}
+ * (s_{-1} = init).  s_all is the forward output.  dinit (fp32 [B,D]) may be NULL.
+ */
+int sc_decay_scan_bwd(const void* decay, const void* s_all, const void* dout, void* dkv,
+                      void* ddecay, int dtype, const float* init, float* dinit,
+                      int B, int T, int D, int64_t stride_b, int64_t stride_t, int64_t stride_d,
+                      void* stream);
+
+/* ---------------------------------------------------------------- CTC ------------------- */
+
+/* Workspace bytes for sc_ctc_fwd / sc_ctc_bwd (alpha, beta, row log-sum-exp, label chains). */
+size_t sc_ctc_workspace_bytes(int B, int T, int max_target_len);
+
+/*
+ * CTC forward over x [B,T,V] (x_dtype, v-stride 1, strides stride_b/stride_t):
+ *   is_logits = 1: x are logits, log_softmax is fused (model.py:70 + ATen ctc_loss);
+ *   is_logits = 0: x are log-probabilities (the nn.CTCLoss input convention).
+ * targets: int64 [B, max_target_len] padded (train.py:208), row stride target_stride;
+ * in_lens/tgt_lens: int64 [B] device arrays.  Writes nll [B] fp32 (+inf when infeasible;
+ * the zero_infinity reduction is the caller's) and fills the workspace for sc_ctc_bwd.
+ */
+int sc_ctc_fwd(const void* x, int x_dtype, int is_logits, int B, int T, int V,
+               int64_t stride_b, int64_t stride_t,
+               const int64_t* targets, int64_t target_stride, int max_target_len,
+               const int64_t* in_lens, const int64_t* tgt_lens, int blank,
+               float* nll, void* workspace, size_t workspace_bytes, void* stream);
+
+/*
+ * CTC backward: grad [B,T,V] (grad_dtype, contiguous) =
+ *   scale[b] * (exp(lp) - exp(lcab + nll - lp))  for t < in_len[b], 0 otherwise,
+ * ATen's formula; with is_logits = 1 it is the gradient w.r.t. the logits.  scale: fp32 [B]
+ * (dL/dnll_b, already zero where the loss was zeroed).
+ */
+int sc_ctc_bwd(const void* x, int x_dtype, int is_logits, int B, int T, int V,
+               int64_t stride_b, int64_t stride_t,
+               const int64_t* targets, int64_t target_stride, int max_target_len,
+               const int64_t* in_lens, const int64_t* tgt_lens, int blank,
+               const float* nll, const float* scale, void* grad, int grad_dtype,
+               const void* workspace, size_t workspace_bytes, void* stream);
+
+/* ---------------------------------------------------------------- greedy decode --------- */
+
+/*
+ * decoder.py:3-30 on device: argmax over V (first maximal index; NaN counts as maximal,
+ * as torch.argmax), trim to lengths[b], collapse repeats, drop blank.
+ * tokens: int32 [B,T] (first counts[b] entries valid), counts: int32 [B].
+ */
+int sc_ctc_greedy_decode(const void* log_probs, int dtype, int B, int T, int V,
+                         int64_t stride_b, int64_t stride_t, const int64_t* lengths, int blank,
+                         int32_t* tokens, int32_t* counts, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* STATECATCHER_H */

@@ -1,0 +1,122 @@
+"""Pin the CPU oracle against fixtures produced by the reference itself (CPU, no GPU)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import ctc as octc
+from oracle import decode as odec
+from oracle import lucy_scan as oscan
+from tests.conftest import cases, load_golden
+
+
+@pytest.mark.parametrize("name", cases(load_golden("scan_fwd"), "gates"))
+def test_scan_fwd_vs_reference_triton(name):
+    z = load_golden("scan_fwd")
+    out, s = oscan.lucy_scan_fwd(z[name + "/gates"], z[name + "/h0"], z[name + "/s0"])
+    ref_out = z[name + "/out"]
+    ref_s = z[name + "/s_out"]
+    # reference kernel is fp32: 1e-3 relative (north_star tolerance) with a small abs floor
+    np.testing.assert_allclose(out, ref_out, rtol=1e-3, atol=1e-5)
+    np.testing.assert_allclose(s, ref_s, rtol=1e-3, atol=1e-4 * max(1.0, np.abs(ref_s).max()) * 1e-2)
+
+
+def test_scan_fwd_fp32_oracle_matches_reference_tightly():
+    z = load_golden("scan_fwd")
+    out, s = oscan.lucy_scan_fwd(z["realistic/gates"], z["realistic/h0"], z["realistic/s0"],
+                                 dtype=np.float32)
+    np.testing.assert_allclose(out, z["realistic/out"], rtol=2e-5, atol=2e-6)
+
+
+def test_scan_carry_contiguous_and_aliasing_bug_documented():
+    z = load_golden("scan_fwd")
+    out1, s1 = oscan.lucy_scan_fwd(z["carry/g1"], np.zeros((3, 16)), np.zeros((3, 16)))
+    np.testing.assert_allclose(out1, z["carry/out1"], rtol=1e-4, atol=1e-6)
+    out2, s2 = oscan.lucy_scan_fwd(z["carry/g2"], out1[:, -1], s1)
+    np.testing.assert_allclose(out2, z["carry/out2_contig"], rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(s2, z["carry/s2_contig"], rtol=1e-4, atol=1e-5)
+    # the reference's strided h0 view corrupts rows b >= 1 but not b = 0
+    alias = z["carry/out2_aliased"]
+    np.testing.assert_allclose(alias[0], z["carry/out2_contig"][0], rtol=1e-6)
+    assert np.abs(alias[1:] - z["carry/out2_contig"][1:]).max() > 1e-3
+
+
+@pytest.mark.parametrize("name", cases(load_golden("scan_bwd"), "dgates"))
+def test_scan_bwd_vs_autograd(name):
+    zf = load_golden("scan_fwd")
+    zb = load_golden("scan_bwd")
+    g, h0, s0 = zf[name + "/gates"], zf[name + "/h0"], zf[name + "/s0"]
+    dg, dh0, ds0 = oscan.lucy_scan_bwd(g, h0, s0, zb[name + "/dout"], zb[name + "/ds_last"])
+    ref = zb[name + "/dgates"]
+    scale = np.abs(ref).max()
+    np.testing.assert_allclose(dg, ref, rtol=1e-7, atol=1e-9 * scale)
+    np.testing.assert_allclose(dh0, zb[name + "/dh0"], rtol=1e-7, atol=1e-12)
+    np.testing.assert_allclose(ds0, zb[name + "/ds0"], rtol=1e-7, atol=1e-12)
+
+
+def test_scan_bwd_autograd_forward_matches_reference():
+    """The fp64 restatement that produced the bwd fixtures agrees with the reference forward."""
+    zf = load_golden("scan_fwd")
+    zb = load_golden("scan_bwd")
+    for name in cases(zb, "dgates"):
+        np.testing.assert_allclose(zb[name + "/out64"], zf[name + "/out"], rtol=1e-3, atol=1e-5)
+
+
+@pytest.mark.parametrize("name", ["small", "t1"])
+def test_decay_scan_vs_reference_triton(name):
+    z = load_golden("decay_scan")
+    s = oscan.decay_scan(z[name + "/kv"], z[name + "/decay"])
+    np.testing.assert_allclose(s, z[name + "/s_all"], rtol=1e-6, atol=1e-6)
+
+
+def test_decay_scan_bwd_vs_autograd():
+    rng = np.random.default_rng(0)
+    kv = rng.standard_normal((2, 17, 5))
+    dec = 1 / (1 + np.exp(-rng.standard_normal((2, 17, 5))))
+    dout = rng.standard_normal((2, 17, 5))
+    tk = torch.tensor(kv, requires_grad=True)
+    td = torch.tensor(dec, requires_grad=True)
+    s = torch.zeros(2, 5, dtype=torch.float64)
+    outs = []
+    for t in range(17):
+        s = td[:, t] * s + tk[:, t]
+        outs.append(s)
+    (torch.stack(outs, 1) * torch.tensor(dout)).sum().backward()
+    s_all = oscan.decay_scan(kv, dec, dtype=np.float64)
+    dkv, ddec = oscan.decay_scan_bwd(dec, s_all, dout)
+    np.testing.assert_allclose(dkv, tk.grad.numpy(), rtol=1e-10)
+    np.testing.assert_allclose(ddec, td.grad.numpy(), rtol=1e-10, atol=1e-14)
+
+
+@pytest.mark.parametrize("name", cases(load_golden("ctc"), "logits"))
+def test_ctc_vs_aten(name):
+    z = load_golden("ctc")
+    nll, grad = octc.ctc_loss_grad(z[name + "/logits"], z[name + "/targets"], z[name + "/in_lens"],
+                                   z[name + "/tgt_lens"], blank=0, logits=True)
+    ref = z[name + "/nll"]
+    fin = np.isfinite(ref)
+    assert np.array_equal(fin, np.isfinite(nll))
+    np.testing.assert_allclose(nll[fin], ref[fin], rtol=1e-10)
+    # per-sample grads (zero_infinity=True zeroes infeasible samples)
+    g = np.where(np.isfinite(nll)[:, None, None], grad, 0.0)
+    np.testing.assert_allclose(g, z[name + "/sum_grad"], rtol=1e-8, atol=1e-12)
+    # mean reduction with zero_infinity
+    loss = octc.ctc_mean_zero_inf(nll, z[name + "/tgt_lens"])
+    np.testing.assert_allclose(loss, float(z[name + "/mean_loss"]), rtol=1e-10)
+    sc = octc.ctc_mean_grad_scale(nll, z[name + "/tgt_lens"])
+    gm = np.where(np.isfinite(nll)[:, None, None], grad, 0.0) * sc[:, None, None]
+    np.testing.assert_allclose(gm, z[name + "/mean_grad"], rtol=1e-8, atol=1e-13)
+
+
+def _split(counts, flat):
+    out, o = [], 0
+    for c in counts:
+        out.append(list(flat[o:o + c]))
+        o += c
+    return out
+
+
+@pytest.mark.parametrize("pref", ["ties", "big"])
+def test_greedy_vs_reference_decoder(pref):
+    z = load_golden("greedy")
+    dec = odec.ctc_greedy(z[pref + "_lp"], z[pref + "_in_lens"], blank=0)
+    assert dec == _split(z[pref + "_counts"], z[pref + "_tokens"])
