@@ -1,0 +1,91 @@
+"""ctypes binding of libstatecatcher_hip.so (C ABI: include/statecatcher.h).
+
+The product path has no CPU fallback: every op raises if the library is missing, if a tensor is
+not on a ROCm device, or if a call returns a non-zero status.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (loads torch's HIP runtime first: our .so binds to the same SONAME)
+
+LIB_NAME = "libstatecatcher_hip.so"
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+
+SC_F32, SC_BF16, SC_F16 = 0, 1, 2
+_DTYPE = {torch.float32: SC_F32, torch.bfloat16: SC_BF16, torch.float16: SC_F16}
+
+_c = ctypes
+_i32, _i64, _vp, _fp = _c.c_int, _c.c_int64, _c.c_void_p, _c.c_void_p
+_SIGS = {
+    "sc_abi_version": (_i32, []),
+    "sc_last_error": (_c.c_char_p, []),
+    "sc_lucy_scan_chunk": (_i32, []),
+    "sc_lucy_scan_ckpt_numel": (_i64, [_i32, _i32, _i32]),
+    "sc_lucy_scan_fwd": (_i32, [_vp, _i32, _fp, _fp, _vp, _fp, _i32, _i32, _i32,
+                               _i64, _i64, _i64, _i64, _i64, _fp, _vp]),
+    "sc_lucy_scan_bwd": (_i32, [_vp, _i32, _fp, _vp, _fp, _vp, _fp, _fp, _i32, _i32, _i32,
+                               _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _vp]),
+    "sc_decay_scan_fwd": (_i32, [_vp, _vp, _vp, _i32, _fp, _i32, _i32, _i32, _i64, _i64, _i64, _vp]),
+    "sc_decay_scan_bwd": (_i32, [_vp, _vp, _vp, _vp, _vp, _i32, _fp, _fp, _i32, _i32, _i32,
+                                _i64, _i64, _i64, _vp]),
+    "sc_ctc_workspace_bytes": (_c.c_size_t, [_i32, _i32, _i32]),
+    "sc_ctc_fwd": (_i32, [_vp, _i32, _i32, _i32, _i32, _i32, _i64, _i64, _vp, _i64, _i32, _vp, _vp,
+                         _i32, _fp, _vp, _c.c_size_t, _vp]),
+    "sc_ctc_bwd": (_i32, [_vp, _i32, _i32, _i32, _i32, _i32, _i64, _i64, _vp, _i64, _i32, _vp, _vp,
+                         _i32, _fp, _fp, _vp, _i32, _vp, _c.c_size_t, _vp]),
+    "sc_ctc_greedy_decode": (_i32, [_vp, _i32, _i32, _i32, _i32, _i64, _i64, _vp, _i32, _vp, _vp, _vp]),
+}
+EXPORTED = tuple(_SIGS)
+
+_LIB = None
+
+
+def load():
+    """Load (once) and return the ctypes handle.  Raises RuntimeError if it is not built."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"statecatcher HIP library not built: {LIB_PATH} missing "
+                "(run `python -c 'import __graft_entry__ as g; g.build()'` or "
+                "`make -C statecatcher_amd/csrc`)")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        if lib.sc_abi_version() != 1:
+            raise RuntimeError("statecatcher ABI version mismatch")
+        _LIB = lib
+    return _LIB
+
+
+def check(rc, what):
+    if rc != 0:
+        msg = load().sc_last_error().decode(errors="replace")
+        if rc < 0:
+            raise ValueError(f"{what}: {msg}")
+        raise RuntimeError(f"{what}: HIP error {rc}: {msg}")
+
+
+def dtype_code(t):
+    try:
+        return _DTYPE[t.dtype]
+    except KeyError:
+        raise TypeError(f"unsupported dtype {t.dtype}; expected float32, bfloat16 or float16") from None
+
+
+def require_device(*tensors):
+    for t in tensors:
+        if t is not None and t.device.type != "cuda":
+            raise RuntimeError(
+                "statecatcher ops run only on a ROCm GPU (HIP); got a tensor on "
+                f"{t.device}. There is no CPU fallback.")
+
+
+def stream_of(t):
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None

@@ -1,0 +1,133 @@
+// Greedy CTC decoding on device, integer path bit-exact with the reference.
+//
+// Replaces decoder.py:3-30 `ctc_greedy_decoder` (torch.argmax over V, then a Python loop with
+// one .item() host sync per frame, decoder.py:24).  Two kernels:
+//   greedy_argmax_kernel   one wave per (b,t) row: first index of the maximum, a NaN counting
+//                          as the maximum (torch.argmax semantics); lanes stride the row, then a
+//                          64-lane (value, index) reduction that keeps the lower index on ties
+//   greedy_collapse_kernel one workgroup per b: keep[t] = t < len && tok != blank &&
+//                          tok != tok[t-1]; workgroup prefix sum of keep; compacted write.
+#include "sc_common.h"
+
+namespace sc {
+
+struct GreedyArgs {
+  const void* x;
+  int B, T, V, blank;
+  int64_t sb, st;
+  const int64_t* lengths;
+  int32_t* tokens;
+  int32_t* counts;
+};
+
+// a beats b?  (NaN beats everything; ties -> lower index)
+__device__ __forceinline__ bool beats(float va, int ia, float vb, int ib) {
+  const bool na = va != va, nb = vb != vb;
+  if (na || nb) return na && (!nb || ia < ib);
+  if (va != vb) return va > vb;
+  return ia < ib;
+}
+
+template <int DT>
+__global__ void __launch_bounds__(256) greedy_argmax_kernel(GreedyArgs a) {
+  using E = Elem<DT>;
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= (int64_t)a.B * a.T) return;
+  const int b = (int)(row / a.T), t = (int)(row % a.T);
+  const typename E::T* p = (const typename E::T*)a.x + (int64_t)b * a.sb + (int64_t)t * a.st;
+  float bv = -__builtin_huge_valf();
+  int bi = 0x7fffffff;
+  for (int v = lane; v < a.V; v += 64) {
+    const float xv = E::ld(p[v]);
+    if (bi == 0x7fffffff || beats(xv, v, bv, bi)) {
+      bv = xv;
+      bi = v;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(bv, o);
+    const int oi = __shfl_xor(bi, o);
+    if (oi != 0x7fffffff && (bi == 0x7fffffff || beats(ov, oi, bv, bi))) {
+      bv = ov;
+      bi = oi;
+    }
+  }
+  if (lane == 0) a.tokens[row] = bi;
+}
+
+__global__ void __launch_bounds__(1024) greedy_collapse_kernel(GreedyArgs a) {
+  extern __shared__ __attribute__((aligned(16))) int sh[];   // T predictions + 16 wave sums
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int nthr = blockDim.x;
+  int32_t* row = a.tokens + (int64_t)b * a.T;
+  int len = (int)min<int64_t>(max<int64_t>(a.lengths[b], 0), a.T);
+  for (int t = tid; t < a.T; t += nthr) sh[t] = row[t];
+  __syncthreads();
+  // each thread owns a contiguous span of steps
+  const int per = (a.T + nthr - 1) / nthr;
+  const int t0 = tid * per, t1 = min(t0 + per, len);
+  int cnt = 0;
+  for (int t = t0; t < t1; ++t) {
+    const int tok = sh[t];
+    cnt += (tok != a.blank && (t == 0 || tok != sh[t - 1])) ? 1 : 0;
+  }
+  // exclusive scan of cnt over the workgroup (wave scan + wave totals)
+  const int lane = tid & 63, wv = tid >> 6;
+  int inc = cnt;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(inc, o);
+    if (lane >= o) inc += y;
+  }
+  int* wsum = sh + a.T;
+  if (lane == 63) wsum[wv] = inc;
+  __syncthreads();
+  int base = 0;
+  for (int q = 0; q < wv; ++q) base += wsum[q];
+  int pos = base + inc - cnt;
+  for (int t = t0; t < t1; ++t) {
+    const int tok = sh[t];
+    if (tok != a.blank && (t == 0 || tok != sh[t - 1])) row[pos++] = tok;
+  }
+  if (tid == nthr - 1) a.counts[b] = base + inc;
+}
+
+template <int DT>
+static void launch(const GreedyArgs& a, hipStream_t st) {
+  const int64_t rows = (int64_t)a.B * a.T;
+  hipLaunchKernelGGL((greedy_argmax_kernel<DT>), dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, a);
+  const int nthr = 1024;
+  hipLaunchKernelGGL(greedy_collapse_kernel, dim3(a.B), dim3(nthr), (a.T + 16) * sizeof(int), st, a);
+}
+
+}  // namespace sc
+
+using namespace sc;
+
+extern "C" int sc_ctc_greedy_decode(const void* log_probs, int dtype, int B, int T, int V,
+                                    int64_t stride_b, int64_t stride_t, const int64_t* lengths,
+                                    int blank, int32_t* tokens, int32_t* counts, void* stream) {
+  clear_error();
+  SC_REQUIRE(dtype == SC_F32 || dtype == SC_BF16 || dtype == SC_F16,
+             "sc_ctc_greedy_decode: unsupported dtype %d", dtype);
+  SC_REQUIRE(B >= 0 && T >= 0 && V > 0, "sc_ctc_greedy_decode: bad shape");
+  SC_REQUIRE(T <= 16000, "sc_ctc_greedy_decode: T=%d exceeds the 16000-step LDS row", T);
+  if (B == 0) return 0;
+  SC_REQUIRE(counts && lengths, "sc_ctc_greedy_decode: null pointer");
+  SC_REQUIRE(T == 0 || (log_probs && tokens), "sc_ctc_greedy_decode: null pointer");
+  GreedyArgs a{log_probs, B, T, V, blank, stride_b, stride_t, lengths, tokens, counts};
+  hipStream_t st = (hipStream_t)stream;
+  if (T == 0) {
+    (void)hipMemsetAsync(counts, 0, sizeof(int32_t) * B, st);
+    return launch_status("sc_ctc_greedy_decode");
+  }
+  switch (dtype) {
+    case SC_F32: launch<SC_F32>(a, st); break;
+    case SC_BF16: launch<SC_BF16>(a, st); break;
+    default: launch<SC_F16>(a, st); break;
+  }
+  return launch_status("sc_ctc_greedy_decode");
+}

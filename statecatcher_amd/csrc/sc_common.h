@@ -1,0 +1,123 @@
+// Shared device helpers for the statecatcher gfx950 kernels (CDNA4, wave64).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "statecatcher.h"
+
+namespace sc {
+
+// ------------------------------------------------------------------ errors (host) ------------
+void set_error(const char* fmt, ...);
+void clear_error();
+// Converts the launch status of the kernel(s) just enqueued into the ABI return code.
+int launch_status(const char* what);
+
+#define SC_REQUIRE(cond, ...)            \
+  do {                                   \
+    if (!(cond)) {                       \
+      ::sc::set_error(__VA_ARGS__);      \
+      return SC_EINVAL;                  \
+    }                                    \
+  } while (0)
+
+// ------------------------------------------------------------------ element types ------------
+// Storage type + fp32 conversion per ABI dtype code.  Stores round to nearest-even.
+template <int DT> struct Elem;
+// ldw(): convert a raw load result held ZERO-EXTENDED in a 32-bit register.  Prefetch buffers
+// hold raw words this way on purpose: with 16-bit element types hipcc packs pairs of loaded
+// halves with v_perm right after the load, which forces an s_waitcnt on every prefetch load.
+template <> struct Elem<SC_F32> {
+  using T = float;
+  static __device__ __forceinline__ float ld(T v) { return v; }
+  static __device__ __forceinline__ float ldw(uint32_t w) { return __uint_as_float(w); }
+  static __device__ __forceinline__ T st(float f) { return f; }
+};
+template <> struct Elem<SC_BF16> {
+  // clang's native bf16: conversions lower to v_cvt_pk_bf16_f32 (RNE, NaN kept) on gfx950 and
+  // 16-bit register packing works as for _Float16.
+  using T = __bf16;
+  static __device__ __forceinline__ float ld(T v) { return (float)v; }
+  static __device__ __forceinline__ float ldw(uint32_t w) { return __uint_as_float(w << 16); }
+  static __device__ __forceinline__ T st(float f) { return (T)f; }
+};
+template <> struct Elem<SC_F16> {
+  using T = _Float16;
+  static __device__ __forceinline__ float ld(T v) { return (float)v; }
+  static __device__ __forceinline__ float ldw(uint32_t w) {
+    return (float)__builtin_bit_cast(_Float16, (uint16_t)w);
+  }
+  static __device__ __forceinline__ T st(float f) { return (T)f; }
+};
+
+// ------------------------------------------------------------------ fast math ----------------
+// Single-instruction transcendentals (v_exp_f32 / v_rcp_f32 / v_rsq_f32, ~1 ulp).
+__device__ __forceinline__ float rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+__device__ __forceinline__ float rsq(float x) { return __builtin_amdgcn_rsqf(x); }
+__device__ __forceinline__ float exp2_(float x) { return __builtin_amdgcn_exp2f(x); }
+__device__ __forceinline__ float log2_(float x) { return __builtin_amdgcn_logf(x); }
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kLn2 = 0.6931471805599453f;
+__device__ __forceinline__ float fexp(float x) { return exp2_(x * kLog2e); }
+__device__ __forceinline__ float flog(float x) { return log2_(x) * kLn2; }
+// sigmoid(x) = 1 / (1 + e^-x): saturates cleanly to 0 / 1 (rcp(inf) = 0).
+__device__ __forceinline__ float sigm(float x) { return rcp(1.0f + exp2_(-x * kLog2e)); }
+
+// ------------------------------------------------------------------ buffer I/O ---------------
+// Raw buffer loads/stores through a wave-uniform descriptor: the per-lane part of the address
+// is a 32-bit VGPR offset that stays constant over a whole scan (the column), the per-step part
+// (time, gate plane) is a scalar SGPR offset.  Saves the two VGPRs per in-flight load that a
+// 64-bit flat address costs, which is what lets deep register prefetch fit.
+template <int BYTES> struct RawIO;
+template <> struct RawIO<2> {
+  static __device__ __forceinline__ uint16_t ld(__amdgpu_buffer_rsrc_t r, uint32_t v, uint32_t s) {
+    return __builtin_amdgcn_raw_buffer_load_b16(r, v, s, 0);
+  }
+  static __device__ __forceinline__ void st(uint16_t x, __amdgpu_buffer_rsrc_t r, uint32_t v,
+                                            uint32_t s) {
+    __builtin_amdgcn_raw_buffer_store_b16(x, r, v, s, 0);
+  }
+};
+template <> struct RawIO<4> {
+  static __device__ __forceinline__ uint32_t ld(__amdgpu_buffer_rsrc_t r, uint32_t v, uint32_t s) {
+    return __builtin_amdgcn_raw_buffer_load_b32(r, v, s, 0);
+  }
+  static __device__ __forceinline__ void st(uint32_t x, __amdgpu_buffer_rsrc_t r, uint32_t v,
+                                            uint32_t s) {
+    __builtin_amdgcn_raw_buffer_store_b32(x, r, v, s, 0);
+  }
+};
+
+template <typename T>
+struct Buf {
+  using Raw = RawIO<sizeof(T)>;
+  __amdgpu_buffer_rsrc_t r;
+  // base must be wave-uniform (kernel argument + blockIdx arithmetic only).
+  __device__ __forceinline__ explicit Buf(const void* base)
+      : r(__builtin_amdgcn_make_buffer_rsrc((void*)base, 0, 0x7fffffff, 0x00020000)) {}
+  __device__ __forceinline__ T ld(uint32_t voff, uint32_t soff) const {
+    return __builtin_bit_cast(T, Raw::ld(r, voff, soff));
+  }
+  // raw element bits, zero-extended to 32 bits (see Elem::ldw)
+  __device__ __forceinline__ uint32_t ldw(uint32_t voff, uint32_t soff) const {
+    return (uint32_t)Raw::ld(r, voff, soff);
+  }
+  __device__ __forceinline__ void st(T x, uint32_t voff, uint32_t soff) const {
+    using U = decltype(Raw::ld(r, 0, 0));
+    Raw::st(__builtin_bit_cast(U, x), r, voff, soff);
+  }
+};
+
+__device__ __forceinline__ int uniform(int x) { return __builtin_amdgcn_readfirstlane(x); }
+
+// Workgroup barrier that orders LDS only.  __syncthreads() carries a workgroup fence that makes
+// the compiler drain outstanding global loads (vmcnt(0)); the scans keep their next
+// super-chunk's gate loads in flight across barriers, so the fence is restricted to LDS.
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+}  // namespace sc

@@ -1,0 +1,142 @@
+"""Drop-in replacement of the reference's lucyrnn_triton.py module API on MI355X.
+
+Same classes, constructor arguments, forward signatures, state nesting and state_dict keys as
+/root/reference/lucyrnn_triton.py:8-155 (`LinearSafe`, `LucyRNNCellTriton`, `LucyRNNtriton`),
+so model.py / train.py can import it unchanged.  The Triton kernel launch
+(lucyrnn_triton.py:61-73) is replaced by the HIP scan (statecatcher_amd/csrc/lucy_scan.hip via
+ops.LucyScanFn), which also has a backward.
+
+Differences from the reference, all deliberate:
+  * gradients flow into the recurrent layers (the reference's outputs have no grad_fn, F2);
+  * h0 is read through .contiguous(), so the carried out[:, -1] view is honoured (F3);
+  * bf16 / fp16 gates (e.g. under torch.autocast) run; state arithmetic stays fp32 (F4);
+  * s_last is returned in fp32.
+"""
+import torch
+import torch.nn as nn
+
+from .lucyrnn_conf import LucyRNNConfig
+from .ops import lucy_scan
+
+
+class LinearSafe(nn.Module):
+    """y = x W^T + b over the flattened leading dims (lucyrnn_triton.py:8-25)."""
+
+    def __init__(self, in_features, out_features, bias=True):
+        super().__init__()
+        self.weight = nn.Parameter(torch.empty(out_features, in_features))
+        self.bias = nn.Parameter(torch.empty(out_features)) if bias else None
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        nn.init.xavier_uniform_(self.weight)
+        if self.bias is not None:
+            nn.init.zeros_(self.bias)
+
+    def forward(self, x):
+        x_flat = x.reshape(-1, x.shape[-1])
+        if self.bias is not None:
+            # one GEMM with the bias in its epilogue (hipBLASLt); the reference adds it after
+            out = torch.addmm(self.bias, x_flat, self.weight.t())
+        else:
+            out = torch.matmul(x_flat, self.weight.t())
+        return out.view(*x.shape[:-1], self.weight.shape[0])
+
+
+class LucyRNNCellTriton(nn.Module):
+    """7-gate projection + HIP scan (lucyrnn_triton.py:27-75)."""
+
+    def __init__(self, input_dim, hidden_dim):
+        super().__init__()
+        self.input_dim = input_dim
+        self.hidden_dim = hidden_dim
+        self.linear = LinearSafe(input_dim, 7 * hidden_dim)
+        self._init_weights()
+
+    def _init_weights(self):
+        nn.init.xavier_uniform_(self.linear.weight)
+        if self.linear.bias is not None:
+            D = self.hidden_dim
+            with torch.no_grad():   # gate-aware bias init, lucyrnn_triton.py:41-48
+                self.linear.bias[0 * D:1 * D].zero_()      # r
+                self.linear.bias[1 * D:2 * D].fill_(1.0)   # z
+                self.linear.bias[2 * D:3 * D].zero_()      # k
+                self.linear.bias[3 * D:4 * D].zero_()      # v
+                self.linear.bias[4 * D:5 * D].zero_()      # h_pre
+                self.linear.bias[5 * D:6 * D].fill_(2.0)   # decay
+                self.linear.bias[6 * D:7 * D].fill_(0.5)   # alpha
+
+    def forward(self, x, h0, s0):
+        B, T, _ = x.shape
+        gates = self.linear(x).view(B, T, 7, self.hidden_dim)
+        return lucy_scan(gates, h0, s0)
+
+
+class LucyRNNtriton(nn.Module):
+    """L-layer LucyRNN stack with inter-layer LayerNorm and a vocab projection
+    (lucyrnn_triton.py:77-155).  forward(x, hidden_states=None, masks=None) ->
+    (logits, (final_h, final_s)) with final_h/final_s nested [track][layer] of [B, D]."""
+
+    def __init__(self, config: LucyRNNConfig):
+        super().__init__()
+        assert config.fused_ops
+        assert not config.layer_norm
+        assert config.stack_order == 1
+        assert config.decay_mode == 'learned'
+
+        self.config = config
+        self.num_tracks = getattr(config, "num_tracks", 1)
+
+        self.tracks = nn.ModuleList()
+        self.norms = nn.ModuleList()
+        for _ in range(self.num_tracks):
+            layers = nn.ModuleList()
+            norms = nn.ModuleList()
+            for i in range(config.num_layers):
+                input_dim = config.input_dim if i == 0 else config.hidden_dim
+                layers.append(LucyRNNCellTriton(input_dim, config.hidden_dim))
+                if i < config.num_layers - 1:
+                    norms.append(nn.LayerNorm(config.hidden_dim))
+            self.tracks.append(layers)
+            self.norms.append(norms)
+
+        self.merge_proj = (nn.Identity() if self.num_tracks == 1 else
+                           LinearSafe(config.hidden_dim * self.num_tracks, config.hidden_dim))
+        self.output_proj = LinearSafe(config.hidden_dim, config.vocab_size)
+        nn.init.zeros_(self.output_proj.weight)
+        nn.init.zeros_(self.output_proj.bias)
+
+    def forward(self, x, hidden_states=None, masks=None):
+        B, T, _ = x.shape
+        L = self.config.num_layers
+        H = self.config.hidden_dim
+        if hidden_states is None:
+            z = lambda: torch.zeros(B, H, device=x.device, dtype=x.dtype)  # noqa: E731
+            h = [[z() for _ in range(L)] for _ in range(self.num_tracks)]
+            s = [[z() for _ in range(L)] for _ in range(self.num_tracks)]
+        else:
+            h, s = hidden_states
+
+        track_outputs, final_h, final_s = [], [], []
+        for t in range(self.num_tracks):
+            x_t = x
+            h_t, s_t = h[t], s[t]
+            layers = self.tracks[t]
+            norms = self.norms[t]
+            for l, layer in enumerate(layers):
+                x_t, s_t[l] = layer(x_t, h_t[l], s_t[l])
+                h_t[l] = x_t[:, -1, :]
+                if l < len(norms):
+                    x_t = norms[l](x_t)
+            track_outputs.append(x_t)
+            final_h.append(h_t)
+            final_s.append(s_t)
+
+        if self.num_tracks == 1:
+            x = track_outputs[0]
+        else:
+            x = self.merge_proj(torch.cat(track_outputs, dim=-1))
+        logits = self.output_proj(x.contiguous())
+        if self.config.return_last_states:
+            return logits, (final_h, final_s)
+        return logits

@@ -1,0 +1,219 @@
+"""Autograd wrappers over the HIP C ABI (include/statecatcher.h).
+
+Each op checks device/dtype/shape, allocates outputs through the PyTorch caching allocator,
+launches on the current stream and never synchronises the host.
+"""
+import torch
+
+from . import _lib
+from ._lib import check, dtype_code, ptr, require_device, stream_of
+
+
+# ----------------------------------------------------------------------------- LucyRNN scan --
+class LucyScanFn(torch.autograd.Function):
+    """out, s_last = scan(gates [B,T,7,D], h0 [B,D], s0 [B,D]).
+
+    Forward = lucyrnn_triton.py:179-244 (rnn_forward_unfused_rmsnorm).  Unlike the reference
+     the outputs carry gradients to gates, h0 and s0.  out has the gates' dtype;
+    s_last is fp32 (state arithmetic is fp32 for every gate dtype).
+    """
+
+    @staticmethod
+    def forward(ctx, gates, h0, s0):
+        require_device(gates, h0, s0)
+        if gates.dim() != 4 or gates.shape[2] != 7:
+            raise ValueError(f"gates must be [B,T,7,D], got {tuple(gates.shape)}")
+        B, T, _, D = gates.shape
+        if tuple(h0.shape) != (B, D) or tuple(s0.shape) != (B, D):
+            raise ValueError(f"h0/s0 must be [B,D]=({B},{D}); got {tuple(h0.shape)}, {tuple(s0.shape)}")
+        if gates.stride(3) != 1:
+            gates = gates.contiguous()
+        # the reference reads h0/s0 as contiguous even when handed a strided view
+        h0c = h0.detach().to(torch.float32).contiguous()
+        s0c = s0.detach().to(torch.float32).contiguous()
+        out = torch.empty(B, T, D, dtype=gates.dtype, device=gates.device)
+        s_out = torch.empty(B, D, dtype=torch.float32, device=gates.device)
+        need_bwd = any(ctx.needs_input_grad)
+        lib = _lib.load()
+        ckpt = None
+        if need_bwd:
+            ckpt = torch.empty(lib.sc_lucy_scan_ckpt_numel(B, T, D), dtype=torch.float32,
+                               device=gates.device)
+        rc = lib.sc_lucy_scan_fwd(ptr(gates), dtype_code(gates), ptr(h0c), ptr(s0c), ptr(out),
+                                  ptr(s_out), B, T, D, gates.stride(0), gates.stride(1),
+                                  gates.stride(2), out.stride(0), out.stride(1), ptr(ckpt),
+                                  stream_of(gates))
+        check(rc, "sc_lucy_scan_fwd")
+        if need_bwd:
+            ctx.save_for_backward(gates, ckpt)
+            ctx.state_dtypes = (h0.dtype, s0.dtype)
+        return out, s_out
+
+    @staticmethod
+    def backward(ctx, dout, ds_last):
+        gates, ckpt = ctx.saved_tensors
+        B, T, _, D = gates.shape
+        if dout is None:
+            dout = torch.zeros(B, T, D, dtype=gates.dtype, device=gates.device)
+        dout = dout.to(gates.dtype)
+        if dout.stride(2) != 1:
+            dout = dout.contiguous()
+        if ds_last is not None:
+            ds_last = ds_last.to(torch.float32).contiguous()
+        dgates = torch.empty(B, T, 7, D, dtype=gates.dtype, device=gates.device)
+        dh0 = torch.empty(B, D, dtype=torch.float32, device=gates.device)
+        ds0 = torch.empty(B, D, dtype=torch.float32, device=gates.device)
+        rc = _lib.load().sc_lucy_scan_bwd(
+            ptr(gates), dtype_code(gates), ptr(ckpt), ptr(dout), ptr(ds_last), ptr(dgates),
+            ptr(dh0), ptr(ds0), B, T, D, gates.stride(0), gates.stride(1), gates.stride(2),
+            dout.stride(0), dout.stride(1), dgates.stride(0), dgates.stride(1), dgates.stride(2),
+            stream_of(gates))
+        check(rc, "sc_lucy_scan_bwd")
+        hd, sd = ctx.state_dtypes
+        return dgates, dh0.to(hd), ds0.to(sd)
+
+
+def lucy_scan(gates, h0, s0):
+    return LucyScanFn.apply(gates, h0, s0)
+
+
+# ----------------------------------------------------------------------------- decay scan ----
+class DecayScanFn(torch.autograd.Function):
+    """s_t = decay_t * s_{t-1} + kv_t, s_{-1} = init (zeros if None).  lucyrnn_triton.py:158-177."""
+
+    @staticmethod
+    def forward(ctx, kv, decay, init):
+        require_device(kv, decay, init)
+        if kv.shape != decay.shape or kv.dim() != 3:
+            raise ValueError(f"kv/decay must be equal [B,T,D]; got {tuple(kv.shape)}, {tuple(decay.shape)}")
+        decay = decay.to(kv.dtype)
+        kv = kv.contiguous()
+        decay = decay.contiguous()
+        B, T, D = kv.shape
+        initc = None if init is None else init.detach().to(torch.float32).contiguous()
+        out = torch.empty_like(kv)
+        rc = _lib.load().sc_decay_scan_fwd(ptr(kv), ptr(decay), ptr(out), dtype_code(kv), ptr(initc),
+                                           B, T, D, kv.stride(0), kv.stride(1), 1, stream_of(kv))
+        check(rc, "sc_decay_scan_fwd")
+        ctx.save_for_backward(decay, out, initc)
+        ctx.has_init = init is not None
+        ctx.init_dtype = None if init is None else init.dtype
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        decay, s_all, initc = ctx.saved_tensors
+        B, T, D = decay.shape
+        dout = dout.to(decay.dtype).contiguous()
+        dkv = torch.empty_like(decay)
+        ddec = torch.empty_like(decay)
+        dinit = torch.zeros(B, D, dtype=torch.float32, device=decay.device) if ctx.has_init else None
+        rc = _lib.load().sc_decay_scan_bwd(ptr(decay), ptr(s_all), ptr(dout), ptr(dkv), ptr(ddec),
+                                           dtype_code(decay), ptr(initc),
+                                           ptr(dinit) if T > 0 else None, B, T, D,
+                                           decay.stride(0), decay.stride(1), 1, stream_of(decay))
+        check(rc, "sc_decay_scan_bwd")
+        return dkv, ddec, (dinit.to(ctx.init_dtype) if ctx.has_init else None)
+
+
+def decay_scan(kv, decay, init=None):
+    return DecayScanFn.apply(kv, decay, init)
+
+
+# ----------------------------------------------------------------------------- CTC -----------
+def _as_len_tensor(x, device):
+    if isinstance(x, torch.Tensor):
+        return x.to(device=device, dtype=torch.int64).contiguous()
+    return torch.as_tensor(list(x), dtype=torch.int64).to(device, non_blocking=True)
+
+
+class CTCFn(torch.autograd.Function):
+    """nll [B] fp32 of CTC over x [B,T,V] (logits with fused log_softmax, or log-probs)."""
+
+    @staticmethod
+    def forward(ctx, x, targets, in_lens, tgt_lens, blank, is_logits):
+        require_device(x, targets, in_lens, tgt_lens)
+        if x.dim() != 3:
+            raise ValueError(f"x must be [B,T,V], got {tuple(x.shape)}")
+        B, T, V = x.shape
+        if x.stride(2) != 1:
+            x = x.contiguous()
+        if targets.dim() != 2 or targets.shape[0] != B:
+            raise ValueError("targets must be padded [B, U_max] (the layout train.py:208 builds); "
+                             f"got {tuple(targets.shape)}")
+        targets = targets.to(torch.int64).contiguous()
+        umax = targets.shape[1]
+        nll = torch.empty(B, dtype=torch.float32, device=x.device)
+        lib = _lib.load()
+        wsb = lib.sc_ctc_workspace_bytes(B, max(T, 1), umax)
+        ws = torch.empty(wsb, dtype=torch.uint8, device=x.device)
+        if T == 0:
+            nll = torch.where(tgt_lens == 0, 0.0, float("inf")).to(torch.float32)
+        else:
+            rc = lib.sc_ctc_fwd(ptr(x), dtype_code(x), int(is_logits), B, T, V, x.stride(0),
+                                x.stride(1), ptr(targets), targets.stride(0) if umax else 0, umax,
+                                ptr(in_lens), ptr(tgt_lens), blank, ptr(nll), ptr(ws), wsb,
+                                stream_of(x))
+            check(rc, "sc_ctc_fwd")
+        ctx.save_for_backward(x, targets, in_lens, tgt_lens, nll, ws)
+        ctx.meta = (blank, int(is_logits), umax, wsb)
+        return nll
+
+    @staticmethod
+    def backward(ctx, grad_nll):
+        x, targets, in_lens, tgt_lens, nll, ws = ctx.saved_tensors
+        blank, is_logits, umax, wsb = ctx.meta
+        B, T, V = x.shape
+        grad = torch.empty(B, T, V, dtype=x.dtype, device=x.device)
+        if T > 0:
+            scale = grad_nll.to(torch.float32).contiguous()
+            rc = _lib.load().sc_ctc_bwd(ptr(x), dtype_code(x), is_logits, B, T, V, x.stride(0),
+                                        x.stride(1), ptr(targets), targets.stride(0) if umax else 0,
+                                        umax, ptr(in_lens), ptr(tgt_lens), blank, ptr(nll),
+                                        ptr(scale), ptr(grad), dtype_code(grad), ptr(ws), wsb,
+                                        stream_of(x))
+            check(rc, "sc_ctc_bwd")
+        return grad, None, None, None, None, None
+
+
+def ctc_nll(x, targets, in_lens, tgt_lens, blank=0, is_logits=True):
+    dev = x.device
+    return CTCFn.apply(x, targets.to(dev), _as_len_tensor(in_lens, dev), _as_len_tensor(tgt_lens, dev),
+                       int(blank), bool(is_logits))
+
+
+def ctc_loss(x, targets, in_lens, tgt_lens, blank=0, reduction="mean", zero_infinity=True,
+             is_logits=True):
+    """CTC with the semantics of nn.CTCLoss(blank, reduction, zero_infinity) (train.py:142).
+
+    x: [B,T,V]; logits (log_softmax fused, as model.py:70 applies it) or log-probs.
+    'mean' = mean_b(nll_b / max(U_b, 1)), 'sum' = sum_b nll_b, 'none' = nll.
+    """
+    dev = x.device
+    tl = _as_len_tensor(tgt_lens, dev)
+    nll = CTCFn.apply(x, targets.to(dev), _as_len_tensor(in_lens, dev), tl, int(blank), bool(is_logits))
+    if zero_infinity:
+        nll = torch.where(torch.isinf(nll), torch.zeros_like(nll), nll)
+    if reduction == "none":
+        return nll
+    if reduction == "sum":
+        return nll.sum()
+    if reduction == "mean":
+        return (nll / tl.clamp_min(1).to(nll.dtype)).mean()
+    raise ValueError(f"unknown reduction {reduction!r}")
+
+
+def ctc_greedy_decode(log_probs, lengths, blank=0):
+    """Device greedy decode -> (tokens int32 [B,T], counts int32 [B]) (decoder.py:3-30)."""
+    require_device(log_probs)
+    B, T, V = log_probs.shape
+    if log_probs.stride(2) != 1:
+        log_probs = log_probs.contiguous()
+    lens = _as_len_tensor(lengths, log_probs.device)
+    tokens = torch.empty(B, T, dtype=torch.int32, device=log_probs.device)
+    counts = torch.empty(B, dtype=torch.int32, device=log_probs.device)
+    rc = _lib.load().sc_ctc_greedy_decode(ptr(log_probs), dtype_code(log_probs), B, T, V,
+                                          log_probs.stride(0), log_probs.stride(1), ptr(lens),
+                                          int(blank), ptr(tokens), ptr(counts), stream_of(log_probs))
+    check(rc, "sc_ctc_greedy_decode")
+    return tokens, counts

@@ -1,0 +1,62 @@
+"""CPU checks of the C ABI: the library loads here (no GPU) and exports every symbol that
+include/statecatcher.h declares; argument validation returns SC_EINVAL without touching a GPU."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from tests.conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "statecatcher.h")
+
+
+def header_functions():
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(sc_[a-z0-9_]+)\s*\(", txt)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from statecatcher_amd import _lib
+    return _lib.load()
+
+
+def test_library_exports_every_header_symbol(lib):
+    names = header_functions()
+    assert len(names) >= 12
+    for n in names:
+        assert hasattr(lib, n), n
+
+
+def test_binding_covers_header(lib):
+    from statecatcher_amd import _lib
+    assert sorted(_lib.EXPORTED) == header_functions()
+
+
+def test_abi_version_and_sizes(lib):
+    assert lib.sc_abi_version() == 1
+    assert lib.sc_lucy_scan_chunk() == 64
+    assert lib.sc_lucy_scan_ckpt_numel(32, 1500, 512) == 32 * 24 * 2 * 512
+    assert lib.sc_lucy_scan_ckpt_numel(2, 64, 3) == 2 * 1 * 2 * 3
+    assert lib.sc_lucy_scan_ckpt_numel(2, 65, 3) == 2 * 2 * 2 * 3
+    assert lib.sc_ctc_workspace_bytes(32, 1500, 150) >= 32 * 1500 * (2 * 301 + 1) * 4
+
+
+def test_invalid_arguments_rejected_without_gpu(lib):
+    null = ctypes.c_void_p()
+    rc = lib.sc_lucy_scan_fwd(null, 7, null, null, null, null, 1, 1, 1, 1, 1, 1, 1, 1, null, null)
+    assert rc == -1
+    assert b"dtype" in lib.sc_last_error()
+    rc = lib.sc_lucy_scan_fwd(null, 0, null, null, null, null, -1, 1, 1, 1, 1, 1, 1, 1, null, null)
+    assert rc == -1
+    rc = lib.sc_decay_scan_fwd(null, null, null, 0, null, 1, 1, 1, 1, 1, 2, null)
+    assert rc == -1 and b"stride_d" in lib.sc_last_error()
+    rc = lib.sc_ctc_fwd(null, 0, 1, 1, 1, 4, 4, 4, null, 0, 600, null, null, 0, null, null, 0, null)
+    assert rc == -1 and b"exceeds" in lib.sc_last_error()
+    rc = lib.sc_ctc_fwd(null, 0, 1, 1, 1, 4, 4, 4, null, 0, 1, null, null, 9, null, null, 0, null)
+    assert rc == -1 and b"blank" in lib.sc_last_error()
+    # empty problems are no-ops
+    assert lib.sc_lucy_scan_fwd(null, 0, null, null, null, null, 0, 5, 5, 1, 1, 1, 1, 1, null, null) == 0
+    assert lib.sc_ctc_greedy_decode(null, 0, 0, 5, 5, 1, 1, null, 0, null, null, null) == 0

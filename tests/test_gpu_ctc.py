@@ -1,0 +1,135 @@
+"""GPU parity of the fused CTC (HIP) against ATen fixtures and the fp64 oracle, and of the
+greedy decoder (integer path: bit-exact) against the reference decoder fixtures.
+Tolerances: nll 1e-4 relative (fp32 log-space recursions); gradients 1e-4 absolute on the
+softmax-scale quantities (|grad| <= 1) for fp32 logits, 2e-2 for bf16 logits / bf16 gradients.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import ctc as octc
+from oracle import decode as odec
+from tests.conftest import cases, load_golden
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0") if torch.cuda.is_available() else None
+
+
+def sc():
+    import statecatcher_amd as s
+    return s
+
+
+@pytest.mark.parametrize("name", cases(load_golden("ctc"), "logits"))
+def test_ctc_fused_vs_aten_fixture(name):
+    z = load_golden("ctc")
+    x = torch.as_tensor(z[name + "/logits"]).float().to(DEV).requires_grad_(True)
+    tg = torch.as_tensor(z[name + "/targets"]).to(DEV)
+    il, tl = z[name + "/in_lens"].tolist(), z[name + "/tgt_lens"].tolist()
+    nll = sc().ctc_nll(x, tg, il, tl)
+    ref = z[name + "/nll"]
+    got = nll.detach().cpu().numpy()
+    assert np.array_equal(np.isfinite(got), np.isfinite(ref))
+    fin = np.isfinite(ref)
+    np.testing.assert_allclose(got[fin], ref[fin], rtol=1e-4, atol=1e-4)
+    # mean + zero_infinity reduction and its gradient (nn.CTCLoss semantics)
+    loss = sc().ctc_loss(x, tg, il, tl, blank=0, reduction="mean", zero_infinity=True)
+    np.testing.assert_allclose(loss.item(), float(z[name + "/mean_loss"]), rtol=1e-4, atol=1e-6)
+    loss.backward()
+    np.testing.assert_allclose(x.grad.cpu().numpy(), z[name + "/mean_grad"], rtol=1e-3, atol=2e-6)
+
+
+@pytest.mark.parametrize("name", ["basic", "repeats", "long"])
+def test_ctc_logprob_interface_vs_aten(name):
+    """CTCLoss.forward takes (T,B,V) log-probs exactly like nn.CTCLoss (train.py:142)."""
+    z = load_golden("ctc")
+    x = torch.as_tensor(z[name + "/logits"]).float().to(DEV).requires_grad_(True)
+    tg = torch.as_tensor(z[name + "/targets"]).to(DEV)
+    il, tl = z[name + "/in_lens"].tolist(), z[name + "/tgt_lens"].tolist()
+    crit = sc().CTCLoss(blank=0, zero_infinity=True)
+    loss = crit(x.log_softmax(-1).transpose(0, 1), tg, il, tl)
+    np.testing.assert_allclose(loss.item(), float(z[name + "/mean_loss"]), rtol=1e-4, atol=1e-6)
+    loss.backward()
+    np.testing.assert_allclose(x.grad.cpu().numpy(), z[name + "/mean_grad"], rtol=1e-3, atol=2e-6)
+
+
+def test_ctc_full_size_vs_aten_cpu():
+    """C2 shape: B=32, T=1500, V=1024, U in [50,150] vs ATen ctc_loss on CPU (fp64)."""
+    g = torch.Generator().manual_seed(4321)
+    B, T, V = 32, 1500, 1024
+    logits = torch.randn(B, T, V, generator=g) * 2
+    tl = torch.randint(50, 151, (B,), generator=g)
+    il = torch.full((B,), T, dtype=torch.int64)
+    il[3] = 1000
+    tg = torch.randint(1, V, (B, 150), generator=g)
+    for b in range(B):
+        tg[b, tl[b]:] = 0
+    x = logits.to(DEV).requires_grad_(True)
+    loss = sc().ctc_loss(x, tg.to(DEV), il, tl)
+    loss.backward()
+    xr = logits.double().requires_grad_(True)
+    ref = torch.nn.CTCLoss(blank=0, zero_infinity=True)(xr.log_softmax(-1).transpose(0, 1), tg, il, tl)
+    ref.backward()
+    np.testing.assert_allclose(loss.item(), ref.item(), rtol=1e-4)
+    np.testing.assert_allclose(x.grad.cpu().numpy(), xr.grad.numpy(), rtol=1e-2, atol=2e-6)
+
+
+def test_ctc_bf16_logits_vs_oracle():
+    g = torch.Generator().manual_seed(5)
+    B, T, V = 3, 120, 64
+    logits = (torch.randn(B, T, V, generator=g) * 2).bfloat16()
+    tg = torch.randint(1, V, (B, 20), generator=g)
+    il, tl = [120, 90, 40], [20, 11, 0]
+    x = logits.to(DEV).requires_grad_(True)
+    nll = sc().ctc_nll(x, tg.to(DEV), il, tl)
+    nll.sum().backward()
+    rn, rg = octc.ctc_loss_grad(logits.float().numpy(), tg.numpy(), il, tl)
+    np.testing.assert_allclose(nll.detach().cpu().numpy(), rn, rtol=1e-4)
+    np.testing.assert_allclose(x.grad.float().cpu().numpy(), rg, atol=2e-2)
+
+
+def test_ctc_edge_cases():
+    """U=0, infeasible (T < U + repeats), in_len=0 and in_len=1."""
+    g = torch.Generator().manual_seed(9)
+    B, T, V = 4, 6, 5
+    logits = torch.randn(B, T, V, generator=g)
+    tg = torch.tensor([[1, 1, 1, 1], [2, 3, 0, 0], [4, 0, 0, 0], [0, 0, 0, 0]])
+    il, tl = [6, 0, 1, 6], [4, 2, 1, 0]
+    x = logits.to(DEV).requires_grad_(True)
+    nll = sc().ctc_nll(x, tg.to(DEV), il, tl)
+    rn, rg = octc.ctc_loss_grad(logits.numpy(), tg.numpy(), il, tl)
+    got = nll.detach().cpu().numpy()
+    assert np.isinf(got[0]) and np.isinf(rn[0])          # 1,1,1,1 needs 7 frames
+    assert np.isinf(got[1]) and np.isinf(rn[1])          # in_len 0, U 2
+    np.testing.assert_allclose(got[2:], rn[2:], rtol=1e-5)
+    loss = sc().ctc_loss(x, tg.to(DEV), il, tl)
+    loss.backward()
+    gr = x.grad.cpu().numpy()
+    assert np.all(gr[0] == 0) and np.all(gr[1] == 0)      # zero_infinity zeroes the rows
+    assert np.all(gr[2, 1:] == 0)                          # t >= in_len
+    sc_ = octc.ctc_mean_grad_scale(rn, tl)
+    np.testing.assert_allclose(gr[2:], (rg * sc_[:, None, None])[2:], rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("pref", ["ties", "big"])
+def test_greedy_decoder_bit_exact_vs_reference(pref):
+    z = load_golden("greedy")
+    lp = torch.as_tensor(z[pref + "_lp"]).to(DEV)
+    dec = sc().ctc_greedy_decoder(lp, torch.as_tensor(z[pref + "_in_lens"]), blank=0)
+    counts, flat = z[pref + "_counts"], z[pref + "_tokens"]
+    exp, o = [], 0
+    for c in counts:
+        exp.append(flat[o:o + c].tolist())
+        o += c
+    assert dec == exp
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_greedy_full_size_vs_oracle(dtype):
+    g = torch.Generator().manual_seed(2)
+    B, T, V = 32, 1500, 1024
+    # few distinct values -> many ties; blank-heavy rows
+    lp = torch.randint(-3, 1, (B, T, V), generator=g).to(dtype)
+    lens = torch.randint(0, T + 1, (B,), generator=g)
+    dec = sc().ctc_greedy_decoder(lp.to(DEV), lens, blank=0)
+    assert dec == odec.ctc_greedy(lp.float().numpy(), lens.numpy(), blank=0)

@@ -1,0 +1,105 @@
+"""CPU tests of the host-side mirror of the reference module API (no kernels run here)."""
+import dataclasses
+
+import numpy as np
+import pytest
+import torch
+
+import statecatcher_amd as sc
+from statecatcher_amd.model import build_lucyrnn_config
+
+
+def small_cfg(L=3):
+    return build_lucyrnn_config(input_dim=80, hidden_size=32, num_layers=L, vocab_size=50)
+
+
+def test_config_fields_match_reference_dataclass():
+    names = [f.name for f in dataclasses.fields(sc.LucyRNNConfig)]
+    assert names == ["input_dim", "hidden_dim", "num_layers", "vocab_size", "return_last_states",
+                     "kernel_impl", "is_training", "fused_ops", "layer_norm", "stack_order",
+                     "decay_mode", "lambda_decay"]
+    c = sc.LucyRNNConfig(1, 2, 3, 4)
+    assert (c.kernel_impl, c.fused_ops, c.layer_norm, c.decay_mode) == ("native", False, True, "learned")
+
+
+def test_state_dict_layout_matches_reference():
+    """Key names/shapes of LucyRNNtriton (lucyrnn_triton.py:88-109), as train.py saves them."""
+    m = sc.LucyRNNtriton(small_cfg(3))
+    sd = {k: tuple(v.shape) for k, v in m.state_dict().items()}
+    D, Din, V = 32, 80, 50
+    exp = {"tracks.0.0.linear.weight": (7 * D, Din), "tracks.0.0.linear.bias": (7 * D,),
+           "tracks.0.1.linear.weight": (7 * D, D), "tracks.0.1.linear.bias": (7 * D,),
+           "tracks.0.2.linear.weight": (7 * D, D), "tracks.0.2.linear.bias": (7 * D,),
+           "norms.0.0.weight": (D,), "norms.0.0.bias": (D,), "norms.0.1.weight": (D,),
+           "norms.0.1.bias": (D,), "output_proj.weight": (V, D), "output_proj.bias": (V,)}
+    assert sd == exp
+
+
+def test_reference_init():
+    m = sc.LucyRNNtriton(small_cfg(2))
+    b = m.tracks[0][0].linear.bias.detach().view(7, 32)
+    assert torch.all(b[1] == 1.0) and torch.all(b[5] == 2.0) and torch.all(b[6] == 0.5)
+    assert torch.all(b[[0, 2, 3, 4]] == 0)
+    assert torch.all(m.output_proj.weight == 0) and torch.all(m.output_proj.bias == 0)
+
+
+def test_reference_asserts_kept():
+    with pytest.raises(AssertionError):
+        sc.LucyRNNtriton(sc.LucyRNNConfig(80, 32, 2, 50, fused_ops=False, layer_norm=False))
+    with pytest.raises(AssertionError):
+        sc.LucyRNNtriton(sc.LucyRNNConfig(80, 32, 2, 50, fused_ops=True, layer_norm=True))
+
+
+def test_cpu_tensors_fail_loudly_no_fallback():
+    m = sc.LucyRNNtriton(small_cfg(2))
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        m(torch.randn(2, 5, 80))
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        sc.ctc_nll(torch.randn(2, 5, 7), torch.ones(2, 3, dtype=torch.long), [5, 5], [3, 3])
+
+
+def test_detach_states_nested():
+    a = torch.randn(2, requires_grad=True) * 2
+    st = ([[a, a]], [[a]])
+    d = sc.detach_states(st)
+    assert isinstance(d, tuple) and isinstance(d[0], list) and isinstance(d[0][0], list)
+    assert not d[0][0][1].requires_grad
+    assert sc.detach_states(None) is None
+    assert sc.detach_states({"x": (a,)})["x"][0].requires_grad is False
+
+
+def test_asr_model_wraps_lucyrnn_and_projection():
+    cfg = small_cfg(2)
+    m = sc.ASRModel(None, cfg, vocab_size=50, feat_dim=80, proj_dim=-1)
+    assert isinstance(m.encoder, sc.LucyRNNtriton) and not hasattr(m, "proj")
+    cfg2 = build_lucyrnn_config(input_dim=64, hidden_size=32, num_layers=2, vocab_size=50)
+    m2 = sc.ASRModel(None, cfg2, vocab_size=50, feat_dim=80, proj_dim=64)
+    assert m2.proj.in_features == 80 and m2.proj.out_features == 64
+    with pytest.raises(ValueError):
+        sc.ASRModel(None, object(), 50, 80, -1)
+
+
+def test_compute_loss_rejects_unknown_mode():
+    class Dummy(torch.nn.Module):
+        def forward(self, f, m, s):
+            return f, s
+    with pytest.raises(ValueError):
+        sc.compute_loss("xyz", None, Dummy(), torch.zeros(1, 2, 3), None, None, [2], [1], 0)
+    with pytest.raises(NotImplementedError):
+        sc.compute_loss("rnnt", None, Dummy(), torch.zeros(1, 2, 3), None, None, [2], [1], 0)
+
+
+def test_compute_loss_reference_criterion_path():
+    """With a plain nn.CTCLoss the caller runs log_softmax -> transpose -> criterion (model.py:68-71)."""
+    class Enc(torch.nn.Module):
+        def forward(self, f, m, s):
+            return f, "state"
+    torch.manual_seed(0)
+    feats = torch.randn(2, 10, 6)
+    tok = torch.tensor([[1, 2, 3], [4, 4, 0]])
+    loss, st, enc, st2 = sc.compute_loss("ctc", torch.nn.CTCLoss(blank=0, zero_infinity=True), Enc(),
+                                         feats, None, tok, [10, 8], [3, 2], 0)
+    ref = torch.nn.functional.ctc_loss(feats.log_softmax(-1).transpose(0, 1), tok, [10, 8], [3, 2],
+                                       zero_infinity=True)
+    assert st == "state" and st2 == "state" and torch.equal(enc, feats)
+    np.testing.assert_allclose(loss.item(), ref.item())
