@@ -1,0 +1,232 @@
+#!/usr/bin/env python3
+"""LucyRNN + CTC stateful training step on MI355X: audio-frames/sec (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1]): LucyRNN 6 x 512, 80-d synthetic fbank,
+B=32 per GPU, T=1500 frames per segment, V=1024, CTC (blank 0, mean, zero_infinity),
+bf16 autocast GEMMs + bf16 gates (fp32 recurrent state), Adam lr 3e-4, clip_grad_norm 50,
+4 consecutive segments per batch with the encoder state carried (detached) between them.
+One step = forward + CTC + backward + (DDP all-reduce) + clip + Adam over one B x T segment.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    torchrun --nproc-per-node N ... bench.py --gpus N   (one rank per GPU, RCCL)
+
+Prints ONE JSON line on rank 0.  value = frames processed by all ranks / max-over-ranks time.
+"""
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+PEAK_HBM_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+PEAK_BF16_TFLOPS = 2500.0  # dense bf16 MFMA spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--seq", type=int, default=1500)
+    ap.add_argument("--layers", type=int, default=6)
+    ap.add_argument("--hidden", type=int, default=512)
+    ap.add_argument("--vocab", type=int, default=1024)
+    ap.add_argument("--feat", type=int, default=80)
+    ap.add_argument("--segments", type=int, default=4)
+    ap.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16")
+    ap.add_argument("--bucket-mb", type=float, default=50.0)
+    ap.add_argument("--cpu-baseline", choices=["on", "off"], default="on")
+    ap.add_argument("--cpu-seq", type=int, default=300, help="T of the bounded CPU sample")
+    return ap.parse_args()
+
+
+def synth_segments(args, rank, device):
+    g = torch.Generator().manual_seed(1234 + rank)
+    gt = torch.Generator().manual_seed(4321 + rank)
+    segs = []
+    for _ in range(args.segments):
+        feats = torch.randn(args.batch, args.seq, args.feat, generator=g)
+        U = torch.randint(50, 151, (args.batch,), generator=gt)
+        tok = torch.randint(1, args.vocab, (args.batch, 150), generator=gt)
+        for b in range(args.batch):
+            tok[b, U[b]:] = 0
+        segs.append(dict(feats=feats.to(device), tokens=tok.to(device),
+                         in_lens=torch.full((args.batch,), args.seq, dtype=torch.int64, device=device),
+                         tgt_lens=U.to(device),
+                         masks=torch.ones(args.batch, args.seq, dtype=torch.bool, device=device)))
+    return segs
+
+
+def gemm_flops_per_frame(args):
+    D, L = args.hidden, args.layers
+    fwd = 2 * 7 * D * (args.feat + (L - 1) * D) + 2 * D * args.vocab
+    return 3 * fwd   # fwd + dgrad + wgrad
+
+
+def cpu_baseline(args):
+    """Oracle (numpy port) of the same step on a bounded sample: B=32, T=args.cpu_seq."""
+    from oracle import lucy_step
+    try:
+        from threadpoolctl import threadpool_info
+        threads = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
+    except Exception:   # pragma: no cover
+        threads = 1
+    B, T = args.batch, args.cpu_seq
+    rng = np.random.default_rng(0)
+    p = lucy_step.init_params(args.layers, args.feat, args.hidden, args.vocab)
+    feats = rng.standard_normal((B, T, args.feat)).astype(np.float32)
+    U = rng.integers(max(1, T // 30), max(2, T // 10) + 1, B)
+    tok = rng.integers(1, args.vocab, (B, int(U.max())))
+    in_lens = np.full(B, T)
+    t0 = time.perf_counter()
+    loss, state, _, adam = lucy_step.train_step(p, feats, tok, in_lens, U, args.layers, args.hidden)
+    dt = time.perf_counter() - t0
+    return {"value": round(B * T / dt, 1), "unit": "audio-frames/s", "cores": int(threads),
+            "kind": "port",
+            "sample": f"oracle/lucy_step.py numpy fp32 (CTC fp64) train step, B={B} T={T} "
+                      f"(U~[{T // 30},{T // 10}]), {args.layers}x{args.hidden}, 1 step, "
+                      f"{dt:.1f} s on {platform.processor() or platform.machine()} "
+                      f"(os.cpu_count={os.cpu_count()}, BLAS threads={threads})"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+
+    import statecatcher_amd as sc
+    from statecatcher_amd import ops
+    from statecatcher_amd.model import ASRModel, CTCLoss, build_lucyrnn_config, compute_loss
+
+    torch.manual_seed(0)   # identical init on every rank (DDP also broadcasts)
+    cfg = build_lucyrnn_config(args.feat, args.hidden, args.layers, args.vocab)
+    model = ASRModel(None, cfg, vocab_size=args.vocab, feat_dim=args.feat, proj_dim=-1).to(device)
+    with torch.no_grad():   # reference zero-inits output_proj (lucyrnn_triton.py:108-109); a seeded
+        model.encoder.output_proj.weight.normal_(0, 0.02)   # N(0,0.02) keeps every gradient non-zero
+    net = model
+    if world > 1:
+        net = torch.nn.parallel.DistributedDataParallel(
+            model, device_ids=[local], bucket_cap_mb=args.bucket_mb, gradient_as_bucket_view=True,
+            broadcast_buffers=False)
+    params = [p for p in model.parameters() if p.requires_grad]
+    try:
+        opt = torch.optim.Adam(params, lr=3e-4, fused=True)
+    except Exception:
+        opt = torch.optim.Adam(params, lr=3e-4, foreach=True)
+    crit = CTCLoss(blank=0, zero_infinity=True)
+    segs = synth_segments(args, rank, device)
+    amp = torch.bfloat16 if args.dtype == "bf16" else None
+
+    state = {"s": None, "i": 0}
+
+    def step():
+        seg = segs[state["i"] % args.segments]
+        if state["i"] % args.segments == 0:
+            state["s"] = None   # new batch: state reset (train.py:460)
+        with torch.autocast("cuda", dtype=amp, enabled=amp is not None):
+            loss, out_state, _, _ = compute_loss("ctc", crit, net, seg["feats"], seg["masks"],
+                                                 seg["tokens"], seg["in_lens"], seg["tgt_lens"], 0,
+                                                 input_state=state["s"])
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(params, 50.0)
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+        state["s"] = out_state
+        state["i"] += 1
+        return loss
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ops.LAUNCH_EVENTS = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    events, ops.LAUNCH_EVENTS = ops.LAUNCH_EVENTS, None
+    if world > 1:
+        t = torch.tensor([dt], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    last_loss = float(loss.item())
+
+    # per-kernel average launch duration from the HIP events recorded on the launch stream
+    kstats = {}
+    for name, e0, e1, nbytes in events:
+        k = kstats.setdefault(name, [0.0, 0, 0])
+        k[0] += e0.elapsed_time(e1) * 1e-3
+        k[1] += 1
+        k[2] = nbytes
+    kernels = {}
+    for name, (tsum, n, nbytes) in kstats.items():
+        avg = tsum / n
+        kernels[name] = {"launches": n, "avg_us": round(avg * 1e6, 1), "bytes_per_launch": nbytes,
+                         "achieved_GBs": round(nbytes / avg / 1e9, 1),
+                         "frac_of_peak": round(nbytes / avg / 1e9 / PEAK_HBM_GBS, 4),
+                         "share_of_step": round(tsum / dt, 4)}
+    dom = max(kernels, key=lambda k: kstats[k][0]) if kernels else None
+    traffic = None
+    pmc_file = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if dom and os.path.exists(pmc_file):
+        traffic = json.load(open(pmc_file)).get(dom, {}).get("hbm_bytes_per_launch")
+    roofline = None
+    if dom:
+        kd = kernels[dom]
+        roofline = {"bound": "hbm", "kernel": dom, "achieved": kd["achieved_GBs"],
+                    "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": kd["frac_of_peak"],
+                    "traffic": traffic}
+
+    frames = world * args.batch * args.seq * args.steps
+    value = frames / dt
+    ms = dt / args.steps * 1e3
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_baseline == "on":
+        cpu = cpu_baseline(args)
+    if rank == 0:
+        gemm_tflops = gemm_flops_per_frame(args) * args.batch * args.seq * world * args.steps / dt / 1e12
+        line = {
+            "metric": "audio-frames/sec (LucyRNN+CTC, 80-d fbank, T=1500), whole job",
+            "value": round(value, 1), "unit": "audio-frames/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "bf16" if amp is not None else "fp32",
+            "data": "synthetic N(0,1) 80-d fbank, targets U~U[50,150] of V=1024, random-init weights",
+            "config": {"workload": "LucyRNN 6x512 + CTC training step, stateful 4-segment carry",
+                       "global_batch": args.batch * world, "seq_len": args.seq,
+                       "layers": args.layers, "hidden": args.hidden, "vocab": args.vocab,
+                       "parallelism": f"dp{world}"},
+            "per_gpu_frames_per_s": round(value / world, 1),
+            "roofline": roofline,
+            "kernels": kernels,
+            "gemm_TFLOPs_effective": round(gemm_tflops / world, 1),
+            "cpu_baseline": cpu,
+            "loss_last": round(last_loss, 4),
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -26,10 +26,17 @@ constexpr int kCtcP = 8;           // emission prefetch depth (steps)
 constexpr int kCtcMaxStates = 1024;
 constexpr float kNegInf = -__builtin_huge_valf();
 
+// alpha/beta are stored NORMALISED: stored_t(s) = alpha_t(s) - offA_t where offA_t (fp64) is
+// the running sum of the per-step maxima.  At T=1500 |alpha| reaches ~1e4, where an fp32 ulp is
+// ~1e-3: un-normalised fp32 lattices put ~0.5% error into exp(alpha+beta+nll-lp).  With the
+// offsets in fp64 the posterior exponent is formed from O(10) fp32 terms.
 struct CtcWs {
   float* lse;
   float* alpha;
   float* beta;
+  double* offA;   // [B,T]
+  double* offB;   // [B,T]
+  double* nll64;  // [B]
   int* chain;
   int* first;
 };
@@ -42,6 +49,9 @@ static CtcWs carve(void* ws, int B, int T, int S, int Um) {
   w.lse = (float*)p; p += align256((size_t)B * T * 4);
   w.alpha = (float*)p; p += align256((size_t)B * T * S * 4);
   w.beta = (float*)p; p += align256((size_t)B * T * S * 4);
+  w.offA = (double*)p; p += align256((size_t)B * T * 8);
+  w.offB = (double*)p; p += align256((size_t)B * T * 8);
+  w.nll64 = (double*)p; p += align256((size_t)B * 8);
   w.chain = (int*)p; p += align256((size_t)B * Um * 4);
   w.first = (int*)p;
   return w;
@@ -51,7 +61,7 @@ static size_t ws_bytes(int B, int T, int Umax) {
   const int S = 2 * Umax + 1;
   const int Um = Umax > 0 ? Umax : 1;
   return align256((size_t)B * T * 4) + 2 * align256((size_t)B * T * S * 4) +
-         2 * align256((size_t)B * Um * 4);
+         2 * align256((size_t)B * T * 8) + align256((size_t)B * 8) + 2 * align256((size_t)B * Um * 4);
 }
 
 __device__ __forceinline__ float lse2(float a, float b) {
@@ -187,6 +197,11 @@ __global__ void __launch_bounds__(1024) ctc_ab_kernel(CtcArgs a) {
   load(cx, cl, 0);
   float* prev = buf0;
   float* cur = buf1;
+  __shared__ float wmax[2][16];
+  const int lane = s & 63, wv = s >> 6, nwv = blockDim.x >> 6;
+  double* offp = (is_beta ? a.ws.offB : a.ws.offA) + (int64_t)b * a.T;
+  double off = 0.0;   // log-offset of the values in `prev` (all threads hold the same value)
+  float mprev = 0.0f; // max of the previous step, already folded into `off`
   for (int i0 = 0; i0 < Tb; i0 += kCtcP) {
     if (i0 + kCtcP < Tb) load(nx, nl, i0 + kCtcP);
 #pragma unroll
@@ -203,15 +218,24 @@ __global__ void __launch_bounds__(1024) ctc_ab_kernel(CtcArgs a) {
       } else if (!is_beta) {
         const float a1 = s > 0 ? prev[s - 1] : kNegInf;
         const float a2 = skip ? prev[s - 2] : kNegInf;
-        v = lse3(prev[s], a1, a2) + lp;
+        v = lse3(prev[s], a1, a2) - mprev + lp;
       } else {
         const float b1 = s + 1 < Sb ? prev[s + 1] : kNegInf;
         const float b2 = skip ? prev[s + 2] : kNegInf;
-        v = lse3(prev[s], b1, b2) + lp;
+        v = lse3(prev[s], b1, b2) - mprev + lp;
       }
       cur[s] = v;
       if (act) outp[(int64_t)t * a.S + s] = v;
+      if (s == 0) offp[t] = off;
+      float mx = v;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+      if (lane == 0) wmax[i & 1][wv] = mx;
       lds_barrier();
+      float m = kNegInf;
+      for (int q = 0; q < nwv; ++q) m = fmaxf(m, wmax[i & 1][q]);
+      mprev = (m == kNegInf) ? 0.0f : m;
+      off += (double)mprev;
       float* tmp = prev; prev = cur; cur = tmp;
     }
 #pragma unroll
@@ -221,8 +245,11 @@ __global__ void __launch_bounds__(1024) ctc_ab_kernel(CtcArgs a) {
     }
   }
   if (!is_beta && s == 0) {
+    // prev holds the last step relative to off - mprev
     const float ll = Sb > 1 ? lse2(prev[Sb - 1], prev[Sb - 2]) : prev[0];
-    a.nll[b] = -ll;
+    const double nll = (ll == kNegInf) ? __builtin_huge_val() : -((double)ll + (off - (double)mprev));
+    a.ws.nll64[b] = nll;
+    a.nll[b] = (float)nll;
   }
 }
 
@@ -249,6 +276,9 @@ __global__ void __launch_bounds__(256) ctc_grad_kernel(CtcArgs a) {
   __syncthreads();
   const float* al = a.ws.alpha + ((int64_t)b * a.T + t) * a.S;
   const float* be = a.ws.beta + ((int64_t)b * a.T + t) * a.S;
+  // exp(lcab + nll - lp) with lcab = lse(stored) + offA + offB: fold the fp64 offsets first
+  const float koff = (float)(a.ws.offA[(int64_t)b * a.T + t] + a.ws.offB[(int64_t)b * a.T + t] +
+                             a.ws.nll64[b]);
   const int* chain = a.ws.chain + (int64_t)b * Um;
   const int* first = a.ws.first + (int64_t)b * Um;
   float m = kNegInf, l = 0.0f;   // blank-label occupancy, per thread
@@ -299,10 +329,9 @@ __global__ void __launch_bounds__(256) ctc_grad_kernel(CtcArgs a) {
   __syncthreads();
   const typename E::T* xr = (const typename E::T*)a.x + (int64_t)b * a.sb + (int64_t)t * a.stt;
   const float lse = a.is_logits ? a.ws.lse[(int64_t)b * a.T + t] : 0.0f;
-  const float nll = a.nll[b];
   for (int v = tid; v < a.V; v += 256) {
     const float lp = E::ld(xr[v]) - lse;
-    const float gv = fexp(lp) - fexp(lcab[v] + nll - lp);
+    const float gv = fexp(lp) - fexp(lcab[v] + koff - lp);
     g[v] = G::st(gv * sc);
   }
 }

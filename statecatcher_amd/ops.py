@@ -8,6 +8,31 @@ import torch
 from . import _lib
 from ._lib import check, dtype_code, ptr, require_device, stream_of
 
+# Optional per-launch timing (bench.py roofline): when a list, every scan launch appends
+# (name, start_event, end_event, algorithmic_bytes) recorded on the launch stream.
+LAUNCH_EVENTS = None
+
+
+class _timed:
+    def __init__(self, name, t, nbytes):
+        self.rec = LAUNCH_EVENTS is not None
+        if self.rec:
+            self.name, self.nbytes = name, nbytes
+            self.stream = torch.cuda.current_stream(t.device)
+            self.e0 = torch.cuda.Event(enable_timing=True)
+            self.e1 = torch.cuda.Event(enable_timing=True)
+
+    def __enter__(self):
+        if self.rec:
+            self.e0.record(self.stream)
+        return self
+
+    def __exit__(self, *exc):
+        if self.rec:
+            self.e1.record(self.stream)
+            LAUNCH_EVENTS.append((self.name, self.e0, self.e1, self.nbytes))
+        return False
+
 
 # ----------------------------------------------------------------------------- LucyRNN scan --
 class LucyScanFn(torch.autograd.Function):
@@ -39,10 +64,13 @@ class LucyScanFn(torch.autograd.Function):
         if need_bwd:
             ckpt = torch.empty(lib.sc_lucy_scan_ckpt_numel(B, T, D), dtype=torch.float32,
                                device=gates.device)
-        rc = lib.sc_lucy_scan_fwd(ptr(gates), dtype_code(gates), ptr(h0c), ptr(s0c), ptr(out),
-                                  ptr(s_out), B, T, D, gates.stride(0), gates.stride(1),
-                                  gates.stride(2), out.stride(0), out.stride(1), ptr(ckpt),
-                                  stream_of(gates))
+        e = gates.element_size()
+        nbytes = B * T * D * 8 * e + (ckpt.numel() * 4 if ckpt is not None else 0) + 4 * B * D * 4
+        with _timed("lucy_scan_fwd", gates, nbytes):
+            rc = lib.sc_lucy_scan_fwd(ptr(gates), dtype_code(gates), ptr(h0c), ptr(s0c), ptr(out),
+                                      ptr(s_out), B, T, D, gates.stride(0), gates.stride(1),
+                                      gates.stride(2), out.stride(0), out.stride(1), ptr(ckpt),
+                                      stream_of(gates))
         check(rc, "sc_lucy_scan_fwd")
         if need_bwd:
             ctx.save_for_backward(gates, ckpt)
@@ -63,11 +91,14 @@ class LucyScanFn(torch.autograd.Function):
         dgates = torch.empty(B, T, 7, D, dtype=gates.dtype, device=gates.device)
         dh0 = torch.empty(B, D, dtype=torch.float32, device=gates.device)
         ds0 = torch.empty(B, D, dtype=torch.float32, device=gates.device)
-        rc = _lib.load().sc_lucy_scan_bwd(
-            ptr(gates), dtype_code(gates), ptr(ckpt), ptr(dout), ptr(ds_last), ptr(dgates),
-            ptr(dh0), ptr(ds0), B, T, D, gates.stride(0), gates.stride(1), gates.stride(2),
-            dout.stride(0), dout.stride(1), dgates.stride(0), dgates.stride(1), dgates.stride(2),
-            stream_of(gates))
+        e = gates.element_size()
+        nbytes = B * T * D * 15 * e + ckpt.numel() * 4 + 3 * B * D * 4
+        with _timed("lucy_scan_bwd", gates, nbytes):
+            rc = _lib.load().sc_lucy_scan_bwd(
+                ptr(gates), dtype_code(gates), ptr(ckpt), ptr(dout), ptr(ds_last), ptr(dgates),
+                ptr(dh0), ptr(ds0), B, T, D, gates.stride(0), gates.stride(1), gates.stride(2),
+                dout.stride(0), dout.stride(1), dgates.stride(0), dgates.stride(1),
+                dgates.stride(2), stream_of(gates))
         check(rc, "sc_lucy_scan_bwd")
         hd, sd = ctx.state_dtypes
         return dgates, dh0.to(hd), ds0.to(sd)
