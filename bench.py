@@ -181,11 +181,14 @@ def main():
     kernels = {}
     for name, (tsum, n, nbytes) in kstats.items():
         avg = tsum / n
-        kernels[name] = {"launches": n, "avg_us": round(avg * 1e6, 1), "bytes_per_launch": nbytes,
-                         "achieved_GBs": round(nbytes / avg / 1e9, 1),
-                         "frac_of_peak": round(nbytes / avg / 1e9 / PEAK_HBM_GBS, 4),
+        kernels[name] = {"launches": n, "avg_us": round(avg * 1e6, 1),
                          "share_of_step": round(tsum / dt, 4)}
-    dom = max(kernels, key=lambda k: kstats[k][0]) if kernels else None
+        if nbytes:
+            kernels[name].update({"bytes_per_launch": nbytes,
+                                  "achieved_GBs": round(nbytes / avg / 1e9, 1),
+                                  "frac_of_peak": round(nbytes / avg / 1e9 / PEAK_HBM_GBS, 4)})
+    scans = [k for k in kernels if k.startswith("lucy_scan")]
+    dom = max(scans, key=lambda k: kstats[k][0]) if scans else None
     traffic = None
     pmc_file = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if dom and os.path.exists(pmc_file):

@@ -17,6 +17,7 @@
  *   sc_decay_scan_fwd <- lucyrnn_triton.py:158-177 `fused_decay_scan`, launched at
  *                        lucyrnn.py:147-151; generalised with an optional initial state
  *   sc_decay_scan_bwd <- (absent) adjoint of the above
+ *   sc_layernorm_*    <- nn.LayerNorm between layers, lucyrnn_triton.py:96-97, :136-137
  *   sc_ctc_*          <- ATen ctc_loss behind nn.CTCLoss(blank=0, zero_infinity=True),
  *                        train.py:142 / model.py:68-71
  *   sc_ctc_greedy_decode <- decoder.py:3-30 `ctc_greedy_decoder`
@@ -73,11 +74,13 @@ int sc_lucy_scan_fwd(const void* gates, int gates_dtype, const float* h0, const 
 /*
  * Backward scan.  Inputs: the forward's gates and ckpt, dout = dL/d out (same dtype as gates,
  * strides stride_d_bt/stride_d_bd), ds_last = dL/d s_out (fp32 [B,D], may be NULL = zero).
- * Outputs: dgates (gates_dtype, strides stride_dg_*), dh0, ds0 (fp32 [B,D]).
+ * Outputs: dgates (gates_dtype, strides stride_dg_*), dh0, ds0 (fp32 [B,D]) and, if dbias is
+ * not NULL, dbias fp32 [B,7,D] = sum over t of the stored dgates (per batch row; summing over
+ * b gives the gate-projection bias gradient without another pass over dgates).
  */
 int sc_lucy_scan_bwd(const void* gates, int gates_dtype, const float* ckpt,
                      const void* dout, const float* ds_last,
-                     void* dgates, float* dh0, float* ds0, int B, int T, int D,
+                     void* dgates, float* dh0, float* ds0, float* dbias, int B, int T, int D,
                      int64_t stride_g_bt, int64_t stride_g_td, int64_t stride_g_cd,
                      int64_t stride_d_bt, int64_t stride_d_bd,
                      int64_t stride_dg_bt, int64_t stride_dg_td, int64_t stride_dg_cd,
@@ -103,6 +106,29 @@ int sc_decay_scan_bwd(const void* decay, const void* s_all, const void* dout, vo
                       void* ddecay, int dtype, const float* init, float* dinit,
                       int B, int T, int D, int64_t stride_b, int64_t stride_t, int64_t stride_d,
                       void* stream);
+
+/* ---------------------------------------------------------------- LayerNorm ------------- */
+
+/*
+ * The stack's inter-layer nn.LayerNorm(D) (lucyrnn_triton.py:96-97, :136-137; eps 1e-5,
+ * biased variance) in the activation dtype with fp32 statistics.  Rows of D contiguous
+ * elements, 16-byte aligned; D must be 64 * (16 / element size) * {1, 2, 4, 8}
+ * (sc_layernorm_supported).  gamma/beta fp32 [D]; mean/rstd fp32 [rows].
+ */
+int sc_layernorm_supported(int dtype, int D);
+int sc_layernorm_fwd(const void* x, int dtype, const float* gamma, const float* beta, void* y,
+                     float* mean, float* rstd, int64_t rows, int D, float eps, void* stream);
+
+/* fp32 workspace floats needed by sc_layernorm_bwd (per-workgroup gamma/beta partial rows). */
+int64_t sc_layernorm_bwd_workspace_numel(int64_t rows, int D);
+
+/*
+ * dx (dtype of x) and dgamma_dbeta fp32 [2, D] (row 0 dgamma, row 1 dbeta; fixed-order
+ * reduction, deterministic) from x, dy and the forward's mean/rstd.
+ */
+int sc_layernorm_bwd(const void* x, const void* dy, int dtype, const float* gamma,
+                     const float* mean, const float* rstd, void* dx, float* dgamma_dbeta,
+                     float* workspace, int64_t rows, int D, void* stream);
 
 /* ---------------------------------------------------------------- CTC ------------------- */
 

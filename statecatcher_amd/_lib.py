@@ -23,11 +23,15 @@ _SIGS = {
     "sc_lucy_scan_ckpt_numel": (_i64, [_i32, _i32, _i32]),
     "sc_lucy_scan_fwd": (_i32, [_vp, _i32, _fp, _fp, _vp, _fp, _i32, _i32, _i32,
                                _i64, _i64, _i64, _i64, _i64, _fp, _vp]),
-    "sc_lucy_scan_bwd": (_i32, [_vp, _i32, _fp, _vp, _fp, _vp, _fp, _fp, _i32, _i32, _i32,
+    "sc_lucy_scan_bwd": (_i32, [_vp, _i32, _fp, _vp, _fp, _vp, _fp, _fp, _fp, _i32, _i32, _i32,
                                _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _vp]),
     "sc_decay_scan_fwd": (_i32, [_vp, _vp, _vp, _i32, _fp, _i32, _i32, _i32, _i64, _i64, _i64, _vp]),
     "sc_decay_scan_bwd": (_i32, [_vp, _vp, _vp, _vp, _vp, _i32, _fp, _fp, _i32, _i32, _i32,
                                 _i64, _i64, _i64, _vp]),
+    "sc_layernorm_supported": (_i32, [_i32, _i32]),
+    "sc_layernorm_fwd": (_i32, [_vp, _i32, _fp, _fp, _vp, _fp, _fp, _i64, _i32, _c.c_float, _vp]),
+    "sc_layernorm_bwd_workspace_numel": (_i64, [_i64, _i32]),
+    "sc_layernorm_bwd": (_i32, [_vp, _vp, _i32, _fp, _fp, _fp, _vp, _fp, _fp, _i64, _i32, _vp]),
     "sc_ctc_workspace_bytes": (_c.c_size_t, [_i32, _i32, _i32]),
     "sc_ctc_fwd": (_i32, [_vp, _i32, _i32, _i32, _i32, _i32, _i64, _i64, _vp, _i64, _i32, _vp, _vp,
                          _i32, _fp, _vp, _c.c_size_t, _vp]),

@@ -9,76 +9,80 @@
 // log_softmax is fused (is_logits=1).  The time axis is never transposed: x stays [B,T,V].
 //
 // Kernels (all on the caller's stream):
-//   ctc_lse_kernel      one wave per (b,t) row: log-sum-exp over V (skipped for log-probs)
-//   ctc_chain_kernel    per b: for every target position the next position with the same
-//                       label, so label occupancies are summed in a fixed order (bitwise
-//                       deterministic, no atomics)
-//   ctc_ab_kernel       2B workgroups, one state per lane: B run alpha forward in time, B run
-//                       beta backward, concurrently; emissions x[b,t,label(s)] for the next 8
-//                       steps are gathered into registers while the current 8 steps compute
-//   ctc_grad_kernel     one workgroup per (b,t) row: label occupancies into an LDS row of V
-//                       log-sums, then one coalesced pass writing the gradient row
+//   ctc_emit_kernel   one wave per (b,t) row: log-sum-exp over V (logits only), then the
+//                     emission log-probs of the row's 2U+1 states, base 2, into lpe[b,t,:]
+//   ctc_chain_kernel  per b: for every target position the next position with the same label,
+//                     so label occupancies are summed in a fixed order (deterministic, no atomics)
+//   ctc_ab_kernel     one workgroup per (sequence, direction): 2B workgroups run alpha forward
+//                     and beta backward concurrently.  One state per lane; each wave also
+//                     carries a 2K-state halo of its neighbour's states so it advances K steps
+//                     with DPP wave_shr:1 / wave_shl:1 only (no LDS, no barrier), then exchanges
+//                     halos through LDS.  Emission rows are prefetched 16 steps ahead.
+//                     Values live in base-2 log space with a finite "dead" sentinel (branch-free
+//                     log-sum-exp) and are re-centred on the workgroup max every 16 steps; the
+//                     running offset is kept in fp64 (at T=1500 |alpha| ~ 1e4, where an fp32
+//                     ulp would put ~0.5% error into the posteriors).
+//   ctc_grad_kernel   one workgroup per (b,t) row: label occupancies into an LDS row of V
+//                     log-sums, then one coalesced pass writing the gradient row
 #include "sc_common.h"
 
 namespace sc {
 
-constexpr int kCtcP = 8;           // emission prefetch depth (steps)
-constexpr int kCtcMaxStates = 1024;
 constexpr float kNegInf = -__builtin_huge_valf();
 
-// alpha/beta are stored NORMALISED: stored_t(s) = alpha_t(s) - offA_t where offA_t (fp64) is
-// the running sum of the per-step maxima.  At T=1500 |alpha| reaches ~1e4, where an fp32 ulp is
-// ~1e-3: un-normalised fp32 lattices put ~0.5% error into exp(alpha+beta+nll-lp).  With the
-// offsets in fp64 the posterior exponent is formed from O(10) fp32 terms.
 struct CtcWs {
-  float* lse;
-  float* alpha;
-  float* beta;
-  double* offA;   // [B,T]
+  float* lse;     // [B,T]      natural-log row normaliser (logits input)
+  float* lpe;     // [B,T,Sp]   base-2 emission log-probs of the blank-extended states
+  float* alpha;   // [B,T,Sp]   base-2, relative to offA
+  float* beta;    // [B,T,Sp]   base-2, relative to offB
+  double* offA;   // [B,T]      base-2 offsets
   double* offB;   // [B,T]
-  double* nll64;  // [B]
-  int* chain;
-  int* first;
+  double* nll64;  // [B]        natural log
+  int* chain;     // [B,Um]
+  int* first;     // [B,Um]
 };
 
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-static CtcWs carve(void* ws, int B, int T, int S, int Um) {
-  char* p = (char*)ws;
-  CtcWs w;
-  w.lse = (float*)p; p += align256((size_t)B * T * 4);
-  w.alpha = (float*)p; p += align256((size_t)B * T * S * 4);
-  w.beta = (float*)p; p += align256((size_t)B * T * S * 4);
-  w.offA = (double*)p; p += align256((size_t)B * T * 8);
-  w.offB = (double*)p; p += align256((size_t)B * T * 8);
-  w.nll64 = (double*)p; p += align256((size_t)B * 8);
-  w.chain = (int*)p; p += align256((size_t)B * Um * 4);
-  w.first = (int*)p;
-  return w;
-}
+// states per lane for a given max state count
+static int states_per_lane(int S) { return (S + 63) / 64; }
 
-static size_t ws_bytes(int B, int T, int Umax) {
+static size_t ws_layout(int B, int T, int Umax, CtcWs* w, void* base) {
   const int S = 2 * Umax + 1;
+  const int Sp = 64 * states_per_lane(S);
   const int Um = Umax > 0 ? Umax : 1;
-  return align256((size_t)B * T * 4) + 2 * align256((size_t)B * T * S * 4) +
-         2 * align256((size_t)B * T * 8) + align256((size_t)B * 8) + 2 * align256((size_t)B * Um * 4);
+  char* p = (char*)base;
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    char* r = p + off;
+    off += align256(bytes);
+    return (void*)r;
+  };
+  CtcWs t;
+  t.lse = (float*)take((size_t)B * T * 4);
+  t.lpe = (float*)take((size_t)B * T * Sp * 4);
+  t.alpha = (float*)take((size_t)B * T * Sp * 4);
+  t.beta = (float*)take((size_t)B * T * Sp * 4);
+  t.offA = (double*)take((size_t)B * T * 8);
+  t.offB = (double*)take((size_t)B * T * 8);
+  t.nll64 = (double*)take((size_t)B * 8);
+  t.chain = (int*)take((size_t)B * Um * 4);
+  t.first = (int*)take((size_t)B * Um * 4);
+  if (w) *w = t;
+  return off;
 }
 
-__device__ __forceinline__ float lse2(float a, float b) {
+// log2(2^a + 2^b), base-2 log-sum-exp
+__device__ __forceinline__ float lse2_b2(float a, float b) {
   const float m = fmaxf(a, b);
   if (m == kNegInf) return kNegInf;
-  return m + flog(fexp(a - m) + fexp(b - m));
+  return m + log2_(exp2_(a - m) + exp2_(b - m));
 }
 
-__device__ __forceinline__ float lse3(float a, float b, float c) {
-  const float m = fmaxf(fmaxf(a, b), c);
-  if (m == kNegInf) return kNegInf;
-  return m + flog(fexp(a - m) + fexp(b - m) + fexp(c - m));
-}
 
 struct CtcArgs {
   const void* x;
-  int is_logits, B, T, V, S, Umax, blank;
+  int is_logits, B, T, V, S, Sp, Umax, blank;
   int64_t sb, stt;
   const int64_t* tg;
   int64_t tgs;
@@ -94,32 +98,52 @@ __device__ __forceinline__ int clampi(int64_t v, int lo, int hi) {
   return (int)(v < lo ? lo : (v > hi ? hi : v));
 }
 
-// ---------------------------------------------------------------------------- lse -----------
+// label of blank-extended state s (clamped into [0, V) so no load leaves the row; out-of-range
+// targets are undefined input, as in ATen)
+__device__ __forceinline__ int state_label(const int64_t* tg, int s, int blank, int V) {
+  int lab = (s & 1) ? (int)tg[(s - 1) >> 1] : blank;
+  return lab < 0 ? 0 : (lab >= V ? V - 1 : lab);
+}
+
+// ---------------------------------------------------------------------------- emissions -----
 template <int DT>
-__global__ void __launch_bounds__(256) ctc_lse_kernel(CtcArgs a) {
+__global__ void __launch_bounds__(256) ctc_emit_kernel(CtcArgs a) {
   using E = Elem<DT>;
   using T = typename E::T;
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= (int64_t)a.B * a.T) return;
   const int b = (int)(row / a.T), t = (int)(row % a.T);
+  if (t >= clampi(a.in_lens[b], 0, a.T)) return;     // rows past in_len are never read
   const T* p = (const T*)a.x + (int64_t)b * a.sb + (int64_t)t * a.stt;
-  float m = kNegInf, l = 0.0f;
-  for (int v = lane; v < a.V; v += 64) {
-    const float xv = E::ld(p[v]);
-    const float mn = fmaxf(m, xv);
-    l = l * fexp(m - mn) + fexp(xv - mn);
-    m = mn;
-  }
+  float lse = 0.0f;
+  if (a.is_logits) {
+    float m = kNegInf, l = 0.0f;
+    for (int v = lane; v < a.V; v += 64) {
+      const float xv = E::ld(p[v]);
+      const float mn = fmaxf(m, xv);
+      l = l * fexp(m - mn) + fexp(xv - mn);
+      m = mn;
+    }
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const float mo = __shfl_xor(m, o);
-    const float lo = __shfl_xor(l, o);
-    const float mn = fmaxf(m, mo);
-    l = (mn == kNegInf) ? 0.0f : l * fexp(m - mn) + lo * fexp(mo - mn);
-    m = mn;
+    for (int o = 32; o > 0; o >>= 1) {
+      const float mo = __shfl_xor(m, o);
+      const float lo = __shfl_xor(l, o);
+      const float mn = fmaxf(m, mo);
+      l = (mn == kNegInf) ? 0.0f : l * fexp(m - mn) + lo * fexp(mo - mn);
+      m = mn;
+    }
+    lse = m + flog(l);
+    if (lane == 0) a.ws.lse[row] = lse;
   }
-  if (lane == 0) a.ws.lse[row] = m + flog(l);
+  const int Sb = 2 * clampi(a.tgt_lens[b], 0, a.Umax) + 1;
+  const int64_t* tg = a.tg + (int64_t)b * a.tgs;
+  float* out = a.ws.lpe + row * a.Sp;
+  for (int s = lane; s < a.Sp; s += 64) {
+    float v = -1e30f;
+    if (s < Sb) v = fmaxf((E::ld(p[state_label(tg, s, a.blank, a.V)]) - lse) * kLog2e, -1e30f);
+    out[s] = v;
+  }
 }
 
 // ---------------------------------------------------------------------------- chains --------
@@ -144,113 +168,169 @@ __global__ void __launch_bounds__(256) ctc_chain_kernel(CtcArgs a) {
 }
 
 // ---------------------------------------------------------------------------- alpha / beta --
-template <int DT>
+__device__ __forceinline__ float shr1(float v) {   // value of lane-1 (lane 0: dead)
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(-1e30f), __float_as_int(v),
+                                                     0x138, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float shl1(float v) {   // value of lane+1 (lane 63: dead)
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(-1e30f), __float_as_int(v),
+                                                     0x130, 0xf, 0xf, false));
+}
+
+// Branch-free log2-sum-exp for the lattice: "dead" states carry kDead (finite), so no -inf
+// test is needed; exp2 of anything ~kDead below the max is exactly 0.
+constexpr float kDead = -1e30f;
+__device__ __forceinline__ float lse3_live(float a, float b, float c) {
+  const float m = fmaxf(fmaxf(a, b), c);
+  return m + log2_(exp2_(a - m) + exp2_(b - m) + exp2_(c - m));
+}
+
+constexpr int kAbP = 16;   // emission prefetch depth (steps)
+
+// One workgroup per (sequence, direction).  Wave w computes 64 consecutive states: OW = 64 - 2K
+// of them it OWNS, plus a halo of 2K states owned by the neighbouring wave (left for alpha,
+// right for beta).  A missing neighbour corrupts at most 2 more lanes of the halo per step
+// (s-1, s-2 dependencies), so for K steps the owned states stay exact with no communication:
+// in-wave neighbours come from DPP wave_shr:1 / wave_shl:1, and only every K steps the owned
+// states are published to LDS, one barrier, halo lanes re-read theirs (and every second such
+// exchange re-centres on the workgroup max).
+template <int K>
 __global__ void __launch_bounds__(1024) ctc_ab_kernel(CtcArgs a) {
-  using E = Elem<DT>;
-  using T = typename E::T;
-  extern __shared__ __attribute__((aligned(16))) float sm[];
+  constexpr int H = 2 * K;        // halo lanes
+  constexpr int OW = 64 - H;      // owned states per wave
   const bool is_beta = blockIdx.x >= a.B;
   const int b = is_beta ? blockIdx.x - a.B : blockIdx.x;
-  const int s = threadIdx.x;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int w = uniform(tid >> 6);
+  const int nw = blockDim.x >> 6;
   const int Tb = clampi(a.in_lens[b], 0, a.T);
   const int Ub = clampi(a.tgt_lens[b], 0, a.Umax);
   const int Sb = 2 * Ub + 1;
-  const bool act = s < Sb;
+  if (Tb == 0) {
+    if (!is_beta && tid == 0) {
+      a.nll[b] = (Ub == 0) ? 0.0f : __builtin_huge_valf();
+      a.ws.nll64[b] = (Ub == 0) ? 0.0 : __builtin_huge_val();
+    }
+    return;
+  }
+  // state of this lane and whether this lane owns it
+  const int s = is_beta ? w * OW + lane : w * OW + lane - H;
+  const bool own = is_beta ? (lane < OW) : (lane >= H);
+  const bool live = s >= 0 && s < Sb;
   const int64_t* tg = a.tg + (int64_t)b * a.tgs;
-  int lab = a.blank;
-  bool skip = false;   // alpha: transition s-2 -> s;  beta: transition s+2 -> s
-  if (act && (s & 1)) lab = (int)tg[(s - 1) >> 1];
-  // out-of-range labels are undefined input (as in ATen); clamp so no load leaves the row
-  const int labc = lab < 0 ? 0 : (lab >= a.V ? a.V - 1 : lab);
-  if (act) {
+  bool skip = false;   // alpha: s-2 -> s allowed;  beta: s+2 -> s allowed
+  if (live && (s & 1)) {
+    const int lab = (int)tg[(s - 1) >> 1];
     if (!is_beta) {
-      skip = (s & 1) && s >= 3 && lab != a.blank && lab != (int)tg[(s - 3) >> 1];
-    } else if (s + 2 < Sb && !(s & 1)) {
-      skip = false;
+      skip = s >= 3 && lab != a.blank && lab != (int)tg[(s - 3) >> 1];
     } else if (s + 2 < Sb) {
       const int l2 = (int)tg[(s + 1) >> 1];
       skip = l2 != a.blank && l2 != lab;
     }
   }
-  float* buf0 = sm;
-  float* buf1 = sm + blockDim.x;
-  float* outp = (is_beta ? a.ws.beta : a.ws.alpha) + (int64_t)b * a.T * a.S;
-  if (Tb == 0) {
-    if (!is_beta && s == 0) a.nll[b] = (Ub == 0) ? 0.0f : __builtin_huge_valf();
-    return;
-  }
-  const T* xb = (const T*)a.x + (int64_t)b * a.sb + (act ? labc : 0);
-  const float* lse = a.ws.lse + (int64_t)b * a.T;
-  // time index of the i-th processed step
-  auto tstep = [&](int i) { return is_beta ? Tb - 1 - i : i; };
-  T cx[kCtcP], nx[kCtcP];
-  float cl[kCtcP], nl[kCtcP];
-  auto load = [&](T (&xr)[kCtcP], float (&lr)[kCtcP], int i0) {
-#pragma unroll
-    for (int j = 0; j < kCtcP; ++j) {
-      const int i = min(i0 + j, Tb - 1);
-      const int t = tstep(i);
-      xr[j] = xb[(int64_t)t * a.stt];
-      lr[j] = a.is_logits ? lse[t] : 0.0f;
-    }
-  };
-  load(cx, cl, 0);
-  float* prev = buf0;
-  float* cur = buf1;
-  __shared__ float wmax[2][16];
-  const int lane = s & 63, wv = s >> 6, nwv = blockDim.x >> 6;
+  extern __shared__ __attribute__((aligned(16))) float full[];   // [2][nw*OW] published states
+  __shared__ float wmax[16];
+  const int nst = nw * OW;
+  const int sc = s < 0 ? 0 : (s >= a.Sp ? a.Sp - 1 : s);   // clamped for addressing only
+  const float* lrow = a.ws.lpe + (int64_t)b * a.T * a.Sp + sc;
+  float* orow = (is_beta ? a.ws.beta : a.ws.alpha) + (int64_t)b * a.T * a.Sp + sc;
   double* offp = (is_beta ? a.ws.offB : a.ws.offA) + (int64_t)b * a.T;
-  double off = 0.0;   // log-offset of the values in `prev` (all threads hold the same value)
-  float mprev = 0.0f; // max of the previous step, already folded into `off`
-  for (int i0 = 0; i0 < Tb; i0 += kCtcP) {
-    if (i0 + kCtcP < Tb) load(nx, nl, i0 + kCtcP);
+  auto tstep = [&](int i) { return is_beta ? Tb - 1 - i : i; };
+  float bufA[kAbP], bufB[kAbP];
+  auto load = [&](float (&buf)[kAbP], int i0) {
 #pragma unroll
-    for (int j = 0; j < kCtcP; ++j) {
+    for (int j = 0; j < kAbP; ++j) buf[j] = lrow[(int64_t)tstep(min(i0 + j, Tb - 1)) * a.Sp];
+  };
+  float v = kDead;
+  double off = 0.0;
+  int exch = 0;
+  auto body = [&](const float (&buf)[kAbP], int i0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < kAbP; ++j) {
       const int i = i0 + j;
       if (i >= Tb) break;
       const int t = tstep(i);
-      const float lp = E::ld(cx[j]) - cl[j];
-      float v;
+      const float lp = live ? buf[j] : kDead;
       if (i == 0) {
-        v = (act && (is_beta ? (s >= Sb - 2) : (s <= 1))) ? lp : kNegInf;
-      } else if (!act) {
-        v = kNegInf;
+        const bool init = is_beta ? (s >= Sb - 2) : (s <= 1);
+        v = (live && init) ? lp : kDead;
       } else if (!is_beta) {
-        const float a1 = s > 0 ? prev[s - 1] : kNegInf;
-        const float a2 = skip ? prev[s - 2] : kNegInf;
-        v = lse3(prev[s], a1, a2) - mprev + lp;
+        const float p1 = shr1(v);
+        const float p2 = shr1(p1);
+        v = lse3_live(v, p1, skip ? p2 : kDead) + lp;
       } else {
-        const float b1 = s + 1 < Sb ? prev[s + 1] : kNegInf;
-        const float b2 = skip ? prev[s + 2] : kNegInf;
-        v = lse3(prev[s], b1, b2) - mprev + lp;
+        const float q1 = shl1(v);
+        const float q2 = shl1(q1);
+        v = lse3_live(v, q1, skip ? q2 : kDead) + lp;
       }
-      cur[s] = v;
-      if (act) outp[(int64_t)t * a.S + s] = v;
-      if (s == 0) offp[t] = off;
-      float mx = v;
+      if (j % K == K - 1) {   // halo exchange (+ re-centre every second one)
+        const int par = exch & 1;
+        const bool norm = par == 1;
+        if (own) full[par * nst + s] = v;
+        if (norm) {
+          float m = own ? v : kDead;
 #pragma unroll
-      for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
-      if (lane == 0) wmax[i & 1][wv] = mx;
-      lds_barrier();
-      float m = kNegInf;
-      for (int q = 0; q < nwv; ++q) m = fmaxf(m, wmax[i & 1][q]);
-      mprev = (m == kNegInf) ? 0.0f : m;
-      off += (double)mprev;
-      float* tmp = prev; prev = cur; cur = tmp;
+          for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+          if (lane == 0) wmax[w] = m;
+        }
+        lds_barrier();
+        if (!own) {
+          const bool has = s >= 0 && s < nst;
+          v = has ? full[par * nst + s] : kDead;
+        }
+        if (norm) {
+          float m = kDead;
+          for (int q = 0; q < nw; ++q) m = fmaxf(m, wmax[q]);
+          if (m > 0.5f * kDead) {   // all dead (infeasible): keep the sentinel
+            v -= m;
+            off += (double)m;
+          }
+        }
+        ++exch;
+      }
+      if (own && s < a.Sp) orow[(int64_t)t * a.Sp] = v;
+      if (tid == 0) offp[t] = off;
     }
+  };
+  load(bufA, 0);
+  for (int i0 = 0; i0 < Tb; i0 += 2 * kAbP) {
+    load(bufB, i0 + kAbP);
+    body(bufA, i0);
+    if (i0 + kAbP >= Tb) break;
+    load(bufA, i0 + 2 * kAbP);
+    body(bufB, i0 + kAbP);
+  }
+  if (!is_beta) {
+    // log p = log2sum(alpha_{Tb-1}(Sb-1), alpha_{Tb-1}(Sb-2)) + off, gathered over the workgroup
+    float c = (own && (s == Sb - 1 || s == Sb - 2)) ? v : kDead;
 #pragma unroll
-    for (int j = 0; j < kCtcP; ++j) {
-      cx[j] = nx[j];
-      cl[j] = nl[j];
+    for (int o = 32; o > 0; o >>= 1) {
+      const float co = __shfl_xor(c, o);
+      const float m = fmaxf(c, co);
+      c = m + log2_(exp2_(c - m) + exp2_(co - m));
+    }
+    lds_barrier();
+    if (lane == 0) wmax[w] = c;
+    lds_barrier();
+    if (tid == 0) {
+      float cc = kDead;
+      for (int q = 0; q < nw; ++q) {
+        const float m = fmaxf(cc, wmax[q]);
+        cc = m + log2_(exp2_(cc - m) + exp2_(wmax[q] - m));
+      }
+      const double nll = (cc < 0.5f * kDead) ? __builtin_huge_val() : -((double)cc + off) * (double)kLn2;
+      a.ws.nll64[b] = nll;
+      a.nll[b] = (float)nll;
     }
   }
-  if (!is_beta && s == 0) {
-    // prev holds the last step relative to off - mprev
-    const float ll = Sb > 1 ? lse2(prev[Sb - 1], prev[Sb - 2]) : prev[0];
-    const double nll = (ll == kNegInf) ? __builtin_huge_val() : -((double)ll + (off - (double)mprev));
-    a.ws.nll64[b] = nll;
-    a.nll[b] = (float)nll;
-  }
+}
+
+// K (steps between halo exchanges) so that ceil(S / (64 - 2K)) waves fit a 1024-thread group
+static int ab_halo_k(int S) {
+  for (int K : {8, 4, 2, 1})
+    if ((S + (64 - 2 * K) - 1) / (64 - 2 * K) <= 16) return K;
+  return 0;
 }
 
 // ---------------------------------------------------------------------------- gradient ------
@@ -258,7 +338,7 @@ template <int DT, int GT>
 __global__ void __launch_bounds__(256) ctc_grad_kernel(CtcArgs a) {
   using E = Elem<DT>;
   using G = Elem<GT>;
-  extern __shared__ __attribute__((aligned(16))) float lcab[];   // V log-sums + 8 (m,l) pairs
+  extern __shared__ __attribute__((aligned(16))) float lcab[];   // V base-2 log-sums + 8 (m,l)
   const int b = blockIdx.x / a.T, t = blockIdx.x % a.T;
   const int tid = threadIdx.x;
   const int Tb = clampi(a.in_lens[b], 0, a.T);
@@ -274,39 +354,38 @@ __global__ void __launch_bounds__(256) ctc_grad_kernel(CtcArgs a) {
   const int64_t* tg = a.tg + (int64_t)b * a.tgs;
   for (int v = tid; v < a.V; v += 256) lcab[v] = kNegInf;
   __syncthreads();
-  const float* al = a.ws.alpha + ((int64_t)b * a.T + t) * a.S;
-  const float* be = a.ws.beta + ((int64_t)b * a.T + t) * a.S;
-  // exp(lcab + nll - lp) with lcab = lse(stored) + offA + offB: fold the fp64 offsets first
+  const float* al = a.ws.alpha + ((int64_t)b * a.T + t) * a.Sp;
+  const float* be = a.ws.beta + ((int64_t)b * a.T + t) * a.Sp;
+  // exp(lcab + nll - lp) = 2^(lcab2 + offA + offB + nll*log2e - lp*log2e): fold offsets in fp64
   const float koff = (float)(a.ws.offA[(int64_t)b * a.T + t] + a.ws.offB[(int64_t)b * a.T + t] +
-                             a.ws.nll64[b]);
+                             a.ws.nll64[b] * (double)kLog2e);
   const int* chain = a.ws.chain + (int64_t)b * Um;
   const int* first = a.ws.first + (int64_t)b * Um;
-  float m = kNegInf, l = 0.0f;   // blank-label occupancy, per thread
+  float m = kNegInf, l = 0.0f;   // blank-label occupancy (base 2), per thread
   for (int s = tid; s < Sb; s += 256) {
     const int lab = (s & 1) ? (int)tg[(s - 1) >> 1] : a.blank;
     const float val = al[s] + be[s];
     if (lab == a.blank) {
       const float mn = fmaxf(m, val);
       if (mn != kNegInf) {
-        l = l * fexp(m - mn) + fexp(val - mn);
+        l = l * exp2_(m - mn) + exp2_(val - mn);
         m = mn;
       }
     } else {
       const int u = (s - 1) >> 1;
       if (first[u]) {
         float acc = val;
-        for (int q = chain[u]; q >= 0; q = chain[q]) acc = lse2(acc, al[2 * q + 1] + be[2 * q + 1]);
+        for (int q = chain[u]; q >= 0; q = chain[q]) acc = lse2_b2(acc, al[2 * q + 1] + be[2 * q + 1]);
         if (lab >= 0 && lab < a.V) lcab[lab] = acc;
       }
     }
   }
-  // block reduce of the blank (m, l)
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     const float mo = __shfl_xor(m, o);
     const float lo = __shfl_xor(l, o);
     const float mn = fmaxf(m, mo);
-    l = (mn == kNegInf) ? 0.0f : l * fexp(m - mn) + lo * fexp(mo - mn);
+    l = (mn == kNegInf) ? 0.0f : l * exp2_(m - mn) + lo * exp2_(mo - mn);
     m = mn;
   }
   float* red = lcab + a.V;
@@ -321,30 +400,35 @@ __global__ void __launch_bounds__(256) ctc_grad_kernel(CtcArgs a) {
     for (int q = 0; q < 4; ++q) {
       const float mo = red[2 * q], lo = red[2 * q + 1];
       const float mn = fmaxf(M, mo);
-      L = (mn == kNegInf) ? 0.0f : L * fexp(M - mn) + lo * fexp(mo - mn);
+      L = (mn == kNegInf) ? 0.0f : L * exp2_(M - mn) + lo * exp2_(mo - mn);
       M = mn;
     }
-    if (a.blank >= 0 && a.blank < a.V) lcab[a.blank] = (M == kNegInf) ? kNegInf : M + flog(L);
+    if (a.blank >= 0 && a.blank < a.V) lcab[a.blank] = (M == kNegInf) ? kNegInf : M + log2_(L);
   }
   __syncthreads();
   const typename E::T* xr = (const typename E::T*)a.x + (int64_t)b * a.sb + (int64_t)t * a.stt;
   const float lse = a.is_logits ? a.ws.lse[(int64_t)b * a.T + t] : 0.0f;
   for (int v = tid; v < a.V; v += 256) {
-    const float lp = E::ld(xr[v]) - lse;
-    const float gv = fexp(lp) - fexp(lcab[v] + koff - lp);
+    const float lp2 = (E::ld(xr[v]) - lse) * kLog2e;
+    const float gv = exp2_(lp2) - exp2_(lcab[v] + koff - lp2);
     g[v] = G::st(gv * sc);
   }
 }
 
 template <int DT>
 static void launch_fwd(const CtcArgs& a, hipStream_t st) {
-  if (a.is_logits) {
-    const int64_t rows = (int64_t)a.B * a.T;
-    hipLaunchKernelGGL((ctc_lse_kernel<DT>), dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, a);
-  }
+  const int64_t rows = (int64_t)a.B * a.T;
+  hipLaunchKernelGGL((ctc_emit_kernel<DT>), dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, a);
   hipLaunchKernelGGL(ctc_chain_kernel, dim3(a.B), dim3(256), 0, st, a);
-  const int nthr = ((a.S + 63) / 64) * 64;
-  hipLaunchKernelGGL((ctc_ab_kernel<DT>), dim3(2 * a.B), dim3(nthr), 2 * nthr * sizeof(float), st, a);
+  const int K = ab_halo_k(a.S);
+  const int nw = (a.S + (64 - 2 * K) - 1) / (64 - 2 * K);
+  const size_t sh = 2 * (size_t)nw * (64 - 2 * K) * sizeof(float);
+  switch (K) {
+    case 8: hipLaunchKernelGGL((ctc_ab_kernel<8>), dim3(2 * a.B), dim3(64 * nw), sh, st, a); break;
+    case 4: hipLaunchKernelGGL((ctc_ab_kernel<4>), dim3(2 * a.B), dim3(64 * nw), sh, st, a); break;
+    case 2: hipLaunchKernelGGL((ctc_ab_kernel<2>), dim3(2 * a.B), dim3(64 * nw), sh, st, a); break;
+    default: hipLaunchKernelGGL((ctc_ab_kernel<1>), dim3(2 * a.B), dim3(64 * nw), sh, st, a); break;
+  }
 }
 
 template <int DT, int GT>
@@ -359,25 +443,52 @@ using namespace sc;
 
 extern "C" size_t sc_ctc_workspace_bytes(int B, int T, int max_target_len) {
   if (B <= 0 || T <= 0 || max_target_len < 0) return 256;
-  return ws_bytes(B, T, max_target_len);
+  return ws_layout(B, T, max_target_len, nullptr, nullptr);
 }
 
 static int ctc_check(const void* x, int x_dtype, int B, int T, int V, int max_target_len,
                      const int64_t* targets, const int64_t* in_lens, const int64_t* tgt_lens,
-                     int blank, void* ws, size_t wsb, const char* who) {
+                     int blank, const void* ws, size_t wsb, const char* who) {
   SC_REQUIRE(x_dtype == SC_F32 || x_dtype == SC_BF16 || x_dtype == SC_F16,
              "%s: unsupported dtype %d", who, x_dtype);
   SC_REQUIRE(B >= 0 && T >= 0 && V > 0 && max_target_len >= 0, "%s: bad shape", who);
-  SC_REQUIRE(2 * max_target_len + 1 <= kCtcMaxStates,
-             "%s: max target length %d exceeds %d", who, max_target_len, (kCtcMaxStates - 1) / 2);
+  SC_REQUIRE(ab_halo_k(2 * max_target_len + 1) > 0,
+             "%s: max target length %d exceeds %d", who, max_target_len, (16 * 62 - 1) / 2);
   SC_REQUIRE(blank >= 0 && blank < V, "%s: blank %d outside [0, %d)", who, blank, V);
   SC_REQUIRE((int64_t)B * T <= 0x7fffffff, "%s: B*T too large", who);
   if (B == 0 || T == 0) return 0;
   SC_REQUIRE(x && in_lens && tgt_lens && ws, "%s: null pointer", who);
   SC_REQUIRE(max_target_len == 0 || targets, "%s: null targets", who);
-  SC_REQUIRE(wsb >= ws_bytes(B, T, max_target_len), "%s: workspace %zu < %zu bytes", who, wsb,
-             ws_bytes(B, T, max_target_len));
+  const size_t need = ws_layout(B, T, max_target_len, nullptr, nullptr);
+  SC_REQUIRE(wsb >= need, "%s: workspace %zu < %zu bytes", who, wsb, need);
   return 0;
+}
+
+static CtcArgs make_args(const void* x, int is_logits, int B, int T, int V, int64_t sb, int64_t st,
+                         const int64_t* targets, int64_t tgs, int umax, const int64_t* in_lens,
+                         const int64_t* tgt_lens, int blank, float* nll, const void* ws,
+                         const float* scale, void* grad) {
+  CtcArgs a;
+  a.x = x;
+  a.is_logits = is_logits;
+  a.B = B;
+  a.T = T;
+  a.V = V;
+  a.S = 2 * umax + 1;
+  a.Sp = 64 * states_per_lane(a.S);
+  a.Umax = umax;
+  a.blank = blank;
+  a.sb = sb;
+  a.stt = st;
+  a.tg = targets;
+  a.tgs = tgs;
+  a.in_lens = in_lens;
+  a.tgt_lens = tgt_lens;
+  a.nll = nll;
+  ws_layout(B, T, umax, &a.ws, (void*)ws);
+  a.scale = scale;
+  a.grad = grad;
+  return a;
 }
 
 extern "C" int sc_ctc_fwd(const void* x, int x_dtype, int is_logits, int B, int T, int V,
@@ -391,13 +502,9 @@ extern "C" int sc_ctc_fwd(const void* x, int x_dtype, int is_logits, int B, int 
   if (rc) return rc;
   if (B == 0) return 0;
   SC_REQUIRE(nll, "sc_ctc_fwd: null nll");
-  if (T == 0) {
-    SC_REQUIRE(false, "sc_ctc_fwd: T == 0 is handled by the caller");
-  }
-  const int S = 2 * max_target_len + 1;
-  CtcArgs a{x, is_logits, B, T, V, S, max_target_len, blank, stride_b, stride_t, targets,
-            target_stride, in_lens, tgt_lens, nll, carve(workspace, B, T, S, max_target_len > 0 ? max_target_len : 1),
-            nullptr, nullptr};
+  SC_REQUIRE(T > 0, "sc_ctc_fwd: T == 0 is handled by the caller");
+  CtcArgs a = make_args(x, is_logits, B, T, V, stride_b, stride_t, targets, target_stride,
+                        max_target_len, in_lens, tgt_lens, blank, nll, workspace, nullptr, nullptr);
   hipStream_t st = (hipStream_t)stream;
   switch (x_dtype) {
     case SC_F32: launch_fwd<SC_F32>(a, st); break;
@@ -415,16 +522,15 @@ extern "C" int sc_ctc_bwd(const void* x, int x_dtype, int is_logits, int B, int 
                           size_t workspace_bytes, void* stream) {
   clear_error();
   int rc = ctc_check(x, x_dtype, B, T, V, max_target_len, targets, in_lens, tgt_lens, blank,
-                     (void*)workspace, workspace_bytes, "sc_ctc_bwd");
+                     workspace, workspace_bytes, "sc_ctc_bwd");
   if (rc) return rc;
   if (B == 0 || T == 0) return 0;
   SC_REQUIRE(grad_dtype == SC_F32 || grad_dtype == SC_BF16 || grad_dtype == SC_F16,
              "sc_ctc_bwd: unsupported grad dtype %d", grad_dtype);
   SC_REQUIRE(nll && scale && grad, "sc_ctc_bwd: null pointer");
-  const int S = 2 * max_target_len + 1;
-  CtcArgs a{x, is_logits, B, T, V, S, max_target_len, blank, stride_b, stride_t, targets,
-            target_stride, in_lens, tgt_lens, (float*)nll,
-            carve((void*)workspace, B, T, S, max_target_len > 0 ? max_target_len : 1), scale, grad};
+  CtcArgs a = make_args(x, is_logits, B, T, V, stride_b, stride_t, targets, target_stride,
+                        max_target_len, in_lens, tgt_lens, blank, (float*)nll, workspace, scale,
+                        grad);
   hipStream_t st = (hipStream_t)stream;
 #define SC_CTC_BWD(DT)                                               \
   switch (grad_dtype) {                                              \

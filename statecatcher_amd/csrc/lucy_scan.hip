@@ -60,6 +60,7 @@ struct ScanBwdArgs {
   void* dgates;
   float* dh0;
   float* ds0;
+  float* dbias;   // optional [B,7,D]: sum over t of dgates (gate-projection bias gradient part)
   int B, T, D, nsc;
   int64_t g_bt, g_td, g_cd, d_bt, d_bd, dg_bt, dg_td, dg_cd;
 };
@@ -276,6 +277,7 @@ lucy_scan_bwd_kernel(ScanBwdArgs a) {
       db[j] = dbuf.ldw(vg, t * dtd);
     }
   };
+  float bacc[7] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};   // bias-gradient partial sums
   auto body = [&](const uint32_t (&cur)[LC][7], const uint32_t (&dcur)[LC], const float (&ck)[2],
                   int it) __attribute__((always_inline)) {
     const int k = a.nsc - 1 - it;
@@ -378,7 +380,11 @@ lucy_scan_bwd_kernel(ScanBwdArgs a) {
                    stH[w][j][lane], stS[w][j][lane], x[j], o);
         const uint32_t so = (uint32_t)(t0 + j) * otd;
 #pragma unroll
-        for (int g = 0; g < 7; ++g) obuf.st(E::st(o[g]), vo, so + g * ocd);
+        for (int g = 0; g < 7; ++g) {
+          const T og = E::st(o[g]);
+          obuf.st(og, vo, so + g * ocd);
+          bacc[g] += E::ld(og);   // sum what is stored, so db == dgates.sum() exactly as a GEMM sees it
+        }
       }
     }
     if (w == 0) carGs[(it + 1) & 1][lane] = Cs;
@@ -396,6 +402,19 @@ lucy_scan_bwd_kernel(ScanBwdArgs a) {
   if (w == 0 && dok) {
     a.dh0[(int64_t)b * a.D + d] = carGh[a.nsc & 1][lane];
     a.ds0[(int64_t)b * a.D + d] = carGs[a.nsc & 1][lane];
+  }
+  if (a.dbias) {   // reduce the per-wave partials over the NW waves (fixed order: deterministic)
+#pragma unroll
+    for (int g = 0; g < 7; ++g) {
+      stS[w][0][lane] = bacc[g];
+      lds_barrier();
+      if (w == 0) {
+        float acc = 0.0f;
+        for (int q = 0; q < NW; ++q) acc += stS[q][0][lane];
+        if (dok) a.dbias[((int64_t)b * 7 + g) * a.D + d] = acc;
+      }
+      lds_barrier();
+    }
   }
 }
 
@@ -457,7 +476,7 @@ extern "C" int sc_lucy_scan_fwd(const void* gates, int gates_dtype, const float*
 
 extern "C" int sc_lucy_scan_bwd(const void* gates, int gates_dtype, const float* ckpt,
                                 const void* dout, const float* ds_last, void* dgates, float* dh0,
-                                float* ds0, int B, int T, int D, int64_t stride_g_bt,
+                                float* ds0, float* dbias, int B, int T, int D, int64_t stride_g_bt,
                                 int64_t stride_g_td, int64_t stride_g_cd, int64_t stride_d_bt,
                                 int64_t stride_d_bd, int64_t stride_dg_bt, int64_t stride_dg_td,
                                 int64_t stride_dg_cd, void* stream) {
@@ -467,9 +486,10 @@ extern "C" int sc_lucy_scan_bwd(const void* gates, int gates_dtype, const float*
   SC_REQUIRE(B <= 65535, "sc_lucy_scan_bwd: B=%d exceeds grid limit 65535", B);
   if (B == 0 || D == 0) return 0;
   SC_REQUIRE(dh0 && ds0, "sc_lucy_scan_bwd: null dh0/ds0");
+  if (T == 0 && dbias) (void)hipMemsetAsync(dbias, 0, sizeof(float) * 7 * B * D, (hipStream_t)stream);
   SC_REQUIRE(T == 0 || (gates && ckpt && dout && dgates),
              "sc_lucy_scan_bwd: null gates/ckpt/dout/dgates pointer");
-  ScanBwdArgs a{gates, ckpt, dout, ds_last, dgates, dh0, ds0, B, T, D, (T + kChunk - 1) / kChunk,
+  ScanBwdArgs a{gates, ckpt, dout, ds_last, dgates, dh0, ds0, dbias, B, T, D, (T + kChunk - 1) / kChunk,
                 stride_g_bt, stride_g_td, stride_g_cd, stride_d_bt, stride_d_bd,
                 stride_dg_bt, stride_dg_td, stride_dg_cd};
   hipStream_t st = (hipStream_t)stream;

@@ -16,7 +16,30 @@ import torch
 import torch.nn as nn
 
 from .lucyrnn_conf import LucyRNNConfig
-from .ops import lucy_scan
+from .ops import layer_norm, layer_norm_supported, lucy_cell, wgrad_splitk
+
+
+class _LinearFn(torch.autograd.Function):
+    """y = x W^T + b in the autocast dtype; backward with a split-K weight gradient."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, cdtype):
+        xc = x.to(cdtype)
+        wc = w.to(cdtype)
+        out = torch.addmm(b.to(cdtype), xc, wc.t()) if b is not None else xc @ wc.t()
+        ctx.save_for_backward(xc, wc)
+        ctx.meta = (x.dtype, w.dtype, b is not None)
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        xc, wc = ctx.saved_tensors
+        xdt, wdt, has_b = ctx.meta
+        dy = dy.to(wc.dtype)
+        dx = (dy @ wc).to(xdt) if ctx.needs_input_grad[0] else None
+        dw = wgrad_splitk(dy, xc).to(wdt) if ctx.needs_input_grad[1] else None
+        db = dy.sum(0, dtype=torch.float32).to(wdt) if has_b and ctx.needs_input_grad[2] else None
+        return dx, dw, db, None
 
 
 class LinearSafe(nn.Module):
@@ -35,12 +58,27 @@ class LinearSafe(nn.Module):
 
     def forward(self, x):
         x_flat = x.reshape(-1, x.shape[-1])
-        if self.bias is not None:
-            # one GEMM with the bias in its epilogue (hipBLASLt); the reference adds it after
-            out = torch.addmm(self.bias, x_flat, self.weight.t())
+        if x.is_cuda and torch.is_autocast_enabled("cuda"):
+            cdt = torch.get_autocast_dtype("cuda")
         else:
-            out = torch.matmul(x_flat, self.weight.t())
+            cdt = torch.promote_types(x.dtype, self.weight.dtype)
+        with torch.autocast("cuda", enabled=False):
+            # one GEMM with the bias in its epilogue (hipBLASLt); the reference adds it after
+            out = _LinearFn.apply(x_flat, self.weight, self.bias, cdt)
         return out.view(*x.shape[:-1], self.weight.shape[0])
+
+
+class LayerNormHip(nn.LayerNorm):
+    """nn.LayerNorm (same parameters / state_dict) whose forward runs layernorm.hip in the
+    activation's own dtype: under autocast the bf16 scan output is normalised straight into the
+    bf16 input of the next gate GEMM, with fp32 statistics."""
+
+    def forward(self, x):
+        if x.is_cuda and self.elementwise_affine and len(self.normalized_shape) == 1 \
+                and layer_norm_supported(x):
+            with torch.autocast("cuda", enabled=False):
+                return layer_norm(x, self.weight, self.bias, self.eps)
+        return super().forward(x)
 
 
 class LucyRNNCellTriton(nn.Module):
@@ -67,9 +105,17 @@ class LucyRNNCellTriton(nn.Module):
                 self.linear.bias[6 * D:7 * D].fill_(0.5)   # alpha
 
     def forward(self, x, h0, s0):
-        B, T, _ = x.shape
-        gates = self.linear(x).view(B, T, 7, self.hidden_dim)
-        return lucy_scan(gates, h0, s0)
+        # projection GEMM + scan as one autograd node: the scan backward hands the bias
+        # gradient back from registers, the weight gradient runs split-K
+        w, b = self.linear.weight, self.linear.bias
+        if x.is_cuda and torch.is_autocast_enabled("cuda"):
+            cdt = torch.get_autocast_dtype("cuda")
+        else:
+            cdt = torch.promote_types(x.dtype, w.dtype)
+        if b is None:
+            b = torch.zeros(w.shape[0], dtype=w.dtype, device=w.device)
+        with torch.autocast("cuda", enabled=False):
+            return lucy_cell(x, w, b, h0, s0, cdt)
 
 
 class LucyRNNtriton(nn.Module):
@@ -96,7 +142,7 @@ class LucyRNNtriton(nn.Module):
                 input_dim = config.input_dim if i == 0 else config.hidden_dim
                 layers.append(LucyRNNCellTriton(input_dim, config.hidden_dim))
                 if i < config.num_layers - 1:
-                    norms.append(nn.LayerNorm(config.hidden_dim))
+                    norms.append(LayerNormHip(config.hidden_dim))
             self.tracks.append(layers)
             self.norms.append(norms)
 

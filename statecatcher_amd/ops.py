@@ -35,6 +35,61 @@ class _timed:
 
 
 # ----------------------------------------------------------------------------- LucyRNN scan --
+def _scan_fwd(gates, h0, s0, need_ckpt):
+    require_device(gates, h0, s0)
+    if gates.dim() != 4 or gates.shape[2] != 7:
+        raise ValueError(f"gates must be [B,T,7,D], got {tuple(gates.shape)}")
+    B, T, _, D = gates.shape
+    if tuple(h0.shape) != (B, D) or tuple(s0.shape) != (B, D):
+        raise ValueError(f"h0/s0 must be [B,D]=({B},{D}); got {tuple(h0.shape)}, {tuple(s0.shape)}")
+    if gates.stride(3) != 1:
+        gates = gates.contiguous()
+    # the reference reads h0/s0 as contiguous even when handed a strided view
+    h0c = h0.detach().to(torch.float32).contiguous()
+    s0c = s0.detach().to(torch.float32).contiguous()
+    out = torch.empty(B, T, D, dtype=gates.dtype, device=gates.device)
+    s_out = torch.empty(B, D, dtype=torch.float32, device=gates.device)
+    lib = _lib.load()
+    ckpt = None
+    if need_ckpt:
+        ckpt = torch.empty(lib.sc_lucy_scan_ckpt_numel(B, T, D), dtype=torch.float32,
+                           device=gates.device)
+    e = gates.element_size()
+    nbytes = B * T * D * 8 * e + (ckpt.numel() * 4 if ckpt is not None else 0) + 4 * B * D * 4
+    with _timed("lucy_scan_fwd", gates, nbytes):
+        rc = lib.sc_lucy_scan_fwd(ptr(gates), dtype_code(gates), ptr(h0c), ptr(s0c), ptr(out),
+                                  ptr(s_out), B, T, D, gates.stride(0), gates.stride(1),
+                                  gates.stride(2), out.stride(0), out.stride(1), ptr(ckpt),
+                                  stream_of(gates))
+    check(rc, "sc_lucy_scan_fwd")
+    return gates, out, s_out, ckpt
+
+
+def _scan_bwd(gates, ckpt, dout, ds_last, want_dbias):
+    B, T, _, D = gates.shape
+    if dout is None:
+        dout = torch.zeros(B, T, D, dtype=gates.dtype, device=gates.device)
+    dout = dout.to(gates.dtype)
+    if dout.stride(2) != 1:
+        dout = dout.contiguous()
+    if ds_last is not None:
+        ds_last = ds_last.to(torch.float32).contiguous()
+    dgates = torch.empty(B, T, 7, D, dtype=gates.dtype, device=gates.device)
+    dh0 = torch.empty(B, D, dtype=torch.float32, device=gates.device)
+    ds0 = torch.empty(B, D, dtype=torch.float32, device=gates.device)
+    dbias = torch.empty(B, 7, D, dtype=torch.float32, device=gates.device) if want_dbias else None
+    e = gates.element_size()
+    nbytes = B * T * D * 15 * e + ckpt.numel() * 4 + 3 * B * D * 4
+    with _timed("lucy_scan_bwd", gates, nbytes):
+        rc = _lib.load().sc_lucy_scan_bwd(
+            ptr(gates), dtype_code(gates), ptr(ckpt), ptr(dout), ptr(ds_last), ptr(dgates),
+            ptr(dh0), ptr(ds0), ptr(dbias), B, T, D, gates.stride(0), gates.stride(1),
+            gates.stride(2), dout.stride(0), dout.stride(1), dgates.stride(0), dgates.stride(1),
+            dgates.stride(2), stream_of(gates))
+    check(rc, "sc_lucy_scan_bwd")
+    return dgates, dh0, ds0, dbias
+
+
 class LucyScanFn(torch.autograd.Function):
     """out, s_last = scan(gates [B,T,7,D], h0 [B,D], s0 [B,D]).
 
@@ -45,34 +100,9 @@ class LucyScanFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, gates, h0, s0):
-        require_device(gates, h0, s0)
-        if gates.dim() != 4 or gates.shape[2] != 7:
-            raise ValueError(f"gates must be [B,T,7,D], got {tuple(gates.shape)}")
-        B, T, _, D = gates.shape
-        if tuple(h0.shape) != (B, D) or tuple(s0.shape) != (B, D):
-            raise ValueError(f"h0/s0 must be [B,D]=({B},{D}); got {tuple(h0.shape)}, {tuple(s0.shape)}")
-        if gates.stride(3) != 1:
-            gates = gates.contiguous()
-        # the reference reads h0/s0 as contiguous even when handed a strided view
-        h0c = h0.detach().to(torch.float32).contiguous()
-        s0c = s0.detach().to(torch.float32).contiguous()
-        out = torch.empty(B, T, D, dtype=gates.dtype, device=gates.device)
-        s_out = torch.empty(B, D, dtype=torch.float32, device=gates.device)
-        need_bwd = any(ctx.needs_input_grad)
-        lib = _lib.load()
-        ckpt = None
-        if need_bwd:
-            ckpt = torch.empty(lib.sc_lucy_scan_ckpt_numel(B, T, D), dtype=torch.float32,
-                               device=gates.device)
-        e = gates.element_size()
-        nbytes = B * T * D * 8 * e + (ckpt.numel() * 4 if ckpt is not None else 0) + 4 * B * D * 4
-        with _timed("lucy_scan_fwd", gates, nbytes):
-            rc = lib.sc_lucy_scan_fwd(ptr(gates), dtype_code(gates), ptr(h0c), ptr(s0c), ptr(out),
-                                      ptr(s_out), B, T, D, gates.stride(0), gates.stride(1),
-                                      gates.stride(2), out.stride(0), out.stride(1), ptr(ckpt),
-                                      stream_of(gates))
-        check(rc, "sc_lucy_scan_fwd")
-        if need_bwd:
+        need = any(ctx.needs_input_grad)
+        gates, out, s_out, ckpt = _scan_fwd(gates, h0, s0, need)
+        if need:
             ctx.save_for_backward(gates, ckpt)
             ctx.state_dtypes = (h0.dtype, s0.dtype)
         return out, s_out
@@ -80,32 +110,124 @@ class LucyScanFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dout, ds_last):
         gates, ckpt = ctx.saved_tensors
-        B, T, _, D = gates.shape
-        if dout is None:
-            dout = torch.zeros(B, T, D, dtype=gates.dtype, device=gates.device)
-        dout = dout.to(gates.dtype)
-        if dout.stride(2) != 1:
-            dout = dout.contiguous()
-        if ds_last is not None:
-            ds_last = ds_last.to(torch.float32).contiguous()
-        dgates = torch.empty(B, T, 7, D, dtype=gates.dtype, device=gates.device)
-        dh0 = torch.empty(B, D, dtype=torch.float32, device=gates.device)
-        ds0 = torch.empty(B, D, dtype=torch.float32, device=gates.device)
-        e = gates.element_size()
-        nbytes = B * T * D * 15 * e + ckpt.numel() * 4 + 3 * B * D * 4
-        with _timed("lucy_scan_bwd", gates, nbytes):
-            rc = _lib.load().sc_lucy_scan_bwd(
-                ptr(gates), dtype_code(gates), ptr(ckpt), ptr(dout), ptr(ds_last), ptr(dgates),
-                ptr(dh0), ptr(ds0), B, T, D, gates.stride(0), gates.stride(1), gates.stride(2),
-                dout.stride(0), dout.stride(1), dgates.stride(0), dgates.stride(1),
-                dgates.stride(2), stream_of(gates))
-        check(rc, "sc_lucy_scan_bwd")
+        dgates, dh0, ds0, _ = _scan_bwd(gates, ckpt, dout, ds_last, False)
         hd, sd = ctx.state_dtypes
         return dgates, dh0.to(hd), ds0.to(sd)
 
 
 def lucy_scan(gates, h0, s0):
     return LucyScanFn.apply(gates, h0, s0)
+
+
+def wgrad_splitk(dy, x):
+    """dW = dy^T x (fp32) for dy [M,N], x [M,K] with M = B*T large: at the training shape
+    dW is 3584 x 512 while M = 48000, so a plain GEMM has 28 output tiles for 256 CUs; split M
+    into S batched GEMMs and sum the partials in fp32."""
+    M, N = dy.shape
+    K = x.shape[1]
+    S = 1
+    # measured on MI355X at M=48000, N=3584, K=512 (tools/gemm_probe.py): S=1 410 TF/s,
+    # S=8 760, S=16 860
+    while S < 16 and M % (2 * S) == 0 and M // (2 * S) >= 2048 and \
+            ((N + 255) // 256) * ((K + 255) // 256) * S < 512:
+        S *= 2
+    if S == 1:
+        return torch.matmul(dy.t(), x).float()
+    part = torch.bmm(dy.view(S, M // S, N).transpose(1, 2), x.view(S, M // S, K))
+    return part.sum(0, dtype=torch.float32)
+
+
+class LucyCellFn(torch.autograd.Function):
+    """One LucyRNN layer: gates = x W^T + b (one GEMM, compute dtype `cdt`) -> HIP scan.
+
+    Backward: scan adjoint (which also emits the bias gradient as per-row partial sums),
+    dx = dgates W, dW = split-K dgates^T x.  lucyrnn_triton.py:50-75 fused into one node.
+    """
+
+    @staticmethod
+    def forward(ctx, x2d, w, b, h0, s0, B, T, cdt):
+        xc = x2d.to(cdt)
+        wc = w.to(cdt)
+        with _timed("gate_gemm_fwd", xc, 0):
+            gates = torch.addmm(b.to(cdt), xc, wc.t()).view(B, T, 7, -1)
+        need = any(ctx.needs_input_grad)
+        gates, out, s_out, ckpt = _scan_fwd(gates, h0, s0, need)
+        if need:
+            ctx.save_for_backward(xc, wc, gates, ckpt)
+            ctx.dtypes = (x2d.dtype, w.dtype, h0.dtype, s0.dtype)
+        return out, s_out
+
+    @staticmethod
+    def backward(ctx, dout, ds_last):
+        xc, wc, gates, ckpt = ctx.saved_tensors
+        xdt, wdt, hdt, sdt = ctx.dtypes
+        dgates, dh0, ds0, dbias = _scan_bwd(gates, ckpt, dout, ds_last, ctx.needs_input_grad[2])
+        dg2 = dgates.view(-1, dgates.shape[2] * dgates.shape[3])
+        with _timed("gate_gemm_dgrad", dg2, 0):
+            dx = (dg2 @ wc).to(xdt) if ctx.needs_input_grad[0] else None
+        with _timed("gate_gemm_wgrad", dg2, 0):
+            dw = wgrad_splitk(dg2, xc).to(wdt) if ctx.needs_input_grad[1] else None
+        db = dbias.sum(0).view(-1).to(wdt) if dbias is not None else None
+        return dx, dw, db, dh0.to(hdt), ds0.to(sdt), None, None, None
+
+
+def lucy_cell(x, w, b, h0, s0, cdt=None):
+    """x [B,T,Din] -> (out [B,T,D], s_last [B,D]) through projection + scan."""
+    B, T, Din = x.shape
+    if cdt is None:
+        cdt = torch.promote_types(x.dtype, w.dtype)
+    return LucyCellFn.apply(x.reshape(B * T, Din), w, b, h0, s0, B, T, cdt)
+
+
+# ----------------------------------------------------------------------------- LayerNorm -----
+class LayerNormFn(torch.autograd.Function):
+    """nn.LayerNorm over the last dim in x's dtype with fp32 statistics (layernorm.hip)."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, eps):
+        require_device(x)
+        D = x.shape[-1]
+        x2 = x.reshape(-1, D)
+        if not x2.is_contiguous() or x2.data_ptr() % 16:
+            x2 = x2.contiguous()
+        rows = x2.shape[0]
+        g = gamma.detach().to(torch.float32).contiguous()
+        b = beta.detach().to(torch.float32).contiguous()
+        y = torch.empty_like(x2)
+        mean = torch.empty(rows, dtype=torch.float32, device=x.device)
+        rstd = torch.empty(rows, dtype=torch.float32, device=x.device)
+        rc = _lib.load().sc_layernorm_fwd(ptr(x2), dtype_code(x2), ptr(g), ptr(b), ptr(y), ptr(mean),
+                                          ptr(rstd), rows, D, float(eps), stream_of(x2))
+        check(rc, "sc_layernorm_fwd")
+        ctx.save_for_backward(x2, g, mean, rstd)
+        ctx.pdtypes = (gamma.dtype, beta.dtype)
+        return y.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, g, mean, rstd = ctx.saved_tensors
+        rows, D = x2.shape
+        dy2 = dy.reshape(rows, D).to(x2.dtype)
+        if not dy2.is_contiguous() or dy2.data_ptr() % 16:
+            dy2 = dy2.contiguous()
+        lib = _lib.load()
+        dx = torch.empty_like(x2)
+        dgb = torch.empty(2, D, dtype=torch.float32, device=x2.device)
+        ws = torch.empty(lib.sc_layernorm_bwd_workspace_numel(rows, D), dtype=torch.float32,
+                         device=x2.device)
+        rc = lib.sc_layernorm_bwd(ptr(x2), ptr(dy2), dtype_code(x2), ptr(g), ptr(mean), ptr(rstd),
+                                  ptr(dx), ptr(dgb), ptr(ws), rows, D, stream_of(x2))
+        check(rc, "sc_layernorm_bwd")
+        gd, bd = ctx.pdtypes
+        return dx.view(dy.shape), dgb[0].to(gd), dgb[1].to(bd), None
+
+
+def layer_norm(x, gamma, beta, eps=1e-5):
+    return LayerNormFn.apply(x, gamma, beta, eps)
+
+
+def layer_norm_supported(x):
+    return x.dtype in _lib._DTYPE and bool(_lib.load().sc_layernorm_supported(dtype_code(x), x.shape[-1]))
 
 
 # ----------------------------------------------------------------------------- decay scan ----

@@ -1,0 +1,178 @@
+"""GPU parity of the module-level drop-ins (LucyRNNtriton, LayerNorm, compute_loss) against fp64
+torch restatements on the CPU.  fp32 on the GPU: 1e-3 relative (north_star) with absolute floors
+scaled to each tensor's magnitude; bf16 autocast: loss within 5e-2 of the fp32 run.
+
+Conditioning: the reference normalises each gate element as x / sqrt(x^2 + 1e-6),
+whose slope is ~1e3 at x = 0.  When a model test recomputes the gate GEMM in another precision,
+the few gates per layer that land within ~1e-5 of zero flip, and the inter-layer LayerNorm
+spreads that to every feature: at xavier init ~2% of logits then differ by up to 0.05.  The
+bounded kv = k v / (q (q + 1e-6)), q = (k^2+v^2)/2 + 1e-6, is heavy-tailed (up to ~1e5 when k and
+v are both small), so |s| reaches ~1e5 and its fp32 absolute noise (~1e-2) moves c = tanh(h+s)
+wherever h + s is O(1).  Both are properties of the reference math, not of either
+implementation: the kernel-level tests (test_gpu_scan.py) pin the scan on IDENTICAL gates.  The
+module-level tests here therefore use a well-conditioned init: every gate plane except r (which
+only enters through a smooth normaliser) gets a bias of magnitude 3 and down-scaled weights, so
+no normalised gate approaches zero and kv stays O(0.1).
+"""
+import numpy as np
+import pytest
+import torch
+
+from tests.torch_ref import lucyrnn64, scan64
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0") if torch.cuda.is_available() else None
+
+
+def sc():
+    import statecatcher_amd as s
+    return s
+
+
+def close(got, ref, rtol=1e-3, afrac=1e-3):
+    got = got.detach().double().cpu().numpy() if isinstance(got, torch.Tensor) else got
+    ref = ref.detach().double().cpu().numpy() if isinstance(ref, torch.Tensor) else ref
+    np.testing.assert_allclose(got, ref, rtol=rtol, atol=afrac * max(np.abs(ref).max(), 1e-30))
+
+
+@pytest.mark.parametrize("dtype,D", [(torch.float32, 512), (torch.bfloat16, 512), (torch.float32, 256),
+                                     (torch.bfloat16, 1024), (torch.float16, 512)])
+def test_layernorm_fwd_bwd_vs_torch(dtype, D):
+    from statecatcher_amd import ops
+    torch.manual_seed(0)
+    x = (torch.randn(3, 333, D) * 2 + 0.5).to(dtype)
+    g = torch.randn(D) * 0.5 + 1
+    b = torch.randn(D) * 0.1
+    dy = torch.randn(3, 333, D).to(dtype)
+    xd = x.to(DEV).requires_grad_(True)
+    gd = g.to(DEV).requires_grad_(True)
+    bd = b.to(DEV).requires_grad_(True)
+    y = ops.layer_norm(xd, gd, bd, 1e-5)
+    assert y.dtype == dtype
+    y.backward(dy.to(DEV))
+    xr = x.double().requires_grad_(True)
+    gr = g.double().requires_grad_(True)
+    br = b.double().requires_grad_(True)
+    yr = torch.nn.functional.layer_norm(xr, (D,), gr, br, 1e-5)
+    yr.backward(dy.double())
+    tol = 1e-4 if dtype == torch.float32 else 1e-2
+    close(y, yr, rtol=tol, afrac=tol)
+    close(xd.grad, xr.grad, rtol=tol, afrac=tol)
+    close(gd.grad, gr.grad, rtol=tol, afrac=tol)
+    close(bd.grad, br.grad, rtol=tol, afrac=tol)
+
+
+def condition_(m, D, gen=None):
+    """Well-conditioned gate init (module docstring): |bias| = 3 on z, k, v, h_pre, decay, alpha."""
+    with torch.no_grad():
+        for cell in m.tracks[0]:
+            W, b = cell.linear.weight.view(7, D, -1), cell.linear.bias.view(7, D)
+            for gi in (1, 2, 3, 4, 5, 6):
+                W[gi] *= 0.1
+                sign = torch.randint(0, 2, (D,), generator=gen).float() * 2 - 1
+                b[gi] = 3.0 * sign
+
+
+def make_model(L=3, Din=24, D=64, V=40, seed=0):
+    torch.manual_seed(seed)
+    cfg = sc().LucyRNNConfig(input_dim=Din, hidden_dim=D, num_layers=L, vocab_size=V,
+                             kernel_impl="triton", fused_ops=True, layer_norm=False)
+    m = sc().LucyRNNtriton(cfg)
+    condition_(m, D, torch.Generator().manual_seed(seed + 100))
+    with torch.no_grad():
+        m.output_proj.weight.normal_(0, 0.2)
+        m.output_proj.bias.normal_(0, 0.1)
+        for n in m.norms[0]:
+            n.weight.normal_(1.0, 0.1)
+            n.bias.normal_(0, 0.1)
+    return m
+
+
+def test_lucyrnn_module_fwd_bwd_fp32_vs_fp64_restatement():
+    L, Din, D, V, B, T = 3, 24, 64, 40, 3, 100
+    m = make_model(L, Din, D, V).to(DEV)
+    torch.manual_seed(1)
+    x = torch.randn(B, T, Din)
+    R = torch.randn(B, T, V)
+    logits, (fh, fs) = m(x.to(DEV))
+    (logits * R.to(DEV)).sum().backward()
+    params = {k: v.detach().double().cpu().requires_grad_(True) for k, v in m.named_parameters()}
+    rl, (rh, rs) = lucyrnn64(params, x.double(), L, D)
+    (rl * R.double()).sum().backward()
+    close(logits, rl)
+    for l in range(L):
+        close(fh[0][l], rh[l])
+        close(fs[0][l], rs[l], afrac=1e-4)
+    for k, p in m.named_parameters():
+        close(p.grad, params[k].grad, rtol=2e-3, afrac=2e-3)
+
+
+def test_lucyrnn_state_carry_matches_single_pass():
+    """Two carried segments == one pass over the concatenation (TBPTT forward semantics)."""
+    m = make_model().to(DEV)
+    torch.manual_seed(2)
+    x = torch.randn(2, 150, 24, device=DEV)
+    with torch.no_grad():
+        full, _ = m(x)
+        a, st = m(x[:, :70])
+        b, _ = m(x[:, 70:], st)
+    close(torch.cat([a, b], 1), full, rtol=1e-4, afrac=1e-5)
+
+
+def test_compute_loss_ctc_fused_vs_reference_path():
+    """compute_loss with the fused CTCLoss == log_softmax -> nn.CTCLoss on an fp64 CPU model."""
+    L, Din, D, V, B, T = 2, 24, 64, 40, 3, 120
+    torch.manual_seed(7)
+    model = sc().ASRModel(None, sc().LucyRNNConfig(Din, D, L, V, kernel_impl="triton", fused_ops=True,
+                                                   layer_norm=False), V, Din, -1)
+    condition_(model.encoder, D, torch.Generator().manual_seed(8))
+    with torch.no_grad():
+        model.encoder.output_proj.weight.normal_(0, 0.2)
+    model = model.to(DEV)
+    torch.manual_seed(3)
+    feats = torch.randn(B, T, Din)
+    masks = torch.ones(B, T, dtype=torch.bool)
+    masks[2, 100:] = False
+    tokens = torch.randint(1, V, (B, 20))
+    tgt = [20, 13, 0]
+    inl = [120, 120, 100]
+    for b in range(B):
+        tokens[b, tgt[b]:] = 0
+    loss, st, enc, _ = sc().compute_loss("ctc", sc().CTCLoss(blank=0, zero_infinity=True), model,
+                                         feats.to(DEV), masks.to(DEV), tokens.to(DEV), inl, tgt, 0)
+    loss.backward()
+    params = {k.replace("encoder.", ""): v.detach().double().cpu().requires_grad_(True)
+              for k, v in model.named_parameters()}
+    rl, _ = lucyrnn64(params, (feats * masks.unsqueeze(-1)).double(), L, D)
+    ref = torch.nn.CTCLoss(blank=0, zero_infinity=True)(rl.log_softmax(-1).transpose(0, 1), tokens, inl, tgt)
+    ref.backward()
+    np.testing.assert_allclose(loss.item(), ref.item(), rtol=1e-4)
+    for k, p in model.named_parameters():
+        close(p.grad, params[k.replace("encoder.", "")].grad, rtol=3e-3, afrac=3e-3)
+
+
+def test_bf16_autocast_training_step_close_to_fp32():
+    L, Din, D, V, B, T = 3, 80, 128, 64, 4, 300
+    torch.manual_seed(4)
+    feats = torch.randn(B, T, Din, device=DEV)
+    tokens = torch.randint(1, V, (B, 30), device=DEV)
+    losses = []
+    for amp in [False, True]:
+        m = make_model(L, Din, D, V, seed=5).to(DEV)
+        crit = sc().CTCLoss()
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
+            logits, _ = m(feats)
+            loss = crit.forward_logits(logits, tokens, [T] * B, [30] * B)
+        loss.backward()
+        gn = torch.sqrt(sum((p.grad.float() ** 2).sum() for p in m.parameters()))
+        assert torch.isfinite(gn)
+        losses.append(loss.item())
+    np.testing.assert_allclose(losses[1], losses[0], rtol=5e-2)
+
+
+def test_no_cpu_fallback_on_device_path():
+    """The kernels that ran above came from the in-tree HIP library."""
+    from statecatcher_amd import _lib
+    import os
+    maps = open(f"/proc/{os.getpid()}/maps").read()
+    assert _lib.LIB_PATH in maps
