@@ -46,6 +46,10 @@ def parse():
     ap.add_argument("--bucket-mb", type=float, default=50.0)
     ap.add_argument("--cpu-baseline", choices=["on", "off"], default="on")
     ap.add_argument("--cpu-seq", type=int, default=300, help="T of the bounded CPU sample")
+    ap.add_argument("--tunableop", choices=["on", "off"], default="on",
+                    help="use the shipped PyTorch TunableOp GEMM table (statecatcher_amd/tuning)")
+    ap.add_argument("--tune-out", default=None,
+                    help="rank 0 tunes GEMM shapes missing from the table and writes it here")
     return ap.parse_args()
 
 
@@ -107,6 +111,19 @@ def main():
     device = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=device)
+
+    if args.tunableop == "on":
+        # hipBLASLt/rocBLAS solution table for this model's GEMM shapes (tools/blas_probe.py):
+        # the default heuristics pick e.g. 263 us for the gate GEMM that a tuned solution does
+        # in 146 us.  Tuning itself only ever runs in warmup, and only with --tune-out.
+        import torch.cuda.tunable as tun
+        table = os.path.join(ROOT, "statecatcher_amd", "tuning", "tunableop_gfx950.csv")
+        tun.enable(True)
+        tun.tuning_enable(bool(args.tune_out) and rank == 0)
+        tun.set_max_tuning_duration(200)
+        tun.set_filename(args.tune_out if (args.tune_out and rank == 0) else table)
+        if os.path.exists(table):
+            tun.read_file(table)
 
     import statecatcher_amd as sc
     from statecatcher_amd import ops

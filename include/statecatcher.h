@@ -58,6 +58,9 @@ int64_t sc_lucy_scan_ckpt_numel(int B, int T, int D);
  * s_out_ptr, B, T, D, stride_g_bt, stride_g_td, stride_g_cd, stride_o_bt, stride_o_bd)
  * (lucyrnn_triton.py:180-194).
  *   gates  [B,T,7,D] of gates_dtype, d-stride 1, gate order r,z,k,v,h_pre,decay,alpha
+ *   gate_bias  NULL (gates already include the projection bias, as in the reference), or fp32
+ *          [7,D] added to every step's gates on load (lets the projection GEMM skip its bias
+ *          epilogue; the backward then needs the same pointer)
  *   h0,s0  [B,D] fp32 contiguous (read exactly as contiguous; the caller must not pass the
  *          strided out[:, -1] view the reference passes — SURVEY F3)
  *   out    [B,T,D] of gates_dtype, d-stride 1 (strides stride_o_bt, stride_o_bd)
@@ -66,7 +69,8 @@ int64_t sc_lucy_scan_ckpt_numel(int B, int T, int D);
  *          consumed by sc_lucy_scan_bwd (training)
  * State arithmetic is fp32 for every gates_dtype.
  */
-int sc_lucy_scan_fwd(const void* gates, int gates_dtype, const float* h0, const float* s0,
+int sc_lucy_scan_fwd(const void* gates, int gates_dtype, const float* gate_bias,
+                     const float* h0, const float* s0,
                      void* out, float* s_out, int B, int T, int D,
                      int64_t stride_g_bt, int64_t stride_g_td, int64_t stride_g_cd,
                      int64_t stride_o_bt, int64_t stride_o_bd, float* ckpt, void* stream);
@@ -78,7 +82,7 @@ int sc_lucy_scan_fwd(const void* gates, int gates_dtype, const float* h0, const 
  * not NULL, dbias fp32 [B,7,D] = sum over t of the stored dgates (per batch row; summing over
  * b gives the gate-projection bias gradient without another pass over dgates).
  */
-int sc_lucy_scan_bwd(const void* gates, int gates_dtype, const float* ckpt,
+int sc_lucy_scan_bwd(const void* gates, int gates_dtype, const float* gate_bias, const float* ckpt,
                      const void* dout, const float* ds_last,
                      void* dgates, float* dh0, float* ds0, float* dbias, int B, int T, int D,
                      int64_t stride_g_bt, int64_t stride_g_td, int64_t stride_g_cd,

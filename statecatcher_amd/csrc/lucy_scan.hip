@@ -43,6 +43,7 @@ constexpr float kEps = 1e-6f;
 
 struct ScanFwdArgs {
   const void* gates;
+  const float* bias;   // optional fp32 [7,D] gate bias added on load (NULL: gates are biased)
   const float* h0;
   const float* s0;
   void* out;
@@ -54,6 +55,7 @@ struct ScanFwdArgs {
 
 struct ScanBwdArgs {
   const void* gates;
+  const float* bias;
   const float* ckpt;
   const void* dout;
   const float* ds_last;
@@ -149,6 +151,9 @@ lucy_scan_fwd_kernel(ScanFwdArgs a) {
   // Two register buffers used ping-pong (explicitly, so no register copy ever waits on a
   // load that is still in flight): super-chunk k+1 streams in while k computes.
   uint32_t bufA[LC][7], bufB[LC][7];   // raw gate words (Elem::ldw)
+  float gb[7];
+#pragma unroll
+  for (int g = 0; g < 7; ++g) gb[g] = a.bias ? a.bias[g * a.D + dc] : 0.0f;
   const int Tm1 = a.T - 1;
   auto load = [&](uint32_t (&buf)[LC][7], int k) {
 #pragma unroll
@@ -165,8 +170,9 @@ lucy_scan_fwd_kernel(ScanFwdArgs a) {
 #pragma unroll
     for (int j = 0; j < LC; ++j) {
       if (t0 + j < a.T) {
-        step_terms(E::ldw(cur[j][0]), E::ldw(cur[j][1]), E::ldw(cur[j][2]), E::ldw(cur[j][3]),
-                   E::ldw(cur[j][4]), E::ldw(cur[j][5]), E::ldw(cur[j][6]), zg[j], dec[j], u[j], x[j]);
+        step_terms(E::ldw(cur[j][0]) + gb[0], E::ldw(cur[j][1]) + gb[1], E::ldw(cur[j][2]) + gb[2],
+                   E::ldw(cur[j][3]) + gb[3], E::ldw(cur[j][4]) + gb[4], E::ldw(cur[j][5]) + gb[5],
+                   E::ldw(cur[j][6]) + gb[6], zg[j], dec[j], u[j], x[j]);
       } else {  // identity step past the end of the sequence
         zg[j] = 1.0f; dec[j] = 1.0f; u[j] = 0.0f; x[j] = 0.0f;
       }
@@ -260,6 +266,14 @@ lucy_scan_bwd_kernel(ScanBwdArgs a) {
 
   uint32_t bufA[LC][7], bufB[LC][7];   // raw gate words (Elem::ldw), ping-pong
   uint32_t dbA[LC], dbB[LC];
+  // gate bias through LDS (one word per lane and gate): at 128 VGPRs the backward has no room
+  // for 7 more live registers
+  __shared__ float gbS[7][64];
+  if (w == 0) {
+#pragma unroll
+    for (int g = 0; g < 7; ++g) gbS[g][lane] = a.bias ? a.bias[g * a.D + dc] : 0.0f;
+  }
+#define gb(g) gbS[g][lane]
   float ckA[2], ckB[2];                // (s, h) checkpoint at the super-chunk start
   const Buf<float> cbuf(a.ckpt + (int64_t)b * a.nsc * 2 * a.D);
   const uint32_t vc = (uint32_t)dc * 4;
@@ -294,8 +308,9 @@ lucy_scan_bwd_kernel(ScanBwdArgs a) {
         for (int g = 0; g < 7; ++g) rawS[w][j][g][lane] = (uint16_t)cur[j][g];
       }
       if (t0 + j < a.T) {
-        step_terms(E::ldw(cur[j][0]), E::ldw(cur[j][1]), E::ldw(cur[j][2]), E::ldw(cur[j][3]),
-                   E::ldw(cur[j][4]), E::ldw(cur[j][5]), E::ldw(cur[j][6]), zg[j], dec[j], u[j], x[j]);
+        step_terms(E::ldw(cur[j][0]) + gb(0), E::ldw(cur[j][1]) + gb(1), E::ldw(cur[j][2]) + gb(2),
+                   E::ldw(cur[j][3]) + gb(3), E::ldw(cur[j][4]) + gb(4), E::ldw(cur[j][5]) + gb(5),
+                   E::ldw(cur[j][6]) + gb(6), zg[j], dec[j], u[j], x[j]);
       } else {
         zg[j] = 1.0f; dec[j] = 1.0f; u[j] = 0.0f; x[j] = 0.0f;
       }
@@ -375,7 +390,7 @@ lucy_scan_bwd_kernel(ScanBwdArgs a) {
         float o[7], g7[7];
 #pragma unroll
         for (int g = 0; g < 7; ++g)
-          g7[g] = kStage ? E::ldw((uint32_t)rawS[w][j][g][lane]) : E::ldw(cur[j][g]);
+          g7[g] = (kStage ? E::ldw((uint32_t)rawS[w][j][g][lane]) : E::ldw(cur[j][g])) + gb(g);
         gate_grads(g7[0], g7[1], g7[2], g7[3], g7[4], g7[5], g7[6], u[j], dpre, gs,
                    stH[w][j][lane], stS[w][j][lane], x[j], o);
         const uint32_t so = (uint32_t)(t0 + j) * otd;
@@ -403,6 +418,7 @@ lucy_scan_bwd_kernel(ScanBwdArgs a) {
     a.dh0[(int64_t)b * a.D + d] = carGh[a.nsc & 1][lane];
     a.ds0[(int64_t)b * a.D + d] = carGs[a.nsc & 1][lane];
   }
+#undef gb
   if (a.dbias) {   // reduce the per-wave partials over the NW waves (fixed order: deterministic)
 #pragma unroll
     for (int g = 0; g < 7; ++g) {
@@ -451,7 +467,8 @@ extern "C" int64_t sc_lucy_scan_ckpt_numel(int B, int T, int D) {
 
 static int check_dtype(int dt) { return dt == SC_F32 || dt == SC_BF16 || dt == SC_F16; }
 
-extern "C" int sc_lucy_scan_fwd(const void* gates, int gates_dtype, const float* h0,
+extern "C" int sc_lucy_scan_fwd(const void* gates, int gates_dtype, const float* gate_bias,
+                                const float* h0,
                                 const float* s0, void* out, float* s_out, int B, int T, int D,
                                 int64_t stride_g_bt, int64_t stride_g_td, int64_t stride_g_cd,
                                 int64_t stride_o_bt, int64_t stride_o_bd, float* ckpt,
@@ -463,7 +480,7 @@ extern "C" int sc_lucy_scan_fwd(const void* gates, int gates_dtype, const float*
   if (B == 0 || D == 0) return 0;
   SC_REQUIRE(h0 && s0 && s_out, "sc_lucy_scan_fwd: null state pointer");
   SC_REQUIRE(T == 0 || (gates && out), "sc_lucy_scan_fwd: null gates/out pointer");
-  ScanFwdArgs a{gates, h0, s0, out, s_out, ckpt, B, T, D, (T + kChunk - 1) / kChunk,
+  ScanFwdArgs a{gates, gate_bias, h0, s0, out, s_out, ckpt, B, T, D, (T + kChunk - 1) / kChunk,
                 stride_g_bt, stride_g_td, stride_g_cd, stride_o_bt, stride_o_bd};
   hipStream_t st = (hipStream_t)stream;
   switch (gates_dtype) {
@@ -474,7 +491,8 @@ extern "C" int sc_lucy_scan_fwd(const void* gates, int gates_dtype, const float*
   return launch_status("sc_lucy_scan_fwd");
 }
 
-extern "C" int sc_lucy_scan_bwd(const void* gates, int gates_dtype, const float* ckpt,
+extern "C" int sc_lucy_scan_bwd(const void* gates, int gates_dtype, const float* gate_bias,
+                                const float* ckpt,
                                 const void* dout, const float* ds_last, void* dgates, float* dh0,
                                 float* ds0, float* dbias, int B, int T, int D, int64_t stride_g_bt,
                                 int64_t stride_g_td, int64_t stride_g_cd, int64_t stride_d_bt,
@@ -489,7 +507,8 @@ extern "C" int sc_lucy_scan_bwd(const void* gates, int gates_dtype, const float*
   if (T == 0 && dbias) (void)hipMemsetAsync(dbias, 0, sizeof(float) * 7 * B * D, (hipStream_t)stream);
   SC_REQUIRE(T == 0 || (gates && ckpt && dout && dgates),
              "sc_lucy_scan_bwd: null gates/ckpt/dout/dgates pointer");
-  ScanBwdArgs a{gates, ckpt, dout, ds_last, dgates, dh0, ds0, dbias, B, T, D, (T + kChunk - 1) / kChunk,
+  ScanBwdArgs a{gates, gate_bias, ckpt, dout, ds_last, dgates, dh0, ds0, dbias, B, T, D,
+                (T + kChunk - 1) / kChunk,
                 stride_g_bt, stride_g_td, stride_g_cd, stride_d_bt, stride_d_bd,
                 stride_dg_bt, stride_dg_td, stride_dg_cd};
   hipStream_t st = (hipStream_t)stream;

@@ -35,7 +35,7 @@ class _timed:
 
 
 # ----------------------------------------------------------------------------- LucyRNN scan --
-def _scan_fwd(gates, h0, s0, need_ckpt):
+def _scan_fwd(gates, h0, s0, need_ckpt, bias=None):
     require_device(gates, h0, s0)
     if gates.dim() != 4 or gates.shape[2] != 7:
         raise ValueError(f"gates must be [B,T,7,D], got {tuple(gates.shape)}")
@@ -57,7 +57,8 @@ def _scan_fwd(gates, h0, s0, need_ckpt):
     e = gates.element_size()
     nbytes = B * T * D * 8 * e + (ckpt.numel() * 4 if ckpt is not None else 0) + 4 * B * D * 4
     with _timed("lucy_scan_fwd", gates, nbytes):
-        rc = lib.sc_lucy_scan_fwd(ptr(gates), dtype_code(gates), ptr(h0c), ptr(s0c), ptr(out),
+        rc = lib.sc_lucy_scan_fwd(ptr(gates), dtype_code(gates), ptr(bias), ptr(h0c), ptr(s0c),
+                                  ptr(out),
                                   ptr(s_out), B, T, D, gates.stride(0), gates.stride(1),
                                   gates.stride(2), out.stride(0), out.stride(1), ptr(ckpt),
                                   stream_of(gates))
@@ -65,7 +66,7 @@ def _scan_fwd(gates, h0, s0, need_ckpt):
     return gates, out, s_out, ckpt
 
 
-def _scan_bwd(gates, ckpt, dout, ds_last, want_dbias):
+def _scan_bwd(gates, ckpt, dout, ds_last, want_dbias, bias=None):
     B, T, _, D = gates.shape
     if dout is None:
         dout = torch.zeros(B, T, D, dtype=gates.dtype, device=gates.device)
@@ -82,7 +83,7 @@ def _scan_bwd(gates, ckpt, dout, ds_last, want_dbias):
     nbytes = B * T * D * 15 * e + ckpt.numel() * 4 + 3 * B * D * 4
     with _timed("lucy_scan_bwd", gates, nbytes):
         rc = _lib.load().sc_lucy_scan_bwd(
-            ptr(gates), dtype_code(gates), ptr(ckpt), ptr(dout), ptr(ds_last), ptr(dgates),
+            ptr(gates), dtype_code(gates), ptr(bias), ptr(ckpt), ptr(dout), ptr(ds_last), ptr(dgates),
             ptr(dh0), ptr(ds0), ptr(dbias), B, T, D, gates.stride(0), gates.stride(1),
             gates.stride(2), dout.stride(0), dout.stride(1), dgates.stride(0), dgates.stride(1),
             dgates.stride(2), stream_of(gates))
@@ -138,7 +139,8 @@ def wgrad_splitk(dy, x):
 
 
 class LucyCellFn(torch.autograd.Function):
-    """One LucyRNN layer: gates = x W^T + b (one GEMM, compute dtype `cdt`) -> HIP scan.
+    """One LucyRNN layer: gates = x W^T (one GEMM, compute dtype `cdt`) -> HIP scan, which adds
+    the fp32 bias b to the gates on load (a bias epilogue costs the GEMM ~25%, measured).
 
     Backward: scan adjoint (which also emits the bias gradient as per-row partial sums),
     dx = dgates W, dW = split-K dgates^T x.  lucyrnn_triton.py:50-75 fused into one node.
@@ -148,20 +150,22 @@ class LucyCellFn(torch.autograd.Function):
     def forward(ctx, x2d, w, b, h0, s0, B, T, cdt):
         xc = x2d.to(cdt)
         wc = w.to(cdt)
+        bias = b.detach().to(torch.float32).contiguous()
         with _timed("gate_gemm_fwd", xc, 0):
-            gates = torch.addmm(b.to(cdt), xc, wc.t()).view(B, T, 7, -1)
+            gates = torch.matmul(xc, wc.t()).view(B, T, 7, -1)
         need = any(ctx.needs_input_grad)
-        gates, out, s_out, ckpt = _scan_fwd(gates, h0, s0, need)
+        gates, out, s_out, ckpt = _scan_fwd(gates, h0, s0, need, bias)
         if need:
-            ctx.save_for_backward(xc, wc, gates, ckpt)
+            ctx.save_for_backward(xc, wc, gates, ckpt, bias)
             ctx.dtypes = (x2d.dtype, w.dtype, h0.dtype, s0.dtype)
         return out, s_out
 
     @staticmethod
     def backward(ctx, dout, ds_last):
-        xc, wc, gates, ckpt = ctx.saved_tensors
+        xc, wc, gates, ckpt, bias = ctx.saved_tensors
         xdt, wdt, hdt, sdt = ctx.dtypes
-        dgates, dh0, ds0, dbias = _scan_bwd(gates, ckpt, dout, ds_last, ctx.needs_input_grad[2])
+        dgates, dh0, ds0, dbias = _scan_bwd(gates, ckpt, dout, ds_last, ctx.needs_input_grad[2],
+                                            bias)
         dg2 = dgates.view(-1, dgates.shape[2] * dgates.shape[3])
         with _timed("gate_gemm_dgrad", dg2, 0):
             dx = (dg2 @ wc).to(xdt) if ctx.needs_input_grad[0] else None
