@@ -56,39 +56,48 @@ int64_t sc_lucy_scan_ckpt_numel(int B, int T, int D);
 /*
  * Forward scan.  Mirrors rnn_forward_unfused_rmsnorm(gates_ptr, h0_ptr, s0_ptr, out_ptr,
  * s_out_ptr, B, T, D, stride_g_bt, stride_g_td, stride_g_cd, stride_o_bt, stride_o_bd)
- * (lucyrnn_triton.py:180-194).
- *   gates  [B,T,7,D] of gates_dtype, d-stride 1, gate order r,z,k,v,h_pre,decay,alpha
+ * (lucyrnn_triton.py:180-194), plus one stride the reference does not have:
+ *   gates  gate g (order r,z,k,v,h_pre,decay,alpha) of hidden unit d at step t of row b is at
+ *            b*stride_g_bt + t*stride_g_td + g*stride_g_cd + (d/64)*stride_g_cb + d%64
+ *          i.e. hidden units come in 64-wide column blocks.  The reference's [B,T,7,D] layout
+ *          is stride_g_cb = 64.  The step-blocked layout [B,T,ceil(D/64),7,64] (stride_g_cd = 64,
+ *          stride_g_cb = 448; what a projection GEMM writes when its weight rows are permuted
+ *          accordingly) puts each step's 7 x 64 gates of one column block in one contiguous
+ *          run, which the kernel streams in whole 16-byte pieces.
  *   gate_bias  NULL (gates already include the projection bias, as in the reference), or fp32
- *          [7,D] added to every step's gates on load (lets the projection GEMM skip its bias
- *          epilogue; the backward then needs the same pointer)
+ *          [7,D] (logical order g*D + d) added to every step's gates on load (lets the
+ *          projection GEMM skip its bias epilogue; the backward then needs the same pointer)
  *   h0,s0  [B,D] fp32 contiguous (read exactly as contiguous; the caller must not pass the
  *          strided out[:, -1] view the reference passes — SURVEY F3)
  *   out    [B,T,D] of gates_dtype, d-stride 1 (strides stride_o_bt, stride_o_bd)
  *   s_out  [B,D] fp32 contiguous: state after the last step
  *   ckpt   NULL, or sc_lucy_scan_ckpt_numel() floats: (s,h) at every super-chunk start,
  *          consumed by sc_lucy_scan_bwd (training)
- * State arithmetic is fp32 for every gates_dtype.
+ * State arithmetic is fp32 for every gates_dtype.  Any element strides work; 16-byte aligned
+ * gates with strides (and D) in multiples of 16 bytes take the wide-piece path.
  */
 int sc_lucy_scan_fwd(const void* gates, int gates_dtype, const float* gate_bias,
                      const float* h0, const float* s0,
                      void* out, float* s_out, int B, int T, int D,
                      int64_t stride_g_bt, int64_t stride_g_td, int64_t stride_g_cd,
-                     int64_t stride_o_bt, int64_t stride_o_bd, float* ckpt, void* stream);
+                     int64_t stride_g_cb, int64_t stride_o_bt, int64_t stride_o_bd, float* ckpt,
+                     void* stream);
 
 /*
  * Backward scan.  Inputs: the forward's gates and ckpt, dout = dL/d out (same dtype as gates,
  * strides stride_d_bt/stride_d_bd), ds_last = dL/d s_out (fp32 [B,D], may be NULL = zero).
- * Outputs: dgates (gates_dtype, strides stride_dg_*), dh0, ds0 (fp32 [B,D]) and, if dbias is
- * not NULL, dbias fp32 [B,7,D] = sum over t of the stored dgates (per batch row; summing over
- * b gives the gate-projection bias gradient without another pass over dgates).
+ * Outputs: dgates (gates_dtype, laid out like gates with strides stride_dg_*), dh0, ds0 (fp32
+ * [B,D]) and, if dbias is not NULL, dbias fp32 [B,7,D] = sum over t of the stored dgates (per
+ * batch row; summing over b gives the gate-projection bias gradient without another pass over
+ * dgates).
  */
 int sc_lucy_scan_bwd(const void* gates, int gates_dtype, const float* gate_bias, const float* ckpt,
                      const void* dout, const float* ds_last,
                      void* dgates, float* dh0, float* ds0, float* dbias, int B, int T, int D,
                      int64_t stride_g_bt, int64_t stride_g_td, int64_t stride_g_cd,
-                     int64_t stride_d_bt, int64_t stride_d_bd,
+                     int64_t stride_g_cb, int64_t stride_d_bt, int64_t stride_d_bd,
                      int64_t stride_dg_bt, int64_t stride_dg_td, int64_t stride_dg_cd,
-                     void* stream);
+                     int64_t stride_dg_cb, void* stream);
 
 /* ---------------------------------------------------------------- decay scan ------------ */
 

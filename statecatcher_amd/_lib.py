@@ -16,15 +16,18 @@ _DTYPE = {torch.float32: SC_F32, torch.bfloat16: SC_BF16, torch.float16: SC_F16}
 
 _c = ctypes
 _i32, _i64, _vp, _fp = _c.c_int, _c.c_int64, _c.c_void_p, _c.c_void_p
+ABI_VERSION = 2  # include/statecatcher.h; bumped on any signature change
+
 _SIGS = {
     "sc_abi_version": (_i32, []),
     "sc_last_error": (_c.c_char_p, []),
     "sc_lucy_scan_chunk": (_i32, []),
     "sc_lucy_scan_ckpt_numel": (_i64, [_i32, _i32, _i32]),
     "sc_lucy_scan_fwd": (_i32, [_vp, _i32, _fp, _fp, _fp, _vp, _fp, _i32, _i32, _i32,
-                               _i64, _i64, _i64, _i64, _i64, _fp, _vp]),
+                               _i64, _i64, _i64, _i64, _i64, _i64, _fp, _vp]),
     "sc_lucy_scan_bwd": (_i32, [_vp, _i32, _fp, _fp, _vp, _fp, _vp, _fp, _fp, _fp, _i32, _i32, _i32,
-                               _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _vp]),
+                               _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64,
+                               _vp]),
     "sc_decay_scan_fwd": (_i32, [_vp, _vp, _vp, _i32, _fp, _i32, _i32, _i32, _i64, _i64, _i64, _vp]),
     "sc_decay_scan_bwd": (_i32, [_vp, _vp, _vp, _vp, _vp, _i32, _fp, _fp, _i32, _i32, _i32,
                                 _i64, _i64, _i64, _vp]),
@@ -58,7 +61,7 @@ def load():
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
-        if lib.sc_abi_version() != 1:
+        if lib.sc_abi_version() != ABI_VERSION:
             raise RuntimeError("statecatcher ABI version mismatch")
         _LIB = lib
     return _LIB

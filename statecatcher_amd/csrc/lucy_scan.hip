@@ -13,18 +13,23 @@
 // Gates depend only on the layer input, so both recurrences are first-order LINEAR scans
 // (SURVEY F5): s is affine in s_{t-1}; given s, h is affine in h_{t-1}.
 //
-// Decomposition (MI355X-first): one workgroup = one batch row b x 64 hidden units (lane = d,
-// coalesced 64-wide rows of the [B,T,7,D] gates) x NW waves that split TIME.  Time is walked in
-// super-chunks of 64 steps; wave w owns steps [w*LC, (w+1)*LC) of the super-chunk.  Per
-// super-chunk each wave
-//   1. computes the elementwise gate terms of its LC steps from registers (gates read ONCE),
+// Decomposition (MI355X-first): one workgroup = one batch row b x one 64-wide column block of
+// hidden units (lane = d) x NW waves that split TIME.  Time is walked in super-chunks of 64
+// steps; wave w owns steps [w*LC, (w+1)*LC) of the super-chunk.  Per super-chunk each wave
+//   1. computes the elementwise gate terms of its LC steps (gates read ONCE from HBM),
 //   2. publishes its s-segment as an affine map (prod dec, local scan) in LDS, barrier,
 //      composes the maps of the waves before it with the carried state -> exact s,
 //   3. computes c = tanh(hn + s) and publishes its h-segment map, barrier, composes -> exact h,
 //   4. stores h (out) and hands the super-chunk's final (s, h) to the next one through LDS.
-// The next super-chunk's gates are loaded into registers while the current one computes, and
-// the barriers order LDS only, so those loads stay in flight (HBM stream never drains).
-// B*D/64 workgroups x NW waves: 256 x 8 = 2048 waves at the B=32, D=512 training shape.
+// B*ceil(D/64) workgroups x 16 waves: 256 x 16 at the B=32, D=512 training shape, one per CU.
+//
+// Gate stream (measured, tools/scan_probe.hip): the gates never pass through VGPRs on their
+// way in.  Each wave copies its LC steps x 7 gate rows of 64 units into a private LDS slot with
+// LDS-DMA (global_load_lds, 16-byte pieces), the copy of super-chunk k+1 in flight while k
+// computes, and reads its operands back with ds_read.  Versus register prefetch of 2-byte
+// elements this frees ~56 VGPRs per lane and lifts the probe kernel from 49% to 53% of HBM
+// peak; with the step-blocked gate layout (stride_g_cb = 448, a step's 7 x 64 gates contiguous
+// -> 896-byte runs instead of seven 128-byte rows) it reaches 60%.
 //
 // The forward checkpoints (s, h) at every super-chunk start (B*ceil(T/64)*2*D floats, 1/32 of the
 // output); the backward walks super-chunks in reverse, recomputes s, c, h from the gates it
@@ -33,6 +38,9 @@
 //   Gs_t = Gh_t (1-zg_t)(1-c_t^2) + dec_{t+1} Gs_{t+1},   Gs_{T-1} += ds_last
 // and writes the 7 gate gradients.  Algorithmic HBM bytes per (b,t,d): fwd 7e + e (+ckpt),
 // bwd 7e + e + 7e.
+
+#include <atomic>
+#include <initializer_list>
 
 #include "sc_common.h"
 
@@ -50,7 +58,7 @@ struct ScanFwdArgs {
   float* s_out;
   float* ckpt;
   int B, T, D, nsc;
-  int64_t g_bt, g_td, g_cd, o_bt, o_bd;
+  int64_t g_bt, g_td, g_cd, g_cb, o_bt, o_bd;
 };
 
 struct ScanBwdArgs {
@@ -64,7 +72,23 @@ struct ScanBwdArgs {
   float* ds0;
   float* dbias;   // optional [B,7,D]: sum over t of dgates (gate-projection bias gradient part)
   int B, T, D, nsc;
-  int64_t g_bt, g_td, g_cd, d_bt, d_bd, dg_bt, dg_td, dg_cd;
+  int64_t g_bt, g_td, g_cd, g_cb, d_bt, d_bd, dg_bt, dg_td, dg_cd, dg_cb;
+};
+
+// LDS-DMA piece geometry: a 64-unit row of T elements is PPR pieces of PW bytes.  A partial
+// last column block (D % 64 != 0) clamps pieces past its end onto its last valid piece.
+template <typename T, int PW> struct Pieces {
+  static constexpr int EPP = PW / (int)sizeof(T);   // elements per piece
+  static constexpr int PPR = 64 / EPP;              // pieces per row
+  static_assert(EPP >= 1 && 64 % EPP == 0, "piece width");
+};
+// Bytes per element in an LDS slot.  global_load_lds_ushort writes each lane's 2 bytes at a
+// 4-byte lane stride (measured), so the one-element path of 16-bit types pads to 4 bytes.
+template <typename T, int PW> struct LdsElem {
+  static constexpr int BYTES = PW == 2 ? 4 : (int)sizeof(T);
+  static __device__ __forceinline__ T get(const unsigned char* slot, int idx) {
+    return *(const T*)(slot + idx * BYTES);
+  }
 };
 
 // Elementwise part of lucyrnn_triton.py:213-235 for one (step, chain).
@@ -118,61 +142,80 @@ __device__ __forceinline__ void gate_grads(float r, float z, float k, float v, f
 }
 
 // ------------------------------------------------------------------------ forward ----------
-template <int DT, int NW, int LC>
+template <int DT, int NW, int LC, int PW>
 __global__ void __launch_bounds__(NW * 64)
 lucy_scan_fwd_kernel(ScanFwdArgs a) {
   static_assert(NW * LC == kChunk, "super-chunk must be 64 steps");
   using E = Elem<DT>;
   using T = typename E::T;
+  using P = Pieces<T, PW>;
+  constexpr int ROWS = LC * 7;                       // gate rows per wave per super-chunk
+  constexpr int PIECES = ROWS * P::PPR;
+  constexpr int NI = (PIECES + 63) / 64;             // DMA instructions per wave per super-chunk
   const int lane = threadIdx.x & 63;
   const int w = uniform(threadIdx.x >> 6);
   const int b = blockIdx.y;
-  const int d = blockIdx.x * 64 + lane;
+  const int blk = blockIdx.x;
+  const int d = blk * 64 + lane;
   const bool dok = d < a.D;
-  const int dc = dok ? d : a.D - 1;           // clamped column: loads never leave the row
+  const int dc = dok ? d : a.D - 1;
+  const int pcmax = (min(64, a.D - blk * 64) - 1) / P::EPP;
 
+  extern __shared__ __attribute__((aligned(16))) unsigned char dyn_lds[];
   __shared__ float2 aggS[NW][64];
   __shared__ float2 aggH[NW][64];
   __shared__ float carS[2][64];
   __shared__ float carH[2][64];
+  using L = LdsElem<T, PW>;
+  const unsigned char* slot = dyn_lds + w * ROWS * 64 * L::BYTES;   // wave-private [LC][7][64]
+  const uint32_t slot_lds = lds_addr(slot);
 
-  // per-row buffer descriptors; lane offset = column, scalar offset = (t, gate)
-  const Buf<T> gbuf((const T*)a.gates + (int64_t)b * a.g_bt);
+  const T* gsrc = (const T*)a.gates + (int64_t)b * a.g_bt + (int64_t)blk * a.g_cb;
   const Buf<T> obuf((T*)a.out + (int64_t)b * a.o_bt);
-  const uint32_t vg = (uint32_t)dc * sizeof(T);
   const uint32_t vo = (uint32_t)d * sizeof(T);
-  const uint32_t gtd = (uint32_t)(a.g_td * sizeof(T)), gcd = (uint32_t)(a.g_cd * sizeof(T));
   const uint32_t otd = (uint32_t)(a.o_bd * sizeof(T));
   if (w == 0) {
     carS[0][lane] = dok ? a.s0[(int64_t)b * a.D + d] : 0.0f;
     carH[0][lane] = dok ? a.h0[(int64_t)b * a.D + d] : 0.0f;
   }
-
-  // Two register buffers used ping-pong (explicitly, so no register copy ever waits on a
-  // load that is still in flight): super-chunk k+1 streams in while k computes.
-  uint32_t bufA[LC][7], bufB[LC][7];   // raw gate words (Elem::ldw)
   float gb[7];
 #pragma unroll
   for (int g = 0; g < 7; ++g) gb[g] = a.bias ? a.bias[g * a.D + dc] : 0.0f;
+  settle(gb);
   const int Tm1 = a.T - 1;
-  auto load = [&](uint32_t (&buf)[LC][7], int k) {
+  // Past the end of the sequence the clamped step re-reads row T-1 (never out of bounds).
+  auto issue = [&](int k) {
 #pragma unroll
-    for (int j = 0; j < LC; ++j) {
-      const uint32_t so = (uint32_t)min(k * kChunk + w * LC + j, Tm1) * gtd;
-#pragma unroll
-      for (int g = 0; g < 7; ++g) buf[j][g] = gbuf.ldw(vg, so + g * gcd);
+    for (int i = 0; i < NI; ++i) {
+      const int p = i * 64 + lane;
+      if (PIECES % 64 == 0 || p < PIECES) {
+        const int row = p / P::PPR, pc = p % P::PPR;
+        const int j = row / 7, g = row - 7 * (row / 7);
+        const int t = min(k * kChunk + w * LC + j, Tm1);
+        dma_to_lds<PW>(gsrc + (int64_t)t * a.g_td + (int64_t)g * a.g_cd + min(pc, pcmax) * P::EPP,
+                       slot_lds + i * 64 * (PW == 2 ? 4 : PW));
+      }
     }
   };
-  auto body = [&](const uint32_t (&cur)[LC][7], int k) __attribute__((always_inline)) {
+  if (a.nsc > 0) issue(0);
+  dma_wait();
+  lds_barrier();
+  for (int k = 0; k < a.nsc; ++k) {
     const int t0 = k * kChunk + w * LC;
     float zg[LC], dec[LC], u[LC], x[LC];
+    float gv[LC][7];
+#pragma unroll
+    for (int j = 0; j < LC; ++j)
+#pragma unroll
+      for (int g = 0; g < 7; ++g) gv[j][g] = E::ld(L::get(slot, (j * 7 + g) * 64 + lane)) + gb[g];
+    lds_read_wait();              // slot consumed: it may be refilled with super-chunk k+1
+    if (k + 1 < a.nsc) issue(k + 1);
     float As = 1.0f, Bs = 0.0f;
 #pragma unroll
     for (int j = 0; j < LC; ++j) {
       if (t0 + j < a.T) {
-        step_terms(E::ldw(cur[j][0]) + gb[0], E::ldw(cur[j][1]) + gb[1], E::ldw(cur[j][2]) + gb[2],
-                   E::ldw(cur[j][3]) + gb[3], E::ldw(cur[j][4]) + gb[4], E::ldw(cur[j][5]) + gb[5],
-                   E::ldw(cur[j][6]) + gb[6], zg[j], dec[j], u[j], x[j]);
+        step_terms(gv[j][0], gv[j][1], gv[j][2], gv[j][3], gv[j][4], gv[j][5], gv[j][6], zg[j],
+                   dec[j], u[j], x[j]);
       } else {  // identity step past the end of the sequence
         zg[j] = 1.0f; dec[j] = 1.0f; u[j] = 0.0f; x[j] = 0.0f;
       }
@@ -197,6 +240,7 @@ lucy_scan_fwd_kernel(ScanFwdArgs a) {
     }
     if (w == NW - 1) carS[(k + 1) & 1][lane] = s;
     aggH[w][lane] = make_float2(Ah, Bh);
+    dma_wait();                   // super-chunk k+1 has landed in this wave's slot
     lds_barrier();
     float h = carH[k & 1][lane];
     if (w == 0 && a.ckpt && dok) a.ckpt[((int64_t)(b * a.nsc + k) * 2 + 1) * a.D + d] = h;
@@ -210,112 +254,120 @@ lucy_scan_fwd_kernel(ScanFwdArgs a) {
       if (dok && t0 + j < a.T) obuf.st(E::st(h), vo, (uint32_t)(t0 + j) * otd);
     }
     if (w == NW - 1) carH[(k + 1) & 1][lane] = h;
-  };
-  if (a.nsc > 0) load(bufA, 0);
-  lds_barrier();
-  // Prefetches are unconditional: past the end the clamped time index re-reads row T-1 (a cache
-  // hit); a branch around them would make hipcc's vmcnt bookkeeping fall back to full drains.
-  for (int k = 0; k < a.nsc; k += 2) {
-    load(bufB, k + 1);
-    body(bufA, k);
-    if (k + 1 >= a.nsc) break;
-    load(bufA, k + 2);
-    body(bufB, k + 1);
   }
   lds_barrier();
   if (w == 0 && dok) a.s_out[(int64_t)b * a.D + d] = carS[a.nsc & 1][lane];
 }
 
 // ------------------------------------------------------------------------ backward ---------
-template <int DT, int NW, int LC>
+// NBUF = 2: two LDS slots per wave, the raw gates stay in LDS for the gate-gradient phase while
+// the next super-chunk lands in the other slot (16-bit gates).  NBUF = 1 (fp32, whose two slots
+// would not fit in LDS): the raw gates are copied to VGPRs and the slot is refilled at once.
+template <int DT, int NW, int LC, int PW, int NBUF>
 __global__ void __launch_bounds__(NW * 64)
 lucy_scan_bwd_kernel(ScanBwdArgs a) {
   static_assert(NW * LC == kChunk, "super-chunk must be 64 steps");
   using E = Elem<DT>;
   using T = typename E::T;
+  using P = Pieces<T, PW>;
+  constexpr int GROWS = LC * 7;                      // gate rows, then LC rows of dout
+  constexpr int ROWS = LC * 8;
+  constexpr int PIECES = ROWS * P::PPR;
+  constexpr int NI = (PIECES + 63) / 64;
   const int lane = threadIdx.x & 63;
   const int w = uniform(threadIdx.x >> 6);
   const int b = blockIdx.y;
-  const int d = blockIdx.x * 64 + lane;
+  const int blk = blockIdx.x;
+  const int d = blk * 64 + lane;
   const bool dok = d < a.D;
   const int dc = dok ? d : a.D - 1;
+  const int pcmax = (min(64, a.D - blk * 64) - 1) / P::EPP;
 
+  extern __shared__ __attribute__((aligned(16))) unsigned char dyn_lds[];
   __shared__ float2 aggA[NW][64];
   __shared__ float2 aggB[NW][64];
   __shared__ float carGh[2][64];
   __shared__ float carGs[2][64];
-  __shared__ float stS[NW][LC][64];   // s_{t-1} per step (recomputed forward), LDS not VGPRs
-  __shared__ float stH[NW][LC][64];   // h_{t-1}
-  // 16-bit gates: the current super-chunk's raw gates are parked in LDS (wave-private rows) so
-  // their registers are free while the next super-chunk's prefetch is in flight.
-  constexpr bool kStage = sizeof(T) == 2;
-  __shared__ uint16_t rawS[kStage ? NW : 1][LC][7][64];
+  __shared__ float ckS[2][2][64];   // (s, h) checkpoint of the super-chunk, shared by all waves
+  using L = LdsElem<T, PW>;
+  const unsigned char* slots = dyn_lds + w * NBUF * ROWS * 64 * L::BYTES;   // [NBUF][LC*8][64]
+  const uint32_t slots_lds = lds_addr(slots);
 
-  const Buf<T> gbuf((const T*)a.gates + (int64_t)b * a.g_bt);
-  const Buf<T> dbuf((const T*)a.dout + (int64_t)b * a.d_bt);
-  const Buf<T> obuf((T*)a.dgates + (int64_t)b * a.dg_bt);
-  const uint32_t vg = (uint32_t)dc * sizeof(T);
-  const uint32_t vo = (uint32_t)d * sizeof(T);
-  const uint32_t gtd = (uint32_t)(a.g_td * sizeof(T)), gcd = (uint32_t)(a.g_cd * sizeof(T));
-  const uint32_t dtd = (uint32_t)(a.d_bd * sizeof(T));
-  const uint32_t otd = (uint32_t)(a.dg_td * sizeof(T)), ocd = (uint32_t)(a.dg_cd * sizeof(T));
+  const T* gsrc = (const T*)a.gates + (int64_t)b * a.g_bt + (int64_t)blk * a.g_cb;
+  const T* dsrc = (const T*)a.dout + (int64_t)b * a.d_bt + (int64_t)blk * 64;
+  const float* cksrc = a.ckpt + (int64_t)b * a.nsc * 2 * a.D + dc;
+  const Buf<T> dgbuf((T*)a.dgates + (int64_t)b * a.dg_bt + (int64_t)blk * a.dg_cb);
+  const uint32_t vo = (uint32_t)lane * sizeof(T);
   if (w == 0) {
     carGh[0][lane] = 0.0f;
     carGs[0][lane] = (a.ds_last && dok) ? a.ds_last[(int64_t)b * a.D + d] : 0.0f;
   }
-
-  uint32_t bufA[LC][7], bufB[LC][7];   // raw gate words (Elem::ldw), ping-pong
-  uint32_t dbA[LC], dbB[LC];
-  // gate bias through LDS (one word per lane and gate): at 128 VGPRs the backward has no room
-  // for 7 more live registers
-  __shared__ float gbS[7][64];
-  if (w == 0) {
+  float gb[7];
 #pragma unroll
-    for (int g = 0; g < 7; ++g) gbS[g][lane] = a.bias ? a.bias[g * a.D + dc] : 0.0f;
-  }
-#define gb(g) gbS[g][lane]
-  float ckA[2], ckB[2];                // (s, h) checkpoint at the super-chunk start
-  const Buf<float> cbuf(a.ckpt + (int64_t)b * a.nsc * 2 * a.D);
-  const uint32_t vc = (uint32_t)dc * 4;
+  for (int g = 0; g < 7; ++g) gb[g] = a.bias ? a.bias[g * a.D + dc] : 0.0f;
+  settle(gb);
   const int Tm1 = a.T - 1;
-  // checkpoint words first: they are then the OLDEST loads of the group, so consuming them
-  // never waits on the gate stream behind them
-  auto load = [&](uint32_t (&buf)[LC][7], uint32_t (&db)[LC], float (&ck)[2], int k) {
-    ck[0] = cbuf.ld(vc, (uint32_t)(k * 2) * a.D * 4);
-    ck[1] = cbuf.ld(vc, (uint32_t)(k * 2 + 1) * a.D * 4);
+  auto issue = [&](int it) {
+    const int k = a.nsc - 1 - it;
+    const uint32_t base = slots_lds + (uint32_t)((it % NBUF) * ROWS * 64 * L::BYTES);
 #pragma unroll
-    for (int j = 0; j < LC; ++j) {
-      const uint32_t t = (uint32_t)min(k * kChunk + w * LC + j, Tm1);
-#pragma unroll
-      for (int g = 0; g < 7; ++g) buf[j][g] = gbuf.ldw(vg, t * gtd + g * gcd);
-      db[j] = dbuf.ldw(vg, t * dtd);
+    for (int i = 0; i < NI; ++i) {
+      const int p = i * 64 + lane;
+      if (PIECES % 64 == 0 || p < PIECES) {
+        const int row = p / P::PPR, pc = p % P::PPR;
+        const int col = min(pc, pcmax) * P::EPP;
+        const T* src;
+        if (row < GROWS) {
+          const int j = row / 7, g = row - 7 * (row / 7);
+          const int t = min(k * kChunk + w * LC + j, Tm1);
+          src = gsrc + (int64_t)t * a.g_td + (int64_t)g * a.g_cd + col;
+        } else {
+          const int t = min(k * kChunk + w * LC + (row - GROWS), Tm1);
+          src = dsrc + (int64_t)t * a.d_bd + col;
+        }
+        dma_to_lds<PW>(src, base + i * 64 * (PW == 2 ? 4 : PW));
+      }
+    }
+    if (w == 0) {
+      dma_to_lds<4>(cksrc + (int64_t)(k * 2) * a.D, lds_addr(&ckS[it & 1][0][0]));
+      dma_to_lds<4>(cksrc + (int64_t)(k * 2 + 1) * a.D, lds_addr(&ckS[it & 1][1][0]));
     }
   };
   float bacc[7] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};   // bias-gradient partial sums
-  auto body = [&](const uint32_t (&cur)[LC][7], const uint32_t (&dcur)[LC], const float (&ck)[2],
-                  int it) __attribute__((always_inline)) {
+  if (a.nsc > 0) issue(0);
+  dma_wait();
+  lds_barrier();
+  for (int it = 0; it < a.nsc; ++it) {
     const int k = a.nsc - 1 - it;
     const int t0 = k * kChunk + w * LC;
-    const float s_ck = ck[0];
-    const float h_ck = ck[1];
-    float zg[LC], dec[LC], u[LC], x[LC];
+    const unsigned char* slot = slots + (it % NBUF) * ROWS * 64 * L::BYTES;
+    if (NBUF == 2 && it + 1 < a.nsc) issue(it + 1);     // into the other slot
+    const float s_ck = ckS[it & 1][0][lane];
+    const float h_ck = ckS[it & 1][1][lane];
+    float zg[LC], dec[LC], u[LC], x[LC], dj[LC], sv[LC], hv[LC];
+    float rg[NBUF == 1 ? LC : 1][7];
     // ---- recompute the forward of this super-chunk ----
     float As = 1.0f, Bs = 0.0f;
 #pragma unroll
     for (int j = 0; j < LC; ++j) {
-      if constexpr (kStage) {
+      float g7[7];
 #pragma unroll
-        for (int g = 0; g < 7; ++g) rawS[w][j][g][lane] = (uint16_t)cur[j][g];
+      for (int g = 0; g < 7; ++g) {
+        g7[g] = E::ld(L::get(slot, (j * 7 + g) * 64 + lane)) + gb[g];
+        if constexpr (NBUF == 1) rg[j][g] = g7[g];
       }
+      dj[j] = (t0 + j < a.T) ? E::ld(L::get(slot, (GROWS + j) * 64 + lane)) : 0.0f;
       if (t0 + j < a.T) {
-        step_terms(E::ldw(cur[j][0]) + gb(0), E::ldw(cur[j][1]) + gb(1), E::ldw(cur[j][2]) + gb(2),
-                   E::ldw(cur[j][3]) + gb(3), E::ldw(cur[j][4]) + gb(4), E::ldw(cur[j][5]) + gb(5),
-                   E::ldw(cur[j][6]) + gb(6), zg[j], dec[j], u[j], x[j]);
+        step_terms(g7[0], g7[1], g7[2], g7[3], g7[4], g7[5], g7[6], zg[j], dec[j], u[j], x[j]);
       } else {
         zg[j] = 1.0f; dec[j] = 1.0f; u[j] = 0.0f; x[j] = 0.0f;
       }
       As *= dec[j];
       Bs = dec[j] * Bs + u[j];
+    }
+    if constexpr (NBUF == 1) {
+      lds_read_wait();
+      if (it + 1 < a.nsc) issue(it + 1);                // refill the slot just read
     }
     aggA[w][lane] = make_float2(As, Bs);
     lds_barrier();                                             // B1
@@ -327,7 +379,7 @@ lucy_scan_bwd_kernel(ScanBwdArgs a) {
     float Ah = 1.0f, Bh = 0.0f;
 #pragma unroll
     for (int j = 0; j < LC; ++j) {
-      stS[w][j][lane] = s;
+      sv[j] = s;
       s = dec[j] * s + u[j];
       x[j] = tanh_sig(x[j] + s);
       Ah *= zg[j];
@@ -342,15 +394,14 @@ lucy_scan_bwd_kernel(ScanBwdArgs a) {
     }
 #pragma unroll
     for (int j = 0; j < LC; ++j) {
-      stH[w][j][lane] = h;
+      hv[j] = h;
       h = zg[j] * h + (1.0f - zg[j]) * x[j];
     }
     // ---- adjoint of h: C_t = zg_t Gh_t flows to step t-1 ----
     float Ph = 1.0f, Qh = 0.0f;
 #pragma unroll
     for (int j = LC - 1; j >= 0; --j) {
-      const float dj = (t0 + j < a.T) ? E::ldw(dcur[j]) : 0.0f;
-      Qh = zg[j] * (dj + Qh);
+      Qh = zg[j] * (dj[j] + Qh);
       Ph *= zg[j];
     }
     aggA[w][lane] = make_float2(Ph, Qh);
@@ -362,8 +413,7 @@ lucy_scan_bwd_kernel(ScanBwdArgs a) {
     }
 #pragma unroll
     for (int j = LC - 1; j >= 0; --j) {
-      const float dj = (t0 + j < a.T) ? E::ldw(dcur[j]) : 0.0f;
-      u[j] = dj + C;                                            // Gh_t
+      u[j] = dj[j] + C;                                         // Gh_t
       C = zg[j] * u[j];
     }
     if (w == 0) carGh[(it + 1) & 1][lane] = C;
@@ -375,6 +425,7 @@ lucy_scan_bwd_kernel(ScanBwdArgs a) {
       Ps *= dec[j];
     }
     aggB[w][lane] = make_float2(Ps, Qs);
+    dma_wait();                   // the next super-chunk (and its checkpoint) has landed
     lds_barrier();                                             // B4
     float Cs = carGs[it & 1][lane];
     for (int q = NW - 1; q > w; --q) {
@@ -389,44 +440,36 @@ lucy_scan_bwd_kernel(ScanBwdArgs a) {
       if (dok && t0 + j < a.T) {
         float o[7], g7[7];
 #pragma unroll
-        for (int g = 0; g < 7; ++g)
-          g7[g] = (kStage ? E::ldw((uint32_t)rawS[w][j][g][lane]) : E::ldw(cur[j][g])) + gb(g);
-        gate_grads(g7[0], g7[1], g7[2], g7[3], g7[4], g7[5], g7[6], u[j], dpre, gs,
-                   stH[w][j][lane], stS[w][j][lane], x[j], o);
-        const uint32_t so = (uint32_t)(t0 + j) * otd;
+        for (int g = 0; g < 7; ++g) {
+          if constexpr (NBUF == 1) g7[g] = rg[j][g];
+          else g7[g] = E::ld(L::get(slot, (j * 7 + g) * 64 + lane)) + gb[g];
+        }
+        gate_grads(g7[0], g7[1], g7[2], g7[3], g7[4], g7[5], g7[6], u[j], dpre, gs, hv[j], sv[j],
+                   x[j], o);
+        const uint32_t so = (uint32_t)((t0 + j) * a.dg_td * sizeof(T));
 #pragma unroll
         for (int g = 0; g < 7; ++g) {
           const T og = E::st(o[g]);
-          obuf.st(og, vo, so + g * ocd);
+          dgbuf.st(og, vo, so + (uint32_t)(g * a.dg_cd * sizeof(T)));
           bacc[g] += E::ld(og);   // sum what is stored, so db == dgates.sum() exactly as a GEMM sees it
         }
       }
     }
     if (w == 0) carGs[(it + 1) & 1][lane] = Cs;
-  };
-  if (a.nsc > 0) load(bufA, dbA, ckA, a.nsc - 1);
-  lds_barrier();
-  for (int it = 0; it < a.nsc; it += 2) {
-    load(bufB, dbB, ckB, max(a.nsc - 2 - it, 0));
-    body(bufA, dbA, ckA, it);
-    if (it + 1 >= a.nsc) break;
-    load(bufA, dbA, ckA, max(a.nsc - 3 - it, 0));
-    body(bufB, dbB, ckB, it + 1);
   }
   lds_barrier();
   if (w == 0 && dok) {
     a.dh0[(int64_t)b * a.D + d] = carGh[a.nsc & 1][lane];
     a.ds0[(int64_t)b * a.D + d] = carGs[a.nsc & 1][lane];
   }
-#undef gb
   if (a.dbias) {   // reduce the per-wave partials over the NW waves (fixed order: deterministic)
 #pragma unroll
     for (int g = 0; g < 7; ++g) {
-      stS[w][0][lane] = bacc[g];
+      aggA[w][lane].x = bacc[g];
       lds_barrier();
       if (w == 0) {
         float acc = 0.0f;
-        for (int q = 0; q < NW; ++q) acc += stS[q][0][lane];
+        for (int q = 0; q < NW; ++q) acc += aggA[q][lane].x;
         if (dok) a.dbias[((int64_t)b * 7 + g) * a.D + d] = acc;
       }
       lds_barrier();
@@ -435,23 +478,67 @@ lucy_scan_bwd_kernel(ScanBwdArgs a) {
 }
 
 // ------------------------------------------------------------------------ launchers --------
-// Wave split of the 64-step super-chunk.  NW=8 x LC=8: 8 waves per workgroup (one workgroup
-// per CU at B*D/64 = 256).  Selected per dtype from measurements.
-template <int DT> struct FwdCfg { static constexpr int NW = 16, LC = 4; };
-template <int DT> struct BwdCfg { static constexpr int NW = 16, LC = 4; };
+// 16 waves x 4 steps per wave (one 16-wave workgroup per CU at B*D/64 = 256), every dtype.
+constexpr int kNW = 16, kLC = 4;
 
-template <int DT>
+// > 64 KiB of dynamic LDS must be opted into per kernel (gfx950 has 160 KiB per CU).  Called
+// once per kernel instantiation (function-local static): the call costs host time per launch.
+template <typename K>
+static bool set_lds_limit(K kernel, size_t bytes) {
+  return hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)bytes) == hipSuccess;
+}
+
+template <int DT, int PW>
 static void launch_fwd(const ScanFwdArgs& a, hipStream_t st) {
-  constexpr int NW = FwdCfg<DT>::NW, LC = FwdCfg<DT>::LC;
+  using T = typename Elem<DT>::T;
+  auto kern = lucy_scan_fwd_kernel<DT, kNW, kLC, PW>;
+  const size_t lds = (size_t)kNW * kLC * 7 * 64 * LdsElem<T, PW>::BYTES;
+  static const bool lds_ok = set_lds_limit(kern, lds);
+  (void)lds_ok;
   dim3 grid((a.D + 63) / 64, a.B);
-  hipLaunchKernelGGL((lucy_scan_fwd_kernel<DT, NW, LC>), grid, dim3(NW * 64), 0, st, a);
+  hipLaunchKernelGGL(kern, grid, dim3(kNW * 64), lds, st, a);
+}
+
+template <int DT, int PW>
+static void launch_bwd(const ScanBwdArgs& a, hipStream_t st) {
+  using T = typename Elem<DT>::T;
+  // two slots per wave fit only for 2-byte LDS elements (160 KiB per CU)
+  constexpr int NBUF = LdsElem<T, PW>::BYTES == 2 ? 2 : 1;
+  auto kern = lucy_scan_bwd_kernel<DT, kNW, kLC, PW, NBUF>;
+  const size_t lds = (size_t)NBUF * kNW * kLC * 8 * 64 * LdsElem<T, PW>::BYTES;
+  static const bool lds_ok = set_lds_limit(kern, lds);
+  (void)lds_ok;
+  dim3 grid((a.D + 63) / 64, a.B);
+  hipLaunchKernelGGL(kern, grid, dim3(kNW * 64), lds, st, a);
+}
+
+// 16-byte pieces need a 16-byte aligned base and every stride and D in whole pieces; otherwise
+// pieces of one element (2 or 4 bytes) handle any layout.
+static bool wide_pieces(const void* p, int esize, int D, std::initializer_list<int64_t> strides) {
+  const int epp = 16 / esize;
+  if ((uintptr_t)p % 16 || D % epp) return false;
+  for (int64_t s : strides)
+    if (s % epp) return false;
+  return true;
 }
 
 template <int DT>
-static void launch_bwd(const ScanBwdArgs& a, hipStream_t st) {
-  constexpr int NW = BwdCfg<DT>::NW, LC = BwdCfg<DT>::LC;
-  dim3 grid((a.D + 63) / 64, a.B);
-  hipLaunchKernelGGL((lucy_scan_bwd_kernel<DT, NW, LC>), grid, dim3(NW * 64), 0, st, a);
+static void dispatch_fwd(const ScanFwdArgs& a, hipStream_t st) {
+  if (wide_pieces(a.gates, sizeof(typename Elem<DT>::T), a.D, {a.g_bt, a.g_td, a.g_cd, a.g_cb}))
+    launch_fwd<DT, 16>(a, st);
+  else
+    launch_fwd<DT, (int)sizeof(typename Elem<DT>::T)>(a, st);
+}
+
+template <int DT>
+static void dispatch_bwd(const ScanBwdArgs& a, hipStream_t st) {
+  constexpr int es = sizeof(typename Elem<DT>::T);
+  if (wide_pieces(a.gates, es, a.D, {a.g_bt, a.g_td, a.g_cd, a.g_cb}) &&
+      wide_pieces(a.dout, es, a.D, {a.d_bt, a.d_bd}))
+    launch_bwd<DT, 16>(a, st);
+  else
+    launch_bwd<DT, es>(a, st);
 }
 
 }  // namespace sc
@@ -471,8 +558,8 @@ extern "C" int sc_lucy_scan_fwd(const void* gates, int gates_dtype, const float*
                                 const float* h0,
                                 const float* s0, void* out, float* s_out, int B, int T, int D,
                                 int64_t stride_g_bt, int64_t stride_g_td, int64_t stride_g_cd,
-                                int64_t stride_o_bt, int64_t stride_o_bd, float* ckpt,
-                                void* stream) {
+                                int64_t stride_g_cb, int64_t stride_o_bt, int64_t stride_o_bd,
+                                float* ckpt, void* stream) {
   clear_error();
   SC_REQUIRE(check_dtype(gates_dtype), "sc_lucy_scan_fwd: unsupported gates dtype %d", gates_dtype);
   SC_REQUIRE(B >= 0 && T >= 0 && D >= 0, "sc_lucy_scan_fwd: negative shape B=%d T=%d D=%d", B, T, D);
@@ -480,13 +567,18 @@ extern "C" int sc_lucy_scan_fwd(const void* gates, int gates_dtype, const float*
   if (B == 0 || D == 0) return 0;
   SC_REQUIRE(h0 && s0 && s_out, "sc_lucy_scan_fwd: null state pointer");
   SC_REQUIRE(T == 0 || (gates && out), "sc_lucy_scan_fwd: null gates/out pointer");
+  SC_REQUIRE(stride_g_bt >= 0 && stride_g_td >= 0 && stride_g_cd >= 0 && stride_g_cb >= 0 &&
+                 stride_o_bt >= 0 && stride_o_bd >= 0,
+             "sc_lucy_scan_fwd: negative stride");
+  SC_REQUIRE((int64_t)T * stride_o_bd * 4 < (1ll << 31),
+             "sc_lucy_scan_fwd: one batch row of out spans >= 2 GiB");
   ScanFwdArgs a{gates, gate_bias, h0, s0, out, s_out, ckpt, B, T, D, (T + kChunk - 1) / kChunk,
-                stride_g_bt, stride_g_td, stride_g_cd, stride_o_bt, stride_o_bd};
+                stride_g_bt, stride_g_td, stride_g_cd, stride_g_cb, stride_o_bt, stride_o_bd};
   hipStream_t st = (hipStream_t)stream;
   switch (gates_dtype) {
-    case SC_F32: launch_fwd<SC_F32>(a, st); break;
-    case SC_BF16: launch_fwd<SC_BF16>(a, st); break;
-    default: launch_fwd<SC_F16>(a, st); break;
+    case SC_F32: dispatch_fwd<SC_F32>(a, st); break;
+    case SC_BF16: dispatch_fwd<SC_BF16>(a, st); break;
+    default: dispatch_fwd<SC_F16>(a, st); break;
   }
   return launch_status("sc_lucy_scan_fwd");
 }
@@ -495,9 +587,10 @@ extern "C" int sc_lucy_scan_bwd(const void* gates, int gates_dtype, const float*
                                 const float* ckpt,
                                 const void* dout, const float* ds_last, void* dgates, float* dh0,
                                 float* ds0, float* dbias, int B, int T, int D, int64_t stride_g_bt,
-                                int64_t stride_g_td, int64_t stride_g_cd, int64_t stride_d_bt,
-                                int64_t stride_d_bd, int64_t stride_dg_bt, int64_t stride_dg_td,
-                                int64_t stride_dg_cd, void* stream) {
+                                int64_t stride_g_td, int64_t stride_g_cd, int64_t stride_g_cb,
+                                int64_t stride_d_bt, int64_t stride_d_bd, int64_t stride_dg_bt,
+                                int64_t stride_dg_td, int64_t stride_dg_cd, int64_t stride_dg_cb,
+                                void* stream) {
   clear_error();
   SC_REQUIRE(check_dtype(gates_dtype), "sc_lucy_scan_bwd: unsupported gates dtype %d", gates_dtype);
   SC_REQUIRE(B >= 0 && T >= 0 && D >= 0, "sc_lucy_scan_bwd: negative shape B=%d T=%d D=%d", B, T, D);
@@ -507,15 +600,21 @@ extern "C" int sc_lucy_scan_bwd(const void* gates, int gates_dtype, const float*
   if (T == 0 && dbias) (void)hipMemsetAsync(dbias, 0, sizeof(float) * 7 * B * D, (hipStream_t)stream);
   SC_REQUIRE(T == 0 || (gates && ckpt && dout && dgates),
              "sc_lucy_scan_bwd: null gates/ckpt/dout/dgates pointer");
+  SC_REQUIRE(stride_g_bt >= 0 && stride_g_td >= 0 && stride_g_cd >= 0 && stride_g_cb >= 0 &&
+                 stride_d_bt >= 0 && stride_d_bd >= 0 && stride_dg_bt >= 0 && stride_dg_td >= 0 &&
+                 stride_dg_cd >= 0 && stride_dg_cb >= 0,
+             "sc_lucy_scan_bwd: negative stride");
+  SC_REQUIRE(((int64_t)T * stride_dg_td + 7 * stride_dg_cd) * 4 < (1ll << 31),
+             "sc_lucy_scan_bwd: one batch row of dgates spans >= 2 GiB");
   ScanBwdArgs a{gates, gate_bias, ckpt, dout, ds_last, dgates, dh0, ds0, dbias, B, T, D,
                 (T + kChunk - 1) / kChunk,
-                stride_g_bt, stride_g_td, stride_g_cd, stride_d_bt, stride_d_bd,
-                stride_dg_bt, stride_dg_td, stride_dg_cd};
+                stride_g_bt, stride_g_td, stride_g_cd, stride_g_cb, stride_d_bt, stride_d_bd,
+                stride_dg_bt, stride_dg_td, stride_dg_cd, stride_dg_cb};
   hipStream_t st = (hipStream_t)stream;
   switch (gates_dtype) {
-    case SC_F32: launch_bwd<SC_F32>(a, st); break;
-    case SC_BF16: launch_bwd<SC_BF16>(a, st); break;
-    default: launch_bwd<SC_F16>(a, st); break;
+    case SC_F32: dispatch_bwd<SC_F32>(a, st); break;
+    case SC_BF16: dispatch_bwd<SC_BF16>(a, st); break;
+    default: dispatch_bwd<SC_F16>(a, st); break;
   }
   return launch_status("sc_lucy_scan_bwd");
 }

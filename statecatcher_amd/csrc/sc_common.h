@@ -111,6 +111,47 @@ struct Buf {
 
 __device__ __forceinline__ int uniform(int x) { return __builtin_amdgcn_readfirstlane(x); }
 
+// ------------------------------------------------------------------ LDS-DMA ------------------
+// global_load_lds_{ushort,dword,dwordx4}: each active lane copies PW bytes from its own global
+// address straight into LDS at (wave-uniform lds_addr) + lane * PW; no VGPR destination.
+// Issued from inline asm on purpose: hipcc's waitcnt model would otherwise treat the pending
+// LDS write as aliasing every later LDS access and drain it (vmcnt(0)) at the next ds_read or
+// ds_write.  The issuing wave retires it with dma_wait() (counts stores too on gfx9) and other
+// waves may read the bytes only after a barrier that follows that wait.
+template <int PW>
+__device__ __forceinline__ void dma_to_lds(const void* src, uint32_t lds_addr) {
+  uint32_t keep;
+  if constexpr (PW == 16) {
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                 "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(src), "s"(lds_addr) : "memory");
+  } else if constexpr (PW == 4) {
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                 "global_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(src), "s"(lds_addr) : "memory");
+  } else {
+    static_assert(PW == 2, "LDS-DMA piece width must be 2, 4 or 16 bytes");
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                 "global_load_lds_ushort %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(src), "s"(lds_addr) : "memory");
+  }
+}
+// 32-bit LDS address of a __shared__ pointer, made wave-uniform (it goes to M0)
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)uniform((int)(uint32_t)(size_t)(__attribute__((address_space(3))) const void*)p);
+}
+// Retire (in hipcc's waitcnt model) the global loads that produced v before a loop: hipcc cannot
+// see the asm dma_wait()s, so a first use of such a value inside a DMA-pipelined loop gets a
+// vmcnt(0) in EVERY iteration, draining the in-flight DMA.  Passing the values through an empty
+// asm makes the one wait happen here instead.
+template <int N>
+__device__ __forceinline__ void settle(float (&v)[N]) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) asm volatile("" : "+v"(v[i]));
+}
+__device__ __forceinline__ void dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void lds_read_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
 // Workgroup barrier that orders LDS only.  __syncthreads() carries a workgroup fence that makes
 // the compiler drain outstanding global loads (vmcnt(0)); the scans keep their next
 // super-chunk's gate loads in flight across barriers, so the fence is restricted to LDS.

@@ -35,15 +35,26 @@ class _timed:
 
 
 # ----------------------------------------------------------------------------- LucyRNN scan --
+def gate_layout(gates):
+    """(B, T, D, strides (bt, td, cd, cb)) of a gate tensor in either accepted layout:
+    [B,T,7,D] (the reference's) or step-blocked [B,T,D/64,7,64] (include/statecatcher.h)."""
+    if gates.dim() == 4 and gates.shape[2] == 7 and gates.stride(3) == 1:
+        B, T, _, D = gates.shape
+        return B, T, D, (gates.stride(0), gates.stride(1), gates.stride(2), 64)
+    if gates.dim() == 5 and gates.shape[3] == 7 and gates.shape[4] == 64 and gates.stride(4) == 1:
+        B, T, NB = gates.shape[:3]
+        return B, T, NB * 64, (gates.stride(0), gates.stride(1), gates.stride(3), gates.stride(2))
+    raise ValueError(f"gates must be [B,T,7,D] or [B,T,D/64,7,64] with unit inner stride, got "
+                     f"shape {tuple(gates.shape)} strides {gates.stride()}")
+
+
 def _scan_fwd(gates, h0, s0, need_ckpt, bias=None):
     require_device(gates, h0, s0)
-    if gates.dim() != 4 or gates.shape[2] != 7:
-        raise ValueError(f"gates must be [B,T,7,D], got {tuple(gates.shape)}")
-    B, T, _, D = gates.shape
+    if gates.dim() == 4 and gates.shape[2] == 7 and gates.stride(3) != 1:
+        gates = gates.contiguous()
+    B, T, D, gs = gate_layout(gates)
     if tuple(h0.shape) != (B, D) or tuple(s0.shape) != (B, D):
         raise ValueError(f"h0/s0 must be [B,D]=({B},{D}); got {tuple(h0.shape)}, {tuple(s0.shape)}")
-    if gates.stride(3) != 1:
-        gates = gates.contiguous()
     # the reference reads h0/s0 as contiguous even when handed a strided view (SURVEY F3)
     h0c = h0.detach().to(torch.float32).contiguous()
     s0c = s0.detach().to(torch.float32).contiguous()
@@ -58,16 +69,15 @@ def _scan_fwd(gates, h0, s0, need_ckpt, bias=None):
     nbytes = B * T * D * 8 * e + (ckpt.numel() * 4 if ckpt is not None else 0) + 4 * B * D * 4
     with _timed("lucy_scan_fwd", gates, nbytes):
         rc = lib.sc_lucy_scan_fwd(ptr(gates), dtype_code(gates), ptr(bias), ptr(h0c), ptr(s0c),
-                                  ptr(out),
-                                  ptr(s_out), B, T, D, gates.stride(0), gates.stride(1),
-                                  gates.stride(2), out.stride(0), out.stride(1), ptr(ckpt),
-                                  stream_of(gates))
+                                  ptr(out), ptr(s_out), B, T, D, *gs, out.stride(0), out.stride(1),
+                                  ptr(ckpt), stream_of(gates))
     check(rc, "sc_lucy_scan_fwd")
     return gates, out, s_out, ckpt
 
 
 def _scan_bwd(gates, ckpt, dout, ds_last, want_dbias, bias=None):
-    B, T, _, D = gates.shape
+    """dgates come back in the layout of `gates` (contiguous)."""
+    B, T, D, gs = gate_layout(gates)
     if dout is None:
         dout = torch.zeros(B, T, D, dtype=gates.dtype, device=gates.device)
     dout = dout.to(gates.dtype)
@@ -75,7 +85,8 @@ def _scan_bwd(gates, ckpt, dout, ds_last, want_dbias, bias=None):
         dout = dout.contiguous()
     if ds_last is not None:
         ds_last = ds_last.to(torch.float32).contiguous()
-    dgates = torch.empty(B, T, 7, D, dtype=gates.dtype, device=gates.device)
+    dgates = torch.empty(gates.shape, dtype=gates.dtype, device=gates.device)
+    _, _, _, dgs = gate_layout(dgates)
     dh0 = torch.empty(B, D, dtype=torch.float32, device=gates.device)
     ds0 = torch.empty(B, D, dtype=torch.float32, device=gates.device)
     dbias = torch.empty(B, 7, D, dtype=torch.float32, device=gates.device) if want_dbias else None
@@ -84,9 +95,8 @@ def _scan_bwd(gates, ckpt, dout, ds_last, want_dbias, bias=None):
     with _timed("lucy_scan_bwd", gates, nbytes):
         rc = _lib.load().sc_lucy_scan_bwd(
             ptr(gates), dtype_code(gates), ptr(bias), ptr(ckpt), ptr(dout), ptr(ds_last), ptr(dgates),
-            ptr(dh0), ptr(ds0), ptr(dbias), B, T, D, gates.stride(0), gates.stride(1),
-            gates.stride(2), dout.stride(0), dout.stride(1), dgates.stride(0), dgates.stride(1),
-            dgates.stride(2), stream_of(gates))
+            ptr(dh0), ptr(ds0), ptr(dbias), B, T, D, *gs, dout.stride(0), dout.stride(1), *dgs,
+            stream_of(gates))
     check(rc, "sc_lucy_scan_bwd")
     return dgates, dh0, ds0, dbias
 
@@ -138,6 +148,15 @@ def wgrad_splitk(dy, x):
     return part.sum(0, dtype=torch.float32)
 
 
+def step_blocked_rows(w, D, inverse=False):
+    """Permute the 7*D rows of a gate projection weight from the reference's (gate, unit) order
+    to (column block of 64 units, gate, unit-in-block) order (inverse=True: back)."""
+    K = w.shape[1]
+    if inverse:
+        return w.view(D // 64, 7, 64, K).transpose(0, 1).reshape(7 * D, K)
+    return w.view(7, D // 64, 64, K).transpose(0, 1).reshape(7 * D, K)
+
+
 class LucyCellFn(torch.autograd.Function):
     """One LucyRNN layer: gates = x W^T (one GEMM, compute dtype `cdt`) -> HIP scan, which adds
     the fp32 bias b to the gates on load (a bias epilogue costs the GEMM ~25%, measured).
@@ -149,15 +168,21 @@ class LucyCellFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x2d, w, b, h0, s0, B, T, cdt):
         xc = x2d.to(cdt)
-        wc = w.to(cdt)
+        D = w.shape[0] // 7
+        blocked = D % 64 == 0
+        # step-blocked gates: weight rows permuted to (column block, gate, unit) order so each
+        # step's 7 x 64 gates of a column block are one contiguous 896-byte run for the scan
+        wc = step_blocked_rows(w.to(cdt), D) if blocked else w.to(cdt)
         bias = b.detach().to(torch.float32).contiguous()
         with _timed("gate_gemm_fwd", xc, 0):
-            gates = torch.matmul(xc, wc.t()).view(B, T, 7, -1)
+            gates = torch.matmul(xc, wc.t())
+        gates = gates.view(B, T, D // 64, 7, 64) if blocked else gates.view(B, T, 7, D)
         need = any(ctx.needs_input_grad)
         gates, out, s_out, ckpt = _scan_fwd(gates, h0, s0, need, bias)
         if need:
             ctx.save_for_backward(xc, wc, gates, ckpt, bias)
             ctx.dtypes = (x2d.dtype, w.dtype, h0.dtype, s0.dtype)
+            ctx.blocked = blocked
         return out, s_out
 
     @staticmethod
@@ -166,11 +191,16 @@ class LucyCellFn(torch.autograd.Function):
         xdt, wdt, hdt, sdt = ctx.dtypes
         dgates, dh0, ds0, dbias = _scan_bwd(gates, ckpt, dout, ds_last, ctx.needs_input_grad[2],
                                             bias)
-        dg2 = dgates.view(-1, dgates.shape[2] * dgates.shape[3])
+        dg2 = dgates.view(xc.shape[0], -1)
         with _timed("gate_gemm_dgrad", dg2, 0):
             dx = (dg2 @ wc).to(xdt) if ctx.needs_input_grad[0] else None
-        with _timed("gate_gemm_wgrad", dg2, 0):
-            dw = wgrad_splitk(dg2, xc).to(wdt) if ctx.needs_input_grad[1] else None
+        dw = None
+        if ctx.needs_input_grad[1]:
+            with _timed("gate_gemm_wgrad", dg2, 0):
+                dw = wgrad_splitk(dg2, xc)
+            if ctx.blocked:
+                dw = step_blocked_rows(dw, dw.shape[0] // 7, inverse=True)
+            dw = dw.to(wdt)
         db = dbias.sum(0).view(-1).to(wdt) if dbias is not None else None
         return dx, dw, db, dh0.to(hdt), ds0.to(sdt), None, None, None
 

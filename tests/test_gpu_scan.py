@@ -209,3 +209,61 @@ def test_decay_scan_fwd_bwd_vs_oracle(B, T, D):
     np.testing.assert_allclose(tkv.grad.cpu().numpy(), dkv[:, 1:], rtol=1e-4, atol=1e-4)
     np.testing.assert_allclose(tdec.grad.cpu().numpy(), ddec[:, 1:], rtol=1e-4, atol=1e-3)
     np.testing.assert_allclose(tinit.grad.cpu().numpy(), dkv[:, 0], rtol=1e-4, atol=1e-4)
+
+
+def _blocked(g):
+    """[B,T,7,D] -> step-blocked [B,T,D/64,7,64] (include/statecatcher.h)."""
+    B, T, _, D = g.shape
+    return g.view(B, T, 7, D // 64, 64).permute(0, 1, 3, 2, 4).contiguous()
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_step_blocked_layout_bitwise_equals_plain(dtype):
+    """The step-blocked gate layout (what LucyCellFn's permuted projection writes) gives the
+    same bits as the reference layout, forward and backward, with the gate bias on load."""
+    torch.manual_seed(5)
+    B, T, D = 3, 200, 192
+    g = (torch.randn(B, T, 7, D, device=DEV) * 0.6).to(dtype)
+    bias = torch.randn(7, D, device=DEV) * 0.2
+    h0 = torch.randn(B, D, device=DEV) * 0.3
+    s0 = torch.randn(B, D, device=DEV) * 0.3
+    dout = torch.randn(B, T, D, device=DEV).to(dtype)
+    ds = torch.randn(B, D, device=DEV)
+    o = ops()
+    _, out1, s1, ck1 = o._scan_fwd(g, h0, s0, True, bias)
+    gb = _blocked(g)
+    _, out2, s2, ck2 = o._scan_fwd(gb, h0, s0, True, bias)
+    assert torch.equal(out1, out2) and torch.equal(s1, s2) and torch.equal(ck1, ck2)
+    dg1, dh1, dss1, db1 = o._scan_bwd(g, ck1, dout, ds, True, bias)
+    dg2, dh2, dss2, db2 = o._scan_bwd(gb, ck2, dout, ds, True, bias)
+    assert dg2.shape == gb.shape
+    assert torch.equal(_blocked(dg1), dg2)
+    assert torch.equal(dh1, dh2) and torch.equal(dss1, dss2) and torch.equal(db1, db2)
+
+
+@pytest.mark.parametrize("dtype,D,offset", [(torch.bfloat16, 20, 0), (torch.bfloat16, 64, 1),
+                                            (torch.float16, 36, 0), (torch.float32, 64, 1)])
+def test_narrow_piece_path_vs_oracle(dtype, D, offset):
+    """Gates whose base or strides are not whole 16-byte pieces take the one-element-per-lane
+    LDS-DMA path (unaligned slice, D % 8 != 0)."""
+    rng = np.random.default_rng(D + offset)
+    B, T = 2, 150
+    full = torch.as_tensor(rng.standard_normal((B, T, 7, D + offset)).astype(np.float32) * 0.5)
+    full = full.to(dtype).to(DEV)
+    g = full[..., offset:]
+    assert g.stride(3) == 1 and (offset == 0 or g.data_ptr() % 16)
+    gr = g.detach().float().cpu().numpy()
+    h0 = (rng.standard_normal((B, D)) * 0.3).astype(np.float32)
+    s0 = (rng.standard_normal((B, D)) * 0.3).astype(np.float32)
+    dout = rng.standard_normal((B, T, D)).astype(np.float32)
+    gg = g
+    _, out, s, ck = ops()._scan_fwd(gg, torch.as_tensor(h0).to(DEV), torch.as_tensor(s0).to(DEV), True)
+    ro, rs = oscan.lucy_scan_fwd(gr, h0, s0)
+    tol = 1e-3 if dtype == torch.float32 else 1e-2
+    np.testing.assert_allclose(out.float().cpu().numpy(), ro, rtol=tol, atol=tol)
+    np.testing.assert_allclose(s.cpu().numpy(), rs, rtol=1e-3, atol=1e-4 * max(1.0, np.abs(rs).max()))
+    dg, _, _, _ = ops()._scan_bwd(gg, ck, torch.as_tensor(dout).to(dtype).to(DEV), None, False)
+    rg, _, _ = oscan.lucy_scan_bwd(gr, h0, s0, torch.as_tensor(dout).to(dtype).float().numpy(),
+                                   np.zeros((B, D)))
+    np.testing.assert_allclose(dg.float().cpu().numpy(), rg, rtol=2 * tol,
+                               atol=tol * np.abs(rg).max())

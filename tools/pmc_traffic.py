@@ -1,0 +1,49 @@
+#!/usr/bin/env python3
+"""Per-launch HBM traffic of the scan kernels from two rocprofv3 PMC passes.
+
+usage: tools/pmc_traffic.py FETCH_counter_collection.csv WRITE_counter_collection.csv [out.json]
+
+FETCH_SIZE / WRITE_SIZE are in KiB per dispatch.  On gfx950 FETCH_SIZE reports half the bytes of
+a 16-byte-per-lane streaming read (MI355X_MICROARCH.md, HBM section); the scans read every gate
+byte with 16-byte LDS-DMA pieces, so fetch bytes = 2 x FETCH_SIZE x 1024.  WRITE_SIZE is taken
+as is (calibrated on the scan forward: its 52 MB of bf16 output + checkpoint read back exactly).
+Writes JSON {bench_kernel_name: {"hbm_bytes_per_launch", "fetch_bytes", "write_bytes",
+"dispatches"}} keyed like bench.py's "kernels" entries.
+"""
+import csv
+import json
+import sys
+from collections import defaultdict
+
+NAMES = {"lucy_scan_fwd_kernel": "lucy_scan_fwd", "lucy_scan_bwd_kernel": "lucy_scan_bwd",
+         "decay_scan_fwd_kernel": "decay_scan_fwd", "decay_scan_bwd_kernel": "decay_scan_bwd"}
+
+
+def per_kernel(path, counter):
+    acc = defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] != counter:
+            continue
+        for frag, name in NAMES.items():
+            if frag in r["Kernel_Name"]:
+                acc[name].append(float(r["Counter_Value"]) * 1024.0)
+    return acc
+
+
+def main():
+    fetch = per_kernel(sys.argv[1], "FETCH_SIZE")
+    write = per_kernel(sys.argv[2], "WRITE_SIZE")
+    out = {}
+    for name in sorted(set(fetch) & set(write)):
+        f = 2.0 * sum(fetch[name]) / len(fetch[name])
+        w = sum(write[name]) / len(write[name])
+        out[name] = {"hbm_bytes_per_launch": round(f + w), "fetch_bytes": round(f),
+                     "write_bytes": round(w), "dispatches": len(fetch[name])}
+    txt = json.dumps(out, indent=1)
+    if len(sys.argv) > 3:
+        open(sys.argv[3], "w").write(txt + "\n")
+    print(txt)
+
+
+if __name__ == "__main__":
+    main()

@@ -22,17 +22,23 @@ B, T, D, V = 32, 1500, 512, 1024
 torch.manual_seed(0)
 
 
-def timeit(fn, iters):
-    for _ in range(3):
-        fn()
+def timeit(fn, iters, rounds=5):
+    """min over `rounds` of the mean launch time of `iters` back-to-back calls; fn(i) should
+    rotate its inputs over buffers larger than the 256 MB Infinity Cache (single-buffer
+    repeats of a ~400 MB stream time unreliably, tools/scan_probe.hip)."""
+    for i in range(5):
+        fn(i)
     torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(iters):
-        fn()
-    e1.record()
-    torch.cuda.synchronize()
-    return e0.elapsed_time(e1) / iters * 1e-3
+    best = float("inf")
+    for _ in range(rounds):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for i in range(iters):
+            fn(i)
+        e1.record()
+        torch.cuda.synchronize()
+        best = min(best, e0.elapsed_time(e1) / iters * 1e-3)
+    return best
 
 
 def report(name, sec, nbytes):
@@ -41,33 +47,42 @@ def report(name, sec, nbytes):
 
 
 e = torch.finfo(dt).bits // 8
+NROT = 4
 if args.only in ("all", "scan"):
-    gates = (torch.randn(B, T, 7, D, device=dev) * 0.5).to(dt)
     bias = torch.randn(7, D, device=dev) * 0.1
     h0 = torch.zeros(B, D, device=dev)
     s0 = torch.zeros(B, D, device=dev)
-    g, out, s_out, ckpt = ops._scan_fwd(gates, h0, s0, True, bias)
-    nb_f = B * T * D * 8 * e + ckpt.numel() * 4
-    report(f"lucy_scan_fwd {args.dtype}", timeit(lambda: ops._scan_fwd(gates, h0, s0, True, bias), args.iters), nb_f)
-    dout = torch.randn(B, T, D, device=dev).to(dt)
-    nb_b = B * T * D * 15 * e + ckpt.numel() * 4
-    report(f"lucy_scan_bwd {args.dtype}",
-           timeit(lambda: ops._scan_bwd(g, ckpt, dout, None, True, bias), args.iters), nb_b)
+    dout = [torch.randn(B, T, D, device=dev).to(dt) for _ in range(NROT)]
+    for lay in ["plain", "blocked"]:
+        gs = []
+        for _ in range(NROT):
+            g = (torch.randn(B, T, 7, D, device=dev) * 0.5).to(dt)
+            gs.append(g if lay == "plain" else g.view(B, T, 7, D // 64, 64).permute(0, 1, 3, 2, 4).contiguous())
+        fw = [ops._scan_fwd(g, h0, s0, True, bias) for g in gs]
+        ck = fw[0][3]
+        nb_f = B * T * D * 8 * e + ck.numel() * 4
+        report(f"lucy_scan_fwd {args.dtype} {lay}",
+               timeit(lambda i: ops._scan_fwd(gs[i % NROT], h0, s0, True, bias), args.iters), nb_f)
+        nb_b = B * T * D * 15 * e + ck.numel() * 4
+        report(f"lucy_scan_bwd {args.dtype} {lay}",
+               timeit(lambda i: ops._scan_bwd(gs[i % NROT], fw[i % NROT][3], dout[i % NROT], None, True,
+                                              bias), args.iters), nb_b)
+        del gs, fw
 if args.only in ("all", "ln"):
     x = torch.randn(B * T, D, device=dev).to(dt)
     gam = torch.ones(D, device=dev, requires_grad=True)
     bet = torch.zeros(D, device=dev, requires_grad=True)
-    report("layernorm_fwd", timeit(lambda: ops.layer_norm(x, gam, bet), args.iters), 2 * B * T * D * e)
+    report("layernorm_fwd", timeit(lambda i: ops.layer_norm(x, gam, bet), args.iters), 2 * B * T * D * e)
 if args.only in ("all", "ctc"):
     logits = (torch.randn(B, T, V, device=dev) * 2).to(dt)
     tl = torch.randint(50, 151, (B,), device=dev)
     tg = torch.randint(1, V, (B, 150), device=dev)
     il = torch.full((B,), T, device=dev, dtype=torch.int64)
-    report("ctc_fwd (emit+chain+ab)", timeit(lambda: ops.ctc_nll(logits, tg, il, tl), args.iters),
+    report("ctc_fwd (emit+chain+ab)", timeit(lambda i: ops.ctc_nll(logits, tg, il, tl), args.iters),
            B * T * V * e)
     lg = logits.clone().requires_grad_(True)
 
-    def fb():
+    def fb(i):
         lg.grad = None
         ops.ctc_nll(lg, tg, il, tl).sum().backward()
     report("ctc_fwd+bwd", timeit(fb, args.iters), 2 * B * T * V * e)

@@ -6,10 +6,14 @@
 //   DPL      hidden units per lane (1: 2-byte loads, WG = 64 d; 2: 4-byte loads, WG = 128 d)
 // build: hipcc -O3 --offload-arch=gfx950 -std=c++17 -I include -I statecatcher_amd/csrc \
 //        tools/scan_probe.hip -o build/scan_probe
+//   (+ -DWITH_LIB statecatcher_amd/libstatecatcher_hip.so -Wl,-rpath,$PWD/statecatcher_amd to
+//   time the shipped kernel through the C ABI in the same harness)
 #include <cstdio>
+#include <algorithm>
 #include <vector>
 
 #include "sc_common.h"
+#include "statecatcher.h"
 
 using namespace sc;
 
@@ -99,23 +103,41 @@ __global__ void __launch_bounds__(NW * 64) probe(const uint16_t* gates, uint16_t
   }
 }
 
-template <int NW, int LC, int NBUF, bool COMPUTE, bool BARRIER, int DPL>
-void run(const char* name, const uint16_t* g, uint16_t* o) {
-  dim3 grid(D / (64 * DPL), B);
+
+// Timing: NROT gate buffers used round-robin (1.4 GB, far beyond the 256 MB Infinity Cache,
+// so no launch reads gates a previous launch left in cache), 20 warmup launches, then ROUNDS
+// rounds of ITERS launches; min and median of the per-round means.
+constexpr int NROT = 4, ROUNDS = 7, ITERS = 30;
+static const uint16_t* g_rot[NROT];
+template <typename F>
+void time_variant(const char* name, F launch, size_t lds) {
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
-  for (int i = 0; i < 3; ++i) hipLaunchKernelGGL((probe<NW, LC, NBUF, COMPUTE, BARRIER, DPL>), grid, dim3(NW * 64), 0, 0, g, o);
-  (void)hipEventRecord(e0);
-  const int it = 20;
-  for (int i = 0; i < it; ++i) hipLaunchKernelGGL((probe<NW, LC, NBUF, COMPUTE, BARRIER, DPL>), grid, dim3(NW * 64), 0, 0, g, o);
-  (void)hipEventRecord(e1);
-  (void)hipEventSynchronize(e1);
-  float ms;
-  (void)hipEventElapsedTime(&ms, e0, e1);
-  const double us = ms * 1e3 / it;
+  for (int i = 0; i < 20; ++i) launch(g_rot[i % NROT]);
+  std::vector<double> r;
+  for (int q = 0; q < ROUNDS; ++q) {
+    (void)hipEventRecord(e0);
+    for (int i = 0; i < ITERS; ++i) launch(g_rot[i % NROT]);
+    (void)hipEventRecord(e1);
+    (void)hipEventSynchronize(e1);
+    float ms;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    r.push_back(ms * 1e3 / ITERS);
+  }
+  std::sort(r.begin(), r.end());
   const double bytes = (double)B * T * D * 8 * 2;
-  printf("%-44s %8.1f us %8.1f GB/s %5.1f%%\n", name, us, bytes / us * 1e-3, bytes / us * 1e-3 / 80.0);
+  printf("%-46s min %7.1f us  med %7.1f us  %6.1f GB/s %5.1f%%  (lds %zu, %s)\n", name, r[0],
+         r[ROUNDS / 2], bytes / r[0] * 1e-3, bytes / r[0] * 1e-3 / 80.0, lds,
+         hipGetErrorString(hipGetLastError()));
+}
+
+template <int NW, int LC, int NBUF, bool COMPUTE, bool BARRIER, int DPL>
+void run(const char* name, const uint16_t*, uint16_t* o) {
+  dim3 grid(D / (64 * DPL), B);
+  time_variant(name, [&](const uint16_t* g) {
+    hipLaunchKernelGGL((probe<NW, LC, NBUF, COMPUTE, BARRIER, DPL>), grid, dim3(NW * 64), 0, 0, g, o);
+  }, 0);
 }
 
 // LDS-DMA variant: each wave stages its LC steps x 7 gates x 64 d (bf16) into a private LDS
@@ -123,7 +145,7 @@ void run(const char* name, const uint16_t* g, uint16_t* o) {
 // issued during k, and the one for k+1 retired (counted vmcnt) before barrier B of k.
 // MODE 0: gates [B][T][7][D] (128-B rows); 1: [B][D/64][T][7][64] (a WG's stream contiguous);
 // 2: [B][T][D/64][7][64] (weight rows permuted: 896-B rows per step).
-template <int NW, int LC, int MODE, int NBUF>
+template <int NW, int LC, int MODE, int NBUF, bool GLOBAL = false>
 __global__ void __launch_bounds__(NW * 64) probe_glds(const uint16_t* gates, uint16_t* out) {
   constexpr int SC = NW * LC;                   // steps per super-chunk
   constexpr int PIECES = LC * 7 * 8;            // 16-B pieces per wave per super-chunk
@@ -154,8 +176,14 @@ __global__ void __launch_bounds__(NW * 64) probe_glds(const uint16_t* gates, uin
                                       : (uint32_t)(((t * 7 + g) * D) * 2 + sub * 16);
       const uint32_t la = uniform((int)(uint32_t)(size_t)(__attribute__((address_space(3))) void*)(mybuf + slot * WBUF + i * 1024));
       uint32_t keep;
-      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
-                   : "=&s"(keep) : "v"(voff), "s"(rs), "s"(la) : "memory");
+      if (GLOBAL) {
+        const void* src = (const char*)gbase + voff;
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(src), "s"(la) : "memory");
+      } else {
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(voff), "s"(rs), "s"(la) : "memory");
+      }
     }
   };
   float s = 0.f, h = 0.f;
@@ -206,56 +234,61 @@ __global__ void __launch_bounds__(NW * 64) probe_glds(const uint16_t* gates, uin
   }
 }
 
-template <int NW, int LC, int MODE, int NBUF>
-void run_glds(const char* name, const uint16_t* g, uint16_t* o) {
+template <int NW, int LC, int MODE, int NBUF, bool GLOBAL = false>
+void run_glds(const char* name, const uint16_t*, uint16_t* o) {
   constexpr int NI = (LC * 7 * 8 + 63) / 64;
   const size_t lds = NBUF * NW * NI * 1024;
-  auto kfn = probe_glds<NW, LC, MODE, NBUF>;
+  auto kfn = probe_glds<NW, LC, MODE, NBUF, GLOBAL>;
   (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   dim3 grid(D / 64, B);
-  hipEvent_t e0, e1;
-  (void)hipEventCreate(&e0);
-  (void)hipEventCreate(&e1);
-  for (int i = 0; i < 3; ++i) hipLaunchKernelGGL(kfn, grid, dim3(NW * 64), lds, 0, g, o);
-  (void)hipEventRecord(e0);
-  const int it = 20;
-  for (int i = 0; i < it; ++i) hipLaunchKernelGGL(kfn, grid, dim3(NW * 64), lds, 0, g, o);
-  (void)hipEventRecord(e1);
-  (void)hipEventSynchronize(e1);
-  float ms;
-  (void)hipEventElapsedTime(&ms, e0, e1);
-  const double us = ms * 1e3 / it;
-  const double bytes = (double)B * T * D * 8 * 2;
-  printf("%-44s %8.1f us %8.1f GB/s %5.1f%%  (lds %zu B, err %s)\n", name, us, bytes / us * 1e-3,
-         bytes / us * 1e-3 / 80.0, lds, hipGetErrorString(hipGetLastError()));
+  time_variant(name, [&](const uint16_t* g) {
+    hipLaunchKernelGGL(kfn, grid, dim3(NW * 64), lds, 0, g, o);
+  }, lds);
 }
 
 int main() {
-  uint16_t *g, *o;
-  (void)hipMalloc(&g, (size_t)B * T * 7 * D * 2);
+  uint16_t* o;
   (void)hipMalloc(&o, (size_t)B * T * D * 2);
   std::vector<uint16_t> h((size_t)B * T * 7 * D);
-  for (size_t i = 0; i < h.size(); ++i) h[i] = 0x3f00 + (uint16_t)((i * 2654435761u) >> 24);
-  (void)hipMemcpy(g, h.data(), h.size() * 2, hipMemcpyHostToDevice);
-  run<16, 4, 2, true, true, 1>("NW16 LC4 nbuf2 compute barrier dpl1 (=prod)", g, o);
-  run<16, 4, 2, false, true, 1>("NW16 LC4 nbuf2 NOcompute barrier dpl1", g, o);
-  run<16, 4, 2, true, false, 1>("NW16 LC4 nbuf2 compute NObarrier dpl1", g, o);
-  run<16, 4, 2, false, false, 1>("NW16 LC4 nbuf2 NOcompute NObarrier dpl1", g, o);
-  run<16, 4, 3, true, true, 1>("NW16 LC4 nbuf3 compute barrier dpl1", g, o);
-  run<16, 4, 3, false, false, 1>("NW16 LC4 nbuf3 NOcompute NObarrier dpl1", g, o);
-  run<16, 4, 2, true, true, 2>("NW16 LC4 nbuf2 compute barrier dpl2", g, o);
-  run<16, 4, 2, false, false, 2>("NW16 LC4 nbuf2 NOcompute NObarrier dpl2", g, o);
-  run<8, 8, 2, true, true, 1>("NW8 LC8 nbuf2 compute barrier dpl1", g, o);
-  run<8, 8, 2, false, false, 1>("NW8 LC8 nbuf2 NOcompute NObarrier dpl1", g, o);
-  run<16, 4, 3, true, true, 2>("NW16 LC4 nbuf3 compute barrier dpl2", g, o);
-  run_glds<16, 4, 0, 2>("glds NW16 LC4 standard nbuf2", g, o);
-  run_glds<16, 4, 1, 2>("glds NW16 LC4 blocked nbuf2", g, o);
-  run_glds<16, 4, 2, 2>("glds NW16 LC4 permuted nbuf2", g, o);
-  run_glds<16, 3, 0, 3>("glds NW16 LC3 standard nbuf3", g, o);
-  run_glds<16, 3, 1, 3>("glds NW16 LC3 blocked nbuf3", g, o);
-  run_glds<16, 3, 2, 3>("glds NW16 LC3 permuted nbuf3", g, o);
-  run_glds<16, 3, 2, 2>("glds NW16 LC3 permuted nbuf2", g, o);
-  run_glds<8, 8, 2, 2>("glds NW8 LC8 permuted nbuf2", g, o);
-  run_glds<12, 4, 2, 3>("glds NW12 LC4 permuted nbuf3 (CH48)", g, o);
+  for (int r = 0; r < NROT; ++r) {
+    uint16_t* g;
+    (void)hipMalloc(&g, (size_t)B * T * 7 * D * 2);
+    for (size_t i = 0; i < h.size(); ++i) h[i] = 0x3f00 + (uint16_t)(((i + r) * 2654435761u) >> 24);
+    (void)hipMemcpy(g, h.data(), h.size() * 2, hipMemcpyHostToDevice);
+    g_rot[r] = g;
+  }
+  const uint16_t* g = g_rot[0];
+#ifdef WITH_LIB
+  const bool with_lib = true;
+#else
+  const bool with_lib = false;
+#endif
+  float *bias, *st0, *sout, *ckpt;
+  (void)hipMalloc(&bias, 7 * D * 4);
+  (void)hipMemset(bias, 0, 7 * D * 4);
+  (void)hipMalloc(&st0, B * D * 4);
+  (void)hipMemset(st0, 0, B * D * 4);
+  (void)hipMalloc(&sout, B * D * 4);
+  (void)hipMalloc(&ckpt, (size_t)B * ((T + 63) / 64) * 2 * D * 4);
+  for (int rep = 0; rep < 1; ++rep) {
+    run<16, 4, 2, true, true, 1>("reg NW16 LC4 compute barrier (=old prod)", g, o);
+    run<16, 4, 2, false, false, 1>("reg NW16 LC4 loads+stores only", g, o);
+    run_glds<16, 4, 0, 2>("glds standard (buffer)", g, o);
+    run_glds<16, 4, 0, 2, true>("glds standard (global)", g, o);
+    run_glds<16, 4, 1, 2>("glds blocked (buffer)", g, o);
+    run_glds<16, 4, 2, 2>("glds permuted (buffer)", g, o);
+    run_glds<16, 4, 2, 2, true>("glds permuted (global)", g, o);
+    run_glds<12, 4, 2, 3>("glds NW12 LC4 permuted nbuf3", g, o);
+    if (with_lib) {   // the shipped kernel through the C ABI, step-blocked gates, same harness
+      time_variant("libstatecatcher fwd (blocked, bias, ckpt)", [&](const uint16_t* gg) {
+        sc_lucy_scan_fwd(gg, SC_BF16, bias, st0, st0, o, sout, B, T, D, (int64_t)T * 7 * D, 7 * D,
+                         64, 448, (int64_t)T * D, D, ckpt, nullptr);
+      }, 0);
+      time_variant("libstatecatcher fwd (blocked, no bias/ckpt)", [&](const uint16_t* gg) {
+        sc_lucy_scan_fwd(gg, SC_BF16, nullptr, st0, st0, o, sout, B, T, D, (int64_t)T * 7 * D, 7 * D,
+                         64, 448, (int64_t)T * D, D, nullptr, nullptr);
+      }, 0);
+    }
+  }
   return 0;
 }
