@@ -127,44 +127,33 @@ def main():
 
     import statecatcher_amd as sc
     from statecatcher_amd import ops
-    from statecatcher_amd.model import ASRModel, CTCLoss, build_lucyrnn_config, compute_loss
+    from statecatcher_amd.model import ASRModel, CTCLoss, build_lucyrnn_config
+    from statecatcher_amd.train import SegmentTrainer
 
     torch.manual_seed(0)   # identical init on every rank (DDP also broadcasts)
     cfg = build_lucyrnn_config(args.feat, args.hidden, args.layers, args.vocab)
     model = ASRModel(None, cfg, vocab_size=args.vocab, feat_dim=args.feat, proj_dim=-1).to(device)
     with torch.no_grad():   # reference zero-inits output_proj (lucyrnn_triton.py:108-109); a seeded
         model.encoder.output_proj.weight.normal_(0, 0.02)   # N(0,0.02) keeps every gradient non-zero
-    net = model
-    if world > 1:
-        net = torch.nn.parallel.DistributedDataParallel(
-            model, device_ids=[local], bucket_cap_mb=args.bucket_mb, gradient_as_bucket_view=True,
-            broadcast_buffers=False)
     params = [p for p in model.parameters() if p.requires_grad]
     try:
         opt = torch.optim.Adam(params, lr=3e-4, fused=True)
     except Exception:
         opt = torch.optim.Adam(params, lr=3e-4, foreach=True)
-    crit = CTCLoss(blank=0, zero_infinity=True)
-    segs = synth_segments(args, rank, device)
     amp = torch.bfloat16 if args.dtype == "bf16" else None
-
-    state = {"s": None, "i": 0}
+    # the reference segment loop (train.py:460-581) with DDP over RCCL when world > 1
+    trainer = SegmentTrainer(model, CTCLoss(blank=0, zero_infinity=True), opt, mode="ctc",
+                             accumulation_steps=1, max_grad_norm=50.0, amp_dtype=amp,
+                             bucket_cap_mb=args.bucket_mb)
+    segs = synth_segments(args, rank, device)
 
     def step():
-        seg = segs[state["i"] % args.segments]
-        if state["i"] % args.segments == 0:
-            state["s"] = None   # new batch: state reset (train.py:460)
-        with torch.autocast("cuda", dtype=amp, enabled=amp is not None):
-            loss, out_state, _, _ = compute_loss("ctc", crit, net, seg["feats"], seg["masks"],
-                                                 seg["tokens"], seg["in_lens"], seg["tgt_lens"], 0,
-                                                 input_state=state["s"])
-        loss.backward()
-        torch.nn.utils.clip_grad_norm_(params, 50.0)
-        opt.step()
-        opt.zero_grad(set_to_none=True)
-        state["s"] = out_state
-        state["i"] += 1
-        return loss
+        i = trainer.global_step
+        if i % args.segments == 0:
+            trainer.begin_batch()   # new batch: state reset (train.py:460)
+        seg = segs[i % args.segments]
+        return trainer.train_segment(seg["feats"], seg["masks"], seg["tokens"], seg["in_lens"],
+                                     seg["tgt_lens"])
 
     for _ in range(args.warmup):
         step()

@@ -6,12 +6,13 @@ wrapped in drop-ins of the reference's module API (lucyrnn_triton.py, decoder.py
 """
 from .lucyrnn_conf import LucyRNNConfig
 from .lucyrnn_triton import LinearSafe, LucyRNNCellTriton, LucyRNNtriton
+from .lucyrnn import LucyRNN, LucyRNNCell
 from .model import ASRModel, CTCLoss, compute_loss, detach_states
 from .ops import ctc_greedy_decode, ctc_loss, ctc_nll, decay_scan, lucy_scan
 from .decoder import ctc_greedy_decoder
 
 __all__ = [
-    "LucyRNNConfig", "LinearSafe", "LucyRNNCellTriton", "LucyRNNtriton", "ASRModel", "CTCLoss",
+    "LucyRNNConfig", "LinearSafe", "LucyRNNCellTriton", "LucyRNNtriton", "LucyRNN", "LucyRNNCell", "ASRModel", "CTCLoss",
     "compute_loss", "detach_states", "ctc_greedy_decode", "ctc_loss", "ctc_nll", "decay_scan",
     "lucy_scan", "ctc_greedy_decoder",
 ]

@@ -229,30 +229,56 @@ def gen_greedy():
 
 
 def gen_native():
+    """Cases: (mode, fused_ops, layer_norm, decay_mode, stack_order, carried state)."""
     from lucyrnn import LucyRNN
     from lucyrnn_conf import LucyRNNConfig
     cases = {}
+    specs = []
     for mode in ["train", "infer"]:
         for ln in [True, False]:
-            torch.manual_seed(2024)
-            cfg = LucyRNNConfig(input_dim=12, hidden_dim=16, num_layers=2, vocab_size=10,
-                                kernel_impl="native", is_training=(mode == "train"), fused_ops=True,
-                                layer_norm=ln)
-            m = LucyRNN(cfg)
-            with torch.no_grad():
-                m.output_proj.weight.normal_(0, 0.3)  # zero-init (lucyrnn.py:86) hides the encoder
-                m.output_proj.bias.normal_(0, 0.1)
-            x = torch.randn(2, 9, 12)
-            with torch.no_grad():
-                logits, (h, s) = m(x)
-            name = f"{mode}_ln{int(ln)}"
-            for k, v in m.state_dict().items():
-                cases[name + "/param/" + k] = v.numpy()
-            cases[name + "/x"] = x.numpy()
-            cases[name + "/logits"] = logits.numpy()
-            cases[name + "/h"] = torch.stack(h).numpy()
-            cases[name + "/s"] = torch.stack(s).numpy()
-            print("native", name, flush=True)
+            specs.append((f"{mode}_ln{int(ln)}", mode, True, ln, "learned", 1, False))
+        specs.append((f"{mode}_unfused", mode, False, True, "learned", 1, False))
+        specs.append((f"{mode}_carry", mode, True, True, "learned", 1, True))
+        specs.append((f"{mode}_stack2", mode, True, True, "learned", 2, False))
+    specs.append(("train_prefix", "train", True, True, "prefix_sum", 1, False))
+    for name, mode, fused, ln, dmode, stack, carry in specs:
+        torch.manual_seed(2024)
+        cfg = LucyRNNConfig(input_dim=12, hidden_dim=16, num_layers=2, vocab_size=10,
+                            kernel_impl="native", is_training=(mode == "train"), fused_ops=fused,
+                            layer_norm=ln, decay_mode=dmode, stack_order=stack,
+                            lambda_decay=0.05)
+        m = LucyRNN(cfg)
+        with torch.no_grad():
+            m.output_proj.weight.normal_(0, 0.3)  # zero-init (lucyrnn.py:86) hides the encoder
+            m.output_proj.bias.normal_(0, 0.1)
+        x = torch.randn(2, 9 if stack == 1 else 11, 12)   # stack 2: 11 frames -> 5 steps (trim)
+        hs = None
+        if carry:
+            h0 = [torch.randn(2, 16) * 0.5 for _ in range(2)]
+            s0 = [torch.randn(2, 16) * 0.5 for _ in range(2)]
+            cases[name + "/h0"] = torch.stack(h0).numpy()
+            cases[name + "/s0"] = torch.stack(s0).numpy()
+            hs = ([t.clone() for t in h0], [t.clone() for t in s0])
+        for k, v in m.state_dict().items():
+            cases[name + "/param/" + k] = v.detach().clone().numpy()
+        # backward through the reference's own autograd (the native path is trainable)
+        xg = x.clone().requires_grad_(True)
+        logits, (h, s) = m(xg, hs)
+        R = torch.randn(logits.shape, generator=torch.Generator().manual_seed(7))
+        (logits * R).sum().backward()
+        cases[name + "/R"] = R.numpy()
+        cases[name + "/grad/x"] = xg.grad.numpy()
+        for k, prm in m.named_parameters():
+            if prm.grad is not None:
+                cases[name + "/grad/" + k] = prm.grad.numpy()
+        logits, h, s = logits.detach(), [t.detach() for t in h], [t.detach() for t in s]
+        cases[name + "/x"] = x.numpy()
+        cases[name + "/logits"] = logits.numpy()
+        cases[name + "/h"] = torch.stack(h).numpy()
+        cases[name + "/s"] = torch.stack(s).numpy()
+        cases[name + "/cfg"] = np.array([mode == "train", fused, ln, dmode == "prefix_sum", stack,
+                                         carry], np.int64)
+        print("native", name, flush=True)
     np.savez(os.path.join(HERE, "native.npz"), **cases)
 
 

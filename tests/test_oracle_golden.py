@@ -120,3 +120,30 @@ def test_greedy_vs_reference_decoder(pref):
     z = load_golden("greedy")
     dec = odec.ctc_greedy(z[pref + "_lp"], z[pref + "_in_lens"], blank=0)
     assert dec == _split(z[pref + "_counts"], z[pref + "_tokens"])
+
+
+def native_cases():
+    z = load_golden("native")
+    return sorted({k.split("/")[0] for k in z.files})
+
+
+def native_case(z, name):
+    p = {k[len(name) + 7:]: z[k].astype(np.float64) for k in z.files if k.startswith(name + "/param/")}
+    train, fused, ln, prefix, stack, carry = [int(v) for v in z[name + "/cfg"]]
+    kw = dict(L=2, D=16, train=bool(train), fused=bool(fused), ln=bool(ln),
+              decay_mode="prefix_sum" if prefix else "learned", stack=stack, lambda_decay=0.05)
+    if carry:
+        kw.update(h0=z[name + "/h0"], s0=z[name + "/s0"])
+    return p, kw
+
+
+@pytest.mark.parametrize("name", native_cases())
+def test_native_lucyrnn_oracle_vs_reference(name):
+    """oracle/native.py == reference lucyrnn.LucyRNN (train quirks of SURVEY F9 included)."""
+    from oracle import native
+    z = load_golden("native")
+    p, kw = native_case(z, name)
+    logits, h, s = native.lucyrnn_forward(p, z[name + "/x"], **kw)
+    np.testing.assert_allclose(logits, z[name + "/logits"], rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(np.stack(h), z[name + "/h"], rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(np.stack(s), z[name + "/s"], rtol=1e-4, atol=1e-5)
