@@ -46,7 +46,15 @@
 
 namespace sc {
 
-constexpr int kChunk = 64;   // time steps per super-chunk (== NW * LC for every variant)
+// SC_ABL: ablation bitmask for tools/abl_bench.sh only (never set in a shipped build):
+//   1 trivial gate-gradient math, 2 no dgates stores, 4 no cross-wave compositions,
+//   8 backward barriers B1-B3 removed (wrong results; timing only)
+#ifndef SC_ABL
+#define SC_ABL 0
+#endif
+
+constexpr int kChunk = 64;
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));   // time steps per super-chunk (== NW * LC for every variant)
 constexpr float kEps = 1e-6f;
 
 struct ScanFwdArgs {
@@ -108,27 +116,25 @@ __device__ __forceinline__ void step_terms(float r, float z, float k, float v, f
 __device__ __forceinline__ float tanh_sig(float x) { return sigm(2.0f * x) * 2.0f - 1.0f; }
 
 // Gradient of one step w.r.t. its 7 raw gates, given the step's adjoints.
-//   gh   = dL/dh_t (total), dpre = dL/d(hn + s_t), gs = dL/ds_t (total)
+//   gh   = dL/dh_t (total), dpre = dL/d(hn + s_t), gs = dL/ds_t (total); zg and dec are the
+//   step's gates, kept in registers from the recompute (their sigmoids are not redone).
 __device__ __forceinline__ void gate_grads(float r, float z, float k, float v, float hp, float dc,
-                                           float al, float gh, float dpre, float gs, float hprev,
-                                           float sprev, float c, float (&o)[7]) {
+                                           float al, float zg, float dec, float gh, float dpre,
+                                           float gs, float hprev, float sprev, float c,
+                                           float (&o)[7]) {
   const float rc2 = (r * r + z * z) * 0.5f + kEps;
   const float irc = rsq(rc2);
-  const float zg = sigm(z * irc);
   const float ird = rsq(dc * dc + kEps);
-  const float dec = sigm(dc * ird);
   const float ira = rsq(al * al + kEps);
   const float alp = sigm(al * ira);
   const float irh = rsq(hp * hp + kEps);
   const float q = (k * k + v * v) * 0.5f + kEps;
   const float iq = rsq(q);
   const float iqe = rcp(q + kEps);
-  const float kv = (k * iq) * (v * iq) * iqe;
   // zg = sigm(z / rho_c): d/dz = (r^2/2 + eps)/rho_c^3, d/dr = -z r / (2 rho_c^3)
-  const float d_zn = gh * (hprev - c) * zg * (1.0f - zg);
-  const float irc3 = irc * irc * irc;
-  o[0] = -d_zn * z * r * 0.5f * irc3;
-  o[1] = d_zn * (r * r * 0.5f + kEps) * irc3;
+  const float d_zn = gh * (hprev - c) * zg * (1.0f - zg) * (irc * irc * irc);
+  o[0] = -d_zn * z * r * 0.5f;
+  o[1] = d_zn * (r * r * 0.5f + kEps);
   // kv = k v f(q), f = 1/(q (q+eps)), f' = -(2q+eps) f^2, dq/dk = k, dq/dv = v
   const float d_kv = gs * alp;
   const float f = iq * iq * iqe;
@@ -138,7 +144,47 @@ __device__ __forceinline__ void gate_grads(float r, float z, float k, float v, f
   // x / sqrt(x^2 + eps): derivative eps / rho^3
   o[4] = dpre * kEps * (irh * irh * irh);
   o[5] = gs * sprev * dec * (1.0f - dec) * kEps * (ird * ird * ird);
-  o[6] = gs * kv * alp * (1.0f - alp) * kEps * (ira * ira * ira);
+  o[6] = gs * (k * v * f) * alp * (1.0f - alp) * kEps * (ira * ira * ira);
+}
+
+// Cross-wave composition of the per-wave affine segment maps m_q = (a, b): x -> a x + b, read
+// from LDS.  prefix: x <- m_{w-1} o ... o m_0 (x); suffix: x <- m_{w+1} o ... o m_{NW-1} (x)
+// (reverse time).  Work stays proportional to the wave's position (the chain runs only over
+// the maps it needs: the VALU is the scarce resource); maps are fetched four at a time so the
+// LDS latency is paid once per four links.
+template <int NW>
+__device__ __forceinline__ float compose_prefix(const float2 (*agg)[64], int lane, int w, float x) {
+  int q = 0;
+  for (; q + 4 <= w; q += 4) {
+    const float2 m0 = agg[q][lane], m1 = agg[q + 1][lane], m2 = agg[q + 2][lane],
+                 m3 = agg[q + 3][lane];
+    x = fmaf(m0.x, x, m0.y);
+    x = fmaf(m1.x, x, m1.y);
+    x = fmaf(m2.x, x, m2.y);
+    x = fmaf(m3.x, x, m3.y);
+  }
+  for (; q < w; ++q) {
+    const float2 m = agg[q][lane];
+    x = fmaf(m.x, x, m.y);
+  }
+  return x;
+}
+template <int NW>
+__device__ __forceinline__ float compose_suffix(const float2 (*agg)[64], int lane, int w, float x) {
+  int q = NW - 1;
+  for (; q - 4 >= w; q -= 4) {
+    const float2 m0 = agg[q][lane], m1 = agg[q - 1][lane], m2 = agg[q - 2][lane],
+                 m3 = agg[q - 3][lane];
+    x = fmaf(m0.x, x, m0.y);
+    x = fmaf(m1.x, x, m1.y);
+    x = fmaf(m2.x, x, m2.y);
+    x = fmaf(m3.x, x, m3.y);
+  }
+  for (; q > w; --q) {
+    const float2 m = agg[q][lane];
+    x = fmaf(m.x, x, m.y);
+  }
+  return x;
 }
 
 // ------------------------------------------------------------------------ forward ----------
@@ -226,10 +272,7 @@ lucy_scan_fwd_kernel(ScanFwdArgs a) {
     lds_barrier();
     float s = carS[k & 1][lane];
     if (w == 0 && a.ckpt && dok) a.ckpt[((int64_t)(b * a.nsc + k) * 2) * a.D + d] = s;
-    for (int q = 0; q < w; ++q) {
-      const float2 m = aggS[q][lane];
-      s = m.x * s + m.y;
-    }
+    s = compose_prefix<NW>(aggS, lane, w, s);
     float Ah = 1.0f, Bh = 0.0f;
 #pragma unroll
     for (int j = 0; j < LC; ++j) {
@@ -244,10 +287,7 @@ lucy_scan_fwd_kernel(ScanFwdArgs a) {
     lds_barrier();
     float h = carH[k & 1][lane];
     if (w == 0 && a.ckpt && dok) a.ckpt[((int64_t)(b * a.nsc + k) * 2 + 1) * a.D + d] = h;
-    for (int q = 0; q < w; ++q) {
-      const float2 m = aggH[q][lane];
-      h = m.x * h + m.y;
-    }
+    h = compose_prefix<NW>(aggH, lane, w, h);
 #pragma unroll
     for (int j = 0; j < LC; ++j) {
       h = zg[j] * h + (1.0f - zg[j]) * x[j];
@@ -263,7 +303,10 @@ lucy_scan_fwd_kernel(ScanFwdArgs a) {
 // NBUF = 2: two LDS slots per wave, the raw gates stay in LDS for the gate-gradient phase while
 // the next super-chunk lands in the other slot (16-bit gates).  NBUF = 1 (fp32, whose two slots
 // would not fit in LDS): the raw gates are copied to VGPRs and the slot is refilled at once.
-template <int DT, int NW, int LC, int PW, int NBUF>
+// WST: the 7 gate gradients of each step are written back into the wave's LDS slot over the raw
+// gates they were computed from, then stored as whole 16-byte pieces (3.5 wave-instructions per
+// super-chunk instead of 28 two-byte stores).  Needs NBUF = 2 and 16-byte aligned dgates.
+template <int DT, int NW, int LC, int PW, int NBUF, bool WST>
 __global__ void __launch_bounds__(NW * 64)
 lucy_scan_bwd_kernel(ScanBwdArgs a) {
   static_assert(NW * LC == kChunk, "super-chunk must be 64 steps");
@@ -274,6 +317,7 @@ lucy_scan_bwd_kernel(ScanBwdArgs a) {
   constexpr int ROWS = LC * 8;
   constexpr int PIECES = ROWS * P::PPR;
   constexpr int NI = (PIECES + 63) / 64;
+  static_assert(!WST || (NBUF == 2 && PW == 16), "staged stores need two 16-bit slots");
   const int lane = threadIdx.x & 63;
   const int w = uniform(threadIdx.x >> 6);
   const int b = blockIdx.y;
@@ -290,7 +334,7 @@ lucy_scan_bwd_kernel(ScanBwdArgs a) {
   __shared__ float carGs[2][64];
   __shared__ float ckS[2][2][64];   // (s, h) checkpoint of the super-chunk, shared by all waves
   using L = LdsElem<T, PW>;
-  const unsigned char* slots = dyn_lds + w * NBUF * ROWS * 64 * L::BYTES;   // [NBUF][LC*8][64]
+  unsigned char* slots = dyn_lds + w * NBUF * ROWS * 64 * L::BYTES;   // [NBUF][LC*8][64]
   const uint32_t slots_lds = lds_addr(slots);
 
   const T* gsrc = (const T*)a.gates + (int64_t)b * a.g_bt + (int64_t)blk * a.g_cb;
@@ -340,7 +384,7 @@ lucy_scan_bwd_kernel(ScanBwdArgs a) {
   for (int it = 0; it < a.nsc; ++it) {
     const int k = a.nsc - 1 - it;
     const int t0 = k * kChunk + w * LC;
-    const unsigned char* slot = slots + (it % NBUF) * ROWS * 64 * L::BYTES;
+    unsigned char* slot = slots + (it % NBUF) * ROWS * 64 * L::BYTES;
     if (NBUF == 2 && it + 1 < a.nsc) issue(it + 1);     // into the other slot
     const float s_ck = ckS[it & 1][0][lane];
     const float h_ck = ckS[it & 1][1][lane];
@@ -370,12 +414,9 @@ lucy_scan_bwd_kernel(ScanBwdArgs a) {
       if (it + 1 < a.nsc) issue(it + 1);                // refill the slot just read
     }
     aggA[w][lane] = make_float2(As, Bs);
-    lds_barrier();                                             // B1
+    if (!(SC_ABL & 8)) lds_barrier();                          // B1
     float s = s_ck;
-    for (int q = 0; q < w; ++q) {
-      const float2 m = aggA[q][lane];
-      s = m.x * s + m.y;
-    }
+    if (!(SC_ABL & 4)) s = compose_prefix<NW>(aggA, lane, w, s);
     float Ah = 1.0f, Bh = 0.0f;
 #pragma unroll
     for (int j = 0; j < LC; ++j) {
@@ -386,12 +427,9 @@ lucy_scan_bwd_kernel(ScanBwdArgs a) {
       Bh = zg[j] * Bh + (1.0f - zg[j]) * x[j];
     }
     aggB[w][lane] = make_float2(Ah, Bh);
-    lds_barrier();                                             // B2
+    if (!(SC_ABL & 8)) lds_barrier();                          // B2
     float h = h_ck;
-    for (int q = 0; q < w; ++q) {
-      const float2 m = aggB[q][lane];
-      h = m.x * h + m.y;
-    }
+    if (!(SC_ABL & 4)) h = compose_prefix<NW>(aggB, lane, w, h);
 #pragma unroll
     for (int j = 0; j < LC; ++j) {
       hv[j] = h;
@@ -405,12 +443,9 @@ lucy_scan_bwd_kernel(ScanBwdArgs a) {
       Ph *= zg[j];
     }
     aggA[w][lane] = make_float2(Ph, Qh);
-    lds_barrier();                                             // B3
+    if (!(SC_ABL & 8)) lds_barrier();                          // B3
     float C = carGh[it & 1][lane];
-    for (int q = NW - 1; q > w; --q) {
-      const float2 m = aggA[q][lane];
-      C = m.x * C + m.y;
-    }
+    if (!(SC_ABL & 4)) C = compose_suffix<NW>(aggA, lane, w, C);
 #pragma unroll
     for (int j = LC - 1; j >= 0; --j) {
       u[j] = dj[j] + C;                                         // Gh_t
@@ -428,10 +463,7 @@ lucy_scan_bwd_kernel(ScanBwdArgs a) {
     dma_wait();                   // the next super-chunk (and its checkpoint) has landed
     lds_barrier();                                             // B4
     float Cs = carGs[it & 1][lane];
-    for (int q = NW - 1; q > w; --q) {
-      const float2 m = aggB[q][lane];
-      Cs = m.x * Cs + m.y;
-    }
+    if (!(SC_ABL & 4)) Cs = compose_suffix<NW>(aggB, lane, w, Cs);
 #pragma unroll
     for (int j = LC - 1; j >= 0; --j) {
       const float dpre = u[j] * (1.0f - zg[j]) * (1.0f - x[j] * x[j]);
@@ -444,14 +476,36 @@ lucy_scan_bwd_kernel(ScanBwdArgs a) {
           if constexpr (NBUF == 1) g7[g] = rg[j][g];
           else g7[g] = E::ld(L::get(slot, (j * 7 + g) * 64 + lane)) + gb[g];
         }
-        gate_grads(g7[0], g7[1], g7[2], g7[3], g7[4], g7[5], g7[6], u[j], dpre, gs, hv[j], sv[j],
-                   x[j], o);
+        if (SC_ABL & 1) {
+#pragma unroll
+          for (int g = 0; g < 7; ++g) o[g] = g7[g] * gs + hv[j] * sv[j];
+        } else {
+          gate_grads(g7[0], g7[1], g7[2], g7[3], g7[4], g7[5], g7[6], zg[j], dec[j], u[j], dpre,
+                     gs, hv[j], sv[j], x[j], o);
+        }
         const uint32_t so = (uint32_t)((t0 + j) * a.dg_td * sizeof(T));
 #pragma unroll
         for (int g = 0; g < 7; ++g) {
           const T og = E::st(o[g]);
-          dgbuf.st(og, vo, so + (uint32_t)(g * a.dg_cd * sizeof(T)));
+          if constexpr (WST) ((T*)slot)[(j * 7 + g) * 64 + lane] = og;   // over its raw gate
+          else if (!(SC_ABL & 2)) dgbuf.st(og, vo, so + (uint32_t)(g * a.dg_cd * sizeof(T)));
           bacc[g] += E::ld(og);   // sum what is stored, so db == dgates.sum() exactly as a GEMM sees it
+        }
+      }
+    }
+    if constexpr (WST) {   // staged gradients -> HBM in 16-byte pieces (same wave: LDS in order)
+      constexpr int SP = LC * 7 * 8;
+#pragma unroll
+      for (int i = 0; i < (SP + 63) / 64; ++i) {
+        const int p = i * 64 + lane;
+        if (SP % 64 == 0 || p < SP) {
+          const int row = p >> 3, pc = p & 7;
+          const int j = row / 7, g = row - 7 * (row / 7);
+          if (t0 + j < a.T && pc <= pcmax && !(SC_ABL & 2)) {
+            const v4u v = *(const v4u*)(slot + p * 16);
+            __builtin_amdgcn_raw_buffer_store_b128(
+                v, dgbuf.r, (uint32_t)(((t0 + j) * a.dg_td + g * a.dg_cd + pc * 8) * sizeof(T)), 0, 0);
+          }
         }
       }
     }
@@ -479,7 +533,14 @@ lucy_scan_bwd_kernel(ScanBwdArgs a) {
 
 // ------------------------------------------------------------------------ launchers --------
 // 16 waves x 4 steps per wave (one 16-wave workgroup per CU at B*D/64 = 256), every dtype.
-constexpr int kNW = 16, kLC = 4;
+#ifndef SC_FWD_NW
+#define SC_FWD_NW 16
+#endif
+constexpr int kNW = SC_FWD_NW, kLC = kChunk / SC_FWD_NW;
+#ifndef SC_BWD_NW
+#define SC_BWD_NW 8
+#endif
+constexpr int kBNW = SC_BWD_NW, kBLC = kChunk / SC_BWD_NW;
 
 // > 64 KiB of dynamic LDS must be opted into per kernel (gfx950 has 160 KiB per CU).  Called
 // once per kernel instantiation (function-local static): the call costs host time per launch.
@@ -500,17 +561,17 @@ static void launch_fwd(const ScanFwdArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(kern, grid, dim3(kNW * 64), lds, st, a);
 }
 
-template <int DT, int PW>
+template <int DT, int PW, bool WST>
 static void launch_bwd(const ScanBwdArgs& a, hipStream_t st) {
   using T = typename Elem<DT>::T;
   // two slots per wave fit only for 2-byte LDS elements (160 KiB per CU)
   constexpr int NBUF = LdsElem<T, PW>::BYTES == 2 ? 2 : 1;
-  auto kern = lucy_scan_bwd_kernel<DT, kNW, kLC, PW, NBUF>;
-  const size_t lds = (size_t)NBUF * kNW * kLC * 8 * 64 * LdsElem<T, PW>::BYTES;
+  auto kern = lucy_scan_bwd_kernel<DT, kBNW, kBLC, PW, NBUF, WST>;
+  const size_t lds = (size_t)NBUF * kBNW * kBLC * 8 * 64 * LdsElem<T, PW>::BYTES;
   static const bool lds_ok = set_lds_limit(kern, lds);
   (void)lds_ok;
   dim3 grid((a.D + 63) / 64, a.B);
-  hipLaunchKernelGGL(kern, grid, dim3(kNW * 64), lds, st, a);
+  hipLaunchKernelGGL(kern, grid, dim3(kBNW * 64), lds, st, a);
 }
 
 // 16-byte pieces need a 16-byte aligned base and every stride and D in whole pieces; otherwise
@@ -535,10 +596,14 @@ template <int DT>
 static void dispatch_bwd(const ScanBwdArgs& a, hipStream_t st) {
   constexpr int es = sizeof(typename Elem<DT>::T);
   if (wide_pieces(a.gates, es, a.D, {a.g_bt, a.g_td, a.g_cd, a.g_cb}) &&
-      wide_pieces(a.dout, es, a.D, {a.d_bt, a.d_bd}))
-    launch_bwd<DT, 16>(a, st);
-  else
-    launch_bwd<DT, es>(a, st);
+      wide_pieces(a.dout, es, a.D, {a.d_bt, a.d_bd})) {
+    if (es == 2 && wide_pieces(a.dgates, es, a.D, {a.dg_bt, a.dg_td, a.dg_cd, a.dg_cb}))
+      launch_bwd<DT, 16, es == 2>(a, st);
+    else
+      launch_bwd<DT, 16, false>(a, st);
+  } else {
+    launch_bwd<DT, es, false>(a, st);
+  }
 }
 
 }  // namespace sc

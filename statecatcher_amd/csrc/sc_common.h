@@ -120,6 +120,7 @@ __device__ __forceinline__ int uniform(int x) { return __builtin_amdgcn_readfirs
 // waves may read the bytes only after a barrier that follows that wait.
 template <int PW>
 __device__ __forceinline__ void dma_to_lds(const void* src, uint32_t lds_addr) {
+  lds_addr = __builtin_amdgcn_readfirstlane(lds_addr);   // M0 operand: keep it in an SGPR
   uint32_t keep;
   if constexpr (PW == 16) {
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
