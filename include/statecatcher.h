@@ -21,6 +21,9 @@
  *   sc_ctc_*          <- ATen ctc_loss behind nn.CTCLoss(blank=0, zero_infinity=True),
  *                        train.py:142 / model.py:68-71
  *   sc_ctc_greedy_decode <- decoder.py:3-30 `ctc_greedy_decoder`
+ *   sc_rnnt_*         <- warp_rnnt `rnnt_loss(log_probs, labels, frames_lengths, labels_lengths,
+ *                        blank, compact, gather=True)` called at model.py:97-105 (train.py:38-42,
+ *                        :144); the log_softmax of model.py:93 optionally fused
  */
 #ifndef STATECATCHER_H
 #define STATECATCHER_H
@@ -185,6 +188,39 @@ int sc_ctc_bwd(const void* x, int x_dtype, int is_logits, int B, int T, int V,
 int sc_ctc_greedy_decode(const void* log_probs, int dtype, int B, int T, int V,
                          int64_t stride_b, int64_t stride_t, const int64_t* lengths, int blank,
                          int32_t* tokens, int32_t* counts, void* stream);
+
+/* ---------------------------------------------------------------- RNN-T ----------------- */
+
+/* Workspace bytes for sc_rnnt_fwd / sc_rnnt_bwd (gathered log-probs, alpha, beta, offsets). */
+size_t sc_rnnt_workspace_bytes(int B, int T, int max_labels);
+
+/*
+ * RNN-T negative log-likelihood over the transducer lattice (gather semantics: the blank and
+ * next-label log-probs of every node (t, u), t < frames_lengths[b], u <= labels_lengths[b]).
+ * x: node (b,t,u)'s V-row (v-stride 1) is at
+ *   dense   (row_offsets == NULL): b*stride_b + t*stride_t + u*stride_u   ([B,T,max_labels+1,V])
+ *   compact (row_offsets != NULL): (row_offsets[b] + t*(labels_lengths[b]+1) + u) * stride_u,
+ *           the packed (sum_b T_b (U_b+1), V) layout of RNNTCompactPredictorJoiner (model.py:147-200)
+ *   is_logits = 1: x are joiner logits, log_softmax fused; 0: x are log-probs.
+ * labels: int64 [B, max_labels] (row stride label_stride); lengths: int64 [B] device arrays.
+ * nll: fp32 [B] (+inf when frames_lengths[b] == 0).  max_labels <= 1023.
+ */
+int sc_rnnt_fwd(const void* x, int x_dtype, int is_logits, int B, int T, int max_labels, int V,
+                int64_t stride_b, int64_t stride_t, int64_t stride_u, const int64_t* row_offsets,
+                const int64_t* labels, int64_t label_stride, const int64_t* frames_lengths,
+                const int64_t* labels_lengths, int blank, float* nll, void* workspace,
+                size_t workspace_bytes, void* stream);
+
+/*
+ * Gradient of sum_b scale[b] * nll[b] w.r.t. x, written to grad (grad_dtype = fp32 or x_dtype,
+ * same layout as x; dense rows outside the lattice are zeroed).  Logits: the softmax-corrected
+ * row; log-probs: non-zero only at the blank and label entries (warp_rnnt gather=True).
+ */
+int sc_rnnt_bwd(const void* x, int x_dtype, int is_logits, int B, int T, int max_labels, int V,
+                int64_t stride_b, int64_t stride_t, int64_t stride_u, const int64_t* row_offsets,
+                const int64_t* labels, int64_t label_stride, const int64_t* frames_lengths,
+                const int64_t* labels_lengths, int blank, const float* scale, void* grad,
+                int grad_dtype, const void* workspace, size_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus
 }

@@ -41,6 +41,11 @@ _SIGS = {
     "sc_ctc_bwd": (_i32, [_vp, _i32, _i32, _i32, _i32, _i32, _i64, _i64, _vp, _i64, _i32, _vp, _vp,
                          _i32, _fp, _fp, _vp, _i32, _vp, _c.c_size_t, _vp]),
     "sc_ctc_greedy_decode": (_i32, [_vp, _i32, _i32, _i32, _i32, _i64, _i64, _vp, _i32, _vp, _vp, _vp]),
+    "sc_rnnt_workspace_bytes": (_c.c_size_t, [_i32, _i32, _i32]),
+    "sc_rnnt_fwd": (_i32, [_vp, _i32, _i32, _i32, _i32, _i32, _i32, _i64, _i64, _i64, _vp, _vp, _i64,
+                          _vp, _vp, _i32, _fp, _vp, _c.c_size_t, _vp]),
+    "sc_rnnt_bwd": (_i32, [_vp, _i32, _i32, _i32, _i32, _i32, _i32, _i64, _i64, _i64, _vp, _vp, _i64,
+                          _vp, _vp, _i32, _fp, _vp, _i32, _vp, _c.c_size_t, _vp]),
 }
 EXPORTED = tuple(_SIGS)
 

@@ -1,0 +1,412 @@
+// RNN-T (transducer) loss for gfx950: the lattice the reference gets from warp_rnnt
+// (model.py:73-105, train.py:38-42, :144; gather=True semantics: only the blank and the next
+// label of every (t, u) node enter the loss).
+//
+//   rnnt_emit_kernel   one wave per lattice node (b,t,u): row log-sum-exp over V (when fed
+//                      logits: the log_softmax of model.py:93 is fused), then the node's blank
+//                      and label log-probs in base 2, stored DIAGONAL-MAJOR ([b][t+u][u]) so
+//                      that the wavefront below reads one coalesced row per step.
+//   rnnt_ab_kernel     one workgroup per (sequence, direction): alpha forward and beta backward
+//                      run concurrently.  Lane = label position u; the lattice is swept by
+//                      anti-diagonals n = t + u (all nodes of a diagonal are independent), the
+//                      neighbour (t, u-1) / (t, u+1) value crosses lanes through LDS once per
+//                      diagonal.  Values are base-2 logs with a finite "dead" sentinel and are
+//                      re-centred on the workgroup max every 8 diagonals; the running offset is
+//                      fp64 (|alpha| reaches ~1e4 at T=1500, U=150).
+//   rnnt_grad_kernel   one wave per node: occupancies of the two gathered arcs from alpha, beta
+//                      and log P (offsets recombined in fp64), then the full gradient row
+//                      (softmax-corrected when fed logits, sparse when fed log-probs).
+#include "sc_common.h"
+
+namespace sc {
+
+namespace {
+
+constexpr float kDeadR = -1e30f;
+
+struct RnntWs {
+  float* lse;      // [B][T][U1]      natural-log row normaliser per node (logits input)
+  float* lpb;      // [B][ND][U1p]    base-2 blank log-prob of node (t,u) at [t+u][u]
+  float* lpy;      // [B][ND][U1p]    base-2 log-prob of label y[u] at node (t,u)
+  float* alpha;    // [B][ND][U1p]    base-2, relative to offA[b][t+u]
+  float* beta;     // [B][ND][U1p]    base-2, relative to offB[b][t+u]
+  double* offA;    // [B][ND]
+  double* offB;    // [B][ND]
+  double* logp2;   // [B]             base-2 log P(y|x)
+};
+
+size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+int u1p_of(int Umax) { return 64 * ((Umax + 1 + 63) / 64); }
+
+size_t ws_layout(int B, int T, int Umax, RnntWs* w, void* base) {
+  const int U1 = Umax + 1, U1p = u1p_of(Umax), ND = T + Umax;
+  char* p = (char*)base;
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    char* r = p + off;
+    off += align256(bytes);
+    return (void*)r;
+  };
+  RnntWs t;
+  t.lse = (float*)take((size_t)B * T * U1 * 4);
+  t.lpb = (float*)take((size_t)B * ND * U1p * 4);
+  t.lpy = (float*)take((size_t)B * ND * U1p * 4);
+  t.alpha = (float*)take((size_t)B * ND * U1p * 4);
+  t.beta = (float*)take((size_t)B * ND * U1p * 4);
+  t.offA = (double*)take((size_t)B * ND * 8);
+  t.offB = (double*)take((size_t)B * ND * 8);
+  t.logp2 = (double*)take((size_t)B * 8);
+  if (w) *w = t;
+  return off;
+}
+
+struct RnntArgs {
+  const void* x;
+  int is_logits, B, T, Umax, V, blank, U1, U1p, ND;
+  int64_t sb, st, su;
+  const int64_t* row_off;   // compact layout: first row of sequence b (NULL: dense strides)
+  const int64_t* lab;
+  int64_t labs;
+  const int64_t* flen;
+  const int64_t* llen;
+  float* nll;
+  RnntWs ws;
+  const float* scale;
+  void* grad;
+};
+
+__device__ __forceinline__ int clampr(int64_t v, int lo, int hi) {
+  return (int)(v < lo ? lo : (v > hi ? hi : v));
+}
+
+// element offset of node (b, t, u)'s row
+__device__ __forceinline__ int64_t node_row(const RnntArgs& a, int b, int t, int u, int Ub) {
+  if (a.row_off) return (a.row_off[b] + (int64_t)t * (Ub + 1) + u) * a.su;
+  return (int64_t)b * a.sb + (int64_t)t * a.st + (int64_t)u * a.su;
+}
+
+__device__ __forceinline__ int label_at(const RnntArgs& a, int b, int u) {
+  const int lab = (int)a.lab[(int64_t)b * a.labs + u];
+  return lab < 0 ? 0 : (lab >= a.V ? a.V - 1 : lab);
+}
+
+// ---------------------------------------------------------------------------- emissions -----
+template <int DT>
+__global__ void __launch_bounds__(256) rnnt_emit_kernel(RnntArgs a) {
+  using E = Elem<DT>;
+  using T = typename E::T;
+  const int lane = threadIdx.x & 63;
+  const int64_t node = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (node >= (int64_t)a.B * a.T * a.U1) return;
+  const int b = (int)(node / ((int64_t)a.T * a.U1));
+  const int t = (int)((node / a.U1) % a.T), u = (int)(node % a.U1);
+  const int Tb = clampr(a.flen[b], 0, a.T), Ub = clampr(a.llen[b], 0, a.Umax);
+  if (t >= Tb || u > Ub) return;
+  const T* p = (const T*)a.x + node_row(a, b, t, u, Ub);
+  float lse = 0.0f;
+  if (a.is_logits) {
+    float m = -__builtin_huge_valf(), l = 0.0f;
+    for (int v = lane; v < a.V; v += 64) {
+      const float xv = E::ld(p[v]);
+      const float mn = fmaxf(m, xv);
+      l = l * fexp(m - mn) + fexp(xv - mn);
+      m = mn;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float mo = __shfl_xor(m, o);
+      const float lo = __shfl_xor(l, o);
+      const float mn = fmaxf(m, mo);
+      l = (mn == -__builtin_huge_valf()) ? 0.0f : l * fexp(m - mn) + lo * fexp(mo - mn);
+      m = mn;
+    }
+    lse = m + flog(l);
+  }
+  if (lane == 0) {
+    const int64_t d = ((int64_t)b * a.ND + t + u) * a.U1p + u;
+    a.ws.lse[node] = lse;
+    a.ws.lpb[d] = fmaxf((E::ld(p[a.blank]) - lse) * kLog2e, kDeadR);
+    a.ws.lpy[d] = u < Ub ? fmaxf((E::ld(p[label_at(a, b, u)]) - lse) * kLog2e, kDeadR) : kDeadR;
+  }
+}
+
+// ---------------------------------------------------------------------------- alpha / beta --
+__device__ __forceinline__ float lse2_live(float x, float y) {
+  const float m = fmaxf(x, y);
+  return m + log2_(exp2_(x - m) + exp2_(y - m));
+}
+
+constexpr int kRenorm = 8;   // diagonals between re-centrings
+
+__global__ void __launch_bounds__(1024) rnnt_ab_kernel(RnntArgs a) {
+  const bool is_beta = blockIdx.x >= a.B;
+  const int b = is_beta ? blockIdx.x - a.B : blockIdx.x;
+  const int u = threadIdx.x;
+  const int lane = u & 63;
+  const int w = uniform(u >> 6);
+  const int nw = blockDim.x >> 6;
+  const int Tb = clampr(a.flen[b], 0, a.T), Ub = clampr(a.llen[b], 0, a.Umax);
+  if (Tb == 0) {   // no frames: no alignment exists
+    if (!is_beta && u == 0) {
+      a.nll[b] = __builtin_huge_valf();
+      a.ws.logp2[b] = -__builtin_huge_val();
+    }
+    return;
+  }
+  __shared__ float xb[2][1026];   // per-diagonal values at [u + 1]: entries 0 and nw*64+1 (lanes
+                                  // -1 and nw*64) stay dead
+  __shared__ float wmax[16];
+  const int nd = Tb + Ub;          // diagonals 0 .. nd-1
+  const int64_t base = (int64_t)b * a.ND * a.U1p;
+  const float* lpb = a.ws.lpb + base;
+  const float* lpy = a.ws.lpy + base;
+  float* out = (is_beta ? a.ws.beta : a.ws.alpha) + base;
+  double* offp = (is_beta ? a.ws.offB : a.ws.offA) + (int64_t)b * a.ND;
+  for (int q = u; q < 1026; q += blockDim.x) {
+    xb[0][q] = kDeadR;
+    xb[1][q] = kDeadR;
+  }
+  double off = 0.0;
+  float v = kDeadR, vn = kDeadR;   // own value and neighbour's value from the previous diagonal
+  lds_barrier();
+  for (int i = 0; i < nd; ++i) {
+    const int n = is_beta ? nd - 1 - i : i;
+    const int t = n - u;
+    const bool valid = u <= Ub && t >= 0 && t < Tb;
+    float nv;
+    if (!is_beta) {
+      if (n == 0) {
+        nv = (u == 0) ? 0.0f : kDeadR;
+      } else {
+        // (t-1,u) --blank--> (t,u) and (t,u-1) --y[u-1]--> (t,u); the workspace holds no
+        // values for nodes outside the lattice, so each arc is taken only where it exists
+        const float eb = lpb[(int64_t)(n - 1) * a.U1p + u];
+        const float ey = lpy[(int64_t)(n - 1) * a.U1p + (u > 0 ? u - 1 : 0)];
+        nv = lse2_live(t >= 1 ? v + eb : kDeadR, u >= 1 ? vn + ey : kDeadR);
+      }
+    } else {
+      const float eb = lpb[(int64_t)n * a.U1p + u];
+      if (i == 0) {
+        nv = (u == Ub) ? eb : kDeadR;   // terminal blank of node (Tb-1, Ub)
+      } else {
+        const float ey = lpy[(int64_t)n * a.U1p + u];
+        nv = lse2_live(t + 1 < Tb ? v + eb : kDeadR, u < Ub ? vn + ey : kDeadR);
+      }
+    }
+    nv = valid ? fmaxf(nv, kDeadR) : kDeadR;
+    if (valid) out[(int64_t)n * a.U1p + u] = nv;
+    if (u == 0) offp[n] = off;
+    if (!is_beta && n == nd - 1 && u == Ub) {   // alpha(Tb-1, Ub) + final blank
+      const double lp = (double)nv + (double)lpb[(int64_t)n * a.U1p + u] + off;
+      a.ws.logp2[b] = lp;
+      a.nll[b] = (float)(-lp * (double)kLn2);
+    }
+    const bool renorm = (i % kRenorm) == kRenorm - 1;
+    if (renorm) {
+      float m = nv;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+      if (lane == 0) wmax[w] = m;
+    }
+    xb[i & 1][u + 1] = nv;
+    lds_barrier();
+    // neighbour on the previous diagonal: alpha reads (t, u-1) = lane u-1; beta (t, u+1) = u+1
+    vn = xb[i & 1][is_beta ? u + 2 : u];
+    v = nv;
+    if (renorm) {
+      float m = wmax[0];
+      for (int q = 1; q < nw; ++q) m = fmaxf(m, wmax[q]);
+      if (m > 0.5f * kDeadR) {
+        v -= m;
+        vn -= m;
+        off += (double)m;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------- gradient ------
+template <int DT, int GT>
+__global__ void __launch_bounds__(256) rnnt_grad_kernel(RnntArgs a) {
+  using E = Elem<DT>;
+  using G = Elem<GT>;
+  const int lane = threadIdx.x & 63;
+  const int64_t node = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (node >= (int64_t)a.B * a.T * a.U1) return;
+  const int b = (int)(node / ((int64_t)a.T * a.U1));
+  const int t = (int)((node / a.U1) % a.T), u = (int)(node % a.U1);
+  const int Tb = clampr(a.flen[b], 0, a.T), Ub = clampr(a.llen[b], 0, a.Umax);
+  const bool valid = t < Tb && u <= Ub;
+  if (!valid && a.row_off) return;   // compact rows exist only for valid nodes
+  const int64_t row = valid ? node_row(a, b, t, u, Ub)
+                            : (int64_t)b * a.sb + (int64_t)t * a.st + (int64_t)u * a.su;
+  typename G::T* g = (typename G::T*)a.grad + row;
+  if (!valid) {   // dense padding rows carry no loss
+    for (int v = lane; v < a.V; v += 64) g[v] = G::st(0.0f);
+    return;
+  }
+  const double lp2 = a.ws.logp2[b];
+  const float sc = a.scale[b];
+  float gb = 0.0f, gy = 0.0f;
+  if (lp2 > -1e300 && sc != 0.0f) {
+    const int n = t + u;
+    const int64_t base = (int64_t)b * a.ND * a.U1p;
+    const double al = (double)a.ws.alpha[base + (int64_t)n * a.U1p + u] + a.ws.offA[(int64_t)b * a.ND + n];
+    const float eb = a.ws.lpb[base + (int64_t)n * a.U1p + u];
+    if (t + 1 < Tb) {
+      const double be = (double)a.ws.beta[base + (int64_t)(n + 1) * a.U1p + u] +
+                        a.ws.offB[(int64_t)b * a.ND + n + 1];
+      gb = -exp2_((float)(al + eb + be - lp2));
+    } else if (u == Ub) {
+      gb = -exp2_((float)(al + eb - lp2));
+    }
+    if (u < Ub) {
+      const float ey = a.ws.lpy[base + (int64_t)n * a.U1p + u];
+      const double be = (double)a.ws.beta[base + (int64_t)(n + 1) * a.U1p + u + 1] +
+                        a.ws.offB[(int64_t)b * a.ND + n + 1];
+      gy = -exp2_((float)(al + ey + be - lp2));
+    }
+    gb *= sc;
+    gy *= sc;
+  }
+  const int yl = u < Ub ? label_at(a, b, u) : -1;
+  const typename E::T* x = (const typename E::T*)a.x + row;
+  const float lse = a.ws.lse[node];
+  const float tot = gb + gy;
+  for (int v = lane; v < a.V; v += 64) {
+    float o = a.is_logits ? -fexp(E::ld(x[v]) - lse) * tot : 0.0f;
+    if (v == a.blank) o += gb;
+    if (v == yl) o += gy;
+    g[v] = G::st(o);
+  }
+}
+
+template <int DT>
+void launch_fwd(const RnntArgs& a, hipStream_t st) {
+  const int64_t nodes = (int64_t)a.B * a.T * a.U1;
+  hipLaunchKernelGGL((rnnt_emit_kernel<DT>), dim3((unsigned)((nodes + 3) / 4)), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(rnnt_ab_kernel, dim3(2 * a.B), dim3(a.U1p), 0, st, a);
+}
+
+template <int DT, int GT>
+void launch_bwd(const RnntArgs& a, hipStream_t st) {
+  const int64_t nodes = (int64_t)a.B * a.T * a.U1;
+  hipLaunchKernelGGL((rnnt_grad_kernel<DT, GT>), dim3((unsigned)((nodes + 3) / 4)), dim3(256), 0,
+                     st, a);
+}
+
+int rnnt_check(const void* x, int dt, int B, int T, int Umax, int V, const int64_t* labels,
+               const int64_t* fl, const int64_t* ll, int blank, const void* ws, size_t wsb,
+               const char* who) {
+  SC_REQUIRE(dt == SC_F32 || dt == SC_BF16 || dt == SC_F16, "%s: unsupported dtype %d", who, dt);
+  SC_REQUIRE(B >= 0 && T >= 0 && V > 0 && Umax >= 0, "%s: bad shape", who);
+  SC_REQUIRE(Umax + 1 <= 1024, "%s: max label count %d exceeds 1023", who, Umax);
+  SC_REQUIRE(blank >= 0 && blank < V, "%s: blank %d outside [0, %d)", who, blank, V);
+  SC_REQUIRE((int64_t)B * T * (Umax + 1) < (1ll << 40), "%s: lattice too large", who);
+  if (B == 0 || T == 0) return 0;
+  SC_REQUIRE(x && fl && ll && ws, "%s: null pointer", who);
+  SC_REQUIRE(Umax == 0 || labels, "%s: null labels", who);
+  const size_t need = ws_layout(B, T, Umax, nullptr, nullptr);
+  SC_REQUIRE(wsb >= need, "%s: workspace %zu < %zu bytes", who, wsb, need);
+  return 0;
+}
+
+RnntArgs make_args(const void* x, int is_logits, int B, int T, int Umax, int V, int64_t sb,
+                   int64_t st, int64_t su, const int64_t* row_off, const int64_t* labels,
+                   int64_t labs, const int64_t* fl, const int64_t* ll, int blank, float* nll,
+                   const void* ws, const float* scale, void* grad) {
+  RnntArgs a;
+  a.x = x;
+  a.is_logits = is_logits;
+  a.B = B;
+  a.T = T;
+  a.Umax = Umax;
+  a.V = V;
+  a.blank = blank;
+  a.U1 = Umax + 1;
+  a.U1p = u1p_of(Umax);
+  a.ND = T + Umax;
+  a.sb = sb;
+  a.st = st;
+  a.su = su;
+  a.row_off = row_off;
+  a.lab = labels;
+  a.labs = labs;
+  a.flen = fl;
+  a.llen = ll;
+  a.nll = nll;
+  ws_layout(B, T, Umax, &a.ws, const_cast<void*>(ws));
+  a.scale = scale;
+  a.grad = grad;
+  return a;
+}
+
+}  // namespace
+
+}  // namespace sc
+
+using namespace sc;
+
+extern "C" size_t sc_rnnt_workspace_bytes(int B, int T, int max_labels) {
+  if (B <= 0 || T <= 0 || max_labels < 0) return 256;
+  return ws_layout(B, T, max_labels, nullptr, nullptr);
+}
+
+extern "C" int sc_rnnt_fwd(const void* x, int x_dtype, int is_logits, int B, int T, int max_labels,
+                           int V, int64_t stride_b, int64_t stride_t, int64_t stride_u,
+                           const int64_t* row_offsets, const int64_t* labels,
+                           int64_t label_stride, const int64_t* frames_lengths,
+                           const int64_t* labels_lengths, int blank, float* nll, void* workspace,
+                           size_t workspace_bytes, void* stream) {
+  clear_error();
+  int rc = rnnt_check(x, x_dtype, B, T, max_labels, V, labels, frames_lengths, labels_lengths,
+                      blank, workspace, workspace_bytes, "sc_rnnt_fwd");
+  if (rc) return rc;
+  if (B == 0) return 0;
+  SC_REQUIRE(nll, "sc_rnnt_fwd: null nll");
+  SC_REQUIRE(T > 0, "sc_rnnt_fwd: T == 0 is handled by the caller");
+  RnntArgs a = make_args(x, is_logits, B, T, max_labels, V, stride_b, stride_t, stride_u,
+                         row_offsets, labels, label_stride, frames_lengths, labels_lengths, blank,
+                         nll, workspace, nullptr, nullptr);
+  hipStream_t st = (hipStream_t)stream;
+  switch (x_dtype) {
+    case SC_F32: launch_fwd<SC_F32>(a, st); break;
+    case SC_BF16: launch_fwd<SC_BF16>(a, st); break;
+    default: launch_fwd<SC_F16>(a, st); break;
+  }
+  return launch_status("sc_rnnt_fwd");
+}
+
+extern "C" int sc_rnnt_bwd(const void* x, int x_dtype, int is_logits, int B, int T, int max_labels,
+                           int V, int64_t stride_b, int64_t stride_t, int64_t stride_u,
+                           const int64_t* row_offsets, const int64_t* labels,
+                           int64_t label_stride, const int64_t* frames_lengths,
+                           const int64_t* labels_lengths, int blank, const float* scale,
+                           void* grad, int grad_dtype, const void* workspace,
+                           size_t workspace_bytes, void* stream) {
+  clear_error();
+  int rc = rnnt_check(x, x_dtype, B, T, max_labels, V, labels, frames_lengths, labels_lengths,
+                      blank, workspace, workspace_bytes, "sc_rnnt_bwd");
+  if (rc) return rc;
+  if (B == 0 || T == 0) return 0;
+  SC_REQUIRE(scale && grad, "sc_rnnt_bwd: null scale/grad");
+  SC_REQUIRE(grad_dtype == SC_F32 || grad_dtype == x_dtype,
+             "sc_rnnt_bwd: grad dtype must be fp32 or the input dtype");
+  RnntArgs a = make_args(x, is_logits, B, T, max_labels, V, stride_b, stride_t, stride_u,
+                         row_offsets, labels, label_stride, frames_lengths, labels_lengths, blank,
+                         nullptr, workspace, scale, grad);
+  hipStream_t st = (hipStream_t)stream;
+  if (grad_dtype == SC_F32) {
+    switch (x_dtype) {
+      case SC_F32: launch_bwd<SC_F32, SC_F32>(a, st); break;
+      case SC_BF16: launch_bwd<SC_BF16, SC_F32>(a, st); break;
+      default: launch_bwd<SC_F16, SC_F32>(a, st); break;
+    }
+  } else {
+    switch (x_dtype) {
+      case SC_BF16: launch_bwd<SC_BF16, SC_BF16>(a, st); break;
+      default: launch_bwd<SC_F16, SC_F16>(a, st); break;
+    }
+  }
+  return launch_status("sc_rnnt_bwd");
+}

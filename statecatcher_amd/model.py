@@ -13,7 +13,7 @@ import torch.nn as nn
 
 from .lucyrnn_conf import LucyRNNConfig
 from .lucyrnn_triton import LucyRNNtriton
-from .ops import ctc_loss
+from .ops import ctc_loss, rnnt_loss
 
 
 def detach_states(states):
@@ -85,10 +85,106 @@ def compute_loss(mode: str, criterion: nn.Module, model: nn.Module, feats: torch
             logp = enc_out.log_softmax(-1).transpose(0, 1)
             loss = criterion(logp, tokens, in_lens, tgt_lens)
     elif mode == "rnnt":
-        raise NotImplementedError("RNN-T loss kernels are not built yet (SURVEY §8a a11, next row)")
+        # model.py:73-105: blank-prefixed predictor input, joiner logits (B,T,U+1,V) or compact
+        # rows, log_softmax in fp32, transducer loss with gather semantics
+        assert use_rnnt_joiner is not None, "Joiner module required for RNN-T mode"
+        blank_prefix = torch.full((tokens.size(0), 1), blank_id, dtype=tokens.dtype,
+                                  device=tokens.device)
+        predictor_input = torch.cat([blank_prefix, tokens], dim=1)
+        use_compact = bool(getattr(args, "compact_rnnt", False)) if args is not None else compact
+        if use_compact:
+            logits = use_rnnt_joiner(enc_out, predictor_input, in_lens, tgt_lens)
+        else:
+            logits = use_rnnt_joiner(enc_out, predictor_input)
+        if isinstance(criterion, RNNTLoss):
+            # the log_softmax is fused into the loss kernels (no fp32 copy of the 4-D logits)
+            loss = criterion.forward_logits(logits, tokens, in_lens, tgt_lens, blank_id=blank_id,
+                                            compact=use_compact)
+        else:
+            log_probs = logits.log_softmax(dim=-1)
+            if log_probs.dtype != torch.float32:
+                log_probs = log_probs.to(torch.float32)
+            loss = criterion(log_probs=log_probs, labels=tokens, frames_lengths=in_lens,
+                             labels_lengths=tgt_lens, blank_id=blank_id, compact=compact,
+                             gather=True)
     else:
         raise ValueError(f"Unknown mode: {mode}")
     return loss, output_state, enc_out, output_state
+
+
+class RNNTLoss(nn.Module):
+    """The transducer loss the reference takes from warp_rnnt (train.py:38-42, :144), as a
+    module accepting model.py:97-105's keyword call (blank given as ``blank_id``).  SURVEY F8:
+    the reference assigns the class itself as criterion, so its call constructs a module instead
+    of computing a loss; this is the intended loss (warp_rnnt.rnnt_loss, reduction 'mean')."""
+
+    def __init__(self, blank=0, reduction="mean", average_frames=False):
+        super().__init__()
+        self.blank = blank
+        self.reduction = reduction
+        self.average_frames = average_frames
+
+    def forward(self, log_probs, labels, frames_lengths, labels_lengths, blank_id=None,
+                compact=False, gather=True):
+        return rnnt_loss(log_probs, labels, frames_lengths, labels_lengths,
+                         average_frames=self.average_frames, reduction=self.reduction,
+                         blank=self.blank if blank_id is None else blank_id, gather=gather,
+                         compact=compact, is_logits=False)
+
+    def forward_logits(self, logits, labels, frames_lengths, labels_lengths, blank_id=None,
+                       compact=False):
+        return rnnt_loss(logits, labels, frames_lengths, labels_lengths,
+                         average_frames=self.average_frames, reduction=self.reduction,
+                         blank=self.blank if blank_id is None else blank_id, compact=compact,
+                         is_logits=True)
+
+
+class RNNTPredictorJoiner(nn.Module):
+    """model.py:112-145: embedding predictor + additive joint + tanh + output projection over
+    the full (B, T, U+1) grid.  Parameter names as the reference (embedding, enc_proj,
+    pred_proj, joiner).  debug prints are off by default here."""
+
+    def __init__(self, enc_out_dim: int, pred_emb_dim: int, join_dim: int, vocab_size: int,
+                 debug: bool = False):
+        super().__init__()
+        self.embedding = nn.Embedding(vocab_size, pred_emb_dim)
+        self.enc_proj = nn.Linear(enc_out_dim, join_dim)
+        self.pred_proj = nn.Linear(pred_emb_dim, join_dim)
+        self.debug = debug
+        self.joiner = nn.Linear(join_dim, vocab_size)
+
+    def forward(self, enc_out: torch.Tensor, prefix: torch.Tensor):
+        pred = self.pred_proj(self.embedding(prefix))            # (B, U+1, J)
+        enc = self.enc_proj(enc_out)                             # (B, T, J)
+        joint = torch.tanh(enc.unsqueeze(2) + pred.unsqueeze(1))  # (B, T, U+1, J)
+        return self.joiner(joint)                                # (B, T, U+1, V)
+
+
+class RNNTCompactPredictorJoiner(nn.Module):
+    """model.py:147-200: the joint only over each sequence's valid (T_b, U_b+1) nodes, packed
+    to (sum_b T_b (U_b+1), V) rows in (b, t, u) order."""
+
+    def __init__(self, enc_out_dim: int, pred_emb_dim: int, join_dim: int, vocab_size: int,
+                 debug: bool = False):
+        super().__init__()
+        self.embedding = nn.Embedding(vocab_size, pred_emb_dim)
+        self.enc_proj = nn.Linear(enc_out_dim, join_dim)
+        self.pred_proj = nn.Linear(pred_emb_dim, join_dim)
+        self.joiner = nn.Linear(join_dim, vocab_size)
+        self.debug = debug
+
+    def forward_compact(self, enc_out, prefix, in_lens, tgt_lens):
+        enc = self.enc_proj(enc_out)
+        pred = self.pred_proj(self.embedding(prefix))
+        rows = []
+        for b in range(enc_out.size(0)):
+            T, U = int(in_lens[b]), int(tgt_lens[b]) + 1
+            rows.append(torch.tanh(enc[b, :T].unsqueeze(1) + pred[b, :U].unsqueeze(0))
+                        .reshape(T * U, -1))
+        return self.joiner(torch.cat(rows, 0))
+
+    def forward(self, enc_out, prefix, in_lens, tgt_lens):
+        return self.forward_compact(enc_out, prefix, in_lens, tgt_lens)
 
 
 class ASRModel(nn.Module):

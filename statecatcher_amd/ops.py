@@ -404,3 +404,94 @@ def ctc_greedy_decode(log_probs, lengths, blank=0):
                                           int(blank), ptr(tokens), ptr(counts), stream_of(log_probs))
     check(rc, "sc_ctc_greedy_decode")
     return tokens, counts
+
+
+# ----------------------------------------------------------------------------- RNN-T ---------
+class RNNTFn(torch.autograd.Function):
+    """nll [B] fp32 of the RNN-T lattice (rnnt.hip) over x: dense [B,T,U+1,V] or compact
+    [sum_b T_b (U_b+1), V] rows; logits (log_softmax fused) or log-probs."""
+
+    @staticmethod
+    def forward(ctx, x, labels, flen, llen, blank, is_logits, row_off, T):
+        require_device(x, labels, flen, llen)
+        compact = row_off is not None
+        if x.stride(-1) != 1:
+            x = x.contiguous()
+        if compact:
+            if x.dim() != 2:
+                raise ValueError(f"compact log_probs must be [rows, V], got {tuple(x.shape)}")
+            B = flen.shape[0]
+            V = x.shape[1]
+            sb, st, su = 0, 0, x.stride(0)
+        else:
+            if x.dim() != 4:
+                raise ValueError(f"log_probs must be [B,T,U+1,V], got {tuple(x.shape)}")
+            B, T, U1, V = x.shape
+            sb, st, su = x.stride(0), x.stride(1), x.stride(2)
+        labels = labels.to(torch.int64).contiguous()
+        if labels.dim() != 2 or labels.shape[0] != B:
+            raise ValueError(f"labels must be padded [B, U_max], got {tuple(labels.shape)}")
+        umax = labels.shape[1] if compact else x.shape[2] - 1
+        if not compact and labels.shape[1] < umax:
+            labels = torch.nn.functional.pad(labels, (0, umax - labels.shape[1]))
+        nll = torch.empty(B, dtype=torch.float32, device=x.device)
+        lib = _lib.load()
+        wsb = lib.sc_rnnt_workspace_bytes(B, max(T, 1), umax)
+        ws = torch.empty(wsb, dtype=torch.uint8, device=x.device)
+        if T == 0 or B == 0:
+            nll.fill_(float("inf"))
+        else:
+            rc = lib.sc_rnnt_fwd(ptr(x), dtype_code(x), int(is_logits), B, T, umax, V, sb, st, su,
+                                 ptr(row_off), ptr(labels), labels.stride(0), ptr(flen), ptr(llen),
+                                 blank, ptr(nll), ptr(ws), wsb, stream_of(x))
+            check(rc, "sc_rnnt_fwd")
+        ctx.save_for_backward(x, labels, flen, llen, ws, row_off)
+        ctx.meta = (blank, int(is_logits), umax, wsb, B, T, V, sb, st, su)
+        return nll
+
+    @staticmethod
+    def backward(ctx, grad_nll):
+        x, labels, flen, llen, ws, row_off = ctx.saved_tensors
+        blank, is_logits, umax, wsb, B, T, V, sb, st, su = ctx.meta
+        grad = torch.empty_like(x, memory_format=torch.contiguous_format)
+        if grad.stride() != x.stride():
+            raise RuntimeError("rnnt backward expects a contiguous input")
+        if T > 0 and B > 0:
+            scale = grad_nll.to(torch.float32).contiguous()
+            rc = _lib.load().sc_rnnt_bwd(ptr(x), dtype_code(x), is_logits, B, T, umax, V, sb, st, su,
+                                         ptr(row_off), ptr(labels), labels.stride(0), ptr(flen),
+                                         ptr(llen), blank, ptr(scale), ptr(grad), dtype_code(grad),
+                                         ptr(ws), wsb, stream_of(x))
+            check(rc, "sc_rnnt_bwd")
+        else:
+            grad.zero_()
+        return grad, None, None, None, None, None, None, None
+
+
+def rnnt_loss(log_probs, labels, frames_lengths, labels_lengths, average_frames=False,
+              reduction="mean", blank=0, gather=False, compact=False, is_logits=False):
+    """warp_rnnt.rnnt_loss's interface (model.py:97-105): log_probs [B,T,U+1,V] (or compact
+    [sum_b T_b(U_b+1), V]), labels [B,U] int, lengths [B].  reduction 'mean' = mean_b(cost_b),
+    'sum', 'none'; average_frames divides each cost by its frame count.  `gather` selects a
+    memory strategy in warp_rnnt and does not change the result (the kernels always gather).
+    is_logits=True fuses the log_softmax (x are joiner logits)."""
+    del gather
+    dev = log_probs.device
+    fl = _as_len_tensor(frames_lengths, dev)
+    ll = _as_len_tensor(labels_lengths, dev)
+    row_off = None
+    T = 0
+    if compact:
+        sizes = fl * (ll + 1)
+        row_off = torch.cumsum(sizes, 0) - sizes
+        T = int(fl.max().item()) if fl.numel() else 0
+    nll = RNNTFn.apply(log_probs, labels.to(dev), fl, ll, int(blank), bool(is_logits), row_off, T)
+    if average_frames:
+        nll = nll / fl.clamp_min(1).to(nll.dtype)
+    if reduction == "none":
+        return nll
+    if reduction == "sum":
+        return nll.sum()
+    if reduction == "mean":
+        return nll.mean()
+    raise ValueError(f"unknown reduction {reduction!r}")

@@ -147,3 +147,26 @@ def test_native_lucyrnn_oracle_vs_reference(name):
     np.testing.assert_allclose(logits, z[name + "/logits"], rtol=1e-4, atol=1e-5)
     np.testing.assert_allclose(np.stack(h), z[name + "/h"], rtol=1e-4, atol=1e-5)
     np.testing.assert_allclose(np.stack(s), z[name + "/s"], rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("T,U", [(1, 0), (1, 2), (2, 0), (3, 2), (4, 3), (2, 4)])
+def test_rnnt_oracle_vs_brute_force_alignments(T, U):
+    """RNN-T parity is unpinned against warp_rnnt (absent): the lattice restatement
+    is pinned against the definition, -log of the sum over every monotonic alignment."""
+    from oracle import rnnt
+    rng = np.random.default_rng(10 * T + U)
+    x = rng.standard_normal((T, U + 1, 5))
+    lp = x - np.log(np.exp(x).sum(-1, keepdims=True))
+    y = rng.integers(1, 5, U)
+    nll, g = rnnt.rnnt_single(lp, y)
+    np.testing.assert_allclose(nll, rnnt.brute_force_nll(lp, y), rtol=1e-12)
+    # gradient: central differences of the lattice nll
+    eps = 1e-6
+    for idx in [(0, 0, 0), (T - 1, U, 0)] + ([(0, 0, int(y[0]))] if U else []):
+        d = np.zeros_like(lp)
+        d[idx] = eps
+        fd = (rnnt.rnnt_single(lp + d, y)[0] - rnnt.rnnt_single(lp - d, y)[0]) / (2 * eps)
+        np.testing.assert_allclose(g[idx], fd, rtol=1e-6, atol=1e-9)
+    # occupancies: every alignment spends exactly one blank per frame and emits all U labels
+    np.testing.assert_allclose(g[:, :, 0].sum(axis=1), -1.0, rtol=1e-10)
+    np.testing.assert_allclose(g[:, :, 1:].sum(), -float(U), rtol=1e-10, atol=1e-12)

@@ -86,3 +86,19 @@ if args.only in ("all", "ctc"):
         lg.grad = None
         ops.ctc_nll(lg, tg, il, tl).sum().backward()
     report("ctc_fwd+bwd", timeit(fb, args.iters), 2 * B * T * V * e)
+if args.only in ("all", "rnnt"):
+    # config C5's lattice per sequence (T=1500, U=150, V=1024) at B=4: 1.86 GB of bf16 logits
+    Br, Tr, Ur = 4, 1500, 150
+    lg = (torch.randn(Br, Tr, Ur + 1, V, device=dev) * 2).to(dt)
+    lab = torch.randint(1, V, (Br, Ur), device=dev)
+    fl = torch.full((Br,), Tr, device=dev, dtype=torch.int64)
+    ll = torch.full((Br,), Ur, device=dev, dtype=torch.int64)
+    nb = Br * Tr * (Ur + 1) * V * e
+    report("rnnt fwd (emit+lattice)", timeit(lambda i: ops.rnnt_loss(lg, lab, fl, ll, is_logits=True),
+                                             max(3, args.iters // 4)), nb)
+    lgr = lg.clone().requires_grad_(True)
+
+    def rb(i):
+        lgr.grad = None
+        ops.rnnt_loss(lgr, lab, fl, ll, is_logits=True).backward()
+    report("rnnt fwd+bwd", timeit(rb, max(3, args.iters // 4)), 3 * nb)
