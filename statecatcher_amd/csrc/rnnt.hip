@@ -73,6 +73,7 @@ struct RnntArgs {
   RnntWs ws;
   const float* scale;
   void* grad;
+  int vec, nvec;   // rows read/written as 16-byte vectors: nvec per lane (V = 64 * N * nvec)
 };
 
 __device__ __forceinline__ int clampr(int64_t v, int lo, int hi) {
@@ -91,10 +92,13 @@ __device__ __forceinline__ int label_at(const RnntArgs& a, int b, int u) {
 }
 
 // ---------------------------------------------------------------------------- emissions -----
+constexpr int kNvMax = 4;   // 16-byte vectors per lane held in registers (V <= 64 * N * 4)
+
 template <int DT>
 __global__ void __launch_bounds__(256) rnnt_emit_kernel(RnntArgs a) {
   using E = Elem<DT>;
   using T = typename E::T;
+  using VL = Vec16<DT>;
   const int lane = threadIdx.x & 63;
   const int64_t node = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (node >= (int64_t)a.B * a.T * a.U1) return;
@@ -104,7 +108,30 @@ __global__ void __launch_bounds__(256) rnnt_emit_kernel(RnntArgs a) {
   if (t >= Tb || u > Ub) return;
   const T* p = (const T*)a.x + node_row(a, b, t, u, Ub);
   float lse = 0.0f;
-  if (a.is_logits) {
+  if (a.is_logits && a.vec) {   // whole row in registers: max pass, then one exp per element
+    float f[kNvMax][VL::N];
+    float m = -__builtin_huge_valf();
+#pragma unroll
+    for (int j = 0; j < kNvMax; ++j) {
+      if (j < a.nvec) {
+        VL::ld(p + (j * 64 + lane) * VL::N, f[j]);
+#pragma unroll
+        for (int k = 0; k < VL::N; ++k) m = fmaxf(m, f[j][k]);
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    float l = 0.0f;
+#pragma unroll
+    for (int j = 0; j < kNvMax; ++j)
+      if (j < a.nvec) {
+#pragma unroll
+        for (int k = 0; k < VL::N; ++k) l += fexp(f[j][k] - m);
+      }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) l += __shfl_xor(l, o);
+    lse = m + flog(l);
+  } else if (a.is_logits) {      // any V / alignment: online max-rescaled sum
     float m = -__builtin_huge_valf(), l = 0.0f;
     for (int v = lane; v < a.V; v += 64) {
       const float xv = E::ld(p[v]);
@@ -168,30 +195,27 @@ __global__ void __launch_bounds__(1024) rnnt_ab_kernel(RnntArgs a) {
   }
   double off = 0.0;
   float v = kDeadR, vn = kDeadR;   // own value and neighbour's value from the previous diagonal
+  // emissions of diagonal step i come from workspace row r(i): alpha reads the arcs entering
+  // diagonal n = i from row n-1 ((t-1,u) blank, (t,u-1) label), beta the arcs leaving row n
+  const int uy = is_beta ? u : (u > 0 ? u - 1 : 0);
+  auto row_of = [&](int i) {
+    const int r = is_beta ? nd - 1 - min(i, nd - 1) : min(i, nd - 1) - 1;
+    return r < 0 ? 0 : r;
+  };
   lds_barrier();
-  for (int i = 0; i < nd; ++i) {
+  auto step = [&](int i, float eb, float ey) __attribute__((always_inline)) {
     const int n = is_beta ? nd - 1 - i : i;
     const int t = n - u;
     const bool valid = u <= Ub && t >= 0 && t < Tb;
     float nv;
     if (!is_beta) {
-      if (n == 0) {
-        nv = (u == 0) ? 0.0f : kDeadR;
-      } else {
-        // (t-1,u) --blank--> (t,u) and (t,u-1) --y[u-1]--> (t,u); the workspace holds no
-        // values for nodes outside the lattice, so each arc is taken only where it exists
-        const float eb = lpb[(int64_t)(n - 1) * a.U1p + u];
-        const float ey = lpy[(int64_t)(n - 1) * a.U1p + (u > 0 ? u - 1 : 0)];
-        nv = lse2_live(t >= 1 ? v + eb : kDeadR, u >= 1 ? vn + ey : kDeadR);
-      }
+      // (t-1,u) --blank--> (t,u) and (t,u-1) --y[u-1]--> (t,u); the workspace holds no values
+      // for nodes outside the lattice, so each arc is taken only where it exists
+      nv = n == 0 ? (u == 0 ? 0.0f : kDeadR)
+                  : lse2_live(t >= 1 ? v + eb : kDeadR, u >= 1 ? vn + ey : kDeadR);
     } else {
-      const float eb = lpb[(int64_t)n * a.U1p + u];
-      if (i == 0) {
-        nv = (u == Ub) ? eb : kDeadR;   // terminal blank of node (Tb-1, Ub)
-      } else {
-        const float ey = lpy[(int64_t)n * a.U1p + u];
-        nv = lse2_live(t + 1 < Tb ? v + eb : kDeadR, u < Ub ? vn + ey : kDeadR);
-      }
+      nv = i == 0 ? (u == Ub ? eb : kDeadR)   // terminal blank of node (Tb-1, Ub)
+                  : lse2_live(t + 1 < Tb ? v + eb : kDeadR, u < Ub ? vn + ey : kDeadR);
     }
     nv = valid ? fmaxf(nv, kDeadR) : kDeadR;
     if (valid) out[(int64_t)n * a.U1p + u] = nv;
@@ -222,10 +246,47 @@ __global__ void __launch_bounds__(1024) rnnt_ab_kernel(RnntArgs a) {
         off += (double)m;
       }
     }
+  };
+  // emission rows prefetched kPf diagonals ahead, explicit ping-pong (no register copies)
+  constexpr int kPf = 8;
+  float ebA[kPf], eyA[kPf], ebB[kPf], eyB[kPf];
+  auto load = [&](float (&eb)[kPf], float (&ey)[kPf], int i0) {
+#pragma unroll
+    for (int j = 0; j < kPf; ++j) {
+      const int64_t r = (int64_t)row_of(i0 + j) * a.U1p;
+      eb[j] = lpb[r + u];
+      ey[j] = lpy[r + uy];
+    }
+  };
+  load(ebA, eyA, 0);
+  for (int i0 = 0; i0 < nd; i0 += 2 * kPf) {
+    load(ebB, eyB, i0 + kPf);
+#pragma unroll
+    for (int j = 0; j < kPf; ++j)
+      if (i0 + j < nd) step(i0 + j, ebA[j], eyA[j]);
+    if (i0 + kPf >= nd) break;
+    load(ebA, eyA, i0 + 2 * kPf);
+#pragma unroll
+    for (int j = 0; j < kPf; ++j)
+      if (i0 + kPf + j < nd) step(i0 + kPf + j, ebB[j], eyB[j]);
   }
 }
 
 // ---------------------------------------------------------------------------- gradient ------
+// N consecutive gradient values (N = elements per 16 bytes of the INPUT type) as 16-byte stores
+// of the gradient type (two stores for an fp32 gradient of 16-bit logits).
+template <int GT, int N>
+__device__ __forceinline__ void store_row_vec(typename Elem<GT>::T* g, const float (&f)[N]) {
+  constexpr int NG = Vec16<GT>::N;
+#pragma unroll
+  for (int h = 0; h < N / NG; ++h) {
+    float q[NG];
+#pragma unroll
+    for (int k = 0; k < NG; ++k) q[k] = f[h * NG + k];
+    Vec16<GT>::st(g + h * NG, q);
+  }
+}
+
 template <int DT, int GT>
 __global__ void __launch_bounds__(256) rnnt_grad_kernel(RnntArgs a) {
   using E = Elem<DT>;
@@ -242,7 +303,15 @@ __global__ void __launch_bounds__(256) rnnt_grad_kernel(RnntArgs a) {
                             : (int64_t)b * a.sb + (int64_t)t * a.st + (int64_t)u * a.su;
   typename G::T* g = (typename G::T*)a.grad + row;
   if (!valid) {   // dense padding rows carry no loss
-    for (int v = lane; v < a.V; v += 64) g[v] = G::st(0.0f);
+    if (a.vec) {
+      constexpr int N = Vec16<DT>::N;
+      float z[N];
+#pragma unroll
+      for (int k = 0; k < N; ++k) z[k] = 0.0f;
+      for (int j = 0; j < a.nvec; ++j) store_row_vec<GT, N>(g + (j * 64 + lane) * N, z);
+    } else {
+      for (int v = lane; v < a.V; v += 64) g[v] = G::st(0.0f);
+    }
     return;
   }
   const double lp2 = a.ws.logp2[b];
@@ -273,6 +342,25 @@ __global__ void __launch_bounds__(256) rnnt_grad_kernel(RnntArgs a) {
   const typename E::T* x = (const typename E::T*)a.x + row;
   const float lse = a.ws.lse[node];
   const float tot = gb + gy;
+  if (a.vec) {
+    using VX = Vec16<DT>;
+    for (int j = 0; j < a.nvec; ++j) {
+      const int v0 = (j * 64 + lane) * VX::N;
+      float f[VX::N];
+      if (a.is_logits) {
+        VX::ld(x + v0, f);
+      }
+#pragma unroll
+      for (int k = 0; k < VX::N; ++k) {
+        float o = a.is_logits ? -fexp(f[k] - lse) * tot : 0.0f;
+        if (v0 + k == a.blank) o += gb;
+        if (v0 + k == yl) o += gy;
+        f[k] = o;
+      }
+      store_row_vec<GT, VX::N>(g + v0, f);
+    }
+    return;
+  }
   for (int v = lane; v < a.V; v += 64) {
     float o = a.is_logits ? -fexp(E::ld(x[v]) - lse) * tot : 0.0f;
     if (v == a.blank) o += gb;
@@ -338,8 +426,23 @@ RnntArgs make_args(const void* x, int is_logits, int B, int T, int Umax, int V, 
   ws_layout(B, T, Umax, &a.ws, const_cast<void*>(ws));
   a.scale = scale;
   a.grad = grad;
+  a.vec = 0;
+  a.nvec = 0;
   return a;
 }
+
+// rows as 16-byte vectors when every row start is 16-byte aligned and V fills whole vectors
+void set_vec(RnntArgs& a, int esize) {
+  const int n = 16 / esize;
+  const bool al = ((uintptr_t)a.x % 16 == 0) && (!a.grad || (uintptr_t)a.grad % 16 == 0) &&
+                  a.su % n == 0 && (a.row_off || (a.sb % n == 0 && a.st % n == 0));
+  if (al && a.V % (64 * n) == 0 && a.V / (64 * n) <= kNvMax) {
+    a.vec = 1;
+    a.nvec = a.V / (64 * n);
+  }
+}
+
+int esize_of(int dt) { return dt == SC_F32 ? 4 : 2; }
 
 }  // namespace
 
@@ -368,6 +471,7 @@ extern "C" int sc_rnnt_fwd(const void* x, int x_dtype, int is_logits, int B, int
   RnntArgs a = make_args(x, is_logits, B, T, max_labels, V, stride_b, stride_t, stride_u,
                          row_offsets, labels, label_stride, frames_lengths, labels_lengths, blank,
                          nll, workspace, nullptr, nullptr);
+  set_vec(a, esize_of(x_dtype));
   hipStream_t st = (hipStream_t)stream;
   switch (x_dtype) {
     case SC_F32: launch_fwd<SC_F32>(a, st); break;
@@ -395,6 +499,7 @@ extern "C" int sc_rnnt_bwd(const void* x, int x_dtype, int is_logits, int B, int
   RnntArgs a = make_args(x, is_logits, B, T, max_labels, V, stride_b, stride_t, stride_u,
                          row_offsets, labels, label_stride, frames_lengths, labels_lengths, blank,
                          nullptr, workspace, scale, grad);
+  set_vec(a, esize_of(x_dtype));
   hipStream_t st = (hipStream_t)stream;
   if (grad_dtype == SC_F32) {
     switch (x_dtype) {

@@ -51,6 +51,41 @@ template <> struct Elem<SC_F16> {
   static __device__ __forceinline__ T st(float f) { return (T)f; }
 };
 
+// 16-byte vectors of an element type: N elements per 16 bytes, converted to / from fp32.
+template <int DT> struct Vec16 {
+  using T = typename Elem<DT>::T;
+  static constexpr int N = 16 / (int)sizeof(T);
+  typedef uint32_t raw_t __attribute__((ext_vector_type(4)));
+  static __device__ __forceinline__ void ld(const T* p, float (&f)[N]) {
+    const raw_t r = *(const raw_t*)p;
+    if constexpr (N == 4) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) f[i] = __uint_as_float(r[i]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        f[2 * i] = Elem<DT>::ldw(r[i] & 0xffffu);
+        f[2 * i + 1] = Elem<DT>::ldw(r[i] >> 16);
+      }
+    }
+  }
+  static __device__ __forceinline__ void st(T* p, const float (&f)[N]) {
+    raw_t r;
+    if constexpr (N == 4) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) r[i] = __float_as_uint(f[i]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const T lo = Elem<DT>::st(f[2 * i]), hi = Elem<DT>::st(f[2 * i + 1]);
+        r[i] = (uint32_t)__builtin_bit_cast(uint16_t, lo) |
+               ((uint32_t)__builtin_bit_cast(uint16_t, hi) << 16);
+      }
+    }
+    *(raw_t*)p = r;
+  }
+};
+
 // ------------------------------------------------------------------ fast math ----------------
 // Single-instruction transcendentals (v_exp_f32 / v_rcp_f32 / v_rsq_f32, ~1 ulp).
 __device__ __forceinline__ float rcp(float x) { return __builtin_amdgcn_rcpf(x); }
