@@ -21,6 +21,10 @@
  *   sc_ctc_*          <- ATen ctc_loss behind nn.CTCLoss(blank=0, zero_infinity=True),
  *                        train.py:142 / model.py:68-71
  *   sc_ctc_greedy_decode <- decoder.py:3-30 `ctc_greedy_decoder`
+ *   sc_mlstm_*        <- the xLSTM encoder's mLSTM cell (model.py:214-229, :301-307; fork kernels
+ *                        "chunkwise--native_autograd", train.py:643-645), math as
+ *                        transformers/models/xlstm/modeling_xlstm.py:74-386 (parity vs the fork
+ *                        unpinned)
  *   sc_rnnt_*         <- warp_rnnt `rnnt_loss(log_probs, labels, frames_lengths, labels_lengths,
  *                        blank, compact, gather=True)` called at model.py:97-105 (train.py:38-42,
  *                        :144); the log_softmax of model.py:93 optionally fused
@@ -188,6 +192,43 @@ int sc_ctc_bwd(const void* x, int x_dtype, int is_logits, int B, int T, int V,
 int sc_ctc_greedy_decode(const void* log_probs, int dtype, int B, int T, int V,
                          int64_t stride_b, int64_t stride_t, const int64_t* lengths, int blank,
                          int32_t* tokens, int32_t* counts, void* stream);
+
+/* ---------------------------------------------------------------- mLSTM ----------------- */
+
+/* 1 if the mLSTM kernels are compiled for this compute dtype (bf16/f16) and head dims. */
+int sc_mlstm_supported(int dtype, int DQ, int DV);
+
+/* Floats of the chunk-start state buffer (and of its gradient): BH * (T/64 + 1) * DQ * DV. */
+int64_t sc_mlstm_state_numel(int BH, int T, int DQ, int DV);
+
+/*
+ * mLSTM cell forward over BH = batch x heads independent sequences, chunkwise (chunk 64,
+ * T % 64 == 0).  q, k [BH][T][DQ], v [BH][T][DV] of dtype (bf16 or f16; MFMA with fp32
+ * accumulation); igate, fgate fp32 [BH][T] pre-activations; optional initial state c0 fp32
+ * [BH][DQ][DV], n0 [BH][DQ], m0 [BH] (NULL = zeros).  Outputs: h [BH][T][DV] (dtype);
+ * states_C/n/m = the stabilised state at every chunk boundary (index T/64 is the final state:
+ * [BH][T/64+1][DQ][DV], [BH][T/64+1][DQ], [BH][T/64+1]); m_rows, den_rows fp32 [BH][T] (the
+ * row stabiliser and normaliser, consumed by the backward).  h_t = q~_t C_t / (max(|q~_t n_t|,
+ * e^{-m_t}) + eps) with q~ = q DQ^-1/2.
+ */
+int sc_mlstm_fwd(const void* q, const void* k, const void* v, int dtype, const float* igate,
+                 const float* fgate, const float* c0, const float* n0, const float* m0, int BH,
+                 int T, int DQ, int DV, float eps, void* h, float* states_C, float* states_n,
+                 float* states_m, float* m_rows, float* den_rows, void* stream);
+
+/*
+ * Backward of sc_mlstm_fwd given dh (dtype, [BH][T][DV]) and optional gradients of the final
+ * state (dcT fp32 [BH][DQ][DV], dnT [BH][DQ]; NULL = zero).  Outputs dq, dk, dv (dtype),
+ * dstates_C/n (gradient w.r.t. every chunk-start state; index 0 = the initial state), and the
+ * per-step gate terms qdq = q_t.dq_t, kdk = k_t.dk_t (fp32 [BH][T]): d igate = kdk,
+ * d fgate_t = sigmoid(-f_t) sum_{r>=t} (qdq_r - kdk_r).  The stabiliser is not differentiated.
+ */
+int sc_mlstm_bwd(const void* q, const void* k, const void* v, int dtype, const float* igate,
+                 const float* fgate, const void* h, const void* dh, const float* dcT,
+                 const float* dnT, const float* states_C, const float* states_n,
+                 const float* states_m, const float* m_rows, const float* den_rows, int BH, int T,
+                 int DQ, int DV, float eps, float* dstates_C, float* dstates_n, void* dq,
+                 void* dk, void* dv, float* qdq, float* kdk, void* stream);
 
 /* ---------------------------------------------------------------- RNN-T ----------------- */
 

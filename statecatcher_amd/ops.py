@@ -495,3 +495,91 @@ def rnnt_loss(log_probs, labels, frames_lengths, labels_lengths, average_frames=
     if reduction == "mean":
         return nll.mean()
     raise ValueError(f"unknown reduction {reduction!r}")
+
+
+# ----------------------------------------------------------------------------- mLSTM ---------
+class MLSTMFn(torch.autograd.Function):
+    """mLSTM cell (mlstm.hip) over q, k [B,NH,T,DQ], v [B,NH,T,DV], gate pre-activations
+    [B,NH,T]; returns h [B,NH,T,DV] and the final state (C [B,NH,DQ,DV], n [B,NH,DQ],
+    m [B,NH,1]) like transformers' mlstm_chunkwise_native_autograd(return_last_states=True).
+    Compute dtype bf16/f16 (fp32 inputs are rounded to bf16, as the reference's kernels run
+    under autocast_kernel_dtype); fp32 state."""
+
+    @staticmethod
+    def forward(ctx, q, k, v, igate, fgate, c0, n0, m0, eps):
+        require_device(q, k, v, igate, fgate)
+        B, NH, T, DQ = q.shape
+        DV = v.shape[-1]
+        cdt = q.dtype if q.dtype in (torch.bfloat16, torch.float16) else torch.bfloat16
+        lib = _lib.load()
+        if not lib.sc_mlstm_supported(dtype_code(torch.empty(0, dtype=cdt)), DQ, DV):
+            raise ValueError(f"mLSTM head dims (DQ={DQ}, DV={DV}) not compiled in")
+        if T % 64:
+            raise ValueError(f"T={T} must be a multiple of 64 (the reference pads to 64)")
+        BH, nc = B * NH, T // 64
+        qc, kc, vc = (x.to(cdt).contiguous().view(BH, T, -1) for x in (q, k, v))
+        ig = igate.float().contiguous().view(BH, T)
+        fg = fgate.float().contiguous().view(BH, T)
+        c0c = None if c0 is None else c0.float().contiguous()
+        n0c = None if n0 is None else n0.float().contiguous()
+        m0c = None if m0 is None else m0.float().contiguous()
+        dev = q.device
+        h = torch.empty(BH, T, DV, dtype=cdt, device=dev)
+        Cs = torch.empty(BH, nc + 1, DQ, DV, dtype=torch.float32, device=dev)
+        ns = torch.empty(BH, nc + 1, DQ, dtype=torch.float32, device=dev)
+        ms = torch.empty(BH, nc + 1, dtype=torch.float32, device=dev)
+        mrow = torch.empty(BH, T, dtype=torch.float32, device=dev)
+        den = torch.empty(BH, T, dtype=torch.float32, device=dev)
+        with _timed("mlstm_fwd", qc, 0):
+            rc = lib.sc_mlstm_fwd(ptr(qc), ptr(kc), ptr(vc), dtype_code(qc), ptr(ig), ptr(fg), ptr(c0c),
+                                  ptr(n0c), ptr(m0c), BH, T, DQ, DV, float(eps), ptr(h), ptr(Cs),
+                                  ptr(ns), ptr(ms), ptr(mrow), ptr(den), stream_of(qc))
+        check(rc, "sc_mlstm_fwd")
+        ctx.save_for_backward(qc, kc, vc, ig, fg, h, Cs, ns, ms, mrow, den)
+        ctx.meta = (B, NH, T, DQ, DV, float(eps), q.dtype, k.dtype, v.dtype, c0 is not None,
+                    n0 is not None)
+        cT = Cs[:, nc].view(B, NH, DQ, DV).clone()
+        nT = ns[:, nc].view(B, NH, DQ).clone()
+        mT = ms[:, nc].view(B, NH, 1).clone()
+        ctx.mark_non_differentiable(mT)
+        return h.view(B, NH, T, DV).to(q.dtype), cT, nT, mT
+
+    @staticmethod
+    def backward(ctx, dh, dcT, dnT, dmT):
+        qc, kc, vc, ig, fg, h, Cs, ns, ms, mrow, den = ctx.saved_tensors
+        B, NH, T, DQ, DV, eps, qdt, kdt, vdt, has_c0, has_n0 = ctx.meta
+        BH, nc = B * NH, T // 64
+        dev = qc.device
+        dhc = dh.to(qc.dtype).contiguous().view(BH, T, DV)
+        dcTc = None if dcT is None else dcT.float().contiguous()
+        dnTc = None if dnT is None else dnT.float().contiguous()
+        dCs = torch.empty_like(Cs)
+        dns = torch.empty_like(ns)
+        dq = torch.empty_like(qc)
+        dk = torch.empty_like(kc)
+        dv = torch.empty_like(vc)
+        qdq = torch.empty(BH, T, dtype=torch.float32, device=dev)
+        kdk = torch.empty(BH, T, dtype=torch.float32, device=dev)
+        with _timed("mlstm_bwd", qc, 0):
+            rc = _lib.load().sc_mlstm_bwd(
+                ptr(qc), ptr(kc), ptr(vc), dtype_code(qc), ptr(ig), ptr(fg), ptr(h), ptr(dhc),
+                ptr(dcTc), ptr(dnTc), ptr(Cs), ptr(ns), ptr(ms), ptr(mrow), ptr(den), BH, T, DQ, DV,
+                eps, ptr(dCs), ptr(dns), ptr(dq), ptr(dk), ptr(dv), ptr(qdq), ptr(kdk), stream_of(qc))
+        check(rc, "sc_mlstm_bwd")
+        # d igate_s = k_s.dk_s ; dF_t = q_t.dq_t - k_t.dk_t ; d fgate = sigmoid(-f) revcumsum(dF)
+        dF = qdq - kdk
+        dfg = torch.sigmoid(-fg) * dF.flip(-1).cumsum(-1).flip(-1)
+        shp = (B, NH, T)
+        return (dq.view(B, NH, T, DQ).to(qdt), dk.view(B, NH, T, DQ).to(kdt),
+                dv.view(B, NH, T, DV).to(vdt), kdk.view(shp), dfg.view(shp),
+                dCs[:, 0].view(B, NH, DQ, DV) if has_c0 else None,
+                dns[:, 0].view(B, NH, DQ) if has_n0 else None, None, None)
+
+
+def mlstm_chunkwise(query, key, value, igate, fgate, c_initial=None, n_initial=None,
+                    m_initial=None, return_last_states=False, eps=1e-6, chunk_size=64, **kwargs):
+    """transformers' mlstm_chunkwise_native_autograd interface on the HIP kernels (chunk 64)."""
+    if chunk_size != 64:
+        raise ValueError("the HIP mLSTM kernels use chunk_size 64")
+    h, c, n, m = MLSTMFn.apply(query, key, value, igate, fgate, c_initial, n_initial, m_initial, eps)
+    return (h, (c, n, m)) if return_last_states else h

@@ -1,0 +1,100 @@
+"""GPU parity of the mLSTM cell kernels (mlstm.hip).  The kernels compute in bf16/f16 (the
+reference runs its kernels under autocast_kernel_dtype=float16) with fp32 state, so the
+checkers are evaluated in fp64 on the SAME rounded inputs: oracle/mlstm.py (forward) and its
+torch restatement tests/torch_ref.mlstm64 (gradients), both pinned to HF transformers'
+chunkwise mLSTM by tests/test_oracle_golden.py / tests/golden/mlstm.npz.  Rows whose
+normaliser q.n nearly cancels amplify the unavoidable bf16 rounding of the intermediate tiles,
+so tensors are compared by relative Frobenius error (<= 1e-2 outputs, <= 3e-2 gradients) and
+elementwise at 10% of the tensor's scale.  Parity against the reference's own xLSTM fork is
+unpinned."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import mlstm as omlstm
+from tests.conftest import load_golden
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0") if torch.cuda.is_available() else None
+
+
+def ops():
+    from statecatcher_amd import ops as o
+    return o
+
+
+def close(got, ref, frac):
+    got = got.detach().double().cpu().numpy() if isinstance(got, torch.Tensor) else got
+    ref = ref.detach().double().cpu().numpy() if isinstance(ref, torch.Tensor) else np.asarray(ref)
+    scale = max(float(np.abs(ref).max()), 1e-30)
+    rel = np.linalg.norm(got - ref) / max(np.linalg.norm(ref), 1e-30)
+    assert rel <= frac, f"relative Frobenius error {rel:.3e} > {frac}"
+    np.testing.assert_allclose(got, ref, rtol=0.1, atol=0.1 * scale)
+
+
+@pytest.mark.parametrize("name", ["small", "state", "c4"])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_mlstm_fwd_bwd_vs_fp64_on_rounded_inputs(name, dtype):
+    from tests.torch_ref import mlstm64
+    z = load_golden("mlstm")
+    g = lambda k: torch.as_tensor(z[f"{name}/{k}"]) if f"{name}/{k}" in z.files else None  # noqa
+    ins = {key: g(key).to(dtype) for key in ("q", "k", "v")}
+    ins.update({key: g(key) for key in ("igate", "fgate", "c0", "n0") if g(key) is not None})
+    m0 = g("m0")
+    leaves = {key: t.to(DEV).requires_grad_(True) for key, t in ins.items()}
+    h, (cT, nT, mT) = ops().mlstm_chunkwise(leaves["q"], leaves["k"], leaves["v"], leaves["igate"],
+                                           leaves["fgate"], leaves.get("c0"), leaves.get("n0"),
+                                           None if m0 is None else m0.to(DEV),
+                                           return_last_states=True)
+    ref_leaves = {key: t.double().requires_grad_(True) for key, t in ins.items()}
+    rh, (rc, rn, rm) = mlstm64(ref_leaves["q"], ref_leaves["k"], ref_leaves["v"], ref_leaves["igate"],
+                               ref_leaves["fgate"], ref_leaves.get("c0"), ref_leaves.get("n0"),
+                               None if m0 is None else m0.double())
+    close(h, rh, 1e-2)
+    close(cT, rc, 1e-2)
+    close(nT, rn, 1e-2)
+    np.testing.assert_allclose(mT.cpu().numpy(), rm.detach().numpy(), rtol=1e-5, atol=1e-5)
+    R = g("R")
+    (h.float() * R.to(DEV)).sum().backward()
+    (rh * R.double()).sum().backward()
+    for key, t in leaves.items():
+        close(t.grad, ref_leaves[key].grad, 3e-2)
+
+
+def test_mlstm_fp32_reference_fixture_at_bf16_tolerance():
+    """Against HF's own fp64 outputs on the unrounded inputs (the fixture itself)."""
+    z = load_golden("mlstm")
+    h = ops().mlstm_chunkwise(*[torch.as_tensor(z[f"c4/{k}"]).to(DEV)
+                                for k in ("q", "k", "v", "igate", "fgate", "c0", "n0", "m0")])
+    close(h, z["c4/h"], 3e-2)
+
+
+def test_mlstm_long_sequence_vs_oracle_and_state_carry():
+    """T = 1536 (the C4 segment after padding to 64): h and final state vs the numpy step
+    recurrence; two carried halves equal one pass."""
+    torch.manual_seed(0)
+    B, NH, T, DQ, DV = 1, 2, 1536, 64, 128
+    q, k = torch.randn(B, NH, T, DQ), torch.randn(B, NH, T, DQ)
+    v = torch.randn(B, NH, T, DV)
+    ig, fg = torch.randn(B, NH, T) * 3, torch.randn(B, NH, T) * 2 + 3
+    qb, kb, vb = (x.bfloat16() for x in (q, k, v))
+    args = [x.to(DEV) for x in (qb, kb, vb, ig, fg)]
+    h, (C, n, m) = ops().mlstm_chunkwise(*args, return_last_states=True)
+    rh, (rC, rn, rm) = omlstm.mlstm_recurrent(qb.float().numpy(), kb.float().numpy(),
+                                              vb.float().numpy(), ig.numpy(), fg.numpy())
+    close(h, rh, 2e-2)
+    close(C, rC, 2e-2)
+    np.testing.assert_allclose(m.cpu().numpy(), rm, rtol=1e-4, atol=1e-4)
+    half = T // 2
+    h1, st = ops().mlstm_chunkwise(*[a[:, :, :half] for a in args], return_last_states=True)
+    h2, (C2, _, _) = ops().mlstm_chunkwise(*[a[:, :, half:] for a in args], *st,
+                                           return_last_states=True)
+    torch.testing.assert_close(torch.cat([h1, h2], 2).float(), h.float(), rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(C2, C, rtol=1e-3, atol=1e-3)
+
+
+def test_mlstm_rejects_unsupported_shapes():
+    q = torch.randn(1, 1, 100, 64, device=DEV, dtype=torch.bfloat16)
+    with pytest.raises(ValueError):
+        ops().mlstm_chunkwise(q, q, torch.randn(1, 1, 100, 128, device=DEV, dtype=torch.bfloat16),
+                              torch.zeros(1, 1, 100, device=DEV), torch.zeros(1, 1, 100, device=DEV))

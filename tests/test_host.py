@@ -85,8 +85,9 @@ def test_compute_loss_rejects_unknown_mode():
             return f, s
     with pytest.raises(ValueError):
         sc.compute_loss("xyz", None, Dummy(), torch.zeros(1, 2, 3), None, None, [2], [1], 0)
-    with pytest.raises(NotImplementedError):
-        sc.compute_loss("rnnt", None, Dummy(), torch.zeros(1, 2, 3), None, None, [2], [1], 0)
+    with pytest.raises(AssertionError):   # rnnt needs the joiner (model.py:74)
+        sc.compute_loss("rnnt", None, Dummy(), torch.zeros(1, 2, 3), None, torch.zeros(1, 1,
+                        dtype=torch.int64), [2], [1], 0)
 
 
 def test_compute_loss_reference_criterion_path():

@@ -170,3 +170,17 @@ def test_rnnt_oracle_vs_brute_force_alignments(T, U):
     # occupancies: every alignment spends exactly one blank per frame and emits all U labels
     np.testing.assert_allclose(g[:, :, 0].sum(axis=1), -1.0, rtol=1e-10)
     np.testing.assert_allclose(g[:, :, 1:].sum(), -float(U), rtol=1e-10, atol=1e-12)
+
+
+@pytest.mark.parametrize("name", ["small", "state", "c4"])
+def test_mlstm_oracle_vs_hf_chunkwise(name):
+    """oracle/mlstm.py (step recurrence) == HF transformers' chunkwise mLSTM (fixture)."""
+    from oracle import mlstm
+    z = load_golden("mlstm")
+    g = lambda k: z.get(f"{name}/{k}") if f"{name}/{k}" in z.files else None  # noqa: E731
+    h, (C, n, m) = mlstm.mlstm_recurrent(g("q"), g("k"), g("v"), g("igate"), g("fgate"),
+                                         g("c0"), g("n0"), g("m0"))
+    np.testing.assert_allclose(h, g("h"), rtol=2e-4, atol=2e-5 * np.abs(g("h")).max())
+    np.testing.assert_allclose(C, g("cT"), rtol=2e-4, atol=2e-5 * np.abs(g("cT")).max())
+    np.testing.assert_allclose(n, g("nT"), rtol=2e-4, atol=2e-5 * np.abs(g("nT")).max())
+    np.testing.assert_allclose(m, g("mT"), rtol=1e-5, atol=1e-5)

@@ -43,3 +43,28 @@ def lucyrnn64(params, x, L, D, states=None):
                                                params[f"norms.0.{l}.bias"], 1e-5)
     logits = x @ params["output_proj.weight"].t() + params["output_proj.bias"]
     return logits, (h, s)
+
+
+def mlstm64(q, k, v, ig, fg, c0=None, n0=None, m0=None, eps=1e-6):
+    """fp64 torch restatement of the mLSTM step recurrence (oracle/mlstm.py, itself pinned to
+    transformers' chunkwise mLSTM by tests/test_oracle_golden.py), for autograd gradients."""
+    B, NH, T, DQ = q.shape
+    DV = v.shape[-1]
+    C = torch.zeros(B, NH, DQ, DV, dtype=q.dtype) if c0 is None else c0
+    n = torch.zeros(B, NH, DQ, dtype=q.dtype) if n0 is None else n0
+    m = torch.zeros(B, NH, dtype=q.dtype) if m0 is None else m0.reshape(B, NH)
+    s = DQ ** -0.5
+    hs = []
+    for t in range(T):
+        lf = torch.nn.functional.logsigmoid(fg[..., t])
+        mn = torch.maximum(lf + m, ig[..., t]).detach()   # the stabiliser is not differentiated
+        fa = torch.exp(lf + m - mn)
+        ia = torch.exp(ig[..., t] - mn)
+        C = fa[..., None, None] * C + ia[..., None, None] * (k[..., t, :, None] * v[..., t, None, :])
+        n = fa[..., None] * n + ia[..., None] * k[..., t, :]
+        qs = q[..., t, :] * s
+        num = torch.einsum("bhi,bhij->bhj", qs, C)
+        den = torch.maximum((qs * n).sum(-1).abs(), torch.exp(-mn)) + eps
+        hs.append(num / den[..., None])
+        m = mn
+    return torch.stack(hs, 2), (C, n, m[..., None])
