@@ -7,14 +7,16 @@ wrapped in drop-ins of the reference's module API (lucyrnn_triton.py, decoder.py
 from .lucyrnn_conf import LucyRNNConfig
 from .lucyrnn_triton import LinearSafe, LucyRNNCellTriton, LucyRNNtriton
 from .lucyrnn import LucyRNN, LucyRNNCell
+from .xlstm import xLSTMLarge, xLSTMLargeConfig
 from .model import (ASRModel, CTCLoss, RNNTCompactPredictorJoiner, RNNTLoss, RNNTPredictorJoiner,
                     compute_loss, detach_states)
-from .ops import ctc_greedy_decode, ctc_loss, ctc_nll, decay_scan, lucy_scan, rnnt_loss
+from .ops import (ctc_greedy_decode, ctc_loss, ctc_nll, decay_scan, lucy_scan, mlstm_chunkwise,
+                  rnnt_loss)
 from .decoder import ctc_greedy_decoder
 
 __all__ = [
     "LucyRNNConfig", "LinearSafe", "LucyRNNCellTriton", "LucyRNNtriton", "LucyRNN", "LucyRNNCell", "ASRModel", "CTCLoss",
     "compute_loss", "detach_states", "ctc_greedy_decode", "ctc_loss", "ctc_nll", "decay_scan",
     "lucy_scan", "ctc_greedy_decoder", "rnnt_loss", "RNNTLoss", "RNNTPredictorJoiner",
-    "RNNTCompactPredictorJoiner",
+    "RNNTCompactPredictorJoiner", "xLSTMLarge", "xLSTMLargeConfig", "mlstm_chunkwise",
 ]

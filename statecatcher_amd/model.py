@@ -13,6 +13,7 @@ import torch.nn as nn
 
 from .lucyrnn_conf import LucyRNNConfig
 from .lucyrnn_triton import LucyRNNtriton
+from .xlstm import xLSTMLarge, xLSTMLargeConfig
 from .ops import ctc_loss, rnnt_loss
 
 
@@ -196,7 +197,14 @@ class ASRModel(nn.Module):
         super().__init__()
         self.frontend = frontend
         self.debug = debug
-        if isinstance(encoder, LucyRNNConfig):
+        if isinstance(encoder, xLSTMLargeConfig):   # model.py:301-307
+            self.cfg = encoder
+            self.encoder = xLSTMLarge(self.cfg)
+            self.enc_out_dim = vocab_size
+            self.input_seq_pad_factor = 64
+            if proj_dim > 0:
+                self.proj = nn.Linear(feat_dim, proj_dim)
+        elif isinstance(encoder, LucyRNNConfig):
             self.cfg = encoder
             self.encoder = LucyRNNtriton(self.cfg)
             self.enc_out_dim = vocab_size
@@ -209,6 +217,16 @@ class ASRModel(nn.Module):
     def forward(self, feats, mask, states=None):
         if hasattr(self, "proj"):
             feats = self.proj(feats)
+        if isinstance(self.encoder, xLSTMLarge):
+            # model.py:341-347: pad time to the 64-step chunk.  The reference then multiplies by
+            # the UNPADDED mask (a broadcast error whenever T % 64 != 0); the mask is padded
+            # with zeros here so padded frames are zero, as intended.
+            rem = feats.size(1) % self.input_seq_pad_factor
+            if rem:
+                pad = self.input_seq_pad_factor - rem
+                feats = torch.nn.functional.pad(feats, (0, 0, 0, pad))
+                if mask is not None:
+                    mask = torch.nn.functional.pad(mask, (0, pad))
         if mask is not None:
             feats = feats * mask.unsqueeze(-1).to(feats.dtype)
         if states is not None:
@@ -216,6 +234,14 @@ class ASRModel(nn.Module):
         else:
             logits, new_states = self.encoder(feats)
         return logits, new_states
+
+
+def build_xlstm_config(feat_dim, vocab_size, num_heads=2, num_blocks=3, embedding_dim=None):
+    """model.py:214-229: the xLSTM config train.py builds (embedding_dim = input_dim = feat_dim
+    in the reference; C4 uses a 768-wide model behind the input projection)."""
+    return xLSTMLargeConfig(embedding_dim=embedding_dim or feat_dim, input_dim=feat_dim,
+                            num_heads=num_heads, num_blocks=num_blocks, vocab_size=vocab_size,
+                            return_last_states=True, mode="train")
 
 
 def build_lucyrnn_config(input_dim, hidden_size, num_layers, vocab_size, is_training=True):

@@ -1,0 +1,184 @@
+"""xLSTM encoder (config C4) around the HIP mLSTM cell (csrc/mlstm.hip).
+
+The reference builds ``xLSTMLarge(xLSTMLargeConfig(...))`` from its fork of NX-AI's xlstm
+package (model.py:214-229, :301-307; the fork adds ``input_dim``).  The fork is not available
+(parity w.r.t. the fork unpinned); the block structure here is the published
+xLSTM-large architecture as transformers 5.15.0 restates it
+(transformers/models/xlstm/modeling_xlstm.py:870-1205), with the same parameter names:
+
+  block:  x + mLSTMLayer(RMSNorm(x));  x + FFN(RMSNorm(x))
+  layer:  q, k, v, o = Linear(x);  i, f = softcap(Linear(x), 15)  (one gate per head)
+          h = mLSTM cell (HIP, chunkwise, state carried);  y = out_proj(sigmoid(o) *
+          MultiHeadLayerNorm(h))
+  FFN:    proj_down(silu(proj_up_gate(x)) * proj_up(x))
+  model:  input projection (the fork's input_dim -> embedding_dim; a Linear named
+          ``embedding``), blocks, out_norm, lm_head, logits softcap(30)
+
+Recurrent state: {block index: (C [B,NH,DQ,DV], n [B,NH,DQ], m [B,NH,1])}, carried across
+segments like LucyRNNtriton's (detach_states handles dicts).  Sequences must be a multiple of
+the 64-step chunk: ASRModel pads to 64 exactly as the reference does (model.py:341-347).
+"""
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .ops import mlstm_chunkwise
+
+
+def soft_cap(x, cap):
+    return x if cap is None else cap * torch.tanh(x / cap)
+
+
+def round_up(x, m):
+    return int(((x + m - 1) // m) * m)
+
+
+@dataclass
+class xLSTMLargeConfig:
+    """Fields the reference passes (model.py:216-228) plus xLSTM-large's defaults."""
+    embedding_dim: int
+    num_heads: int
+    num_blocks: int
+    vocab_size: int
+    input_dim: Optional[int] = None
+    return_last_states: bool = True
+    mode: str = "train"
+    chunkwise_kernel: str = "chunkwise--native_autograd"
+    sequence_kernel: str = "native_sequence__native"
+    step_kernel: str = "native"
+    autocast_kernel_dtype: str = "bfloat16"
+    qk_dim_factor: float = 0.5
+    v_dim_factor: float = 1.0
+    gate_soft_cap: float = 15.0
+    output_logit_soft_cap: float = 30.0
+    norm_eps: float = 1e-6
+    norm_reduction_force_float32: bool = True
+    ffn_proj_factor: float = 2.667
+    ffn_round_up_to_multiple_of: int = 64
+    use_bias: bool = False
+    add_out_norm: bool = True
+    eps: float = 1e-6
+    chunk_size: int = 64
+
+
+class RMSNorm(nn.Module):
+    def __init__(self, num_features, eps=1e-6, use_bias=False, force_float32_reductions=True):
+        super().__init__()
+        self.eps = eps
+        self.force_float32_reductions = force_float32_reductions
+        self.weight = nn.Parameter(torch.ones(num_features))
+        self.bias = nn.Parameter(torch.zeros(num_features)) if use_bias else None
+
+    def forward(self, x):
+        dt = x.dtype
+        y = x.float() if self.force_float32_reductions else x
+        y = (y * torch.rsqrt(y.pow(2).mean(-1, keepdim=True) + self.eps)).to(dt)
+        y = y * self.weight
+        return y + self.bias if self.bias is not None else y
+
+
+class MultiHeadLayerNorm(nn.Module):
+    def __init__(self, num_heads, head_dim, eps=1e-6, use_bias=False, force_float32_reductions=True):
+        super().__init__()
+        self.num_heads, self.head_dim, self.eps = num_heads, head_dim, eps
+        self.force_float32_reductions = force_float32_reductions
+        self.weight = nn.Parameter(torch.ones(num_heads * head_dim))
+        self.bias = nn.Parameter(torch.zeros(num_heads * head_dim)) if use_bias else None
+
+    def forward(self, x):   # x [B, T, NH, DH]
+        B, T = x.shape[:2]
+        dt = x.dtype
+        y = x.float() if self.force_float32_reductions else x
+        y = (y - y.mean(-1, keepdim=True)) * torch.rsqrt(y.var(-1, keepdim=True, unbiased=False) + self.eps)
+        y = y.to(dt).reshape(B, T, -1) * self.weight
+        return y + self.bias if self.bias is not None else y
+
+
+class FeedForward(nn.Module):
+    def __init__(self, cfg: xLSTMLargeConfig):
+        super().__init__()
+        up = round_up(cfg.embedding_dim * cfg.ffn_proj_factor, cfg.ffn_round_up_to_multiple_of)
+        self.proj_up_gate = nn.Linear(cfg.embedding_dim, up, bias=cfg.use_bias)
+        self.proj_up = nn.Linear(cfg.embedding_dim, up, bias=cfg.use_bias)
+        self.proj_down = nn.Linear(up, cfg.embedding_dim, bias=cfg.use_bias)
+
+    def forward(self, x):
+        return self.proj_down(F.silu(self.proj_up_gate(x)) * self.proj_up(x))
+
+
+class mLSTMLayer(nn.Module):
+    def __init__(self, cfg: xLSTMLargeConfig):
+        super().__init__()
+        self.cfg = cfg
+        d = cfg.embedding_dim
+        self.v_dim = int(d * cfg.v_dim_factor)
+        self.qk_dim = int(d * cfg.qk_dim_factor)
+        self.q = nn.Linear(d, self.qk_dim, bias=cfg.use_bias)
+        self.k = nn.Linear(d, self.qk_dim, bias=cfg.use_bias)
+        self.v = nn.Linear(d, self.v_dim, bias=cfg.use_bias)
+        self.ogate_preact = nn.Linear(d, self.v_dim, bias=cfg.use_bias)
+        self.igate_preact = nn.Linear(d, cfg.num_heads, bias=True)
+        self.fgate_preact = nn.Linear(d, cfg.num_heads, bias=True)
+        self.multihead_norm = MultiHeadLayerNorm(cfg.num_heads, self.v_dim // cfg.num_heads,
+                                                 cfg.norm_eps, cfg.use_bias,
+                                                 cfg.norm_reduction_force_float32)
+        self.out_proj = nn.Linear(self.v_dim, d, bias=cfg.use_bias)
+
+    def forward(self, x, state=None):
+        B, T, _ = x.shape
+        NH = self.cfg.num_heads
+        q = self.q(x).reshape(B, T, NH, -1).transpose(1, 2)
+        k = self.k(x).reshape(B, T, NH, -1).transpose(1, 2)
+        v = self.v(x).reshape(B, T, NH, -1).transpose(1, 2)
+        o = self.ogate_preact(x)
+        ig = soft_cap(self.igate_preact(x), self.cfg.gate_soft_cap).transpose(1, 2)
+        fg = soft_cap(self.fgate_preact(x), self.cfg.gate_soft_cap).transpose(1, 2)
+        c0, n0, m0 = (None, None, None) if state is None else state
+        h, new_state = mlstm_chunkwise(q, k, v, ig, fg, c0, n0, m0, return_last_states=True,
+                                       eps=self.cfg.eps)
+        h = self.multihead_norm(h.transpose(1, 2))
+        return self.out_proj(torch.sigmoid(o) * h), new_state
+
+
+class xLSTMBlock(nn.Module):
+    def __init__(self, cfg: xLSTMLargeConfig):
+        super().__init__()
+        self.norm_mlstm = RMSNorm(cfg.embedding_dim, cfg.norm_eps, cfg.use_bias,
+                                  cfg.norm_reduction_force_float32)
+        self.mlstm_layer = mLSTMLayer(cfg)
+        self.norm_ffn = RMSNorm(cfg.embedding_dim, cfg.norm_eps, cfg.use_bias,
+                                cfg.norm_reduction_force_float32)
+        self.ffn = FeedForward(cfg)
+
+    def forward(self, x, state=None):
+        y, state = self.mlstm_layer(self.norm_mlstm(x), state)
+        x = x + y
+        return x + self.ffn(self.norm_ffn(x)), state
+
+
+class xLSTMLarge(nn.Module):
+    """The encoder ASRModel builds for ``--encoder xlstm`` (model.py:301-307)."""
+
+    def __init__(self, config: xLSTMLargeConfig):
+        super().__init__()
+        self.config = config
+        d_in = config.input_dim if config.input_dim is not None else config.embedding_dim
+        self.embedding = nn.Linear(d_in, config.embedding_dim)
+        self.blocks = nn.ModuleList([xLSTMBlock(config) for _ in range(config.num_blocks)])
+        self.out_norm = (RMSNorm(config.embedding_dim, config.norm_eps, config.use_bias,
+                                 config.norm_reduction_force_float32)
+                         if config.add_out_norm else nn.Identity())
+        self.lm_head = nn.Linear(config.embedding_dim, config.vocab_size, bias=False)
+
+    def forward(self, x, state=None):
+        x = self.embedding(x)
+        new_state = {}
+        for i, blk in enumerate(self.blocks):
+            x, new_state[i] = blk(x, None if state is None else state.get(i))
+        logits = soft_cap(self.lm_head(self.out_norm(x)), self.config.output_logit_soft_cap)
+        if self.config.return_last_states:
+            return logits, new_state
+        return logits

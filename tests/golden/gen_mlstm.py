@@ -54,9 +54,39 @@ def case(B, NH, T, DQ, DV, seed, init=False):
     return {k: v.astype(np.float32) for k, v in out.items()}
 
 
+def block_case(seed=5):
+    """One HF xLSTMBlock (hidden 128, 2 heads -> DQ 32, DV 64) in fp64: the layer/block
+    structure statecatcher_amd/xlstm.py mirrors."""
+    from transformers import xLSTMConfig
+    cfg = xLSTMConfig(hidden_size=128, embedding_dim=128, num_heads=2, num_blocks=1, vocab_size=10,
+                      mode="train", chunkwise_kernel="chunkwise--native_autograd",
+                      autocast_kernel_dtype="float32", return_last_states=True)
+    torch.manual_seed(seed)
+    blk = M.xLSTMBlock(cfg).double()
+    with torch.no_grad():
+        for name, p in blk.named_parameters():
+            if p.dim() > 1:
+                p.normal_(0.0, 0.08)
+            elif "norm" in name:
+                p.normal_(1.0, 0.1)
+            else:
+                p.normal_(0.0, 1.0)
+    x = torch.randn(2, 128, 128, dtype=torch.float64, requires_grad=True)
+    y, (c, n, m) = blk(x)
+    R = torch.randn(y.shape, dtype=torch.float64)
+    (y * R).sum().backward()
+    out = {"param/" + k: v.detach().numpy() for k, v in blk.state_dict().items()}
+    out.update(x=x.detach().numpy(), y=y.detach().numpy(), cT=c.detach().numpy(),
+               nT=n.detach().numpy(), mT=m.detach().numpy(), R=R.numpy(), dx=x.grad.numpy(),
+               dq_weight=blk.mlstm_layer.q.weight.grad.numpy(),
+               dfgate_bias=blk.mlstm_layer.fgate_preact.bias.grad.numpy())
+    return {k: v.astype(np.float32) for k, v in out.items()}
+
+
 def main():
     cases = {"small": case(1, 2, 128, 32, 64, 1), "state": case(2, 1, 64, 32, 64, 2, init=True),
              "c4": case(1, 1, 128, 96, 192, 3, init=True)}
+    cases["block"] = block_case()
     flat = {f"{c}/{k}": v for c, d in cases.items() for k, v in d.items()}
     np.savez_compressed(os.path.join(HERE, "mlstm.npz"), **flat)
     print({k: v.shape for k, v in flat.items() if k.startswith("c4/")})

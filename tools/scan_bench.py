@@ -102,3 +102,22 @@ if args.only in ("all", "rnnt"):
         lgr.grad = None
         ops.rnnt_loss(lgr, lab, fl, ll, is_logits=True).backward()
     report("rnnt fwd+bwd", timeit(rb, max(3, args.iters // 4)), 3 * nb)
+if args.only in ("all", "mlstm"):
+    # config C4's cell: d=768, 4 heads (DQ 96, DV 192), T=1536 (1500 padded to 64), B=32
+    Bm, NHm, Tm, DQm, DVm = 32, 4, 1536, 96, 192
+    qm = torch.randn(Bm, NHm, Tm, DQm, device=dev, dtype=torch.bfloat16)
+    km = torch.randn(Bm, NHm, Tm, DQm, device=dev, dtype=torch.bfloat16)
+    vm = torch.randn(Bm, NHm, Tm, DVm, device=dev, dtype=torch.bfloat16)
+    igm = torch.randn(Bm, NHm, Tm, device=dev) * 3
+    fgm = torch.randn(Bm, NHm, Tm, device=dev) * 2 + 3
+    nc = Tm // 64
+    io = Bm * NHm * Tm * (2 * DQm + 2 * DVm) * 2
+    st_bytes = Bm * NHm * (nc + 1) * DQm * DVm * 4
+    report("mlstm fwd (C pass + H pass)", timeit(lambda i: ops.mlstm_chunkwise(qm, km, vm, igm, fgm),
+                                                 args.iters), io + 2 * st_bytes)
+    qg, kg, vg = (x.clone().requires_grad_(True) for x in (qm, km, vm))
+
+    def mb(i):
+        qg.grad = kg.grad = vg.grad = None
+        ops.mlstm_chunkwise(qg, kg, vg, igm, fgm).float().sum().backward()
+    report("mlstm fwd+bwd", timeit(mb, args.iters), 3 * io + 6 * st_bytes)
