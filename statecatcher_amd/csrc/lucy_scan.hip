@@ -328,8 +328,10 @@ lucy_scan_bwd_kernel(ScanBwdArgs a) {
   const int pcmax = (min(64, a.D - blk * 64) - 1) / P::EPP;
 
   extern __shared__ __attribute__((aligned(16))) unsigned char dyn_lds[];
-  __shared__ float2 aggA[NW][64];
-  __shared__ float2 aggB[NW][64];
+  __shared__ float2 aggA[NW][64];   // s maps      (B1)
+  __shared__ float2 aggB[NW][64];   // h maps      (B2)
+  __shared__ float2 aggC[NW][64];   // Gh maps     (B1)
+  __shared__ float2 aggD[NW][64];   // Gs maps     (B2)
   __shared__ float carGh[2][64];
   __shared__ float carGs[2][64];
   __shared__ float ckS[2][2][64];   // (s, h) checkpoint of the super-chunk, shared by all waves
@@ -413,7 +415,16 @@ lucy_scan_bwd_kernel(ScanBwdArgs a) {
       lds_read_wait();
       if (it + 1 < a.nsc) issue(it + 1);                // refill the slot just read
     }
+    // The Gh adjoint depends only on zg and dout, so its segment map is published with the
+    // s map (one barrier); Gs needs c = tanh(hn + s) and goes out with the h map.
+    float Ph = 1.0f, Qh = 0.0f;   // adjoint of h: C_t = zg_t Gh_t flows to step t-1
+#pragma unroll
+    for (int j = LC - 1; j >= 0; --j) {
+      Qh = zg[j] * (dj[j] + Qh);
+      Ph *= zg[j];
+    }
     aggA[w][lane] = make_float2(As, Bs);
+    aggC[w][lane] = make_float2(Ph, Qh);
     if (!(SC_ABL & 8)) lds_barrier();                          // B1
     float s = s_ck;
     if (!(SC_ABL & 4)) s = compose_prefix<NW>(aggA, lane, w, s);
@@ -426,8 +437,25 @@ lucy_scan_bwd_kernel(ScanBwdArgs a) {
       Ah *= zg[j];
       Bh = zg[j] * Bh + (1.0f - zg[j]) * x[j];
     }
+    float C = carGh[it & 1][lane];
+    if (!(SC_ABL & 4)) C = compose_suffix<NW>(aggC, lane, w, C);
+#pragma unroll
+    for (int j = LC - 1; j >= 0; --j) {
+      u[j] = dj[j] + C;                                         // Gh_t
+      C = zg[j] * u[j];
+    }
+    if (w == 0) carGh[(it + 1) & 1][lane] = C;
+    // adjoint of s: Cs_t = dec_t Gs_t flows to step t-1
+    float Ps = 1.0f, Qs = 0.0f;
+#pragma unroll
+    for (int j = LC - 1; j >= 0; --j) {
+      Qs = dec[j] * (u[j] * (1.0f - zg[j]) * (1.0f - x[j] * x[j]) + Qs);
+      Ps *= dec[j];
+    }
     aggB[w][lane] = make_float2(Ah, Bh);
-    if (!(SC_ABL & 8)) lds_barrier();                          // B2
+    aggD[w][lane] = make_float2(Ps, Qs);
+    dma_wait();                   // the next super-chunk (and its checkpoint) has landed
+    lds_barrier();                                             // B2
     float h = h_ck;
     if (!(SC_ABL & 4)) h = compose_prefix<NW>(aggB, lane, w, h);
 #pragma unroll
@@ -435,35 +463,8 @@ lucy_scan_bwd_kernel(ScanBwdArgs a) {
       hv[j] = h;
       h = zg[j] * h + (1.0f - zg[j]) * x[j];
     }
-    // ---- adjoint of h: C_t = zg_t Gh_t flows to step t-1 ----
-    float Ph = 1.0f, Qh = 0.0f;
-#pragma unroll
-    for (int j = LC - 1; j >= 0; --j) {
-      Qh = zg[j] * (dj[j] + Qh);
-      Ph *= zg[j];
-    }
-    aggA[w][lane] = make_float2(Ph, Qh);
-    if (!(SC_ABL & 8)) lds_barrier();                          // B3
-    float C = carGh[it & 1][lane];
-    if (!(SC_ABL & 4)) C = compose_suffix<NW>(aggA, lane, w, C);
-#pragma unroll
-    for (int j = LC - 1; j >= 0; --j) {
-      u[j] = dj[j] + C;                                         // Gh_t
-      C = zg[j] * u[j];
-    }
-    if (w == 0) carGh[(it + 1) & 1][lane] = C;
-    // ---- adjoint of s: Cs_t = dec_t Gs_t flows to step t-1 ----
-    float Ps = 1.0f, Qs = 0.0f;
-#pragma unroll
-    for (int j = LC - 1; j >= 0; --j) {
-      Qs = dec[j] * (u[j] * (1.0f - zg[j]) * (1.0f - x[j] * x[j]) + Qs);
-      Ps *= dec[j];
-    }
-    aggB[w][lane] = make_float2(Ps, Qs);
-    dma_wait();                   // the next super-chunk (and its checkpoint) has landed
-    lds_barrier();                                             // B4
     float Cs = carGs[it & 1][lane];
-    if (!(SC_ABL & 4)) Cs = compose_suffix<NW>(aggB, lane, w, Cs);
+    if (!(SC_ABL & 4)) Cs = compose_suffix<NW>(aggD, lane, w, Cs);
 #pragma unroll
     for (int j = LC - 1; j >= 0; --j) {
       const float dpre = u[j] * (1.0f - zg[j]) * (1.0f - x[j] * x[j]);
