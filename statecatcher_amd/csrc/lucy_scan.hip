@@ -147,6 +147,39 @@ __device__ __forceinline__ void gate_grads(float r, float z, float k, float v, f
   o[6] = gs * (k * v * f) * alp * (1.0f - alp) * kEps * (ira * ira * ira);
 }
 
+// gate_grads for two steps at once: the elementwise math runs as packed fp32 (v_pk_fma_f32 /
+// v_pk_mul_f32 on two steps per instruction); the transcendentals stay per component.
+typedef float f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2 rsq2(f2 x) { return f2{rsq(x.x), rsq(x.y)}; }
+__device__ __forceinline__ f2 rcp2(f2 x) { return f2{rcp(x.x), rcp(x.y)}; }
+__device__ __forceinline__ f2 sigm2(f2 x) { return f2{sigm(x.x), sigm(x.y)}; }
+
+__device__ __forceinline__ void gate_grads2(f2 r, f2 z, f2 k, f2 v, f2 hp, f2 dc, f2 al, f2 zg,
+                                            f2 dec, f2 gh, f2 dpre, f2 gs, f2 hprev, f2 sprev,
+                                            f2 c, f2 (&o)[7]) {
+  const f2 one = {1.0f, 1.0f}, eps = {kEps, kEps}, half = {0.5f, 0.5f};
+  const f2 rc2 = (r * r + z * z) * half + eps;
+  const f2 irc = rsq2(rc2);
+  const f2 ird = rsq2(dc * dc + eps);
+  const f2 ira = rsq2(al * al + eps);
+  const f2 alp = sigm2(al * ira);
+  const f2 irh = rsq2(hp * hp + eps);
+  const f2 q = (k * k + v * v) * half + eps;
+  const f2 iq = rsq2(q);
+  const f2 iqe = rcp2(q + eps);
+  const f2 d_zn = gh * (hprev - c) * zg * (one - zg) * (irc * irc * irc);
+  o[0] = -d_zn * z * r * half;
+  o[1] = d_zn * (r * r * half + eps);
+  const f2 d_kv = gs * alp;
+  const f2 f = iq * iq * iqe;
+  const f2 fp = -(q + q + eps) * f * f;
+  o[2] = d_kv * v * (f + k * k * fp);
+  o[3] = d_kv * k * (f + v * v * fp);
+  o[4] = dpre * eps * (irh * irh * irh);
+  o[5] = gs * sprev * dec * (one - dec) * eps * (ird * ird * ird);
+  o[6] = gs * (k * v * f) * alp * (one - alp) * eps * (ira * ira * ira);
+}
+
 // Cross-wave composition of the per-wave affine segment maps m_q = (a, b): x -> a x + b, read
 // from LDS.  prefix: x <- m_{w-1} o ... o m_0 (x); suffix: x <- m_{w+1} o ... o m_{NW-1} (x)
 // (reverse time).  Work stays proportional to the wave's position (the chain runs only over
@@ -465,32 +498,47 @@ lucy_scan_bwd_kernel(ScanBwdArgs a) {
     }
     float Cs = carGs[it & 1][lane];
     if (!(SC_ABL & 4)) Cs = compose_suffix<NW>(aggD, lane, w, Cs);
+    float gsj[LC], dpj[LC];
 #pragma unroll
-    for (int j = LC - 1; j >= 0; --j) {
-      const float dpre = u[j] * (1.0f - zg[j]) * (1.0f - x[j] * x[j]);
-      const float gs = dpre + Cs;
-      Cs = dec[j] * gs;
-      if (dok && t0 + j < a.T) {
-        float o[7], g7[7];
+    for (int j = LC - 1; j >= 0; --j) {   // the serial part of the Gs scan
+      dpj[j] = u[j] * (1.0f - zg[j]) * (1.0f - x[j] * x[j]);
+      gsj[j] = dpj[j] + Cs;
+      Cs = dec[j] * gsj[j];
+    }
+    // gate gradients, two steps per packed instruction
 #pragma unroll
-        for (int g = 0; g < 7; ++g) {
-          if constexpr (NBUF == 1) g7[g] = rg[j][g];
-          else g7[g] = E::ld(L::get(slot, (j * 7 + g) * 64 + lane)) + gb[g];
-        }
-        if (SC_ABL & 1) {
+    for (int jp = 0; jp < LC; jp += 2) {
+      f2 g7[7], o[7];
 #pragma unroll
-          for (int g = 0; g < 7; ++g) o[g] = g7[g] * gs + hv[j] * sv[j];
+      for (int g = 0; g < 7; ++g) {
+        if constexpr (NBUF == 1) {
+          g7[g] = f2{rg[jp][g], rg[jp + 1][g]};
         } else {
-          gate_grads(g7[0], g7[1], g7[2], g7[3], g7[4], g7[5], g7[6], zg[j], dec[j], u[j], dpre,
-                     gs, hv[j], sv[j], x[j], o);
+          g7[g] = f2{E::ld(L::get(slot, (jp * 7 + g) * 64 + lane)),
+                     E::ld(L::get(slot, ((jp + 1) * 7 + g) * 64 + lane))} + gb[g];
         }
-        const uint32_t so = (uint32_t)((t0 + j) * a.dg_td * sizeof(T));
+      }
+      if (SC_ABL & 1) {
 #pragma unroll
-        for (int g = 0; g < 7; ++g) {
-          const T og = E::st(o[g]);
-          if constexpr (WST) ((T*)slot)[(j * 7 + g) * 64 + lane] = og;   // over its raw gate
-          else if (!(SC_ABL & 2)) dgbuf.st(og, vo, so + (uint32_t)(g * a.dg_cd * sizeof(T)));
-          bacc[g] += E::ld(og);   // sum what is stored, so db == dgates.sum() exactly as a GEMM sees it
+        for (int g = 0; g < 7; ++g) o[g] = g7[g] * f2{gsj[jp], gsj[jp + 1]};
+      } else {
+        gate_grads2(g7[0], g7[1], g7[2], g7[3], g7[4], g7[5], g7[6], f2{zg[jp], zg[jp + 1]},
+                    f2{dec[jp], dec[jp + 1]}, f2{u[jp], u[jp + 1]}, f2{dpj[jp], dpj[jp + 1]},
+                    f2{gsj[jp], gsj[jp + 1]}, f2{hv[jp], hv[jp + 1]}, f2{sv[jp], sv[jp + 1]},
+                    f2{x[jp], x[jp + 1]}, o);
+      }
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const int j = jp + h2;
+        if (dok && t0 + j < a.T) {
+          const uint32_t so = (uint32_t)((t0 + j) * a.dg_td * sizeof(T));
+#pragma unroll
+          for (int g = 0; g < 7; ++g) {
+            const T og = E::st(h2 ? o[g].y : o[g].x);
+            if constexpr (WST) ((T*)slot)[(j * 7 + g) * 64 + lane] = og;   // over its raw gate
+            else if (!(SC_ABL & 2)) dgbuf.st(og, vo, so + (uint32_t)(g * a.dg_cd * sizeof(T)));
+            bacc[g] += E::ld(og);   // sum what is stored: db == dgates.sum() as a GEMM sees it
+          }
         }
       }
     }
