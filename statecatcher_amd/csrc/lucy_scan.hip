@@ -113,6 +113,25 @@ __device__ __forceinline__ void step_terms(float r, float z, float k, float v, f
   u = alp * kv;
 }
 
+typedef float f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2 rsq2(f2 x) { return f2{rsq(x.x), rsq(x.y)}; }
+__device__ __forceinline__ f2 rcp2(f2 x) { return f2{rcp(x.x), rcp(x.y)}; }
+__device__ __forceinline__ f2 sigm2(f2 x) { return f2{sigm(x.x), sigm(x.y)}; }
+
+// step_terms for two steps at once (packed fp32 for the elementwise math)
+__device__ __forceinline__ void step_terms2(f2 r, f2 z, f2 k, f2 v, f2 hp, f2 dc, f2 al, f2& zg,
+                                            f2& dec, f2& u, f2& hn) {
+  const f2 eps = {kEps, kEps}, half = {0.5f, 0.5f};
+  const f2 rc2 = (r * r + z * z) * half + eps;
+  const f2 q = (k * k + v * v) * half + eps;
+  zg = sigm2(z * rsq2(rc2));
+  dec = sigm2(dc * rsq2(dc * dc + eps));
+  const f2 alp = sigm2(al * rsq2(al * al + eps));
+  hn = hp * rsq2(hp * hp + eps);
+  const f2 iq = rsq2(q);
+  u = alp * ((k * iq) * (v * iq) * rcp2(q + eps));
+}
+
 __device__ __forceinline__ float tanh_sig(float x) { return sigm(2.0f * x) * 2.0f - 1.0f; }
 
 // Gradient of one step w.r.t. its 7 raw gates, given the step's adjoints.
@@ -149,10 +168,6 @@ __device__ __forceinline__ void gate_grads(float r, float z, float k, float v, f
 
 // gate_grads for two steps at once: the elementwise math runs as packed fp32 (v_pk_fma_f32 /
 // v_pk_mul_f32 on two steps per instruction); the transcendentals stay per component.
-typedef float f2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ f2 rsq2(f2 x) { return f2{rsq(x.x), rsq(x.y)}; }
-__device__ __forceinline__ f2 rcp2(f2 x) { return f2{rcp(x.x), rcp(x.y)}; }
-__device__ __forceinline__ f2 sigm2(f2 x) { return f2{sigm(x.x), sigm(x.y)}; }
 
 __device__ __forceinline__ void gate_grads2(f2 r, f2 z, f2 k, f2 v, f2 hp, f2 dc, f2 al, f2 zg,
                                             f2 dec, f2 gh, f2 dpre, f2 gs, f2 hprev, f2 sprev,
@@ -289,13 +304,20 @@ lucy_scan_fwd_kernel(ScanFwdArgs a) {
       for (int g = 0; g < 7; ++g) gv[j][g] = E::ld(L::get(slot, (j * 7 + g) * 64 + lane)) + gb[g];
     lds_read_wait();              // slot consumed: it may be refilled with super-chunk k+1
     if (k + 1 < a.nsc) issue(k + 1);
+#pragma unroll
+    for (int j = 0; j < LC; j += 2) {   // two steps per packed instruction
+      f2 z2, d2, u2, x2;
+      step_terms2(f2{gv[j][0], gv[j + 1][0]}, f2{gv[j][1], gv[j + 1][1]},
+                  f2{gv[j][2], gv[j + 1][2]}, f2{gv[j][3], gv[j + 1][3]},
+                  f2{gv[j][4], gv[j + 1][4]}, f2{gv[j][5], gv[j + 1][5]},
+                  f2{gv[j][6], gv[j + 1][6]}, z2, d2, u2, x2);
+      zg[j] = z2.x; zg[j + 1] = z2.y; dec[j] = d2.x; dec[j + 1] = d2.y;
+      u[j] = u2.x; u[j + 1] = u2.y; x[j] = x2.x; x[j + 1] = x2.y;
+    }
     float As = 1.0f, Bs = 0.0f;
 #pragma unroll
     for (int j = 0; j < LC; ++j) {
-      if (t0 + j < a.T) {
-        step_terms(gv[j][0], gv[j][1], gv[j][2], gv[j][3], gv[j][4], gv[j][5], gv[j][6], zg[j],
-                   dec[j], u[j], x[j]);
-      } else {  // identity step past the end of the sequence
+      if (t0 + j >= a.T) {   // identity step past the end of the sequence
         zg[j] = 1.0f; dec[j] = 1.0f; u[j] = 0.0f; x[j] = 0.0f;
       }
       As *= dec[j];
@@ -426,19 +448,28 @@ lucy_scan_bwd_kernel(ScanBwdArgs a) {
     float zg[LC], dec[LC], u[LC], x[LC], dj[LC], sv[LC], hv[LC];
     float rg[NBUF == 1 ? LC : 1][7];
     // ---- recompute the forward of this super-chunk ----
+#pragma unroll
+    for (int j = 0; j < LC; j += 2) {   // two steps per packed instruction
+      f2 g7[7];
+#pragma unroll
+      for (int g = 0; g < 7; ++g) {
+        g7[g] = f2{E::ld(L::get(slot, (j * 7 + g) * 64 + lane)),
+                   E::ld(L::get(slot, ((j + 1) * 7 + g) * 64 + lane))} + gb[g];
+        if constexpr (NBUF == 1) {
+          rg[j][g] = g7[g].x;
+          rg[j + 1][g] = g7[g].y;
+        }
+      }
+      f2 z2, d2, u2, x2;
+      step_terms2(g7[0], g7[1], g7[2], g7[3], g7[4], g7[5], g7[6], z2, d2, u2, x2);
+      zg[j] = z2.x; zg[j + 1] = z2.y; dec[j] = d2.x; dec[j + 1] = d2.y;
+      u[j] = u2.x; u[j + 1] = u2.y; x[j] = x2.x; x[j + 1] = x2.y;
+    }
     float As = 1.0f, Bs = 0.0f;
 #pragma unroll
     for (int j = 0; j < LC; ++j) {
-      float g7[7];
-#pragma unroll
-      for (int g = 0; g < 7; ++g) {
-        g7[g] = E::ld(L::get(slot, (j * 7 + g) * 64 + lane)) + gb[g];
-        if constexpr (NBUF == 1) rg[j][g] = g7[g];
-      }
       dj[j] = (t0 + j < a.T) ? E::ld(L::get(slot, (GROWS + j) * 64 + lane)) : 0.0f;
-      if (t0 + j < a.T) {
-        step_terms(g7[0], g7[1], g7[2], g7[3], g7[4], g7[5], g7[6], zg[j], dec[j], u[j], x[j]);
-      } else {
+      if (t0 + j >= a.T) {
         zg[j] = 1.0f; dec[j] = 1.0f; u[j] = 0.0f; x[j] = 0.0f;
       }
       As *= dec[j];
