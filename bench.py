@@ -45,7 +45,8 @@ def parse():
     ap.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16")
     ap.add_argument("--bucket-mb", type=float, default=50.0)
     ap.add_argument("--cpu-baseline", choices=["on", "off"], default="on")
-    ap.add_argument("--cpu-seq", type=int, default=300, help="T of the bounded CPU sample")
+    ap.add_argument("--cpu-seq", type=int, default=1500,
+                    help="T of the bounded CPU sample (default: one full C2 segment, ~10 s)")
     ap.add_argument("--tunableop", choices=["on", "off"], default="on",
                     help="use the shipped PyTorch TunableOp GEMM table (statecatcher_amd/tuning)")
     ap.add_argument("--tune-out", default=None,
