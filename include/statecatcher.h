@@ -21,6 +21,9 @@
  *   sc_ctc_*          <- ATen ctc_loss behind nn.CTCLoss(blank=0, zero_infinity=True),
  *                        train.py:142 / model.py:68-71
  *   sc_ctc_greedy_decode <- decoder.py:3-30 `ctc_greedy_decoder`
+ *   sc_ctc_greedy_step   <- decoder.py:3-30 applied one frame at a time (streaming)
+ *   sc_lucy_step_*    <- the native LucyRNN's infer-mode frame loop, lucyrnn.py:172-184, i.e.
+ *                        LucyRNNCell.forward (lucyrnn.py:44-70) at T = 1 (streaming decode)
  *   sc_mlstm_*        <- the xLSTM encoder's mLSTM cell (model.py:214-229, :301-307; fork kernels
  *                        "chunkwise--native_autograd", train.py:643-645), math as
  *                        transformers/models/xlstm/modeling_xlstm.py:74-386 (parity vs the fork
@@ -192,6 +195,47 @@ int sc_ctc_bwd(const void* x, int x_dtype, int is_logits, int B, int T, int V,
 int sc_ctc_greedy_decode(const void* log_probs, int dtype, int B, int T, int V,
                          int64_t stride_b, int64_t stride_t, const int64_t* lengths, int blank,
                          int32_t* tokens, int32_t* counts, void* stream);
+
+/*
+ * decoder.py:3-30 for ONE frame of B streams (streaming decode): tok = argmax of logits row b
+ * (same tie/NaN rule); emit[b*emit_stride] = tok if the frame is live (mask null or mask[b] != 0)
+ * and tok != blank and tok != prev[b], else -1; prev[b] = tok for live frames (start streams
+ * with prev = -1, decoder.py's prev_token = None).  logits row stride stride_b (elements).
+ */
+int sc_ctc_greedy_step(const void* logits, int dtype, int B, int V, int64_t stride_b,
+                       const float* mask, int blank, int32_t* prev, int32_t* emit,
+                       int64_t emit_stride, void* stream);
+
+/* ---------------------------------------------------------------- streaming LucyRNN step -- */
+
+/*
+ * Native LucyRNN, infer mode, one frame (lucyrnn.py:172-184 -> LucyRNNCell.forward :44-70).
+ * Per layer the caller runs a = input_proj(x) (GEMM), sc_lucy_step_ln (layernorm_in), the gate
+ * GEMM, then sc_lucy_step_cell.  State h, s: fp32 [B,D] contiguous, updated in place.  All other
+ * activations share `dtype` (f32/bf16/f16), rows contiguous except g (row stride g_stride).
+ * 1 <= D <= 1024.  LayerNorm eps as given (nn.LayerNorm: 1e-5).
+ */
+int sc_lucy_step_supported(int dtype, int D);
+
+/* y = LayerNorm(x; w, b) per row of D (layernorm_in, lucyrnn.py:45). */
+int sc_lucy_step_ln(const void* x, int dtype, const float* w, const float* b, float eps, void* y,
+                    int B, int D, void* stream);
+
+/*
+ * mode 0 (fused_ops, :47-54):  g = [z | k | v | h_pre | decay_logits] (5D per row; the
+ *   reference's r chunk is computed and never used, so the caller drops W_fused's first D rows);
+ *   s' = sigmoid(dl) s + k v;  c = tanh(LN_h(h_pre + s'));  h' = (1 - z~) c + z~ h with
+ *   z~ = sigmoid(LN_z(z));  masked blend (:66-68) with mask[b];  out = new h.
+ * mode 1 (unfused, :55-60):  g = [W_z u | W_k u | W_v u | W_decay u];  s updated as above;
+ *   out = u + s' (the input of W_h).
+ * mode 2 (unfused, :61-68):  hp = W_h(u + s');  c = tanh(LN_h(hp));  z~ from g as in mode 0;
+ *   h updated and masked;  out = new h.
+ * LayerNorm pointers null = layer_norm False (nn.Identity).  mask: fp32 [B] or null.
+ */
+int sc_lucy_step_cell(int mode, const void* g, int dtype, int64_t g_stride, const void* u,
+                      const void* hp, const float* lnz_w, const float* lnz_b, const float* lnh_w,
+                      const float* lnh_b, float eps, float* h, float* s, void* out,
+                      const float* mask, int B, int D, void* stream);
 
 /* ---------------------------------------------------------------- mLSTM ----------------- */
 

@@ -7,6 +7,11 @@
 //                          64-lane (value, index) reduction that keeps the lower index on ties
 //   greedy_collapse_kernel one workgroup per b: keep[t] = t < len && tok != blank &&
 //                          tok != tok[t-1]; workgroup prefix sum of keep; compacted write.
+// and, for streaming (one frame per call, statecatcher_amd/streaming.py):
+//   greedy_step_kernel     one wave per stream: the same argmax, then the collapse against the
+//                          stream's previous frame (prev[b], -1 at stream start as decoder.py's
+//                          prev_token = None); emits the token or -1.  Masked frames (mask 0,
+//                          past the stream's length) emit -1 and leave prev unchanged.
 #include "sc_common.h"
 
 namespace sc {
@@ -28,17 +33,13 @@ __device__ __forceinline__ bool beats(float va, int ia, float vb, int ib) {
   return ia < ib;
 }
 
+// argmax of one row by one wave (first maximal index, NaN maximal); the result in every lane
 template <int DT>
-__global__ void __launch_bounds__(256) greedy_argmax_kernel(GreedyArgs a) {
+__device__ __forceinline__ int wave_argmax(const typename Elem<DT>::T* p, int V, int lane) {
   using E = Elem<DT>;
-  const int lane = threadIdx.x & 63;
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= (int64_t)a.B * a.T) return;
-  const int b = (int)(row / a.T), t = (int)(row % a.T);
-  const typename E::T* p = (const typename E::T*)a.x + (int64_t)b * a.sb + (int64_t)t * a.st;
   float bv = -__builtin_huge_valf();
   int bi = 0x7fffffff;
-  for (int v = lane; v < a.V; v += 64) {
+  for (int v = lane; v < V; v += 64) {
     const float xv = E::ld(p[v]);
     if (bi == 0x7fffffff || beats(xv, v, bv, bi)) {
       bv = xv;
@@ -54,7 +55,42 @@ __global__ void __launch_bounds__(256) greedy_argmax_kernel(GreedyArgs a) {
       bi = oi;
     }
   }
-  if (lane == 0) a.tokens[row] = bi;
+  return bi;
+}
+
+template <int DT>
+__global__ void __launch_bounds__(256) greedy_argmax_kernel(GreedyArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= (int64_t)a.B * a.T) return;
+  const int b = (int)(row / a.T), t = (int)(row % a.T);
+  const int tok = wave_argmax<DT>(
+      (const typename Elem<DT>::T*)a.x + (int64_t)b * a.sb + (int64_t)t * a.st, a.V, lane);
+  if (lane == 0) a.tokens[row] = tok;
+}
+
+struct GreedyStepArgs {
+  const void* x;
+  int B, V, blank;
+  int64_t sb;
+  const float* mask;
+  int32_t* prev;
+  int32_t* emit;
+  int64_t emit_stride;
+};
+
+template <int DT>
+__global__ void __launch_bounds__(256) greedy_step_kernel(GreedyStepArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= a.B) return;
+  const int tok = wave_argmax<DT>((const typename Elem<DT>::T*)a.x + (int64_t)b * a.sb, a.V, lane);
+  if (lane == 0) {
+    const bool live = !a.mask || a.mask[b] != 0.0f;
+    const int pv = a.prev[b];
+    a.emit[(int64_t)b * a.emit_stride] = (live && tok != a.blank && tok != pv) ? tok : -1;
+    if (live) a.prev[b] = tok;
+  }
 }
 
 __global__ void __launch_bounds__(1024) greedy_collapse_kernel(GreedyArgs a) {
@@ -130,4 +166,24 @@ extern "C" int sc_ctc_greedy_decode(const void* log_probs, int dtype, int B, int
     default: launch<SC_F16>(a, st); break;
   }
   return launch_status("sc_ctc_greedy_decode");
+}
+
+extern "C" int sc_ctc_greedy_step(const void* logits, int dtype, int B, int V, int64_t stride_b,
+                                  const float* mask, int blank, int32_t* prev, int32_t* emit,
+                                  int64_t emit_stride, void* stream) {
+  clear_error();
+  SC_REQUIRE(dtype == SC_F32 || dtype == SC_BF16 || dtype == SC_F16,
+             "sc_ctc_greedy_step: unsupported dtype %d", dtype);
+  SC_REQUIRE(B >= 0 && V > 0, "sc_ctc_greedy_step: bad shape");
+  if (B == 0) return 0;
+  SC_REQUIRE(logits && prev && emit, "sc_ctc_greedy_step: null pointer");
+  GreedyStepArgs a{logits, B, V, blank, stride_b, mask, prev, emit, emit_stride};
+  const dim3 grid((unsigned)((B + 3) / 4));
+  hipStream_t st = (hipStream_t)stream;
+  switch (dtype) {
+    case SC_F32: hipLaunchKernelGGL(greedy_step_kernel<SC_F32>, grid, dim3(256), 0, st, a); break;
+    case SC_BF16: hipLaunchKernelGGL(greedy_step_kernel<SC_BF16>, grid, dim3(256), 0, st, a); break;
+    default: hipLaunchKernelGGL(greedy_step_kernel<SC_F16>, grid, dim3(256), 0, st, a); break;
+  }
+  return launch_status("sc_ctc_greedy_step");
 }

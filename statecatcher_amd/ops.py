@@ -406,6 +406,49 @@ def ctc_greedy_decode(log_probs, lengths, blank=0):
     return tokens, counts
 
 
+def ctc_greedy_step(logits, prev, emit, mask=None, blank=0):
+    """One streaming frame of decoder.py:3-30 for B streams, in place: logits [B,V] (unit inner
+    stride), prev int32 [B] (-1 = stream start), emit int32 view [B] (any stride) <- token or -1.
+    mask fp32 [B] or None (0 = frame past the stream's end: emits -1, prev kept)."""
+    require_device(logits, prev, emit)
+    B, V = logits.shape
+    if logits.stride(1) != 1 or prev.dtype != torch.int32 or emit.dtype != torch.int32:
+        raise ValueError("ctc_greedy_step: logits need unit inner stride, prev/emit int32")
+    if prev.numel() != B or emit.numel() != B or not prev.is_contiguous():
+        raise ValueError("ctc_greedy_step: prev/emit must hold B entries (prev contiguous)")
+    if mask is not None and (mask.dtype != torch.float32 or mask.numel() != B or mask.stride(0) != 1):
+        raise ValueError("ctc_greedy_step: mask must be contiguous fp32 [B]")
+    rc = _lib.load().sc_ctc_greedy_step(ptr(logits), dtype_code(logits), B, V, logits.stride(0),
+                                        ptr(mask), int(blank), ptr(prev), ptr(emit),
+                                        emit.stride(0), stream_of(logits))
+    check(rc, "sc_ctc_greedy_step")
+
+
+# ------------------------------------------------------------------- streaming LucyRNN step --
+STEP_FUSED, STEP_UNFUSED_A, STEP_UNFUSED_B = 0, 1, 2
+
+
+def lucy_step_ln(x, w, b, out, eps=1e-5):
+    """out = LayerNorm(x) rows of D (layernorm_in, lucyrnn.py:45), no allocation."""
+    B, D = x.shape
+    rc = _lib.load().sc_lucy_step_ln(ptr(x), dtype_code(x), ptr(w), ptr(b), float(eps), ptr(out),
+                                     B, D, stream_of(x))
+    check(rc, "sc_lucy_step_ln")
+
+
+def lucy_step_cell(mode, g, h, s, out, lnz=None, lnh=None, u=None, hp=None, mask=None, eps=1e-5):
+    """One LucyRNNCell step (lucyrnn.py:44-70) on GEMM outputs, state h/s fp32 [B,D] in place
+    (include/statecatcher.h sc_lucy_step_cell for the three modes).  lnz/lnh: (weight, bias)
+    fp32 or None (layer_norm=False).  No allocation: safe inside a hipGraph capture."""
+    B, D = h.shape
+    lzw, lzb = lnz if lnz is not None else (None, None)
+    lhw, lhb = lnh if lnh is not None else (None, None)
+    rc = _lib.load().sc_lucy_step_cell(int(mode), ptr(g), dtype_code(g), g.stride(0), ptr(u),
+                                       ptr(hp), ptr(lzw), ptr(lzb), ptr(lhw), ptr(lhb), float(eps),
+                                       ptr(h), ptr(s), ptr(out), ptr(mask), B, D, stream_of(g))
+    check(rc, "sc_lucy_step_cell")
+
+
 # ----------------------------------------------------------------------------- RNN-T ---------
 class RNNTFn(torch.autograd.Function):
     """nll [B] fp32 of the RNN-T lattice (rnnt.hip) over x: dense [B,T,U+1,V] or compact

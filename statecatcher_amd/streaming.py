@@ -1,0 +1,190 @@
+"""Streaming (frame-synchronous) decode of a native LucyRNN with fused greedy CTC — SURVEY §8(f)
+row 2.
+
+The reference's streaming path is the infer-mode loop of lucyrnn.py:172-184: for every frame,
+every layer runs ``LucyRNNCell.forward`` (lucyrnn.py:44-70) on the previous layer's h, then
+``output_proj`` (:186), and decoding is decoder.py:3-30 (argmax, collapse repeats, drop blanks)
+over the finished sequence.  Here a frame is:
+
+    per layer:  a = input_proj(x)             library GEMM (hipBLASLt)
+                u = LayerNorm_in(a)           sc_lucy_step_ln      (csrc/lucy_step.hip)
+                g = gate projection(u)        library GEMM; fused: W_fused minus the dead r rows
+                h, s <- cell(g, h, s)         sc_lucy_step_cell    (+ W_h GEMM + a second cell
+                                                                    stage when fused_ops=False)
+    logits = output_proj(h_L)                 library GEMM
+    emit   = greedy step(logits, prev)        sc_ctc_greedy_step   (csrc/decode.hip)
+
+with h, s resident on the GPU in fp32 between calls and every buffer static, so one block of
+``frames_per_call`` frames is captured once as a hipGraph (torch.cuda.CUDAGraph) and replayed:
+one host launch per block instead of ~(4-6 L + 2) kernel launches per frame.
+
+The decode is incremental: ``prev`` holds each stream's last argmax (-1 at stream start, as
+decoder.py's ``prev_token = None``), and emit[b, t] is the token decoder.py would append at
+frame t, or -1.  Frames with mask 0 (past a stream's end) keep state (lucyrnn.py:66-68) and
+emit nothing.
+"""
+import torch
+
+from . import ops
+from .lucyrnn import LucyRNN
+
+
+def _ln_params(mod, on):
+    return (mod.weight.detach().float().contiguous(), mod.bias.detach().float().contiguous()) \
+        if on else None
+
+
+class StreamingLucyRNN:
+    """Decode ``batch`` concurrent streams through ``model`` (a native LucyRNN; its weights are
+    snapshotted at construction) ``frames_per_call`` model frames per call.
+
+    dtype: activation/weight dtype of the GEMMs (fp32 = the reference's arithmetic; bf16 for
+    throughput); state is fp32 either way.  graph: capture the block as a hipGraph.
+    """
+
+    def __init__(self, model: LucyRNN, batch: int, frames_per_call: int = 1,
+                 dtype=torch.float32, blank: int = 0, graph: bool = True):
+        cfg = model.config
+        dev = next(model.parameters()).device
+        ops._lib.require_device(next(model.parameters()))
+        self.cfg, self.B, self.K, self.dtype, self.blank = cfg, batch, frames_per_call, dtype, blank
+        self.L, self.D, self.V = cfg.num_layers, cfg.hidden_dim, cfg.vocab_size
+        self.Din = cfg.input_dim * cfg.stack_order
+        D, B, K = self.D, batch, frames_per_call
+        if not ops._lib.load().sc_lucy_step_supported(ops.dtype_code(torch.empty(0, dtype=dtype)), D):
+            raise ValueError(f"streaming step: hidden_dim {D} / dtype {dtype} unsupported")
+        w = lambda t: t.detach().to(dtype).contiguous()   # noqa: E731
+        ln = cfg.layer_norm
+        self.layers = []
+        for cell in model.layers:
+            e = {"w_in": w(cell.input_proj.weight), "b_in": w(cell.input_proj.bias),
+                 "ln_in": _ln_params(cell.layernorm_in, ln), "lnz": _ln_params(cell.layernorm_z, ln),
+                 "lnh": _ln_params(cell.layernorm_h, ln)}
+            if cfg.fused_ops:
+                # rows [0, D) are r: sigmoid(LN_r(r)) is computed by the reference and never used
+                e["w_g"], e["b_g"] = w(cell.W_fused.weight[D:]), w(cell.W_fused.bias[D:])
+            else:
+                mods = (cell.W_z, cell.W_k, cell.W_v, cell.W_decay)
+                e["w_g"] = w(torch.cat([m.weight for m in mods]))
+                e["b_g"] = w(torch.cat([m.bias for m in mods]))
+                e["w_h"], e["b_h"] = w(cell.W_h.weight), w(cell.W_h.bias)
+            self.layers.append(e)
+        self.w_out, self.b_out = w(model.output_proj.weight), w(model.output_proj.bias)
+        z = lambda *s, dt=dtype: torch.zeros(*s, dtype=dt, device=dev)   # noqa: E731
+        ng = 5 if cfg.fused_ops else 4
+        self.x = z(K, B, self.Din)
+        self.mask = torch.ones(K, B, dtype=torch.float32, device=dev)
+        self.a, self.u, self.g = z(B, D), z(B, D), z(B, ng * D)
+        self.y, self.hp = z(B, D), z(B, D)
+        self.xo = [z(B, D) for _ in range(self.L)]
+        self.h = [z(B, D, dt=torch.float32) for _ in range(self.L)]
+        self.s = [z(B, D, dt=torch.float32) for _ in range(self.L)]
+        self.logits = z(K, B, self.V)
+        self.emit = torch.full((K, B), -1, dtype=torch.int32, device=dev)
+        self.prev = torch.full((B,), -1, dtype=torch.int32, device=dev)
+        self.graph = None
+        if graph:
+            self._capture()
+        self.reset()
+
+    # ------------------------------------------------------------------------------ frame --
+    def _frame(self, j):
+        cfg, m = self.cfg, self.mask[j]
+        inp = self.x[j]
+        for l, e in enumerate(self.layers):
+            torch.addmm(e["b_in"], inp, e["w_in"].t(), out=self.a)
+            u = self.a
+            if e["ln_in"] is not None:
+                ops.lucy_step_ln(self.a, *e["ln_in"], self.u)
+                u = self.u
+            torch.addmm(e["b_g"], u, e["w_g"].t(), out=self.g)
+            if cfg.fused_ops:
+                ops.lucy_step_cell(ops.STEP_FUSED, self.g, self.h[l], self.s[l], self.xo[l],
+                                   e["lnz"], e["lnh"], mask=m)
+            else:
+                ops.lucy_step_cell(ops.STEP_UNFUSED_A, self.g, self.h[l], self.s[l], self.y,
+                                   e["lnz"], e["lnh"], u=u, mask=m)
+                torch.addmm(e["b_h"], self.y, e["w_h"].t(), out=self.hp)
+                ops.lucy_step_cell(ops.STEP_UNFUSED_B, self.g, self.h[l], self.s[l], self.xo[l],
+                                   e["lnz"], e["lnh"], hp=self.hp, mask=m)
+            inp = self.xo[l]
+        torch.addmm(self.b_out, inp, self.w_out.t(), out=self.logits[j])
+        ops.ctc_greedy_step(self.logits[j], self.prev, self.emit[j], mask=m, blank=self.blank)
+
+    def _block(self):
+        for j in range(self.K):
+            self._frame(j)
+
+    def _capture(self):
+        side = torch.cuda.Stream(self.x.device)
+        side.wait_stream(torch.cuda.current_stream(self.x.device))
+        with torch.cuda.stream(side):   # warm-up: library workspaces, kernel loading
+            self._block()
+        torch.cuda.current_stream(self.x.device).wait_stream(side)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self._block()
+
+    # ------------------------------------------------------------------------------- API ---
+    def reset(self, hidden_states=None, streams=None):
+        """Start streams afresh: state from ``hidden_states`` ((h list, s list) of [B,D], as the
+        reference's forward takes) or zero, prev token = none.  ``streams``: index tensor/list
+        of the streams to reset (default all)."""
+        idx = slice(None) if streams is None else torch.as_tensor(streams, device=self.x.device)
+        for l in range(self.L):
+            for buf, src in ((self.h[l], None if hidden_states is None else hidden_states[0][l]),
+                             (self.s[l], None if hidden_states is None else hidden_states[1][l])):
+                if src is None:
+                    buf[idx] = 0.0
+                else:
+                    buf[idx] = src.to(buf.device, torch.float32)[idx]
+        self.prev[idx] = -1
+
+    def state(self):
+        """(h list, s list) fp32 copies — the reference's (h, s) return (lucyrnn.py:188-189)."""
+        return [t.clone() for t in self.h], [t.clone() for t in self.s]
+
+    def step(self, x, mask=None):
+        """Advance every stream by K = frames_per_call model frames.  x [B, K, input_dim *
+        stack_order] (already stacked); mask [B, K] (bool/float, None = all live).  Returns
+        emit int32 [B, K] on the device: the token decoder.py appends at that frame, or -1.
+        The logits of the block stay in ``self.logits`` ([K, B, V])."""
+        self.x.copy_(x.transpose(0, 1))
+        if mask is None:
+            self.mask.fill_(1.0)
+        else:
+            self.mask.copy_(mask.transpose(0, 1))
+        if self.graph is not None:
+            self.graph.replay()
+        else:
+            self._block()
+        return self.emit.t()
+
+    def decode(self, feats, masks=None, return_logits=False):
+        """Whole utterances through the streaming path: feats [B, T, input_dim] raw frames,
+        stacked as the model does (lucyrnn.py:92-99: the tail T % stack_order is dropped, a
+        stacked frame is live when all its frames are).  Returns the decoder.py token lists
+        (and logits [B, T', V] if asked).  One host sync at the end."""
+        B, T, F = feats.shape
+        k = self.cfg.stack_order
+        Tt = T - T % k
+        x = feats[:, :Tt].reshape(B, Tt // k, F * k)
+        m = None
+        if masks is not None:
+            m = masks.reshape(B, -1)[:, :Tt].reshape(B, Tt // k, k).all(-1).float()
+        T2 = x.shape[1]
+        emits, logits = [], []
+        for t0 in range(0, T2, self.K):
+            n = min(self.K, T2 - t0)
+            xb = torch.zeros(B, self.K, x.shape[2], dtype=self.dtype, device=self.x.device)
+            xb[:, :n] = x[:, t0:t0 + n]
+            mb = torch.zeros(B, self.K, device=self.x.device)   # padding frames are masked out
+            mb[:, :n] = 1.0 if m is None else m[:, t0:t0 + n]
+            emits.append(self.step(xb, mb)[:, :n].clone())
+            if return_logits:
+                logits.append(self.logits[:n].transpose(0, 1).clone())
+        em = torch.cat(emits, 1).cpu() if emits else torch.zeros(B, 0, dtype=torch.int32)
+        toks = [[int(t) for t in row if t >= 0] for row in em]
+        if return_logits:
+            return toks, torch.cat(logits, 1) if logits else None
+        return toks

@@ -1,0 +1,182 @@
+"""GPU parity of the streaming LucyRNN step + fused greedy decode (statecatcher_amd/streaming.py,
+csrc/lucy_step.hip, sc_ctc_greedy_step in csrc/decode.hip) — SURVEY §8(f) row 2.
+
+* the reference's own infer-mode outputs (tests/golden/native.npz, lucyrnn.LucyRNN run with
+  is_training=False: fused/unfused, LayerNorm on/off, frame stacking, carried state) replayed
+  frame by frame: logits and final (h, s) at fp32 tolerance 1e-4 relative;
+* larger random models against the numpy oracle's cell loop (oracle/native.py, lucyrnn.py:44-70)
+  with ragged frame masks, every (fused, layer_norm) combination, hipGraph on and off, 1 and 4
+  frames per call;
+* tokens: bit-exact with oracle/decode.py (decoder.py:3-30) applied to the same logits.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import decode as odec
+from oracle import native as onat
+from tests.conftest import load_golden
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0") if torch.cuda.is_available() else None
+
+
+def close(got, ref, rtol=1e-4, afrac=1e-5):
+    got = got.detach().double().cpu().numpy() if isinstance(got, torch.Tensor) else got
+    np.testing.assert_allclose(got, ref, rtol=rtol, atol=afrac * max(np.abs(ref).max(), 1e-30))
+
+
+def golden_model(z, name):
+    import statecatcher_amd as sc
+    train, fused, ln, prefix, stack, carry = [int(v) for v in z[name + "/cfg"]]
+    cfg = sc.LucyRNNConfig(input_dim=12, hidden_dim=16, num_layers=2, vocab_size=10,
+                           kernel_impl="native", is_training=False, fused_ops=bool(fused),
+                           layer_norm=bool(ln), stack_order=stack)
+    m = sc.LucyRNN(cfg)
+    m.load_state_dict({k[len(name) + 7:]: torch.as_tensor(z[k]) for k in z.files
+                       if k.startswith(name + "/param/")})
+    return m.to(DEV), bool(carry)
+
+
+@pytest.mark.parametrize("name", ["infer_carry", "infer_ln0", "infer_ln1", "infer_stack2",
+                                  "infer_unfused"])
+@pytest.mark.parametrize("K,graph", [(1, True), (4, True), (3, False)])
+def test_streaming_vs_reference_infer_golden(name, K, graph):
+    from statecatcher_amd.streaming import StreamingLucyRNN
+    z = load_golden("native")
+    m, carry = golden_model(z, name)
+    st = StreamingLucyRNN(m, batch=2, frames_per_call=K, graph=graph)
+    if carry:
+        st.reset(([torch.as_tensor(t) for t in z[name + "/h0"]],
+                  [torch.as_tensor(t) for t in z[name + "/s0"]]))
+    toks, logits = st.decode(torch.as_tensor(z[name + "/x"]).to(DEV), return_logits=True)
+    close(logits, z[name + "/logits"])
+    h, s = st.state()
+    close(torch.stack(h), z[name + "/h"])
+    close(torch.stack(s), z[name + "/s"])
+    lg = logits.cpu().numpy()
+    assert toks == odec.ctc_greedy(lg, [lg.shape[1]] * 2)
+
+
+def oracle_params(m):
+    return {k: v.detach().double().cpu().numpy() for k, v in m.state_dict().items()}
+
+
+def oracle_stream(p, x, masks, L, fused, ln):
+    """lucyrnn.py:172-186 frame loop with the per-frame mask blend of :66-68."""
+    B, T, _ = x.shape
+    D = p["layers.0.input_proj.weight"].shape[0]
+    h = [np.zeros((B, D)) for _ in range(L)]
+    s = [np.zeros((B, D)) for _ in range(L)]
+    out = []
+    for t in range(T):
+        it = x[:, t]
+        mk = masks[:, t][:, None].astype(np.float64)
+        for l in range(L):
+            h[l], s[l] = onat.cell(p, f"layers.{l}.", it, h[l], s[l], fused, ln, mask=mk)
+            it = h[l]
+        out.append(onat._lin(it, p, "output_proj"))
+    return np.stack(out, 1), h, s
+
+
+@pytest.mark.parametrize("fused", [True, False])
+@pytest.mark.parametrize("ln", [True, False])
+@pytest.mark.parametrize("D", [128, 200])
+def test_streaming_vs_oracle_ragged(fused, ln, D):
+    import statecatcher_amd as sc
+    from statecatcher_amd.streaming import StreamingLucyRNN
+    torch.manual_seed(D + 2 * fused + ln)
+    L, F, V, B, T = 3, 40, 50, 5, 23
+    m = sc.LucyRNN(sc.LucyRNNConfig(input_dim=F, hidden_dim=D, num_layers=L, vocab_size=V,
+                                    is_training=False, fused_ops=fused, layer_norm=ln))
+    with torch.no_grad():   # the reference zero-inits output_proj; make the logits informative
+        m.output_proj.weight.normal_(0.0, 0.3)
+        m.output_proj.bias.normal_(0.0, 0.3)
+    m = m.to(DEV)
+    x = torch.randn(B, T, F)
+    lens = torch.tensor([23, 1, 17, 0, 9])
+    masks = torch.arange(T)[None, :] < lens[:, None]
+    p = oracle_params(m)
+    rl, rh, rs = oracle_stream(p, x.double().numpy(), masks.numpy(), L, fused, ln)
+    for K, graph in ((1, True), (4, True), (2, False)):
+        st = StreamingLucyRNN(m, batch=B, frames_per_call=K, graph=graph)
+        toks, logits = st.decode(x.to(DEV), masks.to(DEV), return_logits=True)
+        close(logits, rl, rtol=1e-4, afrac=1e-4)
+        h, s = st.state()
+        close(torch.stack(h), np.stack(rh), rtol=1e-4, afrac=1e-4)
+        close(torch.stack(s), np.stack(rs), rtol=1e-4, afrac=1e-4)
+        lg = logits.cpu().numpy()
+        assert toks == odec.ctc_greedy(lg, lens.numpy())
+
+
+def test_streaming_bf16_tracks_fp32():
+    """bf16 GEMMs/activations (fp32 state) drift from the fp32 stream no more than the
+    reference's own frame loop run under bf16 autocast (lucyrnn.py:172-184, as train.py runs
+    the model under autocast) drifts from its fp32 run."""
+    import statecatcher_amd as sc
+    from statecatcher_amd.streaming import StreamingLucyRNN
+    torch.manual_seed(3)
+    m = sc.LucyRNN(sc.LucyRNNConfig(input_dim=80, hidden_dim=512, num_layers=6, vocab_size=256,
+                                    is_training=False)).to(DEV)
+    with torch.no_grad():
+        m.output_proj.weight.normal_(0.0, 0.05)
+    x = torch.randn(8, 40, 80, device=DEV)
+    _, l32 = StreamingLucyRNN(m, 8, 8).decode(x, return_logits=True)
+    _, l16 = StreamingLucyRNN(m, 8, 8, dtype=torch.bfloat16).decode(x, return_logits=True)
+    rel = float((l16.float() - l32).norm() / l32.norm())
+    z = [torch.zeros(8, 512, device=DEV) for _ in range(6)]
+    st, outs = (list(z), list(z)), []
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+        for t in range(40):
+            lg, st = m.step(x[:, t], st)
+            outs.append(lg.float())
+    rel_ac = float((torch.stack(outs, 1) - l32).norm() / l32.norm())
+    assert rel < 1.5 * rel_ac + 1e-3, (rel, rel_ac)
+
+
+def test_streaming_reset_subset_and_blocks_equal_one_pass():
+    """Feeding an utterance in two calls equals one call; resetting one stream restarts only
+    that stream (its tokens equal a fresh decoder's)."""
+    import statecatcher_amd as sc
+    from statecatcher_amd.streaming import StreamingLucyRNN
+    torch.manual_seed(5)
+    m = sc.LucyRNN(sc.LucyRNNConfig(input_dim=20, hidden_dim=64, num_layers=2, vocab_size=12,
+                                    is_training=False, fused_ops=True))
+    with torch.no_grad():
+        m.output_proj.weight.normal_(0.0, 0.5)
+    m = m.to(DEV)
+    x = torch.randn(3, 16, 20, device=DEV)
+    one = StreamingLucyRNN(m, 3, 4)
+    e_all = torch.cat([one.step(x[:, i:i + 4]).clone() for i in range(0, 16, 4)], 1)
+    two = StreamingLucyRNN(m, 3, 4)
+    for i in range(0, 8, 4):
+        two.step(x[:, i:i + 4])
+    two.reset(streams=[1])
+    e_tail = torch.cat([two.step(x[:, i:i + 4]).clone() for i in range(8, 16, 4)], 1)
+    fresh = StreamingLucyRNN(m, 3, 4)
+    e_fresh = torch.cat([fresh.step(x[:, i:i + 4]).clone() for i in range(8, 16, 4)], 1)
+    assert torch.equal(e_tail[[0, 2]], e_all[[0, 2], 8:])
+    assert torch.equal(e_tail[1], e_fresh[1])
+
+
+def test_greedy_step_kernel_ties_nan_masks_vs_oracle():
+    """sc_ctc_greedy_step frame by frame == decoder.py over the sequence (ties -> lowest index,
+    NaN wins, masked frames past the length emit nothing), bf16 and fp32 logits."""
+    from statecatcher_amd import ops
+    rng = np.random.default_rng(7)
+    B, T, V = 6, 40, 37
+    for dt in (torch.float32, torch.bfloat16):
+        x = rng.integers(0, 4, (B, T, V)).astype(np.float32)    # many ties
+        x[1, 5, 3] = np.nan
+        x[2, :, :] = 0.0                                         # all-tie rows -> blank (0)
+        lens = np.array([40, 33, 40, 0, 1, 12])
+        xt = torch.as_tensor(x).to(dt)
+        ref = odec.ctc_greedy(xt.float().numpy(), lens)
+        prev = torch.full((B,), -1, dtype=torch.int32, device=DEV)
+        emit = torch.empty(T, B, dtype=torch.int32, device=DEV)
+        xd = xt.to(DEV)
+        for t in range(T):
+            mk = torch.as_tensor((t < lens).astype(np.float32), device=DEV)
+            ops.ctc_greedy_step(xd[:, t], prev, emit[t], mask=mk)
+        got = [[int(v) for v in row if v >= 0] for row in emit.t().cpu()]
+        assert got == ref

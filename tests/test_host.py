@@ -56,6 +56,10 @@ def test_cpu_tensors_fail_loudly_no_fallback():
         m(torch.randn(2, 5, 80))
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         sc.ctc_nll(torch.randn(2, 5, 7), torch.ones(2, 3, dtype=torch.long), [5, 5], [3, 3])
+    native = sc.LucyRNN(sc.LucyRNNConfig(input_dim=8, hidden_dim=64, num_layers=1, vocab_size=5,
+                                         is_training=False))
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        sc.StreamingLucyRNN(native, batch=2)
 
 
 def test_detach_states_nested():
