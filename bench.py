@@ -49,6 +49,12 @@ def parse():
                     help="T of the bounded CPU sample (default: one full C2 segment, ~10 s)")
     ap.add_argument("--tunableop", choices=["on", "off"], default="on",
                     help="use the shipped PyTorch TunableOp GEMM table (statecatcher_amd/tuning)")
+    ap.add_argument("--timing-steps", type=int, default=2,
+                    help="per-kernel HIP-event timing is recorded over the last N timed steps (each "
+                         "event pair idles the GPU ~6 us; timing every step would tax the step time)")
+    ap.add_argument("--host-probe", action="store_true",
+                    help="diagnostics on stderr: synchronising ops in one step (sync debug mode) and "
+                         "host issue time per step")
     ap.add_argument("--tune-out", default=None,
                     help="rank 0 tunes GEMM shapes missing from the table and writes it here")
     return ap.parse_args()
@@ -159,12 +165,26 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    if args.host_probe:
+        torch.cuda.set_sync_debug_mode(1)
+        step()
+        torch.cuda.set_sync_debug_mode(0)
+        torch.cuda.synchronize()
+        for _ in range(3):
+            h0 = time.perf_counter()
+            step()
+            h1 = time.perf_counter()
+            torch.cuda.synchronize()
+            h2 = time.perf_counter()
+            print(f"host issue {1e3 * (h1 - h0):.3f} ms, step wall {1e3 * (h2 - h0):.3f} ms",
+                  file=sys.stderr)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    ops.LAUNCH_EVENTS = []
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for k in range(args.steps):
+        if k == max(0, args.steps - args.timing_steps):
+            ops.LAUNCH_EVENTS = []
         loss = step()
     torch.cuda.synchronize()
     if world > 1:
@@ -188,8 +208,9 @@ def main():
     kernels = {}
     for name, (tsum, n, nbytes) in kstats.items():
         avg = tsum / n
+        tsteps = max(1, min(args.timing_steps, args.steps))
         kernels[name] = {"launches": n, "avg_us": round(avg * 1e6, 1),
-                         "share_of_step": round(tsum / dt, 4)}
+                         "share_of_step": round(tsum / tsteps / (dt / args.steps), 4)}
         if nbytes:
             kernels[name].update({"bytes_per_launch": nbytes,
                                   "achieved_GBs": round(nbytes / avg / 1e9, 1),
@@ -229,6 +250,8 @@ def main():
             "per_gpu_frames_per_s": round(value / world, 1),
             "roofline": roofline,
             "kernels": kernels,
+            "kernel_timing": f"HIP events on the launch stream, last {min(args.timing_steps, args.steps)} "
+                             "timed steps",
             "gemm_TFLOPs_effective": round(gemm_tflops / world, 1),
             "cpu_baseline": cpu,
             "loss_last": round(last_loss, 4),

@@ -163,7 +163,7 @@ size_t sc_ctc_workspace_bytes(int B, int T, int max_target_len);
  *   is_logits = 1: x are logits, log_softmax is fused (model.py:70 + ATen ctc_loss);
  *   is_logits = 0: x are log-probabilities (the nn.CTCLoss input convention).
  * targets: int64 [B, max_target_len] padded (train.py:208), row stride target_stride;
- * in_lens/tgt_lens: int64 [B] device arrays.  Writes nll [B] fp32 (+inf when infeasible;
+ * max_target_len <= 1007.  in_lens/tgt_lens: int64 [B] device arrays.  Writes nll [B] fp32 (+inf when infeasible;
  * the zero_infinity reduction is the caller's) and fills the workspace for sc_ctc_bwd.
  */
 int sc_ctc_fwd(const void* x, int x_dtype, int is_logits, int B, int T, int V,

@@ -9,7 +9,9 @@ import os
 import torch  # noqa: F401  (loads torch's HIP runtime first: our .so binds to the same SONAME)
 
 LIB_NAME = "libstatecatcher_hip.so"
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+# SC_LIB_PATH: load another build of the same ABI (ablation builds under tools/); default in-tree
+LIB_PATH = os.environ.get("SC_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                         LIB_NAME)
 
 SC_F32, SC_BF16, SC_F16 = 0, 1, 2
 _DTYPE = {torch.float32: SC_F32, torch.bfloat16: SC_BF16, torch.float16: SC_F16}

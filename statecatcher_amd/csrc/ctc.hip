@@ -14,10 +14,11 @@
 //   ctc_chain_kernel  per b: for every target position the next position with the same label,
 //                     so label occupancies are summed in a fixed order (deterministic, no atomics)
 //   ctc_ab_kernel     one workgroup per (sequence, direction): 2B workgroups run alpha forward
-//                     and beta backward concurrently.  One state per lane; each wave also
-//                     carries a 2K-state halo of its neighbour's states so it advances K steps
-//                     with DPP wave_shr:1 / wave_shl:1 only (no LDS, no barrier), then exchanges
-//                     halos through LDS.  Emission rows are prefetched 16 steps ahead.
+//                     and beta backward concurrently.  Two states (a blank and its label) per
+//                     lane; each wave also carries a K-pair halo of its neighbour's pairs so it
+//                     advances K steps with DPP wave_shr:1 / wave_shl:1 only (no LDS, no
+//                     barrier), then exchanges halos through LDS.  Emission rows are prefetched
+//                     16 steps ahead.
 //                     Values live in base-2 log space with a finite "dead" sentinel (branch-free
 //                     log-sum-exp) and are re-centred on the workgroup max every 16 steps; the
 //                     running offset is kept in fp64 (at T=1500 |alpha| ~ 1e4, where an fp32
@@ -25,6 +26,13 @@
 //   ctc_grad_kernel   one workgroup per (b,t) row: label occupancies into an LDS row of V
 //                     log-sums, then one coalesced pass writing the gradient row
 #include "sc_common.h"
+
+#ifndef SC_CTC_ABL   // ablation bitmask (timing studies only; results are wrong when set):
+#define SC_CTC_ABL 0  // 1 no halo exchange, 2 no per-step stores, 4 max instead of log-sum-exp
+#endif
+#ifndef SC_CTC_KMAX   // most steps between halo exchanges (8 or 16)
+#define SC_CTC_KMAX 16
+#endif
 
 namespace sc {
 
@@ -35,8 +43,8 @@ struct CtcWs {
   float* lpe;     // [B,T,Sp]   base-2 emission log-probs of the blank-extended states
   float* alpha;   // [B,T,Sp]   base-2, relative to offA
   float* beta;    // [B,T,Sp]   base-2, relative to offB
-  double* offA;   // [B,T]      base-2 offsets
-  double* offB;   // [B,T]
+  double* offA;   // [B,T]      base-2 offsets: entry n = offset after the n-th re-centring (at
+  double* offB;   // [B,T]      step i = 2Kn - 1 of the direction), so step i has entry (i+1)/2K
   double* nll64;  // [B]        natural log
   int* chain;     // [B,Um]
   int* first;     // [B,Um]
@@ -83,6 +91,7 @@ __device__ __forceinline__ float lse2_b2(float a, float b) {
 struct CtcArgs {
   const void* x;
   int is_logits, B, T, V, S, Sp, Umax, blank;
+  int kh;   // steps between halo exchanges of ctc_ab_kernel (re-centring every 2 kh steps)
   int64_t sb, stt;
   const int64_t* tg;
   int64_t tgs;
@@ -182,115 +191,137 @@ __device__ __forceinline__ float shl1(float v) {   // value of lane+1 (lane 63: 
 constexpr float kDead = -1e30f;
 __device__ __forceinline__ float lse3_live(float a, float b, float c) {
   const float m = fmaxf(fmaxf(a, b), c);
-  return m + log2_(exp2_(a - m) + exp2_(b - m) + exp2_(c - m));
+  if (SC_CTC_ABL & 4) return m;
+  // the max term is exp2(0) = 1: two exponentials (median and minimum), not three
+  const float md = __builtin_amdgcn_fmed3f(a, b, c);
+  const float lo = fminf(fminf(a, b), c);
+  return m + log2_(1.0f + exp2_(md - m) + exp2_(lo - m));
 }
 
 constexpr int kAbP = 16;   // emission prefetch depth (steps)
 
-// One workgroup per (sequence, direction).  Wave w computes 64 consecutive states: OW = 64 - 2K
-// of them it OWNS, plus a halo of 2K states owned by the neighbouring wave (left for alpha,
-// right for beta).  A missing neighbour corrupts at most 2 more lanes of the halo per step
-// (s-1, s-2 dependencies), so for K steps the owned states stay exact with no communication:
-// in-wave neighbours come from DPP wave_shr:1 / wave_shl:1, and only every K steps the owned
-// states are published to LDS, one barrier, halo lanes re-read theirs (and every second such
-// exchange re-centres on the workgroup max).
-template <int K>
-__global__ void __launch_bounds__(1024) ctc_ab_kernel(CtcArgs a) {
-  constexpr int H = 2 * K;        // halo lanes
-  constexpr int OW = 64 - H;      // owned states per wave
-  const bool is_beta = blockIdx.x >= a.B;
-  const int b = is_beta ? blockIdx.x - a.B : blockIdx.x;
+
+__device__ __forceinline__ float lse2_live(float a, float b) {
+  const float m = fmaxf(a, b);
+  if (SC_CTC_ABL & 4) return m;
+  return m + log2_(1.0f + exp2_(fminf(a, b) - m));
+}
+
+// One workgroup per (sequence, direction).  Each lane holds a PAIR of blank-extended states,
+// p -> (blank 2p, label 2p+1), so one step is
+//   alpha:  B' = lse(B, L[p-1]) + e(2p);    L' = lse(L, B, skip ? L[p-1] : dead) + e(2p+1)
+//   beta:   B' = lse(B, L) + e(2p);         L' = lse(L, B[p+1], skip ? L[p+1] : dead) + e(2p+1)
+// i.e. one DPP lane shift (two independent ones for beta) and two independent log-sum-exps per
+// step, half the lanes of a state-per-lane layout.  Wave w computes 64 consecutive pairs: OW =
+// 64 - K it OWNS plus a K-pair halo owned by the neighbouring wave (left for alpha, right for
+// beta); a missing neighbour corrupts one more halo pair per step, so for K steps the owned
+// pairs stay exact with no communication, then they are published to LDS, one barrier, and the
+// halo lanes re-read theirs (every second such exchange also re-centres on the workgroup max).
+template <int K, bool BETA>
+__device__ __forceinline__ void ab_run(const CtcArgs& a, int b, int Tb, int Ub) {
+  constexpr int OW = 64 - K;      // owned pairs per wave
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int w = uniform(tid >> 6);
   const int nw = blockDim.x >> 6;
-  const int Tb = clampi(a.in_lens[b], 0, a.T);
-  const int Ub = clampi(a.tgt_lens[b], 0, a.Umax);
-  const int Sb = 2 * Ub + 1;
-  if (Tb == 0) {
-    if (!is_beta && tid == 0) {
-      a.nll[b] = (Ub == 0) ? 0.0f : __builtin_huge_valf();
-      a.ws.nll64[b] = (Ub == 0) ? 0.0 : __builtin_huge_val();
-    }
-    return;
-  }
-  // state of this lane and whether this lane owns it
-  const int s = is_beta ? w * OW + lane : w * OW + lane - H;
-  const bool own = is_beta ? (lane < OW) : (lane >= H);
-  const bool live = s >= 0 && s < Sb;
+  const int p = BETA ? w * OW + lane : w * OW + lane - K;
+  const bool own = BETA ? (lane < OW) : (lane >= K);
+  const bool liveB = p >= 0 && p <= Ub;    // state 2p   < 2Ub + 1
+  const bool liveL = p >= 0 && p < Ub;     // state 2p+1 < 2Ub + 1
   const int64_t* tg = a.tg + (int64_t)b * a.tgs;
-  bool skip = false;   // alpha: s-2 -> s allowed;  beta: s+2 -> s allowed
-  if (live && (s & 1)) {
-    const int lab = (int)tg[(s - 1) >> 1];
-    if (!is_beta) {
-      skip = s >= 3 && lab != a.blank && lab != (int)tg[(s - 3) >> 1];
-    } else if (s + 2 < Sb) {
-      const int l2 = (int)tg[(s + 1) >> 1];
+  bool skip = false;   // alpha: 2p-1 -> 2p+1 allowed;  beta: 2p+3 -> 2p+1 allowed
+  if (liveL) {
+    const int lab = (int)tg[p];
+    if (!BETA) {
+      skip = p >= 1 && lab != a.blank && lab != (int)tg[p - 1];
+    } else if (p + 1 < Ub) {
+      const int l2 = (int)tg[p + 1];
       skip = l2 != a.blank && l2 != lab;
     }
   }
-  extern __shared__ __attribute__((aligned(16))) float full[];   // [2][nw*OW] published states
+  extern __shared__ __attribute__((aligned(16))) float2 full2[];   // [2][nw*OW] published pairs
   __shared__ float wmax[16];
   const int nst = nw * OW;
-  const int sc = s < 0 ? 0 : (s >= a.Sp ? a.Sp - 1 : s);   // clamped for addressing only
-  const float* lrow = a.ws.lpe + (int64_t)b * a.T * a.Sp + sc;
-  float* orow = (is_beta ? a.ws.beta : a.ws.alpha) + (int64_t)b * a.T * a.Sp + sc;
-  double* offp = (is_beta ? a.ws.offB : a.ws.offA) + (int64_t)b * a.T;
-  auto tstep = [&](int i) { return is_beta ? Tb - 1 - i : i; };
-  float bufA[kAbP], bufB[kAbP];
-  auto load = [&](float (&buf)[kAbP], int i0) {
+  const int pc = p < 0 ? 0 : (2 * p >= a.Sp ? a.Sp / 2 - 1 : p);   // clamped for addressing only
+  const float2* lrow = (const float2*)(a.ws.lpe + (int64_t)b * a.T * a.Sp) + pc;
+  const int64_t rs = a.Sp / 2;   // row stride in pairs
+  // Per-step outputs through buffer descriptors: lanes that must not write (halo lanes, pairs
+  // past the row; every lane but 0 for the offset) get an out-of-range offset, which the buffer
+  // unit drops, so the stores need no exec-mask branch in the step loop.
+  constexpr uint32_t kDrop = 0x80000000u;
+  const uint32_t rowb = (uint32_t)(a.Sp * 4);
+  const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
+      (BETA ? a.ws.beta : a.ws.alpha) + (int64_t)b * a.T * a.Sp, 0, (int)(rowb * (uint32_t)a.T),
+      0x00020000);
+  const uint32_t ovo = (own && 2 * p < a.Sp) ? (uint32_t)(8 * pc) : kDrop;
+  double* offn = (BETA ? a.ws.offB : a.ws.offA) + (int64_t)b * a.T;
+  if (tid == 0) offn[0] = 0.0;
+  auto tstep = [&](int i) { return BETA ? Tb - 1 - i : i; };
+  float2 bufA[kAbP], bufB[kAbP];
+  auto load = [&](float2 (&buf)[kAbP], int i0) {
 #pragma unroll
-    for (int j = 0; j < kAbP; ++j) buf[j] = lrow[(int64_t)tstep(min(i0 + j, Tb - 1)) * a.Sp];
+    for (int j = 0; j < kAbP; ++j) buf[j] = lrow[(int64_t)tstep(min(i0 + j, Tb - 1)) * rs];
   };
-  float v = kDead;
+  auto emit = [&](int t, float vB, float vL) {
+    __builtin_amdgcn_raw_buffer_store_b64(
+        __builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, make_float2(vB, vL)), ors,
+        ovo, (uint32_t)t * rowb, 0);
+  };
+  float vB = kDead, vL = kDead;
   double off = 0.0;
   int exch = 0;
-  auto body = [&](const float (&buf)[kAbP], int i0) __attribute__((always_inline)) {
+  auto body = [&](const float2 (&buf)[kAbP], int i0) __attribute__((always_inline)) {
 #pragma unroll
     for (int j = 0; j < kAbP; ++j) {
       const int i = i0 + j;
       if (i >= Tb) break;
-      const int t = tstep(i);
-      const float lp = live ? buf[j] : kDead;
+      const float eB = liveB ? buf[j].x : kDead;
+      const float eL = liveL ? buf[j].y : kDead;
       if (i == 0) {
-        const bool init = is_beta ? (s >= Sb - 2) : (s <= 1);
-        v = (live && init) ? lp : kDead;
-      } else if (!is_beta) {
-        const float p1 = shr1(v);
-        const float p2 = shr1(p1);
-        v = lse3_live(v, p1, skip ? p2 : kDead) + lp;
+        vB = (liveB && p == (BETA ? Ub : 0)) ? eB : kDead;
+        vL = (liveL && p == (BETA ? Ub - 1 : 0)) ? eL : kDead;
+      } else if (!BETA) {
+        const float lp = shr1(vL);
+        const float nB = lse2_live(vB, lp) + eB;
+        vL = lse3_live(vL, vB, skip ? lp : kDead) + eL;
+        vB = nB;
       } else {
-        const float q1 = shl1(v);
-        const float q2 = shl1(q1);
-        v = lse3_live(v, q1, skip ? q2 : kDead) + lp;
+        const float bn = shl1(vB);
+        const float ln = shl1(vL);
+        const float nB = lse2_live(vB, vL) + eB;
+        vL = lse3_live(vL, bn, skip ? ln : kDead) + eL;
+        vB = nB;
       }
-      if (j % K == K - 1) {   // halo exchange (+ re-centre every second one)
+      if (!(SC_CTC_ABL & 1) && j % K == K - 1) {   // halo exchange (+ re-centre every 2nd)
         const int par = exch & 1;
         const bool norm = par == 1;
-        if (own) full[par * nst + s] = v;
+        if (own) full2[par * nst + p] = make_float2(vB, vL);
         if (norm) {
-          float m = own ? v : kDead;
+          float m = own ? fmaxf(vB, vL) : kDead;
 #pragma unroll
           for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
           if (lane == 0) wmax[w] = m;
         }
         lds_barrier();
         if (!own) {
-          const bool has = s >= 0 && s < nst;
-          v = has ? full[par * nst + s] : kDead;
+          const bool has = p >= 0 && p < nst;
+          const float2 q = has ? full2[par * nst + p] : make_float2(kDead, kDead);
+          vB = q.x;
+          vL = q.y;
         }
         if (norm) {
           float m = kDead;
           for (int q = 0; q < nw; ++q) m = fmaxf(m, wmax[q]);
           if (m > 0.5f * kDead) {   // all dead (infeasible): keep the sentinel
-            v -= m;
+            vB -= m;
+            vL -= m;
             off += (double)m;
           }
+          if (tid == 0) offn[(exch + 1) >> 1] = off;
         }
         ++exch;
       }
-      if (own && s < a.Sp) orow[(int64_t)t * a.Sp] = v;
-      if (tid == 0) offp[t] = off;
+      if (!(SC_CTC_ABL & 2)) emit(tstep(i), vB, vL);
     }
   };
   load(bufA, 0);
@@ -301,9 +332,9 @@ __global__ void __launch_bounds__(1024) ctc_ab_kernel(CtcArgs a) {
     load(bufA, i0 + 2 * kAbP);
     body(bufB, i0 + kAbP);
   }
-  if (!is_beta) {
-    // log p = log2sum(alpha_{Tb-1}(Sb-1), alpha_{Tb-1}(Sb-2)) + off, gathered over the workgroup
-    float c = (own && (s == Sb - 1 || s == Sb - 2)) ? v : kDead;
+  if (!BETA) {
+    // log p = log2sum(alpha_{Tb-1}(2Ub), alpha_{Tb-1}(2Ub-1)) + off, gathered over the workgroup
+    float c = lse2_live((own && p == Ub) ? vB : kDead, (own && p == Ub - 1) ? vL : kDead);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
       const float co = __shfl_xor(c, o);
@@ -326,10 +357,28 @@ __global__ void __launch_bounds__(1024) ctc_ab_kernel(CtcArgs a) {
   }
 }
 
-// K (steps between halo exchanges) so that ceil(S / (64 - 2K)) waves fit a 1024-thread group
-static int ab_halo_k(int S) {
-  for (int K : {8, 4, 2, 1})
-    if ((S + (64 - 2 * K) - 1) / (64 - 2 * K) <= 16) return K;
+template <int K>
+__global__ void __launch_bounds__(1024) ctc_ab_kernel(CtcArgs a) {
+  const bool is_beta = blockIdx.x >= a.B;
+  const int b = is_beta ? blockIdx.x - a.B : blockIdx.x;
+  const int Tb = clampi(a.in_lens[b], 0, a.T);
+  const int Ub = clampi(a.tgt_lens[b], 0, a.Umax);
+  if (Tb == 0) {
+    if (!is_beta && threadIdx.x == 0) {
+      a.nll[b] = (Ub == 0) ? 0.0f : __builtin_huge_valf();
+      a.ws.nll64[b] = (Ub == 0) ? 0.0 : __builtin_huge_val();
+    }
+    return;
+  }
+  if (is_beta) ab_run<K, true>(a, b, Tb, Ub);
+  else ab_run<K, false>(a, b, Tb, Ub);
+}
+
+// K (steps between halo exchanges) so that ceil((Umax + 1) / (64 - K)) waves of state pairs fit
+// a 1024-thread group
+static int ab_halo_k(int Umax) {
+  for (int K : {SC_CTC_KMAX, 4, 2, 1})
+    if ((Umax + 1 + (64 - K) - 1) / (64 - K) <= 16) return K;
   return 0;
 }
 
@@ -357,7 +406,9 @@ __global__ void __launch_bounds__(256) ctc_grad_kernel(CtcArgs a) {
   const float* al = a.ws.alpha + ((int64_t)b * a.T + t) * a.Sp;
   const float* be = a.ws.beta + ((int64_t)b * a.T + t) * a.Sp;
   // exp(lcab + nll - lp) = 2^(lcab2 + offA + offB + nll*log2e - lp*log2e): fold offsets in fp64
-  const float koff = (float)(a.ws.offA[(int64_t)b * a.T + t] + a.ws.offB[(int64_t)b * a.T + t] +
+  const int per = 2 * a.kh;   // steps per re-centring
+  const float koff = (float)(a.ws.offA[(int64_t)b * a.T + (t + 1) / per] +
+                             a.ws.offB[(int64_t)b * a.T + (Tb - t) / per] +
                              a.ws.nll64[b] * (double)kLog2e);
   const int* chain = a.ws.chain + (int64_t)b * Um;
   const int* first = a.ws.first + (int64_t)b * Um;
@@ -420,10 +471,13 @@ static void launch_fwd(const CtcArgs& a, hipStream_t st) {
   const int64_t rows = (int64_t)a.B * a.T;
   hipLaunchKernelGGL((ctc_emit_kernel<DT>), dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, a);
   hipLaunchKernelGGL(ctc_chain_kernel, dim3(a.B), dim3(256), 0, st, a);
-  const int K = ab_halo_k(a.S);
-  const int nw = (a.S + (64 - 2 * K) - 1) / (64 - 2 * K);
-  const size_t sh = 2 * (size_t)nw * (64 - 2 * K) * sizeof(float);
+  const int K = a.kh;
+  const int nw = (a.Umax + 1 + (64 - K) - 1) / (64 - K);
+  const size_t sh = 2 * (size_t)nw * (64 - K) * sizeof(float2);
   switch (K) {
+#if SC_CTC_KMAX == 16
+    case 16: hipLaunchKernelGGL((ctc_ab_kernel<16>), dim3(2 * a.B), dim3(64 * nw), sh, st, a); break;
+#endif
     case 8: hipLaunchKernelGGL((ctc_ab_kernel<8>), dim3(2 * a.B), dim3(64 * nw), sh, st, a); break;
     case 4: hipLaunchKernelGGL((ctc_ab_kernel<4>), dim3(2 * a.B), dim3(64 * nw), sh, st, a); break;
     case 2: hipLaunchKernelGGL((ctc_ab_kernel<2>), dim3(2 * a.B), dim3(64 * nw), sh, st, a); break;
@@ -452,8 +506,8 @@ static int ctc_check(const void* x, int x_dtype, int B, int T, int V, int max_ta
   SC_REQUIRE(x_dtype == SC_F32 || x_dtype == SC_BF16 || x_dtype == SC_F16,
              "%s: unsupported dtype %d", who, x_dtype);
   SC_REQUIRE(B >= 0 && T >= 0 && V > 0 && max_target_len >= 0, "%s: bad shape", who);
-  SC_REQUIRE(ab_halo_k(2 * max_target_len + 1) > 0,
-             "%s: max target length %d exceeds %d", who, max_target_len, (16 * 62 - 1) / 2);
+  SC_REQUIRE(ab_halo_k(max_target_len) > 0,
+             "%s: max target length %d exceeds %d", who, max_target_len, 16 * 63 - 1);
   SC_REQUIRE(blank >= 0 && blank < V, "%s: blank %d outside [0, %d)", who, blank, V);
   SC_REQUIRE((int64_t)B * T <= 0x7fffffff, "%s: B*T too large", who);
   if (B == 0 || T == 0) return 0;
@@ -477,6 +531,7 @@ static CtcArgs make_args(const void* x, int is_logits, int B, int T, int V, int6
   a.S = 2 * umax + 1;
   a.Sp = 64 * states_per_lane(a.S);
   a.Umax = umax;
+  a.kh = ab_halo_k(umax);
   a.blank = blank;
   a.sb = sb;
   a.stt = st;

@@ -53,7 +53,7 @@ def test_invalid_arguments_rejected_without_gpu(lib):
     assert rc == -1
     rc = lib.sc_decay_scan_fwd(null, null, null, 0, null, 1, 1, 1, 1, 1, 2, null)
     assert rc == -1 and b"stride_d" in lib.sc_last_error()
-    rc = lib.sc_ctc_fwd(null, 0, 1, 1, 1, 4, 4, 4, null, 0, 600, null, null, 0, null, null, 0, null)
+    rc = lib.sc_ctc_fwd(null, 0, 1, 1, 1, 4, 4, 4, null, 0, 1008, null, null, 0, null, null, 0, null)
     assert rc == -1 and b"exceeds" in lib.sc_last_error()
     rc = lib.sc_ctc_fwd(null, 0, 1, 1, 1, 4, 4, 4, null, 0, 1, null, null, 9, null, null, 0, null)
     assert rc == -1 and b"blank" in lib.sc_last_error()

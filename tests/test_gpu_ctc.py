@@ -74,6 +74,32 @@ def test_ctc_full_size_vs_aten_cpu():
     np.testing.assert_allclose(x.grad.cpu().numpy(), xr.grad.numpy(), rtol=1e-2, atol=2e-6)
 
 
+@pytest.mark.parametrize("U", [57, 300, 1007])
+def test_ctc_long_targets_many_waves_vs_aten_cpu(U):
+    """Targets spanning 1-16 waves of state pairs (K = 8 / 4 steps between halo exchanges), with
+    runs of repeated labels (no skip transition) and blank-free stretches, vs ATen fp64 on CPU;
+    U = 1007 is the longest target the ABI accepts."""
+    g = torch.Generator().manual_seed(U)
+    B, V = 2, 40
+    T = 2 * U + 40
+    logits = torch.randn(B, T, V, generator=g) * 2
+    tg = torch.randint(1, V, (B, U), generator=g)
+    tg[0, 10:20] = 7                      # a run of repeats
+    tl = torch.tensor([U, U - 3])
+    tg[1, U - 3:] = 0
+    il = torch.tensor([T, T - 17])
+    x = logits.to(DEV).requires_grad_(True)
+    nll = sc().ctc_nll(x, tg.to(DEV), il, tl)
+    nll.sum().backward()
+    xr = logits.double().requires_grad_(True)
+    ref = torch.nn.functional.ctc_loss(xr.log_softmax(-1).transpose(0, 1), tg, il, tl,
+                                       reduction="none", zero_infinity=False)
+    ref.sum().backward()
+    np.testing.assert_allclose(nll.detach().cpu().numpy(), ref.detach().numpy(), rtol=1e-4)
+    # |grad| <= 1; fp32 log-space lattices over T = 2054 steps: 1e-4 absolute
+    np.testing.assert_allclose(x.grad.cpu().numpy(), xr.grad.numpy(), rtol=1e-2, atol=1e-4)
+
+
 def test_ctc_bf16_logits_vs_oracle():
     g = torch.Generator().manual_seed(5)
     B, T, V = 3, 120, 64
