@@ -155,20 +155,29 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(LnArgs a) {
 }
 
 // fixed-order sum of the P partial rows: out[n] = sum_p part[p][n].  A workgroup owns 64
-// columns; wave q sums rows q, q+4, ... (coalesced 256-B row segments), then 4-way LDS sum.
+// columns; wave q sums rows q, q+4, ... (coalesced 256-B row segments) into 8 interleaved
+// accumulators (8 independent loads in flight), then a fixed-order 8-way and 4-way LDS sum.
 __global__ void __launch_bounds__(256) ln_part_sum_kernel(const float* part, int P, int n, float* out) {
   __shared__ float acc4[4][64];
   const int lane = threadIdx.x & 63, q = threadIdx.x >> 6;
   const int e = blockIdx.x * 64 + lane;
   float acc = 0.0f;
-  if (e < n)
-    for (int p = q; p < P; p += 4) acc += part[(int64_t)p * n + e];
+  if (e < n) {
+    float r[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+    int p = q;
+    for (; p + 28 < P; p += 32) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) r[j] += part[(int64_t)(p + 4 * j) * n + e];
+    }
+    for (int j = 0; p < P; p += 4, ++j) r[j & 7] += part[(int64_t)p * n + e];
+    acc = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  }
   acc4[q][lane] = acc;
   __syncthreads();
   if (q == 0 && e < n) out[e] = (acc4[0][lane] + acc4[1][lane]) + (acc4[2][lane] + acc4[3][lane]);
 }
 
-constexpr int kLnBwdBlocks = 256;
+constexpr int kLnBwdBlocks = 1024;   // 4 per CU: 16 waves/CU keep x and dy loads in flight
 
 template <int DT>
 static int ln_chunks(int D) {

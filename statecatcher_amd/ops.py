@@ -130,10 +130,11 @@ def lucy_scan(gates, h0, s0):
     return LucyScanFn.apply(gates, h0, s0)
 
 
-def wgrad_splitk(dy, x):
+def wgrad_splitk(dy, x, blocked_d=0):
     """dW = dy^T x (fp32) for dy [M,N], x [M,K] with M = B*T large: at the training shape
     dW is 3584 x 512 while M = 48000, so a plain GEMM has 28 output tiles for 256 CUs; split M
-    into S batched GEMMs and sum the partials in fp32."""
+    into S batched GEMMs and sum the partials in fp32.  blocked_d = D: dy's columns are in
+    step-blocked order (step_blocked_rows); the sum writes dW back in the reference's order."""
     M, N = dy.shape
     K = x.shape[1]
     S = 1
@@ -143,18 +144,25 @@ def wgrad_splitk(dy, x):
             ((N + 255) // 256) * ((K + 255) // 256) * S < 512:
         S *= 2
     if S == 1:
-        return torch.matmul(dy.t(), x).float()
+        dw = torch.matmul(dy.t(), x).float()
+        return step_blocked_rows(dw, blocked_d, inverse=True) if blocked_d else dw
     part = torch.bmm(dy.view(S, M // S, N).transpose(1, 2), x.view(S, M // S, K))
+    if blocked_d:   # the reduction's output order un-permutes the rows (one pass)
+        D = blocked_d
+        return part.view(S, D // 64, 7, 64, K).transpose(1, 2).sum(0, dtype=torch.float32) \
+            .reshape(7 * D, K)
     return part.sum(0, dtype=torch.float32)
 
 
-def step_blocked_rows(w, D, inverse=False):
+def step_blocked_rows(w, D, inverse=False, dtype=None):
     """Permute the 7*D rows of a gate projection weight from the reference's (gate, unit) order
-    to (column block of 64 units, gate, unit-in-block) order (inverse=True: back)."""
+    to (column block of 64 units, gate, unit-in-block) order (inverse=True: back), converting to
+    `dtype` in the same copy."""
     K = w.shape[1]
-    if inverse:
-        return w.view(D // 64, 7, 64, K).transpose(0, 1).reshape(7 * D, K)
-    return w.view(7, D // 64, 64, K).transpose(0, 1).reshape(7 * D, K)
+    v = w.view(D // 64, 7, 64, K) if inverse else w.view(7, D // 64, 64, K)
+    out = torch.empty((v.shape[1], v.shape[0], 64, K), dtype=dtype or w.dtype, device=w.device)
+    out.copy_(v.transpose(0, 1))
+    return out.view(7 * D, K)
 
 
 class LucyCellFn(torch.autograd.Function):
@@ -167,12 +175,13 @@ class LucyCellFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x2d, w, b, h0, s0, B, T, cdt):
+        ctx.set_materialize_grads(False)   # unused state outputs: no zero-filled gradients
         xc = x2d.to(cdt)
         D = w.shape[0] // 7
         blocked = D % 64 == 0
         # step-blocked gates: weight rows permuted to (column block, gate, unit) order so each
         # step's 7 x 64 gates of a column block are one contiguous 896-byte run for the scan
-        wc = step_blocked_rows(w.to(cdt), D) if blocked else w.to(cdt)
+        wc = step_blocked_rows(w, D, dtype=cdt) if blocked else w.to(cdt)
         bias = b.detach().to(torch.float32).contiguous()
         with _timed("gate_gemm_fwd", xc, 0):
             gates = torch.matmul(xc, wc.t())
@@ -197,9 +206,7 @@ class LucyCellFn(torch.autograd.Function):
         dw = None
         if ctx.needs_input_grad[1]:
             with _timed("gate_gemm_wgrad", dg2, 0):
-                dw = wgrad_splitk(dg2, xc)
-            if ctx.blocked:
-                dw = step_blocked_rows(dw, dw.shape[0] // 7, inverse=True)
+                dw = wgrad_splitk(dg2, xc, blocked_d=(dg2.shape[1] // 7) if ctx.blocked else 0)
             dw = dw.to(wdt)
         db = dbias.sum(0).view(-1).to(wdt) if dbias is not None else None
         return dx, dw, db, dh0.to(hdt), ds0.to(sdt), None, None, None
