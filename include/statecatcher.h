@@ -185,6 +185,15 @@ int sc_ctc_bwd(const void* x, int x_dtype, int is_logits, int B, int T, int V,
                const float* nll, const float* scale, void* grad, int grad_dtype,
                const void* workspace, size_t workspace_bytes, void* stream);
 
+/*
+ * The reduction nn.CTCLoss(reduction='mean', zero_infinity=True) applies to sc_ctc_fwd's nll
+ * (train.py:142): loss[0] = mean_b(nll_b / max(U_b, 1)) with infinite nll_b counted as 0, and
+ * factor[b] = d loss / d nll_b (0 for infinite nll_b), the `scale` sc_ctc_bwd takes times the
+ * loss's upstream gradient.  nll, factor: fp32 [B]; tgt_lens int64 [B]; loss fp32 [1].
+ */
+int sc_ctc_mean(const float* nll, const int64_t* tgt_lens, int B, float* loss, float* factor,
+                void* stream);
+
 /* ---------------------------------------------------------------- greedy decode --------- */
 
 /*

@@ -43,6 +43,7 @@ _SIGS = {
     "sc_ctc_bwd": (_i32, [_vp, _i32, _i32, _i32, _i32, _i32, _i64, _i64, _vp, _i64, _i32, _vp, _vp,
                          _i32, _fp, _fp, _vp, _i32, _vp, _c.c_size_t, _vp]),
     "sc_ctc_greedy_decode": (_i32, [_vp, _i32, _i32, _i32, _i32, _i64, _i64, _vp, _i32, _vp, _vp, _vp]),
+    "sc_ctc_mean": (_i32, [_fp, _vp, _i32, _fp, _fp, _vp]),
     "sc_ctc_greedy_step": (_i32, [_vp, _i32, _i32, _i32, _i64, _fp, _i32, _vp, _vp, _i64, _vp]),
     "sc_lucy_step_supported": (_i32, [_i32, _i32]),
     "sc_lucy_step_ln": (_i32, [_vp, _i32, _fp, _fp, _c.c_float, _vp, _i32, _i32, _vp]),

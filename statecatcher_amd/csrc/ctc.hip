@@ -491,6 +491,30 @@ static void launch_bwd(const CtcArgs& a, hipStream_t st) {
                      (a.V + 8) * sizeof(float), st, a);
 }
 
+// nn.CTCLoss(reduction='mean', zero_infinity=True) on device in one launch: loss =
+// mean_b(z_b / max(U_b, 1)) with z_b = 0 where nll_b is infinite, and the per-sequence factor
+// d loss / d nll_b = (finite ? 1 / (B max(U_b, 1)) : 0) for the backward.  One workgroup, fixed
+// summation order.
+__global__ void __launch_bounds__(256) ctc_mean_kernel(const float* nll, const int64_t* tgt_lens,
+                                                       int B, float* loss, float* factor) {
+  __shared__ float part[256];
+  float acc = 0.0f;
+  for (int b = threadIdx.x; b < B; b += 256) {
+    const float u = (float)(tgt_lens[b] > 1 ? tgt_lens[b] : 1);
+    const float v = nll[b];
+    const bool fin = !__builtin_isinf(v);
+    acc += fin ? v / u : 0.0f;
+    factor[b] = fin ? 1.0f / ((float)B * u) : 0.0f;
+  }
+  part[threadIdx.x] = acc;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) part[threadIdx.x] += part[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *loss = part[0] / (float)B;
+}
+
 }  // namespace sc
 
 using namespace sc;
@@ -600,4 +624,14 @@ extern "C" int sc_ctc_bwd(const void* x, int x_dtype, int is_logits, int B, int 
   }
 #undef SC_CTC_BWD
   return launch_status("sc_ctc_bwd");
+}
+
+extern "C" int sc_ctc_mean(const float* nll, const int64_t* tgt_lens, int B, float* loss,
+                           float* factor, void* stream) {
+  clear_error();
+  SC_REQUIRE(B > 0, "sc_ctc_mean: B must be positive");
+  SC_REQUIRE(nll && tgt_lens && loss && factor, "sc_ctc_mean: null pointer");
+  hipLaunchKernelGGL(ctc_mean_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, nll, tgt_lens, B,
+                     loss, factor);
+  return launch_status("sc_ctc_mean");
 }

@@ -156,10 +156,10 @@ class LucyRNNtriton(nn.Module):
         B, T, _ = x.shape
         L = self.config.num_layers
         H = self.config.hidden_dim
-        if hidden_states is None:
-            z = lambda: torch.zeros(B, H, device=x.device, dtype=x.dtype)  # noqa: E731
-            h = [[z() for _ in range(L)] for _ in range(self.num_tracks)]
-            s = [[z() for _ in range(L)] for _ in range(self.num_tracks)]
+        if hidden_states is None:   # lucyrnn_triton.py:119-120, one zero-fill for all states
+            z = torch.zeros(2, self.num_tracks, L, B, H, device=x.device, dtype=x.dtype)
+            h = [[z[0, k, l] for l in range(L)] for k in range(self.num_tracks)]
+            s = [[z[1, k, l] for l in range(L)] for k in range(self.num_tracks)]
         else:
             h, s = hidden_states
 

@@ -370,6 +370,31 @@ class CTCFn(torch.autograd.Function):
         return grad, None, None, None, None, None
 
 
+class CTCMeanFn(torch.autograd.Function):
+    """nn.CTCLoss(reduction='mean', zero_infinity=True) as one autograd node: the lattice
+    (sc_ctc_fwd), the reduction and its per-sequence gradient factors (sc_ctc_mean) in the
+    forward; the backward is one scale (factor x upstream gradient) and sc_ctc_bwd."""
+
+    @staticmethod
+    def forward(ctx, x, targets, in_lens, tgt_lens, blank, is_logits):
+        nll = CTCFn.forward(ctx, x, targets, in_lens, tgt_lens, blank, is_logits)
+        B = nll.shape[0]
+        loss = torch.empty((), dtype=torch.float32, device=x.device)
+        factor = torch.empty(B, dtype=torch.float32, device=x.device)
+        if B:
+            rc = _lib.load().sc_ctc_mean(ptr(nll), ptr(tgt_lens), B, ptr(loss), ptr(factor),
+                                         stream_of(x))
+            check(rc, "sc_ctc_mean")
+        else:
+            loss.fill_(float("nan"))   # mean over an empty batch
+        ctx.factor = factor
+        return loss
+
+    @staticmethod
+    def backward(ctx, grad_loss):
+        return CTCFn.backward(ctx, ctx.factor * grad_loss)
+
+
 def ctc_nll(x, targets, in_lens, tgt_lens, blank=0, is_logits=True):
     dev = x.device
     return CTCFn.apply(x, targets.to(dev), _as_len_tensor(in_lens, dev), _as_len_tensor(tgt_lens, dev),
@@ -385,6 +410,9 @@ def ctc_loss(x, targets, in_lens, tgt_lens, blank=0, reduction="mean", zero_infi
     """
     dev = x.device
     tl = _as_len_tensor(tgt_lens, dev)
+    if reduction == "mean" and zero_infinity:   # the training criterion (train.py:142): fused
+        return CTCMeanFn.apply(x, targets.to(dev), _as_len_tensor(in_lens, dev), tl, int(blank),
+                               bool(is_logits))
     nll = CTCFn.apply(x, targets.to(dev), _as_len_tensor(in_lens, dev), tl, int(blank), bool(is_logits))
     if zero_infinity:
         nll = torch.where(torch.isinf(nll), torch.zeros_like(nll), nll)
