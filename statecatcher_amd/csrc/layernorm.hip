@@ -155,26 +155,33 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(LnArgs a) {
 }
 
 // fixed-order sum of the P partial rows: out[n] = sum_p part[p][n].  A workgroup owns 64
-// columns; wave q sums rows q, q+4, ... (coalesced 256-B row segments) into 8 interleaved
-// accumulators (8 independent loads in flight), then a fixed-order 8-way and 4-way LDS sum.
-__global__ void __launch_bounds__(256) ln_part_sum_kernel(const float* part, int P, int n, float* out) {
-  __shared__ float acc4[4][64];
+// columns; its 16 waves each sum a contiguous block of rows (coalesced 256-B row segments) into
+// 8 interleaved accumulators (8 independent loads in flight), then a fixed-order LDS sum.
+__global__ void __launch_bounds__(1024) ln_part_sum_kernel(const float* part, int P, int n, float* out) {
+  __shared__ float accw[16][64];
   const int lane = threadIdx.x & 63, q = threadIdx.x >> 6;
   const int e = blockIdx.x * 64 + lane;
+  const int per = (P + 15) / 16;
+  const int p0 = q * per, p1 = min(P, p0 + per);
   float acc = 0.0f;
   if (e < n) {
     float r[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
-    int p = q;
-    for (; p + 28 < P; p += 32) {
+    int p = p0;
+    for (; p + 8 <= p1; p += 8) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) r[j] += part[(int64_t)(p + 4 * j) * n + e];
+      for (int j = 0; j < 8; ++j) r[j] += part[(int64_t)(p + j) * n + e];
     }
-    for (int j = 0; p < P; p += 4, ++j) r[j & 7] += part[(int64_t)p * n + e];
+    for (int j = 0; p < p1; ++p, ++j) r[j] += part[(int64_t)p * n + e];
     acc = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
   }
-  acc4[q][lane] = acc;
+  accw[q][lane] = acc;
   __syncthreads();
-  if (q == 0 && e < n) out[e] = (acc4[0][lane] + acc4[1][lane]) + (acc4[2][lane] + acc4[3][lane]);
+  if (q == 0 && e < n) {
+    float t = 0.0f;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) t += accw[w][lane];
+    out[e] = t;
+  }
 }
 
 constexpr int kLnBwdBlocks = 1024;   // 4 per CU: 16 waves/CU keep x and dy loads in flight
@@ -277,7 +284,7 @@ extern "C" int sc_layernorm_bwd(const void* x, const void* dy, int dtype, const 
     case SC_BF16: launch_ln_bwd<SC_BF16>(a, ch, P, st); break;
     default: launch_ln_bwd<SC_F16>(a, ch, P, st); break;
   }
-  hipLaunchKernelGGL(ln_part_sum_kernel, dim3((2 * D + 63) / 64), dim3(256), 0, st,
+  hipLaunchKernelGGL(ln_part_sum_kernel, dim3((2 * D + 63) / 64), dim3(1024), 0, st,
                      (const float*)workspace, P, 2 * D, dgamma);
   return launch_status("sc_layernorm_bwd");
 }

@@ -96,6 +96,30 @@ class SegmentTrainer:
         self.epoch = 0
         self.encoder_state: Optional[Any] = None
 
+    def _fused_clip_ok(self) -> bool:
+        opt = self.optimizer
+        return (isinstance(opt, (torch.optim.Adam, torch.optim.AdamW))
+                and all(g.get("fused") for g in opt.param_groups)
+                and getattr(opt, "found_inf", None) is None)
+
+    def _clip_and_step(self):
+        """clip_grad_norm_(max_norm) then optimizer.step() (train.py:543-552).  With a fused
+        Adam the clip coefficient is handed to the optimizer kernel as its gradient divisor
+        (grads / max(1, (norm + 1e-6) / max_norm)), which equals clip_grad_norm_'s in-place
+        scaling followed by the step, without the extra pass over every gradient."""
+        params = [p for p in self.model.parameters() if p.grad is not None]
+        if not (self._fused_clip_ok() and params and params[0].grad.is_cuda):
+            torch.nn.utils.clip_grad_norm_(self.model.parameters(), self.max_grad_norm)
+            self.optimizer.step()
+            return
+        total = torch.nn.utils.get_total_norm([p.grad for p in params], 2.0)
+        self.optimizer.grad_scale = torch.clamp((total + 1e-6) / self.max_grad_norm, min=1.0) \
+            .to(torch.float32)
+        try:
+            self.optimizer.step()
+        finally:
+            self.optimizer.grad_scale = None
+
     def begin_batch(self):
         """New server batch: the carried encoder state starts empty (train.py:460)."""
         self.encoder_state = None
@@ -116,8 +140,7 @@ class SegmentTrainer:
                     self.blank_id, input_state=self.encoder_state)
             (loss / self.accumulation_steps).backward()
         if stepping:
-            torch.nn.utils.clip_grad_norm_(self.model.parameters(), self.max_grad_norm)
-            self.optimizer.step()
+            self._clip_and_step()
             self.optimizer.zero_grad(set_to_none=True)
         if self.save_every_n_updates and (self.global_step + 1) % self.save_every_n_updates == 0 \
                 and (self.world == 1 or dist.get_rank() == 0) and self.model_dir:

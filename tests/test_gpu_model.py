@@ -14,6 +14,8 @@ module-level tests here therefore use a well-conditioned init: every gate plane 
 only enters through a smooth normaliser) gets a bias of magnitude 3 and down-scaled weights, so
 no normalised gate approaches zero and kv stays O(0.1).
 """
+import copy
+
 import numpy as np
 import pytest
 import torch
@@ -203,3 +205,30 @@ def test_segment_trainer_drives_the_hip_model_and_learns():
     assert tr.encoder_state is not None and len(tr.encoder_state[0][0]) == L
     assert all(np.isfinite(losses))
     assert np.mean(losses[-3:]) < 0.8 * np.mean(losses[:3])
+
+
+@pytest.mark.parametrize("max_norm", [50.0, 1e-3])
+def test_fused_clip_step_equals_clip_grad_norm_then_adam(max_norm):
+    """SegmentTrainer hands the clip coefficient to the fused Adam kernel as its gradient
+    divisor; parameters after the step equal torch's clip_grad_norm_ (train.py:543) followed by
+    the same fused Adam step, both when the clip is inactive (50) and active (1e-3)."""
+    from statecatcher_amd.train import SegmentTrainer
+    torch.manual_seed(4)
+    lin = [torch.nn.Linear(32, 48), torch.nn.Linear(48, 8)]
+    a = torch.nn.Sequential(*lin).to(DEV)
+    b = copy.deepcopy(a)
+    grads = [torch.randn_like(p) for p in a.parameters()]
+    oa = torch.optim.Adam(a.parameters(), lr=1e-2, fused=True)
+    ob = torch.optim.Adam(b.parameters(), lr=1e-2, fused=True)
+    tr = SegmentTrainer(a, None, oa, max_grad_norm=max_norm)
+    for _ in range(3):
+        for p, g in zip(a.parameters(), grads):
+            p.grad = g.clone()
+        for p, g in zip(b.parameters(), grads):
+            p.grad = g.clone()
+        tr._clip_and_step()
+        torch.nn.utils.clip_grad_norm_(b.parameters(), max_norm)
+        ob.step()
+        assert getattr(oa, "grad_scale", None) is None
+    for pa, pb in zip(a.parameters(), b.parameters()):
+        torch.testing.assert_close(pa, pb, rtol=1e-6, atol=1e-7)
