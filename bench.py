@@ -43,7 +43,9 @@ def parse():
     ap.add_argument("--feat", type=int, default=80)
     ap.add_argument("--segments", type=int, default=4)
     ap.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16")
-    ap.add_argument("--bucket-mb", type=float, default=50.0)
+    ap.add_argument("--bucket-mb", type=float, default=8.0,
+                    help="DDP gradient bucket size: ~one layer (7.3 MB fp32) per bucket, so each "
+                         "layer's all-reduce overlaps the backward of the layers below it")
     ap.add_argument("--cpu-baseline", choices=["on", "off"], default="on")
     ap.add_argument("--cpu-seq", type=int, default=1500,
                     help="T of the bounded CPU sample (default: one full C2 segment, ~10 s)")
@@ -191,7 +193,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    events, ops.LAUNCH_EVENTS = ops.LAUNCH_EVENTS, None
+    events, ops.LAUNCH_EVENTS = ops.LAUNCH_EVENTS or [], None
     if world > 1:
         t = torch.tensor([dt], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
