@@ -128,11 +128,28 @@ __global__ void __launch_bounds__(256) ctc_emit_kernel(CtcArgs a) {
   float lse = 0.0f;
   if (a.is_logits) {
     float m = kNegInf, l = 0.0f;
-    for (int v = lane; v < a.V; v += 64) {
-      const float xv = E::ld(p[v]);
-      const float mn = fmaxf(m, xv);
-      l = l * fexp(m - mn) + fexp(xv - mn);
-      m = mn;
+    constexpr int N = Vec16<DT>::N;
+    if ((a.V % N) == 0 && ((uintptr_t)p & 15) == 0) {   // 16-byte loads (online max per chunk)
+      for (int c = lane; c < a.V / N; c += 64) {
+        float xv[N];
+        Vec16<DT>::ld(p + N * c, xv);
+        float cm = xv[0];
+#pragma unroll
+        for (int k = 1; k < N; ++k) cm = fmaxf(cm, xv[k]);
+        const float mn = fmaxf(m, cm);
+        float cs = 0.0f;
+#pragma unroll
+        for (int k = 0; k < N; ++k) cs += fexp(xv[k] - mn);
+        l = l * fexp(m - mn) + cs;
+        m = mn;
+      }
+    } else {
+      for (int v = lane; v < a.V; v += 64) {
+        const float xv = E::ld(p[v]);
+        const float mn = fmaxf(m, xv);
+        l = l * fexp(m - mn) + fexp(xv - mn);
+        m = mn;
+      }
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -157,19 +174,22 @@ __global__ void __launch_bounds__(256) ctc_emit_kernel(CtcArgs a) {
 
 // ---------------------------------------------------------------------------- chains --------
 __global__ void __launch_bounds__(256) ctc_chain_kernel(CtcArgs a) {
+  __shared__ int lt[1024];   // the target row (Umax <= 1007)
   const int b = blockIdx.x;
   const int Ub = clampi(a.tgt_lens[b], 0, a.Umax);
   const int64_t* tg = a.tg + (int64_t)b * a.tgs;
   const int Um = a.Umax > 0 ? a.Umax : 1;
+  for (int u = threadIdx.x; u < Ub; u += blockDim.x) lt[u] = (int)tg[u];
+  __syncthreads();
   for (int u = threadIdx.x; u < Um; u += blockDim.x) {
     int nxt = -1, first = 0;
     if (u < Ub) {
-      const int64_t lab = tg[u];
+      const int lab = lt[u];
       for (int q = u + 1; q < Ub; ++q)
-        if (tg[q] == lab) { nxt = q; break; }
+        if (lt[q] == lab) { nxt = q; break; }
       first = 1;
       for (int q = 0; q < u; ++q)
-        if (tg[q] == lab) { first = 0; break; }
+        if (lt[q] == lab) { first = 0; break; }
     }
     a.ws.chain[(int64_t)b * Um + u] = nxt;
     a.ws.first[(int64_t)b * Um + u] = first;
@@ -459,6 +479,34 @@ __global__ void __launch_bounds__(256) ctc_grad_kernel(CtcArgs a) {
   __syncthreads();
   const typename E::T* xr = (const typename E::T*)a.x + (int64_t)b * a.sb + (int64_t)t * a.stt;
   const float lse = a.is_logits ? a.ws.lse[(int64_t)b * a.T + t] : 0.0f;
+  // grad = (softmax - occupancy) * scale, 8 elements per thread-iteration with 16-byte accesses
+  // when the rows allow it (the C2 shape: V = 1024 bf16)
+  const bool vec = (a.V & 7) == 0 && (((uintptr_t)xr | (uintptr_t)g) & 15) == 0;
+  if (vec) {
+    for (int c = tid; c < (a.V >> 3); c += 256) {
+      float xv[8], gv[8];
+      if constexpr (Vec16<DT>::N == 8) {
+        Vec16<DT>::ld(xr + 8 * c, xv);
+      } else {
+        Vec16<DT>::ld(xr + 8 * c, *(float(*)[4])&xv[0]);
+        Vec16<DT>::ld(xr + 8 * c + 4, *(float(*)[4])&xv[4]);
+      }
+      const float4 l0 = *(const float4*)&lcab[8 * c], l1 = *(const float4*)&lcab[8 * c + 4];
+      const float lc[8] = {l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, l1.z, l1.w};
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float lp2 = (xv[k] - lse) * kLog2e;
+        gv[k] = (exp2_(lp2) - exp2_(lc[k] + koff - lp2)) * sc;
+      }
+      if constexpr (Vec16<GT>::N == 8) {
+        Vec16<GT>::st(g + 8 * c, gv);
+      } else {
+        Vec16<GT>::st(g + 8 * c, *(float(*)[4])&gv[0]);
+        Vec16<GT>::st(g + 8 * c + 4, *(float(*)[4])&gv[4]);
+      }
+    }
+    return;
+  }
   for (int v = tid; v < a.V; v += 256) {
     const float lp2 = (E::ld(xr[v]) - lse) * kLog2e;
     const float gv = exp2_(lp2) - exp2_(lcab[v] + koff - lp2);
