@@ -22,6 +22,8 @@
  *                        train.py:142 / model.py:68-71
  *   sc_ctc_greedy_decode <- decoder.py:3-30 `ctc_greedy_decoder`
  *   sc_ctc_greedy_step   <- decoder.py:3-30 applied one frame at a time (streaming)
+ *   sc_fbank          <- make_frontend (model.py:250-279, applied at train.py:473-475):
+ *                        torchaudio MFCC / MelSpectrogram + AmplitudeToDB (unpinned, absent)
  *   sc_lucy_step_*    <- the native LucyRNN's infer-mode frame loop, lucyrnn.py:172-184, i.e.
  *                        LucyRNNCell.forward (lucyrnn.py:44-70) at T = 1 (streaming decode)
  *   sc_mlstm_*        <- the xLSTM encoder's mLSTM cell (model.py:214-229, :301-307; fork kernels
@@ -245,6 +247,25 @@ int sc_lucy_step_cell(int mode, const void* g, int dtype, int64_t g_stride, cons
                       const void* hp, const float* lnz_w, const float* lnz_b, const float* lnh_w,
                       const float* lnh_b, float eps, float* h, float* s, void* out,
                       const float* mask, int B, int D, void* stream);
+
+/* ---------------------------------------------------------------- feature frontend ------ */
+
+/* Frames of a row of n_samples (center=False): 1 + (n - 400) / 160, or 0 below 400 samples. */
+int64_t sc_fbank_frames(int64_t n_samples);
+size_t sc_fbank_workspace_bytes(void);
+
+/*
+ * make_frontend(kind)(audio).transpose(1, 2) (model.py:250-279, train.py:473-475):
+ * audio fp32 [B][audio_stride] (n_samples used per row) -> out fp32 [B][frames][80].
+ * n_fft = win = 400 (periodic Hann), hop 160, center=False, power 2, 80 HTK mel bands over
+ * [0, sample_rate/2], no filter normalisation.
+ *   kind 0 (mfcc): log(mel + 1e-6), orthonormal DCT-II, 80 coefficients;
+ *   kind 1 (mel):  10 log10(max(mel, 1e-10)), then max(x, max over the whole call - 80)
+ *                  (AmplitudeToDB(top_db=80) on a (B, 80, frames) spectrogram).
+ * workspace: sc_fbank_workspace_bytes() device bytes (kind 1 only).
+ */
+int sc_fbank(const float* audio, int B, int64_t n_samples, int64_t audio_stride, int kind,
+             float sample_rate, float* out, void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------- mLSTM ----------------- */
 

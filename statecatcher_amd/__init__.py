@@ -14,11 +14,12 @@ from .ops import (ctc_greedy_decode, ctc_loss, ctc_nll, decay_scan, lucy_scan, m
                   rnnt_loss)
 from .decoder import ctc_greedy_decoder
 from .streaming import StreamingLucyRNN
+from .frontend import make_frontend
 
 __all__ = [
     "LucyRNNConfig", "LinearSafe", "LucyRNNCellTriton", "LucyRNNtriton", "LucyRNN", "LucyRNNCell", "ASRModel", "CTCLoss",
     "compute_loss", "detach_states", "ctc_greedy_decode", "ctc_loss", "ctc_nll", "decay_scan",
     "lucy_scan", "ctc_greedy_decoder", "rnnt_loss", "RNNTLoss", "RNNTPredictorJoiner",
     "RNNTCompactPredictorJoiner", "xLSTMLarge", "xLSTMLargeConfig", "mlstm_chunkwise",
-    "StreamingLucyRNN",
+    "StreamingLucyRNN", "make_frontend",
 ]

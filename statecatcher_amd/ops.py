@@ -484,6 +484,32 @@ def lucy_step_cell(mode, g, h, s, out, lnz=None, lnh=None, u=None, hp=None, mask
     check(rc, "sc_lucy_step_cell")
 
 
+# ------------------------------------------------------------------- feature frontend --------
+def fbank(audio, kind="mfcc", sample_rate=16000):
+    """make_frontend(kind)(audio).transpose(-1, -2) on the GPU (fbank.hip): audio fp32
+    [B, N] -> [B, frames, 80] (kind "mfcc" or "mel"; see include/statecatcher.h sc_fbank).
+    For "mel", AmplitudeToDB's top_db clamp is relative to the max over the whole call."""
+    require_device(audio)
+    if audio.dim() != 2:
+        raise ValueError(f"fbank: audio must be [B, N], got {tuple(audio.shape)}")
+    codes = {"mfcc": 0, "mel": 1}
+    if kind not in codes:
+        raise ValueError(f"Unsupported frontend: {kind}")
+    a = audio.to(torch.float32)
+    if a.stride(1) != 1:
+        a = a.contiguous()
+    lib = _lib.load()
+    B, N = a.shape
+    F = lib.sc_fbank_frames(N)
+    out = torch.empty(B, F, 80, dtype=torch.float32, device=a.device)
+    wsb = lib.sc_fbank_workspace_bytes()
+    ws = torch.empty(wsb, dtype=torch.uint8, device=a.device)
+    rc = lib.sc_fbank(ptr(a), B, N, a.stride(0), codes[kind], float(sample_rate), ptr(out), ptr(ws),
+                      wsb, stream_of(a))
+    check(rc, "sc_fbank")
+    return out
+
+
 # ----------------------------------------------------------------------------- RNN-T ---------
 class RNNTFn(torch.autograd.Function):
     """nll [B] fp32 of the RNN-T lattice (rnnt.hip) over x: dense [B,T,U+1,V] or compact

@@ -184,3 +184,19 @@ def test_mlstm_oracle_vs_hf_chunkwise(name):
     np.testing.assert_allclose(C, g("cT"), rtol=2e-4, atol=2e-5 * np.abs(g("cT")).max())
     np.testing.assert_allclose(n, g("nT"), rtol=2e-4, atol=2e-5 * np.abs(g("nT")).max())
     np.testing.assert_allclose(m, g("mT"), rtol=1e-5, atol=1e-5)
+
+
+def test_fbank_oracle_vs_independent_restatement():
+    """oracle/fbank.py (torchaudio's MFCC / MelSpectrogram+AmplitudeToDB as make_frontend builds
+    them, model.py:250-279) against tests/golden/fbank.npz, produced by transformers'
+    audio_utils spectrogram / mel_filter_bank / power_to_db and scipy's orthonormal DCT
+    (tests/golden/gen_fbank.py); parity w.r.t. torchaudio itself is unpinned (absent)."""
+    from oracle import fbank as ofb
+    z = load_golden("fbank")
+    a = z["audio"]
+    p = ofb.power_spectrogram(a)
+    np.testing.assert_allclose(p, z["power"], rtol=1e-5, atol=1e-6 * np.abs(z["power"]).max())
+    np.testing.assert_allclose(p @ ofb.melscale_fbanks(), z["mel"], rtol=1e-5, atol=1e-9)
+    np.testing.assert_allclose(ofb.frontend(a, "mfcc"), z["mfcc"], rtol=1e-5, atol=1e-4)
+    np.testing.assert_allclose(ofb.frontend(a, "mel"), z["logmel_db"], rtol=1e-5, atol=1e-4)
+    assert ofb.frontend(a[:, :399], "mfcc").shape == (3, 0, 80)

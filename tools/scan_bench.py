@@ -121,3 +121,15 @@ if args.only in ("all", "mlstm"):
         qg.grad = kg.grad = vg.grad = None
         ops.mlstm_chunkwise(qg, kg, vg, igm, fgm).float().sum().backward()
     report("mlstm fwd+bwd", timeit(mb, args.iters), 3 * io + 6 * st_bytes)
+if args.only in ("all", "fbank"):
+    # one C2 batch of audio: 32 x 15 s at 16 kHz -> 1500 frames per row (make_frontend, mfcc)
+    ns = (T - 1) * 160 + 400
+    audio = [torch.randn(B, ns, device=dev) * 0.3 for _ in range(2)]
+    for kind in ("mfcc", "mel"):
+        sec = timeit(lambda i: ops.fbank(audio[i % 2], kind), args.iters)
+        # FLOPs per frame: two 20-point DFT stages (20 x 400 real MACs + 20 x 201 complex MACs),
+        # twiddles, mel bands (~2 x 201 MACs) and, for mfcc, the 80 x 80 DCT
+        flops = 2 * (20 * 400 * 2 + 20 * 201 * 4 + 400 * 4 + 402) + (2 * 80 * 80 if kind == "mfcc" else 0)
+        print(f"fbank_{kind:4s} {sec * 1e6:9.1f} us  {B * T / sec / 1e6:8.2f} M frames/s  "
+              f"{B * T * flops / sec / 1e12:6.2f} TFLOP/s fp32  "
+              f"({B * T / sec / 100:.0f}x realtime of one 100-fps stream)", flush=True)
