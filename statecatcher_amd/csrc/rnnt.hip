@@ -9,10 +9,11 @@
 //   rnnt_ab_kernel     one workgroup per (sequence, direction): alpha forward and beta backward
 //                      run concurrently.  Lane = label position u; the lattice is swept by
 //                      anti-diagonals n = t + u (all nodes of a diagonal are independent), the
-//                      neighbour (t, u-1) / (t, u+1) value crosses lanes through LDS once per
-//                      diagonal.  Values are base-2 logs with a finite "dead" sentinel and are
-//                      re-centred on the workgroup max every 8 diagonals; the running offset is
-//                      fp64 (|alpha| reaches ~1e4 at T=1500, U=150).
+//                      neighbour (t, u-1) / (t, u+1) value crosses lanes by a DPP lane shift;
+//                      waves carry a K-lane halo and exchange through LDS every K diagonals.
+//                      Values are base-2 logs with a finite "dead" sentinel and are re-centred
+//                      on the workgroup max every 2K diagonals; the running offset is fp64
+//                      (|alpha| reaches ~1e4 at T=1500, U=150), stored once per re-centring.
 //   rnnt_grad_kernel   one wave per node: occupancies of the two gathered arcs from alpha, beta
 //                      and log P (offsets recombined in fp64), then the full gradient row
 //                      (softmax-corrected when fed logits, sparse when fed log-probs).
@@ -74,6 +75,7 @@ struct RnntArgs {
   const float* scale;
   void* grad;
   int vec, nvec;   // rows read/written as 16-byte vectors: nvec per lane (V = 64 * N * nvec)
+  int kh;          // diagonals between halo exchanges of rnnt_ab_kernel (re-centring: 2 kh)
 };
 
 __device__ __forceinline__ int clampr(int64_t v, int lo, int hi) {
@@ -163,113 +165,152 @@ __device__ __forceinline__ float lse2_live(float x, float y) {
   return m + log2_(exp2_(x - m) + exp2_(y - m));
 }
 
-constexpr int kRenorm = 8;   // diagonals between re-centrings
+__device__ __forceinline__ float dpp_shr1(float v) {   // value of lane-1 (lane 0: dead)
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(kDeadR), __float_as_int(v),
+                                                     0x138, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float dpp_shl1(float v) {   // value of lane+1 (lane 63: dead)
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(kDeadR), __float_as_int(v),
+                                                     0x130, 0xf, 0xf, false));
+}
 
-__global__ void __launch_bounds__(1024) rnnt_ab_kernel(RnntArgs a) {
-  const bool is_beta = blockIdx.x >= a.B;
-  const int b = is_beta ? blockIdx.x - a.B : blockIdx.x;
-  const int u = threadIdx.x;
-  const int lane = u & 63;
-  const int w = uniform(u >> 6);
+// K (diagonals between halo exchanges) so that ceil((Umax + 1) / (64 - K)) waves fit a
+// 1024-thread group; 0 if none does
+int ab_halo_k(int Umax) {
+  for (int K : {16, 8, 4, 2, 1})
+    if ((Umax + 1 + (64 - K) - 1) / (64 - K) <= 16) return K;
+  return 0;
+}
+
+// Lane = label position u; the lattice is swept by anti-diagonals n = t + u.  On diagonal n the
+// value of node (t, u) needs (t-1, u) — the same lane on the previous diagonal — and (t, u-1)
+// (alpha) or (t, u+1) (beta) — the neighbouring lane — so a wave advances K diagonals with one
+// DPP lane shift each and no LDS.  Each wave owns 64 - K consecutive u and carries a K-lane
+// halo of its neighbour's (left for alpha, right for beta), which a missing neighbour corrupts
+// one lane per diagonal; every K diagonals the owned values are published to LDS, one barrier,
+// and the halo lanes re-read theirs.  Every second exchange re-centres on the workgroup max
+// (fp64 offset, stored once per re-centring).  Alpha/beta rows go out through buffer stores
+// whose out-of-range offset drops invalid and halo lanes (no exec-mask branches in the loop).
+template <int K, bool BETA>
+__device__ __forceinline__ void ab_run(const RnntArgs& a, int b, int Tb, int Ub) {
+  constexpr int OW = 64 - K;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int w = uniform(tid >> 6);
   const int nw = blockDim.x >> 6;
-  const int Tb = clampr(a.flen[b], 0, a.T), Ub = clampr(a.llen[b], 0, a.Umax);
-  if (Tb == 0) {   // no frames: no alignment exists
-    if (!is_beta && u == 0) {
-      a.nll[b] = __builtin_huge_valf();
-      a.ws.logp2[b] = -__builtin_huge_val();
-    }
-    return;
-  }
-  __shared__ float xb[2][1026];   // per-diagonal values at [u + 1]: entries 0 and nw*64+1 (lanes
-                                  // -1 and nw*64) stay dead
-  __shared__ float wmax[16];
+  const int u = BETA ? w * OW + lane : w * OW + lane - K;
+  const bool own = BETA ? (lane < OW) : (lane >= K);
   const int nd = Tb + Ub;          // diagonals 0 .. nd-1
   const int64_t base = (int64_t)b * a.ND * a.U1p;
+  const int uc = u < 0 ? 0 : (u >= a.U1p ? a.U1p - 1 : u);   // clamped, for addressing only
+  const int uy = BETA ? uc : (u > 0 ? min(u - 1, a.U1p - 1) : 0);
   const float* lpb = a.ws.lpb + base;
   const float* lpy = a.ws.lpy + base;
-  float* out = (is_beta ? a.ws.beta : a.ws.alpha) + base;
-  double* offp = (is_beta ? a.ws.offB : a.ws.offA) + (int64_t)b * a.ND;
-  for (int q = u; q < 1026; q += blockDim.x) {
-    xb[0][q] = kDeadR;
-    xb[1][q] = kDeadR;
-  }
-  double off = 0.0;
-  float v = kDeadR, vn = kDeadR;   // own value and neighbour's value from the previous diagonal
+  constexpr uint32_t kDrop = 0x80000000u;
+  const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
+      (BETA ? a.ws.beta : a.ws.alpha) + base, 0, (int)(4u * (uint32_t)a.ND * (uint32_t)a.U1p),
+      0x00020000);
+  double* offn = (BETA ? a.ws.offB : a.ws.offA) + (int64_t)b * a.ND;
+  if (tid == 0) offn[0] = 0.0;
+  extern __shared__ __attribute__((aligned(16))) float pub[];   // [2][nw*OW] published values
+  __shared__ float wmax[16];
+  const int nst = nw * OW;
   // emissions of diagonal step i come from workspace row r(i): alpha reads the arcs entering
   // diagonal n = i from row n-1 ((t-1,u) blank, (t,u-1) label), beta the arcs leaving row n
-  const int uy = is_beta ? u : (u > 0 ? u - 1 : 0);
   auto row_of = [&](int i) {
-    const int r = is_beta ? nd - 1 - min(i, nd - 1) : min(i, nd - 1) - 1;
+    const int r = BETA ? nd - 1 - min(i, nd - 1) : min(i, nd - 1) - 1;
     return r < 0 ? 0 : r;
   };
-  lds_barrier();
-  auto step = [&](int i, float eb, float ey) __attribute__((always_inline)) {
-    const int n = is_beta ? nd - 1 - i : i;
-    const int t = n - u;
-    const bool valid = u <= Ub && t >= 0 && t < Tb;
-    float nv;
-    if (!is_beta) {
-      // (t-1,u) --blank--> (t,u) and (t,u-1) --y[u-1]--> (t,u); the workspace holds no values
-      // for nodes outside the lattice, so each arc is taken only where it exists
-      nv = n == 0 ? (u == 0 ? 0.0f : kDeadR)
-                  : lse2_live(t >= 1 ? v + eb : kDeadR, u >= 1 ? vn + ey : kDeadR);
-    } else {
-      nv = i == 0 ? (u == Ub ? eb : kDeadR)   // terminal blank of node (Tb-1, Ub)
-                  : lse2_live(t + 1 < Tb ? v + eb : kDeadR, u < Ub ? vn + ey : kDeadR);
-    }
-    nv = valid ? fmaxf(nv, kDeadR) : kDeadR;
-    if (valid) out[(int64_t)n * a.U1p + u] = nv;
-    if (u == 0) offp[n] = off;
-    if (!is_beta && n == nd - 1 && u == Ub) {   // alpha(Tb-1, Ub) + final blank
-      const double lp = (double)nv + (double)lpb[(int64_t)n * a.U1p + u] + off;
-      a.ws.logp2[b] = lp;
-      a.nll[b] = (float)(-lp * (double)kLn2);
-    }
-    const bool renorm = (i % kRenorm) == kRenorm - 1;
-    if (renorm) {
-      float m = nv;
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-      if (lane == 0) wmax[w] = m;
-    }
-    xb[i & 1][u + 1] = nv;
-    lds_barrier();
-    // neighbour on the previous diagonal: alpha reads (t, u-1) = lane u-1; beta (t, u+1) = u+1
-    vn = xb[i & 1][is_beta ? u + 2 : u];
-    v = nv;
-    if (renorm) {
-      float m = wmax[0];
-      for (int q = 1; q < nw; ++q) m = fmaxf(m, wmax[q]);
-      if (m > 0.5f * kDeadR) {
-        v -= m;
-        vn -= m;
-        off += (double)m;
-      }
-    }
-  };
-  // emission rows prefetched kPf diagonals ahead, explicit ping-pong (no register copies)
-  constexpr int kPf = 8;
+  constexpr int kPf = 16;
   float ebA[kPf], eyA[kPf], ebB[kPf], eyB[kPf];
   auto load = [&](float (&eb)[kPf], float (&ey)[kPf], int i0) {
 #pragma unroll
     for (int j = 0; j < kPf; ++j) {
       const int64_t r = (int64_t)row_of(i0 + j) * a.U1p;
-      eb[j] = lpb[r + u];
+      eb[j] = lpb[r + uc];
       ey[j] = lpy[r + uy];
+    }
+  };
+  double off = 0.0;
+  float v = kDeadR;
+  int exch = 0;
+  auto body = [&](const float (&eb)[kPf], const float (&ey)[kPf], int i0)
+      __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < kPf; ++j) {
+      const int i = i0 + j;
+      if (i >= nd) break;
+      const int n = BETA ? nd - 1 - i : i;
+      const int t = n - u;
+      const bool valid = u >= 0 && u <= Ub && t >= 0 && t < Tb;
+      float nv;
+      if (!BETA) {
+        const float vn = dpp_shr1(v);                      // (t, u-1) on diagonal n-1
+        nv = i == 0 ? (u == 0 ? 0.0f : kDeadR)
+                    : lse2_live(t >= 1 ? v + eb[j] : kDeadR, u >= 1 ? vn + ey[j] : kDeadR);
+      } else {
+        const float vn = dpp_shl1(v);                      // (t, u+1) on diagonal n+1
+        nv = i == 0 ? (u == Ub ? eb[j] : kDeadR)           // terminal blank of (Tb-1, Ub)
+                    : lse2_live(t + 1 < Tb ? v + eb[j] : kDeadR, u < Ub ? vn + ey[j] : kDeadR);
+      }
+      v = valid ? fmaxf(nv, kDeadR) : kDeadR;
+      if (j % K == K - 1) {   // halo exchange (+ re-centre every second one)
+        const int par = exch & 1;
+        const bool norm = par == 1;
+        if (own && u < nst) pub[par * nst + u] = v;
+        if (norm) {
+          float m = own ? v : kDeadR;
+#pragma unroll
+          for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+          if (lane == 0) wmax[w] = m;
+        }
+        lds_barrier();
+        if (!own) v = (u >= 0 && u < nst) ? pub[par * nst + u] : kDeadR;
+        if (norm) {
+          float m = kDeadR;
+          for (int q = 0; q < nw; ++q) m = fmaxf(m, wmax[q]);
+          if (m > 0.5f * kDeadR) {   // all dead: keep the sentinel
+            v -= m;
+            off += (double)m;
+          }
+          if (tid == 0) offn[(exch + 1) >> 1] = off;
+        }
+        ++exch;
+      }
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), ors,
+                                            (own && valid) ? (uint32_t)(4 * u) : kDrop,
+                                            (uint32_t)n * 4u * (uint32_t)a.U1p, 0);
     }
   };
   load(ebA, eyA, 0);
   for (int i0 = 0; i0 < nd; i0 += 2 * kPf) {
     load(ebB, eyB, i0 + kPf);
-#pragma unroll
-    for (int j = 0; j < kPf; ++j)
-      if (i0 + j < nd) step(i0 + j, ebA[j], eyA[j]);
+    body(ebA, eyA, i0);
     if (i0 + kPf >= nd) break;
     load(ebA, eyA, i0 + 2 * kPf);
-#pragma unroll
-    for (int j = 0; j < kPf; ++j)
-      if (i0 + kPf + j < nd) step(i0 + kPf + j, ebB[j], eyB[j]);
+    body(ebB, eyB, i0 + kPf);
   }
+  if (!BETA && own && u == Ub) {   // log P = alpha(Tb-1, Ub) + its terminal blank
+    const double lp = (double)v + (double)lpb[(int64_t)(nd - 1) * a.U1p + Ub] + off;
+    a.ws.logp2[b] = lp;
+    a.nll[b] = (float)(-lp * (double)kLn2);
+  }
+}
+
+template <int K>
+__global__ void __launch_bounds__(1024) rnnt_ab_kernel(RnntArgs a) {
+  const bool is_beta = blockIdx.x >= a.B;
+  const int b = is_beta ? blockIdx.x - a.B : blockIdx.x;
+  const int Tb = clampr(a.flen[b], 0, a.T), Ub = clampr(a.llen[b], 0, a.Umax);
+  if (Tb == 0) {   // no frames: no alignment exists
+    if (!is_beta && threadIdx.x == 0) {
+      a.nll[b] = __builtin_huge_valf();
+      a.ws.logp2[b] = -__builtin_huge_val();
+    }
+    return;
+  }
+  if (is_beta) ab_run<K, true>(a, b, Tb, Ub);
+  else ab_run<K, false>(a, b, Tb, Ub);
 }
 
 // ---------------------------------------------------------------------------- gradient ------
@@ -320,19 +361,22 @@ __global__ void __launch_bounds__(256) rnnt_grad_kernel(RnntArgs a) {
   if (lp2 > -1e300 && sc != 0.0f) {
     const int n = t + u;
     const int64_t base = (int64_t)b * a.ND * a.U1p;
-    const double al = (double)a.ws.alpha[base + (int64_t)n * a.U1p + u] + a.ws.offA[(int64_t)b * a.ND + n];
+    // offsets: one per re-centring (every 2 kh diagonals); alpha's step index is n, beta's
+    // nd - 1 - n' for diagonal n' = n + 1
+    const int per = 2 * a.kh, nd = Tb + Ub;
+    const double oA = a.ws.offA[(int64_t)b * a.ND + (n + 1) / per];
+    const double oB = a.ws.offB[(int64_t)b * a.ND + (nd - n - 1) / per];
+    const double al = (double)a.ws.alpha[base + (int64_t)n * a.U1p + u] + oA;
     const float eb = a.ws.lpb[base + (int64_t)n * a.U1p + u];
     if (t + 1 < Tb) {
-      const double be = (double)a.ws.beta[base + (int64_t)(n + 1) * a.U1p + u] +
-                        a.ws.offB[(int64_t)b * a.ND + n + 1];
+      const double be = (double)a.ws.beta[base + (int64_t)(n + 1) * a.U1p + u] + oB;
       gb = -exp2_((float)(al + eb + be - lp2));
     } else if (u == Ub) {
       gb = -exp2_((float)(al + eb - lp2));
     }
     if (u < Ub) {
       const float ey = a.ws.lpy[base + (int64_t)n * a.U1p + u];
-      const double be = (double)a.ws.beta[base + (int64_t)(n + 1) * a.U1p + u + 1] +
-                        a.ws.offB[(int64_t)b * a.ND + n + 1];
+      const double be = (double)a.ws.beta[base + (int64_t)(n + 1) * a.U1p + u + 1] + oB;
       gy = -exp2_((float)(al + ey + be - lp2));
     }
     gb *= sc;
@@ -373,7 +417,16 @@ template <int DT>
 void launch_fwd(const RnntArgs& a, hipStream_t st) {
   const int64_t nodes = (int64_t)a.B * a.T * a.U1;
   hipLaunchKernelGGL((rnnt_emit_kernel<DT>), dim3((unsigned)((nodes + 3) / 4)), dim3(256), 0, st, a);
-  hipLaunchKernelGGL(rnnt_ab_kernel, dim3(2 * a.B), dim3(a.U1p), 0, st, a);
+  const int K = a.kh;
+  const int nw = (a.U1 + (64 - K) - 1) / (64 - K);
+  const size_t sh = 2 * (size_t)nw * (64 - K) * sizeof(float);
+  switch (K) {
+    case 16: hipLaunchKernelGGL((rnnt_ab_kernel<16>), dim3(2 * a.B), dim3(64 * nw), sh, st, a); break;
+    case 8: hipLaunchKernelGGL((rnnt_ab_kernel<8>), dim3(2 * a.B), dim3(64 * nw), sh, st, a); break;
+    case 4: hipLaunchKernelGGL((rnnt_ab_kernel<4>), dim3(2 * a.B), dim3(64 * nw), sh, st, a); break;
+    case 2: hipLaunchKernelGGL((rnnt_ab_kernel<2>), dim3(2 * a.B), dim3(64 * nw), sh, st, a); break;
+    default: hipLaunchKernelGGL((rnnt_ab_kernel<1>), dim3(2 * a.B), dim3(64 * nw), sh, st, a); break;
+  }
 }
 
 template <int DT, int GT>
@@ -388,7 +441,7 @@ int rnnt_check(const void* x, int dt, int B, int T, int Umax, int V, const int64
                const char* who) {
   SC_REQUIRE(dt == SC_F32 || dt == SC_BF16 || dt == SC_F16, "%s: unsupported dtype %d", who, dt);
   SC_REQUIRE(B >= 0 && T >= 0 && V > 0 && Umax >= 0, "%s: bad shape", who);
-  SC_REQUIRE(Umax + 1 <= 1024, "%s: max label count %d exceeds 1023", who, Umax);
+  SC_REQUIRE(ab_halo_k(Umax) > 0, "%s: max label count %d exceeds %d", who, Umax, 16 * 63 - 1);
   SC_REQUIRE(blank >= 0 && blank < V, "%s: blank %d outside [0, %d)", who, blank, V);
   SC_REQUIRE((int64_t)B * T * (Umax + 1) < (1ll << 40), "%s: lattice too large", who);
   if (B == 0 || T == 0) return 0;
@@ -428,6 +481,7 @@ RnntArgs make_args(const void* x, int is_logits, int B, int T, int Umax, int V, 
   a.grad = grad;
   a.vec = 0;
   a.nvec = 0;
+  a.kh = ab_halo_k(Umax);
   return a;
 }
 
