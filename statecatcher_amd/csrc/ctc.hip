@@ -23,8 +23,8 @@
 //                     log-sum-exp) and are re-centred on the workgroup max every 16 steps; the
 //                     running offset is kept in fp64 (at T=1500 |alpha| ~ 1e4, where an fp32
 //                     ulp would put ~0.5% error into the posteriors).
-//   ctc_grad_kernel   one workgroup per (b,t) row: label occupancies into an LDS row of V
-//                     log-sums, then one coalesced pass writing the gradient row
+//   ctc_grad_kernel   one wave per (b,t) row: label occupancies into an LDS row of V
+//                     log-sums, then one coalesced 16-byte pass writing the gradient row
 #include "sc_common.h"
 
 #ifndef SC_CTC_ABL   // ablation bitmask (timing studies only; results are wrong when set):
@@ -403,26 +403,50 @@ static int ab_halo_k(int Umax) {
 }
 
 // ---------------------------------------------------------------------------- gradient ------
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// One WAVE per (b,t) row (4 rows per workgroup, no workgroup barriers): label occupancies into a
+// per-wave LDS row of V base-2 log-sums, then the gradient row with 16-byte accesses.
 template <int DT, int GT>
 __global__ void __launch_bounds__(256) ctc_grad_kernel(CtcArgs a) {
   using E = Elem<DT>;
   using G = Elem<GT>;
-  extern __shared__ __attribute__((aligned(16))) float lcab[];   // V base-2 log-sums + 8 (m,l)
-  const int b = blockIdx.x / a.T, t = blockIdx.x % a.T;
-  const int tid = threadIdx.x;
+  extern __shared__ __attribute__((aligned(16))) float lcab_all[];   // [4][V + 4]
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t row = (int64_t)blockIdx.x * (blockDim.x >> 6) + w;
+  if (row >= (int64_t)a.B * a.T) return;
+  float* lcab = lcab_all + w * (a.V + 4);
+  const int b = (int)(row / a.T), t = (int)(row % a.T);
   const int Tb = clampi(a.in_lens[b], 0, a.T);
-  typename G::T* g = (typename G::T*)a.grad + ((int64_t)b * a.T + t) * a.V;
+  typename G::T* g = (typename G::T*)a.grad + row * a.V;
   const float sc = a.scale[b];
+  const bool gvec = (a.V & 7) == 0 && ((uintptr_t)g & 15) == 0;
   if (t >= Tb || sc == 0.0f) {
-    for (int v = tid; v < a.V; v += 256) g[v] = G::st(0.0f);
+    if (gvec) {
+      const float z[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      for (int c = lane; c < (a.V >> 3); c += 64) {
+        if constexpr (Vec16<GT>::N == 8) {
+          Vec16<GT>::st(g + 8 * c, z);
+        } else {
+          Vec16<GT>::st(g + 8 * c, *(const float(*)[4])&z[0]);
+          Vec16<GT>::st(g + 8 * c + 4, *(const float(*)[4])&z[4]);
+        }
+      }
+    } else {
+      for (int v = lane; v < a.V; v += 64) g[v] = G::st(0.0f);
+    }
     return;
   }
   const int Ub = clampi(a.tgt_lens[b], 0, a.Umax);
   const int Sb = 2 * Ub + 1;
   const int Um = a.Umax > 0 ? a.Umax : 1;
   const int64_t* tg = a.tg + (int64_t)b * a.tgs;
-  for (int v = tid; v < a.V; v += 256) lcab[v] = kNegInf;
-  __syncthreads();
+  for (int v = lane; v < a.V; v += 64) lcab[v] = kNegInf;
+  wave_lds_sync();
   const float* al = a.ws.alpha + ((int64_t)b * a.T + t) * a.Sp;
   const float* be = a.ws.beta + ((int64_t)b * a.T + t) * a.Sp;
   // exp(lcab + nll - lp) = 2^(lcab2 + offA + offB + nll*log2e - lp*log2e): fold offsets in fp64
@@ -432,8 +456,8 @@ __global__ void __launch_bounds__(256) ctc_grad_kernel(CtcArgs a) {
                              a.ws.nll64[b] * (double)kLog2e);
   const int* chain = a.ws.chain + (int64_t)b * Um;
   const int* first = a.ws.first + (int64_t)b * Um;
-  float m = kNegInf, l = 0.0f;   // blank-label occupancy (base 2), per thread
-  for (int s = tid; s < Sb; s += 256) {
+  float m = kNegInf, l = 0.0f;   // blank-label occupancy (base 2), per lane
+  for (int s = lane; s < Sb; s += 64) {
     const int lab = (s & 1) ? (int)tg[(s - 1) >> 1] : a.blank;
     const float val = al[s] + be[s];
     if (lab == a.blank) {
@@ -459,31 +483,13 @@ __global__ void __launch_bounds__(256) ctc_grad_kernel(CtcArgs a) {
     l = (mn == kNegInf) ? 0.0f : l * exp2_(m - mn) + lo * exp2_(mo - mn);
     m = mn;
   }
-  float* red = lcab + a.V;
-  const int wv = tid >> 6;
-  if ((tid & 63) == 0) {
-    red[2 * wv] = m;
-    red[2 * wv + 1] = l;
-  }
-  __syncthreads();
-  if (tid == 0) {
-    float M = kNegInf, L = 0.0f;
-    for (int q = 0; q < 4; ++q) {
-      const float mo = red[2 * q], lo = red[2 * q + 1];
-      const float mn = fmaxf(M, mo);
-      L = (mn == kNegInf) ? 0.0f : L * exp2_(M - mn) + lo * exp2_(mo - mn);
-      M = mn;
-    }
-    if (a.blank >= 0 && a.blank < a.V) lcab[a.blank] = (M == kNegInf) ? kNegInf : M + log2_(L);
-  }
-  __syncthreads();
+  if (lane == 0 && a.blank >= 0 && a.blank < a.V) lcab[a.blank] = (m == kNegInf) ? kNegInf : m + log2_(l);
+  wave_lds_sync();
   const typename E::T* xr = (const typename E::T*)a.x + (int64_t)b * a.sb + (int64_t)t * a.stt;
   const float lse = a.is_logits ? a.ws.lse[(int64_t)b * a.T + t] : 0.0f;
-  // grad = (softmax - occupancy) * scale, 8 elements per thread-iteration with 16-byte accesses
-  // when the rows allow it (the C2 shape: V = 1024 bf16)
-  const bool vec = (a.V & 7) == 0 && (((uintptr_t)xr | (uintptr_t)g) & 15) == 0;
-  if (vec) {
-    for (int c = tid; c < (a.V >> 3); c += 256) {
+  // grad = (softmax - occupancy) * scale
+  if (gvec && ((uintptr_t)xr & 15) == 0) {
+    for (int c = lane; c < (a.V >> 3); c += 64) {
       float xv[8], gv[8];
       if constexpr (Vec16<DT>::N == 8) {
         Vec16<DT>::ld(xr + 8 * c, xv);
@@ -507,7 +513,7 @@ __global__ void __launch_bounds__(256) ctc_grad_kernel(CtcArgs a) {
     }
     return;
   }
-  for (int v = tid; v < a.V; v += 256) {
+  for (int v = lane; v < a.V; v += 64) {
     const float lp2 = (E::ld(xr[v]) - lse) * kLog2e;
     const float gv = exp2_(lp2) - exp2_(lcab[v] + koff - lp2);
     g[v] = G::st(gv * sc);
@@ -535,8 +541,10 @@ static void launch_fwd(const CtcArgs& a, hipStream_t st) {
 
 template <int DT, int GT>
 static void launch_bwd(const CtcArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL((ctc_grad_kernel<DT, GT>), dim3((unsigned)((int64_t)a.B * a.T)), dim3(256),
-                     (a.V + 8) * sizeof(float), st, a);
+  // 4 rows (waves) per workgroup while their LDS rows fit the default 64 KB, else 1
+  const int R = 4 * (a.V + 4) * (int)sizeof(float) <= 65536 ? 4 : 1;
+  hipLaunchKernelGGL((ctc_grad_kernel<DT, GT>), dim3((unsigned)(((int64_t)a.B * a.T + R - 1) / R)),
+                     dim3(64 * R), R * (a.V + 4) * sizeof(float), st, a);
 }
 
 // nn.CTCLoss(reduction='mean', zero_infinity=True) on device in one launch: loss =
