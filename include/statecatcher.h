@@ -248,6 +248,20 @@ int sc_lucy_step_cell(int mode, const void* g, int dtype, int64_t g_stride, cons
                       const float* lnh_b, float eps, float* h, float* s, void* out,
                       const float* mask, int B, int D, void* stream);
 
+/* ---------------------------------------------------------------- column sums ----------- */
+
+/*
+ * out[n] = sum_m x[m][n] in fp32, fixed summation order (deterministic), x row-major [M][ld]
+ * (16-byte aligned rows) of dtype f32/bf16/f16.  The step's row reductions: the output
+ * projection's bias gradient (dy.sum(0), lucyrnn_triton.py:8-25 Linear backward), split-K
+ * weight-gradient partial sums, per-row gate-bias partials.  Optional block transpose of the
+ * output index: with N = perm_a * perm_b * C, column (a, b, c) is written at (b, a, c)
+ * (perm_a = perm_b = 1: identity).  workspace: sc_colsum_workspace_bytes(M, N) device bytes.
+ */
+size_t sc_colsum_workspace_bytes(int64_t M, int64_t N);
+int sc_colsum(const void* x, int dtype, int64_t M, int64_t N, int64_t ld, int64_t perm_a,
+              int64_t perm_b, float* out, void* workspace, size_t workspace_bytes, void* stream);
+
 /* ---------------------------------------------------------------- feature frontend ------ */
 
 /* Frames of a row of n_samples (center=False): 1 + (n - 400) / 160, or 0 below 400 samples. */

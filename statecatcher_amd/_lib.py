@@ -43,6 +43,8 @@ _SIGS = {
     "sc_ctc_bwd": (_i32, [_vp, _i32, _i32, _i32, _i32, _i32, _i64, _i64, _vp, _i64, _i32, _vp, _vp,
                          _i32, _fp, _fp, _vp, _i32, _vp, _c.c_size_t, _vp]),
     "sc_ctc_greedy_decode": (_i32, [_vp, _i32, _i32, _i32, _i32, _i64, _i64, _vp, _i32, _vp, _vp, _vp]),
+    "sc_colsum_workspace_bytes": (_c.c_size_t, [_i64, _i64]),
+    "sc_colsum": (_i32, [_vp, _i32, _i64, _i64, _i64, _i64, _i64, _fp, _vp, _c.c_size_t, _vp]),
     "sc_fbank_frames": (_i64, [_i64]),
     "sc_fbank_workspace_bytes": (_c.c_size_t, []),
     "sc_fbank": (_i32, [_vp, _i32, _i64, _i64, _i32, _c.c_float, _fp, _vp, _c.c_size_t, _vp]),

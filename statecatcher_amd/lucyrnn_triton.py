@@ -16,7 +16,7 @@ import torch
 import torch.nn as nn
 
 from .lucyrnn_conf import LucyRNNConfig
-from .ops import layer_norm, layer_norm_supported, lucy_cell, wgrad_splitk
+from .ops import colsum, layer_norm, layer_norm_supported, lucy_cell, wgrad_splitk
 
 
 class _LinearFn(torch.autograd.Function):
@@ -38,7 +38,7 @@ class _LinearFn(torch.autograd.Function):
         dy = dy.to(wc.dtype)
         dx = (dy @ wc).to(xdt) if ctx.needs_input_grad[0] else None
         dw = wgrad_splitk(dy, xc).to(wdt) if ctx.needs_input_grad[1] else None
-        db = dy.sum(0, dtype=torch.float32).to(wdt) if has_b and ctx.needs_input_grad[2] else None
+        db = colsum(dy).to(wdt) if has_b and ctx.needs_input_grad[2] else None
         return dx, dw, db, None
 
 

@@ -130,6 +130,33 @@ def lucy_scan(gates, h0, s0):
     return LucyScanFn.apply(gates, h0, s0)
 
 
+def colsum(x2d, perm=(1, 1)):
+    """fp32 column sums of a row-major [M, N] matrix (sc_colsum, deterministic); perm = (A, B)
+    writes input column (a, b, c) of an (A, B, N/(A*B)) factorisation at (b, a, c).  CPU tensors
+    (gloo tests of the training loop) use torch.sum — there is no GPU fallback."""
+    M, N = x2d.shape
+    if x2d.device.type == "cpu":
+        out = x2d.sum(0, dtype=torch.float32)
+        A, Bf = perm
+        return out if A == 1 else out.view(A, Bf, -1).transpose(0, 1).reshape(-1)
+    per16 = 16 // x2d.element_size()
+    if x2d.stride(1) != 1 or (x2d.data_ptr() % 16) or x2d.stride(0) % per16:
+        if N % per16 or perm != (1, 1):
+            # rows padded to 16 bytes (the kernel's vector loads); zero columns add nothing
+            xp = torch.zeros(M, N + (-N) % per16, dtype=x2d.dtype, device=x2d.device)
+            xp[:, :N] = x2d
+            return colsum(xp, perm)[:N]
+        x2d = x2d.contiguous()
+    lib = _lib.load()
+    out = torch.empty(N, dtype=torch.float32, device=x2d.device)
+    wsb = lib.sc_colsum_workspace_bytes(M, N)
+    ws = torch.empty(wsb, dtype=torch.uint8, device=x2d.device)
+    rc = lib.sc_colsum(ptr(x2d), dtype_code(x2d), M, N, x2d.stride(0), int(perm[0]), int(perm[1]),
+                       ptr(out), ptr(ws), wsb, stream_of(x2d))
+    check(rc, "sc_colsum")
+    return out
+
+
 def wgrad_splitk(dy, x, blocked_d=0):
     """dW = dy^T x (fp32) for dy [M,N], x [M,K] with M = B*T large: at the training shape
     dW is 3584 x 512 while M = 48000, so a plain GEMM has 28 output tiles for 256 CUs; split M
@@ -147,11 +174,9 @@ def wgrad_splitk(dy, x, blocked_d=0):
         dw = torch.matmul(dy.t(), x).float()
         return step_blocked_rows(dw, blocked_d, inverse=True) if blocked_d else dw
     part = torch.bmm(dy.view(S, M // S, N).transpose(1, 2), x.view(S, M // S, K))
-    if blocked_d:   # the reduction's output order un-permutes the rows (one pass)
-        D = blocked_d
-        return part.view(S, D // 64, 7, 64, K).transpose(1, 2).sum(0, dtype=torch.float32) \
-            .reshape(7 * D, K)
-    return part.sum(0, dtype=torch.float32)
+    # fp32 sum over the S partials; with blocked rows the sum's output order un-permutes them
+    perm = (blocked_d // 64, 7) if blocked_d else (1, 1)
+    return colsum(part.view(S, N * K), perm).view(N, K)
 
 
 def step_blocked_rows(w, D, inverse=False, dtype=None):
@@ -208,7 +233,7 @@ class LucyCellFn(torch.autograd.Function):
             with _timed("gate_gemm_wgrad", dg2, 0):
                 dw = wgrad_splitk(dg2, xc, blocked_d=(dg2.shape[1] // 7) if ctx.blocked else 0)
             dw = dw.to(wdt)
-        db = dbias.sum(0).view(-1).to(wdt) if dbias is not None else None
+        db = colsum(dbias.view(dbias.shape[0], -1)).to(wdt) if dbias is not None else None
         return dx, dw, db, dh0.to(hdt), ds0.to(sdt), None, None, None
 
 

@@ -232,3 +232,23 @@ def test_fused_clip_step_equals_clip_grad_norm_then_adam(max_norm):
         assert getattr(oa, "grad_scale", None) is None
     for pa, pb in zip(a.parameters(), b.parameters()):
         torch.testing.assert_close(pa, pb, rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("M,N,perm", [(48000, 1024, (1, 1)), (16, 3584 * 64, (8, 7)), (32, 3584, (1, 1)),
+                                      (3, 100, (1, 1)), (0, 64, (1, 1))])
+def test_colsum_vs_torch(dtype, M, N, perm):
+    """sc_colsum (the bias-gradient and split-K sums of the step): fp32 column sums equal torch's
+    fp64 sum of the same values within fp32 rounding, deterministic across calls, with the
+    step-blocked block transpose of the output index."""
+    from statecatcher_amd.ops import colsum
+    g = torch.Generator().manual_seed(M + N)
+    x = torch.randn(M, N, generator=g).to(dtype)
+    got = colsum(x.to(DEV), perm)
+    ref = x.double().sum(0)
+    A, Bf = perm
+    if A > 1:
+        ref = ref.view(A, Bf, -1).transpose(0, 1).reshape(-1)
+    tol = 1e-5 * max(1.0, float(np.sqrt(max(M, 1))))
+    torch.testing.assert_close(got.double().cpu(), ref, rtol=1e-5, atol=tol)
+    assert torch.equal(got, colsum(x.to(DEV), perm))
