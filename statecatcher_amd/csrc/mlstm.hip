@@ -12,10 +12,11 @@
 //           den_t = sum_{s<=t} W_ts (q_t.k_s)     + s e^{b_t + m_k - m_t} q_t.n~_k
 //           h_t = num_t / (max(|den_t|, e^{-m_t}) + eps)
 // Kernels (one 4-wave workgroup each; 16x16x32 bf16/f16 MFMA, fp32 accumulation, fp32 state):
-//   mlstm_fw_C   per (b,h): walks the chunks in order, the state C~ lives in MFMA accumulators,
-//                stores every chunk-start state (C~_k, n~_k, m_k) for the parallel kernels
-//   mlstm_fw_H   per (b,h,chunk): S = Q K^T, causal decay mask, H = M V + Q~ C~_k, normaliser;
-//                keeps m_t and den_t for the backward
+//   mlstm_fw_C   per (b,h, 64-column block of C~): walks the chunks in order, the state block
+//                lives in MFMA accumulators, stores every chunk-start state (C~_k, n~_k, m_k)
+//   mlstm_fw_H   per (b,h,chunk, 64-column block): S = Q K^T, causal decay mask,
+//                H[:, block] = M V[:, block] + Q~ C~_k[:, block], normaliser (S, the normaliser
+//                recomputed per block); keeps m_t and den_t for the backward
 //   mlstm_bw_dC  per (b,h): reverse walk, dC~_k = e^{g+m_k-m_{k+1}} dC~_{k+1} + Q~^T dnum
 //   mlstm_bw_dQ / _dK / _dV  per (b,h,chunk): the three input gradients (intra-chunk terms
 //                through dA = W o (dnum V^T + dden), inter-chunk terms through C~_k / dC~_{k+1})
@@ -129,6 +130,19 @@ __device__ __forceinline__ void load_rows_t(T* dst, const T* src, int tid) {
   }
 }
 
+// columns [c0, c0 + W) of chunk rows [t0, t0+64) of a [T][D] matrix, transposed into LDS
+// [W][64+kPad] (16-byte global loads; W % 8 == 0)
+template <typename T, int D, int W>
+__device__ __forceinline__ void load_cols_t(T* dst, const T* src, int c0, int tid) {
+  for (int e = tid; e < kL * W / 8; e += 256) {
+    const int r = e / (W / 8), c = (e % (W / 8)) * 8;
+    const uint4 raw = *(const uint4*)(src + (int64_t)r * D + c0 + c);
+    const T* x = (const T*)&raw;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dst[(c + j) * (kL + kPad) + r] = x[j];
+  }
+}
+
 // Gate prefix quantities of one chunk, computed by wave 0 (lane = step s) into LDS:
 // sb[s] = b_s (inclusive cumulative logsig f), si[s] = i_s; returns g = b_{L-1} in every lane
 // of wave 0 (others get 0).
@@ -170,24 +184,30 @@ __device__ __forceinline__ float sum16(float x) {
 }
 
 // ------------------------------------------------------------------------- forward: states --
+// Column block of the state: C~'s columns evolve independently (C~ += K^T diag(f) V), so each
+// workgroup owns kCB = 64 columns of one (b,h) — DV/64 x BH workgroups instead of BH; n~ and m
+// are recomputed by every block (they need K and the gates only) and stored by block 0.
+constexpr int kCB = 64;
+
 template <int DT, int DQ, int DV>
 __global__ void __launch_bounds__(256) mlstm_fw_C(MArgs a) {
   using M = MF<DT>;
   using T = typename M::T;
   using V8 = typename M::v8;
-  constexpr int TJ = DV / 16, NT = (DQ / 16) * TJ, PW = NT / 4;
+  constexpr int TJ = kCB / 16, NT = (DQ / 16) * TJ, PW = NT / 4;
   static_assert(NT % 4 == 0, "tile count must split over 4 waves");
-  const int bh = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int cb = blockIdx.x, bh = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int cj0 = cb * kCB;   // first state column of this block
   __shared__ __attribute__((aligned(16))) T KT[DQ * (kL + kPad)];
-  __shared__ __attribute__((aligned(16))) T VT[DV * (kL + kPad)];
+  __shared__ __attribute__((aligned(16))) T VT[kCB * (kL + kPad)];
   __shared__ float sb[kL], si[kL], fs[kL], scal[2];
   const T* K = (const T*)a.k + (int64_t)bh * a.T * DQ;
   const T* V = (const T*)a.v + (int64_t)bh * a.T * DV;
   f32x4 acc[PW];
-  // tile q = w + 4p: rows i in [16 (q / TJ), +16), cols j in [16 (q % TJ), +16)
+  // tile q = w + 4p: rows i in [16 (q / TJ), +16), cols j in cj0 + [16 (q % TJ), +16)
 #pragma unroll
   for (int p = 0; p < PW; ++p) {
-    const int q = w + 4 * p, i0 = 16 * (q / TJ), j0 = 16 * (q % TJ);
+    const int q = w + 4 * p, i0 = 16 * (q / TJ), j0 = cj0 + 16 * (q % TJ);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int i = i0 + 4 * (lane >> 4) + r, j = j0 + (lane & 15);
@@ -200,17 +220,19 @@ __global__ void __launch_bounds__(256) mlstm_fw_C(MArgs a) {
     float* C = a.Cs + ((int64_t)bh * (a.nc + 1) + k) * DQ * DV;
 #pragma unroll
     for (int p = 0; p < PW; ++p) {
-      const int q = w + 4 * p, i0 = 16 * (q / TJ), j0 = 16 * (q % TJ);
+      const int q = w + 4 * p, i0 = 16 * (q / TJ), j0 = cj0 + 16 * (q % TJ);
 #pragma unroll
       for (int r = 0; r < 4; ++r) C[(i0 + 4 * (lane >> 4) + r) * DV + j0 + (lane & 15)] = acc[p][r];
     }
-    if (tid < DQ) a.ns[((int64_t)bh * (a.nc + 1) + k) * DQ + tid] = n;
-    if (tid == 0) a.ms[(int64_t)bh * (a.nc + 1) + k] = m;
+    if (cb == 0) {
+      if (tid < DQ) a.ns[((int64_t)bh * (a.nc + 1) + k) * DQ + tid] = n;
+      if (tid == 0) a.ms[(int64_t)bh * (a.nc + 1) + k] = m;
+    }
   };
   for (int k = 0; k < a.nc; ++k) {
     store_state(k);
     load_rows_t<T, DQ>(KT, K + (int64_t)k * kL * DQ, tid);
-    load_rows_t<T, DV>(VT, V + (int64_t)k * kL * DV, tid);
+    load_cols_t<T, DV, kCB>(VT, V + (int64_t)k * kL * DV, cj0, tid);
     chunk_gates(a, bh, k, sb, si, tid);
     if (tid < 64) {
       const float g = __shfl(sb[63], 0);   // sb written by this wave; LDS in order
@@ -251,24 +273,26 @@ __global__ void __launch_bounds__(256) mlstm_fw_H(MArgs a) {
   using M = MF<DT>;
   using T = typename M::T;
   using V8 = typename M::v8;
-  constexpr int TJ = DV / 16;
-  const int k = blockIdx.x, bh = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  constexpr int TJ = kCB / 16;   // output column tiles of this block
+  const int k = blockIdx.x, bh = blockIdx.y, cb = blockIdx.z, tid = threadIdx.x, lane = tid & 63,
+            w = tid >> 6;
+  const int cj0 = cb * kCB;
   __shared__ __attribute__((aligned(16))) T Qs[kL * (DQ + kPad)];
   __shared__ __attribute__((aligned(16))) T Ks[kL * (DQ + kPad)];
-  __shared__ __attribute__((aligned(16))) T VT[DV * (kL + kPad)];
+  __shared__ __attribute__((aligned(16))) T VT[kCB * (kL + kPad)];
   __shared__ __attribute__((aligned(16))) T Ms[kL * (kL + kPad)];
-  __shared__ __attribute__((aligned(16))) T CT[DV * (DQ + kPad)];
+  __shared__ __attribute__((aligned(16))) T CT[kCB * (DQ + kPad)];
   __shared__ float sb[kL], si[kL], mt[kL], rowf[kL], dsum[kL], qn[kL], nk[DQ];
   const int64_t t0 = (int64_t)k * kL;
   const T* Q = (const T*)a.q + ((int64_t)bh * a.T + t0) * DQ;
   load_rows<T, DQ>(Qs, Q, tid);
   load_rows<T, DQ>(Ks, (const T*)a.k + ((int64_t)bh * a.T + t0) * DQ, tid);
-  load_rows_t<T, DV>(VT, (const T*)a.v + ((int64_t)bh * a.T + t0) * DV, tid);
+  load_cols_t<T, DV, kCB>(VT, (const T*)a.v + ((int64_t)bh * a.T + t0) * DV, cj0, tid);
   const int64_t st = (int64_t)bh * (a.nc + 1) + k;
   const float* Ck = a.Cs + st * DQ * DV;
-  for (int e = tid; e < DQ * DV; e += 256) {   // C~_k transposed to [j][i] (B operand of Q C)
-    const int i = e / DV, j = e % DV;
-    CT[j * (DQ + kPad) + i] = (T)Ck[e];
+  for (int e = tid; e < DQ * kCB; e += 256) {   // C~_k[:, block] transposed to [j][i] (B of Q C)
+    const int i = e / kCB, j = e % kCB;
+    CT[j * (DQ + kPad) + i] = (T)Ck[(int64_t)i * DV + cj0 + j];
   }
   if (tid < DQ) nk[tid] = a.ns[st * DQ + tid];
   const float mk = a.ms[st];
@@ -335,10 +359,10 @@ __global__ void __launch_bounds__(256) mlstm_fw_H(MArgs a) {
       const int t = 16 * w + 4 * (lane >> 4) + r;
       const float dn = dsum[t] + rowf[t] * qn[t];
       const float z = fmaxf(fabsf(dn), expf(-mt[t])) + a.eps;
-      H[t * DV + 16 * cj + (lane & 15)] = (T)(h4[r] / z);
+      H[t * DV + cj0 + 16 * cj + (lane & 15)] = (T)(h4[r] / z);
     }
   }
-  if (tid < kL) {
+  if (cb == 0 && tid < kL) {
     const float dn = dsum[tid] + rowf[tid] * qn[tid];
     a.mrow[(int64_t)bh * a.T + t0 + tid] = mt[tid];
     a.den[(int64_t)bh * a.T + t0 + tid] = dn;
@@ -664,8 +688,8 @@ __global__ void __launch_bounds__(256) mlstm_bw_dV(MArgs a) {
 
 template <int DT, int DQ, int DV>
 void launch_fwd(const MArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL((mlstm_fw_C<DT, DQ, DV>), dim3(a.BH), dim3(256), 0, st, a);
-  hipLaunchKernelGGL((mlstm_fw_H<DT, DQ, DV>), dim3(a.nc, a.BH), dim3(256), 0, st, a);
+  hipLaunchKernelGGL((mlstm_fw_C<DT, DQ, DV>), dim3(DV / kCB, a.BH), dim3(256), 0, st, a);
+  hipLaunchKernelGGL((mlstm_fw_H<DT, DQ, DV>), dim3(a.nc, a.BH, DV / kCB), dim3(256), 0, st, a);
 }
 template <int DT, int DQ, int DV>
 void launch_bwd(const MArgs& a, hipStream_t st) {
