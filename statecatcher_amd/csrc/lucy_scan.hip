@@ -41,6 +41,7 @@
 
 #include <atomic>
 #include <initializer_list>
+#include <type_traits>
 
 #include "sc_common.h"
 
@@ -116,7 +117,23 @@ __device__ __forceinline__ void step_terms(float r, float z, float k, float v, f
 typedef float f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f2 rsq2(f2 x) { return f2{rsq(x.x), rsq(x.y)}; }
 __device__ __forceinline__ f2 rcp2(f2 x) { return f2{rcp(x.x), rcp(x.y)}; }
-__device__ __forceinline__ f2 sigm2(f2 x) { return f2{sigm(x.x), sigm(x.y)}; }
+// sigmoid / tanh of two values: the scale and the 1 + e run as packed fp32, the exp2 and rcp
+// per component
+__device__ __forceinline__ f2 sigm2(f2 x) {
+  const f2 t = x * f2{-kLog2e, -kLog2e};
+  return rcp2(f2{1.0f, 1.0f} + f2{exp2_(t.x), exp2_(t.y)});
+}
+__device__ __forceinline__ f2 tanh2(f2 x) {   // 2 sigm(2x) - 1
+  const f2 t = x * f2{-2.0f * kLog2e, -2.0f * kLog2e};
+  const f2 r = rcp2(f2{1.0f, 1.0f} + f2{exp2_(t.x), exp2_(t.y)});
+  return r + r - f2{1.0f, 1.0f};
+}
+// Two fp32 values rounded to the element type (one v_cvt_pk_bf16_f32 for bf16).
+template <int DT> struct Pair {
+  using T = typename Elem<DT>::T;
+  typedef T t2 __attribute__((ext_vector_type(2)));
+  static __device__ __forceinline__ t2 st(f2 v) { return __builtin_convertvector(v, t2); }
+};
 
 // step_terms for two steps at once (packed fp32 for the elementwise math)
 __device__ __forceinline__ void step_terms2(f2 r, f2 z, f2 k, f2 v, f2 hp, f2 dc, f2 al, f2& zg,
@@ -278,7 +295,7 @@ lucy_scan_fwd_kernel(ScanFwdArgs a) {
   settle(gb);
   const int Tm1 = a.T - 1;
   // Past the end of the sequence the clamped step re-reads row T-1 (never out of bounds).
-  auto issue = [&](int k) {
+  auto issue = [&](int k) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
       const int p = i * 64 + lane;
@@ -291,50 +308,87 @@ lucy_scan_fwd_kernel(ScanFwdArgs a) {
       }
     }
   };
+  // Pieces of a super-chunk wholly inside the sequence need no time clamp: loop-invariant
+  // per-lane byte offsets from the wave's first step, one saddr DMA each (16-byte pieces).
+  constexpr bool kFast = NI <= 16;   // (one-element pieces: too many offsets to hold)
+  uint32_t voff[kFast ? NI : 1];
+#pragma unroll
+  for (int i = 0; i < (kFast ? NI : 0); ++i) {
+    const int p = min(i * 64 + lane, PIECES - 1);
+    const int row = p / P::PPR, pc = p % P::PPR;
+    voff[i] = (uint32_t)((row / 7) * a.g_td + (row % 7) * a.g_cd + min(pc, pcmax) * P::EPP) *
+              (uint32_t)sizeof(T);
+  }
+  auto issue_next = [&](int k) __attribute__((always_inline)) {
+    if (kFast && (k + 1) * kChunk <= a.T) {
+      const T* gt = gsrc + ((int64_t)k * kChunk + w * LC) * a.g_td;
+#pragma unroll
+      for (int i = 0; i < (kFast ? NI : 0); ++i)
+        if (PIECES % 64 == 0 || i * 64 + lane < PIECES)
+          dma_to_lds_s<PW>(gt, voff[i], slot_lds + i * 64 * (PW == 2 ? 4 : PW));
+    } else {
+      issue(k);
+    }
+  };
   if (a.nsc > 0) issue(0);
   dma_wait();
   lds_barrier();
-  for (int k = 0; k < a.nsc; ++k) {
+  // One super-chunk.  FULL: every step inside the sequence and every lane inside D (no
+  // per-step conditions); the tail super-chunk and a partial column block take the guarded one.
+  auto chunk = [&](int k, auto fullc) __attribute__((always_inline)) {
+    constexpr bool FULL = decltype(fullc)::value;
+    constexpr int LP = LC / 2;
     const int t0 = k * kChunk + w * LC;
-    float zg[LC], dec[LC], u[LC], x[LC];
+    f2 zg[LP], dec[LP], u[LP], x[LP], wz[LP];
     float gv[LC][7];
 #pragma unroll
     for (int j = 0; j < LC; ++j)
 #pragma unroll
       for (int g = 0; g < 7; ++g) gv[j][g] = E::ld(L::get(slot, (j * 7 + g) * 64 + lane)) + gb[g];
     lds_read_wait();              // slot consumed: it may be refilled with super-chunk k+1
-    if (k + 1 < a.nsc) issue(k + 1);
+    if (k + 1 < a.nsc) issue_next(k + 1);
 #pragma unroll
-    for (int j = 0; j < LC; j += 2) {   // two steps per packed instruction
-      f2 z2, d2, u2, x2;
+    for (int p = 0; p < LP; ++p) {   // two steps per packed instruction
+      const int j = 2 * p;
       step_terms2(f2{gv[j][0], gv[j + 1][0]}, f2{gv[j][1], gv[j + 1][1]},
                   f2{gv[j][2], gv[j + 1][2]}, f2{gv[j][3], gv[j + 1][3]},
                   f2{gv[j][4], gv[j + 1][4]}, f2{gv[j][5], gv[j + 1][5]},
-                  f2{gv[j][6], gv[j + 1][6]}, z2, d2, u2, x2);
-      zg[j] = z2.x; zg[j + 1] = z2.y; dec[j] = d2.x; dec[j + 1] = d2.y;
-      u[j] = u2.x; u[j + 1] = u2.y; x[j] = x2.x; x[j + 1] = x2.y;
+                  f2{gv[j][6], gv[j + 1][6]}, zg[p], dec[p], u[p], x[p]);
+      if constexpr (!FULL) {
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2) {
+          if (t0 + j + h2 >= a.T) {   // identity step past the end of the sequence
+            zg[p][h2] = 1.0f; dec[p][h2] = 1.0f; u[p][h2] = 0.0f; x[p][h2] = 0.0f;
+          }
+        }
+      }
     }
     float As = 1.0f, Bs = 0.0f;
 #pragma unroll
     for (int j = 0; j < LC; ++j) {
-      if (t0 + j >= a.T) {   // identity step past the end of the sequence
-        zg[j] = 1.0f; dec[j] = 1.0f; u[j] = 0.0f; x[j] = 0.0f;
-      }
-      As *= dec[j];
-      Bs = dec[j] * Bs + u[j];
+      As *= dec[j >> 1][j & 1];
+      Bs = fmaf(dec[j >> 1][j & 1], Bs, u[j >> 1][j & 1]);
     }
     aggS[w][lane] = make_float2(As, Bs);
     lds_barrier();
     float s = carS[k & 1][lane];
     if (w == 0 && a.ckpt && dok) a.ckpt[((int64_t)(b * a.nsc + k) * 2) * a.D + d] = s;
     s = compose_prefix<NW>(aggS, lane, w, s);
+#pragma unroll
+    for (int j = 0; j < LC; ++j) {
+      s = fmaf(dec[j >> 1][j & 1], s, u[j >> 1][j & 1]);
+      x[j >> 1][j & 1] += s;
+    }
+#pragma unroll
+    for (int p = 0; p < LP; ++p) {   // c = tanh(hn + s) and (1 - zg) c, two steps at a time
+      x[p] = tanh2(x[p]);
+      wz[p] = x[p] - zg[p] * x[p];
+    }
     float Ah = 1.0f, Bh = 0.0f;
 #pragma unroll
     for (int j = 0; j < LC; ++j) {
-      s = dec[j] * s + u[j];
-      x[j] = tanh_sig(x[j] + s);
-      Ah *= zg[j];
-      Bh = zg[j] * Bh + (1.0f - zg[j]) * x[j];
+      Ah *= zg[j >> 1][j & 1];
+      Bh = fmaf(zg[j >> 1][j & 1], Bh, wz[j >> 1][j & 1]);
     }
     if (w == NW - 1) carS[(k + 1) & 1][lane] = s;
     aggH[w][lane] = make_float2(Ah, Bh);
@@ -345,10 +399,17 @@ lucy_scan_fwd_kernel(ScanFwdArgs a) {
     h = compose_prefix<NW>(aggH, lane, w, h);
 #pragma unroll
     for (int j = 0; j < LC; ++j) {
-      h = zg[j] * h + (1.0f - zg[j]) * x[j];
-      if (dok && t0 + j < a.T) obuf.st(E::st(h), vo, (uint32_t)(t0 + j) * otd);
+      h = fmaf(zg[j >> 1][j & 1], h, wz[j >> 1][j & 1]);
+      if (FULL || (dok && t0 + j < a.T)) obuf.st(E::st(h), vo, (uint32_t)(t0 + j) * otd);
     }
     if (w == NW - 1) carH[(k + 1) & 1][lane] = h;
+  };
+  const bool blk_full = (blk + 1) * 64 <= a.D;
+  for (int k = 0; k < a.nsc; ++k) {
+    if (blk_full && (k + 1) * kChunk <= a.T)
+      chunk(k, std::true_type{});
+    else
+      chunk(k, std::false_type{});
   }
   lds_barrier();
   if (w == 0 && dok) a.s_out[(int64_t)b * a.D + d] = carS[a.nsc & 1][lane];
@@ -408,7 +469,7 @@ lucy_scan_bwd_kernel(ScanBwdArgs a) {
   for (int g = 0; g < 7; ++g) gb[g] = a.bias ? a.bias[g * a.D + dc] : 0.0f;
   settle(gb);
   const int Tm1 = a.T - 1;
-  auto issue = [&](int it) {
+  auto issue = [&](int it) __attribute__((always_inline)) {
     const int k = a.nsc - 1 - it;
     const uint32_t base = slots_lds + (uint32_t)((it % NBUF) * ROWS * 64 * L::BYTES);
 #pragma unroll
@@ -434,22 +495,69 @@ lucy_scan_bwd_kernel(ScanBwdArgs a) {
       dma_to_lds<4>(cksrc + (int64_t)(k * 2 + 1) * a.D, lds_addr(&ckS[it & 1][1][0]));
     }
   };
-  float bacc[7] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};   // bias-gradient partial sums
+  // Every super-chunk after the first one issued (the tail, k = nsc - 1) lies wholly inside
+  // the sequence, so its pieces need no time clamp: each lane's byte offset from the wave's
+  // first step is loop-invariant, and a piece is one saddr DMA off a uniform time base.  An
+  // instruction's 64 pieces are all gate rows or all dout rows (GROWS * PPR % 64 == 0).
+  static_assert((GROWS * P::PPR) % 64 == 0 && PIECES % 64 == 0, "uniform row kind per DMA");
+  uint32_t voff[NI];
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int p = i * 64 + lane;
+    const int row = p / P::PPR, pc = p % P::PPR;
+    const int col = min(pc, pcmax) * P::EPP;
+    voff[i] = (uint32_t)(row < GROWS ? (row / 7) * a.g_td + (row % 7) * a.g_cd + col
+                                     : (row - GROWS) * a.d_bd + col) * (uint32_t)sizeof(T);
+  }
+  auto issue_full = [&](int it) __attribute__((always_inline)) {
+    const int k = a.nsc - 1 - it;
+    const uint32_t base = slots_lds + (uint32_t)((it % NBUF) * ROWS * 64 * L::BYTES);
+    const int64_t t = (int64_t)k * kChunk + w * LC;
+    const T* gt = gsrc + t * a.g_td;
+    const T* dt = dsrc + t * a.d_bd;
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+      dma_to_lds_s<PW>((i * 64) / P::PPR < GROWS ? (const void*)gt : (const void*)dt, voff[i],
+                       base + i * 64 * (PW == 2 ? 4 : PW));
+    if (w == 0) {
+      dma_to_lds<4>(cksrc + (int64_t)(k * 2) * a.D, lds_addr(&ckS[it & 1][0][0]));
+      dma_to_lds<4>(cksrc + (int64_t)(k * 2 + 1) * a.D, lds_addr(&ckS[it & 1][1][0]));
+    }
+  };
+  // (one-element pieces take 64 instructions per super-chunk: too many offsets to hold)
+  auto issue_next = [&](int it) __attribute__((always_inline)) {
+    if constexpr (NI <= 16) issue_full(it); else issue(it);
+  };
+  // bias-gradient partial sums: NBUF = 2 of the fp32 gradients, even / odd steps in the two
+  // halves; NBUF = 1 (raw gates held in VGPRs) of the stored values, one register per gate
+  f2 bacc[7];
+  float bacc1[7];
+#pragma unroll
+  for (int g = 0; g < 7; ++g) {
+    bacc[g] = f2{0.0f, 0.0f};
+    bacc1[g] = 0.0f;
+  }
   if (a.nsc > 0) issue(0);
   dma_wait();
   lds_barrier();
-  for (int it = 0; it < a.nsc; ++it) {
+  // One super-chunk.  FULL: every step is inside the sequence and every lane inside D, so the
+  // body carries no per-step conditions (one basic block the scheduler can interleave); the
+  // tail super-chunk and a partial column block take the guarded instance.
+  auto chunk = [&](int it, auto fullc) __attribute__((always_inline)) {
+    constexpr bool FULL = decltype(fullc)::value;
+    constexpr int LP = LC / 2;   // step pairs: per-step values live as packed (even, odd) pairs
     const int k = a.nsc - 1 - it;
     const int t0 = k * kChunk + w * LC;
     unsigned char* slot = slots + (it % NBUF) * ROWS * 64 * L::BYTES;
-    if (NBUF == 2 && it + 1 < a.nsc) issue(it + 1);     // into the other slot
+    if (NBUF == 2 && it + 1 < a.nsc) issue_next(it + 1);     // into the other slot
     const float s_ck = ckS[it & 1][0][lane];
     const float h_ck = ckS[it & 1][1][lane];
-    float zg[LC], dec[LC], u[LC], x[LC], dj[LC], sv[LC], hv[LC];
+    f2 zg[LP], dec[LP], u[LP], x[LP], dj[LP], sv[LP], hv[LP], wz[LP];
     float rg[NBUF == 1 ? LC : 1][7];
     // ---- recompute the forward of this super-chunk ----
 #pragma unroll
-    for (int j = 0; j < LC; j += 2) {   // two steps per packed instruction
+    for (int p = 0; p < LP; ++p) {
+      const int j = 2 * p;
       f2 g7[7];
 #pragma unroll
       for (int g = 0; g < 7; ++g) {
@@ -460,61 +568,78 @@ lucy_scan_bwd_kernel(ScanBwdArgs a) {
           rg[j + 1][g] = g7[g].y;
         }
       }
-      f2 z2, d2, u2, x2;
-      step_terms2(g7[0], g7[1], g7[2], g7[3], g7[4], g7[5], g7[6], z2, d2, u2, x2);
-      zg[j] = z2.x; zg[j + 1] = z2.y; dec[j] = d2.x; dec[j + 1] = d2.y;
-      u[j] = u2.x; u[j + 1] = u2.y; x[j] = x2.x; x[j + 1] = x2.y;
+      step_terms2(g7[0], g7[1], g7[2], g7[3], g7[4], g7[5], g7[6], zg[p], dec[p], u[p], x[p]);
+      dj[p] = f2{E::ld(L::get(slot, (GROWS + j) * 64 + lane)),
+                 E::ld(L::get(slot, (GROWS + j + 1) * 64 + lane))};
+      if constexpr (!FULL) {
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2) {
+          if (t0 + j + h2 >= a.T) {   // identity step past the end of the sequence
+            zg[p][h2] = 1.0f; dec[p][h2] = 1.0f; u[p][h2] = 0.0f; x[p][h2] = 0.0f;
+            dj[p][h2] = 0.0f;
+          }
+        }
+      }
     }
     float As = 1.0f, Bs = 0.0f;
 #pragma unroll
     for (int j = 0; j < LC; ++j) {
-      dj[j] = (t0 + j < a.T) ? E::ld(L::get(slot, (GROWS + j) * 64 + lane)) : 0.0f;
-      if (t0 + j >= a.T) {
-        zg[j] = 1.0f; dec[j] = 1.0f; u[j] = 0.0f; x[j] = 0.0f;
-      }
-      As *= dec[j];
-      Bs = dec[j] * Bs + u[j];
+      As *= dec[j >> 1][j & 1];
+      Bs = fmaf(dec[j >> 1][j & 1], Bs, u[j >> 1][j & 1]);
     }
     if constexpr (NBUF == 1) {
       lds_read_wait();
-      if (it + 1 < a.nsc) issue(it + 1);                // refill the slot just read
+      if (it + 1 < a.nsc) issue_next(it + 1);                // refill the slot just read
     }
     // The Gh adjoint depends only on zg and dout, so its segment map is published with the
     // s map (one barrier); Gs needs c = tanh(hn + s) and goes out with the h map.
     float Ph = 1.0f, Qh = 0.0f;   // adjoint of h: C_t = zg_t Gh_t flows to step t-1
 #pragma unroll
     for (int j = LC - 1; j >= 0; --j) {
-      Qh = zg[j] * (dj[j] + Qh);
-      Ph *= zg[j];
+      Qh = zg[j >> 1][j & 1] * (dj[j >> 1][j & 1] + Qh);
+      Ph *= zg[j >> 1][j & 1];
     }
     aggA[w][lane] = make_float2(As, Bs);
     aggC[w][lane] = make_float2(Ph, Qh);
     if (!(SC_ABL & 8)) lds_barrier();                          // B1
     float s = s_ck;
     if (!(SC_ABL & 4)) s = compose_prefix<NW>(aggA, lane, w, s);
+    // s chain (serial), then c = tanh(hn + s) and (1 - zg) c two steps per instruction
+#pragma unroll
+    for (int j = 0; j < LC; ++j) {
+      sv[j >> 1][j & 1] = s;
+      s = fmaf(dec[j >> 1][j & 1], s, u[j >> 1][j & 1]);
+      x[j >> 1][j & 1] += s;
+    }
+#pragma unroll
+    for (int p = 0; p < LP; ++p) {
+      x[p] = tanh2(x[p]);
+      wz[p] = x[p] - zg[p] * x[p];
+    }
     float Ah = 1.0f, Bh = 0.0f;
 #pragma unroll
     for (int j = 0; j < LC; ++j) {
-      sv[j] = s;
-      s = dec[j] * s + u[j];
-      x[j] = tanh_sig(x[j] + s);
-      Ah *= zg[j];
-      Bh = zg[j] * Bh + (1.0f - zg[j]) * x[j];
+      Ah *= zg[j >> 1][j & 1];
+      Bh = fmaf(zg[j >> 1][j & 1], Bh, wz[j >> 1][j & 1]);
     }
     float C = carGh[it & 1][lane];
     if (!(SC_ABL & 4)) C = compose_suffix<NW>(aggC, lane, w, C);
 #pragma unroll
     for (int j = LC - 1; j >= 0; --j) {
-      u[j] = dj[j] + C;                                         // Gh_t
-      C = zg[j] * u[j];
+      u[j >> 1][j & 1] = dj[j >> 1][j & 1] + C;                // Gh_t
+      C = zg[j >> 1][j & 1] * u[j >> 1][j & 1];
     }
     if (w == 0) carGh[(it + 1) & 1][lane] = C;
+    // dL/d(hn + s_t) = Gh_t (1 - zg_t)(1 - c_t^2), two steps per instruction
+    f2 dp[LP];
+#pragma unroll
+    for (int p = 0; p < LP; ++p) dp[p] = (u[p] - u[p] * zg[p]) * (f2{1.0f, 1.0f} - x[p] * x[p]);
     // adjoint of s: Cs_t = dec_t Gs_t flows to step t-1
     float Ps = 1.0f, Qs = 0.0f;
 #pragma unroll
     for (int j = LC - 1; j >= 0; --j) {
-      Qs = dec[j] * (u[j] * (1.0f - zg[j]) * (1.0f - x[j] * x[j]) + Qs);
-      Ps *= dec[j];
+      Qs = dec[j >> 1][j & 1] * (dp[j >> 1][j & 1] + Qs);
+      Ps *= dec[j >> 1][j & 1];
     }
     aggB[w][lane] = make_float2(Ah, Bh);
     aggD[w][lane] = make_float2(Ps, Qs);
@@ -524,21 +649,21 @@ lucy_scan_bwd_kernel(ScanBwdArgs a) {
     if (!(SC_ABL & 4)) h = compose_prefix<NW>(aggB, lane, w, h);
 #pragma unroll
     for (int j = 0; j < LC; ++j) {
-      hv[j] = h;
-      h = zg[j] * h + (1.0f - zg[j]) * x[j];
+      hv[j >> 1][j & 1] = h;
+      h = fmaf(zg[j >> 1][j & 1], h, wz[j >> 1][j & 1]);
     }
     float Cs = carGs[it & 1][lane];
     if (!(SC_ABL & 4)) Cs = compose_suffix<NW>(aggD, lane, w, Cs);
-    float gsj[LC], dpj[LC];
+    f2 gsj[LP];
 #pragma unroll
     for (int j = LC - 1; j >= 0; --j) {   // the serial part of the Gs scan
-      dpj[j] = u[j] * (1.0f - zg[j]) * (1.0f - x[j] * x[j]);
-      gsj[j] = dpj[j] + Cs;
-      Cs = dec[j] * gsj[j];
+      gsj[j >> 1][j & 1] = dp[j >> 1][j & 1] + Cs;
+      Cs = dec[j >> 1][j & 1] * gsj[j >> 1][j & 1];
     }
     // gate gradients, two steps per packed instruction
 #pragma unroll
-    for (int jp = 0; jp < LC; jp += 2) {
+    for (int p = 0; p < LP; ++p) {
+      const int jp = 2 * p;
       f2 g7[7], o[7];
 #pragma unroll
       for (int g = 0; g < 7; ++g) {
@@ -551,24 +676,37 @@ lucy_scan_bwd_kernel(ScanBwdArgs a) {
       }
       if (SC_ABL & 1) {
 #pragma unroll
-        for (int g = 0; g < 7; ++g) o[g] = g7[g] * f2{gsj[jp], gsj[jp + 1]};
+        for (int g = 0; g < 7; ++g) o[g] = g7[g] * gsj[p];
       } else {
-        gate_grads2(g7[0], g7[1], g7[2], g7[3], g7[4], g7[5], g7[6], f2{zg[jp], zg[jp + 1]},
-                    f2{dec[jp], dec[jp + 1]}, f2{u[jp], u[jp + 1]}, f2{dpj[jp], dpj[jp + 1]},
-                    f2{gsj[jp], gsj[jp + 1]}, f2{hv[jp], hv[jp + 1]}, f2{sv[jp], sv[jp + 1]},
-                    f2{x[jp], x[jp + 1]}, o);
+        gate_grads2(g7[0], g7[1], g7[2], g7[3], g7[4], g7[5], g7[6], zg[p], dec[p], u[p], dp[p],
+                    gsj[p], hv[p], sv[p], x[p], o);
       }
+      if constexpr (FULL && NBUF == 2) {
 #pragma unroll
-      for (int h2 = 0; h2 < 2; ++h2) {
-        const int j = jp + h2;
-        if (dok && t0 + j < a.T) {
-          const uint32_t so = (uint32_t)((t0 + j) * a.dg_td * sizeof(T));
+        for (int g = 0; g < 7; ++g) bacc[g] += o[g];
+      }
+      if constexpr (FULL && WST) {   // both steps' gradients rounded by one v_cvt_pk_bf16_f32
 #pragma unroll
-          for (int g = 0; g < 7; ++g) {
-            const T og = E::st(h2 ? o[g].y : o[g].x);
-            if constexpr (WST) ((T*)slot)[(j * 7 + g) * 64 + lane] = og;   // over its raw gate
-            else if (!(SC_ABL & 2)) dgbuf.st(og, vo, so + (uint32_t)(g * a.dg_cd * sizeof(T)));
-            bacc[g] += E::ld(og);   // sum what is stored: db == dgates.sum() as a GEMM sees it
+        for (int g = 0; g < 7; ++g) {
+          const auto pr = Pair<DT>::st(o[g]);
+          ((T*)slot)[(jp * 7 + g) * 64 + lane] = pr.x;          // over its raw gate
+          ((T*)slot)[((jp + 1) * 7 + g) * 64 + lane] = pr.y;
+        }
+      } else {
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2) {
+          const int j = jp + h2;
+          if (FULL || (dok && t0 + j < a.T)) {
+            const uint32_t so = (uint32_t)((t0 + j) * a.dg_td * sizeof(T));
+#pragma unroll
+            for (int g = 0; g < 7; ++g) {
+              const float og = o[g][h2];
+              const T ogt = E::st(og);
+              if constexpr (WST) ((T*)slot)[(j * 7 + g) * 64 + lane] = ogt;   // over its raw gate
+              else if (!(SC_ABL & 2)) dgbuf.st(ogt, vo, so + (uint32_t)(g * a.dg_cd * sizeof(T)));
+              if constexpr (NBUF == 1) bacc1[g] += E::ld(ogt);
+              else if constexpr (!FULL) bacc[g][h2] += og;
+            }
           }
         }
       }
@@ -581,7 +719,7 @@ lucy_scan_bwd_kernel(ScanBwdArgs a) {
         if (SP % 64 == 0 || p < SP) {
           const int row = p >> 3, pc = p & 7;
           const int j = row / 7, g = row - 7 * (row / 7);
-          if (t0 + j < a.T && pc <= pcmax && !(SC_ABL & 2)) {
+          if ((FULL || (t0 + j < a.T && pc <= pcmax)) && !(SC_ABL & 2)) {
             const v4u v = *(const v4u*)(slot + p * 16);
             __builtin_amdgcn_raw_buffer_store_b128(
                 v, dgbuf.r, (uint32_t)(((t0 + j) * a.dg_td + g * a.dg_cd + pc * 8) * sizeof(T)), 0, 0);
@@ -590,6 +728,17 @@ lucy_scan_bwd_kernel(ScanBwdArgs a) {
       }
     }
     if (w == 0) carGs[(it + 1) & 1][lane] = Cs;
+  };
+  const bool blk_full = (blk + 1) * 64 <= a.D;
+  for (int it = 0; it < a.nsc; ++it) {
+    // (NBUF = 1 keeps 56 raw gates in VGPRs: the freer schedule of the FULL body would spill)
+    if constexpr (NBUF == 2) {
+      if (blk_full && (a.nsc - it) * kChunk <= a.T) {
+        chunk(it, std::true_type{});
+        continue;
+      }
+    }
+    chunk(it, std::false_type{});
   }
   lds_barrier();
   if (w == 0 && dok) {
@@ -599,7 +748,7 @@ lucy_scan_bwd_kernel(ScanBwdArgs a) {
   if (a.dbias) {   // reduce the per-wave partials over the NW waves (fixed order: deterministic)
 #pragma unroll
     for (int g = 0; g < 7; ++g) {
-      aggA[w][lane].x = bacc[g];
+      aggA[w][lane].x = NBUF == 1 ? bacc1[g] : bacc[g].x + bacc[g].y;
       lds_barrier();
       if (w == 0) {
         float acc = 0.0f;

@@ -172,6 +172,28 @@ __device__ __forceinline__ void dma_to_lds(const void* src, uint32_t lds_addr) {
                  : "=&s"(keep) : "v"(src), "s"(lds_addr) : "memory");
   }
 }
+// Same copy with a wave-uniform 64-bit base in SGPRs plus a per-lane 32-bit byte offset
+// (the saddr form): a loop that walks time with loop-invariant lane offsets issues each piece
+// as one instruction, with no per-lane 64-bit address arithmetic.
+template <int PW>
+__device__ __forceinline__ void dma_to_lds_s(const void* sbase, uint32_t voff, uint32_t lds_addr) {
+  lds_addr = __builtin_amdgcn_readfirstlane(lds_addr);
+  uint32_t keep;
+  if constexpr (PW == 16) {
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+                 "global_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(lds_addr) : "memory");
+  } else if constexpr (PW == 4) {
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+                 "global_load_lds_dword %1, %2\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(lds_addr) : "memory");
+  } else {
+    static_assert(PW == 2, "LDS-DMA piece width must be 2, 4 or 16 bytes");
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+                 "global_load_lds_ushort %1, %2\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(lds_addr) : "memory");
+  }
+}
 // 32-bit LDS address of a __shared__ pointer, made wave-uniform (it goes to M0)
 __device__ __forceinline__ uint32_t lds_addr(const void* p) {
   return (uint32_t)uniform((int)(uint32_t)(size_t)(__attribute__((address_space(3))) const void*)p);
