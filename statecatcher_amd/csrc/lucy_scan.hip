@@ -212,6 +212,40 @@ __device__ __forceinline__ void gate_grads2(f2 r, f2 z, f2 k, f2 v, f2 hp, f2 dc
   o[6] = gs * (k * v * f) * alp * (one - alp) * eps * (ira * ira * ira);
 }
 
+// step_terms2 for the backward's recompute, which also returns the seven per-step
+// coefficients of the gate gradients (the transcendentals are shared with the recompute, so the
+// gradient phase needs neither the raw gates nor a second pass of rsq / rcp / exp):
+//   dr = gh (h_{t-1} - c) cf0    dz = gh (h_{t-1} - c) cf1    dk = gs cf2    dv = gs cf3
+//   dh_pre = dpre cf4            ddecay = gs s_{t-1} cf5      dalpha = gs cf6
+// (gh = dL/dh_t, gs = dL/ds_t, dpre = dL/d(hn + s_t); same formulas as gate_grads).
+__device__ __forceinline__ void step_terms_bwd2(f2 r, f2 z, f2 k, f2 v, f2 hp, f2 dc, f2 al,
+                                                f2& zg, f2& dec, f2& u, f2& hn, f2 (&cf)[7]) {
+  const f2 one = {1.0f, 1.0f}, eps = {kEps, kEps}, half = {0.5f, 0.5f};
+  const f2 rc2 = (r * r + z * z) * half + eps;
+  const f2 q = (k * k + v * v) * half + eps;
+  const f2 irc = rsq2(rc2);
+  zg = sigm2(z * irc);
+  const f2 ird = rsq2(dc * dc + eps);
+  dec = sigm2(dc * ird);
+  const f2 ira = rsq2(al * al + eps);
+  const f2 alp = sigm2(al * ira);
+  const f2 irh = rsq2(hp * hp + eps);
+  hn = hp * irh;
+  const f2 iq = rsq2(q);
+  const f2 f = iq * iq * rcp2(q + eps);
+  const f2 kv = k * v * f;
+  u = alp * kv;
+  const f2 kz = zg * (one - zg) * (irc * irc * irc);
+  cf[0] = -kz * z * r * half;
+  cf[1] = kz * (r * r * half + eps);
+  const f2 fp = -(q + q + eps) * f * f;
+  cf[2] = alp * v * (f + k * k * fp);
+  cf[3] = alp * k * (f + v * v * fp);
+  cf[4] = eps * (irh * irh * irh);
+  cf[5] = dec * (one - dec) * eps * (ird * ird * ird);
+  cf[6] = kv * alp * (one - alp) * eps * (ira * ira * ira);
+}
+
 // Cross-wave composition of the per-wave affine segment maps m_q = (a, b): x -> a x + b, read
 // from LDS.  prefix: x <- m_{w-1} o ... o m_0 (x); suffix: x <- m_{w+1} o ... o m_{NW-1} (x)
 // (reverse time).  Work stays proportional to the wave's position (the chain runs only over
@@ -500,14 +534,25 @@ lucy_scan_bwd_kernel(ScanBwdArgs a) {
   // first step is loop-invariant, and a piece is one saddr DMA off a uniform time base.  An
   // instruction's 64 pieces are all gate rows or all dout rows (GROWS * PPR % 64 == 0).
   static_assert((GROWS * P::PPR) % 64 == 0 && PIECES % 64 == 0, "uniform row kind per DMA");
-  uint32_t voff[NI];
+  // The offsets are the same for every wave (the wave's first step is in the uniform base) and
+  // live in LDS, not VGPRs: the backward needs every register for its gate-gradient
+  // coefficients, and a spilled offset's scratch reload would wait vmcnt(0) on the DMA in flight.
+  constexpr int NIF = NI <= 16 ? NI : 1;
+  // dgates laid out like gates (always, from the module): the staged gradient stores of a full
+  // super-chunk reuse the gate rows' lane offsets
+  const bool same_layout = NI <= 16 && a.dg_td == a.g_td && a.dg_cd == a.g_cd;
+  __shared__ uint32_t voffT[NIF][64];
+  if constexpr (NI <= 16) {
 #pragma unroll
-  for (int i = 0; i < NI; ++i) {
-    const int p = i * 64 + lane;
-    const int row = p / P::PPR, pc = p % P::PPR;
-    const int col = min(pc, pcmax) * P::EPP;
-    voff[i] = (uint32_t)(row < GROWS ? (row / 7) * a.g_td + (row % 7) * a.g_cd + col
-                                     : (row - GROWS) * a.d_bd + col) * (uint32_t)sizeof(T);
+    for (int i = 0; i < NI; ++i) {
+      if (i % NW != w) continue;
+      const int p = i * 64 + lane;
+      const int row = p / P::PPR, pc = p % P::PPR;
+      const int col = min(pc, pcmax) * P::EPP;
+      voffT[i][lane] = (uint32_t)(row < GROWS ? (row / 7) * a.g_td + (row % 7) * a.g_cd + col
+                                              : (row - GROWS) * a.d_bd + col) *
+                       (uint32_t)sizeof(T);
+    }
   }
   auto issue_full = [&](int it) __attribute__((always_inline)) {
     const int k = a.nsc - 1 - it;
@@ -517,11 +562,12 @@ lucy_scan_bwd_kernel(ScanBwdArgs a) {
     const T* dt = dsrc + t * a.d_bd;
 #pragma unroll
     for (int i = 0; i < NI; ++i)
-      dma_to_lds_s<PW>((i * 64) / P::PPR < GROWS ? (const void*)gt : (const void*)dt, voff[i],
+      dma_to_lds_s<PW>((i * 64) / P::PPR < GROWS ? (const void*)gt : (const void*)dt, voffT[i][lane],
                        base + i * 64 * (PW == 2 ? 4 : PW));
     if (w == 0) {
-      dma_to_lds<4>(cksrc + (int64_t)(k * 2) * a.D, lds_addr(&ckS[it & 1][0][0]));
-      dma_to_lds<4>(cksrc + (int64_t)(k * 2 + 1) * a.D, lds_addr(&ckS[it & 1][1][0]));
+      const float* ck = a.ckpt + ((int64_t)b * a.nsc + k) * 2 * a.D;
+      dma_to_lds_s<4>(ck, (uint32_t)dc * 4u, lds_addr(&ckS[it & 1][0][0]));
+      dma_to_lds_s<4>(ck + a.D, (uint32_t)dc * 4u, lds_addr(&ckS[it & 1][1][0]));
     }
   };
   // (one-element pieces take 64 instructions per super-chunk: too many offsets to hold)
@@ -553,6 +599,10 @@ lucy_scan_bwd_kernel(ScanBwdArgs a) {
     const float s_ck = ckS[it & 1][0][lane];
     const float h_ck = ckS[it & 1][1][lane];
     f2 zg[LP], dec[LP], u[LP], x[LP], dj[LP], sv[LP], hv[LP], wz[LP];
+    // NBUF = 2: the gate-gradient coefficients of step_terms_bwd2 (0-3 stashed in the slot
+    // once its raw gates are consumed).  NBUF = 1 refills the slot at once: the raw gates stay
+    // in VGPRs and gate_grads2 recomputes from them.
+    f2 cf[LP][7];
     float rg[NBUF == 1 ? LC : 1][7];
     // ---- recompute the forward of this super-chunk ----
 #pragma unroll
@@ -568,7 +618,11 @@ lucy_scan_bwd_kernel(ScanBwdArgs a) {
           rg[j + 1][g] = g7[g].y;
         }
       }
-      step_terms2(g7[0], g7[1], g7[2], g7[3], g7[4], g7[5], g7[6], zg[p], dec[p], u[p], x[p]);
+      if constexpr (NBUF == 2)
+        step_terms_bwd2(g7[0], g7[1], g7[2], g7[3], g7[4], g7[5], g7[6], zg[p], dec[p], u[p],
+                        x[p], cf[p]);
+      else
+        step_terms2(g7[0], g7[1], g7[2], g7[3], g7[4], g7[5], g7[6], zg[p], dec[p], u[p], x[p]);
       dj[p] = f2{E::ld(L::get(slot, (GROWS + j) * 64 + lane)),
                  E::ld(L::get(slot, (GROWS + j + 1) * 64 + lane))};
       if constexpr (!FULL) {
@@ -580,6 +634,16 @@ lucy_scan_bwd_kernel(ScanBwdArgs a) {
           }
         }
       }
+    }
+    // Stash cf0-3 as [pair][coefficient][lane] f2 over the consumed raw gates: the gradient
+    // phase reads them back pair by pair before it writes that pair's gradients, whose bytes
+    // [1792 p, 1792 (p + 1)) never reach a later pair's stash [2048 p', ...) (p' > p).
+    f2* stash = (f2*)slot;
+    if constexpr (NBUF == 2) {
+#pragma unroll
+      for (int p = 0; p < LP; ++p)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) stash[(p * 4 + c) * 64 + lane] = cf[p][c];
     }
     float As = 1.0f, Bs = 0.0f;
 #pragma unroll
@@ -615,6 +679,7 @@ lucy_scan_bwd_kernel(ScanBwdArgs a) {
     for (int p = 0; p < LP; ++p) {
       x[p] = tanh2(x[p]);
       wz[p] = x[p] - zg[p] * x[p];
+      if constexpr (NBUF == 2) cf[p][5] *= sv[p];
     }
     float Ah = 1.0f, Bh = 0.0f;
 #pragma unroll
@@ -649,7 +714,10 @@ lucy_scan_bwd_kernel(ScanBwdArgs a) {
     if (!(SC_ABL & 4)) h = compose_prefix<NW>(aggB, lane, w, h);
 #pragma unroll
     for (int j = 0; j < LC; ++j) {
-      hv[j >> 1][j & 1] = h;
+      if constexpr (NBUF == 2)
+        hv[j >> 1][j & 1] = u[j >> 1][j & 1] * (h - x[j >> 1][j & 1]);   // Gh_t (h_{t-1} - c_t)
+      else
+        hv[j >> 1][j & 1] = h;
       h = fmaf(zg[j >> 1][j & 1], h, wz[j >> 1][j & 1]);
     }
     float Cs = carGs[it & 1][lane];
@@ -664,22 +732,26 @@ lucy_scan_bwd_kernel(ScanBwdArgs a) {
 #pragma unroll
     for (int p = 0; p < LP; ++p) {
       const int jp = 2 * p;
-      f2 g7[7], o[7];
+      f2 o[7];
+      if constexpr (NBUF == 2) {
+        const f2 gz = hv[p];   // Gh_t (h_{t-1} - c_t)
+        o[0] = gz * stash[(p * 4 + 0) * 64 + lane];
+        o[1] = gz * stash[(p * 4 + 1) * 64 + lane];
+        o[2] = gsj[p] * stash[(p * 4 + 2) * 64 + lane];
+        o[3] = gsj[p] * stash[(p * 4 + 3) * 64 + lane];
+        o[4] = dp[p] * cf[p][4];
+        o[5] = gsj[p] * cf[p][5];   // cf5 carries s_{t-1} (folded after the s scan)
+        o[6] = gsj[p] * cf[p][6];
+      } else {
+        f2 g7[7];
 #pragma unroll
-      for (int g = 0; g < 7; ++g) {
-        if constexpr (NBUF == 1) {
-          g7[g] = f2{rg[jp][g], rg[jp + 1][g]};
-        } else {
-          g7[g] = f2{E::ld(L::get(slot, (jp * 7 + g) * 64 + lane)),
-                     E::ld(L::get(slot, ((jp + 1) * 7 + g) * 64 + lane))} + gb[g];
-        }
+        for (int g = 0; g < 7; ++g) g7[g] = f2{rg[jp][g], rg[jp + 1][g]};
+        gate_grads2(g7[0], g7[1], g7[2], g7[3], g7[4], g7[5], g7[6], zg[p], dec[p], u[p], dp[p],
+                    gsj[p], hv[p], sv[p], x[p], o);
       }
       if (SC_ABL & 1) {
 #pragma unroll
-        for (int g = 0; g < 7; ++g) o[g] = g7[g] * gsj[p];
-      } else {
-        gate_grads2(g7[0], g7[1], g7[2], g7[3], g7[4], g7[5], g7[6], zg[p], dec[p], u[p], dp[p],
-                    gsj[p], hv[p], sv[p], x[p], o);
+        for (int g = 0; g < 7; ++g) o[g] = gsj[p];
       }
       if constexpr (FULL && NBUF == 2) {
 #pragma unroll
@@ -721,15 +793,23 @@ lucy_scan_bwd_kernel(ScanBwdArgs a) {
           const int j = row / 7, g = row - 7 * (row / 7);
           if ((FULL || (t0 + j < a.T && pc <= pcmax)) && !(SC_ABL & 2)) {
             const v4u v = *(const v4u*)(slot + p * 16);
-            __builtin_amdgcn_raw_buffer_store_b128(
-                v, dgbuf.r, (uint32_t)(((t0 + j) * a.dg_td + g * a.dg_cd + pc * 8) * sizeof(T)), 0, 0);
+            if constexpr (FULL)   // lane offset from the gate DMA table, time in soffset
+              __builtin_amdgcn_raw_buffer_store_b128(v, dgbuf.r, voffT[i][lane],
+                                                     (uint32_t)(t0 * a.dg_td * sizeof(T)), 0);
+            else
+              __builtin_amdgcn_raw_buffer_store_b128(   // (a batch row is < 2 GiB: 32-bit math)
+                  v, dgbuf.r,
+                  ((uint32_t)(t0 + j) * (uint32_t)a.dg_td + (uint32_t)g * (uint32_t)a.dg_cd +
+                   (uint32_t)pc * 8u) * (uint32_t)sizeof(T),
+                  0, 0);
           }
         }
       }
     }
     if (w == 0) carGs[(it + 1) & 1][lane] = Cs;
   };
-  const bool blk_full = (blk + 1) * 64 <= a.D;
+  // (WST: the FULL body stores through the gate offset table, so dgates must share the layout)
+  const bool blk_full = (blk + 1) * 64 <= a.D && (!WST || same_layout);
   for (int it = 0; it < a.nsc; ++it) {
     // (NBUF = 1 keeps 56 raw gates in VGPRs: the freer schedule of the FULL body would spill)
     if constexpr (NBUF == 2) {
