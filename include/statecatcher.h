@@ -262,6 +262,21 @@ size_t sc_colsum_workspace_bytes(int64_t M, int64_t N);
 int sc_colsum(const void* x, int dtype, int64_t M, int64_t N, int64_t ld, int64_t perm_a,
               int64_t perm_b, float* out, void* workspace, size_t workspace_bytes, void* stream);
 
+/* ---------------------------------------------------------------- weight-gradient GEMM -- */
+
+/*
+ * Split-L weight gradient of a projection: part[s] = A[Ls]^T B[Ls] (fp32 [I][J] slab per
+ * L-split s) for A = dY bf16 [L][lda], B = X bf16 [L][ldb] — the backward of LinearSafe
+ * (lucyrnn_triton.py:20-25: dW = dgates^T x) and of output_proj (lucyrnn_triton.py:107-109).
+ * Sum the S slabs with sc_colsum (fixed order; it also un-permutes step-blocked rows).
+ * Needs L % 64 == 0, J % 256 == 0, I % 224 == 0 or I % 256 == 0, 16-byte aligned operands and
+ * leading dimensions; sc_gemm_wgrad_splits returns the split count for a shape (0: unsupported,
+ * use a library GEMM).  part: S * I * J floats.
+ */
+int sc_gemm_wgrad_splits(int L, int I, int J);
+int sc_gemm_wgrad_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, float* part, int L,
+                       int I, int J, int S, void* stream);
+
 /* ---------------------------------------------------------------- feature frontend ------ */
 
 /* Frames of a row of n_samples (center=False): 1 + (n - 400) / 160, or 0 below 400 samples. */

@@ -22,6 +22,8 @@ ABI_VERSION = 2  # include/statecatcher.h; bumped on any signature change
 
 _SIGS = {
     "sc_abi_version": (_i32, []),
+    "sc_gemm_wgrad_splits": (_i32, [_i32, _i32, _i32]),
+    "sc_gemm_wgrad_bf16": (_i32, [_vp, _i64, _vp, _i64, _fp, _i32, _i32, _i32, _i32, _vp]),
     "sc_last_error": (_c.c_char_p, []),
     "sc_lucy_scan_chunk": (_i32, []),
     "sc_lucy_scan_ckpt_numel": (_i64, [_i32, _i32, _i32]),

@@ -164,6 +164,10 @@ def wgrad_splitk(dy, x, blocked_d=0):
     step-blocked order (step_blocked_rows); the sum writes dW back in the reference's order."""
     M, N = dy.shape
     K = x.shape[1]
+    if dy.device.type != "cpu" and dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16:
+        dw = wgrad_mfma(dy, x, blocked_d)
+        if dw is not None:
+            return dw
     S = 1
     # measured on MI355X at M=48000, N=3584, K=512 (tools/gemm_probe.py): S=1 410 TF/s,
     # S=8 760, S=16 860
@@ -175,6 +179,25 @@ def wgrad_splitk(dy, x, blocked_d=0):
         return step_blocked_rows(dw, blocked_d, inverse=True) if blocked_d else dw
     part = torch.bmm(dy.view(S, M // S, N).transpose(1, 2), x.view(S, M // S, K))
     # fp32 sum over the S partials; with blocked rows the sum's output order un-permutes them
+    perm = (blocked_d // 64, 7) if blocked_d else (1, 1)
+    return colsum(part.view(S, N * K), perm).view(N, K)
+
+
+def wgrad_mfma(dy, x, blocked_d=0):
+    """dW = dy^T x in fp32 on the MFMA split-L kernel (sc_gemm_wgrad_bf16: gemm.hip) plus the
+    fixed-order slab sum (sc_colsum, which also un-permutes step-blocked rows), or None when the
+    shape is outside the kernel's tiling (the caller uses the library GEMM)."""
+    M, N = dy.shape
+    K = x.shape[1]
+    lib = _lib.load()
+    S = lib.sc_gemm_wgrad_splits(M, N, K)
+    if not S or dy.stride(1) != 1 or x.stride(1) != 1 or dy.stride(0) % 8 or x.stride(0) % 8 \
+            or dy.data_ptr() % 16 or x.data_ptr() % 16:
+        return None
+    part = torch.empty(S, N, K, dtype=torch.float32, device=dy.device)
+    rc = lib.sc_gemm_wgrad_bf16(ptr(dy), dy.stride(0), ptr(x), x.stride(0), ptr(part), M, N, K, S,
+                                stream_of(dy))
+    check(rc, "sc_gemm_wgrad_bf16")
     perm = (blocked_d // 64, 7) if blocked_d else (1, 1)
     return colsum(part.view(S, N * K), perm).view(N, K)
 
