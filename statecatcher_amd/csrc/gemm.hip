@@ -58,6 +58,15 @@ constexpr int kSlots = SC_GEMM_SLOTS;
 #ifndef SC_GEMM_STAGGER
 #define SC_GEMM_STAGGER 0
 #endif
+// SC_GEMM_PRIO: s_setprio(1) around each half-stage's MFMAs (measured 1-2% slower).
+// SC_GEMM_SGB: sched_group_barrier interleave of the transposed reads with the MFMAs, one read
+// after each MFMA (measured 2-3% faster than the compiler's own order: 184-187 vs 191 us)
+#ifndef SC_GEMM_PRIO
+#define SC_GEMM_PRIO 0
+#endif
+#ifndef SC_GEMM_SGB
+#define SC_GEMM_SGB 1
+#endif
 
 struct WgradArgs {
   const __bf16* A;   // dY [L][lda]
@@ -207,7 +216,18 @@ __global__ void __launch_bounds__(512) wgrad_kernel(WgradArgs a) {
     const bool st = h + kSlots < nh && !(SC_GEMM_ABL & 2);
     if (!late && st) stage(h + kSlots);
     if (h + 1 < nh) load_frags(h + 1, bn, an);
+    if (SC_GEMM_PRIO) __builtin_amdgcn_s_setprio(1);
     mfmas(bc, ac);
+    if (SC_GEMM_PRIO) __builtin_amdgcn_s_setprio(0);
+#if SC_GEMM_SGB
+    // interleave: one transposed read after each MFMA, then the remaining MFMAs
+#pragma unroll
+    for (int q = 0; q < 2 * (4 + TTI); ++q) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // DS read
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 4 * TTI - 2 * (4 + TTI), 0);
+#endif
     if (late && st) stage(h + kSlots);
   };
   int h = 0;
