@@ -53,6 +53,22 @@ namespace sc {
 #ifndef SC_ABL
 #define SC_ABL 0
 #endif
+// SC_SCAN_LW (forward): retire the next super-chunk's gate DMA at the END of the current one
+// (just before its own output stores) instead of before its second barrier, so the DMA has the
+// whole super-chunk to land.  (The backward keeps its wait before B2: its checkpoint rows are one
+// shared copy that other waves read after B2, and per-wave copies measured 3% slower in-step.)  The slots are wave-private: the issuing wave's own vmcnt orders its later
+// ds_reads, no barrier needed (MI355X_MICROARCH.md item 7).  SC_FWD_FD: LDS slots per wave in the
+// forward (2: two super-chunks in flight, 16-bit gates).  SC_FWD_CSW: forward prefix
+// compositions with the wave's position as a compile-time count (one LDS round trip).
+#ifndef SC_SCAN_LW
+#define SC_SCAN_LW 1
+#endif
+#ifndef SC_FWD_FD
+#define SC_FWD_FD 1
+#endif
+#ifndef SC_FWD_CSW
+#define SC_FWD_CSW 0
+#endif
 
 constexpr int kChunk = 64;
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));   // time steps per super-chunk (== NW * LC for every variant)
@@ -286,8 +302,31 @@ __device__ __forceinline__ float compose_suffix(const float2 (*agg)[64], int lan
   return x;
 }
 
+// Prefix composition with the wave's position as a compile-time count: one uniform branch picks
+// the instance, whose W map fetches all issue before the first link (one LDS round trip instead
+// of one per group of four).  Forward only: the backward has no registers for 2 W map values.
+template <int W>
+__device__ __forceinline__ float prefix_fixed(const float2 (*agg)[64], int lane, float x) {
+  if constexpr (W > 0) {
+    float2 m[W];
+#pragma unroll
+    for (int q = 0; q < W; ++q) m[q] = agg[q][lane];
+#pragma unroll
+    for (int q = 0; q < W; ++q) x = fmaf(m[q].x, x, m[q].y);
+  }
+  return x;
+}
+template <int NW, int W = 0>
+__device__ __forceinline__ float compose_prefix_sw(const float2 (*agg)[64], int lane, int w, float x) {
+  if constexpr (W == NW - 1)
+    return prefix_fixed<W>(agg, lane, x);
+  else
+    return w == W ? prefix_fixed<W>(agg, lane, x) : compose_prefix_sw<NW, W + 1>(agg, lane, w, x);
+}
+
 // ------------------------------------------------------------------------ forward ----------
-template <int DT, int NW, int LC, int PW>
+// FD: LDS slots per wave (fetch depth), ring by super-chunk index.
+template <int DT, int NW, int LC, int PW, int FD>
 __global__ void __launch_bounds__(NW * 64)
 lucy_scan_fwd_kernel(ScanFwdArgs a) {
   static_assert(NW * LC == kChunk, "super-chunk must be 64 steps");
@@ -312,8 +351,9 @@ lucy_scan_fwd_kernel(ScanFwdArgs a) {
   __shared__ float carS[2][64];
   __shared__ float carH[2][64];
   using L = LdsElem<T, PW>;
-  const unsigned char* slot = dyn_lds + w * ROWS * 64 * L::BYTES;   // wave-private [LC][7][64]
-  const uint32_t slot_lds = lds_addr(slot);
+  constexpr int SLOTB = ROWS * 64 * L::BYTES;                       // wave-private [LC][7][64]
+  const unsigned char* slots = dyn_lds + w * FD * SLOTB;            // FD of them
+  const uint32_t slots_lds = lds_addr(slots);
 
   const T* gsrc = (const T*)a.gates + (int64_t)b * a.g_bt + (int64_t)blk * a.g_cb;
   const Buf<T> obuf((T*)a.out + (int64_t)b * a.o_bt);
@@ -338,7 +378,7 @@ lucy_scan_fwd_kernel(ScanFwdArgs a) {
         const int j = row / 7, g = row - 7 * (row / 7);
         const int t = min(k * kChunk + w * LC + j, Tm1);
         dma_to_lds<PW>(gsrc + (int64_t)t * a.g_td + (int64_t)g * a.g_cd + min(pc, pcmax) * P::EPP,
-                       slot_lds + i * 64 * (PW == 2 ? 4 : PW));
+                       slots_lds + (uint32_t)((k % FD) * SLOTB) + i * 64 * (PW == 2 ? 4 : PW));
       }
     }
   };
@@ -359,13 +399,19 @@ lucy_scan_fwd_kernel(ScanFwdArgs a) {
 #pragma unroll
       for (int i = 0; i < (kFast ? NI : 0); ++i)
         if (PIECES % 64 == 0 || i * 64 + lane < PIECES)
-          dma_to_lds_s<PW>(gt, voff[i], slot_lds + i * 64 * (PW == 2 ? 4 : PW));
+          dma_to_lds_s<PW>(gt, voff[i], slots_lds + (uint32_t)((k % FD) * SLOTB) + i * 64 * (PW == 2 ? 4 : PW));
     } else {
       issue(k);
     }
   };
+  // retire super-chunk k+1's DMA; with two slots, k+2's (the only younger loads) may fly on
+  auto wait_next = [&](int k) __attribute__((always_inline)) {
+    if (FD == 2 && k + 2 < a.nsc) dma_wait_younger<NI>();
+    else dma_wait();
+  };
   if (a.nsc > 0) issue(0);
-  dma_wait();
+  if (FD == 2 && a.nsc > 1) issue(1);
+  wait_next(-1);
   lds_barrier();
   // One super-chunk.  FULL: every step inside the sequence and every lane inside D (no
   // per-step conditions); the tail super-chunk and a partial column block take the guarded one.
@@ -375,12 +421,13 @@ lucy_scan_fwd_kernel(ScanFwdArgs a) {
     const int t0 = k * kChunk + w * LC;
     f2 zg[LP], dec[LP], u[LP], x[LP], wz[LP];
     float gv[LC][7];
+    const unsigned char* slot = slots + (k % FD) * SLOTB;
 #pragma unroll
     for (int j = 0; j < LC; ++j)
 #pragma unroll
       for (int g = 0; g < 7; ++g) gv[j][g] = E::ld(L::get(slot, (j * 7 + g) * 64 + lane)) + gb[g];
-    lds_read_wait();              // slot consumed: it may be refilled with super-chunk k+1
-    if (k + 1 < a.nsc) issue_next(k + 1);
+    lds_read_wait();              // slot consumed: it may be refilled with super-chunk k+FD
+    if (k + FD < a.nsc) issue_next(k + FD);
 #pragma unroll
     for (int p = 0; p < LP; ++p) {   // two steps per packed instruction
       const int j = 2 * p;
@@ -406,8 +453,8 @@ lucy_scan_fwd_kernel(ScanFwdArgs a) {
     aggS[w][lane] = make_float2(As, Bs);
     lds_barrier();
     float s = carS[k & 1][lane];
-    if (w == 0 && a.ckpt && dok) a.ckpt[((int64_t)(b * a.nsc + k) * 2) * a.D + d] = s;
-    s = compose_prefix<NW>(aggS, lane, w, s);
+    const float s_in = s;
+    s = SC_FWD_CSW ? compose_prefix_sw<NW>(aggS, lane, w, s) : compose_prefix<NW>(aggS, lane, w, s);
 #pragma unroll
     for (int j = 0; j < LC; ++j) {
       s = fmaf(dec[j >> 1][j & 1], s, u[j >> 1][j & 1]);
@@ -426,17 +473,28 @@ lucy_scan_fwd_kernel(ScanFwdArgs a) {
     }
     if (w == NW - 1) carS[(k + 1) & 1][lane] = s;
     aggH[w][lane] = make_float2(Ah, Bh);
-    dma_wait();                   // super-chunk k+1 has landed in this wave's slot
+    if (!SC_SCAN_LW) wait_next(k);   // super-chunk k+1 has landed in this wave's slot
     lds_barrier();
     float h = carH[k & 1][lane];
-    if (w == 0 && a.ckpt && dok) a.ckpt[((int64_t)(b * a.nsc + k) * 2 + 1) * a.D + d] = h;
-    h = compose_prefix<NW>(aggH, lane, w, h);
+    const float h_in = h;
+    h = SC_FWD_CSW ? compose_prefix_sw<NW>(aggH, lane, w, h) : compose_prefix<NW>(aggH, lane, w, h);
+    float hs[LC];
 #pragma unroll
     for (int j = 0; j < LC; ++j) {
       h = fmaf(zg[j >> 1][j & 1], h, wz[j >> 1][j & 1]);
-      if (FULL || (dok && t0 + j < a.T)) obuf.st(E::st(h), vo, (uint32_t)(t0 + j) * otd);
+      hs[j] = h;
     }
     if (w == NW - 1) carH[(k + 1) & 1][lane] = h;
+    // late wait: retire super-chunk k+1's DMA before this super-chunk's own stores (a store
+    // issued before a full vmcnt wait would be drained with it)
+    if (SC_SCAN_LW) wait_next(k);
+    if (w == 0 && a.ckpt && dok) {
+      a.ckpt[((int64_t)(b * a.nsc + k) * 2) * a.D + d] = s_in;
+      a.ckpt[((int64_t)(b * a.nsc + k) * 2 + 1) * a.D + d] = h_in;
+    }
+#pragma unroll
+    for (int j = 0; j < LC; ++j)
+      if (FULL || (dok && t0 + j < a.T)) obuf.st(E::st(hs[j]), vo, (uint32_t)(t0 + j) * otd);
   };
   const bool blk_full = (blk + 1) * 64 <= a.D;
   for (int k = 0; k < a.nsc; ++k) {
@@ -862,8 +920,9 @@ static bool set_lds_limit(K kernel, size_t bytes) {
 template <int DT, int PW>
 static void launch_fwd(const ScanFwdArgs& a, hipStream_t st) {
   using T = typename Elem<DT>::T;
-  auto kern = lucy_scan_fwd_kernel<DT, kNW, kLC, PW>;
-  const size_t lds = (size_t)kNW * kLC * 7 * 64 * LdsElem<T, PW>::BYTES;
+  constexpr int FD = (SC_FWD_FD >= 2 && LdsElem<T, PW>::BYTES == 2) ? 2 : 1;   // 2 x 56 KiB fit
+  auto kern = lucy_scan_fwd_kernel<DT, kNW, kLC, PW, FD>;
+  const size_t lds = (size_t)FD * kNW * kLC * 7 * 64 * LdsElem<T, PW>::BYTES;
   static const bool lds_ok = set_lds_limit(kern, lds);
   (void)lds_ok;
   dim3 grid((a.D + 63) / 64, a.B);

@@ -208,6 +208,15 @@ __device__ __forceinline__ void settle(float (&v)[N]) {
   for (int i = 0; i < N; ++i) asm volatile("" : "+v"(v[i]));
 }
 __device__ __forceinline__ void dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// Retire every DMA but the N youngest vector-memory LOADS.  Loads complete in issue order among
+// themselves; stores may complete out of order with them, but they only make the counter larger:
+// with at most N operations outstanding and the N youngest loads possibly among them, every
+// older load has completed.  (Valid only when no other load was issued after those N.)
+template <int N>
+__device__ __forceinline__ void dma_wait_younger() {
+  static_assert(N >= 0 && N <= 63, "gfx9 vmcnt is 6 bits");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
 __device__ __forceinline__ void lds_read_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 // Workgroup barrier that orders LDS only.  __syncthreads() carries a workgroup fence that makes
