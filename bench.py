@@ -7,7 +7,7 @@ bf16 autocast GEMMs + bf16 gates (fp32 recurrent state), Adam lr 3e-4, clip_grad
 4 consecutive segments per batch with the encoder state carried (detached) between them.
 One step = forward + CTC + backward + (DDP all-reduce) + clip + Adam over one B x T segment.
 
-    python bench.py [--gpus N --steps K --warmup W]
+    python bench.py [--gpus N --steps K --warmup W]   (N > 1: spawns N rank processes itself)
     torchrun --nproc-per-node N ... bench.py --gpus N   (one rank per GPU, RCCL)
 
 Prints ONE JSON line on rank 0.  value = frames processed by all ranks / max-over-ranks time.
@@ -103,19 +103,125 @@ def cpu_baseline(args):
     t0 = time.perf_counter()
     loss, state, _, adam = lucy_step.train_step(p, feats, tok, in_lens, U, args.layers, args.hidden)
     dt = time.perf_counter() - t0
+    model = cpu_model()
     return {"value": round(B * T / dt, 1), "unit": "audio-frames/s", "cores": int(threads),
             "kind": "port",
             "sample": f"oracle/lucy_step.py numpy fp32 (CTC fp64) train step, B={B} T={T} "
                       f"(U~[{T // 30},{T // 10}]), {args.layers}x{args.hidden}, 1 step, "
-                      f"{dt:.1f} s on {platform.processor() or platform.machine()} "
-                      f"(os.cpu_count={os.cpu_count()}, BLAS threads={threads})"}
+                      f"{dt:.1f} s on {model} (os.cpu_count={os.cpu_count()}, BLAS threads="
+                      f"{threads} = this job's CPU share)",
+            "c1_nn_lstm": c1_lstm_baseline()}
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:   # pragma: no cover
+        pass
+    return platform.processor() or platform.machine()
+
+
+def c1_lstm_baseline(seconds=4.0):
+    """BASELINE.json configs[0] (C1): torch.nn.LSTM(80, 256, 2) + Linear(256 -> 1024) +
+    nn.CTCLoss(blank=0, zero_infinity=True), fwd + bwd + Adam, B=4, T=200, on the host CPU with
+    torch's intra-op threads (model.py:203-212, train.py:142).  Pure PyTorch, not reference code."""
+    import torch.nn as nn
+    g = torch.Generator().manual_seed(7)
+    B, T, V = 4, 200, 1024
+    lstm = nn.LSTM(80, 256, num_layers=2, batch_first=True)
+    cls = nn.Linear(256, V)
+    crit = nn.CTCLoss(blank=0, zero_infinity=True)
+    opt = torch.optim.Adam(list(lstm.parameters()) + list(cls.parameters()), lr=3e-4)
+    feats = torch.randn(B, T, 80, generator=g)
+    U = torch.randint(5, 21, (B,), generator=g)
+    tok = torch.randint(1, V, (B, 20), generator=g)
+
+    def step():
+        out, _ = lstm(feats)
+        loss = crit(cls(out).log_softmax(-1).transpose(0, 1), tok, [T] * B, U.tolist())
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+
+    step()   # warm-up (first call allocates)
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        step()
+        n += 1
+    dt = time.perf_counter() - t0
+    return {"value": round(n * B * T / dt, 1), "unit": "audio-frames/s",
+            "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"C1 nn.LSTM 2x256 + Linear + CTC fwd+bwd+Adam, B={B} T={T}, {n} steps in "
+                      f"{dt:.1f} s, torch CPU threads={torch.get_num_threads()}"}
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def rank_envs(n, port, base=None):
+    """torchrun's per-rank environment for n ranks on this node (rendezvous on 127.0.0.1)."""
+    base = dict(os.environ if base is None else base)
+    base.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # dmabuf IPC for RCCL on this host
+    envs = []
+    for r in range(n):
+        e = dict(base)
+        e.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                 GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        envs.append(e)
+    return envs
+
+
+def spawn_ranks(n, cmd, port=None):
+    """Run `cmd` as n child processes, one per GPU rank, and return the first non-zero exit
+    code (0 if all ranks succeed).  The parent never initialises HIP: children are started as
+    new processes (no fork of a HIP context, no exec of this one).  If a rank fails the others
+    are terminated, so a hung collective cannot outlive the failure."""
+    import subprocess
+    port = port or free_port()
+    procs = [subprocess.Popen(cmd, env=e) for e in rank_envs(n, port)]
+    rc = 0
+    try:
+        pending = set(range(n))
+        while pending:
+            for r in sorted(pending):
+                code = procs[r].poll()
+                if code is None:
+                    continue
+                pending.discard(r)
+                if code != 0 and rc == 0:
+                    rc = code
+                    for q in pending:
+                        procs[q].terminate()
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    return rc
 
 
 def main():
     args = parse()
+    if args.gpus < 1:
+        sys.exit(f"bench.py: --gpus must be >= 1, got {args.gpus}")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # plain `python bench.py --gpus N`: start N ranks ourselves (torchrun's environment)
+        ndev = torch.cuda.device_count()   # counts devices without initialising HIP
+        if ndev < args.gpus:
+            sys.exit(f"bench.py: --gpus {args.gpus} but only {ndev} GPU(s) visible")
+        sys.exit(spawn_ranks(args.gpus, [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        sys.exit(f"bench.py: WORLD_SIZE={world} does not match --gpus {args.gpus}")
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     if world > 1:

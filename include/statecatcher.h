@@ -269,9 +269,10 @@ int sc_colsum(const void* x, int dtype, int64_t M, int64_t N, int64_t ld, int64_
  * L-split s) for A = dY bf16 [L][lda], B = X bf16 [L][ldb] — the backward of LinearSafe
  * (lucyrnn_triton.py:20-25: dW = dgates^T x) and of output_proj (lucyrnn_triton.py:107-109).
  * Sum the S slabs with sc_colsum (fixed order; it also un-permutes step-blocked rows).
- * Needs L % 64 == 0, J % 256 == 0, I % 224 == 0 or I % 256 == 0, 16-byte aligned operands and
- * leading dimensions; sc_gemm_wgrad_splits returns the split count for a shape (0: unsupported,
- * use a library GEMM).  part: S * I * J floats.
+ * Needs L % 64 == 0, J % 256 == 0, and I % 256 == 0 -- or I % 224 == 0 only at the 256-workgroup
+ * shape (I/224)*(J/256)*8 == 256 (e.g. I = 3584 = 7 * 512 with J = 512) -- plus 16-byte aligned
+ * operands and leading dimensions.  Gate on sc_gemm_wgrad_splits: it returns the split count
+ * for a shape, 0 when unsupported (use a library GEMM).  part: S * I * J floats.
  */
 int sc_gemm_wgrad_splits(int L, int I, int J);
 int sc_gemm_wgrad_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, float* part, int L,

@@ -281,7 +281,9 @@ extern "C" int sc_gemm_wgrad_bf16(const void* A, int64_t lda, const void* B, int
   SC_REQUIRE(A && B && part, "sc_gemm_wgrad_bf16: null pointer");
   SC_REQUIRE(L > 0 && L % kTL == 0, "sc_gemm_wgrad_bf16: L=%d must be a positive multiple of 64", L);
   SC_REQUIRE(J > 0 && J % kTJ == 0, "sc_gemm_wgrad_bf16: J=%d must be a multiple of 256", J);
-  SC_REQUIRE(I > 0 && (I % 224 == 0 || I % 256 == 0), "sc_gemm_wgrad_bf16: I=%d not a multiple of 224 or 256", I);
+  SC_REQUIRE(I > 0 && (I % 256 == 0 || (I % 224 == 0 && (I / 224) * (J / kTJ) * 8 == 256)),
+             "sc_gemm_wgrad_bf16: I=%d must be a multiple of 256, or of 224 when (I/224)*(J/256)*8 "
+             "== 256 (use sc_gemm_wgrad_splits to gate)", I);
   SC_REQUIRE(lda >= I && ldb >= J && lda % 8 == 0 && ldb % 8 == 0,
              "sc_gemm_wgrad_bf16: leading dimensions must cover the rows in 16-byte pieces");
   SC_REQUIRE((uintptr_t)A % 16 == 0 && (uintptr_t)B % 16 == 0, "sc_gemm_wgrad_bf16: unaligned operand");

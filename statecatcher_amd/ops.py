@@ -142,10 +142,14 @@ def colsum(x2d, perm=(1, 1)):
     per16 = 16 // x2d.element_size()
     if x2d.stride(1) != 1 or (x2d.data_ptr() % 16) or x2d.stride(0) % per16:
         if N % per16 or perm != (1, 1):
-            # rows padded to 16 bytes (the kernel's vector loads); zero columns add nothing
+            # rows padded to 16 bytes (the kernel's vector loads); zero columns add nothing.  The
+            # (A, B, N/(A*B)) un-permutation is defined on the unpadded width: applied here
+            # after the slice, never to the padded columns
             xp = torch.zeros(M, N + (-N) % per16, dtype=x2d.dtype, device=x2d.device)
             xp[:, :N] = x2d
-            return colsum(xp, perm)[:N]
+            out = colsum(xp)[:N]
+            A, Bf = perm
+            return out if A == 1 else out.view(A, Bf, -1).transpose(0, 1).reshape(-1)
         x2d = x2d.contiguous()
     lib = _lib.load()
     out = torch.empty(N, dtype=torch.float32, device=x2d.device)

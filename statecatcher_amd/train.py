@@ -72,8 +72,13 @@ class SegmentTrainer:
     def __init__(self, model: nn.Module, criterion: nn.Module, optimizer, mode: str = "ctc",
                  blank_id: int = 0, accumulation_steps: int = 1, max_grad_norm: float = 50.0,
                  amp_dtype: Optional[torch.dtype] = None, bucket_cap_mb: float = 50.0,
-                 save_every_n_updates: Optional[int] = None, model_dir: Optional[str] = None):
+                 save_every_n_updates: Optional[int] = None, model_dir: Optional[str] = None,
+                 joiner: Optional[nn.Module] = None, compact_rnnt: bool = False):
+        if mode == "rnnt" and joiner is None:
+            raise ValueError("mode='rnnt' needs the joiner module (train.py:144-146 builds it)")
         self.model = model
+        self.joiner = joiner
+        self.compact_rnnt = compact_rnnt
         self.world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
         if self.world > 1:
             dev = next(model.parameters()).device
@@ -81,8 +86,13 @@ class SegmentTrainer:
                 model, device_ids=[dev.index] if dev.type == "cuda" else None,
                 bucket_cap_mb=bucket_cap_mb, gradient_as_bucket_view=True,
                 broadcast_buffers=False)
+            self.joiner_net = None if joiner is None else nn.parallel.DistributedDataParallel(
+                joiner, device_ids=[dev.index] if dev.type == "cuda" else None,
+                bucket_cap_mb=bucket_cap_mb, gradient_as_bucket_view=True,
+                broadcast_buffers=False)
         else:
             self.net = model
+            self.joiner_net = joiner
         self.criterion = criterion
         self.optimizer = optimizer
         self.mode = mode
@@ -97,10 +107,16 @@ class SegmentTrainer:
         self.encoder_state: Optional[Any] = None
 
     def _fused_clip_ok(self) -> bool:
+        """The clip coefficient may ride on the fused Adam kernel only when every parameter the
+        optimizer steps is one clip_grad_norm_ covers: the reference clips model.parameters()
+        alone (train.py:553), so e.g. an RNN-T joiner in the same optimizer stays unscaled."""
         opt = self.optimizer
-        return (isinstance(opt, (torch.optim.Adam, torch.optim.AdamW))
+        if not (isinstance(opt, (torch.optim.Adam, torch.optim.AdamW))
                 and all(g.get("fused") for g in opt.param_groups)
-                and getattr(opt, "found_inf", None) is None)
+                and getattr(opt, "found_inf", None) is None):
+            return False
+        own = {id(p) for p in self.model.parameters()}
+        return all(id(p) in own for g in opt.param_groups for p in g["params"])
 
     def _clip_and_step(self):
         """clip_grad_norm_(max_norm) then optimizer.step() (train.py:543-552).  With a fused
@@ -130,21 +146,28 @@ class SegmentTrainer:
     def train_segment(self, feats, masks, tokens, in_lens, tgt_lens):
         """One segment (train.py:508-581).  Returns the (un-divided) loss tensor."""
         stepping = self._steps_now()
-        sync = contextlib.nullcontext() if (stepping or self.world == 1) else self.net.no_sync()
+        sync = contextlib.ExitStack()
+        if not (stepping or self.world == 1):
+            sync.enter_context(self.net.no_sync())
+            if self.joiner_net is not None:
+                sync.enter_context(self.joiner_net.no_sync())
         dev_type = feats.device.type
         with sync:
             with torch.autocast(dev_type, dtype=self.amp_dtype or torch.float32,
                                 enabled=self.amp_dtype is not None):
                 loss, output_state, _, _ = compute_loss(
                     self.mode, self.criterion, self.net, feats, masks, tokens, in_lens, tgt_lens,
-                    self.blank_id, input_state=self.encoder_state)
+                    self.blank_id, use_rnnt_joiner=self.joiner_net, input_state=self.encoder_state,
+                    compact=self.compact_rnnt)
             (loss / self.accumulation_steps).backward()
         if stepping:
             self._clip_and_step()
             self.optimizer.zero_grad(set_to_none=True)
         if self.save_every_n_updates and (self.global_step + 1) % self.save_every_n_updates == 0 \
                 and (self.world == 1 or dist.get_rank() == 0) and self.model_dir:
-            save_checkpoint(self.model_dir, self.model, None, self.epoch, self.global_step + 1)
+            # train.py:576-578: the joiner is saved alongside the model in RNN-T mode
+            save_checkpoint(self.model_dir, self.model, self.joiner if self.mode == "rnnt" else None,
+                            self.epoch, self.global_step + 1)
         self.encoder_state = output_state
         self.global_step += 1
         return loss

@@ -71,3 +71,31 @@ def test_wgrad_unsupported_shape_falls_back():
     dw = ops().wgrad_splitk(dy, x)
     ref = _ref(dy, x)
     assert (dw - ref).abs().max().item() <= 2e-2 * ref.abs().max().item()
+
+
+def test_wgrad_i448_is_rejected_by_the_split_gate():
+    """I=448 is a multiple of 224 but not at the 256-workgroup shape: the split gate says 0 and
+    the launch itself refuses (the C-ABI contract of statecatcher.h)."""
+    from statecatcher_amd import _lib
+    lib = _lib.load()
+    assert lib.sc_gemm_wgrad_splits(4096, 448, 512) == 0
+    dy = torch.randn(4096, 448, device=DEV).to(torch.bfloat16)
+    x = torch.randn(4096, 512, device=DEV).to(torch.bfloat16)
+    assert ops().wgrad_mfma(dy, x) is None
+    part = torch.empty(1, 448, 512, device=DEV)
+    rc = lib.sc_gemm_wgrad_bf16(dy.data_ptr(), 448, x.data_ptr(), 512, part.data_ptr(), 4096, 448,
+                                512, 1, None)
+    assert rc != 0
+
+
+@pytest.mark.parametrize("N", [7 * 5 * 3, 7 * 2 * 64 + 0])
+def test_colsum_perm_with_unaligned_rows(N):
+    """sc_colsum's (A, B) un-permutation on a view whose rows are not 16-byte pieces (the padded
+    path): the permutation applies to the unpadded width."""
+    A, Bf = (5, 7) if N == 105 else (2, 7)
+    M = 300
+    big = torch.randn(M, N + 3, device=DEV)
+    x = big[:, 1:N + 1]   # unaligned base and row pitch
+    out = ops().colsum(x, (A, Bf))
+    ref = x.double().sum(0).view(A, Bf, -1).transpose(0, 1).reshape(-1)
+    torch.testing.assert_close(out.double(), ref, rtol=1e-5, atol=1e-4)

@@ -159,3 +159,48 @@ def test_frame_mask_and_lengths_match_reference_semantics():
     assert fm.shape == (2, 10)
     assert fm[0].all() and fm[1, :7].all() and not fm[1, 7:].any()   # frame 6 partially covered
     assert frame_lengths(mask, 160.0, 10) == [10, 6]                  # floor(1000/160) = 6
+
+
+class TorchRNNTLoss(nn.Module):
+    """warp_rnnt's keyword interface (model.py:97-105) over a tiny differentiable torch lattice
+    (test stand-in: the product loss is HIP-only)."""
+
+    def forward(self, log_probs, labels, frames_lengths, labels_lengths, blank_id=0, compact=False,
+                gather=True):
+        nll = []
+        for b in range(log_probs.shape[0]):
+            Tb, Ub = int(frames_lengths[b]), int(labels_lengths[b])
+            lp = log_probs[b]
+            alpha = [[None] * (Ub + 1) for _ in range(Tb)]
+            for t in range(Tb):
+                for u in range(Ub + 1):
+                    terms = []
+                    if t == 0 and u == 0:
+                        terms.append(lp.new_zeros(()))
+                    if t > 0:
+                        terms.append(alpha[t - 1][u] + lp[t - 1, u, blank_id])
+                    if u > 0:
+                        terms.append(alpha[t][u - 1] + lp[t, u - 1, labels[b, u - 1]])
+                    alpha[t][u] = torch.logsumexp(torch.stack(terms), 0)
+            nll.append(-(alpha[Tb - 1][Ub] + lp[Tb - 1, Ub, blank_id]))
+        return torch.stack(nll).mean()
+
+
+def test_rnnt_segment_through_trainer_saves_joiner_and_skips_joiner_clip(tmp_path):
+    from statecatcher_amd.model import RNNTPredictorJoiner
+    torch.manual_seed(0)
+    model = TinyStateful()
+    joiner = RNNTPredictorJoiner(V, 4, 6, V)
+    opt = torch.optim.Adam(list(model.parameters()) + list(joiner.parameters()), lr=1e-2)
+    with pytest.raises(ValueError):
+        SegmentTrainer(model, TorchRNNTLoss(), opt, mode="rnnt")
+    tr = SegmentTrainer(model, TorchRNNTLoss(), opt, mode="rnnt", joiner=joiner, max_grad_norm=1e-3,
+                        save_every_n_updates=1, model_dir=str(tmp_path))
+    assert not tr._fused_clip_ok()   # the joiner is in the optimizer: clip model params only
+    j0 = {k: v.clone() for k, v in joiner.state_dict().items()}
+    feats, mask, tok, il, tl = data(3)[0][0]
+    loss = tr.train_segment(feats, mask, tok, il, tl)
+    assert torch.isfinite(loss)
+    assert any(not torch.equal(j0[k], v) for k, v in joiner.state_dict().items())   # joiner trained
+    ck = torch.load(os.path.join(tmp_path, "model_epoch1_step1.pt"), weights_only=True)
+    assert set(ck) == {"model", "joiner"} and set(ck["joiner"]) == set(joiner.state_dict())
