@@ -83,6 +83,8 @@ int64_t sc_lucy_scan_ckpt_numel(int B, int T, int D);
  *          strided out[:, -1] view the reference passes — SURVEY F3)
  *   out    [B,T,D] of gates_dtype, d-stride 1 (strides stride_o_bt, stride_o_bd)
  *   s_out  [B,D] fp32 contiguous: state after the last step
+ *   h_out  NULL, or [B,D] fp32 contiguous: h after the last step in fp32 (the reference carries
+ *          out[:, -1] in x.dtype = fp32; with a 16-bit out this keeps the carry unrounded)
  *   ckpt   NULL, or sc_lucy_scan_ckpt_numel() floats: (s,h) at every super-chunk start,
  *          consumed by sc_lucy_scan_bwd (training)
  * State arithmetic is fp32 for every gates_dtype.  Any element strides work; 16-byte aligned
@@ -90,7 +92,7 @@ int64_t sc_lucy_scan_ckpt_numel(int B, int T, int D);
  */
 int sc_lucy_scan_fwd(const void* gates, int gates_dtype, const float* gate_bias,
                      const float* h0, const float* s0,
-                     void* out, float* s_out, int B, int T, int D,
+                     void* out, float* s_out, float* h_out, int B, int T, int D,
                      int64_t stride_g_bt, int64_t stride_g_td, int64_t stride_g_cd,
                      int64_t stride_g_cb, int64_t stride_o_bt, int64_t stride_o_bd, float* ckpt,
                      void* stream);

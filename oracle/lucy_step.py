@@ -48,9 +48,10 @@ def _ln_bwd(dy, g, cache):
     return dx, (dy * xh).reshape(-1, D).sum(0), dy.reshape(-1, D).sum(0)
 
 
-def train_step(p, feats, tokens, in_lens, tgt_lens, L, D, state=None, adam=None, lr=3e-4,
-               max_norm=50.0):
-    """One segment step.  Returns (loss, new_state, grads)."""
+def forward(p, feats, L, D, state=None):
+    """LucyRNNtriton.forward (lucyrnn_triton.py:111-155) with one track: per layer GEMM + bias
+    (:20-25, :56) -> scan (fp32 state) -> h carry = out[:, -1] (:135) -> LayerNorm for l < L-1
+    (:136-137); output_proj (:150).  Returns (logits, (h list, s list), x_last, caches)."""
     B, T, _ = feats.shape
     f32 = np.float32
     h = [np.zeros((B, D), f32)] * L if state is None else state[0]
@@ -71,7 +72,16 @@ def train_step(p, feats, tokens, in_lens, tgt_lens, L, D, state=None, adam=None,
             x = out
         caches.append((xin, gates, ln))
     logits = x.reshape(-1, D) @ p["Wo"].T + p["bo"]
-    logits = logits.reshape(B, T, -1)
+    return logits.reshape(B, T, -1), (new_h, new_s), x, (caches, h, s)
+
+
+def train_step(p, feats, tokens, in_lens, tgt_lens, L, D, state=None, adam=None, lr=3e-4,
+               max_norm=50.0):
+    """One segment step: forward, CTC, backward, clip, Adam (updates p in place).
+    Returns (loss, new_state, grads before clipping, adam state)."""
+    B, T, _ = feats.shape
+    f32 = np.float32
+    logits, (new_h, new_s), x, (caches, h, s) = forward(p, feats, L, D, state)
     nll, grad = octc.ctc_loss_grad(logits, tokens, in_lens, tgt_lens, blank=0, logits=True)
     loss = octc.ctc_mean_zero_inf(nll, tgt_lens)
     scale = octc.ctc_mean_grad_scale(nll, tgt_lens)

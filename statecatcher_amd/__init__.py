@@ -9,7 +9,7 @@ from .lucyrnn_triton import LinearSafe, LucyRNNCellTriton, LucyRNNtriton
 from .lucyrnn import LucyRNN, LucyRNNCell
 from .xlstm import xLSTMLarge, xLSTMLargeConfig
 from .model import (ASRModel, CTCLoss, RNNTCompactPredictorJoiner, RNNTLoss, RNNTPredictorJoiner,
-                    compute_loss, detach_states)
+                    build_lucyrnn_config, build_xlstm_config, compute_loss, detach_states)
 from .ops import (ctc_greedy_decode, ctc_loss, ctc_nll, decay_scan, lucy_scan, mlstm_chunkwise,
                   rnnt_loss)
 from .decoder import ctc_greedy_decoder
@@ -18,7 +18,7 @@ from .frontend import make_frontend
 
 __all__ = [
     "LucyRNNConfig", "LinearSafe", "LucyRNNCellTriton", "LucyRNNtriton", "LucyRNN", "LucyRNNCell", "ASRModel", "CTCLoss",
-    "compute_loss", "detach_states", "ctc_greedy_decode", "ctc_loss", "ctc_nll", "decay_scan",
+    "compute_loss", "detach_states", "build_lucyrnn_config", "build_xlstm_config", "ctc_greedy_decode", "ctc_loss", "ctc_nll", "decay_scan",
     "lucy_scan", "ctc_greedy_decoder", "rnnt_loss", "RNNTLoss", "RNNTPredictorJoiner",
     "RNNTCompactPredictorJoiner", "xLSTMLarge", "xLSTMLargeConfig", "mlstm_chunkwise",
     "StreamingLucyRNN", "make_frontend",

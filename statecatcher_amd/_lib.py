@@ -27,7 +27,7 @@ _SIGS = {
     "sc_last_error": (_c.c_char_p, []),
     "sc_lucy_scan_chunk": (_i32, []),
     "sc_lucy_scan_ckpt_numel": (_i64, [_i32, _i32, _i32]),
-    "sc_lucy_scan_fwd": (_i32, [_vp, _i32, _fp, _fp, _fp, _vp, _fp, _i32, _i32, _i32,
+    "sc_lucy_scan_fwd": (_i32, [_vp, _i32, _fp, _fp, _fp, _vp, _fp, _fp, _i32, _i32, _i32,
                                _i64, _i64, _i64, _i64, _i64, _i64, _fp, _vp]),
     "sc_lucy_scan_bwd": (_i32, [_vp, _i32, _fp, _fp, _vp, _fp, _vp, _fp, _fp, _fp, _i32, _i32, _i32,
                                _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64,

@@ -81,6 +81,7 @@ struct ScanFwdArgs {
   const float* s0;
   void* out;
   float* s_out;
+  float* h_out;   // optional fp32 [B,D]: h after the last step, unrounded (the segment carry)
   float* ckpt;
   int B, T, D, nsc;
   int64_t g_bt, g_td, g_cd, g_cb, o_bt, o_bd;
@@ -504,7 +505,10 @@ lucy_scan_fwd_kernel(ScanFwdArgs a) {
       chunk(k, std::false_type{});
   }
   lds_barrier();
-  if (w == 0 && dok) a.s_out[(int64_t)b * a.D + d] = carS[a.nsc & 1][lane];
+  if (w == 0 && dok) {
+    a.s_out[(int64_t)b * a.D + d] = carS[a.nsc & 1][lane];
+    if (a.h_out) a.h_out[(int64_t)b * a.D + d] = carH[a.nsc & 1][lane];
+  }
 }
 
 // ------------------------------------------------------------------------ backward ---------
@@ -989,7 +993,8 @@ static int check_dtype(int dt) { return dt == SC_F32 || dt == SC_BF16 || dt == S
 
 extern "C" int sc_lucy_scan_fwd(const void* gates, int gates_dtype, const float* gate_bias,
                                 const float* h0,
-                                const float* s0, void* out, float* s_out, int B, int T, int D,
+                                const float* s0, void* out, float* s_out, float* h_out, int B,
+                                int T, int D,
                                 int64_t stride_g_bt, int64_t stride_g_td, int64_t stride_g_cd,
                                 int64_t stride_g_cb, int64_t stride_o_bt, int64_t stride_o_bd,
                                 float* ckpt, void* stream) {
@@ -1005,7 +1010,7 @@ extern "C" int sc_lucy_scan_fwd(const void* gates, int gates_dtype, const float*
              "sc_lucy_scan_fwd: negative stride");
   SC_REQUIRE((int64_t)T * stride_o_bd * 4 < (1ll << 31),
              "sc_lucy_scan_fwd: one batch row of out spans >= 2 GiB");
-  ScanFwdArgs a{gates, gate_bias, h0, s0, out, s_out, ckpt, B, T, D, (T + kChunk - 1) / kChunk,
+  ScanFwdArgs a{gates, gate_bias, h0, s0, out, s_out, h_out, ckpt, B, T, D, (T + kChunk - 1) / kChunk,
                 stride_g_bt, stride_g_td, stride_g_cd, stride_g_cb, stride_o_bt, stride_o_bd};
   hipStream_t st = (hipStream_t)stream;
   switch (gates_dtype) {

@@ -10,7 +10,8 @@ Differences from the reference, all deliberate:
   * gradients flow into the recurrent layers (the reference's outputs have no grad_fn, F2);
   * h0 is read through .contiguous(), so the carried out[:, -1] view is honoured (F3);
   * bf16 / fp16 gates (e.g. under torch.autocast) run; state arithmetic stays fp32 (F4);
-  * s_last is returned in fp32.
+  * s_last and the carried h (out[:, -1]) are returned in fp32 whatever the gate dtype, so a
+    bf16-autocast run carries its state across segments unrounded, as the fp32 reference does.
 """
 import torch
 import torch.nn as nn
@@ -105,8 +106,15 @@ class LucyRNNCellTriton(nn.Module):
                 self.linear.bias[6 * D:7 * D].fill_(0.5)   # alpha
 
     def forward(self, x, h0, s0):
-        # projection GEMM + scan as one autograd node: the scan backward hands the bias
-        # gradient back from registers, the weight gradient runs split-K
+        """(out [B,T,D], s_out [B,D]) as lucyrnn_triton.py:50-75 returns them."""
+        out, s_out, _ = self.forward_with_h(x, h0, s0)
+        return out, s_out
+
+    def forward_with_h(self, x, h0, s0):
+        """(out, s_out, h_last): h_last = out[:, -1] in fp32, unrounded by a 16-bit out (the
+        state LucyRNNtriton carries).  Projection GEMM + scan are one autograd node: the scan
+        backward hands the bias gradient back from registers, the weight gradient runs on the
+        MFMA split-L kernel."""
         w, b = self.linear.weight, self.linear.bias
         if x.is_cuda and torch.is_autocast_enabled("cuda"):
             cdt = torch.get_autocast_dtype("cuda")
@@ -170,8 +178,9 @@ class LucyRNNtriton(nn.Module):
             layers = self.tracks[t]
             norms = self.norms[t]
             for l, layer in enumerate(layers):
-                x_t, s_t[l] = layer(x_t, h_t[l], s_t[l])
-                h_t[l] = x_t[:, -1, :]
+                # h carry = out[:, -1] (lucyrnn_triton.py:135), taken in fp32 from the scan and
+                # contiguous
+                x_t, s_t[l], h_t[l] = layer.forward_with_h(x_t, h_t[l], s_t[l])
                 if l < len(norms):
                     x_t = norms[l](x_t)
             track_outputs.append(x_t)

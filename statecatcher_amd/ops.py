@@ -48,7 +48,7 @@ def gate_layout(gates):
                      f"shape {tuple(gates.shape)} strides {gates.stride()}")
 
 
-def _scan_fwd(gates, h0, s0, need_ckpt, bias=None):
+def _scan_fwd(gates, h0, s0, need_ckpt, bias=None, want_h=False):
     require_device(gates, h0, s0)
     if gates.dim() == 4 and gates.shape[2] == 7 and gates.stride(3) != 1:
         gates = gates.contiguous()
@@ -60,6 +60,7 @@ def _scan_fwd(gates, h0, s0, need_ckpt, bias=None):
     s0c = s0.detach().to(torch.float32).contiguous()
     out = torch.empty(B, T, D, dtype=gates.dtype, device=gates.device)
     s_out = torch.empty(B, D, dtype=torch.float32, device=gates.device)
+    h_out = torch.empty(B, D, dtype=torch.float32, device=gates.device) if want_h else None
     lib = _lib.load()
     ckpt = None
     if need_ckpt:
@@ -69,10 +70,10 @@ def _scan_fwd(gates, h0, s0, need_ckpt, bias=None):
     nbytes = B * T * D * 8 * e + (ckpt.numel() * 4 if ckpt is not None else 0) + 4 * B * D * 4
     with _timed("lucy_scan_fwd", gates, nbytes):
         rc = lib.sc_lucy_scan_fwd(ptr(gates), dtype_code(gates), ptr(bias), ptr(h0c), ptr(s0c),
-                                  ptr(out), ptr(s_out), B, T, D, *gs, out.stride(0), out.stride(1),
-                                  ptr(ckpt), stream_of(gates))
+                                  ptr(out), ptr(s_out), ptr(h_out), B, T, D, *gs, out.stride(0),
+                                  out.stride(1), ptr(ckpt), stream_of(gates))
     check(rc, "sc_lucy_scan_fwd")
-    return gates, out, s_out, ckpt
+    return (gates, out, s_out, ckpt, h_out) if want_h else (gates, out, s_out, ckpt)
 
 
 def _scan_bwd(gates, ckpt, dout, ds_last, want_dbias, bias=None):
@@ -220,6 +221,9 @@ def step_blocked_rows(w, D, inverse=False, dtype=None):
 class LucyCellFn(torch.autograd.Function):
     """One LucyRNN layer: gates = x W^T (one GEMM, compute dtype `cdt`) -> HIP scan, which adds
     the fp32 bias b to the gates on load (a bias epilogue costs the GEMM ~25%, measured).
+    Returns (out [B,T,D] in cdt, s_last fp32, h_last fp32): h_last is out[:, -1] before the
+    output rounding, the state the next segment starts from (the reference carries out[:, -1]
+    in x.dtype, fp32, lucyrnn_triton.py:58/135).
 
     Backward: scan adjoint (which also emits the bias gradient as per-row partial sums),
     dx = dgates W, dW = split-K dgates^T x.  lucyrnn_triton.py:50-75 fused into one node.
@@ -239,17 +243,24 @@ class LucyCellFn(torch.autograd.Function):
             gates = torch.matmul(xc, wc.t())
         gates = gates.view(B, T, D // 64, 7, 64) if blocked else gates.view(B, T, 7, D)
         need = any(ctx.needs_input_grad)
-        gates, out, s_out, ckpt = _scan_fwd(gates, h0, s0, need, bias)
+        gates, out, s_out, ckpt, h_out = _scan_fwd(gates, h0, s0, need, bias, want_h=True)
         if need:
             ctx.save_for_backward(xc, wc, gates, ckpt, bias)
             ctx.dtypes = (x2d.dtype, w.dtype, h0.dtype, s0.dtype)
             ctx.blocked = blocked
-        return out, s_out
+        return out, s_out, h_out
 
     @staticmethod
-    def backward(ctx, dout, ds_last):
+    def backward(ctx, dout, ds_last, dh_last):
         xc, wc, gates, ckpt, bias = ctx.saved_tensors
         xdt, wdt, hdt, sdt = ctx.dtypes
+        if dh_last is not None:   # h_last is out[:, -1]: its gradient joins dout's last step
+            B, T = gates.shape[:2]
+            if dout is None:
+                dout = torch.zeros(B, T, dh_last.shape[-1], dtype=gates.dtype, device=gates.device)
+            else:
+                dout = dout.clone()
+            dout[:, -1] += dh_last.to(dout.dtype)
         dgates, dh0, ds0, dbias = _scan_bwd(gates, ckpt, dout, ds_last, ctx.needs_input_grad[2],
                                             bias)
         dg2 = dgates.view(xc.shape[0], -1)
@@ -265,7 +276,8 @@ class LucyCellFn(torch.autograd.Function):
 
 
 def lucy_cell(x, w, b, h0, s0, cdt=None):
-    """x [B,T,Din] -> (out [B,T,D], s_last [B,D]) through projection + scan."""
+    """x [B,T,Din] -> (out [B,T,D], s_last [B,D] fp32, h_last [B,D] fp32) through projection
+    + scan."""
     B, T, Din = x.shape
     if cdt is None:
         cdt = torch.promote_types(x.dtype, w.dtype)

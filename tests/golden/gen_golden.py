@@ -16,6 +16,10 @@ Sources of truth, per fixture file:
                    ``nn.CTCLoss(blank=0, zero_infinity=True)`` (train.py:142, model.py:68-71).
   greedy.npz       reference ``decoder.ctc_greedy_decoder`` (decoder.py:3-30).
   native.npz       reference ``lucyrnn.LucyRNN`` (lucyrnn.py:72-191), train and infer modes.
+  module.npz       reference ``lucyrnn_triton.LucyRNNtriton`` (lucyrnn_triton.py:77-155) at its
+                   own init, fp32, Triton interpreter: 3 layers with the inter-layer LayerNorms
+                   and output_proj, two segments with the state carried (h made contiguous
+                   between them).
 
 Only arrays are stored (np.savez, allow_pickle not needed).  Seeds are fixed below.
 """
@@ -282,9 +286,54 @@ def gen_native():
     np.savez(os.path.join(HERE, "native.npz"), **cases)
 
 
+def gen_module():
+    """Cases: (Din, D, V, B, T, output_proj init).  'init' keeps the reference's zero output_proj
+    (lucyrnn_triton.py:108-109: logits are exactly 0, the carried states carry the check);
+    'proj' draws output_proj from N(0, 0.3) after construction so the logits see every layer."""
+    from lucyrnn_conf import LucyRNNConfig
+    from lucyrnn_triton import LucyRNNtriton
+    cases = {}
+    specs = [("d64_init", 10, 64, 12, 2, 11, False), ("d64_proj", 10, 64, 12, 2, 11, True),
+             ("d40_proj", 6, 40, 9, 3, 7, True)]
+    for name, Din, D, V, B, T, proj in specs:
+        torch.manual_seed(77)
+        cfg = LucyRNNConfig(input_dim=Din, hidden_dim=D, num_layers=3, vocab_size=V,
+                            kernel_impl="triton", fused_ops=True, layer_norm=False, stack_order=1)
+        m = LucyRNNtriton(cfg)
+        if proj:
+            with torch.no_grad():
+                m.output_proj.weight.normal_(0, 0.3)
+                m.output_proj.bias.normal_(0, 0.1)
+        for k, v in m.state_dict().items():
+            cases[name + "/param/" + k] = v.detach().clone().numpy()
+        # the same module in fp64 (the interpreter runs the kernel in fp64 too): the reference's
+        # own fp32 rounding noise |fp32 - fp64| is the conditioning floor of the parity tests
+        m64 = LucyRNNtriton(cfg).double()
+        m64.load_state_dict({k: v.double() for k, v in m.state_dict().items()})
+        state, state64 = None, None
+        for seg in range(2):
+            x = torch.randn(B, T, Din)
+            with torch.no_grad():
+                logits, (fh, fs) = m(x, state) if state is not None else m(x)
+                l64, (h64, s64) = m64(x.double(), state64) if state64 is not None else m64(x.double())
+            cases[f"{name}/seg{seg}/x"] = x.numpy()
+            cases[f"{name}/seg{seg}/logits"] = logits.numpy()
+            cases[f"{name}/seg{seg}/h"] = torch.stack(fh[0]).numpy()
+            cases[f"{name}/seg{seg}/s"] = torch.stack(fs[0]).numpy()
+            cases[f"{name}/seg{seg}/logits64"] = l64.numpy()
+            cases[f"{name}/seg{seg}/h64"] = torch.stack(h64[0]).numpy()
+            cases[f"{name}/seg{seg}/s64"] = torch.stack(s64[0]).numpy()
+            # next segment's state: detached and contiguous (the reference kernel reads h0 as
+            # contiguous memory; its strided out[:, -1] view would mis-read rows b >= 1, F3)
+            state = ([[t.detach().contiguous() for t in fh[0]]], [[t.detach().clone() for t in fs[0]]])
+            state64 = ([[t.detach().contiguous() for t in h64[0]]], [[t.detach().clone() for t in s64[0]]])
+        print("module", name, flush=True)
+    np.savez(os.path.join(HERE, "module.npz"), **cases)
+
+
 if __name__ == "__main__":
     torch.set_num_threads(8)
-    which = sys.argv[1:] or ["scan", "decay", "ctc", "greedy", "native"]
+    which = sys.argv[1:] or ["scan", "decay", "ctc", "greedy", "native", "module"]
     for w in which:
         {"scan": gen_scan, "decay": gen_decay, "ctc": gen_ctc, "greedy": gen_greedy,
-         "native": gen_native}[w]()
+         "native": gen_native, "module": gen_module}[w]()

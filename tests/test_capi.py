@@ -46,10 +46,10 @@ def test_abi_version_and_sizes(lib):
 
 def test_invalid_arguments_rejected_without_gpu(lib):
     null = ctypes.c_void_p()
-    rc = lib.sc_lucy_scan_fwd(null, 7, null, null, null, null, null, 1, 1, 1, 1, 1, 1, 64, 1, 1, null, null)
+    rc = lib.sc_lucy_scan_fwd(null, 7, null, null, null, null, null, null, 1, 1, 1, 1, 1, 1, 64, 1, 1, null, null)
     assert rc == -1
     assert b"dtype" in lib.sc_last_error()
-    rc = lib.sc_lucy_scan_fwd(null, 0, null, null, null, null, null, -1, 1, 1, 1, 1, 1, 64, 1, 1, null, null)
+    rc = lib.sc_lucy_scan_fwd(null, 0, null, null, null, null, null, null, -1, 1, 1, 1, 1, 1, 64, 1, 1, null, null)
     assert rc == -1
     rc = lib.sc_decay_scan_fwd(null, null, null, 0, null, 1, 1, 1, 1, 1, 2, null)
     assert rc == -1 and b"stride_d" in lib.sc_last_error()
@@ -58,5 +58,5 @@ def test_invalid_arguments_rejected_without_gpu(lib):
     rc = lib.sc_ctc_fwd(null, 0, 1, 1, 1, 4, 4, 4, null, 0, 1, null, null, 9, null, null, 0, null)
     assert rc == -1 and b"blank" in lib.sc_last_error()
     # empty problems are no-ops
-    assert lib.sc_lucy_scan_fwd(null, 0, null, null, null, null, null, 0, 5, 5, 1, 1, 1, 64, 1, 1, null, null) == 0
+    assert lib.sc_lucy_scan_fwd(null, 0, null, null, null, null, null, null, 0, 5, 5, 1, 1, 1, 64, 1, 1, null, null) == 0
     assert lib.sc_ctc_greedy_decode(null, 0, 0, 5, 5, 1, 1, null, 0, null, null, null) == 0

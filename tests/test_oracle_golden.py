@@ -200,3 +200,41 @@ def test_fbank_oracle_vs_independent_restatement():
     np.testing.assert_allclose(ofb.frontend(a, "mfcc"), z["mfcc"], rtol=1e-5, atol=1e-4)
     np.testing.assert_allclose(ofb.frontend(a, "mel"), z["logmel_db"], rtol=1e-5, atol=1e-4)
     assert ofb.frontend(a[:, :399], "mfcc").shape == (3, 0, 80)
+
+
+MODULE_CASES = ["d64_init", "d64_proj", "d40_proj"]
+
+
+def module_params(z, name):
+    """module.npz's reference state_dict -> oracle.lucy_step parameter names."""
+    pre = name + "/param/"
+    L = len([k for k in z.files if k.startswith(pre + "tracks.0.") and k.endswith(".linear.weight")])
+    p = {}
+    for l in range(L):
+        p[f"W{l}"] = z[pre + f"tracks.0.{l}.linear.weight"]
+        p[f"b{l}"] = z[pre + f"tracks.0.{l}.linear.bias"]
+        if l < L - 1:
+            p[f"g{l}"] = z[pre + f"norms.0.{l}.weight"]
+            p[f"be{l}"] = z[pre + f"norms.0.{l}.bias"]
+    p["Wo"] = z[pre + "output_proj.weight"]
+    p["bo"] = z[pre + "output_proj.bias"]
+    return p, L, p["W0"].shape[0] // 7
+
+
+@pytest.mark.parametrize("name", MODULE_CASES)
+def test_lucy_step_forward_vs_reference_module(name):
+    """oracle.lucy_step.forward against the reference LucyRNNtriton itself (Triton interpreter,
+    fp32, its own init, 3 layers + LayerNorms + output_proj, two segments with state carry);
+    tolerance: tests.conftest.assert_ref_parity (the reference's own fp32-vs-fp64 noise)."""
+    from oracle import lucy_step
+    from tests.conftest import assert_ref_parity
+    z = load_golden("module")
+    p, L, D = module_params(z, name)
+    state = None
+    for seg in range(2):
+        logits, (h, s), _, _ = lucy_step.forward(p, z[f"{name}/seg{seg}/x"], L, D, state)
+        pre = f"{name}/seg{seg}/"
+        assert_ref_parity(logits, z[pre + "logits"], z[pre + "logits64"])
+        assert_ref_parity(np.stack(h), z[pre + "h"], z[pre + "h64"])
+        assert_ref_parity(np.stack(s), z[pre + "s"], z[pre + "s64"])
+        state = (h, s)

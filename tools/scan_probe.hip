@@ -281,11 +281,11 @@ int main() {
     run_glds<12, 4, 2, 3>("glds NW12 LC4 permuted nbuf3", g, o);
     if (with_lib) {   // the shipped kernel through the C ABI, step-blocked gates, same harness
       time_variant("libstatecatcher fwd (blocked, bias, ckpt)", [&](const uint16_t* gg) {
-        sc_lucy_scan_fwd(gg, SC_BF16, bias, st0, st0, o, sout, B, T, D, (int64_t)T * 7 * D, 7 * D,
+        sc_lucy_scan_fwd(gg, SC_BF16, bias, st0, st0, o, sout, nullptr, B, T, D, (int64_t)T * 7 * D, 7 * D,
                          64, 448, (int64_t)T * D, D, ckpt, nullptr);
       }, 0);
       time_variant("libstatecatcher fwd (blocked, no bias/ckpt)", [&](const uint16_t* gg) {
-        sc_lucy_scan_fwd(gg, SC_BF16, nullptr, st0, st0, o, sout, B, T, D, (int64_t)T * 7 * D, 7 * D,
+        sc_lucy_scan_fwd(gg, SC_BF16, nullptr, st0, st0, o, sout, nullptr, B, T, D, (int64_t)T * 7 * D, 7 * D,
                          64, 448, (int64_t)T * D, D, nullptr, nullptr);
       }, 0);
     }
