@@ -29,14 +29,15 @@ def cases(z, suffix):
     return sorted({k.split("/")[0] for k in z.files if k.endswith("/" + suffix)})
 
 
-def assert_ref_parity(got, ref32, ref64, rtol=1e-3, afrac=1e-4, frac_ok=0.995):
+def assert_ref_parity(got, ref32, ref64, rtol=1e-3, afrac=1e-4, frac_ok=0.95):
     """Parity with a reference fp32 output whose own rounding noise is known (ref64 = the same
     reference module run in fp64).  Two checks:
       * conditioning: max |got - ref64| <= 2 max |ref32 - ref64| + afrac * scale -- ``got`` is at
         least as close to the exact answer as the reference's own fp32 result, up to 2x;
       * element-wise: |got - ref32| <= rtol |ref32| + afrac * scale for >= frac_ok of the elements
-        (the rest are the few gates within ~1e-5 of 0 where x / sqrt(x^2 + 1e-6) amplifies any
-        rounding ~1e3x).
+        (the rest sit downstream of a gate within ~1e-5 of 0, where x / sqrt(x^2 + 1e-6) amplifies any
+        rounding ~1e3x; one such gate moves all V logits of its frame, so on the tiny
+        fixtures a single flipped gate is several % of the elements).
     scale = max(1, max |ref32|)."""
     got = np.asarray(got, np.float64)
     ref32 = np.asarray(ref32, np.float64)

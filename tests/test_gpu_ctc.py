@@ -72,6 +72,14 @@ def test_ctc_full_size_vs_aten_cpu():
     ref.backward()
     np.testing.assert_allclose(loss.item(), ref.item(), rtol=1e-4)
     np.testing.assert_allclose(x.grad.cpu().numpy(), xr.grad.numpy(), rtol=1e-2, atol=2e-6)
+    # at least as accurate as the reference's own criterion in fp32 (ATen ctc_loss, CPU fp32)
+    x32 = logits.clone().requires_grad_(True)
+    torch.nn.CTCLoss(blank=0, zero_infinity=True)(x32.log_softmax(-1).transpose(0, 1), tg, il, tl).backward()
+    rg = xr.grad.numpy()
+    ours = np.linalg.norm(x.grad.cpu().numpy() - rg) / np.linalg.norm(rg)
+    aten32 = np.linalg.norm(x32.grad.numpy() - rg) / np.linalg.norm(rg)
+    print(f"CTC grad rel err vs fp64: HIP {ours:.2e}, ATen fp32 {aten32:.2e}")
+    assert ours <= max(aten32, 1e-4)
 
 
 @pytest.mark.parametrize("U", [57, 300, 1007])
