@@ -413,10 +413,7 @@ __global__ void __launch_bounds__(256) rnnt_grad_kernel(RnntArgs a) {
   }
 }
 
-template <int DT>
-void launch_fwd(const RnntArgs& a, hipStream_t st) {
-  const int64_t nodes = (int64_t)a.B * a.T * a.U1;
-  hipLaunchKernelGGL((rnnt_emit_kernel<DT>), dim3((unsigned)((nodes + 3) / 4)), dim3(256), 0, st, a);
+void launch_ab(const RnntArgs& a, hipStream_t st) {
   const int K = a.kh;
   const int nw = (a.U1 + (64 - K) - 1) / (64 - K);
   const size_t sh = 2 * (size_t)nw * (64 - K) * sizeof(float);
@@ -427,6 +424,13 @@ void launch_fwd(const RnntArgs& a, hipStream_t st) {
     case 2: hipLaunchKernelGGL((rnnt_ab_kernel<2>), dim3(2 * a.B), dim3(64 * nw), sh, st, a); break;
     default: hipLaunchKernelGGL((rnnt_ab_kernel<1>), dim3(2 * a.B), dim3(64 * nw), sh, st, a); break;
   }
+}
+
+template <int DT>
+void launch_fwd(const RnntArgs& a, hipStream_t st) {
+  const int64_t nodes = (int64_t)a.B * a.T * a.U1;
+  hipLaunchKernelGGL((rnnt_emit_kernel<DT>), dim3((unsigned)((nodes + 3) / 4)), dim3(256), 0, st, a);
+  launch_ab(a, st);
 }
 
 template <int DT, int GT>
@@ -498,6 +502,533 @@ void set_vec(RnntArgs& a, int esize) {
 
 int esize_of(int dt) { return dt == SC_F32 ? 4 : 2; }
 
+// ------------------------------------------------------------------ fused joiner (C5) -----
+// RNNTPredictorJoiner (model.py:112-145) + the fp32 log_softmax of model.py:93 + the gathered
+// lattice, WITHOUT the (B, T, U+1, V) logits (928 MB per utterance in fp32 at T=1500, U=150,
+// V=1024).  Node n = (b, t, u): z_n = tanh(enc[b,t] + pred[b,u]) (J = 64), logits_n = W z_n + bias.
+//
+//   joint_fwd_kernel  logits on MFMA (v_mfma_f32_32x32x16_bf16, W resident in LDS, z as the B
+//                     operand computed in registers), online log-sum-exp over V with the node on the
+//                     lane (the 32x32 accumulator holds one node's 16 logits per lane), blank and
+//                     label logits as direct dot products -> lse, lpb, lpy in rnnt_ab's layout.
+//   joint_dz_kernel   backward, node-major: recompute logits, dense dlogits = a_n softmax_n
+//                     (a_n = occupancy of the node's two arcs x scale), dZ^T = W^T dlogits on MFMA
+//                     with the accumulator as the operand (the sum runs over its row index, no
+//                     LDS transpose; W^T fragments by ds_read_b64_tr_b16), the sparse blank/label
+//                     terms, dpre = dZ (1 - z^2) -> d enc (accumulated over u in registers), d pred
+//                     and the blank/label rows' z sums (lane reductions over the t-block).
+//   joint_dw_kernel   backward, vocab-major: logits recomputed with v on the lane so that
+//                     dW = dlogits^T Z sums over the accumulator's row index again; 8 waves of a
+//                     workgroup own 128 rows of W each and accumulate their dW slice in registers
+//                     over the workgroup's nodes (one fp32 partial per workgroup, summed on the host
+//                     side in a fixed order).
+// Each kernel evaluates exp once per logit; the logits themselves never leave registers.
+constexpr int kJ = 64;
+constexpr int kVmaxJ = 1024;   // W image [V][64] bf16 = 128 KB of LDS
+typedef __bf16 jbf8 __attribute__((ext_vector_type(8)));
+typedef float jf16 __attribute__((ext_vector_type(16)));
+typedef short js4 __attribute__((ext_vector_type(4)));
+
+struct JointArgs {
+  RnntArgs r;
+  const float* enc;    // [B][T][64]   enc_proj(enc_out), contiguous
+  const float* pred;   // [B][U1][64]  pred_proj(embedding(blank-prefixed labels)), contiguous
+  const __bf16* W;     // [V][64]      joiner.weight
+  const float* bias;   // [V]          joiner.bias
+  int ntb, nus, S;
+  float* d_enc;        // [nus][B][T][64]
+  float* d_pred;       // [B][ntb][U1][64]
+  float* g_blank;      // [B][ntb][U1][64]  sum over the t-block of sc occ_blank z
+  float* g_label;      // [B][ntb][U1][64]  sum over the t-block of sc occ_label z
+  float* s_bl;         // [B][ntb][U1][2]   sum over the t-block of sc occ_blank, sc occ_label
+  float* dW;           // [S][V][64]       dense part a_n softmax_n z_n^T
+  float* db;           // [S][V]
+};
+
+__device__ __forceinline__ uint32_t wimg(int row, int chunk) {   // [row][8 x 16 B], XOR-swizzled
+  return (uint32_t)(row * 128 + 16 * (chunk ^ (row & 7)));
+}
+
+__device__ __forceinline__ jbf8 lds_b128(const unsigned char* lds, uint32_t off) {
+  return *(const jbf8*)(lds + off);
+}
+
+// ds_read_b64_tr_b16: group lane 4q+p addresses row R0+q, columns C0+4p..+3 of the image; lane i
+// of the group receives column C0+i of rows R0..R0+3
+__device__ __forceinline__ js4 tr_rd(const unsigned char* lds, int R0, int C0, int lane) {
+  const int i = lane & 15, q = i >> 2, p = i & 3;
+  const int row = R0 + q, col = C0 + 4 * p;
+  const uint32_t off = wimg(row, col >> 3) + 8 * ((col >> 2) & 1);
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (js4 __attribute__((address_space(3)))*)(size_t)(lds_addr(lds) + off));
+}
+
+__device__ __forceinline__ jbf8 cat8(js4 lo, js4 hi) {
+  typedef short s8 __attribute__((ext_vector_type(8)));
+  s8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(jbf8, r);
+}
+
+__device__ __forceinline__ jf16 mfma32(jbf8 a, jbf8 b, jf16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ float tanh_(float x) {
+  return 1.0f - 2.0f * rcp(exp2_(2.0f * kLog2e * x) + 1.0f);
+}
+
+// registers 8s..8s+7 of an accumulator as a bf16 fragment (k-step s of a following MFMA that
+// sums over the accumulator's row index)
+__device__ __forceinline__ jbf8 pack8(const float* p) {
+  jbf8 r;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) r[e] = (__bf16)p[e];
+  return r;
+}
+
+// the two arcs' occupancies of node (b, t, u) x the sequence's loss scale (as rnnt_grad_kernel;
+// both <= 0 there, returned here as positive weights wb, wy)
+__device__ __forceinline__ void node_weights(const RnntArgs& a, int b, int t, int u, int Tb, int Ub,
+                                             float& wb, float& wy) {
+  wb = 0.0f;
+  wy = 0.0f;
+  const double lp2 = a.ws.logp2[b];
+  const float sc = a.scale[b];
+  if (!(lp2 > -1e300) || sc == 0.0f) return;
+  const int n = t + u;
+  const int64_t base = (int64_t)b * a.ND * a.U1p;
+  const int per = 2 * a.kh, nd = Tb + Ub;
+  const double oA = a.ws.offA[(int64_t)b * a.ND + (n + 1) / per];
+  const double oB = a.ws.offB[(int64_t)b * a.ND + (nd - n - 1) / per];
+  const double al = (double)a.ws.alpha[base + (int64_t)n * a.U1p + u] + oA;
+  const float eb = a.ws.lpb[base + (int64_t)n * a.U1p + u];
+  if (t + 1 < Tb) {
+    const double be = (double)a.ws.beta[base + (int64_t)(n + 1) * a.U1p + u] + oB;
+    wb = exp2_((float)(al + eb + be - lp2));
+  } else if (u == Ub) {
+    wb = exp2_((float)(al + eb - lp2));
+  }
+  if (u < Ub) {
+    const float ey = a.ws.lpy[base + (int64_t)n * a.U1p + u];
+    const double be = (double)a.ws.beta[base + (int64_t)(n + 1) * a.U1p + u + 1] + oB;
+    wy = exp2_((float)(al + ey + be - lp2));
+  }
+  wb *= sc;
+  wy *= sc;
+}
+
+// cooperative copy of W (bf16 [V][64]) and bias into the LDS images
+__device__ __forceinline__ void load_w(const JointArgs& a, unsigned char* lds) {
+  const int V = a.r.V;
+  for (int i = threadIdx.x; i < V * 8; i += blockDim.x) {
+    const int v = i >> 3, c = i & 7;
+    *(uint4*)(lds + wimg(v, c)) = *(const uint4*)(a.W + (int64_t)v * kJ + 8 * c);
+  }
+  float* bias = (float*)(lds + kVmaxJ * 128);
+  for (int i = threadIdx.x; i < V; i += blockDim.x) bias[i] = a.bias[i];
+}
+
+// z of (b, t, u) at j = 16 s + 8 h + e (the B operand of the node-on-lane logits MFMA), bf16
+__device__ __forceinline__ void z_frags(const JointArgs& a, int b, int t, int u, bool ok, int h,
+                                        jbf8 (&zb)[4]) {
+  const float* ep = a.enc + ((int64_t)b * a.r.T + t) * kJ;
+  const float* pp = a.pred + ((int64_t)b * a.r.U1 + u) * kJ;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int j0 = 16 * s + 8 * h;
+    const float4 e0 = *(const float4*)(ep + j0), e1 = *(const float4*)(ep + j0 + 4);
+    const float4 p0 = *(const float4*)(pp + j0), p1 = *(const float4*)(pp + j0 + 4);
+    const float x[8] = {e0.x + p0.x, e0.y + p0.y, e0.z + p0.z, e0.w + p0.w,
+                        e1.x + p1.x, e1.y + p1.y, e1.z + p1.z, e1.w + p1.w};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) zb[s][e] = (__bf16)(ok ? tanh_(x[e]) : 0.0f);
+  }
+}
+
+// logits of one 32-row vocab block for the lane's node (node-on-lane orientation):
+// acc[r] = bias[v] + sum_j W[v][j] z[j], v = v0 + (r&3) + 8(r>>2) + 4h
+__device__ __forceinline__ jf16 logits_vblock(const unsigned char* lds, int v0, int lane,
+                                              const jbf8 (&zb)[4]) {
+  const int h = lane >> 5;
+  const float* bias = (const float*)(lds + kVmaxJ * 128);
+  jf16 acc;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float4 bb = *(const float4*)(bias + v0 + 8 * q + 4 * h);
+    acc[4 * q + 0] = bb.x;
+    acc[4 * q + 1] = bb.y;
+    acc[4 * q + 2] = bb.z;
+    acc[4 * q + 3] = bb.w;
+  }
+  const int row = v0 + (lane & 31);
+#pragma unroll
+  for (int s = 0; s < 4; ++s) acc = mfma32(lds_b128(lds, wimg(row, 2 * s + h)), zb[s], acc);
+  return acc;
+}
+
+// sum over the lane's half (32 lanes) of 32 values per lane; lane l ends with the total of value
+// index (l & 31) in v[0]
+__device__ __forceinline__ void half_reduce32(float (&v)[32], int lane) {
+#pragma unroll
+  for (int st = 16; st >= 1; st >>= 1) {
+    const bool up = (lane & st) != 0;
+#pragma unroll
+    for (int i = 0; i < st; ++i) {
+      const float keep = up ? v[i + st] : v[i];
+      const float send = up ? v[i] : v[i + st];
+      v[i] = keep + __shfl_xor(send, st);
+    }
+  }
+}
+
+__device__ __forceinline__ float half_sum(float x) {
+#pragma unroll
+  for (int o = 16; o >= 1; o >>= 1) x += __shfl_xor(x, o);
+  return x;
+}
+
+__global__ void __launch_bounds__(256) joint_fwd_kernel(JointArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  load_w(a, lds);
+  __syncthreads();
+  const RnntArgs& r = a.r;
+  const int lane = threadIdx.x & 63, h = lane >> 5;
+  const int nup = (r.U1 + 1) / 2;
+  const int64_t ntask = (int64_t)r.B * a.ntb * nup;
+  const int64_t wid = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6), nwv = (int64_t)gridDim.x * 4;
+  for (int64_t task = wid; task < ntask; task += nwv) {
+    const int b = (int)(task / ((int64_t)a.ntb * nup));
+    const int tb = (int)((task / nup) % a.ntb), up = (int)(task % nup);
+    const int Tb = clampr(r.flen[b], 0, r.T), Ub = clampr(r.llen[b], 0, r.Umax);
+    const int t = tb * 32 + (lane & 31);
+    if (uniform(tb * 32) >= Tb || 2 * up > Ub) continue;
+    const bool tok = t < Tb;
+    const int tc = tok ? t : Tb - 1;
+    const int nc = (2 * up + 1 <= Ub) ? 2 : 1;
+    jbf8 zb[2][4];
+    float m[2], s[2];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      if (c < nc) z_frags(a, b, tc, 2 * up + c, tok, h, zb[c]);
+      m[c] = -__builtin_huge_valf();
+      s[c] = 0.0f;
+    }
+    for (int v0 = 0; v0 < r.V; v0 += 32) {
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        if (c >= nc) break;
+        const jf16 x = logits_vblock(lds, v0, lane, zb[c]);
+        float bm = x[0];
+#pragma unroll
+        for (int q = 1; q < 16; ++q) bm = fmaxf(bm, x[q]);
+        const float mn = fmaxf(m[c], bm), ml = mn * kLog2e;
+        float acc = s[c] * exp2_(m[c] * kLog2e - ml);
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc += exp2_(fmaf(x[q], kLog2e, -ml));
+        s[c] = acc;
+        m[c] = mn;
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      if (c >= nc) break;
+      const int u = 2 * up + c;
+      const float mo = __shfl_xor(m[c], 32), so = __shfl_xor(s[c], 32);
+      const float M = fmaxf(m[c], mo);
+      const float lse = M + flog(s[c] * exp2_((m[c] - M) * kLog2e) + so * exp2_((mo - M) * kLog2e));
+      // blank and label logits: dot products over the lane's 32 j, halves combined
+      const int yl = u < Ub ? label_at(r, b, u) : r.blank;
+      float lb = 0.0f, ly = 0.0f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const jbf8 wb = lds_b128(lds, wimg(r.blank, 2 * q + h));
+        const jbf8 wy = lds_b128(lds, wimg(yl, 2 * q + h));
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float zf = (float)zb[c][q][e];
+          lb = fmaf((float)wb[e], zf, lb);
+          ly = fmaf((float)wy[e], zf, ly);
+        }
+      }
+      lb += __shfl_xor(lb, 32);
+      ly += __shfl_xor(ly, 32);
+      const float* bias = (const float*)(lds + kVmaxJ * 128);
+      lb += bias[r.blank];
+      ly += bias[yl];
+      if (h == 0 && tok) {
+        const int64_t node = ((int64_t)b * r.T + t) * r.U1 + u;
+        const int64_t d = ((int64_t)b * r.ND + t + u) * r.U1p + u;
+        r.ws.lse[node] = lse;
+        r.ws.lpb[d] = fmaxf((lb - lse) * kLog2e, kDeadR);
+        r.ws.lpy[d] = u < Ub ? fmaxf((ly - lse) * kLog2e, kDeadR) : kDeadR;
+      }
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) joint_dz_kernel(JointArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  load_w(a, lds);
+  __syncthreads();
+  const RnntArgs& r = a.r;
+  const int lane = threadIdx.x & 63, h = lane >> 5, g1 = (lane >> 4) & 1;
+  const int64_t ntask = (int64_t)r.B * a.ntb * a.nus;
+  const int64_t wid = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6), nwv = (int64_t)gridDim.x * 4;
+  const float* bias = (const float*)(lds + kVmaxJ * 128);
+  for (int64_t task = wid; task < ntask; task += nwv) {
+    const int b = (int)(task / ((int64_t)a.ntb * a.nus));
+    const int tb = (int)((task / a.nus) % a.ntb), us = (int)(task % a.nus);
+    const int Tb = clampr(r.flen[b], 0, r.T), Ub = clampr(r.llen[b], 0, r.Umax);
+    const int t = tb * 32 + (lane & 31);
+    const bool tok = t < Tb;
+    const int tc = tok ? t : max(Tb - 1, 0);
+    // this task's u range (pairs of columns)
+    const int ua = (int)((int64_t)us * r.U1 / a.nus), ue = (int)((int64_t)(us + 1) * r.U1 / a.nus);
+    float de[32];
+#pragma unroll
+    for (int i = 0; i < 32; ++i) de[i] = 0.0f;
+    const bool live = uniform(tb * 32) < Tb;
+    for (int u0 = ua; live && u0 < ue && u0 <= Ub; u0 += 2) {
+      const int nc = (u0 + 1 < ue && u0 + 1 <= Ub) ? 2 : 1;
+      jbf8 zb[2][4];
+      float lse2[2], an[2], wbn[2], wyn[2];
+      jf16 Y[2][2];
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        if (c >= nc) break;
+        const int u = u0 + c;
+        z_frags(a, b, tc, u, tok, h, zb[c]);
+        float wb = 0.0f, wy = 0.0f;
+        if (tok) node_weights(r, b, t, u, Tb, Ub, wb, wy);
+        wbn[c] = wb;
+        wyn[c] = wy;
+        an[c] = wb + wy;
+        lse2[c] = tok ? r.ws.lse[((int64_t)b * r.T + t) * r.U1 + u] * kLog2e : 1e30f;
+#pragma unroll
+        for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+          for (int q = 0; q < 16; ++q) Y[c][jb][q] = 0.0f;
+      }
+      for (int v0 = 0; v0 < r.V; v0 += 32) {
+        // W^T fragments for dZ^T = W^T dlogits: k-step s covers rows v0 + 16 s + 8 (e>>2) + 4 h + (e&3)
+        jbf8 wt[2][2];
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+          for (int jb = 0; jb < 2; ++jb)
+            wt[s2][jb] = cat8(tr_rd(lds, v0 + 16 * s2 + 4 * h, jb * 32 + 16 * g1, lane),
+                              tr_rd(lds, v0 + 16 * s2 + 8 + 4 * h, jb * 32 + 16 * g1, lane));
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          if (c >= nc) break;
+          const jf16 x = logits_vblock(lds, v0, lane, zb[c]);
+          float p[16];
+#pragma unroll
+          for (int q = 0; q < 16; ++q) p[q] = an[c] * exp2_(fmaf(x[q], kLog2e, -lse2[c]));
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2) {
+            const jbf8 xf = pack8(p + 8 * s2);
+#pragma unroll
+            for (int jb = 0; jb < 2; ++jb) Y[c][jb] = mfma32(wt[s2][jb], xf, Y[c][jb]);
+          }
+        }
+      }
+      // Y[c][jb][q] = dZ_dense[node][j], j = jb*32 + (q&3) + 8(q>>2) + 4h
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        if (c >= nc) break;
+        const int u = u0 + c;
+        const int yl = u < Ub ? label_at(r, b, u) : r.blank;
+        const float* ep = r.T ? a.enc + ((int64_t)b * r.T + tc) * kJ : a.enc;
+        const float* pp = a.pred + ((int64_t)b * r.U1 + u) * kJ;
+        float dp[32], gbz[32], gyz[32];
+#pragma unroll
+        for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int j0 = jb * 32 + 8 * q + 4 * h;
+            const float4 ev = *(const float4*)(ep + j0);
+            const float4 pv = *(const float4*)(pp + j0);
+            const js4 wbv = *(const js4*)(lds + wimg(r.blank, j0 >> 3) + 8 * h);
+            const js4 wyv = *(const js4*)(lds + wimg(yl, j0 >> 3) + 8 * h);
+            const float xs[4] = {ev.x + pv.x, ev.y + pv.y, ev.z + pv.z, ev.w + pv.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const int i = jb * 16 + 4 * q + e;
+              const float z = tok ? tanh_(xs[e]) : 0.0f;
+              const float wbj = __uint_as_float((uint32_t)(uint16_t)wbv[e] << 16);
+              const float wyj = __uint_as_float((uint32_t)(uint16_t)wyv[e] << 16);
+              const float dz = Y[c][jb][4 * q + e] - wbn[c] * wbj - wyn[c] * wyj;
+              dp[i] = dz * (1.0f - z * z);
+              de[i] += dp[i];
+              gbz[i] = wbn[c] * z;
+              gyz[i] = wyn[c] * z;
+            }
+          }
+        half_reduce32(dp, lane);
+        half_reduce32(gbz, lane);
+        half_reduce32(gyz, lane);
+        const int i = lane & 31;
+        const int j = (i >> 4) * 32 + (i & 3) + 8 * ((i & 15) >> 2) + 4 * h;
+        const int64_t row = (((int64_t)b * a.ntb + tb) * r.U1 + u) * kJ + j;
+        a.d_pred[row] = dp[0];
+        a.g_blank[row] = gbz[0];
+        a.g_label[row] = gyz[0];
+        const float sb = half_sum(wbn[c]), sy = half_sum(wyn[c]);
+        if (lane == 0) {
+          const int64_t srow = (((int64_t)b * a.ntb + tb) * r.U1 + u) * 2;
+          a.s_bl[srow] = sb;
+          a.s_bl[srow + 1] = sy;
+        }
+      }
+    }
+    if (t < r.T) {
+      float* dst = a.d_enc + (((int64_t)us * r.B + b) * r.T + t) * kJ;
+#pragma unroll
+      for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int i = jb * 16 + 4 * q;
+          *(float4*)(dst + jb * 32 + 8 * q + 4 * h) = make_float4(de[i], de[i + 1], de[i + 2], de[i + 3]);
+        }
+    }
+  }
+}
+
+__global__ void __launch_bounds__(512) joint_dw_kernel(JointArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  load_w(a, lds);
+  unsigned char* zimg = lds + kVmaxJ * 128 + kVmaxJ * 4;   // [32 nodes][64] bf16, swizzled rows
+  float* s_lse2 = (float*)(zimg + 32 * 128);
+  float* s_a = s_lse2 + 32;
+  const RnntArgs& r = a.r;
+  const int lane = threadIdx.x & 63, h = lane >> 5, g1 = (lane >> 4) & 1;
+  const int w = threadIdx.x >> 6;
+  const float* bias = (const float*)(lds + kVmaxJ * 128);
+  const int nvb = r.V / 32;
+  // wave w owns vocab blocks w, w + 8, ... (nvb <= 32: at most 4 each)
+  jf16 acc[4][2];
+  float dbs[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    dbs[k] = 0.0f;
+#pragma unroll
+    for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[k][jb][q] = 0.0f;
+  }
+  const int64_t ncol = (int64_t)r.B * a.ntb * r.U1;
+  const int64_t c0 = (int64_t)blockIdx.x * ncol / gridDim.x, c1 = (int64_t)(blockIdx.x + 1) * ncol / gridDim.x;
+  for (int64_t col = c0; col < c1; ++col) {
+    const int b = (int)(col / ((int64_t)a.ntb * r.U1));
+    const int tb = (int)((col / r.U1) % a.ntb), u = (int)(col % r.U1);
+    const int Tb = clampr(r.flen[b], 0, r.T), Ub = clampr(r.llen[b], 0, r.Umax);
+    if (tb * 32 >= Tb || u > Ub) continue;   // uniform over the workgroup
+    __syncthreads();   // the previous column's readers are done with zimg / scalars
+    {
+      const int n = threadIdx.x >> 4, jq = threadIdx.x & 15;   // node, 4-j group
+      const int t = tb * 32 + n;
+      const bool ok = t < Tb;
+      const int tc = ok ? t : Tb - 1;
+      const float4 ev = *(const float4*)(a.enc + ((int64_t)b * r.T + tc) * kJ + 4 * jq);
+      const float4 pv = *(const float4*)(a.pred + ((int64_t)b * r.U1 + u) * kJ + 4 * jq);
+      js4 zz;
+      const float xs[4] = {ev.x + pv.x, ev.y + pv.y, ev.z + pv.z, ev.w + pv.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        zz[e] = __builtin_bit_cast(short, (__bf16)(ok ? tanh_(xs[e]) : 0.0f));
+      *(js4*)(zimg + wimg(n, jq >> 1) + 8 * (jq & 1)) = zz;
+      if (threadIdx.x < 32) {   // node scalars, one thread per node
+        const int tn = tb * 32 + threadIdx.x;
+        const bool okn = tn < Tb;
+        float wb = 0.0f, wy = 0.0f;
+        if (okn) node_weights(r, b, tn, u, Tb, Ub, wb, wy);
+        s_a[threadIdx.x] = wb + wy;
+        s_lse2[threadIdx.x] = okn ? r.ws.lse[((int64_t)b * r.T + tn) * r.U1 + u] * kLog2e : 1e30f;
+      }
+    }
+    __syncthreads();
+    // node scalars of this lane's 16 accumulator rows: node = (q&3) + 8(q>>2) + 4h
+    float l2[16], an[16];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 lv = *(const float4*)(s_lse2 + 8 * q + 4 * h);
+      const float4 av = *(const float4*)(s_a + 8 * q + 4 * h);
+      l2[4 * q] = lv.x; l2[4 * q + 1] = lv.y; l2[4 * q + 2] = lv.z; l2[4 * q + 3] = lv.w;
+      an[4 * q] = av.x; an[4 * q + 1] = av.y; an[4 * q + 2] = av.z; an[4 * q + 3] = av.w;
+    }
+    // Z is the A operand of the logits (node on the row, j = 16 s + 8 h + e) and the B operand of
+    // dW (k = node in the accumulator's row order, column j): one image, row and tr reads,
+    // re-read per vocab block (LDS reads are cheaper than the registers to hold them)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int vb = w + 8 * k;
+      if (vb >= nvb) break;
+      const int v = vb * 32 + (lane & 31);
+      jf16 x;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) x[q] = 0.0f;
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+        x = mfma32(lds_b128(zimg, wimg(lane & 31, 2 * s + h)), lds_b128(lds, wimg(v, 2 * s + h)), x);
+      const float bl = bias[v] * kLog2e;
+      float p[16], ps = 0.0f;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        p[q] = an[q] * exp2_(fmaf(x[q], kLog2e, bl - l2[q]));
+        ps += p[q];
+      }
+      dbs[k] += ps;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const jbf8 xf = pack8(p + 8 * s2);
+#pragma unroll
+        for (int jb = 0; jb < 2; ++jb) {
+          const jbf8 zt = cat8(tr_rd(zimg, 16 * s2 + 4 * h, jb * 32 + 16 * g1, lane),
+                               tr_rd(zimg, 16 * s2 + 8 + 4 * h, jb * 32 + 16 * g1, lane));
+          acc[k][jb] = mfma32(xf, zt, acc[k][jb]);
+        }
+      }
+    }
+  }
+  // acc[k][jb][q] = dW[v = vb*32 + (q&3) + 8(q>>2) + 4h][j = jb*32 + (lane&31)]
+  float* dw = a.dW + (int64_t)blockIdx.x * r.V * kJ;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int vb = w + 8 * k;
+    if (vb >= nvb) break;
+#pragma unroll
+    for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int v = vb * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
+        dw[(int64_t)v * kJ + jb * 32 + (lane & 31)] = acc[k][jb][q];
+      }
+    const float tot = dbs[k] + __shfl_xor(dbs[k], 32);
+    if (h == 0) a.db[(int64_t)blockIdx.x * r.V + vb * 32 + (lane & 31)] = tot;
+  }
+}
+
+size_t joint_lds_fwd() { return (size_t)kVmaxJ * 128 + kVmaxJ * 4; }
+
+template <typename K>
+bool joint_lds_attr(K kern, size_t bytes) {
+  return hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)bytes) == hipSuccess;
+}
+size_t joint_lds_dw() { return joint_lds_fwd() + 32 * 128 + 2 * 32 * 4; }
+
+void joint_geometry(int B, int T, int Umax, int* ntb, int* nus, int* S) {
+  *ntb = (T + 31) / 32;
+  // d enc is accumulated over u in registers; split u only as far as needed to give every SIMD
+  // about three (b, t-block) tasks
+  const int64_t base = (int64_t)B * *ntb;
+  int n = 1;
+  while (n < 8 && base * n < 3 * 1024 && n < Umax + 1) n *= 2;
+  *nus = n;
+  *S = 256;
+}
+
 }  // namespace
 
 }  // namespace sc
@@ -568,4 +1099,105 @@ extern "C" int sc_rnnt_bwd(const void* x, int x_dtype, int is_logits, int B, int
     }
   }
   return launch_status("sc_rnnt_bwd");
+}
+
+// ------------------------------------------------------------------ fused joiner entry points --
+
+namespace sc {
+namespace {
+int joint_check(const float* enc, const float* pred, const void* W, const float* bias, int B, int T,
+                int Umax, int V, int J, const int64_t* labels, const int64_t* fl,
+                const int64_t* ll, int blank, const void* ws, size_t wsb, const char* who) {
+  SC_REQUIRE(J == kJ, "%s: join_dim %d (only 64, train.py:639's default, is compiled)", who, J);
+  SC_REQUIRE(V > 0 && V % 32 == 0 && V <= kVmaxJ, "%s: V=%d must be a multiple of 32 <= %d", who, V,
+             kVmaxJ);
+  SC_REQUIRE(B >= 0 && T >= 0 && Umax >= 0, "%s: bad shape", who);
+  SC_REQUIRE(ab_halo_k(Umax) > 0, "%s: max label count %d exceeds %d", who, Umax, 16 * 63 - 1);
+  SC_REQUIRE(blank >= 0 && blank < V, "%s: blank %d outside [0, %d)", who, blank, V);
+  SC_REQUIRE((int64_t)B * T * (Umax + 1) < (1ll << 40), "%s: lattice too large", who);
+  if (B == 0 || T == 0) return 0;
+  SC_REQUIRE(enc && pred && W && bias && fl && ll && ws, "%s: null pointer", who);
+  SC_REQUIRE(Umax == 0 || labels, "%s: null labels", who);
+  SC_REQUIRE(((uintptr_t)enc | (uintptr_t)pred | (uintptr_t)W) % 16 == 0, "%s: unaligned operand", who);
+  SC_REQUIRE(wsb >= ws_layout(B, T, Umax, nullptr, nullptr), "%s: workspace too small", who);
+  return 0;
+}
+
+JointArgs joint_args(const float* enc, const float* pred, const void* W, const float* bias, int B,
+                     int T, int Umax, int V, const int64_t* labels, int64_t labs,
+                     const int64_t* fl, const int64_t* ll, int blank, float* nll, const void* ws,
+                     const float* scale) {
+  JointArgs j;
+  j.r = make_args(enc, 1, B, T, Umax, V, 0, 0, 0, nullptr, labels, labs, fl, ll, blank, nll, ws,
+                  scale, nullptr);
+  j.enc = enc;
+  j.pred = pred;
+  j.W = (const __bf16*)W;
+  j.bias = bias;
+  joint_geometry(B, T, Umax, &j.ntb, &j.nus, &j.S);
+  j.d_enc = j.d_pred = j.g_blank = j.g_label = j.s_bl = j.dW = j.db = nullptr;
+  return j;
+}
+}  // namespace
+}  // namespace sc
+
+extern "C" int sc_rnnt_joint_geometry(int B, int T, int max_labels, int* t_blocks, int* u_splits,
+                                      int* slices) {
+  clear_error();
+  SC_REQUIRE(t_blocks && u_splits && slices, "sc_rnnt_joint_geometry: null pointer");
+  joint_geometry(B, T, max_labels, t_blocks, u_splits, slices);
+  return 0;
+}
+
+extern "C" int sc_rnnt_joint_fwd(const float* enc, const float* pred, const void* W, const float* bias,
+                                 int B, int T, int max_labels, int V, int J, const int64_t* labels,
+                                 int64_t label_stride, const int64_t* frames_lengths,
+                                 const int64_t* labels_lengths, int blank, float* nll,
+                                 void* workspace, size_t workspace_bytes, void* stream) {
+  clear_error();
+  int rc = joint_check(enc, pred, W, bias, B, T, max_labels, V, J, labels, frames_lengths,
+                       labels_lengths, blank, workspace, workspace_bytes, "sc_rnnt_joint_fwd");
+  if (rc) return rc;
+  if (B == 0) return 0;
+  SC_REQUIRE(nll && T > 0, "sc_rnnt_joint_fwd: null nll / T == 0 is handled by the caller");
+  JointArgs j = joint_args(enc, pred, W, bias, B, T, max_labels, V, labels, label_stride,
+                           frames_lengths, labels_lengths, blank, nll, workspace, nullptr);
+  static const bool ok = joint_lds_attr(joint_fwd_kernel, joint_lds_fwd());
+  SC_REQUIRE(ok, "sc_rnnt_joint_fwd: LDS attribute");
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(joint_fwd_kernel, dim3(256), dim3(256), joint_lds_fwd(), st, j);
+  launch_ab(j.r, st);
+  return launch_status("sc_rnnt_joint_fwd");
+}
+
+extern "C" int sc_rnnt_joint_bwd(const float* enc, const float* pred, const void* W, const float* bias,
+                                 int B, int T, int max_labels, int V, int J, const int64_t* labels,
+                                 int64_t label_stride, const int64_t* frames_lengths,
+                                 const int64_t* labels_lengths, int blank, const float* scale,
+                                 float* d_enc, float* d_pred, float* g_blank, float* g_label,
+                                 float* s_bl, float* dW, float* db, const void* workspace,
+                                 size_t workspace_bytes, void* stream) {
+  clear_error();
+  int rc = joint_check(enc, pred, W, bias, B, T, max_labels, V, J, labels, frames_lengths,
+                       labels_lengths, blank, workspace, workspace_bytes, "sc_rnnt_joint_bwd");
+  if (rc) return rc;
+  if (B == 0 || T == 0) return 0;
+  SC_REQUIRE(scale && d_enc && d_pred && g_blank && g_label && s_bl && dW && db,
+             "sc_rnnt_joint_bwd: null output");
+  JointArgs j = joint_args(enc, pred, W, bias, B, T, max_labels, V, labels, label_stride,
+                           frames_lengths, labels_lengths, blank, nullptr, workspace, scale);
+  j.d_enc = d_enc;
+  j.d_pred = d_pred;
+  j.g_blank = g_blank;
+  j.g_label = g_label;
+  j.s_bl = s_bl;
+  j.dW = dW;
+  j.db = db;
+  static const bool ok1 = joint_lds_attr(joint_dz_kernel, joint_lds_fwd());
+  static const bool ok2 = joint_lds_attr(joint_dw_kernel, joint_lds_dw());
+  SC_REQUIRE(ok1 && ok2, "sc_rnnt_joint_bwd: LDS attribute");
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(joint_dz_kernel, dim3(256), dim3(256), joint_lds_fwd(), st, j);
+  hipLaunchKernelGGL(joint_dw_kernel, dim3(j.S), dim3(512), joint_lds_dw(), st, j);
+  return launch_status("sc_rnnt_joint_bwd");
 }

@@ -14,7 +14,7 @@ import torch.nn as nn
 from .lucyrnn_conf import LucyRNNConfig
 from .lucyrnn_triton import LucyRNNtriton
 from .xlstm import xLSTMLarge, xLSTMLargeConfig
-from .ops import ctc_loss, rnnt_loss
+from .ops import ctc_loss, rnnt_joint_loss, rnnt_loss
 
 
 def detach_states(states):
@@ -93,6 +93,15 @@ def compute_loss(mode: str, criterion: nn.Module, model: nn.Module, feats: torch
                                   device=tokens.device)
         predictor_input = torch.cat([blank_prefix, tokens], dim=1)
         use_compact = bool(getattr(args, "compact_rnnt", False)) if args is not None else compact
+        if isinstance(criterion, RNNTLoss) and enc_out.is_cuda:
+            # fused joiner + log_softmax + lattice (rnnt.hip joint_*): the (B, T, U+1, V) logits
+            # are never materialised; same value as the compact and dense paths below
+            enc_p, pred_p, W, bias = (use_rnnt_joiner(enc_out, predictor_input, in_lens, tgt_lens,
+                                                      project_only=True) if use_compact else
+                                      use_rnnt_joiner(enc_out, predictor_input, project_only=True))
+            loss = criterion.forward_joint(enc_p, pred_p, W, bias, tokens, in_lens, tgt_lens,
+                                           blank_id=blank_id)
+            return loss, output_state, enc_out, output_state
         if use_compact:
             logits = use_rnnt_joiner(enc_out, predictor_input, in_lens, tgt_lens)
         else:
@@ -139,6 +148,13 @@ class RNNTLoss(nn.Module):
                          blank=self.blank if blank_id is None else blank_id, compact=compact,
                          is_logits=True)
 
+    def forward_joint(self, enc_p, pred_p, W, bias, labels, frames_lengths, labels_lengths,
+                      blank_id=None):
+        """The loss straight from the joiner's projections (ops.RNNTJointFn)."""
+        return rnnt_joint_loss(enc_p, pred_p, W, bias, labels, frames_lengths, labels_lengths,
+                               blank=self.blank if blank_id is None else blank_id,
+                               reduction=self.reduction, average_frames=self.average_frames)
+
 
 class RNNTPredictorJoiner(nn.Module):
     """model.py:112-145: embedding predictor + additive joint + tanh + output projection over
@@ -154,9 +170,11 @@ class RNNTPredictorJoiner(nn.Module):
         self.debug = debug
         self.joiner = nn.Linear(join_dim, vocab_size)
 
-    def forward(self, enc_out: torch.Tensor, prefix: torch.Tensor):
+    def forward(self, enc_out: torch.Tensor, prefix: torch.Tensor, project_only: bool = False):
         pred = self.pred_proj(self.embedding(prefix))            # (B, U+1, J)
         enc = self.enc_proj(enc_out)                             # (B, T, J)
+        if project_only:   # inputs of the fused joiner + loss (compute_loss); through forward()
+            return enc, pred, self.joiner.weight, self.joiner.bias   # so DDP sees the call
         joint = torch.tanh(enc.unsqueeze(2) + pred.unsqueeze(1))  # (B, T, U+1, J)
         return self.joiner(joint)                                # (B, T, U+1, V)
 
@@ -184,7 +202,10 @@ class RNNTCompactPredictorJoiner(nn.Module):
                         .reshape(T * U, -1))
         return self.joiner(torch.cat(rows, 0))
 
-    def forward(self, enc_out, prefix, in_lens, tgt_lens):
+    def forward(self, enc_out, prefix, in_lens, tgt_lens, project_only: bool = False):
+        if project_only:   # the fused path needs no packing: it never builds the rows
+            return (self.enc_proj(enc_out), self.pred_proj(self.embedding(prefix)),
+                    self.joiner.weight, self.joiner.bias)
         return self.forward_compact(enc_out, prefix, in_lens, tgt_lens)
 
 

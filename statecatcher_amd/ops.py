@@ -665,6 +665,129 @@ def rnnt_loss(log_probs, labels, frames_lengths, labels_lengths, average_frames=
     raise ValueError(f"unknown reduction {reduction!r}")
 
 
+class RNNTJointFn(torch.autograd.Function):
+    """nll [B] fp32 of the fused joiner + lattice (rnnt.hip joint_* kernels): z = tanh(enc_p[b,t]
+    + pred_p[b,u]), logits = z W^T + bias, log_softmax, gathered RNN-T lattice -- the reference's
+    RNNTPredictorJoiner (model.py:129-145) + log_softmax (model.py:93) + warp_rnnt, with the
+    (B, T, U+1, V) logits never materialised.  enc_p [B,T,64], pred_p [B,U+1,64] are the
+    joiner's enc_proj / pred_proj outputs; W [V,64] enters the MFMA in bf16, everything else fp32.
+    Backward: d enc_p, d pred_p, dW, d bias (partials summed here in a fixed order)."""
+
+    @staticmethod
+    def forward(ctx, enc_p, pred_p, W, bias, labels, flen, llen, blank):
+        require_device(enc_p, pred_p, W, bias, labels, flen, llen)
+        B, T, J = enc_p.shape
+        U1 = pred_p.shape[1]
+        Umax = U1 - 1
+        V = W.shape[0]
+        if pred_p.shape[0] != B or pred_p.shape[2] != J or W.shape[1] != J or bias.shape != (V,):
+            raise ValueError(f"joint shapes: enc {tuple(enc_p.shape)} pred {tuple(pred_p.shape)} "
+                             f"W {tuple(W.shape)} bias {tuple(bias.shape)}")
+        encc = enc_p.detach().float().contiguous()
+        predc = pred_p.detach().float().contiguous()
+        wb = W.detach().to(torch.bfloat16).contiguous()
+        bf = bias.detach().float().contiguous()
+        labels = labels.to(torch.int64)
+        if labels.dim() != 2 or labels.shape[0] != B:
+            raise ValueError(f"labels must be padded [B, U], got {tuple(labels.shape)}")
+        if labels.shape[1] < Umax:
+            labels = torch.nn.functional.pad(labels, (0, Umax - labels.shape[1]))
+        labels = labels[:, :Umax].contiguous()
+        lib = _lib.load()
+        wsb = lib.sc_rnnt_workspace_bytes(B, max(T, 1), Umax)
+        ws = torch.empty(wsb, dtype=torch.uint8, device=enc_p.device)
+        nll = torch.empty(B, dtype=torch.float32, device=enc_p.device)
+        if T == 0 or B == 0:
+            nll.fill_(float("inf"))
+        else:
+            with _timed("rnnt_joint_fwd", encc, 0):
+                rc = lib.sc_rnnt_joint_fwd(ptr(encc), ptr(predc), ptr(wb), ptr(bf), B, T, Umax, V, J,
+                                           ptr(labels), labels.stride(0) if Umax else 0, ptr(flen),
+                                           ptr(llen), int(blank), ptr(nll), ptr(ws), wsb,
+                                           stream_of(encc))
+            check(rc, "sc_rnnt_joint_fwd")
+        ctx.save_for_backward(encc, predc, wb, bf, labels, flen, llen, ws)
+        ctx.meta = (int(blank), wsb, enc_p.dtype, pred_p.dtype, W.dtype, bias.dtype)
+        return nll
+
+    @staticmethod
+    def backward(ctx, grad_nll):
+        encc, predc, wb, bf, labels, flen, llen, ws = ctx.saved_tensors
+        blank, wsb, edt, pdt, wdt, bdt = ctx.meta
+        B, T, J = encc.shape
+        U1 = predc.shape[1]
+        Umax = U1 - 1
+        V = wb.shape[0]
+        dev = encc.device
+        if T == 0 or B == 0:
+            return (torch.zeros_like(encc).to(edt), torch.zeros_like(predc).to(pdt),
+                    torch.zeros(V, J, dtype=wdt, device=dev), torch.zeros(V, dtype=bdt, device=dev),
+                    None, None, None, None)
+        lib = _lib.load()
+        geo = [ctypes_int() for _ in range(3)]
+        check(lib.sc_rnnt_joint_geometry(B, T, Umax, *[_addr(g) for g in geo]), "sc_rnnt_joint_geometry")
+        ntb, nus, S = (g.value for g in geo)
+        f32 = dict(dtype=torch.float32, device=dev)
+        d_enc = torch.empty(nus, B, T, J, **f32)
+        d_pred = torch.zeros(B, ntb, U1, J, **f32)
+        g_blank = torch.zeros(B, ntb, U1, J, **f32)
+        g_label = torch.zeros(B, ntb, U1, J, **f32)
+        s_bl = torch.zeros(B, ntb, U1, 2, **f32)
+        dW = torch.empty(S, V, J, **f32)
+        db = torch.empty(S, V, **f32)
+        scale = grad_nll.to(torch.float32).contiguous()
+        with _timed("rnnt_joint_bwd", encc, 0):
+            rc = lib.sc_rnnt_joint_bwd(ptr(encc), ptr(predc), ptr(wb), ptr(bf), B, T, Umax, V, J,
+                                       ptr(labels), labels.stride(0) if Umax else 0, ptr(flen),
+                                       ptr(llen), blank, ptr(scale), ptr(d_enc), ptr(d_pred),
+                                       ptr(g_blank), ptr(g_label), ptr(s_bl), ptr(dW), ptr(db),
+                                       ptr(ws), wsb, stream_of(encc))
+        check(rc, "sc_rnnt_joint_bwd")
+        # fixed-order sums of the partials, then the sparse blank / label arcs of dW and d bias:
+        # dlogits_n = a_n softmax_n - w_blank,n e_blank - w_label,n e_{y[b,u]}
+        dWt = colsum(dW.view(S, V * J)).view(V, J)
+        dbt = colsum(db)
+        gl = g_label.sum(1)[:, :Umax].reshape(-1, J)                 # [B*Umax, J]
+        sl = s_bl.sum(1)                                             # [B, U1, 2]
+        onehot = torch.nn.functional.one_hot(labels.clamp(0, V - 1), V).to(torch.float32)
+        onehot = onehot.view(-1, V)                                  # [B*Umax, V]
+        dWt[blank] -= g_blank.sum((0, 1, 2))
+        dbt[blank] -= sl[..., 0].sum()
+        if Umax:
+            dWt -= onehot.t() @ gl
+            dbt -= onehot.t() @ sl[:, :Umax, 1].reshape(-1)
+        return (d_enc.sum(0).to(edt), d_pred.sum(1).to(pdt), dWt.to(wdt), dbt.to(bdt),
+                None, None, None, None)
+
+
+def ctypes_int():
+    import ctypes
+    return ctypes.c_int(0)
+
+
+def _addr(c):
+    import ctypes
+    return ctypes.addressof(c)
+
+
+def rnnt_joint_loss(enc_p, pred_p, W, bias, labels, frames_lengths, labels_lengths, blank=0,
+                    reduction="mean", average_frames=False):
+    """warp_rnnt's reductions over the fused joiner + lattice (RNNTJointFn)."""
+    dev = enc_p.device
+    fl = _as_len_tensor(frames_lengths, dev)
+    ll = _as_len_tensor(labels_lengths, dev)
+    nll = RNNTJointFn.apply(enc_p, pred_p, W, bias, labels.to(dev), fl, ll, int(blank))
+    if average_frames:
+        nll = nll / fl.clamp_min(1).to(nll.dtype)
+    if reduction == "none":
+        return nll
+    if reduction == "sum":
+        return nll.sum()
+    if reduction == "mean":
+        return nll.mean()
+    raise ValueError(f"unknown reduction {reduction!r}")
+
+
 # ----------------------------------------------------------------------------- mLSTM ---------
 class MLSTMFn(torch.autograd.Function):
     """mLSTM cell (mlstm.hip) over q, k [B,NH,T,DQ], v [B,NH,T,DV], gate pre-activations

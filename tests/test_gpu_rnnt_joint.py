@@ -1,0 +1,173 @@
+"""GPU parity of the fused RNN-T joiner + loss (rnnt.hip joint_* kernels, ops.RNNTJointFn).
+
+The reference computes RNNTPredictorJoiner (model.py:129-145) -> (B, T, U+1, V) logits ->
+log_softmax in fp32 (model.py:93) -> warp_rnnt (gather=True).  The fused kernels never build the
+logits; W and z = tanh(enc + pred) enter the MFMA in bf16 with fp32 accumulation.
+
+* Small lattices against an fp64 CPU restatement with the SAME bf16 rounding of W and z
+  (oracle/rnnt.py lattice, pinned by brute-force alignment sums): nll to 1e-4 relative; the
+  gradients of enc_proj / pred_proj outputs, W and bias to 1e-2 in norm (the backward's dlogits
+  also enter its MFMAs in bf16).
+* A C5-sized lattice (T=1500, U=150, V=1024, B=2) against the unfused HIP path on materialised
+  logits (the validated sc_rnnt_* kernels): nll 1e-3, gradients 2e-2 in norm; deterministic.
+* compute_loss(mode="rnnt") with RNNTLoss runs the fused path for both joiners, DDP-safe
+  (through the joiner's forward), and equals the materialised path.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import rnnt as ornnt
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0") if torch.cuda.is_available() else None
+
+
+def sc():
+    import statecatcher_amd as s
+    return s
+
+
+def ref_fp64(enc_p, pred_p, W, bias, labels, fl, ll, blank):
+    """nll and gradients (enc_p, pred_p, W, bias) in fp64 with the kernels' bf16 roundings."""
+    e = enc_p.double().cpu().requires_grad_(True)
+    p = pred_p.double().cpu().requires_grad_(True)
+    w = W.double().cpu().requires_grad_(True)
+    b = bias.double().cpu().requires_grad_(True)
+    z = torch.tanh(e.unsqueeze(2) + p.unsqueeze(1))
+    zq = z + (z.to(torch.bfloat16).double() - z).detach()          # bf16 value, identity grad
+    wq = w + (w.to(torch.bfloat16).double() - w).detach()
+    logits = zq @ wq.t() + b
+    lp = logits.log_softmax(-1)
+    nll = []
+    glp = torch.zeros_like(lp)
+    for i in range(lp.shape[0]):
+        Tb, Ub = int(fl[i]), int(ll[i])
+        if Tb == 0:
+            nll.append(np.inf)
+            continue
+        n, g = ornnt.rnnt_single(lp[i, :Tb, :Ub + 1].detach().numpy(), labels[i, :Ub].numpy(), blank)
+        nll.append(n)
+        glp[i, :Tb, :Ub + 1] = torch.from_numpy(g) / lp.shape[0]   # mean reduction
+    lp.backward(glp)
+    return np.array(nll), e.grad, p.grad, w.grad, b.grad
+
+
+def case(B, T, Umax, V, seed, Tb=None, Ub=None, Din=24):
+    g = torch.Generator().manual_seed(seed)
+    torch.manual_seed(seed)
+    joiner = sc().RNNTPredictorJoiner(Din, 16, 64, V)
+    with torch.no_grad():
+        joiner.joiner.weight.mul_(3.0)   # sharper output than nn.Linear's init
+    enc_out = torch.randn(B, T, Din, generator=g)
+    labels = torch.randint(1, V, (B, Umax), generator=g)
+    fl = torch.tensor(Tb if Tb is not None else [T] * B)
+    ll = torch.tensor(Ub if Ub is not None else [Umax] * B)
+    return joiner, enc_out, labels, fl, ll
+
+
+def rel(a, b):
+    a = a.double().cpu()
+    b = b.double().cpu()
+    return float((a - b).norm() / max(b.norm(), 1e-30))
+
+
+@pytest.mark.parametrize("B,T,Umax,V,Tb,Ub", [(3, 37, 7, 64, [37, 20, 33], [7, 3, 0]),
+                                              (2, 64, 12, 96, None, [12, 5]),
+                                              (2, 5, 1, 32, [5, 1], [1, 1]),
+                                              (1, 70, 40, 128, None, None)])
+def test_fused_joint_vs_fp64(B, T, Umax, V, Tb, Ub):
+    joiner, enc_out, labels, fl, ll = case(B, T, Umax, V, B * 100 + T, Tb, Ub)
+    joiner = joiner.to(DEV)
+    prefix = torch.cat([torch.zeros(B, 1, dtype=torch.long), labels], 1).to(DEV)
+    enc_p, pred_p, W, bias = joiner(enc_out.to(DEV), prefix, project_only=True)
+    enc_p = enc_p.detach().requires_grad_(True)
+    pred_p = pred_p.detach().requires_grad_(True)
+    W = W.detach().requires_grad_(True)
+    bias = bias.detach().requires_grad_(True)
+    nll = sc().ops.RNNTJointFn.apply(enc_p, pred_p, W, bias, labels.to(DEV), fl.to(DEV), ll.to(DEV), 0)
+    nll.mean().backward()
+    rn, ge, gp, gw, gb = ref_fp64(enc_p.detach(), pred_p.detach(), W.detach(), bias.detach(), labels,
+                                  fl, ll, 0)
+    np.testing.assert_allclose(nll.detach().cpu().numpy(), rn, rtol=1e-4)
+    for got, ref, name in [(enc_p.grad, ge, "enc"), (pred_p.grad, gp, "pred"), (W.grad, gw, "W"),
+                           (bias.grad, gb, "bias")]:
+        assert torch.isfinite(got).all(), name
+        assert rel(got, ref) < 1e-2, (name, rel(got, ref))
+
+
+def test_fused_joint_zero_frames_is_inf():
+    joiner, enc_out, labels, fl, ll = case(2, 9, 3, 32, 5, [9, 0], [3, 2])
+    joiner = joiner.to(DEV)
+    prefix = torch.cat([torch.zeros(2, 1, dtype=torch.long), labels], 1).to(DEV)
+    enc_p, pred_p, W, bias = joiner(enc_out.to(DEV), prefix, project_only=True)
+    nll = sc().ops.RNNTJointFn.apply(enc_p, pred_p, W, bias, labels.to(DEV), fl.to(DEV), ll.to(DEV), 0)
+    v = nll.detach().cpu().numpy()
+    assert np.isfinite(v[0]) and np.isinf(v[1])
+
+
+def test_fused_joint_c5_size_vs_materialised_path():
+    """T=1500, U=150, V=1024 (C5 lattice), B=2: fused vs the unfused sc_rnnt_* kernels on
+    materialised fp32 logits built from the same bf16-rounded z and W."""
+    B, T, Umax, V = 2, 1500, 150, 1024
+    joiner, enc_out, labels, fl, ll = case(B, T, Umax, V, 77, Din=512)
+    joiner = joiner.to(DEV)
+    prefix = torch.cat([torch.zeros(B, 1, dtype=torch.long), labels], 1).to(DEV)
+    enc_p, pred_p, W, bias = (t.detach() for t in joiner(enc_out.to(DEV), prefix, project_only=True))
+    labels, fl, ll = labels.to(DEV), fl.to(DEV), ll.to(DEV)
+    outs = []
+    for _ in range(2):
+        e, p, w, b = (t.clone().requires_grad_(True) for t in (enc_p, pred_p, W, bias))
+        nll = sc().ops.RNNTJointFn.apply(e, p, w, b, labels, fl, ll, 0)
+        nll.mean().backward()
+        outs.append([nll.detach(), e.grad, p.grad, w.grad, b.grad])
+    for x, y in zip(*outs):
+        assert torch.equal(x, y)   # deterministic: fixed-order partial sums, no atomics
+    assert all(torch.isfinite(t).all() for t in outs[0])
+    # materialised path, same roundings
+    e, p, w, b = (t.clone().requires_grad_(True) for t in (enc_p, pred_p, W, bias))
+    z = torch.tanh(e.unsqueeze(2) + p.unsqueeze(1))
+    zq = z + (z.to(torch.bfloat16).float() - z).detach()
+    wq = w + (w.to(torch.bfloat16).float() - w).detach()
+    logits = zq @ wq.t() + b
+    nll_u = sc().rnnt_loss(logits, labels, fl, ll, reduction="none", is_logits=True)
+    nll_u.mean().backward()
+    np.testing.assert_allclose(outs[0][0].cpu().numpy(), nll_u.detach().cpu().numpy(), rtol=1e-3)
+    for got, ref, name in zip(outs[0][1:], [e.grad, p.grad, w.grad, b.grad], ["enc", "pred", "W", "bias"]):
+        r = rel(got, ref)
+        print(f"C5 lattice {name}: rel {r:.2e}")
+        assert r < 2e-2, (name, r)
+
+
+@pytest.mark.parametrize("compact", [False, True])
+def test_compute_loss_rnnt_uses_fused_path(compact):
+    """compute_loss(mode='rnnt') with statecatcher RNNTLoss: the fused path, equal to the
+    materialised joiner + criterion.forward_logits (the reference's data flow)."""
+    B, T, Umax, V = 2, 50, 6, 64
+    Cls = sc().RNNTCompactPredictorJoiner if compact else sc().RNNTPredictorJoiner
+    torch.manual_seed(3)
+    joiner = Cls(V, 16, 64, V).to(DEV)
+    enc = torch.randn(B, T, V, device=DEV)
+    tokens = torch.randint(1, V, (B, Umax), device=DEV)
+    in_lens, tgt_lens = [T, 41], [Umax, 4]
+    tokens[1, 4:] = 0
+
+    class Enc(torch.nn.Module):
+        def forward(self, feats, masks, states=None):
+            return feats, None
+    crit = sc().RNNTLoss(blank=0)
+    loss, _, _, _ = sc().compute_loss("rnnt", crit, Enc(), enc, None, tokens, in_lens, tgt_lens, 0,
+                                      use_rnnt_joiner=joiner, compact=compact)
+    loss.backward()
+    g_fused = [p.grad.clone() for p in joiner.parameters()]
+    joiner.zero_grad()
+    prefix = torch.cat([torch.zeros(B, 1, dtype=torch.long, device=DEV), tokens], 1)
+    if compact:
+        logits = joiner(enc, prefix, in_lens, tgt_lens)
+    else:
+        logits = joiner(enc, prefix)
+    ref = crit.forward_logits(logits, tokens, in_lens, tgt_lens, blank_id=0, compact=compact)
+    ref.backward()
+    np.testing.assert_allclose(loss.item(), ref.item(), rtol=2e-3)
+    for gf, p in zip(g_fused, joiner.parameters()):
+        assert rel(gf, p.grad) < 3e-2
