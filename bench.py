@@ -33,6 +33,9 @@ PEAK_BF16_TFLOPS = 2500.0  # dense bf16 MFMA spec
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--workload", choices=["ctc", "rnnt", "xlstm"], default="ctc",
+                    help="ctc: C2/C3 LucyRNN 6x512 + CTC (the BASELINE metric); rnnt: C5 LucyRNN "
+                         "6x512 + RNN-T (fused joiner, U=150); xlstm: C4 xLSTM 12 x 768 + CTC")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=32)
@@ -69,6 +72,8 @@ def synth_segments(args, rank, device):
     for _ in range(args.segments):
         feats = torch.randn(args.batch, args.seq, args.feat, generator=g)
         U = torch.randint(50, 151, (args.batch,), generator=gt)
+        if args.workload == "rnnt":   # U = 150 for C5
+            U = torch.full((args.batch,), 150, dtype=torch.int64)
         tok = torch.randint(1, args.vocab, (args.batch, 150), generator=gt)
         for b in range(args.batch):
             tok[b, U[b]:] = 0
@@ -80,9 +85,43 @@ def synth_segments(args, rank, device):
 
 
 def gemm_flops_per_frame(args):
+    if args.workload == "xlstm":
+        return None
     D, L = args.hidden, args.layers
     fwd = 2 * 7 * D * (args.feat + (L - 1) * D) + 2 * D * args.vocab
     return 3 * fwd   # fwd + dgrad + wgrad
+
+
+def build_workload(args, device):
+    """(model, criterion, optimizer params, trainer kwargs, config dict) per workload."""
+    from statecatcher_amd.model import (ASRModel, CTCLoss, RNNTLoss, RNNTPredictorJoiner,
+                                        build_lucyrnn_config, build_xlstm_config)
+    torch.manual_seed(0)   # identical init on every rank (DDP also broadcasts)
+    if args.workload == "xlstm":
+        # C4: xLSTM-large 12 blocks x 768 (4 heads: DQK 96, DV 192) behind the 80 -> 768 input
+        # projection, CTC; T padded to the 64-step chunk inside ASRModel (model.py:341-347)
+        cfg = build_xlstm_config(args.feat, args.vocab, num_heads=4, num_blocks=12, embedding_dim=768)
+        model = ASRModel(None, cfg, vocab_size=args.vocab, feat_dim=args.feat, proj_dim=-1).to(device)
+        conf = {"workload": "xLSTM 12x768 (mLSTM, 4 heads) + CTC training step, stateful "
+                            f"{args.segments}-segment carry", "blocks": 12, "embedding_dim": 768}
+        return model, CTCLoss(blank=0, zero_infinity=True), list(model.parameters()), \
+            dict(mode="ctc"), conf
+    cfg = build_lucyrnn_config(args.feat, args.hidden, args.layers, args.vocab)
+    model = ASRModel(None, cfg, vocab_size=args.vocab, feat_dim=args.feat, proj_dim=-1).to(device)
+    with torch.no_grad():   # reference zero-inits output_proj (lucyrnn_triton.py:108-109); a seeded
+        model.encoder.output_proj.weight.normal_(0, 0.02)   # N(0,0.02) keeps every gradient non-zero
+    conf = {"layers": args.layers, "hidden": args.hidden}
+    if args.workload == "rnnt":
+        # C5: RNNTPredictorJoiner(enc_out_dim=V, 64, 64, V) (train.py:368-375, :638-639), trained
+        # by the same optimizer; clip covers the model only (train.py:553)
+        joiner = RNNTPredictorJoiner(args.vocab, 64, 64, args.vocab).to(device)
+        conf["workload"] = (f"LucyRNN {args.layers}x{args.hidden} + RNN-T (fused joiner, J=64, "
+                            f"U=150) training step, stateful {args.segments}-segment carry")
+        return model, RNNTLoss(blank=0), list(model.parameters()) + list(joiner.parameters()), \
+            dict(mode="rnnt", joiner=joiner), conf
+    conf["workload"] = (f"LucyRNN {args.layers}x{args.hidden} + CTC training step, stateful "
+                        f"{args.segments}-segment carry")
+    return model, CTCLoss(blank=0, zero_infinity=True), list(model.parameters()), dict(mode="ctc"), conf
 
 
 def cpu_baseline(args):
@@ -240,26 +279,19 @@ def main():
         if os.path.exists(table):
             tun.read_file(table)
 
-    import statecatcher_amd as sc
     from statecatcher_amd import ops
-    from statecatcher_amd.model import ASRModel, CTCLoss, build_lucyrnn_config
     from statecatcher_amd.train import SegmentTrainer
 
-    torch.manual_seed(0)   # identical init on every rank (DDP also broadcasts)
-    cfg = build_lucyrnn_config(args.feat, args.hidden, args.layers, args.vocab)
-    model = ASRModel(None, cfg, vocab_size=args.vocab, feat_dim=args.feat, proj_dim=-1).to(device)
-    with torch.no_grad():   # reference zero-inits output_proj (lucyrnn_triton.py:108-109); a seeded
-        model.encoder.output_proj.weight.normal_(0, 0.02)   # N(0,0.02) keeps every gradient non-zero
-    params = [p for p in model.parameters() if p.requires_grad]
+    model, criterion, params, tkw, conf = build_workload(args, device)
+    params = [p for p in params if p.requires_grad]
     try:
         opt = torch.optim.Adam(params, lr=3e-4, fused=True)
     except Exception:
         opt = torch.optim.Adam(params, lr=3e-4, foreach=True)
     amp = torch.bfloat16 if args.dtype == "bf16" else None
     # the reference segment loop (train.py:460-581) with DDP over RCCL when world > 1
-    trainer = SegmentTrainer(model, CTCLoss(blank=0, zero_infinity=True), opt, mode="ctc",
-                             accumulation_steps=1, max_grad_norm=50.0, amp_dtype=amp,
-                             bucket_cap_mb=args.bucket_mb)
+    trainer = SegmentTrainer(model, criterion, opt, accumulation_steps=1, max_grad_norm=50.0,
+                             amp_dtype=amp, bucket_cap_mb=args.bucket_mb, **tkw)
     segs = synth_segments(args, rank, device)
 
     def step():
@@ -323,7 +355,7 @@ def main():
             kernels[name].update({"bytes_per_launch": nbytes,
                                   "achieved_GBs": round(nbytes / avg / 1e9, 1),
                                   "frac_of_peak": round(nbytes / avg / 1e9 / PEAK_HBM_GBS, 4)})
-    scans = [k for k in kernels if k.startswith("lucy_scan")]
+    scans = [k for k in kernels if k.startswith("lucy_scan") or k.startswith("mlstm")]
     dom = max(scans, key=lambda k: kstats[k][0]) if scans else None
     traffic = None
     pmc_file = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -340,27 +372,30 @@ def main():
     value = frames / dt
     ms = dt / args.steps * 1e3
     cpu = None
-    if rank == 0 and world == 1 and args.cpu_baseline == "on":
+    if rank == 0 and world == 1 and args.cpu_baseline == "on" and args.workload == "ctc":
         cpu = cpu_baseline(args)
     if rank == 0:
-        gemm_tflops = gemm_flops_per_frame(args) * args.batch * args.seq * world * args.steps / dt / 1e12
+        gf = gemm_flops_per_frame(args)
+        gemm_tflops = gf * args.batch * args.seq * world * args.steps / dt / 1e12 if gf else None
         line = {
-            "metric": "audio-frames/sec (LucyRNN+CTC, 80-d fbank, T=1500), whole job",
+            "metric": {"ctc": "audio-frames/sec (LucyRNN+CTC, 80-d fbank, T=1500), whole job",
+                       "rnnt": "audio-frames/sec (LucyRNN+RNN-T, 80-d fbank, T=1500, U=150), whole job",
+                       "xlstm": "audio-frames/sec (xLSTM+CTC, 80-d fbank, T=1500), whole job"}[args.workload],
             "value": round(value, 1), "unit": "audio-frames/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "bf16" if amp is not None else "fp32",
-            "data": "synthetic N(0,1) 80-d fbank, targets U~U[50,150] of V=1024, random-init weights",
-            "config": {"workload": "LucyRNN 6x512 + CTC training step, stateful 4-segment carry",
-                       "global_batch": args.batch * world, "seq_len": args.seq,
-                       "layers": args.layers, "hidden": args.hidden, "vocab": args.vocab,
-                       "parallelism": f"dp{world}"},
+            "data": "synthetic N(0,1) 80-d fbank, targets " +
+                    ("U=150" if args.workload == "rnnt" else "U~U[50,150]") +
+                    " of V=1024, random-init weights",
+            "config": {**conf, "global_batch": args.batch * world, "seq_len": args.seq,
+                       "vocab": args.vocab, "parallelism": f"dp{world}"},
             "per_gpu_frames_per_s": round(value / world, 1),
             "roofline": roofline,
             "kernels": kernels,
             "kernel_timing": f"HIP events on the launch stream, last {min(args.timing_steps, args.steps)} "
                              "timed steps",
-            "gemm_TFLOPs_effective": round(gemm_tflops / world, 1),
+            "gemm_TFLOPs_effective": round(gemm_tflops / world, 1) if gemm_tflops else None,
             "cpu_baseline": cpu,
             "loss_last": round(last_loss, 4),
         }

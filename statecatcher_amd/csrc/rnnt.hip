@@ -594,7 +594,6 @@ __device__ __forceinline__ void node_weights(const RnntArgs& a, int b, int t, in
   wy = 0.0f;
   const double lp2 = a.ws.logp2[b];
   const float sc = a.scale[b];
-  if (!(lp2 > -1e300) || sc == 0.0f) return;
   const int n = t + u;
   const int64_t base = (int64_t)b * a.ND * a.U1p;
   const int per = 2 * a.kh, nd = Tb + Ub;
@@ -613,8 +612,9 @@ __device__ __forceinline__ void node_weights(const RnntArgs& a, int b, int t, in
     const double be = (double)a.ws.beta[base + (int64_t)(n + 1) * a.U1p + u + 1] + oB;
     wy = exp2_((float)(al + ey + be - lp2));
   }
-  wb *= sc;
-  wy *= sc;
+  const bool live = lp2 > -1e300 && sc != 0.0f;   // infeasible sequence or no gradient: zero
+  wb = live ? wb * sc : 0.0f;
+  wy = live ? wy * sc : 0.0f;
 }
 
 // cooperative copy of W (bf16 [V][64]) and bias into the LDS images
@@ -687,7 +687,7 @@ __device__ __forceinline__ float half_sum(float x) {
   return x;
 }
 
-__global__ void __launch_bounds__(256) joint_fwd_kernel(JointArgs a) {
+__global__ void __launch_bounds__(512) joint_fwd_kernel(JointArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   load_w(a, lds);
   __syncthreads();
@@ -695,7 +695,7 @@ __global__ void __launch_bounds__(256) joint_fwd_kernel(JointArgs a) {
   const int lane = threadIdx.x & 63, h = lane >> 5;
   const int nup = (r.U1 + 1) / 2;
   const int64_t ntask = (int64_t)r.B * a.ntb * nup;
-  const int64_t wid = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6), nwv = (int64_t)gridDim.x * 4;
+  const int64_t wid = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 6), nwv = (int64_t)gridDim.x * 8;
   for (int64_t task = wid; task < ntask; task += nwv) {
     const int b = (int)(task / ((int64_t)a.ntb * nup));
     const int tb = (int)((task / nup) % a.ntb), up = (int)(task % nup);
@@ -766,131 +766,126 @@ __global__ void __launch_bounds__(256) joint_fwd_kernel(JointArgs a) {
   }
 }
 
-__global__ void __launch_bounds__(256) joint_dz_kernel(JointArgs a) {
+__global__ void __launch_bounds__(512) joint_dz_kernel(JointArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   load_w(a, lds);
+  // per-wave scratch: the column's blank / label weights, written lane-major, read per register
+  float* scr = (float*)(lds + kVmaxJ * 128 + kVmaxJ * 4) + (threadIdx.x >> 6) * 64;
   __syncthreads();
   const RnntArgs& r = a.r;
   const int lane = threadIdx.x & 63, h = lane >> 5, g1 = (lane >> 4) & 1;
+  const int jl = lane & 31;
   const int64_t ntask = (int64_t)r.B * a.ntb * a.nus;
-  const int64_t wid = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6), nwv = (int64_t)gridDim.x * 4;
-  const float* bias = (const float*)(lds + kVmaxJ * 128);
+  const int64_t wid = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 6), nwv = (int64_t)gridDim.x * 8;
   for (int64_t task = wid; task < ntask; task += nwv) {
     const int b = (int)(task / ((int64_t)a.ntb * a.nus));
     const int tb = (int)((task / a.nus) % a.ntb), us = (int)(task % a.nus);
     const int Tb = clampr(r.flen[b], 0, r.T), Ub = clampr(r.llen[b], 0, r.Umax);
-    const int t = tb * 32 + (lane & 31);
+    const int t = tb * 32 + jl;   // the lane's node in the logits (node-on-lane) orientation
     const bool tok = t < Tb;
     const int tc = tok ? t : max(Tb - 1, 0);
-    // this task's u range (pairs of columns)
     const int ua = (int)((int64_t)us * r.U1 / a.nus), ue = (int)((int64_t)(us + 1) * r.U1 / a.nus);
-    float de[32];
+    // d enc accumulated over this task's u in the dZ layout: [jb][q] = (node (q&3)+8(q>>2)+4h,
+    // j = jb*32 + (lane&31))
+    float de[2][16];
 #pragma unroll
-    for (int i = 0; i < 32; ++i) de[i] = 0.0f;
+    for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) de[jb][q] = 0.0f;
     const bool live = uniform(tb * 32) < Tb;
-    for (int u0 = ua; live && u0 < ue && u0 <= Ub; u0 += 2) {
-      const int nc = (u0 + 1 < ue && u0 + 1 <= Ub) ? 2 : 1;
-      jbf8 zb[2][4];
-      float lse2[2], an[2], wbn[2], wyn[2];
-      jf16 Y[2][2];
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        if (c >= nc) break;
-        const int u = u0 + c;
-        z_frags(a, b, tc, u, tok, h, zb[c]);
-        float wb = 0.0f, wy = 0.0f;
-        if (tok) node_weights(r, b, t, u, Tb, Ub, wb, wy);
-        wbn[c] = wb;
-        wyn[c] = wy;
-        an[c] = wb + wy;
-        lse2[c] = tok ? r.ws.lse[((int64_t)b * r.T + t) * r.U1 + u] * kLog2e : 1e30f;
-#pragma unroll
-        for (int jb = 0; jb < 2; ++jb)
-#pragma unroll
-          for (int q = 0; q < 16; ++q) Y[c][jb][q] = 0.0f;
+    for (int u = ua; live && u < ue && u <= Ub; ++u) {
+      jbf8 zb[4];
+      z_frags(a, b, tc, u, tok, h, zb);
+      float wb = 0.0f, wy = 0.0f;
+      if (tok) node_weights(r, b, t, u, Tb, Ub, wb, wy);
+      const float an = wb + wy;
+      const float lse2 = tok ? r.ws.lse[((int64_t)b * r.T + t) * r.U1 + u] * kLog2e : 1e30f;
+      if (h == 0) {
+        scr[jl] = wb;
+        scr[32 + jl] = wy;
       }
-      for (int v0 = 0; v0 < r.V; v0 += 32) {
-        // W^T fragments for dZ^T = W^T dlogits: k-step s covers rows v0 + 16 s + 8 (e>>2) + 4 h + (e&3)
-        jbf8 wt[2][2];
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-          for (int jb = 0; jb < 2; ++jb)
-            wt[s2][jb] = cat8(tr_rd(lds, v0 + 16 * s2 + 4 * h, jb * 32 + 16 * g1, lane),
-                              tr_rd(lds, v0 + 16 * s2 + 8 + 4 * h, jb * 32 + 16 * g1, lane));
-#pragma unroll
-        for (int c = 0; c < 2; ++c) {
-          if (c >= nc) break;
-          const jf16 x = logits_vblock(lds, v0, lane, zb[c]);
-          float p[16];
-#pragma unroll
-          for (int q = 0; q < 16; ++q) p[q] = an[c] * exp2_(fmaf(x[q], kLog2e, -lse2[c]));
-#pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2) {
-            const jbf8 xf = pack8(p + 8 * s2);
-#pragma unroll
-            for (int jb = 0; jb < 2; ++jb) Y[c][jb] = mfma32(wt[s2][jb], xf, Y[c][jb]);
-          }
-        }
-      }
-      // Y[c][jb][q] = dZ_dense[node][j], j = jb*32 + (q&3) + 8(q>>2) + 4h
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        if (c >= nc) break;
-        const int u = u0 + c;
-        const int yl = u < Ub ? label_at(r, b, u) : r.blank;
-        const float* ep = r.T ? a.enc + ((int64_t)b * r.T + tc) * kJ : a.enc;
-        const float* pp = a.pred + ((int64_t)b * r.U1 + u) * kJ;
-        float dp[32], gbz[32], gyz[32];
-#pragma unroll
-        for (int jb = 0; jb < 2; ++jb)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const int j0 = jb * 32 + 8 * q + 4 * h;
-            const float4 ev = *(const float4*)(ep + j0);
-            const float4 pv = *(const float4*)(pp + j0);
-            const js4 wbv = *(const js4*)(lds + wimg(r.blank, j0 >> 3) + 8 * h);
-            const js4 wyv = *(const js4*)(lds + wimg(yl, j0 >> 3) + 8 * h);
-            const float xs[4] = {ev.x + pv.x, ev.y + pv.y, ev.z + pv.z, ev.w + pv.w};
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const int i = jb * 16 + 4 * q + e;
-              const float z = tok ? tanh_(xs[e]) : 0.0f;
-              const float wbj = __uint_as_float((uint32_t)(uint16_t)wbv[e] << 16);
-              const float wyj = __uint_as_float((uint32_t)(uint16_t)wyv[e] << 16);
-              const float dz = Y[c][jb][4 * q + e] - wbn[c] * wbj - wyn[c] * wyj;
-              dp[i] = dz * (1.0f - z * z);
-              de[i] += dp[i];
-              gbz[i] = wbn[c] * z;
-              gyz[i] = wyn[c] * z;
-            }
-          }
-        half_reduce32(dp, lane);
-        half_reduce32(gbz, lane);
-        half_reduce32(gyz, lane);
-        const int i = lane & 31;
-        const int j = (i >> 4) * 32 + (i & 3) + 8 * ((i & 15) >> 2) + 4 * h;
-        const int64_t row = (((int64_t)b * a.ntb + tb) * r.U1 + u) * kJ + j;
-        a.d_pred[row] = dp[0];
-        a.g_blank[row] = gbz[0];
-        a.g_label[row] = gyz[0];
-        const float sb = half_sum(wbn[c]), sy = half_sum(wyn[c]);
-        if (lane == 0) {
-          const int64_t srow = (((int64_t)b * a.ntb + tb) * r.U1 + u) * 2;
-          a.s_bl[srow] = sb;
-          a.s_bl[srow + 1] = sy;
-        }
-      }
-    }
-    if (t < r.T) {
-      float* dst = a.d_enc + (((int64_t)us * r.B + b) * r.T + t) * kJ;
+      jf16 Y[2];
 #pragma unroll
       for (int jb = 0; jb < 2; ++jb)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int i = jb * 16 + 4 * q;
-          *(float4*)(dst + jb * 32 + 8 * q + 4 * h) = make_float4(de[i], de[i + 1], de[i + 2], de[i + 3]);
+        for (int q = 0; q < 16; ++q) Y[jb][q] = 0.0f;
+      for (int v0 = 0; v0 < r.V; v0 += 32) {
+        const jf16 x = logits_vblock(lds, v0, lane, zb);
+        float p[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) p[q] = an * exp2_(fmaf(x[q], kLog2e, -lse2));
+        // dZ[node][j] += sum_v dlogits[v][node] W[v][j]: the accumulator's rows (v) are the sum,
+        // so x is the A operand as is; W[v][j] with j on the lane comes from tr reads
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const jbf8 xf = pack8(p + 8 * s2);
+#pragma unroll
+          for (int jb = 0; jb < 2; ++jb) {
+            const jbf8 wt = cat8(tr_rd(lds, v0 + 16 * s2 + 4 * h, jb * 32 + 16 * g1, lane),
+                                 tr_rd(lds, v0 + 16 * s2 + 8 + 4 * h, jb * 32 + 16 * g1, lane));
+            Y[jb] = mfma32(xf, wt, Y[jb]);
+          }
         }
+      }
+      // Y[jb][q] = dZ_dense[node n_q][j]; per-register node weights back from the scratch
+      float wbr[16], wyr[16];
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4) {
+        const float4 bv = *(const float4*)(scr + 8 * q4 + 4 * h);
+        const float4 yv = *(const float4*)(scr + 32 + 8 * q4 + 4 * h);
+        wbr[4 * q4] = bv.x; wbr[4 * q4 + 1] = bv.y; wbr[4 * q4 + 2] = bv.z; wbr[4 * q4 + 3] = bv.w;
+        wyr[4 * q4] = yv.x; wyr[4 * q4 + 1] = yv.y; wyr[4 * q4 + 2] = yv.z; wyr[4 * q4 + 3] = yv.w;
+      }
+      const int yl = u < Ub ? label_at(r, b, u) : r.blank;
+      const float* pp = a.pred + ((int64_t)b * r.U1 + u) * kJ;
+      const float* eb = a.enc + (int64_t)b * r.T * kJ;
+      const float* bias = (const float*)(lds + kVmaxJ * 128);
+      (void)bias;
+#pragma unroll
+      for (int jb = 0; jb < 2; ++jb) {
+        const int j = jb * 32 + jl;
+        const float pj = pp[j];
+        const float wbj = (float)*(const __bf16*)(lds + wimg(r.blank, j >> 3) + 2 * (j & 7));
+        const float wyj = (float)*(const __bf16*)(lds + wimg(yl, j >> 3) + 2 * (j & 7));
+        float sp = 0.0f, sgb = 0.0f, sgy = 0.0f;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int n = (q & 3) + 8 * (q >> 2) + 4 * h;
+          const int tq = tb * 32 + n;
+          const bool ok = tq < Tb;
+          const float z = ok ? tanh_(eb[(int64_t)min(tq, r.T - 1) * kJ + j] + pj) : 0.0f;
+          const float dz = Y[jb][q] - wbr[q] * wbj - wyr[q] * wyj;
+          const float dp = ok ? dz * (1.0f - z * z) : 0.0f;
+          de[jb][q] += dp;
+          sp += dp;
+          sgb = fmaf(wbr[q], z, sgb);
+          sgy = fmaf(wyr[q], z, sgy);
+        }
+        sp += __shfl_xor(sp, 32);
+        sgb += __shfl_xor(sgb, 32);
+        sgy += __shfl_xor(sgy, 32);
+        if (h == 0) {
+          const int64_t row = (((int64_t)b * a.ntb + tb) * r.U1 + u) * kJ + j;
+          a.d_pred[row] = sp;
+          a.g_blank[row] = sgb;
+          a.g_label[row] = sgy;
+        }
+      }
+      const float sb = half_sum(wb), sy = half_sum(wy);
+      if (lane == 0) {
+        const int64_t srow = (((int64_t)b * a.ntb + tb) * r.U1 + u) * 2;
+        a.s_bl[srow] = sb;
+        a.s_bl[srow + 1] = sy;
+      }
+    }
+    float* dst = a.d_enc + ((int64_t)us * r.B + b) * r.T * kJ;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int tq = tb * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
+      if (tq < r.T) {
+#pragma unroll
+        for (int jb = 0; jb < 2; ++jb) dst[(int64_t)tq * kJ + jb * 32 + jl] = de[jb][q];
+      }
     }
   }
 }
@@ -898,9 +893,9 @@ __global__ void __launch_bounds__(256) joint_dz_kernel(JointArgs a) {
 __global__ void __launch_bounds__(512) joint_dw_kernel(JointArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   load_w(a, lds);
-  unsigned char* zimg = lds + kVmaxJ * 128 + kVmaxJ * 4;   // [32 nodes][64] bf16, swizzled rows
-  float* s_lse2 = (float*)(zimg + 32 * 128);
-  float* s_a = s_lse2 + 32;
+  // two column buffers: [32 nodes][64] bf16 z image + node scalars (lse2, a)
+  unsigned char* zimg0 = lds + kVmaxJ * 128 + kVmaxJ * 4;
+  float* scal0 = (float*)(zimg0 + 2 * 32 * 128);
   const RnntArgs& r = a.r;
   const int lane = threadIdx.x & 63, h = lane >> 5, g1 = (lane >> 4) & 1;
   const int w = threadIdx.x >> 6;
@@ -919,35 +914,59 @@ __global__ void __launch_bounds__(512) joint_dw_kernel(JointArgs a) {
   }
   const int64_t ncol = (int64_t)r.B * a.ntb * r.U1;
   const int64_t c0 = (int64_t)blockIdx.x * ncol / gridDim.x, c1 = (int64_t)(blockIdx.x + 1) * ncol / gridDim.x;
-  for (int64_t col = c0; col < c1; ++col) {
+  auto valid_col = [&](int64_t col) {
+    const int b = (int)(col / ((int64_t)a.ntb * r.U1));
+    const int tb = (int)((col / r.U1) % a.ntb), u = (int)(col % r.U1);
+    return tb * 32 < clampr(r.flen[b], 0, r.T) && u <= clampr(r.llen[b], 0, r.Umax);
+  };
+  auto next_col = [&](int64_t col) {
+    while (col < c1 && !valid_col(col)) ++col;
+    return col;
+  };
+  // the column's inputs, loaded one column ahead: this thread's z element group and, for
+  // threads < 32, its node's scalars
+  const int zn = threadIdx.x >> 4, jq = threadIdx.x & 15;
+  float4 pe = make_float4(0, 0, 0, 0), pq = pe;
+  float pa = 0.0f, pl = 1e30f;
+  bool pok = false;
+  auto prefetch = [&](int64_t col) {
     const int b = (int)(col / ((int64_t)a.ntb * r.U1));
     const int tb = (int)((col / r.U1) % a.ntb), u = (int)(col % r.U1);
     const int Tb = clampr(r.flen[b], 0, r.T), Ub = clampr(r.llen[b], 0, r.Umax);
-    if (tb * 32 >= Tb || u > Ub) continue;   // uniform over the workgroup
-    __syncthreads();   // the previous column's readers are done with zimg / scalars
-    {
-      const int n = threadIdx.x >> 4, jq = threadIdx.x & 15;   // node, 4-j group
-      const int t = tb * 32 + n;
-      const bool ok = t < Tb;
-      const int tc = ok ? t : Tb - 1;
-      const float4 ev = *(const float4*)(a.enc + ((int64_t)b * r.T + tc) * kJ + 4 * jq);
-      const float4 pv = *(const float4*)(a.pred + ((int64_t)b * r.U1 + u) * kJ + 4 * jq);
+    const int t = tb * 32 + zn;
+    pok = t < Tb;
+    pe = *(const float4*)(a.enc + ((int64_t)b * r.T + (pok ? t : Tb - 1)) * kJ + 4 * jq);
+    pq = *(const float4*)(a.pred + ((int64_t)b * r.U1 + u) * kJ + 4 * jq);
+    if (threadIdx.x < 32) {
+      const int tn = tb * 32 + threadIdx.x;
+      const bool okn = tn < Tb;
+      float wb = 0.0f, wy = 0.0f;
+      if (okn) node_weights(r, b, tn, u, Tb, Ub, wb, wy);
+      pa = wb + wy;
+      pl = okn ? r.ws.lse[((int64_t)b * r.T + tn) * r.U1 + u] * kLog2e : 1e30f;
+    }
+  };
+  int64_t col = next_col(c0);
+  if (col < c1) prefetch(col);
+  for (int it = 0; col < c1; ++it) {
+    unsigned char* zimg = zimg0 + (it & 1) * 32 * 128;
+    float* s_lse2 = scal0 + (it & 1) * 64;
+    float* s_a = s_lse2 + 32;
+    {   // stage the prefetched column into this iteration's buffer
       js4 zz;
-      const float xs[4] = {ev.x + pv.x, ev.y + pv.y, ev.z + pv.z, ev.w + pv.w};
+      const float xs[4] = {pe.x + pq.x, pe.y + pq.y, pe.z + pq.z, pe.w + pq.w};
 #pragma unroll
       for (int e = 0; e < 4; ++e)
-        zz[e] = __builtin_bit_cast(short, (__bf16)(ok ? tanh_(xs[e]) : 0.0f));
-      *(js4*)(zimg + wimg(n, jq >> 1) + 8 * (jq & 1)) = zz;
-      if (threadIdx.x < 32) {   // node scalars, one thread per node
-        const int tn = tb * 32 + threadIdx.x;
-        const bool okn = tn < Tb;
-        float wb = 0.0f, wy = 0.0f;
-        if (okn) node_weights(r, b, tn, u, Tb, Ub, wb, wy);
-        s_a[threadIdx.x] = wb + wy;
-        s_lse2[threadIdx.x] = okn ? r.ws.lse[((int64_t)b * r.T + tn) * r.U1 + u] * kLog2e : 1e30f;
+        zz[e] = __builtin_bit_cast(short, (__bf16)(pok ? tanh_(xs[e]) : 0.0f));
+      *(js4*)(zimg + wimg(zn, jq >> 1) + 8 * (jq & 1)) = zz;
+      if (threadIdx.x < 32) {
+        s_a[threadIdx.x] = pa;
+        s_lse2[threadIdx.x] = pl;
       }
     }
-    __syncthreads();
+    __syncthreads();   // buffer it&1 complete; every wave is past its reads of column it-2
+    const int64_t nxt = next_col(col + 1);
+    if (nxt < c1) prefetch(nxt);   // in flight during this column's MFMAs
     // node scalars of this lane's 16 accumulator rows: node = (q&3) + 8(q>>2) + 4h
     float l2[16], an[16];
 #pragma unroll
@@ -990,6 +1009,7 @@ __global__ void __launch_bounds__(512) joint_dw_kernel(JointArgs a) {
         }
       }
     }
+    col = nxt;
   }
   // acc[k][jb][q] = dW[v = vb*32 + (q&3) + 8(q>>2) + 4h][j = jb*32 + (lane&31)]
   float* dw = a.dW + (int64_t)blockIdx.x * r.V * kJ;
@@ -1016,7 +1036,8 @@ bool joint_lds_attr(K kern, size_t bytes) {
   return hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                              (int)bytes) == hipSuccess;
 }
-size_t joint_lds_dw() { return joint_lds_fwd() + 32 * 128 + 2 * 32 * 4; }
+size_t joint_lds_dz() { return joint_lds_fwd() + 8 * 64 * 4; }
+size_t joint_lds_dw() { return joint_lds_fwd() + 2 * (32 * 128 + 2 * 32 * 4); }
 
 void joint_geometry(int B, int T, int Umax, int* ntb, int* nus, int* S) {
   *ntb = (T + 31) / 32;
@@ -1024,7 +1045,7 @@ void joint_geometry(int B, int T, int Umax, int* ntb, int* nus, int* S) {
   // about three (b, t-block) tasks
   const int64_t base = (int64_t)B * *ntb;
   int n = 1;
-  while (n < 8 && base * n < 3 * 1024 && n < Umax + 1) n *= 2;
+  while (n < 8 && base * n < 3 * 2048 && n < Umax + 1) n *= 2;
   *nus = n;
   *S = 256;
 }
@@ -1165,7 +1186,7 @@ extern "C" int sc_rnnt_joint_fwd(const float* enc, const float* pred, const void
   static const bool ok = joint_lds_attr(joint_fwd_kernel, joint_lds_fwd());
   SC_REQUIRE(ok, "sc_rnnt_joint_fwd: LDS attribute");
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(joint_fwd_kernel, dim3(256), dim3(256), joint_lds_fwd(), st, j);
+  hipLaunchKernelGGL(joint_fwd_kernel, dim3(256), dim3(512), joint_lds_fwd(), st, j);
   launch_ab(j.r, st);
   return launch_status("sc_rnnt_joint_fwd");
 }
@@ -1193,11 +1214,11 @@ extern "C" int sc_rnnt_joint_bwd(const float* enc, const float* pred, const void
   j.s_bl = s_bl;
   j.dW = dW;
   j.db = db;
-  static const bool ok1 = joint_lds_attr(joint_dz_kernel, joint_lds_fwd());
+  static const bool ok1 = joint_lds_attr(joint_dz_kernel, joint_lds_dz());
   static const bool ok2 = joint_lds_attr(joint_dw_kernel, joint_lds_dw());
   SC_REQUIRE(ok1 && ok2, "sc_rnnt_joint_bwd: LDS attribute");
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(joint_dz_kernel, dim3(256), dim3(256), joint_lds_fwd(), st, j);
+  hipLaunchKernelGGL(joint_dz_kernel, dim3(256), dim3(512), joint_lds_dz(), st, j);
   hipLaunchKernelGGL(joint_dw_kernel, dim3(j.S), dim3(512), joint_lds_dw(), st, j);
   return launch_status("sc_rnnt_joint_bwd");
 }

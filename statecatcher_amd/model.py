@@ -14,7 +14,7 @@ import torch.nn as nn
 from .lucyrnn_conf import LucyRNNConfig
 from .lucyrnn_triton import LucyRNNtriton
 from .xlstm import xLSTMLarge, xLSTMLargeConfig
-from .ops import ctc_loss, rnnt_joint_loss, rnnt_loss
+from .ops import ctc_loss, rnnt_joint_loss, rnnt_joint_supported, rnnt_loss
 
 
 def detach_states(states):
@@ -93,7 +93,9 @@ def compute_loss(mode: str, criterion: nn.Module, model: nn.Module, feats: torch
                                   device=tokens.device)
         predictor_input = torch.cat([blank_prefix, tokens], dim=1)
         use_compact = bool(getattr(args, "compact_rnnt", False)) if args is not None else compact
-        if isinstance(criterion, RNNTLoss) and enc_out.is_cuda:
+        jm = getattr(use_rnnt_joiner, "module", use_rnnt_joiner)   # DDP-wrapped or not
+        if isinstance(criterion, RNNTLoss) and enc_out.is_cuda and \
+                rnnt_joint_supported(jm.joiner.in_features, jm.joiner.out_features):
             # fused joiner + log_softmax + lattice (rnnt.hip joint_*): the (B, T, U+1, V) logits
             # are never materialised; same value as the compact and dense paths below
             enc_p, pred_p, W, bias = (use_rnnt_joiner(enc_out, predictor_input, in_lens, tgt_lens,

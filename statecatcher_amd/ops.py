@@ -770,6 +770,12 @@ def _addr(c):
     return ctypes.addressof(c)
 
 
+def rnnt_joint_supported(join_dim, vocab):
+    """Shapes the fused joiner kernels are compiled for (J = 64, V % 32 == 0, V <= 1024); other
+    joiners take the materialised HIP path (logits -> sc_rnnt_*)."""
+    return join_dim == 64 and vocab % 32 == 0 and 0 < vocab <= 1024
+
+
 def rnnt_joint_loss(enc_p, pred_p, W, bias, labels, frames_lengths, labels_lengths, blank=0,
                     reduction="mean", average_frames=False):
     """warp_rnnt's reductions over the fused joiner + lattice (RNNTJointFn)."""
@@ -821,7 +827,9 @@ class MLSTMFn(torch.autograd.Function):
         ms = torch.empty(BH, nc + 1, dtype=torch.float32, device=dev)
         mrow = torch.empty(BH, T, dtype=torch.float32, device=dev)
         den = torch.empty(BH, T, dtype=torch.float32, device=dev)
-        with _timed("mlstm_fwd", qc, 0):
+        st_b = BH * (nc + 1) * (DQ * DV + DQ + 1) * 4
+        fwd_b = BH * T * ((2 * DQ + 2 * DV) * qc.element_size() + 4 * 4) + st_b   # q k v h, 4 rows
+        with _timed("mlstm_fwd", qc, fwd_b):
             rc = lib.sc_mlstm_fwd(ptr(qc), ptr(kc), ptr(vc), dtype_code(qc), ptr(ig), ptr(fg), ptr(c0c),
                                   ptr(n0c), ptr(m0c), BH, T, DQ, DV, float(eps), ptr(h), ptr(Cs),
                                   ptr(ns), ptr(ms), ptr(mrow), ptr(den), stream_of(qc))
@@ -851,7 +859,10 @@ class MLSTMFn(torch.autograd.Function):
         dv = torch.empty_like(vc)
         qdq = torch.empty(BH, T, dtype=torch.float32, device=dev)
         kdk = torch.empty(BH, T, dtype=torch.float32, device=dev)
-        with _timed("mlstm_bwd", qc, 0):
+        st_b = BH * (nc + 1) * (DQ * DV + DQ + 1) * 4
+        # reads q k v h dh + 4 fp32 rows + states; writes dq dk dv + 2 rows + state gradients
+        bwd_b = BH * T * ((4 * DQ + 4 * DV) * qc.element_size() + 6 * 4) + 2 * st_b
+        with _timed("mlstm_bwd", qc, bwd_b):
             rc = _lib.load().sc_mlstm_bwd(
                 ptr(qc), ptr(kc), ptr(vc), dtype_code(qc), ptr(ig), ptr(fg), ptr(h), ptr(dhc),
                 ptr(dcTc), ptr(dnTc), ptr(Cs), ptr(ns), ptr(ms), ptr(mrow), ptr(den), BH, T, DQ, DV,
