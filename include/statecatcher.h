@@ -280,6 +280,18 @@ int sc_gemm_wgrad_splits(int L, int I, int J);
 int sc_gemm_wgrad_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, float* part, int L,
                        int I, int J, int S, void* stream);
 
+/*
+ * Frame-major projection GEMM C = A B^T, bf16 in / fp32 accumulate / bf16 out, for A [M][lda]
+ * and B [N][ldb] both K-contiguous, C [M][ldc].  Replaces the library GEMMs of LinearSafe's
+ * forward (lucyrnn_triton.py:20-25, gates = x W^T; layer 0's Din = 80 zero-padded to 128) and of
+ * the input gradients (dx = dgates W as dgates (W^T)^T; output_proj's dh = dlogits Wo,
+ * lucyrnn_triton.py:107-109).  Needs K % 64 == 0, N % 256 == 0, 16-byte aligned operands and
+ * leading dimensions, every operand < 4 GiB.  tile_m: rows per tile, 0 (default 192), 128 or 192.
+ * Deterministic (no atomics, fixed K order).  Returns 0, SC_EINVAL, or a HIP error code.
+ */
+int sc_gemm_tn_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc,
+                    int M, int N, int K, int tile_m, void* stream);
+
 /* ---------------------------------------------------------------- feature frontend ------ */
 
 /* Frames of a row of n_samples (center=False): 1 + (n - 400) / 160, or 0 below 400 samples. */

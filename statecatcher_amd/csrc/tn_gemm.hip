@@ -1,0 +1,303 @@
+// Frame-major projection GEMMs of the LucyRNN training step on gfx950 MFMA (CDNA4, wave64).
+//
+//   C[M][N] = A[M][K] · B[N][K]ᵀ     bf16 in, fp32 accumulate, bf16 out
+//
+// with both operands K-contiguous.  The step's forward and input-gradient projections are all
+// this shape (M = B*T = 48,000 frames at C2):
+//   * gate forward, LinearSafe (lucyrnn_triton.py:20-25):  x [M][Din] · W [7D][Din]ᵀ, Din = 512,
+//     and layer 0 with Din = 80 padded to 128 (the caller's bf16 cast writes the zero columns);
+//   * gate input gradient:  dgates [M][7D] · (Wᵀ) [D][7D]ᵀ  (a 3.7 MB transposed weight copy);
+//   * output-projection input gradient (lucyrnn_triton.py:107-109): dlogits [M][V] · (Woᵀ)[D][V]ᵀ.
+//
+// Design (one 512-thread workgroup per CU, persistent over its tiles):
+//   * output tile TM x 256 (TM = 32 MF: 192 by default (256 would spill), so 48,000 rows are 250 whole panels and
+//     the 3584-column forward is 3,500 tiles = 13.7 per CU; the 512-column gradients 500 tiles);
+//     8 waves as 2 (rows) x 4 (columns), per wave 16 MF x 64 outputs;
+//   * the MFMA A operand is the B matrix: a lane's accumulators then hold 4 consecutive output
+//     columns, and the B rows of each 16-row fragment are drawn so that a lane ends the tile with
+//     16 consecutive columns of one row: two 16-byte stores per row fragment;
+//   * K in half-stages of 32 columns (one v_mfma_f32_16x16x32_bf16 k-step).  A ring of four LDS
+//     slots ([TM + 256 rows][64 B], 28 KiB at TM = 192) is filled by LDS-DMA (16-byte pieces,
+//     saddr form), three half-stages in flight;
+//   * the ring runs CONTINUOUSLY over the workgroup's tiles: the DMA of the next tile's first
+//     half-stages is issued while the current tile finishes, so no tile restarts the pipeline;
+//   * the 16-byte chunk index of LDS row r is XOR-swizzled by F[((r >> 2) ^ (r >> 4)) & 3],
+//     F = {0, 2, 3, 1}, applied on the DMA SOURCE address (the LDS side of a DMA is lane-linear);
+//     with ds_read_b128's lane groups ({0-3,12-15,20-27}, {4-11,16-19,28-31}, ...) every
+//     fragment read of both operands is conflict-free;
+//   * epilogue: the finished tile is packed to bf16 in registers and its stores are spread over
+//     the next tile's half-stages (buffer stores: rows >= M fall outside the descriptor's range
+//     and are dropped), so the output stream overlaps the MFMAs instead of stalling them;
+//   * waits are counted: vmcnt counts LDS-DMA pieces and stores together in issue order
+//     (MI355X_MICROARCH.md), and each half-stage waits for exactly the vector-memory operations
+//     issued up to its own last DMA piece.
+// XCD-aware: consecutive tiles (the 14 column tiles of one 192-row panel, or the two of a
+// gradient panel) are taken by co-resident workgroups of one XCD, so the A panel is fetched from
+// HBM once per XCD and shared through its L2.
+
+#include "sc_common.h"
+
+namespace sc {
+namespace {
+
+typedef __bf16 b8v __attribute__((ext_vector_type(8)));
+typedef __bf16 b2v __attribute__((ext_vector_type(2)));
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef int i4v __attribute__((ext_vector_type(4)));
+
+// SC_TN_ABL (tools timing only, never in a shipped build): 1 no MFMAs, 2 no DMA after the
+// prologue (wrong results)
+#ifndef SC_TN_ABL
+#define SC_TN_ABL 0
+#endif
+
+constexpr int kBK = 64;      // K columns per stage (two v_mfma_f32_16x16x32_bf16 k-steps)
+constexpr int kRowB = 128;   // LDS image row pitch (bytes): whole 128-byte lines per DMA row
+constexpr int kTN = 256;     // output columns per tile
+constexpr int kSlots = 2;    // LDS stages
+
+struct TnArgs {
+  const __bf16* A;
+  const __bf16* B;
+  __bf16* C;
+  int M, N, K, ntn, tiles;
+  uint32_t lda, ldb, ldc;   // elements
+  uint32_t cbytes;          // addressable bytes of C (M * ldc * 2)
+};
+
+// physical-chunk XOR of image row r (8 chunks of 16 B per 128-byte row)
+__device__ __forceinline__ int swz(int r) { return (r ^ (r >> 2) ^ (r >> 4)) & 7; }
+
+__device__ __forceinline__ i4v lds_read16(uint32_t byte) {
+  return *(const __attribute__((address_space(3))) i4v*)(size_t)byte;
+}
+
+template <int MF, int SPI>
+__global__ void __launch_bounds__(512) tn_kernel(TnArgs a) {
+  constexpr int TM = 32 * MF;
+  constexpr int NP = (TM + kTN) / 8;           // 1-KiB DMA pieces (8 rows of 128 B) per stage
+  constexpr int NPW = NP / 8;                  // per wave
+  static_assert(NP % 8 == 0, "pieces must split evenly over the 8 waves");
+  constexpr int kSlotB = (TM + kTN) * kRowB;   // bytes per LDS stage
+  constexpr int NST = 2 * MF;                  // 16-byte stores per wave per tile
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const int lane = threadIdx.x & 63;
+  const int w = uniform(threadIdx.x >> 6);
+  const int wm = w >> 2, wn = w & 3;
+  const int fr = lane & 15, fq = lane >> 4;
+
+  // XCD-aware logical id (bids go round-robin over the 8 XCDs): consecutive lids share an XCD
+  const int G = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid % 8, qq = G / 8, rr = G % 8;
+  const int lid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + bid / 8;
+  const int nks = a.K / kBK;
+  const int ntw = lid < a.tiles ? (a.tiles - lid + G - 1) / G : 0;
+  const int NH = ntw * nks;
+  const uint32_t lds0 = lds_addr(lds);
+
+  // ---- DMA geometry: piece g = NPW w + q covers image rows 8g .. 8g+7 of [A; B] ----
+  int prow[NPW];        // row within its image (A: 0..TM-1, B: 0..255)
+  uint32_t pcol[NPW];   // logical element column within the stage (8 c)
+#pragma unroll
+  for (int q = 0; q < NPW; ++q) {
+    const int R = 8 * (NPW * w + q) + (lane >> 3);
+    prow[q] = R < TM ? R : R - TM;
+    pcol[q] = 8u * (uint32_t)((lane & 7) ^ swz(prow[q]));
+  }
+  int st_h = 0, st_ks = 0, st_tile = lid;
+  int st_m0 = (st_tile / a.ntn) * TM, st_n0 = (st_tile % a.ntn) * kTN;
+  auto stage = [&]() __attribute__((always_inline)) {
+    const uint32_t sb = lds0 + (st_h % kSlots) * kSlotB;
+    const uint32_t k0 = (uint32_t)st_ks * kBK;
+#pragma unroll
+    for (int q = 0; q < NPW; ++q) {
+      const int g = NPW * w + q;
+      if (8 * g < TM) {
+        const uint32_t row = (uint32_t)min(st_m0 + prow[q], a.M - 1);
+        dma_to_lds_s<16>(a.A, (row * a.lda + k0 + pcol[q]) * 2u, sb + g * 1024);
+      } else {
+        const uint32_t row = (uint32_t)(st_n0 + prow[q]);
+        dma_to_lds_s<16>(a.B, (row * a.ldb + k0 + pcol[q]) * 2u, sb + g * 1024);
+      }
+    }
+    ++st_h;
+    if (++st_ks == nks) {
+      st_ks = 0;
+      st_tile += G;
+      st_m0 = (st_tile / a.ntn) * TM;
+      st_n0 = (st_tile % a.ntn) * kTN;
+    }
+  };
+
+  // ---- fragment geometry (byte offsets within a stage; k-step kk flips address bit 6) ----
+  // MFMA A operand = B rows: fragment nf, lane row fr -> image row wn*64 + (fr>>2)*16 + nf*4 +
+  // (fr&3), so the lane's accumulators over nf hold output columns wn*64 + fq*16 + 0..15.
+  uint32_t offB[4];
+#pragma unroll
+  for (int nf = 0; nf < 4; ++nf) {
+    const int r = wn * 64 + (fr >> 2) * 16 + nf * 4 + (fr & 3);
+    offB[nf] = (uint32_t)(TM * kRowB + r * kRowB + 16 * (fq ^ swz(r)));
+  }
+  // MFMA B operand = A rows wm*TM/2 + mf*16 + fr
+  uint32_t offA[MF];
+#pragma unroll
+  for (int mf = 0; mf < MF; ++mf) {
+    const int r = wm * (TM / 2) + mf * 16 + fr;
+    offA[mf] = (uint32_t)(r * kRowB + 16 * (fq ^ swz(r)));
+  }
+  auto load_frags = [&](uint32_t sb, int kk, i4v (&bf)[4], i4v (&af)[MF]) __attribute__((always_inline)) {
+    const uint32_t x = 64u * kk;
+#pragma unroll
+    for (int nf = 0; nf < 4; ++nf) bf[nf] = lds_read16(sb + (offB[nf] ^ x));
+#pragma unroll
+    for (int mf = 0; mf < MF; ++mf) af[mf] = lds_read16(sb + (offA[mf] ^ x));
+  };
+
+  f4v acc[MF][4];
+#pragma unroll
+  for (int mf = 0; mf < MF; ++mf)
+#pragma unroll
+    for (int nf = 0; nf < 4; ++nf) acc[mf][nf] = f4v{0.f, 0.f, 0.f, 0.f};
+  auto mfmas = [&](const i4v (&bf)[4], const i4v (&af)[MF]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int mf = 0; mf < MF; ++mf)
+#pragma unroll
+      for (int nf = 0; nf < 4; ++nf)
+        acc[mf][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+            __builtin_bit_cast(b8v, bf[nf]), __builtin_bit_cast(b8v, af[mf]), acc[mf][nf], 0, 0, 0);
+  };
+
+  // ---- epilogue: packed bf16 rows waiting to be stored, SPI per stage over the next tile ----
+  const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(a.C, 0, a.cbytes, 0x00020000);
+  i4v outv[NST];
+  int st_done = NST;   // stores of the pending tile already issued
+  uint32_t obase = 0;  // lane byte offset of the pending tile's first row fragment
+  auto pack = [&](int tile) __attribute__((always_inline)) {
+    const int m0 = (tile / a.ntn) * TM, n0 = (tile % a.ntn) * kTN;
+    const uint32_t row = (uint32_t)(m0 + wm * (TM / 2) + fr);
+    obase = (row * a.ldc + (uint32_t)(n0 + wn * 64 + fq * 16)) * 2u;
+#pragma unroll
+    for (int mf = 0; mf < MF; ++mf)
+#pragma unroll
+      for (int hlf = 0; hlf < 2; ++hlf) {
+        i4v v;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          const int nf = 2 * hlf + (d >> 1), j = 2 * (d & 1);
+          const b2v p = {(__bf16)acc[mf][nf][j], (__bf16)acc[mf][nf][j + 1]};
+          v[d] = __builtin_bit_cast(int, p);
+        }
+        outv[2 * mf + hlf] = v;
+      }
+#pragma unroll
+    for (int mf = 0; mf < MF; ++mf)
+#pragma unroll
+      for (int nf = 0; nf < 4; ++nf) acc[mf][nf] = f4v{0.f, 0.f, 0.f, 0.f};
+    st_done = 0;
+  };
+  auto store_some = [&](int n) __attribute__((always_inline)) {
+    const int lo = st_done, hi = min(NST, st_done + n);
+#pragma unroll
+    for (int s = 0; s < NST; ++s)
+      if (s >= lo && s < hi) {
+        const uint32_t off = obase + (uint32_t)((s >> 1) * 16) * a.ldc * 2u + (uint32_t)((s & 1) * 16);
+        __builtin_amdgcn_raw_buffer_store_b128(outv[s], crs, off, 0, 0);
+      }
+    st_done = hi;
+  };
+
+  // ---- pipeline: stage h+1 streams in while stage h computes ----
+  // Iteration h: the earlier tile's stores (issued first, so they are older than the DMA) ->
+  // DMA of stage h+1 into the other slot (its last readers passed the previous barrier) ->
+  // k-step 0 fragments, MFMAs with k-step 1's fragments in flight, k-step 1 MFMAs -> vmcnt(0)
+  // (stage h+1 landed, this wave's stores done) -> barrier.
+  if (NH > 0) {
+    stage();
+    dma_wait();
+    lds_barrier();
+  }
+  int cur_ks = 0, cur_tile = lid;
+  i4v bf0[4], af0[MF], bf1[4], af1[MF];
+  for (int h = 0; h < NH; ++h) {
+    if (st_done < NST) store_some(SPI);
+    if (st_h < NH && !(SC_TN_ABL & 2)) stage();
+    const uint32_t sb = lds0 + (h % kSlots) * kSlotB;
+    load_frags(sb, 0, bf0, af0);
+    load_frags(sb, 1, bf1, af1);
+    if (SC_TN_ABL & 1) {
+#pragma unroll
+      for (int mf = 0; mf < MF; ++mf)
+        acc[mf][0][0] += (float)(bf0[mf & 3][0] ^ af1[mf][1]) + (float)(bf1[mf & 3][2] ^ af0[mf][3]);
+    } else {
+      mfmas(bf0, af0);
+      mfmas(bf1, af1);
+    }
+    if (++cur_ks == nks) {
+      pack(cur_tile);
+      cur_ks = 0;
+      cur_tile += G;
+    }
+    dma_wait();
+    lds_barrier();
+  }
+  if (st_done < NST) store_some(NST);
+}
+
+template <int MF, int SPI>
+int launch_tn(const TnArgs& a, hipStream_t st) {
+  auto kern = tn_kernel<MF, SPI>;
+  constexpr size_t lds = (size_t)kSlots * (32 * MF + kTN) * kRowB;
+  static const bool ok = hipFuncSetAttribute((const void*)kern,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             (int)lds) == hipSuccess;
+  (void)ok;
+  const int grid = a.tiles < 256 ? a.tiles : 256;
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(512), lds, st, a);
+  return 0;
+}
+
+}  // namespace
+}  // namespace sc
+
+using namespace sc;
+
+extern "C" int sc_gemm_tn_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, void* C,
+                               int64_t ldc, int M, int N, int K, int tile_m, void* stream) {
+  clear_error();
+  SC_REQUIRE(A && B && C, "sc_gemm_tn_bf16: null pointer");
+  SC_REQUIRE(M > 0 && N > 0 && K > 0, "sc_gemm_tn_bf16: empty shape M=%d N=%d K=%d", M, N, K);
+  SC_REQUIRE(K % kBK == 0, "sc_gemm_tn_bf16: K=%d must be a multiple of 64 (zero-pad it)", K);
+  SC_REQUIRE(N % kTN == 0, "sc_gemm_tn_bf16: N=%d must be a multiple of 256", N);
+  SC_REQUIRE(tile_m == 0 || tile_m == 128 || tile_m == 192,
+             "sc_gemm_tn_bf16: tile_m=%d must be 0 (default 192), 128 or 192", tile_m);
+  SC_REQUIRE(lda >= K && ldb >= K && ldc >= N && lda % 8 == 0 && ldb % 8 == 0 && ldc % 8 == 0,
+             "sc_gemm_tn_bf16: leading dimensions must cover the rows in 16-byte pieces");
+  SC_REQUIRE((uintptr_t)A % 16 == 0 && (uintptr_t)B % 16 == 0 && (uintptr_t)C % 16 == 0,
+             "sc_gemm_tn_bf16: operands must be 16-byte aligned");
+  SC_REQUIRE((int64_t)M * lda * 2 < (1ll << 32) && (int64_t)N * ldb * 2 < (1ll << 32) &&
+                 ((int64_t)M + 256) * ldc * 2 < (1ll << 32),
+             "sc_gemm_tn_bf16: operands must be smaller than 4 GiB");
+  const int tm = tile_m ? tile_m : 192;
+  const int ntn = N / kTN;
+  const int64_t tiles = (int64_t)((M + tm - 1) / tm) * ntn;
+  SC_REQUIRE(tiles < (1 << 30), "sc_gemm_tn_bf16: too many tiles");
+  TnArgs a{(const __bf16*)A, (const __bf16*)B, (__bf16*)C, M, N, K, ntn, (int)tiles,
+           (uint32_t)lda, (uint32_t)ldb, (uint32_t)ldc, (uint32_t)((int64_t)M * ldc * 2)};
+  hipStream_t st = (hipStream_t)stream;
+  // stores per stage: a tile's 2 MF stores must be issued within the next tile's K / 64 stages
+  const int nks = K / kBK, nst = 2 * (tm / 32);
+  const int spi = (nst + nks - 1) / nks;
+  if (tm == 128) {
+    if (spi <= 1) launch_tn<4, 1>(a, st);
+    else if (spi <= 2) launch_tn<4, 2>(a, st);
+    else if (spi <= 4) launch_tn<4, 4>(a, st);
+    else launch_tn<4, 8>(a, st);
+  } else {
+    if (spi <= 1) launch_tn<6, 1>(a, st);
+    else if (spi <= 2) launch_tn<6, 2>(a, st);
+    else if (spi <= 4) launch_tn<6, 4>(a, st);
+    else if (spi <= 6) launch_tn<6, 6>(a, st);
+    else launch_tn<6, 12>(a, st);
+  }
+  return launch_status("sc_gemm_tn_bf16");
+}

@@ -17,7 +17,7 @@ import torch
 import torch.nn as nn
 
 from .lucyrnn_conf import LucyRNNConfig
-from .ops import colsum, layer_norm, layer_norm_supported, lucy_cell, wgrad_splitk
+from .ops import colsum, layer_norm, layer_norm_supported, lucy_cell, proj_dgrad, wgrad_splitk
 
 
 class _LinearFn(torch.autograd.Function):
@@ -37,7 +37,9 @@ class _LinearFn(torch.autograd.Function):
         xc, wc = ctx.saved_tensors
         xdt, wdt, has_b = ctx.meta
         dy = dy.to(wc.dtype)
-        dx = (dy @ wc).to(xdt) if ctx.needs_input_grad[0] else None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = proj_dgrad(dy, wc).to(xdt)
         dw = wgrad_splitk(dy, xc).to(wdt) if ctx.needs_input_grad[1] else None
         db = colsum(dy).to(wdt) if has_b and ctx.needs_input_grad[2] else None
         return dx, dw, db, None

@@ -3,6 +3,8 @@
 Each op checks device/dtype/shape, allocates outputs through the PyTorch caching allocator,
 launches on the current stream and never synchronises the host.
 """
+import os
+
 import torch
 
 from . import _lib
@@ -207,6 +209,61 @@ def wgrad_mfma(dy, x, blocked_d=0):
     return colsum(part.view(S, N * K), perm).view(N, K)
 
 
+# SC_TN=0 routes the projection GEMMs back to the library (A/B timing in tools/ only)
+USE_TN = os.environ.get("SC_TN", "1") != "0"
+
+
+def tn_ok(a, b):
+    """True when C = a b^T runs on the hand-written MFMA kernel (sc_gemm_tn_bf16): bf16 ROCm
+    operands, K-contiguous, K % 64 == 0, N % 256 == 0, 16-byte aligned rows."""
+    return (USE_TN and a.is_cuda and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16
+            and a.dim() == 2 and b.dim() == 2 and a.shape[1] == b.shape[1]
+            and a.shape[1] % 64 == 0 and b.shape[0] % 256 == 0 and a.shape[0] > 0
+            and a.stride(1) == 1 and b.stride(1) == 1 and a.stride(0) % 8 == 0
+            and b.stride(0) % 8 == 0 and a.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0
+            and (a.shape[0] + 256) * max(a.stride(0), b.shape[0]) * 2 < 2 ** 32
+            and b.shape[0] * b.stride(0) * 2 < 2 ** 32)
+
+
+def proj_fwd(x, w):
+    """x [M,K] @ w [N,K]^T for the frame-major projections.  Measured at the C2 shapes
+    (tools/tn_bench.py): the hand-written kernel wins where the output stream dominates (layer 0,
+    K = 80 padded to 128: 116 vs 128 us); at K = 512 the library's 256 x 192 tiles win (157 vs
+    246 us; csrc/tn_gemm.hip header)."""
+    if x.shape[1] <= 128 and tn_ok(x, w):
+        return gemm_tn(x, w)
+    return torch.matmul(x, w.t())
+
+
+def proj_dgrad(dy, w):
+    """dy [M,N] @ w [N,K] as dy (w^T)^T: the library's NT kernels beat its NN choice for these
+    shapes (gate input gradient 142 vs 160 us; output projection 52 vs 143 us in-step with the
+    stream-K kernel the NN form picks); w^T is a 3.7 MB / 1 MB copy."""
+    wt = w.t().contiguous()
+    return torch.matmul(dy, wt.t())
+
+
+def gemm_tn(a, b, tile_m=0):
+    """C [M,N] bf16 = a [M,K] b [N,K]^T on the persistent MFMA kernel (csrc/tn_gemm.hip);
+    the caller checks tn_ok(a, b)."""
+    M, K = a.shape
+    N = b.shape[0]
+    c = torch.empty(M, N, dtype=torch.bfloat16, device=a.device)
+    rc = _lib.load().sc_gemm_tn_bf16(ptr(a), a.stride(0), ptr(b), b.stride(0), ptr(c), c.stride(0),
+                                     M, N, K, tile_m, stream_of(a))
+    check(rc, "sc_gemm_tn_bf16")
+    return c
+
+
+def pad_cols(x, k, dtype):
+    """x [M, K0] -> [M, k] in `dtype` with zero columns K0..k-1 (one cast-copy + one fill)."""
+    M, k0 = x.shape
+    out = torch.empty(M, k, dtype=dtype, device=x.device)
+    out[:, k0:].zero_()
+    out[:, :k0].copy_(x)
+    return out
+
+
 def step_blocked_rows(w, D, inverse=False, dtype=None):
     """Permute the 7*D rows of a gate projection weight from the reference's (gate, unit) order
     to (column block of 64 units, gate, unit-in-block) order (inverse=True: back), converting to
@@ -232,21 +289,29 @@ class LucyCellFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x2d, w, b, h0, s0, B, T, cdt):
         ctx.set_materialize_grads(False)   # unused state outputs: no zero-filled gradients
-        xc = x2d.to(cdt)
         D = w.shape[0] // 7
         blocked = D % 64 == 0
+        Din = x2d.shape[1]
+        # layer 0 (Din = 80): the bf16 cast writes zero columns up to a multiple of 64, the
+        # MFMA kernel's K stage (the weight gets the same zero columns)
+        kp = Din + (-Din) % 64
+        tn = USE_TN and x2d.is_cuda and cdt == torch.bfloat16 and (7 * D) % 256 == 0
+        xc = pad_cols(x2d, kp, cdt) if tn and kp != Din else x2d.to(cdt)
         # step-blocked gates: weight rows permuted to (column block, gate, unit) order so each
         # step's 7 x 64 gates of a column block are one contiguous 896-byte run for the scan
         wc = step_blocked_rows(w, D, dtype=cdt) if blocked else w.to(cdt)
+        if tn and kp != Din:
+            wc = pad_cols(wc, kp, cdt)
         bias = b.detach().to(torch.float32).contiguous()
         with _timed("gate_gemm_fwd", xc, 0):
-            gates = torch.matmul(xc, wc.t())
+            gates = proj_fwd(xc, wc)
         gates = gates.view(B, T, D // 64, 7, 64) if blocked else gates.view(B, T, 7, D)
         need = any(ctx.needs_input_grad)
         gates, out, s_out, ckpt, h_out = _scan_fwd(gates, h0, s0, need, bias, want_h=True)
         if need:
             ctx.save_for_backward(xc, wc, gates, ckpt, bias)
             ctx.dtypes = (x2d.dtype, w.dtype, h0.dtype, s0.dtype)
+            ctx.din = Din
             ctx.blocked = blocked
         return out, s_out, h_out
 
@@ -264,13 +329,17 @@ class LucyCellFn(torch.autograd.Function):
         dgates, dh0, ds0, dbias = _scan_bwd(gates, ckpt, dout, ds_last, ctx.needs_input_grad[2],
                                             bias)
         dg2 = dgates.view(xc.shape[0], -1)
-        with _timed("gate_gemm_dgrad", dg2, 0):
-            dx = (dg2 @ wc).to(xdt) if ctx.needs_input_grad[0] else None
+        din = ctx.din
+        dx = None
+        if ctx.needs_input_grad[0]:
+            with _timed("gate_gemm_dgrad", dg2, 0):
+                dx = proj_dgrad(dg2, wc[:, :din])
+            dx = dx.to(xdt)
         dw = None
         if ctx.needs_input_grad[1]:
             with _timed("gate_gemm_wgrad", dg2, 0):
                 dw = wgrad_splitk(dg2, xc, blocked_d=(dg2.shape[1] // 7) if ctx.blocked else 0)
-            dw = dw.to(wdt)
+            dw = (dw[:, :din] if dw.shape[1] != din else dw).to(wdt)
         db = colsum(dbias.view(dbias.shape[0], -1)).to(wdt) if dbias is not None else None
         return dx, dw, db, dh0.to(hdt), ds0.to(sdt), None, None, None
 

@@ -99,3 +99,79 @@ def test_colsum_perm_with_unaligned_rows(N):
     out = ops().colsum(x, (A, Bf))
     ref = x.double().sum(0).view(A, Bf, -1).transpose(0, 1).reshape(-1)
     torch.testing.assert_close(out.double(), ref, rtol=1e-5, atol=1e-4)
+
+
+# ----------------------------------------------------------- frame-major TN GEMM (tn_gemm.hip) --
+# C = A B^T in bf16 with fp32 accumulation: products of bf16 values are exact in fp32, so the
+# kernel differs from an fp32 reference only by summation order (~1e-6 relative) and then by the
+# final bf16 rounding (<= 2^-8 relative); tolerance 2^-8 of the value + 1e-5 of the largest |C|.
+def _tn_ref(a, b):
+    return a.float() @ b.float().t()
+
+
+def _tn_check(c, ref):
+    assert c.dtype == torch.bfloat16 and c.shape == ref.shape
+    err = (c.float() - ref).abs()
+    tol = ref.abs() * 2.0 ** -8 + 1e-5 * ref.abs().max()
+    assert bool((err <= tol).all()), (err - tol).max().item()
+
+
+@pytest.mark.parametrize("M,N,K,tm", [(48000, 3584, 512, 0),    # gate forward, layers 1-5 (C2)
+                                      (48000, 3584, 128, 0),    # layer 0 (Din 80 padded to 128)
+                                      (48000, 512, 3584, 0),    # gate input gradient
+                                      (48000, 512, 1024, 0),    # output-projection input gradient
+                                      (5000, 1024, 512, 128),   # ragged rows, 128-row tiles
+                                      (193, 256, 64, 0),        # one row past a panel
+                                      (7, 512, 64, 128)])       # fewer rows than a fragment
+def test_tn_gemm_vs_fp32(M, N, K, tm):
+    g = torch.Generator(device=DEV).manual_seed(M + N + K)
+    a = torch.randn(M, K, device=DEV, generator=g).to(torch.bfloat16)
+    b = (torch.randn(N, K, device=DEV, generator=g) + torch.arange(K, device=DEV) / K).to(torch.bfloat16)
+    assert ops().tn_ok(a, b)
+    _tn_check(ops().gemm_tn(a, b, tm), _tn_ref(a, b))
+
+
+@pytest.mark.parametrize("tm", [128, 192])
+def test_tn_gemm_structured_exact(tm):
+    """Small-integer operands: every sum is exact in fp32 and |C| <= 256 is exact in bf16, so the
+    result must equal the reference bitwise — pins the fragment maps, the swizzle and the
+    column order of the packed stores independent of rounding."""
+    M, N, K = 1000, 512, 192
+    mi = torch.arange(M, device=DEV)[:, None]
+    a = ((mi * 3 + torch.arange(K, device=DEV)[None, :] * 7) % 5 - 2).to(torch.bfloat16)
+    ni = torch.arange(N, device=DEV)[:, None]
+    b = (((ni * 5 + torch.arange(K, device=DEV)[None, :] * 11) % 3) - 1).to(torch.bfloat16)
+    ref = _tn_ref(a, b)
+    assert ref.abs().max() <= 256
+    assert torch.equal(ops().gemm_tn(a, b, tm).float(), ref)
+
+
+def test_tn_gemm_strided_operands_and_row_bound():
+    """Leading dimensions wider than K / N, and C rows >= M left untouched (the buffer
+    descriptor's range drops the stores of a partial panel)."""
+    from statecatcher_amd import _lib
+    M, N, K = 300, 512, 128
+    g = torch.Generator(device=DEV).manual_seed(5)
+    abig = torch.randn(M, K + 40, device=DEV, generator=g).to(torch.bfloat16)
+    bbig = torch.randn(N, K + 8, device=DEV, generator=g).to(torch.bfloat16)
+    a, b = abig[:, :K], bbig[:, :K]
+    cbig = torch.full((M + 100, N + 64), 7.0, device=DEV, dtype=torch.bfloat16)
+    rc = _lib.load().sc_gemm_tn_bf16(a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0),
+                                     cbig.data_ptr(), cbig.stride(0), M, N, K, 0, None)
+    assert rc == 0
+    torch.cuda.synchronize()
+    _tn_check(cbig[:M, :N], _tn_ref(a, b))
+    assert bool((cbig[M:] == 7).all()) and bool((cbig[:, N:] == 7).all())
+
+
+def test_tn_gemm_rejects_bad_shapes():
+    from statecatcher_amd import _lib
+    lib = _lib.load()
+    a = torch.zeros(64, 80, device=DEV, dtype=torch.bfloat16)
+    b = torch.zeros(256, 80, device=DEV, dtype=torch.bfloat16)
+    c = torch.zeros(64, 256, device=DEV, dtype=torch.bfloat16)
+    assert lib.sc_gemm_tn_bf16(a.data_ptr(), 80, b.data_ptr(), 80, c.data_ptr(), 256, 64, 256, 80,
+                               0, None) != 0   # K % 32
+    assert lib.sc_gemm_tn_bf16(a.data_ptr(), 80, b.data_ptr(), 80, c.data_ptr(), 256, 64, 200, 64,
+                               0, None) != 0   # N % 256
+    assert not ops().tn_ok(a, b)

@@ -1,0 +1,10 @@
+set -e -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out; mkdir -p $O
+cd /tmp && export TMPDIR=/tmp
+for w in xlstm rnnt; do
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$O/prof_$w" -o run -- \
+  python3 "$R/bench.py" --workload $w --steps 2 --warmup 2 --cpu-baseline off > "$O/bench_prof_$w.json" 2> "$O/bench_prof_$w.err"
+find "$O/prof_$w" -type f ! -name "*kernel_stats.csv" -delete
+done
+echo done
