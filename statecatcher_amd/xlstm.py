@@ -106,7 +106,15 @@ class FeedForward(nn.Module):
         self.proj_down = nn.Linear(up, cfg.embedding_dim, bias=cfg.use_bias)
 
     def forward(self, x):
-        return self.proj_down(F.silu(self.proj_up_gate(x)) * self.proj_up(x))
+        # proj_up_gate and proj_up as ONE GEMM over the concatenated weight (parameters and
+        # state_dict unchanged): one read and one autocast cast of x instead of two
+        up = self.proj_up.weight.shape[0]
+        w = torch.cat([self.proj_up_gate.weight, self.proj_up.weight])
+        b = None
+        if self.proj_up.bias is not None:
+            b = torch.cat([self.proj_up_gate.bias, self.proj_up.bias])
+        g, u = F.linear(x, w, b).split([up, up], -1)
+        return self.proj_down(F.silu(g) * u)
 
 
 class mLSTMLayer(nn.Module):
@@ -127,15 +135,29 @@ class mLSTMLayer(nn.Module):
                                                  cfg.norm_reduction_force_float32)
         self.out_proj = nn.Linear(self.v_dim, d, bias=cfg.use_bias)
 
+    def projections(self, x):
+        """q, k, v, o and the two gate pre-activations from ONE GEMM over the concatenated
+        weight (the parameters and state_dict keep HF's six Linears): x is read and, under
+        autocast, cast once instead of six times, and the two NH-wide gate projections (4 output
+        columns each at C4) stop being GEMMs of their own."""
+        mods = (self.q, self.k, self.v, self.ogate_preact, self.igate_preact, self.fgate_preact)
+        w = torch.cat([m.weight for m in mods])
+        b = None
+        if any(m.bias is not None for m in mods):
+            b = torch.cat([m.bias if m.bias is not None else
+                           torch.zeros(m.weight.shape[0], dtype=m.weight.dtype, device=m.weight.device)
+                           for m in mods])
+        return F.linear(x, w, b).split([m.weight.shape[0] for m in mods], -1)
+
     def forward(self, x, state=None):
         B, T, _ = x.shape
         NH = self.cfg.num_heads
-        q = self.q(x).reshape(B, T, NH, -1).transpose(1, 2)
-        k = self.k(x).reshape(B, T, NH, -1).transpose(1, 2)
-        v = self.v(x).reshape(B, T, NH, -1).transpose(1, 2)
-        o = self.ogate_preact(x)
-        ig = soft_cap(self.igate_preact(x), self.cfg.gate_soft_cap).transpose(1, 2)
-        fg = soft_cap(self.fgate_preact(x), self.cfg.gate_soft_cap).transpose(1, 2)
+        q, k, v, o, ig, fg = self.projections(x)
+        q = q.reshape(B, T, NH, -1).transpose(1, 2)
+        k = k.reshape(B, T, NH, -1).transpose(1, 2)
+        v = v.reshape(B, T, NH, -1).transpose(1, 2)
+        ig = soft_cap(ig, self.cfg.gate_soft_cap).transpose(1, 2)
+        fg = soft_cap(fg, self.cfg.gate_soft_cap).transpose(1, 2)
         c0, n0, m0 = (None, None, None) if state is None else state
         h, new_state = mlstm_chunkwise(q, k, v, ig, fg, c0, n0, m0, return_last_states=True,
                                        eps=self.cfg.eps)
