@@ -389,19 +389,18 @@ int sc_rnnt_bwd(const void* x, int x_dtype, int is_logits, int B, int T, int max
  *   W     bf16 [V][J]          joiner.weight (MFMA operand); bias fp32 [V] = joiner.bias
  * J must be 64 (train.py:639's --rnnt-joiner-dim default), V a multiple of 32, <= 1024.
  * Forward: nll fp32 [B] as sc_rnnt_fwd (same workspace, sc_rnnt_workspace_bytes).
- * Backward (after the forward, same workspace) of sum_b scale[b] nll[b]:
- *   d_enc   fp32 [u_splits][B][T][J]   partials over u (sum them: d enc)
- *   d_pred  fp32 [B][t_blocks][U1][J]  partials over t-blocks of 32 (sum: d pred); zero-filled by
+ * Backward (after the forward, same workspace) of sum_b scale[b] nll[b], one pass over the
+ * logits (the workgroups split the vocabulary; t_blocks and u_splits count those splits too):
+ *   d_enc   fp32 [u_splits][B][T][J]   partials (sum them: d enc)
+ *   d_pred  fp32 [B][t_blocks][U1][J]  partials (sum over t_blocks: d pred); zero-filled by
  *                                      the caller (columns outside the lattice are not written)
- *   g_blank, g_label  fp32 [B][t_blocks][U1][J]  (zero-filled) sums of scale occ z over each
- *                                      t-block for the blank arc and the label arc y[b][u]
- *   s_bl    fp32 [B][t_blocks][U1][2]  (zero-filled) the same sums of scale occ without z
- *   dW      fp32 [slices][V][J], db fp32 [slices][V]: partials of the dense part sum_n a_n
- *           softmax_n z_n^T, a_n = scale (occ_blank + occ_label)
- * d W = sum_s dW[s] - e_blank (sum g_blank) - sum_{b,u<U_b} e_{y[b][u]} (sum_tb g_label[b][tb][u]);
- * d bias likewise with s_bl.  t_blocks / u_splits / slices: sc_rnnt_joint_geometry.
+ *   dW      fp32 [slices][V][J], db fp32 [slices][V]: partials of sum_n dlogits_n z_n^T and
+ *           sum_n dlogits_n, dlogits_n = a_n softmax_n - w_blank,n e_blank - w_label,n e_y,
+ *           a_n = scale (occ_blank + occ_label) (sum them in a fixed order: d W, d bias)
+ * t_blocks / u_splits / slices: sc_rnnt_joint_geometry.
  */
-int sc_rnnt_joint_geometry(int B, int T, int max_labels, int* t_blocks, int* u_splits, int* slices);
+int sc_rnnt_joint_geometry(int B, int T, int max_labels, int V, int* t_blocks, int* u_splits,
+                           int* slices);
 int sc_rnnt_joint_fwd(const float* enc, const float* pred, const void* W, const float* bias, int B,
                       int T, int max_labels, int V, int J, const int64_t* labels,
                       int64_t label_stride, const int64_t* frames_lengths,
@@ -411,8 +410,8 @@ int sc_rnnt_joint_bwd(const float* enc, const float* pred, const void* W, const 
                       int T, int max_labels, int V, int J, const int64_t* labels,
                       int64_t label_stride, const int64_t* frames_lengths,
                       const int64_t* labels_lengths, int blank, const float* scale, float* d_enc,
-                      float* d_pred, float* g_blank, float* g_label, float* s_bl, float* dW,
-                      float* db, const void* workspace, size_t workspace_bytes, void* stream);
+                      float* d_pred, float* dW, float* db, const void* workspace,
+                      size_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus
 }

@@ -511,17 +511,10 @@ int esize_of(int dt) { return dt == SC_F32 ? 4 : 2; }
 //                     operand computed in registers), online log-sum-exp over V with the node on the
 //                     lane (the 32x32 accumulator holds one node's 16 logits per lane), blank and
 //                     label logits as direct dot products -> lse, lpb, lpy in rnnt_ab's layout.
-//   joint_dz_kernel   backward, node-major: recompute logits, dense dlogits = a_n softmax_n
-//                     (a_n = occupancy of the node's two arcs x scale), dZ^T = W^T dlogits on MFMA
-//                     with the accumulator as the operand (the sum runs over its row index, no
-//                     LDS transpose; W^T fragments by ds_read_b64_tr_b16), the sparse blank/label
-//                     terms, dpre = dZ (1 - z^2) -> d enc (accumulated over u in registers), d pred
-//                     and the blank/label rows' z sums (lane reductions over the t-block).
-//   joint_dw_kernel   backward, vocab-major: logits recomputed with v on the lane so that
-//                     dW = dlogits^T Z sums over the accumulator's row index again; 8 waves of a
-//                     workgroup own 128 rows of W each and accumulate their dW slice in registers
-//                     over the workgroup's nodes (one fp32 partial per workgroup, summed on the host
-//                     side in a fixed order).
+//   joint_bwd_kernel  backward in one pass: logits recomputed once, dense dlogits = a_n softmax_n
+//                     (a_n = occupancy of the node's two arcs x scale) feed both dW (accumulator
+//                     as the next MFMA's operand, dW resident in registers) and dZ (p transposed
+//                     through LDS); d pre = dZ (1 - z^2) -> d enc / d pred partials (see below).
 // Each kernel evaluates exp once per logit; the logits themselves never leave registers.
 constexpr int kJ = 64;
 constexpr int kVmaxJ = 1024;   // W image [V][64] bf16 = 128 KB of LDS
@@ -535,13 +528,10 @@ struct JointArgs {
   const float* pred;   // [B][U1][64]  pred_proj(embedding(blank-prefixed labels)), contiguous
   const __bf16* W;     // [V][64]      joiner.weight
   const float* bias;   // [V]          joiner.bias
-  int ntb, nus, S;
-  float* d_enc;        // [nus][B][T][64]
-  float* d_pred;       // [B][ntb][U1][64]
-  float* g_blank;      // [B][ntb][U1][64]  sum over the t-block of sc occ_blank z
-  float* g_label;      // [B][ntb][U1][64]  sum over the t-block of sc occ_label z
-  float* s_bl;         // [B][ntb][U1][2]   sum over the t-block of sc occ_blank, sc occ_label
-  float* dW;           // [S][V][64]       dense part a_n softmax_n z_n^T
+  int ntb, nus, S, vs;   // t-blocks, u-splits, dW slices, vocab splits of the backward
+  float* d_enc;        // [vs * nus][B][T][64]
+  float* d_pred;       // [B][vs * ntb][U1][64]   (vocab split vh at t-block row vh * ntb + tb)
+  float* dW;           // [S][V][64]       partials of sum_n dlogits_n z_n^T
   float* db;           // [S][V]
 };
 
@@ -766,266 +756,352 @@ __global__ void __launch_bounds__(512) joint_fwd_kernel(JointArgs a) {
   }
 }
 
-__global__ void __launch_bounds__(512) joint_dz_kernel(JointArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-  load_w(a, lds);
-  // per-wave scratch: the column's blank / label weights, written lane-major, read per register
-  float* scr = (float*)(lds + kVmaxJ * 128 + kVmaxJ * 4) + (threadIdx.x >> 6) * 64;
-  __syncthreads();
-  const RnntArgs& r = a.r;
-  const int lane = threadIdx.x & 63, h = lane >> 5, g1 = (lane >> 4) & 1;
-  const int jl = lane & 31;
-  const int64_t ntask = (int64_t)r.B * a.ntb * a.nus;
-  const int64_t wid = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 6), nwv = (int64_t)gridDim.x * 8;
-  for (int64_t task = wid; task < ntask; task += nwv) {
-    const int b = (int)(task / ((int64_t)a.ntb * a.nus));
-    const int tb = (int)((task / a.nus) % a.ntb), us = (int)(task % a.nus);
-    const int Tb = clampr(r.flen[b], 0, r.T), Ub = clampr(r.llen[b], 0, r.Umax);
-    const int t = tb * 32 + jl;   // the lane's node in the logits (node-on-lane) orientation
-    const bool tok = t < Tb;
-    const int tc = tok ? t : max(Tb - 1, 0);
-    const int ua = (int)((int64_t)us * r.U1 / a.nus), ue = (int)((int64_t)(us + 1) * r.U1 / a.nus);
-    // d enc accumulated over this task's u in the dZ layout: [jb][q] = (node (q&3)+8(q>>2)+4h,
-    // j = jb*32 + (lane&31))
-    float de[2][16];
-#pragma unroll
-    for (int jb = 0; jb < 2; ++jb)
-#pragma unroll
-      for (int q = 0; q < 16; ++q) de[jb][q] = 0.0f;
-    const bool live = uniform(tb * 32) < Tb;
-    for (int u = ua; live && u < ue && u <= Ub; ++u) {
-      jbf8 zb[4];
-      z_frags(a, b, tc, u, tok, h, zb);
-      float wb = 0.0f, wy = 0.0f;
-      if (tok) node_weights(r, b, t, u, Tb, Ub, wb, wy);
-      const float an = wb + wy;
-      const float lse2 = tok ? r.ws.lse[((int64_t)b * r.T + t) * r.U1 + u] * kLog2e : 1e30f;
-      if (h == 0) {
-        scr[jl] = wb;
-        scr[32 + jl] = wy;
-      }
-      jf16 Y[2];
-#pragma unroll
-      for (int jb = 0; jb < 2; ++jb)
-#pragma unroll
-        for (int q = 0; q < 16; ++q) Y[jb][q] = 0.0f;
-      for (int v0 = 0; v0 < r.V; v0 += 32) {
-        const jf16 x = logits_vblock(lds, v0, lane, zb);
-        float p[16];
-#pragma unroll
-        for (int q = 0; q < 16; ++q) p[q] = an * exp2_(fmaf(x[q], kLog2e, -lse2));
-        // dZ[node][j] += sum_v dlogits[v][node] W[v][j]: the accumulator's rows (v) are the sum,
-        // so x is the A operand as is; W[v][j] with j on the lane comes from tr reads
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          const jbf8 xf = pack8(p + 8 * s2);
-#pragma unroll
-          for (int jb = 0; jb < 2; ++jb) {
-            const jbf8 wt = cat8(tr_rd(lds, v0 + 16 * s2 + 4 * h, jb * 32 + 16 * g1, lane),
-                                 tr_rd(lds, v0 + 16 * s2 + 8 + 4 * h, jb * 32 + 16 * g1, lane));
-            Y[jb] = mfma32(xf, wt, Y[jb]);
-          }
-        }
-      }
-      // Y[jb][q] = dZ_dense[node n_q][j]; per-register node weights back from the scratch
-      float wbr[16], wyr[16];
-#pragma unroll
-      for (int q4 = 0; q4 < 4; ++q4) {
-        const float4 bv = *(const float4*)(scr + 8 * q4 + 4 * h);
-        const float4 yv = *(const float4*)(scr + 32 + 8 * q4 + 4 * h);
-        wbr[4 * q4] = bv.x; wbr[4 * q4 + 1] = bv.y; wbr[4 * q4 + 2] = bv.z; wbr[4 * q4 + 3] = bv.w;
-        wyr[4 * q4] = yv.x; wyr[4 * q4 + 1] = yv.y; wyr[4 * q4 + 2] = yv.z; wyr[4 * q4 + 3] = yv.w;
-      }
-      const int yl = u < Ub ? label_at(r, b, u) : r.blank;
-      const float* pp = a.pred + ((int64_t)b * r.U1 + u) * kJ;
-      const float* eb = a.enc + (int64_t)b * r.T * kJ;
-      const float* bias = (const float*)(lds + kVmaxJ * 128);
-      (void)bias;
-#pragma unroll
-      for (int jb = 0; jb < 2; ++jb) {
-        const int j = jb * 32 + jl;
-        const float pj = pp[j];
-        const float wbj = (float)*(const __bf16*)(lds + wimg(r.blank, j >> 3) + 2 * (j & 7));
-        const float wyj = (float)*(const __bf16*)(lds + wimg(yl, j >> 3) + 2 * (j & 7));
-        float sp = 0.0f, sgb = 0.0f, sgy = 0.0f;
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-          const int n = (q & 3) + 8 * (q >> 2) + 4 * h;
-          const int tq = tb * 32 + n;
-          const bool ok = tq < Tb;
-          const float z = ok ? tanh_(eb[(int64_t)min(tq, r.T - 1) * kJ + j] + pj) : 0.0f;
-          const float dz = Y[jb][q] - wbr[q] * wbj - wyr[q] * wyj;
-          const float dp = ok ? dz * (1.0f - z * z) : 0.0f;
-          de[jb][q] += dp;
-          sp += dp;
-          sgb = fmaf(wbr[q], z, sgb);
-          sgy = fmaf(wyr[q], z, sgy);
-        }
-        sp += __shfl_xor(sp, 32);
-        sgb += __shfl_xor(sgb, 32);
-        sgy += __shfl_xor(sgy, 32);
-        if (h == 0) {
-          const int64_t row = (((int64_t)b * a.ntb + tb) * r.U1 + u) * kJ + j;
-          a.d_pred[row] = sp;
-          a.g_blank[row] = sgb;
-          a.g_label[row] = sgy;
-        }
-      }
-      const float sb = half_sum(wb), sy = half_sum(wy);
-      if (lane == 0) {
-        const int64_t srow = (((int64_t)b * a.ntb + tb) * r.U1 + u) * 2;
-        a.s_bl[srow] = sb;
-        a.s_bl[srow + 1] = sy;
-      }
-    }
-    float* dst = a.d_enc + ((int64_t)us * r.B + b) * r.T * kJ;
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int tq = tb * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
-      if (tq < r.T) {
-#pragma unroll
-        for (int jb = 0; jb < 2; ++jb) dst[(int64_t)tq * kJ + jb * 32 + jl] = de[jb][q];
-      }
-    }
-  }
+// Backward in ONE pass over the logits (joint_bwd_kernel).  A workgroup of 4 waves (one per
+// SIMD, up to 512 registers each) owns half of the vocabulary (16 blocks of 32 rows of W, 64 KB of
+// LDS) and walks node columns (b, 32-frame t-block, u); every wave takes 4 of the vocab blocks of
+// every column:
+//   x[n][v] = z_n . W_v          (v_mfma_f32_32x32x16_bf16: node on the row, v on the lane)
+//   p[n][v] = a_n exp(x + b_v - lse_n)                 (dense dlogits, once per logit)
+//   dW[v][j] += sum_n p[n][v] z[n][j]   (p's registers are the A operand: the sum runs over the
+//                                        accumulator's row index; dW stays in registers)
+//   dZ[n][j] += sum_v p[n][v] W[v][j]   (p transposed through a 4 KB per-wave LDS image and read
+//                                        back by ds_read_b64_tr_b16)
+// The gathered lattice's sparse arcs enter p itself (p[n][blank] -= wb_n, p[n][y_u] -= wy_n in
+// the one or two blocks holding those rows), so dW, d bias and dZ need no separate terms.
+// dZ is a partial over the wave's vocab blocks; everything downstream of it is linear, so each
+// wave folds its partial straight into d pre = dZ (1 - z^2), d enc (accumulated over u in a
+// per-wave LDS partial) and d pred (summed over the t-block), and the partials meet only in small
+// LDS reductions (d pred per column, d enc per task) and in the host's fixed-order sums over the
+// vocab halves.  Node occupancies (alpha, beta, lse: fp64 offsets) of the next column are loaded
+// while the current one computes.
+// SC_JOINT_SB: a scheduling barrier between the vocab blocks of a column (A/B in tools only)
+#ifndef SC_JOINT_SB
+#define SC_JOINT_SB 1
+#endif
+#ifndef SC_JOINT_BF
+#define SC_JOINT_BF 0
+#endif
+constexpr int kVbWg = 16;   // vocab blocks (of 32) per workgroup
+constexpr int kVbW = 4;     // per wave
+
+struct NodeLd {   // the loads of node_weights, issued one column ahead
+  double lp2, oA, oB, be_b, be_y;
+  float al, eb, ey, sc, lse;
+  bool ok;
+};
+
+__device__ __forceinline__ NodeLd node_load(const RnntArgs& a, int b, int t, int u, int Tb, int Ub) {
+  NodeLd d;
+  d.ok = t < Tb && u <= Ub;
+  const int tc = d.ok ? t : 0, uc = d.ok ? u : 0;
+  d.lp2 = a.ws.logp2[b];
+  d.sc = a.scale[b];
+  const int n = tc + uc;
+  const int64_t base = (int64_t)b * a.ND * a.U1p;
+  const int per = 2 * a.kh, nd = Tb + Ub;
+  d.oA = a.ws.offA[(int64_t)b * a.ND + (n + 1) / per];
+  d.oB = a.ws.offB[(int64_t)b * a.ND + max(nd - n - 1, 0) / per];
+  d.al = a.ws.alpha[base + (int64_t)n * a.U1p + uc];
+  d.eb = a.ws.lpb[base + (int64_t)n * a.U1p + uc];
+  d.ey = a.ws.lpy[base + (int64_t)n * a.U1p + uc];
+  d.be_b = a.ws.beta[base + (int64_t)(n + 1) * a.U1p + uc];
+  d.be_y = a.ws.beta[base + (int64_t)(n + 1) * a.U1p + min(uc + 1, a.U1p - 1)];
+  d.lse = a.ws.lse[((int64_t)b * a.T + tc) * a.U1 + uc];
+  return d;
 }
 
-__global__ void __launch_bounds__(512) joint_dw_kernel(JointArgs a) {
+// (wb, wy, lse2) of a loaded node, as node_weights computes them
+__device__ __forceinline__ void node_finish(const NodeLd& d, int t, int u, int Tb, int Ub, float& wb,
+                                            float& wy, float& l2) {
+  wb = 0.0f;
+  wy = 0.0f;
+  const double al = (double)d.al + d.oA;
+  if (t + 1 < Tb) wb = exp2_((float)(al + d.eb + ((double)d.be_b + d.oB) - d.lp2));
+  else if (u == Ub) wb = exp2_((float)(al + d.eb - d.lp2));
+  if (u < Ub) wy = exp2_((float)(al + d.ey + ((double)d.be_y + d.oB) - d.lp2));
+  const bool live = d.ok && d.lp2 > -1e300 && d.sc != 0.0f;
+  wb = live ? wb * d.sc : 0.0f;
+  wy = live ? wy * d.sc : 0.0f;
+  l2 = d.ok ? d.lse * kLog2e : 1e30f;
+}
+
+struct BwdLds {   // byte offsets of the LDS regions
+  static constexpr int kDeP = 36;                       // d enc partial row pitch (floats)
+  static constexpr int kW = 0;                          // W half image [512][128 B]
+  static constexpr int kBias = kW + kVbWg * 32 * 128;   // [512] fp32, x log2(e)
+  static constexpr int kZ = kBias + kVbWg * 32 * 4;     // z bf16 image [32][128 B]
+  static constexpr int kZ32 = kZ + 32 * 128;            // 1 - z^2 fp32 [32][64]
+  static constexpr int kEnc = kZ32 + 32 * 64 * 4;       // the task's enc rows fp32 [32][64]
+  static constexpr int kNs = kEnc + 32 * 64 * 4;        // node scalars: c, wb, wy [3][32]
+  static constexpr int kP = kNs + 3 * 32 * 4;           // per-wave p image [4][32][128 B]
+  static constexpr int kRed = kP + 4 * 32 * 128;        // d pred partials [4][64]
+  static constexpr int kDe = kRed + 4 * 64 * 4;         // per-wave d enc partials [4][64 j][36]
+  static constexpr int kEnd = kDe + 4 * 64 * kDeP * 4;
+};
+
+__global__ void __launch_bounds__(256) joint_bwd_kernel(JointArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-  load_w(a, lds);
-  // two column buffers: [32 nodes][64] bf16 z image + node scalars (lse2, a)
-  unsigned char* zimg0 = lds + kVmaxJ * 128 + kVmaxJ * 4;
-  float* scal0 = (float*)(zimg0 + 2 * 32 * 128);
   const RnntArgs& r = a.r;
-  const int lane = threadIdx.x & 63, h = lane >> 5, g1 = (lane >> 4) & 1;
-  const int w = threadIdx.x >> 6;
-  const float* bias = (const float*)(lds + kVmaxJ * 128);
-  const int nvb = r.V / 32;
-  // wave w owns vocab blocks w, w + 8, ... (nvb <= 32: at most 4 each)
-  jf16 acc[4][2];
-  float dbs[4];
+  const int nvb = r.V / 32, VS = a.vs;
+  const int vh = blockIdx.x % VS, slot = blockIdx.x / VS, nslot = gridDim.x / VS;
+  const int vb0 = vh * kVbWg, nvw = min(kVbWg, nvb - vb0);   // this workgroup's vocab blocks
+  const int th = threadIdx.x, lane = th & 63, w = uniform(th >> 6), h = lane >> 5;
+  const int g1 = (lane >> 4) & 1;
+  unsigned char* wl = lds + BwdLds::kW;
+  float* bias_l = (float*)(lds + BwdLds::kBias);
+  unsigned char* zimg = lds + BwdLds::kZ;
+  float* z32 = (float*)(lds + BwdLds::kZ32);   // 1 - z^2
+  float* encl = (float*)(lds + BwdLds::kEnc);
+  float* ns_c = (float*)(lds + BwdLds::kNs);
+  float* ns_wb = ns_c + 32;
+  float* ns_wy = ns_c + 64;
+  unsigned char* pimg = lds + BwdLds::kP + w * 32 * 128;
+  float* red = (float*)(lds + BwdLds::kRed);
+  float* dep = (float*)(lds + BwdLds::kDe);              // [4][64][kDeP]
+  float* dew = dep + w * 64 * BwdLds::kDeP;
+  // this half of W and its bias (x log2 e)
+  for (int i = th; i < nvw * 32 * 8; i += 256) {
+    const int v = i >> 3, c = i & 7;
+    *(uint4*)(wl + wimg(v, c)) = *(const uint4*)(a.W + (int64_t)(vb0 * 32 + v) * kJ + 8 * c);
+  }
+  for (int i = th; i < nvw * 32; i += 256) bias_l[i] = a.bias[vb0 * 32 + i] * kLog2e;
+
+  jf16 acc[kVbW][2];
+  float dbs[kVbW];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
+  for (int k = 0; k < kVbW; ++k) {
     dbs[k] = 0.0f;
 #pragma unroll
     for (int jb = 0; jb < 2; ++jb)
 #pragma unroll
       for (int q = 0; q < 16; ++q) acc[k][jb][q] = 0.0f;
   }
-  const int64_t ncol = (int64_t)r.B * a.ntb * r.U1;
-  const int64_t c0 = (int64_t)blockIdx.x * ncol / gridDim.x, c1 = (int64_t)(blockIdx.x + 1) * ncol / gridDim.x;
-  auto valid_col = [&](int64_t col) {
-    const int b = (int)(col / ((int64_t)a.ntb * r.U1));
-    const int tb = (int)((col / r.U1) % a.ntb), u = (int)(col % r.U1);
-    return tb * 32 < clampr(r.flen[b], 0, r.T) && u <= clampr(r.llen[b], 0, r.Umax);
-  };
-  auto next_col = [&](int64_t col) {
-    while (col < c1 && !valid_col(col)) ++col;
-    return col;
-  };
-  // the column's inputs, loaded one column ahead: this thread's z element group and, for
-  // threads < 32, its node's scalars
-  const int zn = threadIdx.x >> 4, jq = threadIdx.x & 15;
-  float4 pe = make_float4(0, 0, 0, 0), pq = pe;
-  float pa = 0.0f, pl = 1e30f;
-  bool pok = false;
-  auto prefetch = [&](int64_t col) {
-    const int b = (int)(col / ((int64_t)a.ntb * r.U1));
-    const int tb = (int)((col / r.U1) % a.ntb), u = (int)(col % r.U1);
+  const int ntbp = VS * a.ntb;   // t-block rows of the d pred / g partial layouts
+  const int64_t ntask = (int64_t)r.B * a.ntb * a.nus;
+  const int zn = th >> 3, jg = th & 7;   // staging: node zn, j = 8 jg .. 8 jg + 7
+  for (int64_t task = slot; task < ntask; task += nslot) {
+    const int b = (int)(task / ((int64_t)a.ntb * a.nus));
+    const int tb = (int)((task / a.nus) % a.ntb), us = (int)(task % a.nus);
     const int Tb = clampr(r.flen[b], 0, r.T), Ub = clampr(r.llen[b], 0, r.Umax);
-    const int t = tb * 32 + zn;
-    pok = t < Tb;
-    pe = *(const float4*)(a.enc + ((int64_t)b * r.T + (pok ? t : Tb - 1)) * kJ + 4 * jq);
-    pq = *(const float4*)(a.pred + ((int64_t)b * r.U1 + u) * kJ + 4 * jq);
-    if (threadIdx.x < 32) {
-      const int tn = tb * 32 + threadIdx.x;
-      const bool okn = tn < Tb;
-      float wb = 0.0f, wy = 0.0f;
-      if (okn) node_weights(r, b, tn, u, Tb, Ub, wb, wy);
-      pa = wb + wy;
-      pl = okn ? r.ws.lse[((int64_t)b * r.T + tn) * r.U1 + u] * kLog2e : 1e30f;
+    // columns of this task (none when the t-block or the u-range lies outside the lattice: the
+    // task still writes its zero d enc partial)
+    const int ua = (int)((int64_t)us * r.U1 / a.nus);
+    const int ue = tb * 32 < Tb ? min((int)((int64_t)(us + 1) * r.U1 / a.nus), Ub + 1) : ua;
+    const bool zok = tb * 32 + zn < Tb;
+    lds_barrier();   // the previous task's reads of encl / d enc partials are done
+    if (ua < ue) {
+      const float* ep = a.enc + ((int64_t)b * r.T + (zok ? tb * 32 + zn : Tb - 1)) * kJ + 8 * jg;
+      *(float4*)(encl + zn * 64 + 8 * jg) = *(const float4*)ep;
+      *(float4*)(encl + zn * 64 + 8 * jg + 4) = *(const float4*)(ep + 4);
     }
-  };
-  int64_t col = next_col(c0);
-  if (col < c1) prefetch(col);
-  for (int it = 0; col < c1; ++it) {
-    unsigned char* zimg = zimg0 + (it & 1) * 32 * 128;
-    float* s_lse2 = scal0 + (it & 1) * 64;
-    float* s_a = s_lse2 + 32;
-    {   // stage the prefetched column into this iteration's buffer
-      js4 zz;
-      const float xs[4] = {pe.x + pq.x, pe.y + pq.y, pe.z + pq.z, pe.w + pq.w};
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        zz[e] = __builtin_bit_cast(short, (__bf16)(pok ? tanh_(xs[e]) : 0.0f));
-      *(js4*)(zimg + wimg(zn, jq >> 1) + 8 * (jq & 1)) = zz;
-      if (threadIdx.x < 32) {
-        s_a[threadIdx.x] = pa;
-        s_lse2[threadIdx.x] = pl;
+    // node loads and pred row of the first column (then one column ahead; barriers are LDS-only,
+    // so no load is drained before its use)
+    NodeLd nd{};
+    if (th < 32 && ua < ue) nd = node_load(r, b, tb * 32 + th, ua, Tb, Ub);
+    float4 pn0 = make_float4(0.f, 0.f, 0.f, 0.f), pn1 = pn0;
+    if (ua < ue) {
+      const float* pp = a.pred + ((int64_t)b * r.U1 + ua) * kJ + 8 * jg;
+      pn0 = *(const float4*)pp;
+      pn1 = *(const float4*)(pp + 4);
+    }
+    for (int u = ua; u < ue; ++u) {
+      lds_barrier();   // the previous column's LDS reads are done
+      if (u > ua && th < 64) {   // d pred of the previous column: the 4 wave partials
+        const float s = red[th] + red[64 + th] + red[128 + th] + red[192 + th];
+        a.d_pred[(((int64_t)b * ntbp + vh * a.ntb + tb) * r.U1 + u - 1) * kJ + th] = s;
       }
-    }
-    __syncthreads();   // buffer it&1 complete; every wave is past its reads of column it-2
-    const int64_t nxt = next_col(col + 1);
-    if (nxt < c1) prefetch(nxt);   // in flight during this column's MFMAs
-    // node scalars of this lane's 16 accumulator rows: node = (q&3) + 8(q>>2) + 4h
-    float l2[16], an[16];
+      {   // stage column u: z (bf16 image + fp32), node scalars
+        const float4 e0 = *(const float4*)(encl + zn * 64 + 8 * jg);
+        const float4 e1 = *(const float4*)(encl + zn * 64 + 8 * jg + 4);
+        const float xs[8] = {e0.x + pn0.x, e0.y + pn0.y, e0.z + pn0.z, e0.w + pn0.w,
+                             e1.x + pn1.x, e1.y + pn1.y, e1.z + pn1.z, e1.w + pn1.w};
+        if (u + 1 < ue) {
+          const float* pp = a.pred + ((int64_t)b * r.U1 + u + 1) * kJ + 8 * jg;
+          pn0 = *(const float4*)pp;
+          pn1 = *(const float4*)(pp + 4);
+        }
+        float zf[8];
+        jbf8 zb;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const float4 lv = *(const float4*)(s_lse2 + 8 * q + 4 * h);
-      const float4 av = *(const float4*)(s_a + 8 * q + 4 * h);
-      l2[4 * q] = lv.x; l2[4 * q + 1] = lv.y; l2[4 * q + 2] = lv.z; l2[4 * q + 3] = lv.w;
-      an[4 * q] = av.x; an[4 * q + 1] = av.y; an[4 * q + 2] = av.z; an[4 * q + 3] = av.w;
-    }
-    // Z is the A operand of the logits (node on the row, j = 16 s + 8 h + e) and the B operand of
-    // dW (k = node in the accumulator's row order, column j): one image, row and tr reads,
-    // re-read per vocab block (LDS reads are cheaper than the registers to hold them)
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int vb = w + 8 * k;
-      if (vb >= nvb) break;
-      const int v = vb * 32 + (lane & 31);
-      jf16 x;
-#pragma unroll
-      for (int q = 0; q < 16; ++q) x[q] = 0.0f;
-#pragma unroll
-      for (int s = 0; s < 4; ++s)
-        x = mfma32(lds_b128(zimg, wimg(lane & 31, 2 * s + h)), lds_b128(lds, wimg(v, 2 * s + h)), x);
-      const float bl = bias[v] * kLog2e;
-      float p[16], ps = 0.0f;
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        p[q] = an[q] * exp2_(fmaf(x[q], kLog2e, bl - l2[q]));
-        ps += p[q];
-      }
-      dbs[k] += ps;
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        const jbf8 xf = pack8(p + 8 * s2);
-#pragma unroll
-        for (int jb = 0; jb < 2; ++jb) {
-          const jbf8 zt = cat8(tr_rd(zimg, 16 * s2 + 4 * h, jb * 32 + 16 * g1, lane),
-                               tr_rd(zimg, 16 * s2 + 8 + 4 * h, jb * 32 + 16 * g1, lane));
-          acc[k][jb] = mfma32(xf, zt, acc[k][jb]);
+        for (int e = 0; e < 8; ++e) {
+          zf[e] = zok ? tanh_(xs[e]) : 0.0f;
+          zb[e] = (__bf16)zf[e];
+        }
+        *(jbf8*)(zimg + wimg(zn, jg)) = zb;
+        // tanh' = 1 - z^2, once per element (every wave scales its dZ partial by it)
+        *(float4*)(z32 + zn * 64 + 8 * jg) = make_float4(1.0f - zf[0] * zf[0], 1.0f - zf[1] * zf[1],
+                                                         1.0f - zf[2] * zf[2], 1.0f - zf[3] * zf[3]);
+        *(float4*)(z32 + zn * 64 + 8 * jg + 4) = make_float4(1.0f - zf[4] * zf[4], 1.0f - zf[5] * zf[5],
+                                                             1.0f - zf[6] * zf[6], 1.0f - zf[7] * zf[7]);
+        if (th < 32) {
+          float wb, wy, l2;
+          node_finish(nd, tb * 32 + th, u, Tb, Ub, wb, wy, l2);
+          const float an = wb + wy;
+          // p = a exp2(x log2e + b log2e - l2) = exp2(x log2e + b log2e + c), c = log2 a - l2
+          ns_c[th] = an > 0.0f ? log2_(an) - l2 : -1e30f;
+          ns_wb[th] = wb;
+          ns_wy[th] = wy;
+          if (u + 1 < ue) nd = node_load(r, b, tb * 32 + th, u + 1, Tb, Ub);   // in flight
         }
       }
-    }
-    col = nxt;
-  }
-  // acc[k][jb][q] = dW[v = vb*32 + (q&3) + 8(q>>2) + 4h][j = jb*32 + (lane&31)]
-  float* dw = a.dW + (int64_t)blockIdx.x * r.V * kJ;
+      lds_barrier();
+      // column operands: z rows (logits A operand), z^T (dW B operand), node terms per register
+      jbf8 zA[4], zT[2][2];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int vb = w + 8 * k;
-    if (vb >= nvb) break;
+      for (int s = 0; s < 4; ++s) zA[s] = lds_b128(zimg, wimg(lane & 31, 2 * s + h));
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int jb = 0; jb < 2; ++jb)
+          zT[s2][jb] = cat8(tr_rd(zimg, 16 * s2 + 4 * h, jb * 32 + 16 * g1, lane),
+                            tr_rd(zimg, 16 * s2 + 8 + 4 * h, jb * 32 + 16 * g1, lane));
+      float cq[16];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 cv = *(const float4*)(ns_c + 8 * q + 4 * h);
+        cq[4 * q] = cv.x; cq[4 * q + 1] = cv.y; cq[4 * q + 2] = cv.z; cq[4 * q + 3] = cv.w;
+      }
+      jf16 Y[2];
+#pragma unroll
+      for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) Y[jb][q] = 0.0f;
+      const int yl = u < Ub ? label_at(r, b, u) : r.blank;
+#pragma unroll
+      for (int k = 0; k < kVbW; ++k) {
+        // every wave runs all kVbW blocks (no early exit: its PHIs cost a copy of Y); a block past
+        // the vocabulary reads row block 0 and gets p = 0
+        const int lvb = w + 4 * k;
+        const bool vok = lvb < nvw;
+        const int lvc = vok ? lvb : 0;   // (the W rows read for a block past the vocabulary)
+        const int vl = lvc * 32 + (lane & 31);
+        jf16 x;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) x[q] = 0.0f;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) x = mfma32(zA[s], lds_b128(wl, wimg(vl, 2 * s + h)), x);
+        const float bl = vok ? bias_l[vl] : -1e30f;
+        float p[16], ps = 0.0f;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) p[q] = exp2_(fmaf(x[q], kLog2e, bl + cq[q]));
+        // the sparse arcs of the gathered lattice: dlogits[n][blank] -= wb_n, dlogits[n][y_u] -=
+        // wy_n (one or two blocks per column), so dW, d bias and dZ all take them from p
+        const int vg0 = (vb0 + lvb) * 32;
+#if SC_JOINT_BF
+        {   // branch-free (A/B: one scheduling region per column)
+#else
+        if (vok && ((unsigned)(r.blank - vg0) < 32u || (unsigned)(yl - vg0) < 32u)) {
+#endif
+          const int v = vg0 + (lane & 31);
+          const float mb = v == r.blank ? 1.0f : 0.0f, my = v == yl ? 1.0f : 0.0f;
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const float4 bw = *(const float4*)(ns_wb + 8 * g + 4 * h);
+            const float4 yw = *(const float4*)(ns_wy + 8 * g + 4 * h);
+            p[4 * g] -= mb * bw.x + my * yw.x;
+            p[4 * g + 1] -= mb * bw.y + my * yw.y;
+            p[4 * g + 2] -= mb * bw.z + my * yw.z;
+            p[4 * g + 3] -= mb * bw.w + my * yw.w;
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < 16; ++q) ps += p[q];
+        dbs[k] += ps;
+        jbf8 pf[2];
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          pf[s2] = pack8(p + 8 * s2);
+#pragma unroll
+          for (int jb = 0; jb < 2; ++jb) acc[k][jb] = mfma32(pf[s2], zT[s2][jb], acc[k][jb]);
+        }
+        // p^T through the wave's image: registers 4g..4g+3 are rows n = 8g + 4h .. +3 of column
+        // v = lane & 31 -> 8 bytes at [v][8g + 4h] (whole packed dwords: element-wise bf16
+        // extraction from the vector miscompiles into a broadcast of one element)
+        typedef int ji2 __attribute__((ext_vector_type(2)));
+        typedef int ji4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const ji4 d = __builtin_bit_cast(ji4, pf[g >> 1]);
+          *(ji2*)(pimg + wimg(lane & 31, g) + 8 * h) = ji2{d[2 * (g & 1)], d[2 * (g & 1) + 1]};
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const jbf8 pt = cat8(tr_rd(pimg, 16 * s2 + 4 * h, 16 * g1, lane),
+                               tr_rd(pimg, 16 * s2 + 8 + 4 * h, 16 * g1, lane));
+#pragma unroll
+          for (int jb = 0; jb < 2; ++jb) {
+            const jbf8 wt = cat8(tr_rd(wl, lvc * 32 + 16 * s2 + 4 * h, jb * 32 + 16 * g1, lane),
+                                 tr_rd(wl, lvc * 32 + 16 * s2 + 8 + 4 * h, jb * 32 + 16 * g1, lane));
+            Y[jb] = mfma32(pt, wt, Y[jb]);
+          }
+        }
+#if SC_JOINT_SB
+        __builtin_amdgcn_sched_barrier(0);   // one vocab block's live state at a time
+#endif
+      }
+      // Y[jb][q] = this wave's part of dZ[node n_q][j = jb*32 + (lane & 31)],
+      // n_q = (q & 3) + 8 (q >> 2) + 4 h: d pre = dZ (1 - z^2) into the wave's d enc partial
+      // (LDS, [j][n]) and d pred (over n)
+#pragma unroll
+      for (int jb = 0; jb < 2; ++jb) {
+        const int j = jb * 32 + (lane & 31);
+        float sp = 0.0f;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {   // nodes 8g + 4h .. +3 = registers 4g .. 4g+3
+          float* de4 = dew + j * BwdLds::kDeP + 8 * g + 4 * h;
+          float4 dv = u > ua ? *(const float4*)de4 : make_float4(0.f, 0.f, 0.f, 0.f);
+          float o[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int q = 4 * g + e, n = 8 * g + 4 * h + e;
+            o[e] = Y[jb][q] * z32[n * 64 + j];
+            sp += o[e];
+          }
+          dv.x += o[0];
+          dv.y += o[1];
+          dv.z += o[2];
+          dv.w += o[3];
+          *(float4*)de4 = dv;
+        }
+        sp += __shfl_xor(sp, 32);
+        if (h == 0) red[w * 64 + j] = sp;
+      }
+    }
+    lds_barrier();
+    if (ua < ue && th < 64) {
+      const float s = red[th] + red[64 + th] + red[128 + th] + red[192 + th];
+      a.d_pred[(((int64_t)b * ntbp + vh * a.ntb + tb) * r.U1 + ue - 1) * kJ + th] = s;
+    }
+    // d enc of the task: the 4 waves' partials, 8 values per thread, j fastest (coalesced)
+    float* dst = a.d_enc + ((int64_t)(vh * a.nus + us) * r.B + b) * r.T * kJ;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int e = th + 256 * i, n = e >> 6, j = e & 63;
+      const int tq = tb * 32 + n;
+      float s = 0.0f;
+      if (ua < ue) {
+#pragma unroll
+        for (int ww = 0; ww < 4; ++ww) s += dep[(ww * 64 + j) * BwdLds::kDeP + n];
+      }
+      if (tq < r.T) dst[(int64_t)tq * kJ + j] = s;
+    }
+  }
+  // acc[k][jb][q] = dW[v = (vb0 + w + 4k) * 32 + (q&3) + 8(q>>2) + 4h][j = jb*32 + (lane&31)]
+  float* dw = a.dW + (int64_t)slot * r.V * kJ;
+#pragma unroll
+  for (int k = 0; k < kVbW; ++k) {
+    const int lvb = w + 4 * k;
+    if (lvb >= nvw) continue;
+    const int vbg = vb0 + lvb;
 #pragma unroll
     for (int jb = 0; jb < 2; ++jb)
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
-        const int v = vb * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
+        const int v = vbg * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
         dw[(int64_t)v * kJ + jb * 32 + (lane & 31)] = acc[k][jb][q];
       }
     const float tot = dbs[k] + __shfl_xor(dbs[k], 32);
-    if (h == 0) a.db[(int64_t)blockIdx.x * r.V + vb * 32 + (lane & 31)] = tot;
+    if (h == 0) a.db[(int64_t)slot * r.V + vbg * 32 + (lane & 31)] = tot;
   }
 }
 
@@ -1036,9 +1112,10 @@ bool joint_lds_attr(K kern, size_t bytes) {
   return hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                              (int)bytes) == hipSuccess;
 }
-size_t joint_lds_dz() { return joint_lds_fwd() + 8 * 64 * 4; }
-size_t joint_lds_dw() { return joint_lds_fwd() + 2 * (32 * 128 + 2 * 32 * 4); }
+size_t joint_lds_bwd() { return (size_t)BwdLds::kEnd; }
 
+// real t-blocks / u-splits of the task decomposition (the exported geometry multiplies both by
+// the vocab split, the leading partial dimension of d enc and the t-block rows of d pred)
 void joint_geometry(int B, int T, int Umax, int* ntb, int* nus, int* S) {
   *ntb = (T + 31) / 32;
   // d enc is accumulated over u in registers; split u only as far as needed to give every SIMD
@@ -1049,6 +1126,7 @@ void joint_geometry(int B, int T, int Umax, int* ntb, int* nus, int* S) {
   *nus = n;
   *S = 256;
 }
+int joint_vsplit(int V) { return (V / 32 + kVbWg - 1) / kVbWg; }
 
 }  // namespace
 
@@ -1156,17 +1234,23 @@ JointArgs joint_args(const float* enc, const float* pred, const void* W, const f
   j.W = (const __bf16*)W;
   j.bias = bias;
   joint_geometry(B, T, Umax, &j.ntb, &j.nus, &j.S);
-  j.d_enc = j.d_pred = j.g_blank = j.g_label = j.s_bl = j.dW = j.db = nullptr;
+  j.vs = joint_vsplit(V);
+  j.S /= j.vs;
+  j.d_enc = j.d_pred = j.dW = j.db = nullptr;
   return j;
 }
 }  // namespace
 }  // namespace sc
 
-extern "C" int sc_rnnt_joint_geometry(int B, int T, int max_labels, int* t_blocks, int* u_splits,
-                                      int* slices) {
+extern "C" int sc_rnnt_joint_geometry(int B, int T, int max_labels, int V, int* t_blocks,
+                                      int* u_splits, int* slices) {
   clear_error();
   SC_REQUIRE(t_blocks && u_splits && slices, "sc_rnnt_joint_geometry: null pointer");
   joint_geometry(B, T, max_labels, t_blocks, u_splits, slices);
+  const int vs = joint_vsplit(V);
+  *t_blocks *= vs;
+  *u_splits *= vs;
+  *slices /= vs;
   return 0;
 }
 
@@ -1195,30 +1279,23 @@ extern "C" int sc_rnnt_joint_bwd(const float* enc, const float* pred, const void
                                  int B, int T, int max_labels, int V, int J, const int64_t* labels,
                                  int64_t label_stride, const int64_t* frames_lengths,
                                  const int64_t* labels_lengths, int blank, const float* scale,
-                                 float* d_enc, float* d_pred, float* g_blank, float* g_label,
-                                 float* s_bl, float* dW, float* db, const void* workspace,
-                                 size_t workspace_bytes, void* stream) {
+                                 float* d_enc, float* d_pred, float* dW, float* db,
+                                 const void* workspace, size_t workspace_bytes, void* stream) {
   clear_error();
   int rc = joint_check(enc, pred, W, bias, B, T, max_labels, V, J, labels, frames_lengths,
                        labels_lengths, blank, workspace, workspace_bytes, "sc_rnnt_joint_bwd");
   if (rc) return rc;
   if (B == 0 || T == 0) return 0;
-  SC_REQUIRE(scale && d_enc && d_pred && g_blank && g_label && s_bl && dW && db,
-             "sc_rnnt_joint_bwd: null output");
+  SC_REQUIRE(scale && d_enc && d_pred && dW && db, "sc_rnnt_joint_bwd: null output");
   JointArgs j = joint_args(enc, pred, W, bias, B, T, max_labels, V, labels, label_stride,
                            frames_lengths, labels_lengths, blank, nullptr, workspace, scale);
   j.d_enc = d_enc;
   j.d_pred = d_pred;
-  j.g_blank = g_blank;
-  j.g_label = g_label;
-  j.s_bl = s_bl;
   j.dW = dW;
   j.db = db;
-  static const bool ok1 = joint_lds_attr(joint_dz_kernel, joint_lds_dz());
-  static const bool ok2 = joint_lds_attr(joint_dw_kernel, joint_lds_dw());
-  SC_REQUIRE(ok1 && ok2, "sc_rnnt_joint_bwd: LDS attribute");
+  static const bool ok = joint_lds_attr(joint_bwd_kernel, joint_lds_bwd());
+  SC_REQUIRE(ok, "sc_rnnt_joint_bwd: LDS attribute");
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(joint_dz_kernel, dim3(256), dim3(512), joint_lds_dz(), st, j);
-  hipLaunchKernelGGL(joint_dw_kernel, dim3(j.S), dim3(512), joint_lds_dw(), st, j);
+  hipLaunchKernelGGL(joint_bwd_kernel, dim3(j.S * j.vs), dim3(256), joint_lds_bwd(), st, j);
   return launch_status("sc_rnnt_joint_bwd");
 }

@@ -794,14 +794,12 @@ class RNNTJointFn(torch.autograd.Function):
                     None, None, None, None)
         lib = _lib.load()
         geo = [ctypes_int() for _ in range(3)]
-        check(lib.sc_rnnt_joint_geometry(B, T, Umax, *[_addr(g) for g in geo]), "sc_rnnt_joint_geometry")
+        check(lib.sc_rnnt_joint_geometry(B, T, Umax, V, *[_addr(g) for g in geo]),
+              "sc_rnnt_joint_geometry")
         ntb, nus, S = (g.value for g in geo)
         f32 = dict(dtype=torch.float32, device=dev)
         d_enc = torch.empty(nus, B, T, J, **f32)
         d_pred = torch.zeros(B, ntb, U1, J, **f32)
-        g_blank = torch.zeros(B, ntb, U1, J, **f32)
-        g_label = torch.zeros(B, ntb, U1, J, **f32)
-        s_bl = torch.zeros(B, ntb, U1, 2, **f32)
         dW = torch.empty(S, V, J, **f32)
         db = torch.empty(S, V, **f32)
         scale = grad_nll.to(torch.float32).contiguous()
@@ -809,22 +807,12 @@ class RNNTJointFn(torch.autograd.Function):
             rc = lib.sc_rnnt_joint_bwd(ptr(encc), ptr(predc), ptr(wb), ptr(bf), B, T, Umax, V, J,
                                        ptr(labels), labels.stride(0) if Umax else 0, ptr(flen),
                                        ptr(llen), blank, ptr(scale), ptr(d_enc), ptr(d_pred),
-                                       ptr(g_blank), ptr(g_label), ptr(s_bl), ptr(dW), ptr(db),
-                                       ptr(ws), wsb, stream_of(encc))
+                                       ptr(dW), ptr(db), ptr(ws), wsb, stream_of(encc))
         check(rc, "sc_rnnt_joint_bwd")
-        # fixed-order sums of the partials, then the sparse blank / label arcs of dW and d bias:
-        # dlogits_n = a_n softmax_n - w_blank,n e_blank - w_label,n e_{y[b,u]}
+        # fixed-order sums of the partials (the kernel's dlogits include the sparse blank / label
+        # arcs of the gathered lattice)
         dWt = colsum(dW.view(S, V * J)).view(V, J)
         dbt = colsum(db)
-        gl = g_label.sum(1)[:, :Umax].reshape(-1, J)                 # [B*Umax, J]
-        sl = s_bl.sum(1)                                             # [B, U1, 2]
-        onehot = torch.nn.functional.one_hot(labels.clamp(0, V - 1), V).to(torch.float32)
-        onehot = onehot.view(-1, V)                                  # [B*Umax, V]
-        dWt[blank] -= g_blank.sum((0, 1, 2))
-        dbt[blank] -= sl[..., 0].sum()
-        if Umax:
-            dWt -= onehot.t() @ gl
-            dbt -= onehot.t() @ sl[:, :Umax, 1].reshape(-1)
         return (d_enc.sum(0).to(edt), d_pred.sum(1).to(pdt), dWt.to(wdt), dbt.to(bdt),
                 None, None, None, None)
 
