@@ -296,22 +296,23 @@ class LucyCellFn(torch.autograd.Function):
         # MFMA kernel's K stage (the weight gets the same zero columns)
         kp = Din + (-Din) % 64
         tn = USE_TN and x2d.is_cuda and cdt == torch.bfloat16 and (7 * D) % 256 == 0
-        xc = pad_cols(x2d, kp, cdt) if tn and kp != Din else x2d.to(cdt)
+        xc = x2d.to(cdt)
+        # the forward GEMM's copy of x with zero columns up to kp; the weight gradient keeps the
+        # unpadded xc (its GEMM would otherwise sum 48 extra zero columns)
+        xg = pad_cols(x2d, kp, cdt) if tn and kp != Din else xc
         # step-blocked gates: weight rows permuted to (column block, gate, unit) order so each
         # step's 7 x 64 gates of a column block are one contiguous 896-byte run for the scan
         wc = step_blocked_rows(w, D, dtype=cdt) if blocked else w.to(cdt)
-        if tn and kp != Din:
-            wc = pad_cols(wc, kp, cdt)
+        wg = pad_cols(wc, kp, cdt) if tn and kp != Din else wc
         bias = b.detach().to(torch.float32).contiguous()
         with _timed("gate_gemm_fwd", xc, 0):
-            gates = proj_fwd(xc, wc)
+            gates = proj_fwd(xg, wg)
         gates = gates.view(B, T, D // 64, 7, 64) if blocked else gates.view(B, T, 7, D)
         need = any(ctx.needs_input_grad)
         gates, out, s_out, ckpt, h_out = _scan_fwd(gates, h0, s0, need, bias, want_h=True)
         if need:
             ctx.save_for_backward(xc, wc, gates, ckpt, bias)
             ctx.dtypes = (x2d.dtype, w.dtype, h0.dtype, s0.dtype)
-            ctx.din = Din
             ctx.blocked = blocked
         return out, s_out, h_out
 
@@ -329,17 +330,16 @@ class LucyCellFn(torch.autograd.Function):
         dgates, dh0, ds0, dbias = _scan_bwd(gates, ckpt, dout, ds_last, ctx.needs_input_grad[2],
                                             bias)
         dg2 = dgates.view(xc.shape[0], -1)
-        din = ctx.din
         dx = None
         if ctx.needs_input_grad[0]:
             with _timed("gate_gemm_dgrad", dg2, 0):
-                dx = proj_dgrad(dg2, wc[:, :din])
+                dx = proj_dgrad(dg2, wc)
             dx = dx.to(xdt)
         dw = None
         if ctx.needs_input_grad[1]:
             with _timed("gate_gemm_wgrad", dg2, 0):
                 dw = wgrad_splitk(dg2, xc, blocked_d=(dg2.shape[1] // 7) if ctx.blocked else 0)
-            dw = (dw[:, :din] if dw.shape[1] != din else dw).to(wdt)
+            dw = dw.to(wdt)
         db = colsum(dbias.view(dbias.shape[0], -1)).to(wdt) if dbias is not None else None
         return dx, dw, db, dh0.to(hdt), ds0.to(sdt), None, None, None
 
