@@ -292,6 +292,37 @@ int sc_gemm_wgrad_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, f
 int sc_gemm_tn_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc,
                     int M, int N, int K, int tile_m, void* stream);
 
+/* ---------------------------------------------------------------- xLSTM block glue ------ */
+
+/*
+ * The xLSTM-large block's elementwise / row-norm glue (C4 encoder, model.py:214-229; structure
+ * as transformers' modeling_xlstm.py:870-1205), one HBM pass each, bf16 tensors, fp32 math,
+ * bf16 roundings where the torch module rounds.  Weight gradients come back as fp32 partial rows
+ * [sc_xlstm_part_rows(rows)][D] for a fixed-order sum (sc_colsum).
+ *   RMSNorm (force_float32_reductions): y = bf16(bf16(x rsqrt(mean x^2 + eps)) w), x/y [rows][D]
+ *     contiguous, D in {256, 512, 768, 1024}; rstd fp32 [rows] saved for the backward.
+ *   gated head LayerNorm: out[m][n DH + e] = bf16(bf16(sigmoid(o[m][n DH + e])) *
+ *     bf16(LN(h[b][n][t][:])[e]) * w[n DH + e]), m = b T + t: MultiHeadLayerNorm of the mLSTM
+ *     cell output in the cell's [B][NH][T][DH] layout times sigmoid of the output gate (a
+ *     row-strided view, ldo); NH <= 4, DH in {64, 128, 192, 256}; mean/rstd fp32 [M][NH].
+ *     Backward: dh in the cell layout, d o into a [M][lddo] view (the fused projection's
+ *     gradient).
+ *   SwiGLU: y = bf16(bf16(silu(g)) u) for a = [g | u] rows of 2F; the backward writes [dg | du].
+ */
+int sc_xlstm_part_rows(int64_t rows);
+int sc_rmsnorm_fwd(const void* x, const float* w, void* y, float* rstd, int64_t rows, int D,
+                   float eps, void* stream);
+int sc_rmsnorm_bwd(const void* x, const void* dy, const float* w, const float* rstd, void* dx,
+                   float* part, int64_t rows, int D, void* stream);
+int sc_mhln_gate_fwd(const void* h, const void* o, int64_t ldo, const float* w, void* out,
+                     float* mean, float* rstd, int B, int T, int NH, int DH, float eps,
+                     void* stream);
+int sc_mhln_gate_bwd(const void* h, const void* o, int64_t ldo, const float* w, const float* mean,
+                     const float* rstd, const void* dy, int64_t ldy, void* dh, void* dgo,
+                     int64_t lddo, float* part, int B, int T, int NH, int DH, void* stream);
+int sc_swiglu_fwd(const void* a, void* y, int64_t rows, int F, void* stream);
+int sc_swiglu_bwd(const void* a, const void* dy, void* da, int64_t rows, int F, void* stream);
+
 /* ---------------------------------------------------------------- feature frontend ------ */
 
 /* Frames of a row of n_samples (center=False): 1 + (n - 400) / 160, or 0 below 400 samples. */

@@ -942,3 +942,132 @@ def mlstm_chunkwise(query, key, value, igate, fgate, c_initial=None, n_initial=N
         raise ValueError("the HIP mLSTM kernels use chunk_size 64")
     h, c, n, m = MLSTMFn.apply(query, key, value, igate, fgate, c_initial, n_initial, m_initial, eps)
     return (h, (c, n, m)) if return_last_states else h
+
+
+# ----------------------------------------------------------------------------- xLSTM glue ----
+def _part_sum(part):
+    """fixed-order fp32 sum of the [P, D] weight-gradient partial rows (sc_colsum)."""
+    return colsum(part)
+
+
+def xlstm_glue_supported(x, D):
+    return x.is_cuda and x.dtype == torch.bfloat16 and D in (256, 512, 768, 1024)
+
+
+class RMSNormFn(torch.autograd.Function):
+    """xLSTM RMSNorm (force_float32_reductions; transformers modeling_xlstm.py RMSNorm) in one pass:
+    y = bf16(bf16(x rsqrt(mean x^2 + eps)) w), the value autocast hands the next bf16 GEMM."""
+
+    @staticmethod
+    def forward(ctx, x, w, eps):
+        require_device(x)
+        D = x.shape[-1]
+        x2 = x.reshape(-1, D)
+        if not x2.is_contiguous():
+            x2 = x2.contiguous()
+        rows = x2.shape[0]
+        wf = w.detach().float().contiguous()
+        y = torch.empty_like(x2)
+        rstd = torch.empty(rows, dtype=torch.float32, device=x.device)
+        check(_lib.load().sc_rmsnorm_fwd(ptr(x2), ptr(wf), ptr(y), ptr(rstd), rows, D, float(eps),
+                                         stream_of(x2)), "sc_rmsnorm_fwd")
+        ctx.save_for_backward(x2, wf, rstd)
+        ctx.wdt = w.dtype
+        return y.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, wf, rstd = ctx.saved_tensors
+        rows, D = x2.shape
+        dy2 = dy.reshape(rows, D).to(torch.bfloat16).contiguous()
+        lib = _lib.load()
+        dx = torch.empty_like(x2)
+        part = torch.empty(lib.sc_xlstm_part_rows(rows), D, dtype=torch.float32, device=x2.device)
+        check(lib.sc_rmsnorm_bwd(ptr(x2), ptr(dy2), ptr(wf), ptr(rstd), ptr(dx), ptr(part), rows, D,
+                                 stream_of(x2)), "sc_rmsnorm_bwd")
+        return dx.view(dy.shape), _part_sum(part).to(ctx.wdt), None
+
+
+def rms_norm(x, w, eps):
+    return RMSNormFn.apply(x, w, eps)
+
+
+class GatedHeadNormFn(torch.autograd.Function):
+    """bf16(sigmoid(o)) * MultiHeadLayerNorm(h) of the mLSTM layer (modeling_xlstm.py mLSTMLayer:
+    out_proj(sigmoid(o) * multihead_norm(h))) in one pass: h [B,NH,T,DH] the cell output in the
+    cell's own layout, o [B,T,NH*DH] a row-strided view of the fused projection; out bf16
+    [B,T,NH*DH].  Backward: dh [B,NH,T,DH], do [B,T,NH*DH], d weight."""
+
+    @staticmethod
+    def forward(ctx, h, o, w, eps):
+        require_device(h, o)
+        B, NH, T, DH = h.shape
+        h = h.contiguous()
+        if o.stride(2) != 1 or o.stride(0) != T * o.stride(1) or o.stride(1) % 4:
+            o = o.contiguous()
+        wf = w.detach().float().contiguous()
+        out = torch.empty(B, T, NH * DH, dtype=torch.bfloat16, device=h.device)
+        mean = torch.empty(B * T, NH, dtype=torch.float32, device=h.device)
+        rstd = torch.empty_like(mean)
+        check(_lib.load().sc_mhln_gate_fwd(ptr(h), ptr(o), o.stride(1), ptr(wf), ptr(out), ptr(mean),
+                                           ptr(rstd), B, T, NH, DH, float(eps), stream_of(h)),
+              "sc_mhln_gate_fwd")
+        ctx.save_for_backward(h, o, wf, mean, rstd)
+        ctx.wdt = w.dtype
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        h, o, wf, mean, rstd = ctx.saved_tensors
+        B, NH, T, DH = h.shape
+        dy = dout.to(torch.bfloat16)
+        if dy.stride(2) != 1 or dy.stride(0) != T * dy.stride(1) or dy.stride(1) % 4:
+            dy = dy.contiguous()
+        lib = _lib.load()
+        dh = torch.empty_like(h)
+        do = torch.empty(B, T, NH * DH, dtype=torch.bfloat16, device=h.device)
+        part = torch.empty(lib.sc_xlstm_part_rows(B * T), NH * DH, dtype=torch.float32,
+                           device=h.device)
+        check(lib.sc_mhln_gate_bwd(ptr(h), ptr(o), o.stride(1), ptr(wf), ptr(mean), ptr(rstd), ptr(dy),
+                                   dy.stride(1), ptr(dh), ptr(do), do.stride(1), ptr(part), B, T, NH,
+                                   DH, stream_of(h)), "sc_mhln_gate_bwd")
+        return dh, do, _part_sum(part).to(ctx.wdt), None
+
+
+def gated_head_norm(h, o, w, eps):
+    return GatedHeadNormFn.apply(h, o, w, eps)
+
+
+def gated_head_norm_supported(h):
+    return (h.is_cuda and h.dtype == torch.bfloat16 and h.dim() == 4 and h.shape[1] <= 4
+            and h.shape[3] in (64, 128, 192, 256))
+
+
+class SwiGLUFn(torch.autograd.Function):
+    """bf16(silu(g)) * u for a = [g | u] (the fused up-projection of the xLSTM FFN); the
+    backward returns ONE [dg | du] tensor (no concatenation of two slice gradients)."""
+
+    @staticmethod
+    def forward(ctx, a):
+        require_device(a)
+        F2 = a.shape[-1]
+        a2 = a.reshape(-1, F2).contiguous()
+        y = torch.empty(a2.shape[0], F2 // 2, dtype=torch.bfloat16, device=a.device)
+        check(_lib.load().sc_swiglu_fwd(ptr(a2), ptr(y), a2.shape[0], F2 // 2, stream_of(a2)),
+              "sc_swiglu_fwd")
+        ctx.save_for_backward(a2)
+        return y.view(*a.shape[:-1], F2 // 2)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (a2,) = ctx.saved_tensors
+        rows, F2 = a2.shape
+        dy2 = dy.reshape(rows, F2 // 2).to(torch.bfloat16).contiguous()
+        da = torch.empty_like(a2)
+        check(_lib.load().sc_swiglu_bwd(ptr(a2), ptr(dy2), ptr(da), rows, F2 // 2, stream_of(a2)),
+              "sc_swiglu_bwd")
+        return da.view(*dy.shape[:-1], F2)
+
+
+def swiglu(a):
+    return SwiGLUFn.apply(a)

@@ -25,6 +25,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from . import ops
 from .ops import mlstm_chunkwise
 
 
@@ -73,6 +74,11 @@ class RMSNorm(nn.Module):
         self.bias = nn.Parameter(torch.zeros(num_features)) if use_bias else None
 
     def forward(self, x):
+        if (self.bias is None and self.force_float32_reductions
+                and ops.xlstm_glue_supported(x, x.shape[-1])):
+            # one HIP pass (csrc/xlstm_glue.hip), same roundings; bf16 out = what autocast would
+            # hand the next GEMM
+            return ops.rms_norm(x, self.weight, self.eps)
         dt = x.dtype
         y = x.float() if self.force_float32_reductions else x
         y = (y * torch.rsqrt(y.pow(2).mean(-1, keepdim=True) + self.eps)).to(dt)
@@ -113,7 +119,10 @@ class FeedForward(nn.Module):
         b = None
         if self.proj_up.bias is not None:
             b = torch.cat([self.proj_up_gate.bias, self.proj_up.bias])
-        g, u = F.linear(x, w, b).split([up, up], -1)
+        a = F.linear(x, w, b)
+        if a.is_cuda and a.dtype == torch.bfloat16 and up % 4 == 0:
+            return self.proj_down(ops.swiglu(a))   # one HIP pass, one [dg | du] gradient
+        g, u = a.split([up, up], -1)
         return self.proj_down(F.silu(g) * u)
 
 
@@ -161,6 +170,11 @@ class mLSTMLayer(nn.Module):
         c0, n0, m0 = (None, None, None) if state is None else state
         h, new_state = mlstm_chunkwise(q, k, v, ig, fg, c0, n0, m0, return_last_states=True,
                                        eps=self.cfg.eps)
+        mh = self.multihead_norm
+        if (mh.bias is None and mh.force_float32_reductions and o.dtype == torch.bfloat16
+                and ops.gated_head_norm_supported(h)):
+            # sigmoid(o) * MultiHeadLayerNorm(h) in one HIP pass on the cell's [B,NH,T,DH] layout
+            return self.out_proj(ops.gated_head_norm(h, o, mh.weight, mh.eps)), new_state
         h = self.multihead_norm(h.transpose(1, 2))
         return self.out_proj(torch.sigmoid(o) * h), new_state
 

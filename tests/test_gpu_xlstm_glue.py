@@ -1,0 +1,122 @@
+"""GPU parity of the fused xLSTM block glue (csrc/xlstm_glue.hip) against the torch modules' own
+computation under bf16 autocast (statecatcher_amd/xlstm.py's torch path, the restatement of
+transformers' modeling_xlstm.py RMSNorm / MultiHeadLayerNorm / FFN).
+
+The fused kernels round to bf16 at the same points as the torch chain, so outputs agree to a
+bf16 ulp (2^-8 of the value, from reduction order); gradients to 2e-2 in norm (the torch
+backward rounds some intermediates to bf16 that the kernels keep in fp32) and weight gradients
+(fp32 sums over all rows) to 1e-2 in norm."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0") if torch.cuda.is_available() else None
+
+
+def ops():
+    from statecatcher_amd import ops as o
+    return o
+
+
+def rel(a, b):
+    a, b = a.detach().double(), b.detach().double()
+    return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
+def ulp_close(a, b):
+    err = (a.float() - b.float()).abs()
+    return bool((err <= b.float().abs() * 2.0 ** -7 + 1e-3 * b.float().abs().max()).all())
+
+
+@pytest.mark.parametrize("D,rows", [(768, 4000), (512, 33), (1024, 7)])
+def test_rmsnorm_vs_torch(D, rows):
+    g = torch.Generator(device=DEV).manual_seed(D + rows)
+    x = (torch.randn(rows, D, device=DEV, generator=g) * 2).to(torch.bfloat16)
+    w = (1 + 0.3 * torch.randn(D, device=DEV, generator=g))
+    dy = torch.randn(rows, D, device=DEV, generator=g).to(torch.bfloat16)
+    xr = x.clone().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    yr = ((xr.float() * torch.rsqrt(xr.float().pow(2).mean(-1, keepdim=True) + 1e-6)).to(torch.bfloat16)
+          * wr).to(torch.bfloat16)
+    yr.backward(dy)
+    xf = x.clone().requires_grad_(True)
+    wf = w.clone().requires_grad_(True)
+    yf = ops().rms_norm(xf, wf, 1e-6)
+    yf.backward(dy)
+    assert yf.dtype == torch.bfloat16 and ulp_close(yf, yr)
+    assert rel(xf.grad, xr.grad) < 2e-2
+    assert rel(wf.grad, wr.grad) < 1e-2
+
+
+@pytest.mark.parametrize("B,NH,T,DH", [(2, 4, 65, 192), (3, 2, 9, 64), (1, 4, 128, 256)])
+def test_gated_head_norm_vs_torch(B, NH, T, DH):
+    g = torch.Generator(device=DEV).manual_seed(B * T + DH)
+    h = (torch.randn(B, NH, T, DH, device=DEV, generator=g) * 3 + 0.5).to(torch.bfloat16)
+    proj = torch.randn(B, T, NH * DH + 40, device=DEV, generator=g).to(torch.bfloat16)
+    o = proj[..., 8:8 + NH * DH]                     # a row-strided view, as in the layer
+    w = 1 + 0.3 * torch.randn(NH * DH, device=DEV, generator=g)
+    dy = torch.randn(B, T, NH * DH, device=DEV, generator=g).to(torch.bfloat16)
+    hr, orr, wr = (t.clone().requires_grad_(True) for t in (h, o, w))
+    y = hr.transpose(1, 2).float()
+    y = (y - y.mean(-1, keepdim=True)) * torch.rsqrt(y.var(-1, keepdim=True, unbiased=False) + 1e-6)
+    y = y.to(torch.bfloat16).reshape(B, T, -1) * wr
+    outr = (torch.sigmoid(orr) * y).to(torch.bfloat16)
+    outr.backward(dy)
+    hf, of, wf = (t.clone().requires_grad_(True) for t in (h, o, w))
+    outf = ops().gated_head_norm(hf, of, wf, 1e-6)
+    outf.backward(dy)
+    assert outf.shape == outr.shape and ulp_close(outf, outr)
+    assert rel(hf.grad, hr.grad) < 2e-2
+    assert rel(of.grad, orr.grad) < 2e-2
+    assert rel(wf.grad, wr.grad) < 1e-2
+
+
+@pytest.mark.parametrize("rows,Fd", [(3000, 2048), (5, 64)])
+def test_swiglu_vs_torch(rows, Fd):
+    g = torch.Generator(device=DEV).manual_seed(rows)
+    a = (torch.randn(rows, 2 * Fd, device=DEV, generator=g) * 2).to(torch.bfloat16)
+    dy = torch.randn(rows, Fd, device=DEV, generator=g).to(torch.bfloat16)
+    ar = a.clone().requires_grad_(True)
+    gr, ur = ar.split([Fd, Fd], -1)
+    yr = F.silu(gr) * ur
+    yr.backward(dy)
+    af = a.clone().requires_grad_(True)
+    yf = ops().swiglu(af)
+    yf.backward(dy)
+    assert ulp_close(yf, yr)
+    assert rel(af.grad, ar.grad) < 2e-2
+
+
+def test_xlstm_block_fused_equals_torch_path():
+    """A whole xLSTM block under bf16 autocast: fused glue vs the torch path (glue disabled)."""
+    from statecatcher_amd import xlstm
+    cfg = xlstm.xLSTMLargeConfig(embedding_dim=256, num_heads=4, num_blocks=1, vocab_size=64)
+    torch.manual_seed(0)
+    blk = xlstm.xLSTMBlock(cfg).to(DEV)
+    x = torch.randn(2, 128, 256, device=DEV)
+    outs = []
+    for fused in (True, False):
+        saved = (xlstm.ops.xlstm_glue_supported, xlstm.ops.gated_head_norm_supported)
+        if not fused:
+            xlstm.ops.xlstm_glue_supported = lambda *a: False
+            xlstm.ops.gated_head_norm_supported = lambda *a: False
+        try:
+            blk.zero_grad()
+            xi = x.clone().requires_grad_(True)
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                y, _ = blk(xi.to(torch.bfloat16))
+            y.float().square().mean().backward()
+            outs.append((y.float(), xi.grad.clone(),
+                         {n: p.grad.clone() for n, p in blk.named_parameters()}))
+        finally:
+            xlstm.ops.xlstm_glue_supported, xlstm.ops.gated_head_norm_supported = saved
+    (yf, gxf, pf), (yt, gxt, pt) = outs
+    assert rel(yf, yt) < 1e-2
+    assert rel(gxf, gxt) < 3e-2
+    # per parameter, with a floor at 1e-3 of the largest gradient: the gate biases' gradients
+    # (~1e-6 here, 1e5 below the others) are rounding noise in both paths
+    gmax = max(float(t.norm()) for t in pt.values())
+    for n in pt:
+        err = float((pf[n].double() - pt[n].double()).norm())
+        assert err <= 3e-2 * float(pt[n].norm()) + 1e-3 * gmax, (n, err, float(pt[n].norm()))
