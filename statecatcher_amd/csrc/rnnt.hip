@@ -967,19 +967,29 @@ __global__ void __launch_bounds__(256) joint_bwd_kernel(JointArgs a) {
 #pragma unroll
         for (int q = 0; q < 16; ++q) Y[jb][q] = 0.0f;
       const int yl = u < Ub ? label_at(r, b, u) : r.blank;
-#pragma unroll
-      for (int k = 0; k < kVbW; ++k) {
-        // every wave runs all kVbW blocks (no early exit: its PHIs cost a copy of Y); a block past
-        // the vocabulary reads row block 0 and gets p = 0
+      // logits of vocab block k (W rows of a block past the vocabulary: block 0, p forced to 0)
+      auto logits_blk = [&](int k) __attribute__((always_inline)) {
         const int lvb = w + 4 * k;
-        const bool vok = lvb < nvw;
-        const int lvc = vok ? lvb : 0;   // (the W rows read for a block past the vocabulary)
-        const int vl = lvc * 32 + (lane & 31);
+        const int vl = (lvb < nvw ? lvb : 0) * 32 + (lane & 31);
         jf16 x;
 #pragma unroll
         for (int q = 0; q < 16; ++q) x[q] = 0.0f;
 #pragma unroll
         for (int s = 0; s < 4; ++s) x = mfma32(zA[s], lds_b128(wl, wimg(vl, 2 * s + h)), x);
+        return x;
+      };
+      // software pipeline: block k+1's W reads and logits MFMAs are issued before block k's
+      // exp / transpose work, so their latency overlaps it (one wave per SIMD hides nothing)
+      jf16 xnext = logits_blk(0);
+#pragma unroll
+      for (int k = 0; k < kVbW; ++k) {
+        // every wave runs all kVbW blocks (no early exit: its PHIs cost a copy of Y)
+        const int lvb = w + 4 * k;
+        const bool vok = lvb < nvw;
+        const int lvc = vok ? lvb : 0;   // (the W rows read for a block past the vocabulary)
+        const int vl = lvc * 32 + (lane & 31);
+        const jf16 x = xnext;
+        if (k + 1 < kVbW) xnext = logits_blk(k + 1);
         const float bl = vok ? bias_l[vl] : -1e30f;
         float p[16], ps = 0.0f;
 #pragma unroll
