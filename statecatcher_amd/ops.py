@@ -1071,3 +1071,48 @@ class SwiGLUFn(torch.autograd.Function):
 
 def swiglu(a):
     return SwiGLUFn.apply(a)
+
+
+class AutocastLinearFn(torch.autograd.Function):
+    """y = x W^T (+ b) in the autocast dtype (what nn.Linear does under bf16 autocast) with a
+    backward that takes the weight gradient from the MFMA split-L kernel when the shape fits
+    (dW = dY^T X reduces over the B*T rows, hipBLASLt's weakest case): the xLSTM blocks' linears.
+    The input gradient stays a library GEMM (NN form, TunableOp table)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, cdt):
+        xc = x.to(cdt)
+        wc = w.to(cdt)
+        y = torch.nn.functional.linear(xc, wc, None if b is None else b.to(cdt))
+        ctx.save_for_backward(xc, wc)
+        ctx.meta = (x.dtype, w.dtype, None if b is None else b.dtype)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xc, wc = ctx.saved_tensors
+        xdt, wdt, bdt = ctx.meta
+        N, K = wc.shape
+        dy2 = dy.reshape(-1, N).to(wc.dtype)
+        x2 = xc.reshape(-1, K)
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = (dy2 @ wc).view(*dy.shape[:-1], K).to(xdt)
+        if ctx.needs_input_grad[1]:
+            dwm = None
+            if dy2.is_cuda and dy2.dtype == torch.bfloat16:
+                dwm = wgrad_mfma(dy2.contiguous(), x2.contiguous())
+            dw = (dwm if dwm is not None else (dy2.t() @ x2).float()).to(wdt)
+        if bdt is not None and ctx.needs_input_grad[2]:
+            db = colsum(dy2).to(bdt)
+        return dx, dw, db, None
+
+
+def autocast_linear(x, w, b=None):
+    """nn.Linear semantics under autocast (bf16 compute when enabled) through AutocastLinearFn."""
+    if x.is_cuda and torch.is_autocast_enabled("cuda"):
+        cdt = torch.get_autocast_dtype("cuda")
+    else:
+        cdt = torch.promote_types(x.dtype, w.dtype)
+    with torch.autocast("cuda", enabled=False):
+        return AutocastLinearFn.apply(x, w, b, cdt)

@@ -29,6 +29,14 @@ from . import ops
 from .ops import mlstm_chunkwise
 
 
+def _linear(x, w, b=None):
+    """nn.Linear under autocast; on the GPU through ops.autocast_linear, whose backward takes the
+    weight gradient (a reduction over all B*T rows) from the MFMA split-L kernel."""
+    if x.is_cuda:
+        return ops.autocast_linear(x, w, b)
+    return F.linear(x, w, b)
+
+
 def soft_cap(x, cap):
     return x if cap is None else cap * torch.tanh(x / cap)
 
@@ -119,9 +127,10 @@ class FeedForward(nn.Module):
         b = None
         if self.proj_up.bias is not None:
             b = torch.cat([self.proj_up_gate.bias, self.proj_up.bias])
-        a = F.linear(x, w, b)
+        a = _linear(x, w, b)
         if a.is_cuda and a.dtype == torch.bfloat16 and up % 4 == 0:
-            return self.proj_down(ops.swiglu(a))   # one HIP pass, one [dg | du] gradient
+            # one HIP pass, one [dg | du] gradient
+            return _linear(ops.swiglu(a), self.proj_down.weight, self.proj_down.bias)
         g, u = a.split([up, up], -1)
         return self.proj_down(F.silu(g) * u)
 
@@ -156,7 +165,7 @@ class mLSTMLayer(nn.Module):
             b = torch.cat([m.bias if m.bias is not None else
                            torch.zeros(m.weight.shape[0], dtype=m.weight.dtype, device=m.weight.device)
                            for m in mods])
-        return F.linear(x, w, b).split([m.weight.shape[0] for m in mods], -1)
+        return _linear(x, w, b).split([m.weight.shape[0] for m in mods], -1)
 
     def forward(self, x, state=None):
         B, T, _ = x.shape
@@ -174,7 +183,8 @@ class mLSTMLayer(nn.Module):
         if (mh.bias is None and mh.force_float32_reductions and o.dtype == torch.bfloat16
                 and ops.gated_head_norm_supported(h)):
             # sigmoid(o) * MultiHeadLayerNorm(h) in one HIP pass on the cell's [B,NH,T,DH] layout
-            return self.out_proj(ops.gated_head_norm(h, o, mh.weight, mh.eps)), new_state
+            y = ops.gated_head_norm(h, o, mh.weight, mh.eps)
+            return _linear(y, self.out_proj.weight, self.out_proj.bias), new_state
         h = self.multihead_norm(h.transpose(1, 2))
         return self.out_proj(torch.sigmoid(o) * h), new_state
 
