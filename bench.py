@@ -62,6 +62,9 @@ def parse():
                          "host issue time per step")
     ap.add_argument("--tune-out", default=None,
                     help="rank 0 tunes GEMM shapes missing from the table and writes it here")
+    ap.add_argument("--retune", action="store_true",
+                    help="with --tune-out: ignore the shipped table and tune every shape afresh "
+                         "(1 s budget per shape)")
     return ap.parse_args()
 
 
@@ -274,9 +277,9 @@ def main():
         table = os.path.join(ROOT, "statecatcher_amd", "tuning", "tunableop_gfx950.csv")
         tun.enable(True)
         tun.tuning_enable(bool(args.tune_out) and rank == 0)
-        tun.set_max_tuning_duration(200)
+        tun.set_max_tuning_duration(1000 if args.retune else 200)
         tun.set_filename(args.tune_out if (args.tune_out and rank == 0) else table)
-        if os.path.exists(table):
+        if os.path.exists(table) and not (args.retune and args.tune_out):
             tun.read_file(table)
 
     from statecatcher_amd import ops
