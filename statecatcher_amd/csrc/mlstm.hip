@@ -119,10 +119,13 @@ __device__ __forceinline__ void load_rows(T* dst, const T* src, int tid) {
     *(uint4*)(dst + r * (D + kPad) + c) = *(const uint4*)(src + (int64_t)r * D + c);
   }
 }
+// (transposing loaders: consecutive lanes take consecutive ROWS of one 8-column piece, so each
+// of the eight 2-byte LDS stores per piece hits consecutive addresses across the wave; with
+// lanes along the columns every store of a wave landed in one bank, 32-way)
 template <typename T, int D>
 __device__ __forceinline__ void load_rows_t(T* dst, const T* src, int tid) {
   for (int e = tid; e < kL * D / 8; e += 256) {
-    const int r = e / (D / 8), c = (e % (D / 8)) * 8;
+    const int r = e % kL, c = (e / kL) * 8;
     const uint4 raw = *(const uint4*)(src + (int64_t)r * D + c);
     const T* x = (const T*)&raw;
 #pragma unroll
@@ -135,7 +138,7 @@ __device__ __forceinline__ void load_rows_t(T* dst, const T* src, int tid) {
 template <typename T, int D, int W>
 __device__ __forceinline__ void load_cols_t(T* dst, const T* src, int c0, int tid) {
   for (int e = tid; e < kL * W / 8; e += 256) {
-    const int r = e / (W / 8), c = (e % (W / 8)) * 8;
+    const int r = e % kL, c = (e / kL) * 8;
     const uint4 raw = *(const uint4*)(src + (int64_t)r * D + c0 + c);
     const T* x = (const T*)&raw;
 #pragma unroll
