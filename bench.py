@@ -60,6 +60,12 @@ def parse():
     ap.add_argument("--host-probe", action="store_true",
                     help="diagnostics on stderr: synchronising ops in one step (sync debug mode) and "
                          "host issue time per step")
+    ap.add_argument("--optimizer", choices=["hip", "torch-fused"], default="hip",
+                    help="hip: torch.optim.Adam stepped by the HIP clip+Adam kernels (default); "
+                         "torch-fused: torch's fused Adam kernel (A/B)")
+    ap.add_argument("--op-probe", action="store_true",
+                    help="diagnostics on stderr: every ATen op one step dispatches (count, shapes, "
+                         "caller), to find the step's non-HIP kernels")
     ap.add_argument("--tune-out", default=None,
                     help="rank 0 tunes GEMM shapes missing from the table and writes it here")
     ap.add_argument("--retune", action="store_true",
@@ -93,6 +99,39 @@ def gemm_flops_per_frame(args):
     D, L = args.hidden, args.layers
     fwd = 2 * 7 * D * (args.feat + (L - 1) * D) + 2 * D * args.vocab
     return 3 * fwd   # fwd + dgrad + wgrad
+
+
+def op_probe(step):
+    """Run one step under a TorchDispatchMode and print the ATen ops that launch work (views and
+    metadata ops excluded), grouped by op, shapes and the innermost statecatcher_amd caller."""
+    import collections
+    import traceback
+    from torch.utils._python_dispatch import TorchDispatchMode
+    skip = ("view", "_unsafe_view", "t", "transpose", "permute", "expand", "slice", "select",
+            "as_strided", "detach", "alias", "unsqueeze", "squeeze", "split", "empty", "split_with_sizes",
+            "_reshape_alias", "reshape", "unbind", "chunk", "is_same_size", "_to_copy_meta",
+            "empty_strided", "new_empty", "new_empty_strided", "narrow", "lift_fresh", "_local_scalar_dense")
+    seen = collections.Counter()
+
+    class Mode(TorchDispatchMode):
+        def __torch_dispatch__(self, func, types, args=(), kwargs=None):
+            name = func.overloadpacket.__name__
+            if name not in skip:
+                shapes = tuple(tuple(a.shape) for a in args if isinstance(a, torch.Tensor))[:3]
+                where = "?"
+                for fr in reversed(traceback.extract_stack()[:-1]):
+                    if "statecatcher_amd" in fr.filename or fr.filename.endswith("bench.py"):
+                        where = f"{os.path.basename(fr.filename)}:{fr.lineno}"
+                        break
+                seen[(name, shapes, where)] += 1
+            return func(*args, **(kwargs or {}))
+
+    torch.cuda.synchronize()
+    with Mode():
+        step()
+    torch.cuda.synchronize()
+    for (name, shapes, where), n in sorted(seen.items(), key=lambda kv: kv[0][2]):
+        print(f"op-probe {n:3d}x {name:28s} {where:28s} {shapes}", file=sys.stderr)
 
 
 def build_workload(args, device):
@@ -287,10 +326,10 @@ def main():
 
     model, criterion, params, tkw, conf = build_workload(args, device)
     params = [p for p in params if p.requires_grad]
-    try:
+    if args.optimizer == "torch-fused":   # A/B: torch's fused Adam with the clip as grad_scale
         opt = torch.optim.Adam(params, lr=3e-4, fused=True)
-    except Exception:
-        opt = torch.optim.Adam(params, lr=3e-4, foreach=True)
+    else:   # the reference's optim.Adam(params, lr) (train.py:133): clip + step on HIP (optim.py)
+        opt = torch.optim.Adam(params, lr=3e-4)
     amp = torch.bfloat16 if args.dtype == "bf16" else None
     # the reference segment loop (train.py:460-581) with DDP over RCCL when world > 1
     trainer = SegmentTrainer(model, criterion, opt, accumulation_steps=1, max_grad_norm=50.0,
@@ -321,6 +360,8 @@ def main():
             h2 = time.perf_counter()
             print(f"host issue {1e3 * (h1 - h0):.3f} ms, step wall {1e3 * (h2 - h0):.3f} ms",
                   file=sys.stderr)
+    if args.op_probe:
+        op_probe(step)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()

@@ -292,6 +292,52 @@ int sc_gemm_wgrad_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, f
 int sc_gemm_tn_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc,
                     int M, int N, int K, int tile_m, void* stream);
 
+/* ---------------------------------------------------------------- optimizer step -------- */
+
+/*
+ * clip_grad_norm_(params, max_norm) followed by torch.optim.Adam / AdamW's step
+ * (train.py:543-552, :119-136), fp32 tensors of any length, one launch per pass:
+ *   sc_adam_sumsq  sum of squares of the gradients of the clipped tensors into
+ *                  part[sc_adam_parts(t, nt)] (fixed order, no atomics);
+ *   sc_adam_step   coef = max_norm / (sqrt(sum part) + 1e-6) clamped to <= 1 (part = NULL: 1;
+ *                  NaN propagates like torch.clamp), then per element: g *= coef; AdamW
+ *                  (decoupled = 1) p *= 1 - lr wd, Adam g += wd p; m = lerp(m, g, 1 - beta1);
+ *                  v = v beta2 + (1 - beta2) g g; p -= step_size m / (sqrt(v) / bc2_sqrt + eps),
+ *                  step_size = lr / (1 - beta1^step), bc2_sqrt = sqrt(1 - beta2^step).
+ *                  norm_out (optional, one float): the total norm clip_grad_norm_ returns.
+ * The gradients are only read (p.grad keeps its unclipped values; the step loop discards them).
+ * Up to 24 tensors go into one launch's argument table; longer lists take several launches.
+ */
+typedef struct {
+  float* p;        /* parameter */
+  const float* g;  /* gradient */
+  float* m;        /* exp_avg */
+  float* v;        /* exp_avg_sq */
+  int64_t n;       /* elements */
+} sc_adam_tensor;
+int64_t sc_adam_parts(const sc_adam_tensor* t, int nt);
+int sc_adam_sumsq(const sc_adam_tensor* t, int nt, float* part, void* stream);
+int sc_adam_step(const sc_adam_tensor* t, int nt, const float* part, int64_t nparts,
+                 double max_norm, double lr, double beta1, double beta2, double eps,
+                 double weight_decay, int decoupled, double step_size, double bc2_sqrt,
+                 float* norm_out, void* stream);
+
+/*
+ * Per-step bf16 images of the fp32 projection weights, one launch for up to 16 weights: the
+ * autocast casts of LinearSafe (lucyrnn_triton.py:20-25 under train.py's autocast) plus the
+ * layouts the GEMMs want.  Per job: dst bf16 [rows][cols_pad] = src rows (stride ld_src) with
+ * zero columns cols..cols_pad-1, rows in step-blocked order (block, gate, unit) when block_d = D
+ * > 0 (rows = 7 D, D % 64 == 0; dst row (b, g, u) = src row g D + 64 b + u); dst_t (optional)
+ * bf16 [cols][rows] = dst's first cols columns transposed.  Round to nearest even.
+ */
+typedef struct {
+  const float* src;
+  void* dst;
+  void* dst_t;
+  int64_t rows, cols, cols_pad, ld_src, block_d;
+} sc_image_job;
+int sc_weight_images(const sc_image_job* jobs, int njobs, void* stream);
+
 /* ---------------------------------------------------------------- xLSTM block glue ------ */
 
 /*

@@ -18,7 +18,7 @@ _DTYPE = {torch.float32: SC_F32, torch.bfloat16: SC_BF16, torch.float16: SC_F16}
 
 _c = ctypes
 _i32, _i64, _vp, _fp = _c.c_int, _c.c_int64, _c.c_void_p, _c.c_void_p
-ABI_VERSION = 6  # include/statecatcher.h; bumped on any signature change
+ABI_VERSION = 7  # include/statecatcher.h; bumped on any signature change
 
 _SIGS = {
     "sc_abi_version": (_i32, []),
@@ -73,6 +73,12 @@ _SIGS = {
                                 _i32, _i32, _i32, _i32, _vp]),
     "sc_swiglu_fwd": (_i32, [_vp, _vp, _i64, _i32, _vp]),
     "sc_swiglu_bwd": (_i32, [_vp, _vp, _vp, _i64, _i32, _vp]),
+    "sc_adam_parts": (_i64, [_vp, _i32]),
+    "sc_adam_sumsq": (_i32, [_vp, _i32, _fp, _vp]),
+    "sc_adam_step": (_i32, [_vp, _i32, _fp, _i64, _c.c_double, _c.c_double, _c.c_double,
+                           _c.c_double, _c.c_double, _c.c_double, _i32, _c.c_double, _c.c_double,
+                           _fp, _vp]),
+    "sc_weight_images": (_i32, [_vp, _i32, _vp]),
     "sc_rnnt_workspace_bytes": (_c.c_size_t, [_i32, _i32, _i32]),
     "sc_rnnt_joint_geometry": (_i32, [_i32, _i32, _i32, _i32, _vp, _vp, _vp]),
     "sc_rnnt_joint_fwd": (_i32, [_fp, _fp, _vp, _fp, _i32, _i32, _i32, _i32, _i32, _vp, _i64, _vp,
@@ -85,6 +91,17 @@ _SIGS = {
                           _vp, _vp, _i32, _fp, _vp, _i32, _vp, _c.c_size_t, _vp]),
 }
 EXPORTED = tuple(_SIGS)
+
+
+class AdamTensor(ctypes.Structure):
+    """sc_adam_tensor (include/statecatcher.h)."""
+    _fields_ = [("p", _vp), ("g", _vp), ("m", _vp), ("v", _vp), ("n", _i64)]
+
+
+class ImageJob(ctypes.Structure):
+    """sc_image_job (include/statecatcher.h)."""
+    _fields_ = [("src", _vp), ("dst", _vp), ("dst_t", _vp), ("rows", _i64), ("cols", _i64),
+                ("cols_pad", _i64), ("ld_src", _i64), ("block_d", _i64)]
 
 _LIB = None
 

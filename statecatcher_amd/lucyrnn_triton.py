@@ -17,32 +17,38 @@ import torch
 import torch.nn as nn
 
 from .lucyrnn_conf import LucyRNNConfig
-from .ops import colsum, layer_norm, layer_norm_supported, lucy_cell, proj_dgrad, wgrad_splitk
+from .ops import (cell_image_spec, colsum, layer_norm, layer_norm_supported, lucy_cell, proj_dgrad,
+                  weight_images, wgrad_splitk)
 
 
 class _LinearFn(torch.autograd.Function):
-    """y = x W^T + b in the autocast dtype; backward with a split-K weight gradient."""
+    """y = x W^T + b in the autocast dtype; backward with a split-K weight gradient.  imgs:
+    (W, W^T, b) bf16 images from ops.weight_images, or None (cast here)."""
 
     @staticmethod
-    def forward(ctx, x, w, b, cdtype):
+    def forward(ctx, x, w, b, cdtype, imgs=None):
         xc = x.to(cdtype)
-        wc = w.to(cdtype)
-        out = torch.addmm(b.to(cdtype), xc, wc.t()) if b is not None else xc @ wc.t()
-        ctx.save_for_backward(xc, wc)
-        ctx.meta = (x.dtype, w.dtype, b is not None)
+        if imgs is not None:
+            wc, wt, bc = imgs
+        else:
+            wc, wt = w.to(cdtype), None
+            bc = b.to(cdtype) if b is not None else None
+        out = torch.addmm(bc, xc, wc.t()) if b is not None else xc @ wc.t()
+        ctx.save_for_backward(xc, wc if wt is None else None, wt)
+        ctx.meta = (x.dtype, w.dtype, b is not None, cdtype)
         return out
 
     @staticmethod
     def backward(ctx, dy):
-        xc, wc = ctx.saved_tensors
-        xdt, wdt, has_b = ctx.meta
-        dy = dy.to(wc.dtype)
+        xc, wc, wt = ctx.saved_tensors
+        xdt, wdt, has_b, cdt = ctx.meta
+        dy = dy.to(cdt)
         dx = None
         if ctx.needs_input_grad[0]:
-            dx = proj_dgrad(dy, wc).to(xdt)
+            dx = (torch.matmul(dy, wt.t()) if wt is not None else proj_dgrad(dy, wc)).to(xdt)
         dw = wgrad_splitk(dy, xc).to(wdt) if ctx.needs_input_grad[1] else None
         db = colsum(dy).to(wdt) if has_b and ctx.needs_input_grad[2] else None
-        return dx, dw, db, None
+        return dx, dw, db, None, None
 
 
 class LinearSafe(nn.Module):
@@ -59,16 +65,29 @@ class LinearSafe(nn.Module):
         if self.bias is not None:
             nn.init.zeros_(self.bias)
 
-    def forward(self, x):
+    def forward(self, x, imgs=None):
         x_flat = x.reshape(-1, x.shape[-1])
         if x.is_cuda and torch.is_autocast_enabled("cuda"):
             cdt = torch.get_autocast_dtype("cuda")
         else:
             cdt = torch.promote_types(x.dtype, self.weight.dtype)
+        if imgs is not None and cdt != torch.bfloat16:
+            imgs = None
         with torch.autocast("cuda", enabled=False):
             # one GEMM with the bias in its epilogue (hipBLASLt); the reference adds it after
-            out = _LinearFn.apply(x_flat, self.weight, self.bias, cdt)
+            out = _LinearFn.apply(x_flat, self.weight, self.bias, cdt, imgs)
         return out.view(*x.shape[:-1], self.weight.shape[0])
+
+    def image_specs(self, needs_dx):
+        """weight_images specs for a bf16 forward: W (+ W^T for the input gradient), b."""
+        w, b = self.weight, self.bias
+        if not (w.is_cuda and w.dtype == torch.float32 and w.stride(1) == 1
+                and (b is None or (b.dtype == torch.float32 and b.stride(0) == 1))):
+            return None
+        specs = [(w, 0, w.shape[1], needs_dx)]
+        if b is not None:
+            specs.append((b, 0, b.shape[0], False))
+        return specs
 
 
 class LayerNormHip(nn.LayerNorm):
@@ -112,11 +131,11 @@ class LucyRNNCellTriton(nn.Module):
         out, s_out, _ = self.forward_with_h(x, h0, s0)
         return out, s_out
 
-    def forward_with_h(self, x, h0, s0):
+    def forward_with_h(self, x, h0, s0, imgs=None):
         """(out, s_out, h_last): h_last = out[:, -1] in fp32, unrounded by a 16-bit out (the
         state LucyRNNtriton carries).  Projection GEMM + scan are one autograd node: the scan
         backward hands the bias gradient back from registers, the weight gradient runs on the
-        MFMA split-L kernel."""
+        MFMA split-L kernel.  imgs: this layer's entry of ops.weight_images (bf16 only)."""
         w, b = self.linear.weight, self.linear.bias
         if x.is_cuda and torch.is_autocast_enabled("cuda"):
             cdt = torch.get_autocast_dtype("cuda")
@@ -124,8 +143,10 @@ class LucyRNNCellTriton(nn.Module):
             cdt = torch.promote_types(x.dtype, w.dtype)
         if b is None:
             b = torch.zeros(w.shape[0], dtype=w.dtype, device=w.device)
+        if imgs is not None and cdt != torch.bfloat16:
+            imgs = None
         with torch.autocast("cuda", enabled=False):
-            return lucy_cell(x, w, b, h0, s0, cdt)
+            return lucy_cell(x, w, b, h0, s0, cdt, imgs)
 
 
 class LucyRNNtriton(nn.Module):
@@ -173,6 +194,7 @@ class LucyRNNtriton(nn.Module):
         else:
             h, s = hidden_states
 
+        cell_imgs, out_imgs = self._weight_images(x)
         track_outputs, final_h, final_s = [], [], []
         for t in range(self.num_tracks):
             x_t = x
@@ -182,7 +204,8 @@ class LucyRNNtriton(nn.Module):
             for l, layer in enumerate(layers):
                 # h carry = out[:, -1] (lucyrnn_triton.py:135), taken in fp32 from the scan and
                 # contiguous
-                x_t, s_t[l], h_t[l] = layer.forward_with_h(x_t, h_t[l], s_t[l])
+                x_t, s_t[l], h_t[l] = layer.forward_with_h(
+                    x_t, h_t[l], s_t[l], cell_imgs.get((t, l)) if cell_imgs else None)
                 if l < len(norms):
                     x_t = norms[l](x_t)
             track_outputs.append(x_t)
@@ -193,7 +216,33 @@ class LucyRNNtriton(nn.Module):
             x = track_outputs[0]
         else:
             x = self.merge_proj(torch.cat(track_outputs, dim=-1))
-        logits = self.output_proj(x.contiguous())
+        logits = self.output_proj(x.contiguous(), out_imgs)
         if self.config.return_last_states:
             return logits, (final_h, final_s)
         return logits
+
+    def _weight_images(self, x):
+        """bf16 images of every projection weight for this forward (ops.weight_images: one
+        launch after each optimizer step, cached otherwise) when the step runs under bf16
+        autocast on the GPU; ({(track, layer): (W image, W^T image)}, output-projection
+        (W, W^T, b) images) or (None, None)."""
+        if not (x.is_cuda and torch.is_autocast_enabled("cuda")
+                and torch.get_autocast_dtype("cuda") == torch.bfloat16):
+            return None, None
+        grad = torch.is_grad_enabled()
+        specs, where = [], []
+        for t, layers in enumerate(self.tracks):
+            for l, layer in enumerate(layers):
+                sp = cell_image_spec(layer.linear.weight, torch.bfloat16,
+                                     grad and (l > 0 or x.requires_grad))
+                if sp is not None and layer.linear.bias is not None:
+                    specs.append(sp)
+                    where.append((t, l))
+        osp = self.output_proj.image_specs(grad) if self.num_tracks == 1 else None
+        imgs = weight_images(specs + (osp or []))
+        cell = {w: im for w, im in zip(where, imgs)}
+        out = None
+        if osp:
+            (wc, wt), rest = imgs[len(specs)], imgs[len(specs) + 1:]
+            out = (wc, wt, rest[0][0] if rest else None)
+        return cell, out

@@ -264,6 +264,62 @@ def pad_cols(x, k, dtype):
     return out
 
 
+# bf16 images of fp32 weights, per parameter: (key, (img, img_t)).  Rebuilt only when the
+# parameter changed (its version counter moves with every in-place update: torch's optimizers,
+# optim.clip_and_adam_step, load_state_dict) -- so once per optimizer step, in ONE launch for all
+# the weights of a model.
+from torch.utils.weak import WeakIdKeyDictionary  # noqa: E402
+
+_IMAGES = WeakIdKeyDictionary()
+
+
+def weight_images(specs):
+    """specs: [(w, block_d, cols_pad, want_t)] with w fp32 [rows, cols] (or [cols]) on the GPU.
+    Returns [(img bf16 [rows, cols_pad] (step-blocked rows when block_d), img_t bf16 [cols, rows]
+    or None)], reusing cached images of unchanged weights; stale ones are rebuilt together by
+    sc_weight_images (csrc/optim.hip)."""
+    out, jobs, keep = [None] * len(specs), [], []
+    for i, (w, bd, kp, want_t) in enumerate(specs):
+        rows, cols = (1, w.shape[0]) if w.dim() == 1 else tuple(w.shape)
+        key = (w._version, w.data_ptr(), rows, cols, bd, kp, bool(want_t))
+        hit = _IMAGES.get(w)
+        if hit is not None and hit[0] == key:
+            out[i] = hit[1]
+            continue
+        img = torch.empty(rows, kp, dtype=torch.bfloat16, device=w.device)
+        img_t = torch.empty(cols, rows, dtype=torch.bfloat16, device=w.device) if want_t else None
+        ld = w.stride(0) if w.dim() == 2 else cols
+        jobs.append(_lib.ImageJob(w.data_ptr(), img.data_ptr(),
+                                  img_t.data_ptr() if img_t is not None else None,
+                                  rows, cols, kp, ld, bd))
+        keep.append(w)
+        out[i] = (img.view(-1) if w.dim() == 1 else img, img_t)
+        _IMAGES[w] = (key, out[i])
+    if jobs:
+        require_device(*keep)
+        lib = _lib.load()
+        for k in range(0, len(jobs), 16):
+            part = jobs[k:k + 16]
+            rc = lib.sc_weight_images((_lib.ImageJob * len(part))(*part), len(part),
+                                      stream_of(keep[0]))
+            check(rc, "sc_weight_images")
+    return out
+
+
+def cell_image_spec(w, cdt, needs_dx):
+    """The weight image LucyCellFn consumes for w [7D, Din] under compute dtype cdt:
+    (w, block_d, cols_pad, want_t), or None when the cell casts w itself (not bf16 / not a
+    64-multiple D)."""
+    D = w.shape[0] // 7
+    if not (cdt == torch.bfloat16 and w.is_cuda and w.dtype == torch.float32 and w.dim() == 2
+            and w.stride(1) == 1 and D % 64 == 0):
+        return None
+    Din = w.shape[1]
+    kp = Din + (-Din) % 64
+    tn = USE_TN and (7 * D) % 256 == 0
+    return (w, D, kp if tn else Din, needs_dx)
+
+
 def step_blocked_rows(w, D, inverse=False, dtype=None):
     """Permute the 7*D rows of a gate projection weight from the reference's (gate, unit) order
     to (column block of 64 units, gate, unit-in-block) order (inverse=True: back), converting to
@@ -287,7 +343,7 @@ class LucyCellFn(torch.autograd.Function):
     """
 
     @staticmethod
-    def forward(ctx, x2d, w, b, h0, s0, B, T, cdt):
+    def forward(ctx, x2d, w, b, h0, s0, B, T, cdt, imgs=None):
         ctx.set_materialize_grads(False)   # unused state outputs: no zero-filled gradients
         D = w.shape[0] // 7
         blocked = D % 64 == 0
@@ -300,10 +356,19 @@ class LucyCellFn(torch.autograd.Function):
         # the forward GEMM's copy of x with zero columns up to kp; the weight gradient keeps the
         # unpadded xc (its GEMM would otherwise sum 48 extra zero columns)
         xg = pad_cols(x2d, kp, cdt) if tn and kp != Din else xc
-        # step-blocked gates: weight rows permuted to (column block, gate, unit) order so each
-        # step's 7 x 64 gates of a column block are one contiguous 896-byte run for the scan
-        wc = step_blocked_rows(w, D, dtype=cdt) if blocked else w.to(cdt)
-        wg = pad_cols(wc, kp, cdt) if tn and kp != Din else wc
+        wt = None
+        if imgs is not None:
+            # images from weight_images (cell_image_spec): the step-blocked, zero-padded bf16
+            # weight and its unpadded transpose for the input gradient
+            wg, wt = imgs
+            wc = None
+            if wt is None and ctx.needs_input_grad[0]:
+                wt = step_blocked_rows(w, D, dtype=cdt).t().contiguous()
+        else:
+            # step-blocked gates: weight rows permuted to (column block, gate, unit) order so
+            # each step's 7 x 64 gates of a column block are one contiguous 896-byte run
+            wc = step_blocked_rows(w, D, dtype=cdt) if blocked else w.to(cdt)
+            wg = pad_cols(wc, kp, cdt) if tn and kp != Din else wc
         bias = b.detach().to(torch.float32).contiguous()
         with _timed("gate_gemm_fwd", xc, 0):
             gates = proj_fwd(xg, wg)
@@ -311,14 +376,14 @@ class LucyCellFn(torch.autograd.Function):
         need = any(ctx.needs_input_grad)
         gates, out, s_out, ckpt, h_out = _scan_fwd(gates, h0, s0, need, bias, want_h=True)
         if need:
-            ctx.save_for_backward(xc, wc, gates, ckpt, bias)
+            ctx.save_for_backward(xc, wc, wt, gates, ckpt, bias)
             ctx.dtypes = (x2d.dtype, w.dtype, h0.dtype, s0.dtype)
             ctx.blocked = blocked
         return out, s_out, h_out
 
     @staticmethod
     def backward(ctx, dout, ds_last, dh_last):
-        xc, wc, gates, ckpt, bias = ctx.saved_tensors
+        xc, wc, wt, gates, ckpt, bias = ctx.saved_tensors
         xdt, wdt, hdt, sdt = ctx.dtypes
         if dh_last is not None:   # h_last is out[:, -1]: its gradient joins dout's last step
             B, T = gates.shape[:2]
@@ -333,7 +398,7 @@ class LucyCellFn(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0]:
             with _timed("gate_gemm_dgrad", dg2, 0):
-                dx = proj_dgrad(dg2, wc)
+                dx = torch.matmul(dg2, wt.t()) if wt is not None else proj_dgrad(dg2, wc)
             dx = dx.to(xdt)
         dw = None
         if ctx.needs_input_grad[1]:
@@ -341,16 +406,17 @@ class LucyCellFn(torch.autograd.Function):
                 dw = wgrad_splitk(dg2, xc, blocked_d=(dg2.shape[1] // 7) if ctx.blocked else 0)
             dw = dw.to(wdt)
         db = colsum(dbias.view(dbias.shape[0], -1)).to(wdt) if dbias is not None else None
-        return dx, dw, db, dh0.to(hdt), ds0.to(sdt), None, None, None
+        return dx, dw, db, dh0.to(hdt), ds0.to(sdt), None, None, None, None
 
 
-def lucy_cell(x, w, b, h0, s0, cdt=None):
+def lucy_cell(x, w, b, h0, s0, cdt=None, imgs=None):
     """x [B,T,Din] -> (out [B,T,D], s_last [B,D] fp32, h_last [B,D] fp32) through projection
-    + scan."""
+    + scan.  imgs: the (forward weight, transposed weight) images of cell_image_spec, or None
+    (the cell casts w itself)."""
     B, T, Din = x.shape
     if cdt is None:
         cdt = torch.promote_types(x.dtype, w.dtype)
-    return LucyCellFn.apply(x.reshape(B * T, Din), w, b, h0, s0, B, T, cdt)
+    return LucyCellFn.apply(x.reshape(B * T, Din), w, b, h0, s0, B, T, cdt, imgs)
 
 
 # ----------------------------------------------------------------------------- LayerNorm -----

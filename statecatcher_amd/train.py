@@ -26,6 +26,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from .model import compute_loss
+from .optim import clip_and_adam_step, hip_adam_eligible
 
 
 def compute_frame_mask(sample_mask: torch.Tensor, subsample: float) -> torch.Tensor:
@@ -119,11 +120,16 @@ class SegmentTrainer:
         return all(id(p) in own for g in opt.param_groups for p in g["params"])
 
     def _clip_and_step(self):
-        """clip_grad_norm_(max_norm) then optimizer.step() (train.py:543-552).  With a fused
+        """clip_grad_norm_(max_norm) then optimizer.step() (train.py:543-552).  A torch Adam /
+        AdamW built as the reference builds it runs on HIP (optim.clip_and_adam_step).  With a fused
         Adam the clip coefficient is handed to the optimizer kernel as its gradient divisor
         (grads / max(1, (norm + 1e-6) / max_norm)), which equals clip_grad_norm_'s in-place
         scaling followed by the step, without the extra pass over every gradient."""
         params = [p for p in self.model.parameters() if p.grad is not None]
+        if params and params[0].grad.is_cuda and hip_adam_eligible(self.optimizer):
+            # the reference's Adam / AdamW: clip + step as two HIP launches (optim.py)
+            clip_and_adam_step(self.optimizer, params, self.max_grad_norm)
+            return
         if not (self._fused_clip_ok() and params and params[0].grad.is_cuda):
             torch.nn.utils.clip_grad_norm_(self.model.parameters(), self.max_grad_norm)
             self.optimizer.step()
