@@ -296,14 +296,31 @@ def weight_images(specs):
         out[i] = (img.view(-1) if w.dim() == 1 else img, img_t)
         _IMAGES[w] = (key, out[i])
     if jobs:
-        require_device(*keep)
-        lib = _lib.load()
-        for k in range(0, len(jobs), 16):
-            part = jobs[k:k + 16]
-            rc = lib.sc_weight_images((_lib.ImageJob * len(part))(*part), len(part),
-                                      stream_of(keep[0]))
-            check(rc, "sc_weight_images")
+        _image_jobs(jobs, keep)
     return out
+
+
+def _image_jobs(jobs, keep):
+    require_device(*keep)
+    lib = _lib.load()
+    for k in range(0, len(jobs), 16):
+        part = jobs[k:k + 16]
+        rc = lib.sc_weight_images((_lib.ImageJob * len(part))(*part), len(part),
+                                  stream_of(keep[0]))
+        check(rc, "sc_weight_images")
+
+
+def cast_pad_bf16(x, kp):
+    """fp32 x [M, K] (unit column stride) -> (bf16 [M, kp] with zero columns K..kp-1, bf16
+    [M, K]) in one sc_weight_images launch: layer 0's GEMM operand (K padded to the TN kernel's
+    stage) and the weight gradient's unpadded copy, instead of a fill, a cast-copy and a cast."""
+    M, K = x.shape
+    xg = torch.empty(M, kp, dtype=torch.bfloat16, device=x.device)
+    xc = torch.empty(M, K, dtype=torch.bfloat16, device=x.device)
+    jobs = [_lib.ImageJob(x.data_ptr(), xg.data_ptr(), None, M, K, kp, x.stride(0), 0),
+            _lib.ImageJob(x.data_ptr(), xc.data_ptr(), None, M, K, K, x.stride(0), 0)]
+    _image_jobs(jobs, [x])
+    return xg, xc
 
 
 def cell_image_spec(w, cdt, needs_dx):
@@ -352,10 +369,13 @@ class LucyCellFn(torch.autograd.Function):
         # MFMA kernel's K stage (the weight gets the same zero columns)
         kp = Din + (-Din) % 64
         tn = USE_TN and x2d.is_cuda and cdt == torch.bfloat16 and (7 * D) % 256 == 0
-        xc = x2d.to(cdt)
         # the forward GEMM's copy of x with zero columns up to kp; the weight gradient keeps the
         # unpadded xc (its GEMM would otherwise sum 48 extra zero columns)
-        xg = pad_cols(x2d, kp, cdt) if tn and kp != Din else xc
+        if tn and kp != Din and x2d.dtype == torch.float32 and x2d.stride(1) == 1:
+            xg, xc = cast_pad_bf16(x2d, kp)
+        else:
+            xc = x2d.to(cdt)
+            xg = pad_cols(x2d, kp, cdt) if tn and kp != Din else xc
         wt = None
         if imgs is not None:
             # images from weight_images (cell_image_spec): the step-blocked, zero-padded bf16

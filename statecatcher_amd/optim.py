@@ -114,7 +114,6 @@ def clip_and_adam_step(optimizer, clip_params, max_norm):
     if dev is None:
         return torch.zeros((), dtype=torch.float32)
     stream = stream_of(keep[0])
-    norm = torch.zeros(1, dtype=torch.float32, device=dev)
     part, nparts = None, 0
     if clip_entries:
         tab = _table(clip_entries)
@@ -122,6 +121,9 @@ def clip_and_adam_step(optimizer, clip_params, max_norm):
         if nparts:
             part = torch.empty(nparts, dtype=torch.float32, device=dev)
             check(lib.sc_adam_sumsq(tab, len(clip_entries), ptr(part), stream), "sc_adam_sumsq")
+    # the first clipped sc_adam_step launch writes the norm; with nothing to clip it is 0
+    norm = torch.empty(1, dtype=torch.float32, device=dev) if part is not None else \
+        torch.zeros(1, dtype=torch.float32, device=dev)
     norm_out = norm
     for g, members in groups:
         beta1, beta2 = g["betas"]

@@ -165,7 +165,8 @@ class SegmentTrainer:
                     self.mode, self.criterion, self.net, feats, masks, tokens, in_lens, tgt_lens,
                     self.blank_id, use_rnnt_joiner=self.joiner_net, input_state=self.encoder_state,
                     compact=self.compact_rnnt)
-            (loss / self.accumulation_steps).backward()
+            # loss / accumulation_steps (train.py:535); a division by 1 is the identity
+            (loss / self.accumulation_steps if self.accumulation_steps != 1 else loss).backward()
         if stepping:
             self._clip_and_step()
             self.optimizer.zero_grad(set_to_none=True)
