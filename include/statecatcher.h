@@ -405,11 +405,17 @@ int64_t sc_mlstm_state_numel(int BH, int T, int DQ, int DV);
  * [BH][T/64+1][DQ][DV], [BH][T/64+1][DQ], [BH][T/64+1]); m_rows, den_rows fp32 [BH][T] (the
  * row stabiliser and normaliser, consumed by the backward).  h_t = q~_t C_t / (max(|q~_t n_t|,
  * e^{-m_t}) + eps) with q~ = q DQ^-1/2.
+ * layout (optional, 7 int64): {NH, qb, qh, qt, vb, vh, vt} element strides of q / k (and dq /
+ * dk) and v (dv) with sequence bh = b NH + h at step t at (bh / NH) qb + (bh % NH) qh + t qt:
+ * the xLSTM layer reads them in place from its fused projection output [B][T][N] (qh = DQ,
+ * qt = N) and the backward writes the gradients into the projection's gradient the same way.
+ * NULL = contiguous [BH][T][D].  Strides multiples of 8 elements, bases 16-byte aligned.
  */
 int sc_mlstm_fwd(const void* q, const void* k, const void* v, int dtype, const float* igate,
                  const float* fgate, const float* c0, const float* n0, const float* m0, int BH,
                  int T, int DQ, int DV, float eps, void* h, float* states_C, float* states_n,
-                 float* states_m, float* m_rows, float* den_rows, void* stream);
+                 float* states_m, float* m_rows, float* den_rows, const int64_t* layout,
+                 void* stream);
 
 /*
  * Backward of sc_mlstm_fwd given dh (dtype, [BH][T][DV]) and optional gradients of the final
@@ -417,13 +423,15 @@ int sc_mlstm_fwd(const void* q, const void* k, const void* v, int dtype, const f
  * dstates_C/n (gradient w.r.t. every chunk-start state; index 0 = the initial state), and the
  * per-step gate terms qdq = q_t.dq_t, kdk = k_t.dk_t (fp32 [BH][T]): d igate = kdk,
  * d fgate_t = sigmoid(-f_t) sum_{r>=t} (qdq_r - kdk_r).  The stabiliser is not differentiated.
+ * layout: as sc_mlstm_fwd's; dq / dk / dv are written with the same strides as q / k / v.
  */
 int sc_mlstm_bwd(const void* q, const void* k, const void* v, int dtype, const float* igate,
                  const float* fgate, const void* h, const void* dh, const float* dcT,
                  const float* dnT, const float* states_C, const float* states_n,
                  const float* states_m, const float* m_rows, const float* den_rows, int BH, int T,
                  int DQ, int DV, float eps, float* dstates_C, float* dstates_n, void* dq,
-                 void* dk, void* dv, float* qdq, float* kdk, void* stream);
+                 void* dk, void* dv, float* qdq, float* kdk, const int64_t* layout,
+                 void* stream);
 
 /* ---------------------------------------------------------------- RNN-T ----------------- */
 

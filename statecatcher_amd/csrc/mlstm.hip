@@ -25,6 +25,8 @@
 // the pair identities  di_s = k_s.dk_s  and  dF_t = q_t.dq_t - k_t.dk_t  (F = cumulative
 // logsig(f)): the kernels emit the two dot products, the host turns dF into df by a reverse
 // cumulative sum times sigmoid(-f).
+#include <initializer_list>
+
 #include "sc_common.h"
 
 namespace sc {
@@ -80,7 +82,19 @@ struct MArgs {
   float* kdk;       // [BH][T]  k_t . dk_t
   int BH, T, nc;
   float eps, scale;
+  // element offsets of q / k / dq / dk (q*) and v / dv (v*) rows: sequence bh = b NH + h, step t
+  // at (bh / NH) *b + (bh % NH) *h + t *t.  Contiguous [BH][T][D]: NH = 1, b = T D, t = D; the
+  // xLSTM layer reads them in place from its fused projection [B][T][N] (h = D, t = N).
+  int NH;
+  int64_t qb, qh, qt, vb, vh, vt;
 };
+
+__device__ __forceinline__ int64_t qrow(const MArgs& a, int bh, int64_t t) {
+  return (int64_t)(bh / a.NH) * a.qb + (int64_t)(bh % a.NH) * a.qh + t * a.qt;
+}
+__device__ __forceinline__ int64_t vrow(const MArgs& a, int bh, int64_t t) {
+  return (int64_t)(bh / a.NH) * a.vb + (int64_t)(bh % a.NH) * a.vh + t * a.vt;
+}
 
 __device__ __forceinline__ float logsig(float x) { return fminf(x, 0.0f) - log1pf(expf(-fabsf(x))); }
 
@@ -113,20 +127,20 @@ __device__ __forceinline__ V8 frag_ks(const T* tile, int ld, int r0, int k0, int
 // Chunk rows [t0, t0+64) of a [T][D] matrix into LDS, row-major [64][D+kPad] or transposed
 // [D][64+kPad], 16-byte global loads (D % 8 == 0).
 template <typename T, int D>
-__device__ __forceinline__ void load_rows(T* dst, const T* src, int tid) {
+__device__ __forceinline__ void load_rows(T* dst, const T* src, int64_t ld, int tid) {
   for (int e = tid; e < kL * D / 8; e += 256) {
     const int r = e / (D / 8), c = (e % (D / 8)) * 8;
-    *(uint4*)(dst + r * (D + kPad) + c) = *(const uint4*)(src + (int64_t)r * D + c);
+    *(uint4*)(dst + r * (D + kPad) + c) = *(const uint4*)(src + (int64_t)r * ld + c);
   }
 }
 // (transposing loaders: consecutive lanes take consecutive ROWS of one 8-column piece, so each
 // of the eight 2-byte LDS stores per piece hits consecutive addresses across the wave; with
 // lanes along the columns every store of a wave landed in one bank, 32-way)
 template <typename T, int D>
-__device__ __forceinline__ void load_rows_t(T* dst, const T* src, int tid) {
+__device__ __forceinline__ void load_rows_t(T* dst, const T* src, int64_t ld, int tid) {
   for (int e = tid; e < kL * D / 8; e += 256) {
     const int r = e % kL, c = (e / kL) * 8;
-    const uint4 raw = *(const uint4*)(src + (int64_t)r * D + c);
+    const uint4 raw = *(const uint4*)(src + (int64_t)r * ld + c);
     const T* x = (const T*)&raw;
 #pragma unroll
     for (int j = 0; j < 8; ++j) dst[(c + j) * (kL + kPad) + r] = x[j];
@@ -136,10 +150,10 @@ __device__ __forceinline__ void load_rows_t(T* dst, const T* src, int tid) {
 // columns [c0, c0 + W) of chunk rows [t0, t0+64) of a [T][D] matrix, transposed into LDS
 // [W][64+kPad] (16-byte global loads; W % 8 == 0)
 template <typename T, int D, int W>
-__device__ __forceinline__ void load_cols_t(T* dst, const T* src, int c0, int tid) {
+__device__ __forceinline__ void load_cols_t(T* dst, const T* src, int64_t ld, int c0, int tid) {
   for (int e = tid; e < kL * W / 8; e += 256) {
     const int r = e % kL, c = (e / kL) * 8;
-    const uint4 raw = *(const uint4*)(src + (int64_t)r * D + c0 + c);
+    const uint4 raw = *(const uint4*)(src + (int64_t)r * ld + c0 + c);
     const T* x = (const T*)&raw;
 #pragma unroll
     for (int j = 0; j < 8; ++j) dst[(c + j) * (kL + kPad) + r] = x[j];
@@ -204,8 +218,8 @@ __global__ void __launch_bounds__(256) mlstm_fw_C(MArgs a) {
   __shared__ __attribute__((aligned(16))) T KT[DQ * (kL + kPad)];
   __shared__ __attribute__((aligned(16))) T VT[kCB * (kL + kPad)];
   __shared__ float sb[kL], si[kL], fs[kL], scal[2];
-  const T* K = (const T*)a.k + (int64_t)bh * a.T * DQ;
-  const T* V = (const T*)a.v + (int64_t)bh * a.T * DV;
+  const T* K = (const T*)a.k + qrow(a, bh, 0);
+  const T* V = (const T*)a.v + vrow(a, bh, 0);
   f32x4 acc[PW];
   // tile q = w + 4p: rows i in [16 (q / TJ), +16), cols j in cj0 + [16 (q % TJ), +16)
 #pragma unroll
@@ -234,8 +248,8 @@ __global__ void __launch_bounds__(256) mlstm_fw_C(MArgs a) {
   };
   for (int k = 0; k < a.nc; ++k) {
     store_state(k);
-    load_rows_t<T, DQ>(KT, K + (int64_t)k * kL * DQ, tid);
-    load_cols_t<T, DV, kCB>(VT, V + (int64_t)k * kL * DV, cj0, tid);
+    load_rows_t<T, DQ>(KT, K + (int64_t)k * kL * a.qt, a.qt, tid);
+    load_cols_t<T, DV, kCB>(VT, V + (int64_t)k * kL * a.vt, a.vt, cj0, tid);
     chunk_gates(a, bh, k, sb, si, tid);
     if (tid < 64) {
       const float g = __shfl(sb[63], 0);   // sb written by this wave; LDS in order
@@ -287,10 +301,10 @@ __global__ void __launch_bounds__(256) mlstm_fw_H(MArgs a) {
   __shared__ __attribute__((aligned(16))) T CT[kCB * (DQ + kPad)];
   __shared__ float sb[kL], si[kL], mt[kL], rowf[kL], dsum[kL], qn[kL], nk[DQ];
   const int64_t t0 = (int64_t)k * kL;
-  const T* Q = (const T*)a.q + ((int64_t)bh * a.T + t0) * DQ;
-  load_rows<T, DQ>(Qs, Q, tid);
-  load_rows<T, DQ>(Ks, (const T*)a.k + ((int64_t)bh * a.T + t0) * DQ, tid);
-  load_cols_t<T, DV, kCB>(VT, (const T*)a.v + ((int64_t)bh * a.T + t0) * DV, cj0, tid);
+  const T* Q = (const T*)a.q + qrow(a, bh, t0);
+  load_rows<T, DQ>(Qs, Q, a.qt, tid);
+  load_rows<T, DQ>(Ks, (const T*)a.k + qrow(a, bh, t0), a.qt, tid);
+  load_cols_t<T, DV, kCB>(VT, (const T*)a.v + vrow(a, bh, t0), a.vt, cj0, tid);
   const int64_t st = (int64_t)bh * (a.nc + 1) + k;
   const float* Ck = a.Cs + st * DQ * DV;
   for (int e = tid; e < DQ * kCB; e += 256) {   // C~_k[:, block] transposed to [j][i] (B of Q C)
@@ -441,7 +455,7 @@ __global__ void __launch_bounds__(256) mlstm_bw_dC(MArgs a) {
   for (int k = a.nc - 1; k >= 0; --k) {
     store(k + 1);
     const int64_t t0 = (int64_t)k * kL;
-    load_rows_t<T, DQ>(QT, (const T*)a.q + ((int64_t)bh * a.T + t0) * DQ, tid);
+    load_rows_t<T, DQ>(QT, (const T*)a.q + qrow(a, bh, t0), a.qt, tid);
     chunk_dnum<T, DV>(a, bh, t0, (T*)nullptr, DnT, dden, tid);
     chunk_gates(a, bh, k, sb, si, tid);
     if (tid < 64) {
@@ -531,8 +545,8 @@ __global__ void __launch_bounds__(256) mlstm_bw_dQ(MArgs a) {
   __shared__ __attribute__((aligned(16))) T Cm[DQ * (DV + kPad)];
   __shared__ float sb[kL], si[kL], mt[kL], rowf[kL], dden[kL], nk[DQ];
   const int64_t t0 = (int64_t)k * kL;
-  load_rows<T, DV>(Vs, (const T*)a.v + ((int64_t)bh * a.T + t0) * DV, tid);
-  load_rows_t<T, DQ>(KT, (const T*)a.k + ((int64_t)bh * a.T + t0) * DQ, tid);
+  load_rows<T, DV>(Vs, (const T*)a.v + vrow(a, bh, t0), a.vt, tid);
+  load_rows_t<T, DQ>(KT, (const T*)a.k + qrow(a, bh, t0), a.qt, tid);
   const int64_t st = (int64_t)bh * (a.nc + 1) + k;
   const float* Ck = a.Cs + st * DQ * DV;
   for (int e = tid; e < DQ * DV; e += 256) Cm[(e / DV) * (DV + kPad) + e % DV] = (T)Ck[e];
@@ -544,8 +558,8 @@ __global__ void __launch_bounds__(256) mlstm_bw_dQ(MArgs a) {
   __syncthreads();
   const float rf = rowf[16 * w + (lane & 15)];
   const int kin = (16 * (w + 1) + 31) / 32;
-  const T* Q = (const T*)a.q + ((int64_t)bh * a.T + t0) * DQ;
-  T* dQ = (T*)a.dq + ((int64_t)bh * a.T + t0) * DQ;
+  const T* Q = (const T*)a.q + qrow(a, bh, t0);
+  T* dQ = (T*)a.dq + qrow(a, bh, t0);
   float qd[4] = {0.f, 0.f, 0.f, 0.f};
   for (int ci = 0; ci < DQ / 16; ++ci) {
     f32x4 d4 = {0.f, 0.f, 0.f, 0.f};
@@ -561,8 +575,8 @@ __global__ void __launch_bounds__(256) mlstm_bw_dQ(MArgs a) {
     for (int r = 0; r < 4; ++r) {
       const int t = 16 * w + 4 * (lane >> 4) + r;
       const float v = d4[r] + rowf[t] * dden[t] * nk[i];
-      dQ[t * DQ + i] = (T)v;
-      qd[r] += v * (float)Q[t * DQ + i];
+      dQ[t * a.qt + i] = (T)v;
+      qd[r] += v * (float)Q[t * a.qt + i];
     }
   }
 #pragma unroll
@@ -586,8 +600,8 @@ __global__ void __launch_bounds__(256) mlstm_bw_dK(MArgs a) {
   __shared__ __attribute__((aligned(16))) T dCm[DQ * (DV + kPad)];
   __shared__ float sb[kL], si[kL], mt[kL], es[kL], dden[kL], dnk[DQ];
   const int64_t t0 = (int64_t)k * kL;
-  load_rows<T, DV>(Vs, (const T*)a.v + ((int64_t)bh * a.T + t0) * DV, tid);
-  load_rows_t<T, DQ>(QT, (const T*)a.q + ((int64_t)bh * a.T + t0) * DQ, tid);
+  load_rows<T, DV>(Vs, (const T*)a.v + vrow(a, bh, t0), a.vt, tid);
+  load_rows_t<T, DQ>(QT, (const T*)a.q + qrow(a, bh, t0), a.qt, tid);
   const int64_t st1 = (int64_t)bh * (a.nc + 1) + k + 1;
   const float* dC = a.dCs + st1 * DQ * DV;
   for (int e = tid; e < DQ * DV; e += 256) dCm[(e / DV) * (DV + kPad) + e % DV] = (T)dC[e];
@@ -600,8 +614,8 @@ __global__ void __launch_bounds__(256) mlstm_bw_dK(MArgs a) {
   // row block w holds keys s in [16w, 16w+16): intra sums over t >= s
   const float ef = es[16 * w + (lane & 15)];
   const int k0 = (16 * w) / 32;
-  const T* K = (const T*)a.k + ((int64_t)bh * a.T + t0) * DQ;
-  T* dK = (T*)a.dk + ((int64_t)bh * a.T + t0) * DQ;
+  const T* K = (const T*)a.k + qrow(a, bh, t0);
+  T* dK = (T*)a.dk + qrow(a, bh, t0);
   float kd[4] = {0.f, 0.f, 0.f, 0.f};
   for (int ci = 0; ci < DQ / 16; ++ci) {
     f32x4 d4 = {0.f, 0.f, 0.f, 0.f};
@@ -617,8 +631,8 @@ __global__ void __launch_bounds__(256) mlstm_bw_dK(MArgs a) {
     for (int r = 0; r < 4; ++r) {
       const int s = 16 * w + 4 * (lane >> 4) + r;
       const float v = d4[r] + es[s] * dnk[i];
-      dK[s * DQ + i] = (T)v;
-      kd[r] += v * (float)K[s * DQ + i];
+      dK[s * a.qt + i] = (T)v;
+      kd[r] += v * (float)K[s * a.qt + i];
     }
   }
 #pragma unroll
@@ -642,8 +656,8 @@ __global__ void __launch_bounds__(256) mlstm_bw_dV(MArgs a) {
   __shared__ __attribute__((aligned(16))) T dCT[DV * (DQ + kPad)];
   __shared__ float sb[kL], si[kL], mt[kL], es[kL], dden[kL];
   const int64_t t0 = (int64_t)k * kL;
-  load_rows<T, DQ>(Qs, (const T*)a.q + ((int64_t)bh * a.T + t0) * DQ, tid);
-  load_rows<T, DQ>(Ks, (const T*)a.k + ((int64_t)bh * a.T + t0) * DQ, tid);
+  load_rows<T, DQ>(Qs, (const T*)a.q + qrow(a, bh, t0), a.qt, tid);
+  load_rows<T, DQ>(Ks, (const T*)a.k + qrow(a, bh, t0), a.qt, tid);
   const int64_t st1 = (int64_t)bh * (a.nc + 1) + k + 1;
   const float* dC = a.dCs + st1 * DQ * DV;
   for (int e = tid; e < DQ * DV; e += 256) {
@@ -673,7 +687,7 @@ __global__ void __launch_bounds__(256) mlstm_bw_dV(MArgs a) {
   __syncthreads();
   const float ef = es[16 * w + (lane & 15)];
   const int k0 = (16 * w) / 32;
-  T* dV = (T*)a.dv + ((int64_t)bh * a.T + t0) * DV;
+  T* dV = (T*)a.dv + vrow(a, bh, t0);
   for (int cj = 0; cj < DV / 16; ++cj) {
     f32x4 d4 = {0.f, 0.f, 0.f, 0.f};
     for (int kk = k0; kk < kL / 32; ++kk)
@@ -685,7 +699,7 @@ __global__ void __launch_bounds__(256) mlstm_bw_dV(MArgs a) {
                   frag<V8, T>(dCT, DQ + kPad, 16 * cj, 32 * kk, lane), d4);
     const int j = 16 * cj + (lane & 15);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) dV[(16 * w + 4 * (lane >> 4) + r) * DV + j] = (T)d4[r];
+    for (int r = 0; r < 4; ++r) dV[(16 * w + 4 * (lane >> 4) + r) * a.vt + j] = (T)d4[r];
   }
 }
 
@@ -725,6 +739,31 @@ bool dims_supported(int DQ, int DV) {
   return false;
 }
 
+// q/k/v (and gradient) row layout: NULL = contiguous [BH][T][D]; else {NH, qb, qh, qt, vb, vh, vt}
+// element strides (16-byte loads: every stride and base a multiple of 8 elements)
+int set_layout(MArgs& a, const int64_t* layout, int DQ, int DV, const char* what,
+               std::initializer_list<const void*> ptrs) {
+  if (!layout) {
+    a.NH = 1;
+    a.qb = (int64_t)a.T * DQ; a.qh = 0; a.qt = DQ;
+    a.vb = (int64_t)a.T * DV; a.vh = 0; a.vt = DV;
+    return 0;
+  }
+  a.NH = (int)layout[0];
+  a.qb = layout[1]; a.qh = layout[2]; a.qt = layout[3];
+  a.vb = layout[4]; a.vh = layout[5]; a.vt = layout[6];
+  SC_REQUIRE(a.NH > 0 && a.BH % a.NH == 0, "%s: layout NH=%d does not divide BH=%d", what, a.NH,
+             a.BH);
+  for (int i = 1; i < 7; ++i)
+    SC_REQUIRE(layout[i] >= 0 && layout[i] % 8 == 0,
+               "%s: layout stride %lld is not a multiple of 8 elements", what,
+               (long long)layout[i]);
+  SC_REQUIRE(a.qt >= DQ && a.vt >= DV, "%s: layout row strides overlap the rows", what);
+  for (const void* p : ptrs)
+    SC_REQUIRE(((uintptr_t)p & 15) == 0, "%s: strided operands must be 16-byte aligned", what);
+  return 0;
+}
+
 }  // namespace
 
 }  // namespace sc
@@ -744,7 +783,8 @@ extern "C" int sc_mlstm_fwd(const void* q, const void* k, const void* v, int dty
                             const float* igate, const float* fgate, const float* c0,
                             const float* n0, const float* m0, int BH, int T, int DQ, int DV,
                             float eps, void* h, float* states_C, float* states_n,
-                            float* states_m, float* m_rows, float* den_rows, void* stream) {
+                            float* states_m, float* m_rows, float* den_rows,
+                            const int64_t* layout, void* stream) {
   clear_error();
   SC_REQUIRE(dtype == SC_BF16 || dtype == SC_F16, "sc_mlstm_fwd: dtype %d (bf16/f16 only)", dtype);
   SC_REQUIRE(BH >= 0 && T >= 0, "sc_mlstm_fwd: bad shape");
@@ -758,6 +798,7 @@ extern "C" int sc_mlstm_fwd(const void* q, const void* k, const void* v, int dty
   a.q = q; a.k = k; a.v = v; a.ig = igate; a.fg = fgate; a.c0 = c0; a.n0 = n0; a.m0 = m0;
   a.Cs = states_C; a.ns = states_n; a.ms = states_m; a.h = h; a.mrow = m_rows; a.den = den_rows;
   a.BH = BH; a.T = T; a.nc = T / kL; a.eps = eps; a.scale = 1.0f / sqrtf((float)DQ);
+  if (int rc = set_layout(a, layout, DQ, DV, "sc_mlstm_fwd", {q, k, v})) return rc;
   hipStream_t st = (hipStream_t)stream;
   if (dtype == SC_BF16) dispatch<SC_BF16>(a, DQ, DV, false, st);
   else dispatch<SC_F16>(a, DQ, DV, false, st);
@@ -770,7 +811,8 @@ extern "C" int sc_mlstm_bwd(const void* q, const void* k, const void* v, int dty
                             const float* states_C, const float* states_n, const float* states_m,
                             const float* m_rows, const float* den_rows, int BH, int T, int DQ,
                             int DV, float eps, float* dstates_C, float* dstates_n, void* dq,
-                            void* dk, void* dv, float* qdq, float* kdk, void* stream) {
+                            void* dk, void* dv, float* qdq, float* kdk, const int64_t* layout,
+                            void* stream) {
   clear_error();
   SC_REQUIRE(dtype == SC_BF16 || dtype == SC_F16, "sc_mlstm_bwd: dtype %d (bf16/f16 only)", dtype);
   SC_REQUIRE(T % kL == 0, "sc_mlstm_bwd: T=%d is not a multiple of the chunk length %d", T, kL);
@@ -785,6 +827,7 @@ extern "C" int sc_mlstm_bwd(const void* q, const void* k, const void* v, int dty
   a.ms = (float*)states_m; a.mrow = (float*)m_rows; a.den = (float*)den_rows;
   a.dCs = dstates_C; a.dns = dstates_n; a.dq = dq; a.dk = dk; a.dv = dv; a.qdq = qdq; a.kdk = kdk;
   a.BH = BH; a.T = T; a.nc = T / kL; a.eps = eps; a.scale = 1.0f / sqrtf((float)DQ);
+  if (int rc = set_layout(a, layout, DQ, DV, "sc_mlstm_bwd", {q, k, v, dq, dk, dv})) return rc;
   hipStream_t st = (hipStream_t)stream;
   if (dtype == SC_BF16) dispatch<SC_BF16>(a, DQ, DV, true, st);
   else dispatch<SC_F16>(a, DQ, DV, true, st);

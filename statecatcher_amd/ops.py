@@ -3,6 +3,7 @@
 Each op checks device/dtype/shape, allocates outputs through the PyTorch caching allocator,
 launches on the current stream and never synchronises the host.
 """
+import ctypes
 import os
 
 import torch
@@ -975,7 +976,7 @@ class MLSTMFn(torch.autograd.Function):
         with _timed("mlstm_fwd", qc, fwd_b):
             rc = lib.sc_mlstm_fwd(ptr(qc), ptr(kc), ptr(vc), dtype_code(qc), ptr(ig), ptr(fg), ptr(c0c),
                                   ptr(n0c), ptr(m0c), BH, T, DQ, DV, float(eps), ptr(h), ptr(Cs),
-                                  ptr(ns), ptr(ms), ptr(mrow), ptr(den), stream_of(qc))
+                                  ptr(ns), ptr(ms), ptr(mrow), ptr(den), None, stream_of(qc))
         check(rc, "sc_mlstm_fwd")
         ctx.save_for_backward(qc, kc, vc, ig, fg, h, Cs, ns, ms, mrow, den)
         ctx.meta = (B, NH, T, DQ, DV, float(eps), q.dtype, k.dtype, v.dtype, c0 is not None,
@@ -1009,7 +1010,8 @@ class MLSTMFn(torch.autograd.Function):
             rc = _lib.load().sc_mlstm_bwd(
                 ptr(qc), ptr(kc), ptr(vc), dtype_code(qc), ptr(ig), ptr(fg), ptr(h), ptr(dhc),
                 ptr(dcTc), ptr(dnTc), ptr(Cs), ptr(ns), ptr(ms), ptr(mrow), ptr(den), BH, T, DQ, DV,
-                eps, ptr(dCs), ptr(dns), ptr(dq), ptr(dk), ptr(dv), ptr(qdq), ptr(kdk), stream_of(qc))
+                eps, ptr(dCs), ptr(dns), ptr(dq), ptr(dk), ptr(dv), ptr(qdq), ptr(kdk), None,
+                stream_of(qc))
         check(rc, "sc_mlstm_bwd")
         # d igate_s = k_s.dk_s ; dF_t = q_t.dq_t - k_t.dk_t ; d fgate = sigmoid(-f) revcumsum(dF)
         dF = qdq - kdk
@@ -1019,6 +1021,140 @@ class MLSTMFn(torch.autograd.Function):
                 dv.view(B, NH, T, DV).to(vdt), kdk.view(shp), dfg.view(shp),
                 dCs[:, 0].view(B, NH, DQ, DV) if has_c0 else None,
                 dns[:, 0].view(B, NH, DQ) if has_n0 else None, None, None)
+
+
+def _soft_cap(x, cap):
+    return x if cap is None else cap * torch.tanh(x / cap)
+
+
+def _soft_cap_bwd(g, x, cap):
+    """d soft_cap(x) as autograd computes it in x's dtype (Mul, Tanh, Div backward)."""
+    if cap is None:
+        return g
+    return torch.ops.aten.tanh_backward(g * cap, torch.tanh(x / cap)) / cap
+
+
+class MLSTMCoreFn(torch.autograd.Function):
+    """The xLSTM mLSTMLayer between its fused projection and out_proj (modeling_xlstm.py
+    mLSTMLayer.forward; xlstm.mLSTMLayer): for a = [q | k | v | o | i | f] bf16 [B, T, N] (heads
+    NH, per-head DQ / DV) it returns y = bf16(sigmoid(o)) * MultiHeadLayerNorm(h) [B, T, NH DV]
+    with h = mLSTM(q, k, v, soft_cap(i), soft_cap(f)), and the final state (C, n, m).
+
+    q, k, v and o are read in place from a (sc_mlstm_* layout strides, the gated norm's row
+    stride): no split copies or head transposes.  The backward writes dq / dk / dv / do / di / df
+    straight into ONE gradient tensor of a's shape: no concatenation of six slice gradients.
+    Same kernels and roundings as MLSTMFn + GatedHeadNormFn + the torch soft caps."""
+
+    @staticmethod
+    def forward(ctx, a, c0, n0, m0, w_mh, NH, DQ, DV, cap, eps, eps_mh):
+        require_device(a)
+        B, T, N = a.shape
+        lib = _lib.load()
+        qo, ko, vo = 0, NH * DQ, 2 * NH * DQ
+        oo = vo + NH * DV
+        io, fo = oo + NH * DV, oo + NH * DV + NH
+        BH, nc = B * NH, T // 64
+        ig_raw, fg_raw = a[..., io:io + NH], a[..., fo:fo + NH]
+        ig = _soft_cap(ig_raw, cap).transpose(1, 2).float().contiguous()
+        fg = _soft_cap(fg_raw, cap).transpose(1, 2).float().contiguous()
+        c0c = None if c0 is None else c0.float().contiguous()
+        n0c = None if n0 is None else n0.float().contiguous()
+        m0c = None if m0 is None else m0.float().contiguous()
+        dev = a.device
+        esz = a.element_size()
+        base = a.data_ptr()
+        lay = (ctypes.c_int64 * 7)(NH, T * N, DQ, N, T * N, DV, N)
+        h = torch.empty(BH, T, DV, dtype=a.dtype, device=dev)
+        Cs = torch.empty(BH, nc + 1, DQ, DV, dtype=torch.float32, device=dev)
+        ns = torch.empty(BH, nc + 1, DQ, dtype=torch.float32, device=dev)
+        ms = torch.empty(BH, nc + 1, dtype=torch.float32, device=dev)
+        mrow = torch.empty(BH, T, dtype=torch.float32, device=dev)
+        den = torch.empty(BH, T, dtype=torch.float32, device=dev)
+        st_b = BH * (nc + 1) * (DQ * DV + DQ + 1) * 4
+        fwd_b = BH * T * ((2 * DQ + 2 * DV) * esz + 4 * 4) + st_b
+        stream = stream_of(a)
+        with _timed("mlstm_fwd", a, fwd_b):
+            rc = lib.sc_mlstm_fwd(base + qo * esz, base + ko * esz, base + vo * esz, dtype_code(a),
+                                  ptr(ig), ptr(fg), ptr(c0c), ptr(n0c), ptr(m0c), BH, T, DQ, DV,
+                                  float(eps), ptr(h), ptr(Cs), ptr(ns), ptr(ms), ptr(mrow),
+                                  ptr(den), lay, stream)
+        check(rc, "sc_mlstm_fwd")
+        wf = w_mh.detach().float().contiguous()
+        y = torch.empty(B, T, NH * DV, dtype=torch.bfloat16, device=dev)
+        mean = torch.empty(B * T, NH, dtype=torch.float32, device=dev)
+        rstd = torch.empty_like(mean)
+        check(lib.sc_mhln_gate_fwd(ptr(h), base + oo * esz, N, ptr(wf), ptr(y), ptr(mean), ptr(rstd),
+                                   B, T, NH, DV, float(eps_mh), stream), "sc_mhln_gate_fwd")
+        ctx.save_for_backward(a, ig, fg, h, Cs, ns, ms, mrow, den, wf, mean, rstd)
+        ctx.meta = (NH, DQ, DV, cap, float(eps), c0 is not None, n0 is not None, w_mh.dtype)
+        cT = Cs[:, nc].view(B, NH, DQ, DV).clone()
+        nT = ns[:, nc].view(B, NH, DQ).clone()
+        mT = ms[:, nc].view(B, NH, 1).clone()
+        ctx.mark_non_differentiable(mT)
+        return y, cT, nT, mT
+
+    @staticmethod
+    def backward(ctx, dy, dcT, dnT, dmT):
+        a, ig, fg, h, Cs, ns, ms, mrow, den, wf, mean, rstd = ctx.saved_tensors
+        NH, DQ, DV, cap, eps, has_c0, has_n0, wdt = ctx.meta
+        B, T, N = a.shape
+        BH, nc = B * NH, T // 64
+        qo, ko, vo = 0, NH * DQ, 2 * NH * DQ
+        oo = vo + NH * DV
+        io, fo = oo + NH * DV, oo + NH * DV + NH
+        lib = _lib.load()
+        dev = a.device
+        esz = a.element_size()
+        base = a.data_ptr()
+        stream = stream_of(a)
+        dyc = dy.to(torch.bfloat16)
+        if dyc.stride(2) != 1 or dyc.stride(0) != T * dyc.stride(1) or dyc.stride(1) % 4:
+            dyc = dyc.contiguous()
+        da = torch.empty_like(a)
+        dbase = da.data_ptr()
+        dh = torch.empty_like(h)
+        part = torch.empty(lib.sc_xlstm_part_rows(B * T), NH * DV, dtype=torch.float32, device=dev)
+        check(lib.sc_mhln_gate_bwd(ptr(h), base + oo * esz, N, ptr(wf), ptr(mean), ptr(rstd),
+                                   ptr(dyc), dyc.stride(1), ptr(dh), dbase + oo * esz, N, ptr(part),
+                                   B, T, NH, DV, stream), "sc_mhln_gate_bwd")
+        dcTc = None if dcT is None else dcT.float().contiguous()
+        dnTc = None if dnT is None else dnT.float().contiguous()
+        dCs = torch.empty_like(Cs)
+        dns = torch.empty_like(ns)
+        qdq = torch.empty(BH, T, dtype=torch.float32, device=dev)
+        kdk = torch.empty(BH, T, dtype=torch.float32, device=dev)
+        lay = (ctypes.c_int64 * 7)(NH, T * N, DQ, N, T * N, DV, N)
+        st_b = BH * (nc + 1) * (DQ * DV + DQ + 1) * 4
+        bwd_b = BH * T * ((4 * DQ + 4 * DV) * esz + 6 * 4) + 2 * st_b
+        with _timed("mlstm_bwd", a, bwd_b):
+            rc = lib.sc_mlstm_bwd(
+                base + qo * esz, base + ko * esz, base + vo * esz, dtype_code(a), ptr(ig), ptr(fg),
+                ptr(h), ptr(dh), ptr(dcTc), ptr(dnTc), ptr(Cs), ptr(ns), ptr(ms), ptr(mrow),
+                ptr(den), BH, T, DQ, DV, eps, ptr(dCs), ptr(dns), dbase + qo * esz,
+                dbase + ko * esz, dbase + vo * esz, ptr(qdq), ptr(kdk), lay, stream)
+        check(rc, "sc_mlstm_bwd")
+        # gate gradients as MLSTMFn returns them, then through the soft caps in a's dtype
+        dF = (qdq - kdk).view(B, NH, T)
+        dfg = torch.sigmoid(-fg) * dF.flip(-1).cumsum(-1).flip(-1)
+        dig_c = kdk.view(B, NH, T).transpose(1, 2).to(a.dtype)
+        dfg_c = dfg.transpose(1, 2).to(a.dtype)
+        da[..., io:io + NH] = _soft_cap_bwd(dig_c, a[..., io:io + NH], cap)
+        da[..., fo:fo + NH] = _soft_cap_bwd(dfg_c, a[..., fo:fo + NH], cap)
+        return (da, dCs[:, 0].view(B, NH, DQ, DV) if has_c0 else None,
+                dns[:, 0].view(B, NH, DQ) if has_n0 else None, None,
+                _part_sum(part).to(wdt), None, None, None, None, None, None)
+
+
+def mlstm_core_supported(a, NH, DQ, DV):
+    """MLSTMCoreFn's preconditions: bf16 ROCm a [B, T, N] contiguous, T % 64 == 0, the head
+    dims compiled in, 16-byte aligned row pieces for the strided reads."""
+    if not (a.is_cuda and a.dtype == torch.bfloat16 and a.dim() == 3 and a.is_contiguous()):
+        return False
+    B, T, N = a.shape
+    return (T % 64 == 0 and N == 2 * NH * DQ + 2 * NH * DV + 2 * NH and N % 8 == 0
+            and DQ % 8 == 0 and DV % 8 == 0 and NH <= 4 and DV in (64, 128, 192, 256)
+            and a.data_ptr() % 16 == 0
+            and bool(_lib.load().sc_mlstm_supported(_lib.SC_BF16, DQ, DV)))
 
 
 def mlstm_chunkwise(query, key, value, igate, fgate, c_initial=None, n_initial=None,
@@ -1185,10 +1321,19 @@ class AutocastLinearFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = (dy2 @ wc).view(*dy.shape[:-1], K).to(xdt)
         if ctx.needs_input_grad[1]:
-            dwm = None
+            dw = None
             if dy2.is_cuda and dy2.dtype == torch.bfloat16:
-                dwm = wgrad_mfma(dy2.contiguous(), x2.contiguous())
-            dw = (dwm if dwm is not None else (dy2.t() @ x2).float()).to(wdt)
+                dyc, xcc = dy2.contiguous(), x2.contiguous()
+                dw = wgrad_mfma(dyc, xcc)
+                n0 = N - N % 256
+                if dw is None and 256 <= n0 < N:
+                    # e.g. the xLSTM q|k|v|o|i|f projection (N = 2312 at C4): the first N0 rows
+                    # of dW on the MFMA kernel (dy's row stride 2312 is a multiple of 8), the
+                    # gate rows that remain as a small library GEMM
+                    head = wgrad_mfma(dyc[:, :n0], xcc)
+                    if head is not None:
+                        dw = torch.cat([head, dyc[:, n0:].t().float() @ xcc.float()])
+            dw = (dw if dw is not None else (dy2.t() @ x2).float()).to(wdt)
         if bdt is not None and ctx.needs_input_grad[2]:
             db = colsum(dy2).to(bdt)
         return dx, dw, db, None

@@ -153,24 +153,43 @@ class mLSTMLayer(nn.Module):
                                                  cfg.norm_reduction_force_float32)
         self.out_proj = nn.Linear(self.v_dim, d, bias=cfg.use_bias)
 
-    def projections(self, x):
-        """q, k, v, o and the two gate pre-activations from ONE GEMM over the concatenated
-        weight (the parameters and state_dict keep HF's six Linears): x is read and, under
-        autocast, cast once instead of six times, and the two NH-wide gate projections (4 output
-        columns each at C4) stop being GEMMs of their own."""
-        mods = (self.q, self.k, self.v, self.ogate_preact, self.igate_preact, self.fgate_preact)
+    def _mods(self):
+        return (self.q, self.k, self.v, self.ogate_preact, self.igate_preact, self.fgate_preact)
+
+    def projection(self, x):
+        """[q | k | v | o | i | f] from ONE GEMM over the concatenated weight (the parameters and
+        state_dict keep HF's six Linears): x is read and, under autocast, cast once instead of six
+        times, and the two NH-wide gate projections (4 output columns each at C4) stop being
+        GEMMs of their own."""
+        mods = self._mods()
         w = torch.cat([m.weight for m in mods])
         b = None
         if any(m.bias is not None for m in mods):
             b = torch.cat([m.bias if m.bias is not None else
                            torch.zeros(m.weight.shape[0], dtype=m.weight.dtype, device=m.weight.device)
                            for m in mods])
-        return _linear(x, w, b).split([m.weight.shape[0] for m in mods], -1)
+        return _linear(x, w, b)
+
+    def projections(self, x):
+        return self.projection(x).split([m.weight.shape[0] for m in self._mods()], -1)
 
     def forward(self, x, state=None):
         B, T, _ = x.shape
         NH = self.cfg.num_heads
-        q, k, v, o, ig, fg = self.projections(x)
+        mh = self.multihead_norm
+        if x.is_cuda and mh.bias is None and mh.force_float32_reductions:
+            a = self.projection(x)
+            DQ, DV = self.qk_dim // NH, self.v_dim // NH
+            if ops.mlstm_core_supported(a, NH, DQ, DV):
+                # split -> soft caps -> mLSTM cell -> gated head norm as one node reading q / k /
+                # v / o in place from the projection (ops.MLSTMCoreFn); same math and roundings
+                c0, n0, m0 = (None, None, None) if state is None else state
+                y, c, n, m = ops.MLSTMCoreFn.apply(a, c0, n0, m0, mh.weight, NH, DQ, DV,
+                                                   self.cfg.gate_soft_cap, self.cfg.eps, mh.eps)
+                return _linear(y, self.out_proj.weight, self.out_proj.bias), (c, n, m)
+            q, k, v, o, ig, fg = a.split([m.weight.shape[0] for m in self._mods()], -1)
+        else:
+            q, k, v, o, ig, fg = self.projections(x)
         q = q.reshape(B, T, NH, -1).transpose(1, 2)
         k = k.reshape(B, T, NH, -1).transpose(1, 2)
         v = v.reshape(B, T, NH, -1).transpose(1, 2)

@@ -175,3 +175,21 @@ def test_tn_gemm_rejects_bad_shapes():
     assert lib.sc_gemm_tn_bf16(a.data_ptr(), 80, b.data_ptr(), 80, c.data_ptr(), 256, 64, 200, 64,
                                0, None) != 0   # N % 256
     assert not ops().tn_ok(a, b)
+
+
+def test_autocast_linear_wgrad_split_head():
+    """AutocastLinearFn's weight gradient for N not a multiple of 256 (the xLSTM q|k|v|o|i|f
+    projection, N = 2312 at C4): the first N - N % 256 rows on the MFMA kernel, the rest on the
+    library; against fp32 torch at 1e-5 of the largest |dW| (fp32 summation order)."""
+    g = torch.Generator(device=DEV).manual_seed(11)
+    x = torch.randn(4096, 768, device=DEV, generator=g).to(torch.bfloat16).float()
+    w = torch.randn(2312, 768, device=DEV, generator=g) * 0.02
+    dy = torch.randn(4096, 2312, device=DEV, generator=g).to(torch.bfloat16)
+    xr = x.clone().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = ops().autocast_linear(xr, wr)
+    y.backward(dy)
+    ref = dy.float().t() @ x
+    err = (wr.grad - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 1e-5, err

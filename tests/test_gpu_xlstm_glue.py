@@ -97,10 +97,12 @@ def test_xlstm_block_fused_equals_torch_path():
     x = torch.randn(2, 128, 256, device=DEV)
     outs = []
     for fused in (True, False):
-        saved = (xlstm.ops.xlstm_glue_supported, xlstm.ops.gated_head_norm_supported)
+        saved = (xlstm.ops.xlstm_glue_supported, xlstm.ops.gated_head_norm_supported,
+                 xlstm.ops.mlstm_core_supported)
         if not fused:
             xlstm.ops.xlstm_glue_supported = lambda *a: False
             xlstm.ops.gated_head_norm_supported = lambda *a: False
+            xlstm.ops.mlstm_core_supported = lambda *a: False
         try:
             blk.zero_grad()
             xi = x.clone().requires_grad_(True)
@@ -110,7 +112,8 @@ def test_xlstm_block_fused_equals_torch_path():
             outs.append((y.float(), xi.grad.clone(),
                          {n: p.grad.clone() for n, p in blk.named_parameters()}))
         finally:
-            xlstm.ops.xlstm_glue_supported, xlstm.ops.gated_head_norm_supported = saved
+            (xlstm.ops.xlstm_glue_supported, xlstm.ops.gated_head_norm_supported,
+             xlstm.ops.mlstm_core_supported) = saved
     (yf, gxf, pf), (yt, gxt, pt) = outs
     assert rel(yf, yt) < 1e-2
     assert rel(gxf, gxt) < 3e-2
@@ -120,3 +123,40 @@ def test_xlstm_block_fused_equals_torch_path():
     for n in pt:
         err = float((pf[n].double() - pt[n].double()).norm())
         assert err <= 3e-2 * float(pt[n].norm()) + 1e-3 * gmax, (n, err, float(pt[n].norm()))
+
+
+@pytest.mark.parametrize("with_state", [False, True])
+def test_mlstm_core_equals_composed_ops(with_state, monkeypatch):
+    """ops.MLSTMCoreFn (q/k/v/o read in place from the fused projection, one gradient tensor
+    written in place) against the composed path it replaces (split, soft caps, MLSTMFn,
+    GatedHeadNormFn, autograd's concatenation): same kernels and roundings, so the layer output,
+    the final state and every gradient are bit-identical."""
+    from statecatcher_amd import xlstm
+    cfg = xlstm.xLSTMLargeConfig(embedding_dim=256, num_heads=4, num_blocks=1, vocab_size=64)
+    torch.manual_seed(1)
+    layer = xlstm.mLSTMLayer(cfg).to(DEV)
+    with torch.no_grad():
+        for m in layer._mods():
+            m.weight.mul_(3.0)
+        layer.multihead_norm.weight.uniform_(0.5, 1.5)
+    x = torch.randn(2, 192, 256, device=DEV)
+    st = None
+    if with_state:
+        g = torch.Generator(device=DEV).manual_seed(2)
+        st = (torch.randn(2, 4, 32, 64, device=DEV, generator=g) * 0.1,
+              torch.randn(2, 4, 32, device=DEV, generator=g) * 0.1,
+              torch.zeros(2, 4, 1, device=DEV))
+    res = []
+    for core in (True, False):
+        if not core:
+            monkeypatch.setattr(xlstm.ops, "mlstm_core_supported", lambda *a: False)
+        layer.zero_grad(set_to_none=True)
+        xi = x.clone().requires_grad_(True)
+        sti = None if st is None else tuple(t.clone().requires_grad_(i < 2) for i, t in enumerate(st))
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y, (c, n, m) = layer(xi, sti)
+        (y.float().square().mean() + c.square().mean() + n.mean()).backward()
+        res.append([y, c, n, m, xi.grad] + [p.grad for p in layer.parameters()] +
+                   ([sti[0].grad, sti[1].grad] if sti else []))
+    for i, (u, v) in enumerate(zip(*res)):
+        assert torch.equal(u, v), i
