@@ -1295,6 +1295,20 @@ def swiglu(a):
     return SwiGLUFn.apply(a)
 
 
+_MM_DTYPE = [True]
+
+
+def _mm_f32(a, b):
+    """a @ b with fp32 output for bf16 operands (aten::mm.dtype: fp32 accumulate, no rounding
+    of the product to bf16), or in fp32 when that overload is unavailable."""
+    if _MM_DTYPE[0]:
+        try:
+            return torch.mm(a, b, out_dtype=torch.float32)
+        except (RuntimeError, TypeError, NotImplementedError):
+            _MM_DTYPE[0] = False
+    return a.float() @ b.float()
+
+
 class AutocastLinearFn(torch.autograd.Function):
     """y = x W^T (+ b) in the autocast dtype (what nn.Linear does under bf16 autocast) with a
     backward that takes the weight gradient from the MFMA split-L kernel when the shape fits
@@ -1332,7 +1346,7 @@ class AutocastLinearFn(torch.autograd.Function):
                     # gate rows that remain as a small library GEMM
                     head = wgrad_mfma(dyc[:, :n0], xcc)
                     if head is not None:
-                        dw = torch.cat([head, dyc[:, n0:].t().float() @ xcc.float()])
+                        dw = torch.cat([head, _mm_f32(dyc[:, n0:].t(), xcc)])
             dw = (dw if dw is not None else (dy2.t() @ x2).float()).to(wdt)
         if bdt is not None and ctx.needs_input_grad[2]:
             db = colsum(dy2).to(bdt)

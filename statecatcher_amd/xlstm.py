@@ -37,6 +37,19 @@ def _linear(x, w, b=None):
     return F.linear(x, w, b)
 
 
+_ZEROS = {}
+
+
+def _zeros(n, dtype, device):
+    """A cached zero bias piece (read only): the concatenated projection bias of the bias-free
+    q / k / v / o Linears takes no fill launch per call."""
+    key = (n, dtype, str(device))
+    z = _ZEROS.get(key)
+    if z is None:
+        z = _ZEROS[key] = torch.zeros(n, dtype=dtype, device=device)
+    return z
+
+
 def soft_cap(x, cap):
     return x if cap is None else cap * torch.tanh(x / cap)
 
@@ -166,7 +179,7 @@ class mLSTMLayer(nn.Module):
         b = None
         if any(m.bias is not None for m in mods):
             b = torch.cat([m.bias if m.bias is not None else
-                           torch.zeros(m.weight.shape[0], dtype=m.weight.dtype, device=m.weight.device)
+                           _zeros(m.weight.shape[0], m.weight.dtype, m.weight.device)
                            for m in mods])
         return _linear(x, w, b)
 
