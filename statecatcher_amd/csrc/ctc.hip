@@ -220,6 +220,53 @@ __device__ __forceinline__ float lse3_live(float a, float b, float c) {
 
 constexpr int kAbP = 16;   // emission prefetch depth (steps)
 
+#ifndef SC_CTC_V2   // 1: lattice step without canonicalising max/min, emission selects or a swap
+#define SC_CTC_V2 1
+#endif
+// max / min / max3 / min3 as single instructions: fmaxf & co. make LLVM canonicalise loop-carried
+// operands first (one extra v_max per value per step); the lattice never holds NaN it must quiet
+__device__ __forceinline__ float vmax(float a, float b) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ float vmin(float a, float b) {
+  float r;
+  asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ float vmax3(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ float vmin3(float a, float b, float c) {
+  float r;
+  asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+// lane shifts with bound_ctrl: the lane with no source neighbour reads 0, not a "dead" value.
+// That lane is always a halo lane (alpha: lane 0, beta: lane 63 of every wave), whose values
+// are never published and are overwritten at each exchange; saves the v_mov of an old value.
+__device__ __forceinline__ float shr1z(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x138, 0xf, 0xf, true));
+}
+__device__ __forceinline__ float shl1z(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x130, 0xf, 0xf, true));
+}
+typedef float f2v __attribute__((ext_vector_type(2)));
+// (lse2(a2, b2) + e.x, lse3(a3, b3, c3) + e.y) in base 2: the max terms are exp2(0) = 1; the
+// emission pair joins the maxima while the exponentials run, and the two results leave as one
+// packed pair (what the store and the next step's DPP read)
+__device__ __forceinline__ f2v lse23(float a2, float b2, float a3, float b3, float c3, f2v e) {
+  const float m2 = vmax(a2, b2), l2 = vmin(a2, b2);
+  const float m3 = vmax3(a3, b3, c3), d3 = __builtin_amdgcn_fmed3f(a3, b3, c3);
+  const float l3 = vmin3(a3, b3, c3);
+  const f2v me = f2v{m2, m3} + e;
+  const f2v s = f2v{1.0f, 1.0f} + f2v{exp2_(l2 - m2), exp2_(d3 - m3)};
+  return me + f2v{log2_(s.x), log2_(s.y + exp2_(l3 - m3))};
+}
+
 
 __device__ __forceinline__ float lse2_live(float a, float b) {
   const float m = fmaxf(a, b);
@@ -278,10 +325,25 @@ __device__ __forceinline__ void ab_run(const CtcArgs& a, int b, int Tb, int Ub) 
   if (tid == 0) offn[0] = 0.0;
   auto tstep = [&](int i) { return BETA ? Tb - 1 - i : i; };
   float2 bufA[kAbP], bufB[kAbP];
+#if SC_CTC_V2
+  // emission pairs through a buffer descriptor: lanes outside the row (alpha's leading halo,
+  // pairs past Sp) get an out-of-range offset and read 0, which keeps a dead state dead (its
+  // inputs are all dead); live lanes past 2 Ub + 1 read the -1e30 padding ctc_emit wrote
+  const __amdgpu_buffer_rsrc_t ers = __builtin_amdgcn_make_buffer_rsrc(
+      a.ws.lpe + (int64_t)b * a.T * a.Sp, 0, (int)(rowb * (uint32_t)a.T), 0x00020000);
+  const uint32_t evo = (p >= 0 && 2 * p < a.Sp) ? (uint32_t)(8 * p) : kDrop;
+  auto load = [&](float2 (&buf)[kAbP], int i0) {
+#pragma unroll
+    for (int j = 0; j < kAbP; ++j)
+      buf[j] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(
+                                              ers, evo, (uint32_t)tstep(min(i0 + j, Tb - 1)) * rowb, 0));
+  };
+#else
   auto load = [&](float2 (&buf)[kAbP], int i0) {
 #pragma unroll
     for (int j = 0; j < kAbP; ++j) buf[j] = lrow[(int64_t)tstep(min(i0 + j, Tb - 1)) * rs];
   };
+#endif
   auto emit = [&](int t, float vB, float vL) {
     __builtin_amdgcn_raw_buffer_store_b64(
         __builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, make_float2(vB, vL)), ors,
@@ -295,6 +357,23 @@ __device__ __forceinline__ void ab_run(const CtcArgs& a, int b, int Tb, int Ub) 
     for (int j = 0; j < kAbP; ++j) {
       const int i = i0 + j;
       if (i >= Tb) break;
+#if SC_CTC_V2
+      if (i == 0) {
+        vB = (liveB && p == (BETA ? Ub : 0)) ? buf[j].x : kDead;
+        vL = (liveL && p == (BETA ? Ub - 1 : 0)) ? buf[j].y : kDead;
+      } else if (!BETA) {
+        const float lp = shr1z(vL);
+        const f2v r = lse23(vB, lp, vL, vB, skip ? lp : kDead, f2v{buf[j].x, buf[j].y});
+        vB = r.x;
+        vL = r.y;
+      } else {
+        const float bn = shl1z(vB);
+        const float ln = shl1z(vL);
+        const f2v r = lse23(vB, vL, vL, bn, skip ? ln : kDead, f2v{buf[j].x, buf[j].y});
+        vB = r.x;
+        vL = r.y;
+      }
+#else
       const float eB = liveB ? buf[j].x : kDead;
       const float eL = liveL ? buf[j].y : kDead;
       if (i == 0) {
@@ -312,6 +391,7 @@ __device__ __forceinline__ void ab_run(const CtcArgs& a, int b, int Tb, int Ub) 
         vL = lse3_live(vL, bn, skip ? ln : kDead) + eL;
         vB = nB;
       }
+#endif
       if (!(SC_CTC_ABL & 1) && j % K == K - 1) {   // halo exchange (+ re-centre every 2nd)
         const int par = exch & 1;
         const bool norm = par == 1;
