@@ -254,6 +254,23 @@ __device__ __forceinline__ float shr1z(float v) {
 __device__ __forceinline__ float shl1z(float v) {
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x130, 0xf, 0xf, true));
 }
+// max over the 64 lanes through DPP (quad perms, row mirrors, row broadcasts), result read
+// from lane 63: a dozen VALU cycles instead of six LDS round trips of __shfl_xor
+template <int CTRL, int RMASK>
+__device__ __forceinline__ float dpp_max_step(float v) {
+  const float o = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v),
+                                                             CTRL, RMASK, 0xf, false));
+  return vmax(v, o);
+}
+__device__ __forceinline__ float wave_max_dpp(float x) {
+  x = dpp_max_step<0xB1, 0xf>(x);    // quad_perm [1,0,3,2]
+  x = dpp_max_step<0x4E, 0xf>(x);    // quad_perm [2,3,0,1]
+  x = dpp_max_step<0x141, 0xf>(x);   // row_half_mirror
+  x = dpp_max_step<0x140, 0xf>(x);   // row_mirror: every lane holds its row's max
+  x = dpp_max_step<0x142, 0xa>(x);   // row_bcast:15 into rows 1, 3
+  x = dpp_max_step<0x143, 0xc>(x);   // row_bcast:31 into rows 2, 3: lane 63 holds the max
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 63));
+}
 typedef float f2v __attribute__((ext_vector_type(2)));
 // (lse2(a2, b2) + e.x, lse3(a3, b3, c3) + e.y) in base 2: the max terms are exp2(0) = 1; the
 // emission pair joins the maxima while the exponentials run, and the two results leave as one
@@ -398,8 +415,12 @@ __device__ __forceinline__ void ab_run(const CtcArgs& a, int b, int Tb, int Ub) 
         if (own) full2[par * nst + p] = make_float2(vB, vL);
         if (norm) {
           float m = own ? fmaxf(vB, vL) : kDead;
+#if SC_CTC_V2
+          m = wave_max_dpp(m);
+#else
 #pragma unroll
           for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+#endif
           if (lane == 0) wmax[w] = m;
         }
         lds_barrier();
