@@ -304,6 +304,7 @@ __device__ __forceinline__ float lse2_live(float a, float b) {
 template <int K, bool BETA>
 __device__ __forceinline__ void ab_run(const CtcArgs& a, int b, int Tb, int Ub) {
   constexpr int OW = 64 - K;      // owned pairs per wave
+  constexpr int kAbP = K > 16 ? K : 16;   // emission prefetch depth: a multiple of K
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int w = uniform(tid >> 6);
@@ -498,8 +499,13 @@ __global__ void __launch_bounds__(1024) ctc_ab_kernel(CtcArgs a) {
 // K (steps between halo exchanges) so that ceil((Umax + 1) / (64 - K)) waves of state pairs fit
 // a 1024-thread group
 static int ab_halo_k(int Umax) {
+  auto waves = [&](int K) { return (Umax + 1 + (64 - K) - 1) / (64 - K); };
   for (int K : {SC_CTC_KMAX, 4, 2, 1})
-    if ((Umax + 1 + (64 - K) - 1) / (64 - K) <= 16) return K;
+    if (waves(K) <= 16) {
+      // a wider halo with the same wave count: fewer exchanges (barriers) per step
+      if (SC_CTC_KMAX == 16 && K == 16 && waves(24) == waves(16)) return 24;
+      return K;
+    }
   return 0;
 }
 
@@ -631,6 +637,7 @@ static void launch_fwd(const CtcArgs& a, hipStream_t st) {
   const size_t sh = 2 * (size_t)nw * (64 - K) * sizeof(float2);
   switch (K) {
 #if SC_CTC_KMAX == 16
+    case 24: hipLaunchKernelGGL((ctc_ab_kernel<24>), dim3(2 * a.B), dim3(64 * nw), sh, st, a); break;
     case 16: hipLaunchKernelGGL((ctc_ab_kernel<16>), dim3(2 * a.B), dim3(64 * nw), sh, st, a); break;
 #endif
     case 8: hipLaunchKernelGGL((ctc_ab_kernel<8>), dim3(2 * a.B), dim3(64 * nw), sh, st, a); break;
