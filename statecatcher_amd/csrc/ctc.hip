@@ -114,6 +114,33 @@ __device__ __forceinline__ int state_label(const int64_t* tg, int s, int blank, 
   return lab < 0 ? 0 : (lab >= V ? V - 1 : lab);
 }
 
+// ---------------------------------------------------------------------------- wave reductions
+// over the 64 lanes through DPP (quad perms, row mirrors, row broadcasts), result read from lane
+// 63: a dozen VALU cycles instead of six LDS round trips of __shfl_xor
+__device__ __forceinline__ float vmax(float a, float b) {   // no NaN canonicalisation (see below)
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+template <int CTRL, int RMASK, bool MAX>
+__device__ __forceinline__ float dpp_step(float v) {
+  const float o = __int_as_float(__builtin_amdgcn_update_dpp(
+      __float_as_int(MAX ? v : 0.0f), __float_as_int(v), CTRL, RMASK, 0xf, false));
+  return MAX ? vmax(v, o) : v + o;
+}
+template <bool MAX>
+__device__ __forceinline__ float wave_reduce_dpp(float x) {
+  x = dpp_step<0xB1, 0xf, MAX>(x);    // quad_perm [1,0,3,2]
+  x = dpp_step<0x4E, 0xf, MAX>(x);    // quad_perm [2,3,0,1]
+  x = dpp_step<0x141, 0xf, MAX>(x);   // row_half_mirror
+  x = dpp_step<0x140, 0xf, MAX>(x);   // row_mirror: every lane holds its row's result
+  x = dpp_step<0x142, 0xa, MAX>(x);   // row_bcast:15 into rows 1, 3
+  x = dpp_step<0x143, 0xc, MAX>(x);   // row_bcast:31 into rows 2, 3: lane 63 holds the result
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 63));
+}
+__device__ __forceinline__ float wave_max_dpp(float x) { return wave_reduce_dpp<true>(x); }
+__device__ __forceinline__ float wave_sum_dpp(float x) { return wave_reduce_dpp<false>(x); }
+
 // ---------------------------------------------------------------------------- emissions -----
 template <int DT>
 __global__ void __launch_bounds__(256) ctc_emit_kernel(CtcArgs a) {
@@ -151,15 +178,11 @@ __global__ void __launch_bounds__(256) ctc_emit_kernel(CtcArgs a) {
         m = mn;
       }
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const float mo = __shfl_xor(m, o);
-      const float lo = __shfl_xor(l, o);
-      const float mn = fmaxf(m, mo);
-      l = (mn == kNegInf) ? 0.0f : l * fexp(m - mn) + lo * fexp(mo - mn);
-      m = mn;
-    }
-    lse = m + flog(l);
+    // the row max, then every lane's partial sum rescaled to it and summed (NaN in l
+    // propagates as before)
+    const float M = wave_max_dpp(m);
+    l = wave_sum_dpp(m == kNegInf ? 0.0f : l * fexp(m - M));
+    lse = M + flog(l);
     if (lane == 0) a.ws.lse[row] = lse;
   }
   const int Sb = 2 * clampi(a.tgt_lens[b], 0, a.Umax) + 1;
@@ -174,23 +197,39 @@ __global__ void __launch_bounds__(256) ctc_emit_kernel(CtcArgs a) {
 
 // ---------------------------------------------------------------------------- chains --------
 __global__ void __launch_bounds__(256) ctc_chain_kernel(CtcArgs a) {
+  // one wave per target position u (4 per workgroup): the next and any earlier position with
+  // the same label, 64 candidates per ballot
   __shared__ int lt[1024];   // the target row (Umax <= 1007)
   const int b = blockIdx.x;
+  const int lane = threadIdx.x & 63;
   const int Ub = clampi(a.tgt_lens[b], 0, a.Umax);
   const int64_t* tg = a.tg + (int64_t)b * a.tgs;
   const int Um = a.Umax > 0 ? a.Umax : 1;
   for (int u = threadIdx.x; u < Ub; u += blockDim.x) lt[u] = (int)tg[u];
   __syncthreads();
-  for (int u = threadIdx.x; u < Um; u += blockDim.x) {
-    int nxt = -1, first = 0;
-    if (u < Ub) {
-      const int lab = lt[u];
-      for (int q = u + 1; q < Ub; ++q)
-        if (lt[q] == lab) { nxt = q; break; }
-      first = 1;
-      for (int q = 0; q < u; ++q)
-        if (lt[q] == lab) { first = 0; break; }
+  const int u = blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (u >= Um) return;
+  int nxt = -1, first = 0;
+  if (u < Ub) {
+    const int lab = lt[u];
+    for (int q0 = u + 1; q0 < Ub; q0 += 64) {
+      const int q = q0 + lane;
+      const unsigned long long hit = __ballot(q < Ub && lt[q] == lab);
+      if (hit) {
+        nxt = q0 + __ffsll(hit) - 1;
+        break;
+      }
     }
+    first = 1;
+    for (int q0 = 0; q0 < u; q0 += 64) {
+      const int q = q0 + lane;
+      if (__ballot(q < u && lt[q] == lab)) {
+        first = 0;
+        break;
+      }
+    }
+  }
+  if (lane == 0) {
     a.ws.chain[(int64_t)b * Um + u] = nxt;
     a.ws.first[(int64_t)b * Um + u] = first;
   }
@@ -225,11 +264,6 @@ constexpr int kAbP = 16;   // emission prefetch depth (steps)
 #endif
 // max / min / max3 / min3 as single instructions: fmaxf & co. make LLVM canonicalise loop-carried
 // operands first (one extra v_max per value per step); the lattice never holds NaN it must quiet
-__device__ __forceinline__ float vmax(float a, float b) {
-  float r;
-  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-  return r;
-}
 __device__ __forceinline__ float vmin(float a, float b) {
   float r;
   asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
@@ -253,23 +287,6 @@ __device__ __forceinline__ float shr1z(float v) {
 }
 __device__ __forceinline__ float shl1z(float v) {
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x130, 0xf, 0xf, true));
-}
-// max over the 64 lanes through DPP (quad perms, row mirrors, row broadcasts), result read
-// from lane 63: a dozen VALU cycles instead of six LDS round trips of __shfl_xor
-template <int CTRL, int RMASK>
-__device__ __forceinline__ float dpp_max_step(float v) {
-  const float o = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v),
-                                                             CTRL, RMASK, 0xf, false));
-  return vmax(v, o);
-}
-__device__ __forceinline__ float wave_max_dpp(float x) {
-  x = dpp_max_step<0xB1, 0xf>(x);    // quad_perm [1,0,3,2]
-  x = dpp_max_step<0x4E, 0xf>(x);    // quad_perm [2,3,0,1]
-  x = dpp_max_step<0x141, 0xf>(x);   // row_half_mirror
-  x = dpp_max_step<0x140, 0xf>(x);   // row_mirror: every lane holds its row's max
-  x = dpp_max_step<0x142, 0xa>(x);   // row_bcast:15 into rows 1, 3
-  x = dpp_max_step<0x143, 0xc>(x);   // row_bcast:31 into rows 2, 3: lane 63 holds the max
-  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 63));
 }
 typedef float f2v __attribute__((ext_vector_type(2)));
 // (lse2(a2, b2) + e.x, lse3(a3, b3, c3) + e.y) in base 2: the max terms are exp2(0) = 1; the
@@ -631,7 +648,8 @@ template <int DT>
 static void launch_fwd(const CtcArgs& a, hipStream_t st) {
   const int64_t rows = (int64_t)a.B * a.T;
   hipLaunchKernelGGL((ctc_emit_kernel<DT>), dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, a);
-  hipLaunchKernelGGL(ctc_chain_kernel, dim3(a.B), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(ctc_chain_kernel, dim3(a.B, ((a.Umax > 0 ? a.Umax : 1) + 3) / 4), dim3(256), 0,
+                     st, a);
   const int K = a.kh;
   const int nw = (a.Umax + 1 + (64 - K) - 1) / (64 - K);
   const size_t sh = 2 * (size_t)nw * (64 - K) * sizeof(float2);
