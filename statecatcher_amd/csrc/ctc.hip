@@ -599,13 +599,10 @@ __global__ void __launch_bounds__(256) ctc_grad_kernel(CtcArgs a) {
       }
     }
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const float mo = __shfl_xor(m, o);
-    const float lo = __shfl_xor(l, o);
-    const float mn = fmaxf(m, mo);
-    l = (mn == kNegInf) ? 0.0f : l * exp2_(m - mn) + lo * exp2_(mo - mn);
-    m = mn;
+  {   // the blank occupancy's log-sum-exp over the lanes (DPP: max, then rescaled sum)
+    const float M = wave_max_dpp(m);
+    l = wave_sum_dpp(m == kNegInf ? 0.0f : l * exp2_(m - M));
+    m = M;
   }
   if (lane == 0 && a.blank >= 0 && a.blank < a.V) lcab[a.blank] = (m == kNegInf) ? kNegInf : m + log2_(l);
   wave_lds_sync();
