@@ -53,8 +53,7 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(LnArgs a) {
       s += xv[c][k];
     }
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  s = wave_sum_dpp(s);
   const float mu = s / (float)a.D;
   float q2 = 0.0f;
 #pragma unroll
@@ -64,8 +63,7 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(LnArgs a) {
       const float dv = xv[c][k] - mu;
       q2 += dv * dv;
     }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) q2 += __shfl_xor(q2, o);
+  q2 = wave_sum_dpp(q2);
   const float rs = rsq(q2 / (float)a.D + a.eps);
   Vec<T, VEC>* yr = (Vec<T, VEC>*)((T*)a.y + row * a.D);
 #pragma unroll
@@ -121,11 +119,8 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(LnArgs a) {
         s2 += dxh[c][k] * xh[c][k];
       }
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      s1 += __shfl_xor(s1, o);
-      s2 += __shfl_xor(s2, o);
-    }
+    s1 = wave_sum_dpp(s1);
+    s2 = wave_sum_dpp(s2);
     s1 *= invD;
     s2 *= invD;
     Vec<T, VEC>* outr = (Vec<T, VEC>*)((T*)a.y + row * a.D);

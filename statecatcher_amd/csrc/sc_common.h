@@ -228,4 +228,33 @@ __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
+// ------------------------------------------------------------------ wave reductions ---------
+// over the 64 lanes through DPP (quad perms, row mirrors, row broadcasts), result read from lane
+// 63: a dozen VALU cycles instead of six LDS round trips of __shfl_xor
+// v_max_f32 as one instruction: fmaxf makes LLVM canonicalise operands it cannot prove canonical
+// (an extra v_max each); callers never hold a NaN they must quiet
+__device__ __forceinline__ float vmax(float a, float b) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+template <int CTRL, int RMASK, bool MAX>
+__device__ __forceinline__ float dpp_step(float v) {
+  const float o = __int_as_float(__builtin_amdgcn_update_dpp(
+      __float_as_int(MAX ? v : 0.0f), __float_as_int(v), CTRL, RMASK, 0xf, false));
+  return MAX ? vmax(v, o) : v + o;
+}
+template <bool MAX>
+__device__ __forceinline__ float wave_reduce_dpp(float x) {
+  x = dpp_step<0xB1, 0xf, MAX>(x);    // quad_perm [1,0,3,2]
+  x = dpp_step<0x4E, 0xf, MAX>(x);    // quad_perm [2,3,0,1]
+  x = dpp_step<0x141, 0xf, MAX>(x);   // row_half_mirror
+  x = dpp_step<0x140, 0xf, MAX>(x);   // row_mirror: every lane holds its row's result
+  x = dpp_step<0x142, 0xa, MAX>(x);   // row_bcast:15 into rows 1, 3
+  x = dpp_step<0x143, 0xc, MAX>(x);   // row_bcast:31 into rows 2, 3: lane 63 holds the result
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 63));
+}
+__device__ __forceinline__ float wave_max_dpp(float x) { return wave_reduce_dpp<true>(x); }
+__device__ __forceinline__ float wave_sum_dpp(float x) { return wave_reduce_dpp<false>(x); }
+
 }  // namespace sc
