@@ -121,8 +121,7 @@ __global__ void __launch_bounds__(256) rnnt_emit_kernel(RnntArgs a) {
         for (int k = 0; k < VL::N; ++k) m = fmaxf(m, f[j][k]);
       }
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    m = wave_max_dpp(m);
     float l = 0.0f;
 #pragma unroll
     for (int j = 0; j < kNvMax; ++j)
@@ -130,8 +129,7 @@ __global__ void __launch_bounds__(256) rnnt_emit_kernel(RnntArgs a) {
 #pragma unroll
         for (int k = 0; k < VL::N; ++k) l += fexp(f[j][k] - m);
       }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) l += __shfl_xor(l, o);
+    l = wave_sum_dpp(l);
     lse = m + flog(l);
   } else if (a.is_logits) {      // any V / alignment: online max-rescaled sum
     float m = -__builtin_huge_valf(), l = 0.0f;
@@ -259,9 +257,7 @@ __device__ __forceinline__ void ab_run(const RnntArgs& a, int b, int Tb, int Ub)
         const bool norm = par == 1;
         if (own && u < nst) pub[par * nst + u] = v;
         if (norm) {
-          float m = own ? v : kDeadR;
-#pragma unroll
-          for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+          const float m = wave_max_dpp(own ? v : kDeadR);
           if (lane == 0) wmax[w] = m;
         }
         lds_barrier();
