@@ -1,0 +1,443 @@
+// TORCH_LIBRARY(statecatcher, m): the hot-path ops of include/statecatcher.h registered with the
+// PyTorch dispatcher, so they are visible to torch.compile, FakeTensor and
+// torch.library.opcheck instead of being opaque ctypes calls.
+//
+//   CUDA (= HIP on ROCm) kernels: thin wrappers that check shapes, allocate outputs through the
+//     caching allocator and call the C-ABI on the current HIP stream (no host synchronisation);
+//   Meta kernels: the output shapes/dtypes only, for FakeTensor tracing;
+//   autograd: registered from Python (statecatcher_amd/torch_library.py) over the *_bwd ops.
+//
+// Reference interfaces these replace (the Triton launches / torch calls of the hot path):
+//   lucy_scan_fwd   rnn_forward_unfused_rmsnorm[(B, D)](...)      lucyrnn_triton.py:61-73, :180-244
+//   lucy_scan_bwd   (absent in the reference: its Triton kernel has no backward)
+//   decay_scan_fwd  fused_decay_scan[(B, D)](...)                  lucyrnn_triton.py:158-177
+//   layer_norm_*    nn.LayerNorm(D) between layers                 lucyrnn_triton.py:96-97, :136-137
+//   ctc_fwd/_bwd    nn.CTCLoss(blank, zero_infinity) on log_softmax  train.py:142, model.py:60-71
+//   ctc_greedy_decode  decoder.py:3-30
+// There is no CPU kernel: calling an op on CPU tensors raises (no silent fallback).
+
+#include <ATen/ATen.h>
+#include <c10/core/DeviceGuard.h>
+#include <c10/hip/HIPStream.h>
+#include <torch/library.h>
+
+#include <tuple>
+
+#include "statecatcher.h"
+
+namespace {
+
+using at::Tensor;
+using c10::optional;
+
+void sc_check(int rc, const char* what) {
+  TORCH_CHECK(rc == 0, what, ": ", (rc < 0 ? "invalid argument: " : "HIP error: "),
+              sc_last_error());
+}
+
+void* stream_for(const Tensor& t) {
+  return (void*)c10::hip::getCurrentHIPStream(t.device().index()).stream();
+}
+
+int dtype_code(const Tensor& t) {
+  switch (t.scalar_type()) {
+    case at::kFloat: return SC_F32;
+    case at::kBFloat16: return SC_BF16;
+    case at::kHalf: return SC_F16;
+    default: TORCH_CHECK(false, "statecatcher: unsupported dtype ", t.scalar_type(),
+                         " (float32, bfloat16 or float16)");
+  }
+  return -1;
+}
+
+const void* opt_ptr(const optional<Tensor>& t) { return t && t->defined() ? t->data_ptr() : nullptr; }
+
+// (B, T, D, gate strides bt, td, cd, cb) of [B,T,7,D] or step-blocked [B,T,D/64,7,64] gates
+// (include/statecatcher.h, sc_lucy_scan_fwd)
+struct GateLayout { int64_t B, T, D, bt, td, cd, cb; };
+
+GateLayout gate_layout(const Tensor& g) {
+  if (g.dim() == 4 && g.size(2) == 7 && g.stride(3) == 1)
+    return {g.size(0), g.size(1), g.size(3), g.stride(0), g.stride(1), g.stride(2), 64};
+  if (g.dim() == 5 && g.size(3) == 7 && g.size(4) == 64 && g.stride(4) == 1)
+    return {g.size(0), g.size(1), g.size(2) * 64, g.stride(0), g.stride(1), g.stride(3), g.stride(2)};
+  TORCH_CHECK(false, "statecatcher::lucy_scan: gates must be [B,T,7,D] or [B,T,D/64,7,64] with unit "
+              "inner stride, got ", g.sizes(), " strides ", g.strides());
+  return {};
+}
+
+// shape-only part of gate_layout (meta tensors carry strides too, but a fake [B,T,7,D] may be
+// non-contiguous in the inner dim; the real kernel makes it contiguous first)
+std::tuple<int64_t, int64_t, int64_t> gate_dims(const Tensor& g) {
+  if (g.dim() == 4 && g.size(2) == 7) return {g.size(0), g.size(1), g.size(3)};
+  if (g.dim() == 5 && g.size(3) == 7 && g.size(4) == 64) return {g.size(0), g.size(1), g.size(2) * 64};
+  TORCH_CHECK(false, "statecatcher::lucy_scan: gates must be [B,T,7,D] or [B,T,D/64,7,64], got ",
+              g.sizes());
+  return {};
+}
+
+Tensor f32c(const Tensor& t) { return t.to(at::kFloat).contiguous(); }
+
+// ------------------------------------------------------------------------ LucyRNN scan --------
+std::tuple<Tensor, Tensor, Tensor, Tensor> lucy_scan_fwd_hip(const Tensor& gates_in, const Tensor& h0,
+                                                             const Tensor& s0,
+                                                             const optional<Tensor>& bias,
+                                                             bool need_ckpt) {
+  c10::DeviceGuard guard(gates_in.device());
+  Tensor gates = gates_in;
+  if (gates.dim() == 4 && gates.size(2) == 7 && gates.stride(3) != 1) gates = gates.contiguous();
+  const GateLayout L = gate_layout(gates);
+  TORCH_CHECK(h0.sizes() == at::IntArrayRef({L.B, L.D}) && s0.sizes() == at::IntArrayRef({L.B, L.D}),
+              "statecatcher::lucy_scan_fwd: h0/s0 must be [B,D]=[", L.B, ",", L.D, "]");
+  // the reference reads h0/s0 as contiguous even when handed a strided view
+  Tensor h0c = f32c(h0), s0c = f32c(s0);
+  optional<Tensor> bc;
+  if (bias && bias->defined()) {
+    TORCH_CHECK(bias->numel() == 7 * L.D, "statecatcher::lucy_scan_fwd: gate_bias must have 7*D elements");
+    bc = f32c(*bias);
+  }
+  auto opt = gates.options();
+  Tensor out = at::empty({L.B, L.T, L.D}, opt);
+  Tensor s_out = at::empty({L.B, L.D}, opt.dtype(at::kFloat));
+  Tensor h_out = at::empty({L.B, L.D}, opt.dtype(at::kFloat));
+  Tensor ckpt = at::empty({need_ckpt ? sc_lucy_scan_ckpt_numel(L.B, L.T, L.D) : 0}, opt.dtype(at::kFloat));
+  sc_check(sc_lucy_scan_fwd(gates.data_ptr(), dtype_code(gates), (const float*)opt_ptr(bc),
+                            h0c.data_ptr<float>(), s0c.data_ptr<float>(), out.data_ptr(),
+                            s_out.data_ptr<float>(), h_out.data_ptr<float>(), L.B, L.T, L.D, L.bt,
+                            L.td, L.cd, L.cb, out.stride(0), out.stride(1),
+                            need_ckpt ? ckpt.data_ptr<float>() : nullptr, stream_for(gates)),
+           "statecatcher::lucy_scan_fwd");
+  return {out, s_out, h_out, ckpt};
+}
+
+std::tuple<Tensor, Tensor, Tensor, Tensor> lucy_scan_fwd_meta(const Tensor& gates, const Tensor& h0,
+                                                              const Tensor& s0,
+                                                              const optional<Tensor>& bias,
+                                                              bool need_ckpt) {
+  auto [B, T, D] = gate_dims(gates);
+  auto opt = gates.options();
+  return {at::empty({B, T, D}, opt), at::empty({B, D}, opt.dtype(at::kFloat)),
+          at::empty({B, D}, opt.dtype(at::kFloat)),
+          at::empty({need_ckpt ? sc_lucy_scan_ckpt_numel(B, T, D) : 0}, opt.dtype(at::kFloat))};
+}
+
+std::tuple<Tensor, Tensor, Tensor, Tensor> lucy_scan_bwd_hip(const Tensor& gates, const Tensor& ckpt,
+                                                             const Tensor& dout_in,
+                                                             const optional<Tensor>& ds_last,
+                                                             const optional<Tensor>& bias,
+                                                             bool want_dbias) {
+  c10::DeviceGuard guard(gates.device());
+  const GateLayout L = gate_layout(gates);
+  TORCH_CHECK(ckpt.numel() == sc_lucy_scan_ckpt_numel(L.B, L.T, L.D) && ckpt.scalar_type() == at::kFloat,
+              "statecatcher::lucy_scan_bwd: ckpt is not the forward's checkpoint (run the forward "
+              "with need_ckpt=True)");
+  TORCH_CHECK(dout_in.sizes() == at::IntArrayRef({L.B, L.T, L.D}),
+              "statecatcher::lucy_scan_bwd: dout must be [B,T,D]");
+  Tensor dout = dout_in.to(gates.scalar_type());
+  if (dout.stride(2) != 1) dout = dout.contiguous();
+  optional<Tensor> dsl, bc;
+  if (ds_last && ds_last->defined()) dsl = f32c(*ds_last);
+  if (bias && bias->defined()) bc = f32c(*bias);
+  Tensor dgates = at::empty(gates.sizes(), gates.options().memory_format(at::MemoryFormat::Contiguous));
+  const GateLayout G = gate_layout(dgates);
+  auto fo = gates.options().dtype(at::kFloat);
+  Tensor dh0 = at::empty({L.B, L.D}, fo), ds0 = at::empty({L.B, L.D}, fo);
+  Tensor dbias = at::empty({want_dbias ? L.B : 0, 7, L.D}, fo);
+  sc_check(sc_lucy_scan_bwd(gates.data_ptr(), dtype_code(gates), (const float*)opt_ptr(bc),
+                            ckpt.data_ptr<float>(), dout.data_ptr(), (const float*)opt_ptr(dsl),
+                            dgates.data_ptr(), dh0.data_ptr<float>(), ds0.data_ptr<float>(),
+                            want_dbias ? dbias.data_ptr<float>() : nullptr, L.B, L.T, L.D, L.bt,
+                            L.td, L.cd, L.cb, dout.stride(0), dout.stride(1), G.bt, G.td, G.cd,
+                            G.cb, stream_for(gates)),
+           "statecatcher::lucy_scan_bwd");
+  return {dgates, dh0, ds0, dbias};
+}
+
+std::tuple<Tensor, Tensor, Tensor, Tensor> lucy_scan_bwd_meta(const Tensor& gates, const Tensor& ckpt,
+                                                              const Tensor& dout,
+                                                              const optional<Tensor>& ds_last,
+                                                              const optional<Tensor>& bias,
+                                                              bool want_dbias) {
+  auto [B, T, D] = gate_dims(gates);
+  auto fo = gates.options().dtype(at::kFloat);
+  return {at::empty(gates.sizes(), gates.options()), at::empty({B, D}, fo), at::empty({B, D}, fo),
+          at::empty({want_dbias ? B : 0, 7, D}, fo)};
+}
+
+// ------------------------------------------------------------------------ decay scan ----------
+void check_kv(const Tensor& kv, const Tensor& decay) {
+  TORCH_CHECK(kv.dim() == 3 && kv.sizes() == decay.sizes(),
+              "statecatcher::decay_scan: kv/decay must be equal [B,T,D]; got ", kv.sizes(), ", ",
+              decay.sizes());
+}
+
+Tensor decay_scan_fwd_hip(const Tensor& kv_in, const Tensor& decay_in, const optional<Tensor>& init) {
+  c10::DeviceGuard guard(kv_in.device());
+  check_kv(kv_in, decay_in);
+  Tensor kv = kv_in.contiguous(), decay = decay_in.to(kv.scalar_type()).contiguous();
+  const int64_t B = kv.size(0), T = kv.size(1), D = kv.size(2);
+  optional<Tensor> ic;
+  if (init && init->defined()) ic = f32c(*init);
+  Tensor out = at::empty_like(kv);
+  sc_check(sc_decay_scan_fwd(kv.data_ptr(), decay.data_ptr(), out.data_ptr(), dtype_code(kv),
+                             (const float*)opt_ptr(ic), B, T, D, kv.stride(0), kv.stride(1), 1,
+                             stream_for(kv)),
+           "statecatcher::decay_scan_fwd");
+  return out;
+}
+
+Tensor decay_scan_fwd_meta(const Tensor& kv, const Tensor& decay, const optional<Tensor>& init) {
+  check_kv(kv, decay);
+  return at::empty(kv.sizes(), kv.options());
+}
+
+std::tuple<Tensor, Tensor, Tensor> decay_scan_bwd_hip(const Tensor& decay_in, const Tensor& s_all,
+                                                      const Tensor& dout_in,
+                                                      const optional<Tensor>& init) {
+  c10::DeviceGuard guard(decay_in.device());
+  check_kv(s_all, decay_in);
+  Tensor decay = decay_in.to(s_all.scalar_type()).contiguous(), s = s_all.contiguous();
+  Tensor dout = dout_in.to(s.scalar_type()).contiguous();
+  const int64_t B = s.size(0), T = s.size(1), D = s.size(2);
+  optional<Tensor> ic;
+  const bool has_init = init && init->defined();
+  if (has_init) ic = f32c(*init);
+  Tensor dkv = at::empty_like(s), ddec = at::empty_like(s);
+  Tensor dinit = at::zeros({has_init ? B : 0, D}, s.options().dtype(at::kFloat));
+  sc_check(sc_decay_scan_bwd(decay.data_ptr(), s.data_ptr(), dout.data_ptr(), dkv.data_ptr(),
+                             ddec.data_ptr(), dtype_code(s), (const float*)opt_ptr(ic),
+                             has_init && T > 0 ? dinit.data_ptr<float>() : nullptr, B, T, D,
+                             s.stride(0), s.stride(1), 1, stream_for(s)),
+           "statecatcher::decay_scan_bwd");
+  return {dkv, ddec, dinit};
+}
+
+std::tuple<Tensor, Tensor, Tensor> decay_scan_bwd_meta(const Tensor& decay, const Tensor& s_all,
+                                                       const Tensor& dout,
+                                                       const optional<Tensor>& init) {
+  check_kv(s_all, decay);
+  const bool has_init = init && init->defined();
+  return {at::empty(s_all.sizes(), s_all.options()), at::empty(s_all.sizes(), s_all.options()),
+          at::empty({has_init ? s_all.size(0) : 0, s_all.size(2)}, s_all.options().dtype(at::kFloat))};
+}
+
+// ------------------------------------------------------------------------ LayerNorm -----------
+std::tuple<Tensor, Tensor, Tensor> layer_norm_fwd_hip(const Tensor& x, const Tensor& gamma,
+                                                      const Tensor& beta, double eps) {
+  c10::DeviceGuard guard(x.device());
+  const int64_t D = x.size(-1);
+  Tensor x2 = x.reshape({-1, D}).contiguous();
+  const int64_t rows = x2.size(0);
+  TORCH_CHECK(sc_layernorm_supported(dtype_code(x2), (int)D),
+              "statecatcher::layer_norm_fwd: D=", D, " not supported for ", x2.scalar_type());
+  Tensor g = f32c(gamma), b = f32c(beta);
+  Tensor y = at::empty_like(x2);
+  auto fo = x.options().dtype(at::kFloat);
+  Tensor mean = at::empty({rows}, fo), rstd = at::empty({rows}, fo);
+  sc_check(sc_layernorm_fwd(x2.data_ptr(), dtype_code(x2), g.data_ptr<float>(), b.data_ptr<float>(),
+                            y.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(), rows, (int)D,
+                            (float)eps, stream_for(x2)),
+           "statecatcher::layer_norm_fwd");
+  return {y.view(x.sizes()), mean, rstd};
+}
+
+std::tuple<Tensor, Tensor, Tensor> layer_norm_fwd_meta(const Tensor& x, const Tensor& gamma,
+                                                       const Tensor& beta, double eps) {
+  const int64_t rows = x.numel() / std::max<int64_t>(x.size(-1), 1);
+  auto fo = x.options().dtype(at::kFloat);
+  return {at::empty(x.sizes(), x.options()), at::empty({rows}, fo), at::empty({rows}, fo)};
+}
+
+std::tuple<Tensor, Tensor, Tensor> layer_norm_bwd_hip(const Tensor& x, const Tensor& dy,
+                                                      const Tensor& gamma, const Tensor& mean,
+                                                      const Tensor& rstd) {
+  c10::DeviceGuard guard(x.device());
+  const int64_t D = x.size(-1);
+  Tensor x2 = x.reshape({-1, D}).contiguous();
+  const int64_t rows = x2.size(0);
+  Tensor dy2 = dy.reshape({rows, D}).to(x2.scalar_type()).contiguous();
+  Tensor g = f32c(gamma);
+  Tensor dx = at::empty_like(x2);
+  auto fo = x.options().dtype(at::kFloat);
+  Tensor dgb = at::empty({2, D}, fo);
+  Tensor ws = at::empty({sc_layernorm_bwd_workspace_numel(rows, (int)D)}, fo);
+  sc_check(sc_layernorm_bwd(x2.data_ptr(), dy2.data_ptr(), dtype_code(x2), g.data_ptr<float>(),
+                            mean.data_ptr<float>(), rstd.data_ptr<float>(), dx.data_ptr(),
+                            dgb.data_ptr<float>(), ws.data_ptr<float>(), rows, (int)D, stream_for(x2)),
+           "statecatcher::layer_norm_bwd");
+  return {dx.view(x.sizes()), dgb[0], dgb[1]};
+}
+
+std::tuple<Tensor, Tensor, Tensor> layer_norm_bwd_meta(const Tensor& x, const Tensor& dy,
+                                                       const Tensor& gamma, const Tensor& mean,
+                                                       const Tensor& rstd) {
+  auto fo = x.options().dtype(at::kFloat);
+  return {at::empty(x.sizes(), x.options()), at::empty({x.size(-1)}, fo), at::empty({x.size(-1)}, fo)};
+}
+
+// ------------------------------------------------------------------------ CTC -----------------
+void check_ctc(const Tensor& x, const Tensor& targets, const Tensor& in_lens, const Tensor& tgt_lens) {
+  TORCH_CHECK(x.dim() == 3, "statecatcher::ctc: x must be [B,T,V], got ", x.sizes());
+  TORCH_CHECK(targets.dim() == 2 && targets.size(0) == x.size(0),
+              "statecatcher::ctc: targets must be padded [B, U_max] (train.py:208), got ", targets.sizes());
+  TORCH_CHECK(in_lens.numel() == x.size(0) && tgt_lens.numel() == x.size(0),
+              "statecatcher::ctc: in_lens/tgt_lens must have B entries");
+}
+
+int64_t ctc_ws_bytes(const Tensor& x, const Tensor& targets) {
+  return (int64_t)sc_ctc_workspace_bytes((int)x.size(0), (int)std::max<int64_t>(x.size(1), 1),
+                                         (int)targets.size(1));
+}
+
+std::tuple<Tensor, Tensor> ctc_fwd_hip(const Tensor& x_in, const Tensor& targets_in,
+                                       const Tensor& in_lens_in, const Tensor& tgt_lens_in,
+                                       int64_t blank, bool is_logits) {
+  c10::DeviceGuard guard(x_in.device());
+  check_ctc(x_in, targets_in, in_lens_in, tgt_lens_in);
+  Tensor x = x_in.stride(2) == 1 ? x_in : x_in.contiguous();
+  Tensor targets = targets_in.to(at::kLong).contiguous();
+  Tensor in_lens = in_lens_in.to(at::kLong).contiguous(), tgt_lens = tgt_lens_in.to(at::kLong).contiguous();
+  const int64_t B = x.size(0), T = x.size(1), V = x.size(2), umax = targets.size(1);
+  const int64_t wsb = ctc_ws_bytes(x, targets);
+  Tensor ws = at::empty({wsb}, x.options().dtype(at::kByte));
+  if (T == 0) {   // an empty lattice: nll 0 for empty targets, +inf otherwise (ATen)
+    Tensor nll = at::where(tgt_lens == 0, 0.0, std::numeric_limits<double>::infinity()).to(at::kFloat);
+    return {nll, ws};
+  }
+  Tensor nll = at::empty({B}, x.options().dtype(at::kFloat));
+  sc_check(sc_ctc_fwd(x.data_ptr(), dtype_code(x), is_logits ? 1 : 0, B, T, V, x.stride(0), x.stride(1),
+                      targets.data_ptr<int64_t>(), umax ? targets.stride(0) : 0, (int)umax,
+                      in_lens.data_ptr<int64_t>(), tgt_lens.data_ptr<int64_t>(), (int)blank,
+                      nll.data_ptr<float>(), ws.data_ptr(), (size_t)wsb, stream_for(x)),
+           "statecatcher::ctc_fwd");
+  return {nll, ws};
+}
+
+std::tuple<Tensor, Tensor> ctc_fwd_meta(const Tensor& x, const Tensor& targets, const Tensor& in_lens,
+                                        const Tensor& tgt_lens, int64_t blank, bool is_logits) {
+  check_ctc(x, targets, in_lens, tgt_lens);
+  return {at::empty({x.size(0)}, x.options().dtype(at::kFloat)),
+          at::empty({ctc_ws_bytes(x, targets)}, x.options().dtype(at::kByte))};
+}
+
+Tensor ctc_bwd_hip(const Tensor& x_in, const Tensor& targets_in, const Tensor& in_lens_in,
+                   const Tensor& tgt_lens_in, const Tensor& nll, const Tensor& ws, const Tensor& scale_in,
+                   int64_t blank, bool is_logits) {
+  c10::DeviceGuard guard(x_in.device());
+  check_ctc(x_in, targets_in, in_lens_in, tgt_lens_in);
+  Tensor x = x_in.stride(2) == 1 ? x_in : x_in.contiguous();
+  Tensor targets = targets_in.to(at::kLong).contiguous();
+  Tensor in_lens = in_lens_in.to(at::kLong).contiguous(), tgt_lens = tgt_lens_in.to(at::kLong).contiguous();
+  const int64_t B = x.size(0), T = x.size(1), V = x.size(2), umax = targets.size(1);
+  TORCH_CHECK(ws.numel() == ctc_ws_bytes(x, targets), "statecatcher::ctc_bwd: workspace is not ctc_fwd's");
+  Tensor grad = at::empty({B, T, V}, x.options());
+  if (T == 0) return grad;
+  Tensor scale = f32c(scale_in.expand({B}));
+  sc_check(sc_ctc_bwd(x.data_ptr(), dtype_code(x), is_logits ? 1 : 0, B, T, V, x.stride(0), x.stride(1),
+                      targets.data_ptr<int64_t>(), umax ? targets.stride(0) : 0, (int)umax,
+                      in_lens.data_ptr<int64_t>(), tgt_lens.data_ptr<int64_t>(), (int)blank,
+                      nll.data_ptr<float>(), scale.data_ptr<float>(), grad.data_ptr(), dtype_code(grad),
+                      ws.data_ptr(), (size_t)ws.numel(), stream_for(x)),
+           "statecatcher::ctc_bwd");
+  return grad;
+}
+
+Tensor ctc_bwd_meta(const Tensor& x, const Tensor& targets, const Tensor& in_lens, const Tensor& tgt_lens,
+                    const Tensor& nll, const Tensor& ws, const Tensor& scale, int64_t blank, bool is_logits) {
+  check_ctc(x, targets, in_lens, tgt_lens);
+  return at::empty(x.sizes(), x.options());
+}
+
+std::tuple<Tensor, Tensor> ctc_mean_hip(const Tensor& nll, const Tensor& tgt_lens_in) {
+  c10::DeviceGuard guard(nll.device());
+  const int64_t B = nll.numel();
+  TORCH_CHECK(tgt_lens_in.numel() == B, "statecatcher::ctc_mean: tgt_lens must have B entries");
+  Tensor n = f32c(nll), tgt_lens = tgt_lens_in.to(at::kLong).contiguous();
+  Tensor loss = at::empty({}, n.options()), factor = at::empty({B}, n.options());
+  if (B == 0) {
+    loss.fill_(std::numeric_limits<double>::quiet_NaN());   // mean over an empty batch
+    return {loss, factor};
+  }
+  sc_check(sc_ctc_mean(n.data_ptr<float>(), tgt_lens.data_ptr<int64_t>(), (int)B, loss.data_ptr<float>(),
+                       factor.data_ptr<float>(), stream_for(n)),
+           "statecatcher::ctc_mean");
+  return {loss, factor};
+}
+
+std::tuple<Tensor, Tensor> ctc_mean_meta(const Tensor& nll, const Tensor& tgt_lens) {
+  auto fo = nll.options().dtype(at::kFloat);
+  return {at::empty({}, fo), at::empty({nll.numel()}, fo)};
+}
+
+std::tuple<Tensor, Tensor> ctc_greedy_decode_hip(const Tensor& lp_in, const Tensor& lengths_in,
+                                                 int64_t blank) {
+  c10::DeviceGuard guard(lp_in.device());
+  TORCH_CHECK(lp_in.dim() == 3, "statecatcher::ctc_greedy_decode: log_probs must be [B,T,V]");
+  Tensor lp = lp_in.stride(2) == 1 ? lp_in : lp_in.contiguous();
+  const int64_t B = lp.size(0), T = lp.size(1), V = lp.size(2);
+  Tensor lengths = lengths_in.to(at::kLong).contiguous();
+  TORCH_CHECK(lengths.numel() == B, "statecatcher::ctc_greedy_decode: lengths must have B entries");
+  auto io = lp.options().dtype(at::kInt);
+  Tensor tokens = at::empty({B, T}, io), counts = at::empty({B}, io);
+  sc_check(sc_ctc_greedy_decode(lp.data_ptr(), dtype_code(lp), B, T, V, lp.stride(0), lp.stride(1),
+                                lengths.data_ptr<int64_t>(), (int)blank, tokens.data_ptr<int32_t>(),
+                                counts.data_ptr<int32_t>(), stream_for(lp)),
+           "statecatcher::ctc_greedy_decode");
+  return {tokens, counts};
+}
+
+std::tuple<Tensor, Tensor> ctc_greedy_decode_meta(const Tensor& lp, const Tensor& lengths, int64_t blank) {
+  auto io = lp.options().dtype(at::kInt);
+  return {at::empty({lp.size(0), lp.size(1)}, io), at::empty({lp.size(0)}, io)};
+}
+
+}  // namespace
+
+TORCH_LIBRARY(statecatcher, m) {
+  m.def("abi_version() -> int", []() -> int64_t { return sc_abi_version(); });
+  m.def("lucy_scan_fwd(Tensor gates, Tensor h0, Tensor s0, Tensor? gate_bias=None, bool need_ckpt=True)"
+        " -> (Tensor out, Tensor s_last, Tensor h_last, Tensor ckpt)");
+  m.def("lucy_scan_bwd(Tensor gates, Tensor ckpt, Tensor dout, Tensor? ds_last=None, "
+        "Tensor? gate_bias=None, bool want_dbias=False) -> (Tensor dgates, Tensor dh0, Tensor ds0, "
+        "Tensor dbias)");
+  m.def("decay_scan_fwd(Tensor kv, Tensor decay, Tensor? init=None) -> Tensor");
+  m.def("decay_scan_bwd(Tensor decay, Tensor s_all, Tensor dout, Tensor? init=None)"
+        " -> (Tensor dkv, Tensor ddecay, Tensor dinit)");
+  m.def("layer_norm_fwd(Tensor x, Tensor gamma, Tensor beta, float eps=1e-5)"
+        " -> (Tensor y, Tensor mean, Tensor rstd)");
+  m.def("layer_norm_bwd(Tensor x, Tensor dy, Tensor gamma, Tensor mean, Tensor rstd)"
+        " -> (Tensor dx, Tensor dgamma, Tensor dbeta)");
+  m.def("ctc_fwd(Tensor x, Tensor targets, Tensor in_lens, Tensor tgt_lens, int blank=0, "
+        "bool is_logits=True) -> (Tensor nll, Tensor workspace)");
+  m.def("ctc_bwd(Tensor x, Tensor targets, Tensor in_lens, Tensor tgt_lens, Tensor nll, "
+        "Tensor workspace, Tensor scale, int blank=0, bool is_logits=True) -> Tensor");
+  m.def("ctc_mean(Tensor nll, Tensor tgt_lens) -> (Tensor loss, Tensor factor)");
+  m.def("ctc_greedy_decode(Tensor log_probs, Tensor lengths, int blank=0)"
+        " -> (Tensor tokens, Tensor counts)");
+}
+
+TORCH_LIBRARY_IMPL(statecatcher, CUDA, m) {
+  m.impl("lucy_scan_fwd", &lucy_scan_fwd_hip);
+  m.impl("lucy_scan_bwd", &lucy_scan_bwd_hip);
+  m.impl("decay_scan_fwd", &decay_scan_fwd_hip);
+  m.impl("decay_scan_bwd", &decay_scan_bwd_hip);
+  m.impl("layer_norm_fwd", &layer_norm_fwd_hip);
+  m.impl("layer_norm_bwd", &layer_norm_bwd_hip);
+  m.impl("ctc_fwd", &ctc_fwd_hip);
+  m.impl("ctc_bwd", &ctc_bwd_hip);
+  m.impl("ctc_mean", &ctc_mean_hip);
+  m.impl("ctc_greedy_decode", &ctc_greedy_decode_hip);
+}
+
+TORCH_LIBRARY_IMPL(statecatcher, Meta, m) {
+  m.impl("lucy_scan_fwd", &lucy_scan_fwd_meta);
+  m.impl("lucy_scan_bwd", &lucy_scan_bwd_meta);
+  m.impl("decay_scan_fwd", &decay_scan_fwd_meta);
+  m.impl("decay_scan_bwd", &decay_scan_bwd_meta);
+  m.impl("layer_norm_fwd", &layer_norm_fwd_meta);
+  m.impl("layer_norm_bwd", &layer_norm_bwd_meta);
+  m.impl("ctc_fwd", &ctc_fwd_meta);
+  m.impl("ctc_bwd", &ctc_bwd_meta);
+  m.impl("ctc_mean", &ctc_mean_meta);
+  m.impl("ctc_greedy_decode", &ctc_greedy_decode_meta);
+}

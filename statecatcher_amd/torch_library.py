@@ -1,0 +1,167 @@
+"""The hot-path ops as dispatcher ops: ``torch.ops.statecatcher.*`` (csrc/torch_ops.cpp,
+``TORCH_LIBRARY(statecatcher, m)``).
+
+The C++ extension registers each op's schema, its HIP kernel (CUDA dispatch key) and a Meta
+kernel (shapes only).  This module loads it and registers the autograd formulas over the
+``*_bwd`` ops, so the functions below are differentiable, traceable by FakeTensor /
+``torch.compile(fullgraph=True)`` and checkable with ``torch.library.opcheck``.  They launch the
+same kernels as the ctypes autograd nodes of ``ops.py`` (the training hot path), which stay the
+lower-overhead route for eager training.
+
+Reference interfaces (what a ``train.py`` user swaps in):
+  lucy_scan   <- rnn_forward_unfused_rmsnorm                        lucyrnn_triton.py:61-73, :180-244
+  decay_scan  <- fused_decay_scan                                    lucyrnn_triton.py:158-177
+  layer_norm  <- nn.LayerNorm(D) between layers                      lucyrnn_triton.py:96-97, :136-137
+  ctc_loss    <- nn.CTCLoss(blank, reduction='mean', zero_infinity)  train.py:142 (on model.py:70's
+                 log_softmax, fused here when is_logits)
+  ctc_greedy_decode <- decoder.py:3-30
+"""
+import os
+
+import torch
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_torch_ops.so")
+OPS = ("abi_version", "lucy_scan_fwd", "lucy_scan_bwd", "decay_scan_fwd", "decay_scan_bwd",
+       "layer_norm_fwd", "layer_norm_bwd", "ctc_fwd", "ctc_bwd", "ctc_mean", "ctc_greedy_decode")
+
+_LOADED = False
+
+
+def load():
+    """Load the extension (once) and register the autograd formulas.  Raises if it is not built:
+    there is no Python fallback for these ops."""
+    global _LOADED
+    if _LOADED:
+        return torch.ops.statecatcher
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"statecatcher TORCH_LIBRARY extension not built: {LIB_PATH} missing "
+                           "(make -C statecatcher_amd/csrc)")
+    torch.ops.load_library(LIB_PATH)
+    _register_autograd()
+    _LOADED = True
+    return torch.ops.statecatcher
+
+
+# ------------------------------------------------------------------------------- autograd -----
+def _scan_setup(ctx, inputs, output):
+    gates, h0, s0, bias, need_ckpt = inputs
+    ctx.save_for_backward(gates, output[3], bias)
+    ctx.has_bias = bias is not None
+    ctx.dtypes = (h0.dtype, s0.dtype, None if bias is None else bias.dtype)
+
+
+def _scan_backward(ctx, dout, ds_last, dh_last, dckpt):
+    gates, ckpt, bias = ctx.saved_tensors
+    sc = torch.ops.statecatcher
+    B, T = gates.shape[:2]
+    D = gates.shape[-1] if gates.dim() == 4 else gates.shape[2] * 64
+    if dout is None:
+        dout = gates.new_zeros(B, T, D)
+    if dh_last is not None:   # h_last is out[:, -1] before rounding: its gradient joins dout's
+        dout = dout.clone()
+        dout[:, -1] += dh_last.to(dout.dtype)
+    want_db = ctx.has_bias and ctx.needs_input_grad[3]
+    dgates, dh0, ds0, dbias = sc.lucy_scan_bwd(gates, ckpt, dout, ds_last, bias, want_db)
+    hd, sd, bd = ctx.dtypes
+    db = None
+    if want_db:   # per-row partials [B,7,D] -> the bias's [7,D] (logical g*D + d) order
+        db = dbias.sum(0).reshape(bias.shape).to(bd)
+    return dgates, dh0.to(hd), ds0.to(sd), db, None
+
+
+def _decay_setup(ctx, inputs, output):
+    kv, decay, init = inputs
+    ctx.save_for_backward(decay, output, init)
+    ctx.init_dtype = None if init is None else init.dtype
+
+
+def _decay_backward(ctx, dout):
+    decay, s_all, init = ctx.saved_tensors
+    dkv, ddec, dinit = torch.ops.statecatcher.decay_scan_bwd(decay, s_all, dout, init)
+    return dkv, ddec.to(decay.dtype), (dinit.to(ctx.init_dtype) if init is not None else None)
+
+
+def _ln_setup(ctx, inputs, output):
+    x, gamma, beta, eps = inputs
+    ctx.save_for_backward(x, gamma, output[1], output[2])
+    ctx.pdtypes = (gamma.dtype, beta.dtype)
+
+
+def _ln_backward(ctx, dy, dmean, drstd):
+    x, gamma, mean, rstd = ctx.saved_tensors
+    dx, dg, db = torch.ops.statecatcher.layer_norm_bwd(x, dy, gamma, mean, rstd)
+    gd, bd = ctx.pdtypes
+    return dx, dg.to(gd), db.to(bd), None
+
+
+def _ctc_setup(ctx, inputs, output):
+    x, targets, in_lens, tgt_lens, blank, is_logits = inputs
+    ctx.save_for_backward(x, targets, in_lens, tgt_lens, output[0], output[1])
+    ctx.meta = (blank, is_logits)
+
+
+def _ctc_backward(ctx, grad_nll, grad_ws):
+    x, targets, in_lens, tgt_lens, nll, ws = ctx.saved_tensors
+    blank, is_logits = ctx.meta
+    if grad_nll is None:
+        return None, None, None, None, None, None
+    grad = torch.ops.statecatcher.ctc_bwd(x, targets, in_lens, tgt_lens, nll, ws, grad_nll,
+                                          blank, is_logits)
+    return grad, None, None, None, None, None
+
+
+def _mean_setup(ctx, inputs, output):
+    ctx.save_for_backward(output[1])
+
+
+def _mean_backward(ctx, grad_loss, grad_factor):
+    (factor,) = ctx.saved_tensors
+    return (factor * grad_loss if grad_loss is not None else None), None
+
+
+def _register_autograd():
+    reg = torch.library.register_autograd
+    reg("statecatcher::lucy_scan_fwd", _scan_backward, setup_context=_scan_setup)
+    reg("statecatcher::decay_scan_fwd", _decay_backward, setup_context=_decay_setup)
+    reg("statecatcher::layer_norm_fwd", _ln_backward, setup_context=_ln_setup)
+    reg("statecatcher::ctc_fwd", _ctc_backward, setup_context=_ctc_setup)
+    reg("statecatcher::ctc_mean", _mean_backward, setup_context=_mean_setup)
+
+
+# ------------------------------------------------------------------------------- functions ----
+def lucy_scan(gates, h0, s0, gate_bias=None):
+    """(out [B,T,D] in gates' dtype, s_last fp32, h_last fp32) of the LucyRNN scan over gates
+    [B,T,7,D] (the reference layout) or step-blocked [B,T,D/64,7,64]; gate_bias fp32 [7,D] is
+    added on load.  Differentiable in gates, h0, s0 and gate_bias."""
+    sc = load()
+    need = torch.is_grad_enabled() and any(
+        t is not None and t.requires_grad for t in (gates, h0, s0, gate_bias))
+    out, s_last, h_last, _ = sc.lucy_scan_fwd(gates, h0, s0, gate_bias, need)
+    return out, s_last, h_last
+
+
+def decay_scan(kv, decay, init=None):
+    """s_t = decay_t s_{t-1} + kv_t with s_{-1} = init (zeros if None); fused_decay_scan."""
+    return load().decay_scan_fwd(kv, decay, init)
+
+
+def layer_norm(x, gamma, beta, eps=1e-5):
+    """nn.LayerNorm over the last dim in x's dtype with fp32 statistics."""
+    return load().layer_norm_fwd(x, gamma, beta, eps)[0]
+
+
+def ctc_nll(x, targets, in_lens, tgt_lens, blank=0, is_logits=True):
+    """Per-sequence CTC negative log-likelihood [B] fp32 (+inf when infeasible)."""
+    return load().ctc_fwd(x, targets, in_lens, tgt_lens, blank, is_logits)[0]
+
+
+def ctc_loss(x, targets, in_lens, tgt_lens, blank=0, is_logits=True):
+    """nn.CTCLoss(blank, reduction='mean', zero_infinity=True) (train.py:142)."""
+    sc = load()
+    nll = sc.ctc_fwd(x, targets, in_lens, tgt_lens, blank, is_logits)[0]
+    return sc.ctc_mean(nll, tgt_lens)[0]
+
+
+def ctc_greedy_decode(log_probs, lengths, blank=0):
+    """(tokens int32 [B,T], counts int32 [B]) of decoder.py's greedy CTC decode."""
+    return load().ctc_greedy_decode(log_probs, lengths, blank)
