@@ -270,9 +270,12 @@ extern "C" int sc_gemm_wgrad_splits(int L, int I, int J) {
   const int ti = I % 224 == 0 && (I / 224) * (J / kTJ) * 8 == 256 ? 224 : 256;
   if (I % ti) return 0;
   const int tiles = (I / ti) * (J / kTJ);
-  int S = 1;
-  while (tiles * S * 2 <= 256 && (L / kTL) / (S * 2) >= 8) S *= 2;
-  return S;
+  // as many L-splits as fill the 256 CUs (any count: the split ranges are nkb * s / S, so they
+  // may differ by one K-block), each of at least 8 K-blocks.  Powers of two left C4's shapes
+  // at 56-84% of the CUs (out_proj 9 tiles x 16, FFN 48 x 4 / 24 x 8, q|k|v|o head 27 x 8).
+  int S = 256 / tiles;
+  S = S < (L / kTL) / 8 ? S : (L / kTL) / 8;
+  return S > 1 ? S : 1;
 }
 
 extern "C" int sc_gemm_wgrad_bf16(const void* A, int64_t lda, const void* B, int64_t ldb,

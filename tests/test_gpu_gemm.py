@@ -23,7 +23,10 @@ def _ref(dy, x):
                                    (48000, 1024, 512),   # output projection
                                    (6400, 3584, 512),
                                    (4096, 512, 256),
-                                   (1024, 768, 768)])
+                                   (1024, 768, 768),
+                                   (14336, 768, 768),    # C4 out_proj: 9 tiles x 28 splits
+                                   (4096, 4096, 768),    # C4 FFN up: 48 x 5, uneven ranges
+                                   (6400, 768, 2048)])   # C4 FFN down: 24 x 10
 def test_wgrad_mfma_vs_fp32(L, I, J):
     from statecatcher_amd import _lib
     assert _lib.load().sc_gemm_wgrad_splits(L, I, J) > 0
@@ -36,6 +39,20 @@ def test_wgrad_mfma_vs_fp32(L, I, J):
     ref = _ref(dy, x)
     err = (dw - ref).abs().max().item() / ref.abs().max().item()
     assert err < 1e-5, err
+
+
+def test_wgrad_splits_fill_the_chip():
+    """The split count fills the 256 CUs for any tile count (not only powers of two), and each
+    split keeps at least 8 K-blocks of 64 rows."""
+    from statecatcher_amd import _lib
+    lib = _lib.load()
+    assert lib.sc_gemm_wgrad_splits(48000, 3584, 512) == 8     # C2 gates: 32 tiles (224 rows)
+    assert lib.sc_gemm_wgrad_splits(48000, 1024, 512) == 32    # C2 output projection: 8 tiles
+    assert lib.sc_gemm_wgrad_splits(48000, 768, 768) == 28     # 9 tiles
+    assert lib.sc_gemm_wgrad_splits(48000, 4096, 768) == 5     # 48 tiles
+    assert lib.sc_gemm_wgrad_splits(48000, 768, 2048) == 10    # 24 tiles
+    assert lib.sc_gemm_wgrad_splits(1024, 768, 768) == 2       # 16 K-blocks: 8 per split
+    assert lib.sc_gemm_wgrad_splits(512, 4096, 4096) == 1
 
 
 def test_wgrad_mfma_structured_exact():
