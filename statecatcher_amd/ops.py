@@ -1346,7 +1346,14 @@ class AutocastLinearFn(torch.autograd.Function):
                     # gate rows that remain as a small library GEMM
                     head = wgrad_mfma(dyc[:, :n0], xcc)
                     if head is not None:
-                        dw = torch.cat([head, _mm_f32(dyc[:, n0:].t(), xcc)])
+                        # the tail rows from the MFMA kernel too, over the last 256-row window
+                        # (a 16-byte aligned view when N % 8 == 0; its first rows repeat the
+                        # head's): an M = 8, K = 48000 library GEMM took 130 us at C4, the
+                        # window ~30 us
+                        win = wgrad_mfma(dyc[:, N - 256:], xcc)
+                        tail = win[256 - (N - n0):] if win is not None else \
+                            _mm_f32(dyc[:, n0:].t(), xcc)
+                        dw = torch.cat([head, tail])
             dw = (dw if dw is not None else (dy2.t() @ x2).float()).to(wdt)
         if bdt is not None and ctx.needs_input_grad[2]:
             db = colsum(dy2).to(bdt)
