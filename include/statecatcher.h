@@ -360,6 +360,15 @@ int sc_rmsnorm_fwd(const void* x, const float* w, void* y, float* rstd, int64_t 
                    float eps, void* stream);
 int sc_rmsnorm_bwd(const void* x, const void* dy, const float* w, const float* rstd, void* dx,
                    float* part, int64_t rows, int D, void* stream);
+/* The block's residual add folded into the next RMSNorm (xLSTM block: x + y then norm_ffn, and
+ * the previous block's x + ffn(..) then norm_mlstm; modeling_xlstm.py block forward):
+ * s = bf16(x + r) (written) and y = RMSNorm(s) as sc_rmsnorm_fwd.  The backward takes s as its x
+ * and adds the residual branch's gradient: dx = bf16(bf16(dRMSNorm) + dres), the sum autograd
+ * forms for the two bf16 gradients of s. */
+int sc_rmsnorm_add_fwd(const void* x, const void* r, void* s, const float* w, void* y, float* rstd,
+                       int64_t rows, int D, float eps, void* stream);
+int sc_rmsnorm_add_bwd(const void* s, const void* dy, const void* dres, const float* w,
+                       const float* rstd, void* dx, float* part, int64_t rows, int D, void* stream);
 int sc_mhln_gate_fwd(const void* h, const void* o, int64_t ldo, const float* w, void* out,
                      float* mean, float* rstd, int B, int T, int NH, int DH, float eps,
                      void* stream);

@@ -67,6 +67,8 @@ _SIGS = {
     "sc_xlstm_part_rows": (_i32, [_i64]),
     "sc_rmsnorm_fwd": (_i32, [_vp, _fp, _vp, _fp, _i64, _i32, _c.c_float, _vp]),
     "sc_rmsnorm_bwd": (_i32, [_vp, _vp, _fp, _fp, _vp, _fp, _i64, _i32, _vp]),
+    "sc_rmsnorm_add_fwd": (_i32, [_vp, _vp, _vp, _fp, _vp, _fp, _i64, _i32, _c.c_float, _vp]),
+    "sc_rmsnorm_add_bwd": (_i32, [_vp, _vp, _vp, _fp, _fp, _vp, _fp, _i64, _i32, _vp]),
     "sc_mhln_gate_fwd": (_i32, [_vp, _vp, _i64, _fp, _vp, _fp, _fp, _i32, _i32, _i32, _i32,
                                 _c.c_float, _vp]),
     "sc_mhln_gate_bwd": (_i32, [_vp, _vp, _i64, _fp, _fp, _fp, _vp, _i64, _vp, _vp, _i64, _fp,

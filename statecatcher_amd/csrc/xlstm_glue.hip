@@ -57,9 +57,12 @@ constexpr int kPartWg = 512;   // workgroups (and partial rows) of the weight-gr
 
 // ------------------------------------------------------------------------------ RMSNorm ------
 // CH = D / 256 chunks of 4 per lane
-template <int CH>
-__global__ void __launch_bounds__(256) rms_fwd_kernel(const u16* x, const float* w, u16* y,
-                                                      float* rstd, int64_t rows, float eps) {
+// ADD: the block's residual add folded in -- s = bf16(x + r) is written and normalised (the
+// torch chain's bf16 add, then RMSNorm of its result)
+template <int CH, bool ADD>
+__global__ void __launch_bounds__(256) rms_fwd_kernel(const u16* x, const u16* r, u16* s,
+                                                      const float* w, u16* y, float* rstd,
+                                                      int64_t rows, float eps) {
   constexpr int D = 256 * CH;
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -69,6 +72,13 @@ __global__ void __launch_bounds__(256) rms_fwd_kernel(const u16* x, const float*
 #pragma unroll
   for (int c = 0; c < CH; ++c) {
     ld4(x + row * D + (c * 64 + lane) * 4, v[c]);
+    if constexpr (ADD) {
+      float rv[4];
+      ld4(r + row * D + (c * 64 + lane) * 4, rv);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[c][k] = rbf(v[c][k] + rv[k]);
+      st4(s + row * D + (c * 64 + lane) * 4, v[c]);
+    }
 #pragma unroll
     for (int k = 0; k < 4; ++k) ss = fmaf(v[c][k], v[c][k], ss);
   }
@@ -86,10 +96,12 @@ __global__ void __launch_bounds__(256) rms_fwd_kernel(const u16* x, const float*
 }
 
 // dx = rstd (g - xh mean(g xh)), g = dy w, xh = x rstd;  dW partial = sum_rows dy bf16(xh)
-template <int CH>
-__global__ void __launch_bounds__(256) rms_bwd_kernel(const u16* x, const u16* dy, const float* w,
-                                                      const float* rstd, u16* dx, float* part,
-                                                      int64_t rows) {
+// ADD: dx = bf16(bf16(dx) + dres), the residual branch's gradient accumulated as autograd
+// accumulates the two bf16 gradients of the block's sum
+template <int CH, bool ADD>
+__global__ void __launch_bounds__(256) rms_bwd_kernel(const u16* x, const u16* dy, const u16* dres,
+                                                      const float* w, const float* rstd, u16* dx,
+                                                      float* part, int64_t rows) {
   constexpr int D = 256 * CH;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   __shared__ float red[4][D];
@@ -128,6 +140,12 @@ __global__ void __launch_bounds__(256) rms_bwd_kernel(const u16* x, const u16* d
       float o[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) o[k] = rs * (gv[c][k] - xv[c][k] * dot);
+      if constexpr (ADD) {
+        float rv[4];
+        ld4(dres + row * D + (c * 64 + lane) * 4, rv);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) o[k] = rbf(o[k]) + rv[k];
+      }
       st4(dx + row * D + (c * 64 + lane) * 4, o);
     }
   }
@@ -314,6 +332,39 @@ using namespace sc;
 
 extern "C" int sc_xlstm_part_rows(int64_t rows) { return rows > 0 ? part_rows(rows) : 1; }
 
+template <bool ADD>
+static int rms_fwd_launch(const void* x, const void* r, void* s, const float* w, void* y,
+                          float* rstd, int64_t rows, int D, float eps, void* stream) {
+  if (rows == 0) return 0;
+  const dim3 g((unsigned)((rows + 3) / 4));
+  hipStream_t st = (hipStream_t)stream;
+  const u16 *xp = (const u16*)x, *rp = (const u16*)r;
+  u16 *sp = (u16*)s, *yp = (u16*)y;
+  switch (D / 256) {
+    case 1: hipLaunchKernelGGL((rms_fwd_kernel<1, ADD>), g, dim3(256), 0, st, xp, rp, sp, w, yp, rstd, rows, eps); break;
+    case 2: hipLaunchKernelGGL((rms_fwd_kernel<2, ADD>), g, dim3(256), 0, st, xp, rp, sp, w, yp, rstd, rows, eps); break;
+    case 3: hipLaunchKernelGGL((rms_fwd_kernel<3, ADD>), g, dim3(256), 0, st, xp, rp, sp, w, yp, rstd, rows, eps); break;
+    default: hipLaunchKernelGGL((rms_fwd_kernel<4, ADD>), g, dim3(256), 0, st, xp, rp, sp, w, yp, rstd, rows, eps); break;
+  }
+  return 0;
+}
+
+template <bool ADD>
+static void rms_bwd_launch(const void* x, const void* dy, const void* dres, const float* w,
+                           const float* rstd, void* dx, float* part, int64_t rows, int D,
+                           void* stream) {
+  const dim3 g((unsigned)part_rows(rows));
+  hipStream_t st = (hipStream_t)stream;
+  const u16 *xp = (const u16*)x, *dyp = (const u16*)dy, *rp = (const u16*)dres;
+  u16* dxp = (u16*)dx;
+  switch (D / 256) {
+    case 1: hipLaunchKernelGGL((rms_bwd_kernel<1, ADD>), g, dim3(256), 0, st, xp, dyp, rp, w, rstd, dxp, part, rows); break;
+    case 2: hipLaunchKernelGGL((rms_bwd_kernel<2, ADD>), g, dim3(256), 0, st, xp, dyp, rp, w, rstd, dxp, part, rows); break;
+    case 3: hipLaunchKernelGGL((rms_bwd_kernel<3, ADD>), g, dim3(256), 0, st, xp, dyp, rp, w, rstd, dxp, part, rows); break;
+    default: hipLaunchKernelGGL((rms_bwd_kernel<4, ADD>), g, dim3(256), 0, st, xp, dyp, rp, w, rstd, dxp, part, rows); break;
+  }
+}
+
 extern "C" int sc_rmsnorm_fwd(const void* x, const float* w, void* y, float* rstd, int64_t rows,
                               int D, float eps, void* stream) {
   clear_error();
@@ -321,16 +372,19 @@ extern "C" int sc_rmsnorm_fwd(const void* x, const float* w, void* y, float* rst
   SC_REQUIRE(D == 256 || D == 512 || D == 768 || D == 1024,
              "sc_rmsnorm_fwd: D=%d (256, 512, 768 or 1024)", D);
   SC_REQUIRE(rows >= 0, "sc_rmsnorm_fwd: rows < 0");
-  if (rows == 0) return 0;
-  const dim3 g((unsigned)((rows + 3) / 4));
-  hipStream_t st = (hipStream_t)stream;
-  switch (D / 256) {
-    case 1: hipLaunchKernelGGL(rms_fwd_kernel<1>, g, dim3(256), 0, st, (const u16*)x, w, (u16*)y, rstd, rows, eps); break;
-    case 2: hipLaunchKernelGGL(rms_fwd_kernel<2>, g, dim3(256), 0, st, (const u16*)x, w, (u16*)y, rstd, rows, eps); break;
-    case 3: hipLaunchKernelGGL(rms_fwd_kernel<3>, g, dim3(256), 0, st, (const u16*)x, w, (u16*)y, rstd, rows, eps); break;
-    default: hipLaunchKernelGGL(rms_fwd_kernel<4>, g, dim3(256), 0, st, (const u16*)x, w, (u16*)y, rstd, rows, eps); break;
-  }
+  rms_fwd_launch<false>(x, nullptr, nullptr, w, y, rstd, rows, D, eps, stream);
   return launch_status("sc_rmsnorm_fwd");
+}
+
+extern "C" int sc_rmsnorm_add_fwd(const void* x, const void* r, void* s, const float* w, void* y,
+                                  float* rstd, int64_t rows, int D, float eps, void* stream) {
+  clear_error();
+  SC_REQUIRE(x && r && s && w && y && rstd, "sc_rmsnorm_add_fwd: null pointer");
+  SC_REQUIRE(D == 256 || D == 512 || D == 768 || D == 1024,
+             "sc_rmsnorm_add_fwd: D=%d (256, 512, 768 or 1024)", D);
+  SC_REQUIRE(rows >= 0, "sc_rmsnorm_add_fwd: rows < 0");
+  rms_fwd_launch<true>(x, r, s, w, y, rstd, rows, D, eps, stream);
+  return launch_status("sc_rmsnorm_add_fwd");
 }
 
 extern "C" int sc_rmsnorm_bwd(const void* x, const void* dy, const float* w, const float* rstd,
@@ -339,15 +393,19 @@ extern "C" int sc_rmsnorm_bwd(const void* x, const void* dy, const float* w, con
   SC_REQUIRE(x && dy && w && rstd && dx && part, "sc_rmsnorm_bwd: null pointer");
   SC_REQUIRE(D == 256 || D == 512 || D == 768 || D == 1024, "sc_rmsnorm_bwd: D=%d", D);
   if (rows <= 0) return 0;
-  const dim3 g((unsigned)part_rows(rows));
-  hipStream_t st = (hipStream_t)stream;
-  switch (D / 256) {
-    case 1: hipLaunchKernelGGL(rms_bwd_kernel<1>, g, dim3(256), 0, st, (const u16*)x, (const u16*)dy, w, rstd, (u16*)dx, part, rows); break;
-    case 2: hipLaunchKernelGGL(rms_bwd_kernel<2>, g, dim3(256), 0, st, (const u16*)x, (const u16*)dy, w, rstd, (u16*)dx, part, rows); break;
-    case 3: hipLaunchKernelGGL(rms_bwd_kernel<3>, g, dim3(256), 0, st, (const u16*)x, (const u16*)dy, w, rstd, (u16*)dx, part, rows); break;
-    default: hipLaunchKernelGGL(rms_bwd_kernel<4>, g, dim3(256), 0, st, (const u16*)x, (const u16*)dy, w, rstd, (u16*)dx, part, rows); break;
-  }
+  rms_bwd_launch<false>(x, dy, nullptr, w, rstd, dx, part, rows, D, stream);
   return launch_status("sc_rmsnorm_bwd");
+}
+
+extern "C" int sc_rmsnorm_add_bwd(const void* s, const void* dy, const void* dres, const float* w,
+                                  const float* rstd, void* dx, float* part, int64_t rows, int D,
+                                  void* stream) {
+  clear_error();
+  SC_REQUIRE(s && dy && dres && w && rstd && dx && part, "sc_rmsnorm_add_bwd: null pointer");
+  SC_REQUIRE(D == 256 || D == 512 || D == 768 || D == 1024, "sc_rmsnorm_add_bwd: D=%d", D);
+  if (rows <= 0) return 0;
+  rms_bwd_launch<true>(s, dy, dres, w, rstd, dx, part, rows, D, stream);
+  return launch_status("sc_rmsnorm_add_bwd");
 }
 
 static int mh_check(int B, int T, int NH, int DH, const char* who) {

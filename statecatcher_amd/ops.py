@@ -1214,6 +1214,60 @@ def rms_norm(x, w, eps):
     return RMSNormFn.apply(x, w, eps)
 
 
+class AddRMSNormFn(torch.autograd.Function):
+    """(s, n) = (x + r, RMSNorm(x + r)) in one pass: the xLSTM block's residual add folded into
+    the RMSNorm that reads its result (sc_rmsnorm_add_fwd).  The backward folds the residual
+    branch's gradient ds into the norm's dx (sc_rmsnorm_add_bwd), so neither the forward add nor
+    autograd's gradient accumulation is a kernel of its own; bf16 roundings as the torch chain."""
+
+    @staticmethod
+    def forward(ctx, x, r, w, eps):
+        require_device(x, r)
+        D = x.shape[-1]
+        x2 = x.reshape(-1, D)
+        r2 = r.reshape(-1, D)
+        if not x2.is_contiguous():
+            x2 = x2.contiguous()
+        if not r2.is_contiguous():
+            r2 = r2.contiguous()
+        rows = x2.shape[0]
+        wf = w.detach().float().contiguous()
+        s = torch.empty_like(x2)
+        y = torch.empty_like(x2)
+        rstd = torch.empty(rows, dtype=torch.float32, device=x.device)
+        check(_lib.load().sc_rmsnorm_add_fwd(ptr(x2), ptr(r2), ptr(s), ptr(wf), ptr(y), ptr(rstd),
+                                             rows, D, float(eps), stream_of(x2)),
+              "sc_rmsnorm_add_fwd")
+        ctx.save_for_backward(s, wf, rstd)
+        ctx.wdt = w.dtype
+        return s.view(x.shape), y.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, ds, dy):
+        s, wf, rstd = ctx.saved_tensors
+        rows, D = s.shape
+        lib = _lib.load()
+        if dy is None:   # the normalised output unused: the add's own gradient only
+            return ds, ds, None, None
+        dy2 = dy.reshape(rows, D).to(torch.bfloat16).contiguous()
+        dx = torch.empty_like(s)
+        part = torch.empty(lib.sc_xlstm_part_rows(rows), D, dtype=torch.float32, device=s.device)
+        if ds is None:
+            check(lib.sc_rmsnorm_bwd(ptr(s), ptr(dy2), ptr(wf), ptr(rstd), ptr(dx), ptr(part), rows,
+                                     D, stream_of(s)), "sc_rmsnorm_bwd")
+        else:
+            ds2 = ds.reshape(rows, D).to(torch.bfloat16).contiguous()
+            check(lib.sc_rmsnorm_add_bwd(ptr(s), ptr(dy2), ptr(ds2), ptr(wf), ptr(rstd), ptr(dx),
+                                         ptr(part), rows, D, stream_of(s)), "sc_rmsnorm_add_bwd")
+        dx = dx.view(dy.shape)
+        return dx, dx, _part_sum(part).to(ctx.wdt), None
+
+
+def add_rms_norm(x, r, w, eps):
+    """(x + r, RMSNorm(x + r)) through AddRMSNormFn (bf16 ROCm tensors, xlstm_glue_supported)."""
+    return AddRMSNormFn.apply(x, r, w, eps)
+
+
 class GatedHeadNormFn(torch.autograd.Function):
     """bf16(sigmoid(o)) * MultiHeadLayerNorm(h) of the mLSTM layer (modeling_xlstm.py mLSTMLayer:
     out_proj(sigmoid(o) * multihead_norm(h))) in one pass: h [B,NH,T,DH] the cell output in the

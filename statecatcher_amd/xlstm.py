@@ -221,6 +221,18 @@ class mLSTMLayer(nn.Module):
         return self.out_proj(torch.sigmoid(o) * h), new_state
 
 
+def _add_norm(x, y, norm):
+    """(x + y, norm(x + y)): the block's residual add and the RMSNorm that reads its result as
+    one HIP pass (ops.AddRMSNormFn, bf16 roundings as the torch chain) where the glue kernels
+    apply, else the torch chain itself."""
+    if (isinstance(norm, RMSNorm) and norm.bias is None and norm.force_float32_reductions
+            and x.shape == y.shape and ops.xlstm_glue_supported(x, x.shape[-1])
+            and ops.xlstm_glue_supported(y, y.shape[-1])):
+        return ops.add_rms_norm(x, y, norm.weight, norm.eps)
+    s = x + y
+    return s, norm(s)
+
+
 class xLSTMBlock(nn.Module):
     def __init__(self, cfg: xLSTMLargeConfig):
         super().__init__()
@@ -233,8 +245,8 @@ class xLSTMBlock(nn.Module):
 
     def forward(self, x, state=None):
         y, state = self.mlstm_layer(self.norm_mlstm(x), state)
-        x = x + y
-        return x + self.ffn(self.norm_ffn(x)), state
+        x, n = _add_norm(x, y, self.norm_ffn)
+        return x + self.ffn(n), state
 
 
 class xLSTMLarge(nn.Module):
@@ -254,9 +266,23 @@ class xLSTMLarge(nn.Module):
     def forward(self, x, state=None):
         x = self.embedding(x)
         new_state = {}
+        # xLSTMBlock.forward unrolled so that every residual add meets the RMSNorm reading its
+        # result in one pass (_add_norm): the FFN branch of block i is added by block i+1's
+        # norm_mlstm (or the output norm), the mLSTM branch by the block's own norm_ffn
+        pending = None
         for i, blk in enumerate(self.blocks):
-            x, new_state[i] = blk(x, None if state is None else state.get(i))
-        logits = soft_cap(self.lm_head(self.out_norm(x)), self.config.output_logit_soft_cap)
+            if pending is None:
+                n = blk.norm_mlstm(x)
+            else:
+                x, n = _add_norm(x, pending, blk.norm_mlstm)
+            y, new_state[i] = blk.mlstm_layer(n, None if state is None else state.get(i))
+            x, n = _add_norm(x, y, blk.norm_ffn)
+            pending = blk.ffn(n)
+        if pending is None:
+            h = self.out_norm(x)
+        else:
+            x, h = _add_norm(x, pending, self.out_norm)
+        logits = soft_cap(self.lm_head(h), self.config.output_logit_soft_cap)
         if self.config.return_last_states:
             return logits, new_state
         return logits

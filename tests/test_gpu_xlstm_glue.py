@@ -88,6 +88,61 @@ def test_swiglu_vs_torch(rows, Fd):
     assert rel(af.grad, ar.grad) < 2e-2
 
 
+@pytest.mark.parametrize("D,rows", [(768, 3000), (512, 5)])
+def test_add_rms_norm_bitwise_vs_add_then_norm(D, rows):
+    """AddRMSNormFn (residual add folded into the RMSNorm, the residual gradient folded into its
+    backward) against x + r followed by RMSNormFn: the same bf16 roundings, so the sum, the
+    normalised output and every gradient are bitwise equal."""
+    g = torch.Generator(device=DEV).manual_seed(D * rows)
+    x = (torch.randn(rows, D, device=DEV, generator=g) * 2).to(torch.bfloat16)
+    r = torch.randn(rows, D, device=DEV, generator=g).to(torch.bfloat16)
+    w = 1 + 0.3 * torch.randn(D, device=DEV, generator=g)
+    ds = torch.randn(rows, D, device=DEV, generator=g).to(torch.bfloat16)
+    dn = torch.randn(rows, D, device=DEV, generator=g).to(torch.bfloat16)
+    res = []
+    for fused in (True, False):
+        xi, ri, wi = (t.clone().requires_grad_(True) for t in (x, r, w))
+        if fused:
+            sm, n = ops().add_rms_norm(xi, ri, wi, 1e-6)
+        else:
+            sm = xi + ri
+            n = ops().rms_norm(sm, wi, 1e-6)
+        torch.autograd.backward((sm, n), (ds, dn))
+        res.append((sm.detach(), n.detach(), xi.grad, ri.grad, wi.grad))
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
+
+
+def test_xlstm_unrolled_model_equals_block_loop():
+    """xLSTMLarge.forward (every residual add folded into the next RMSNorm) against the plain
+    loop over xLSTMBlock.forward with the inter-block adds as torch adds: bitwise equal logits
+    and parameter gradients under bf16 autocast."""
+    from statecatcher_amd import xlstm
+    cfg = xlstm.xLSTMLargeConfig(embedding_dim=256, num_heads=4, num_blocks=2, vocab_size=64,
+                                 input_dim=80)
+    torch.manual_seed(1)
+    model = xlstm.xLSTMLarge(cfg).to(DEV)
+    feats = torch.randn(2, 128, 80, device=DEV)
+
+    def loop(x):
+        x = model.embedding(x)
+        for blk in model.blocks:
+            x, _ = blk(x)
+        return xlstm.soft_cap(model.lm_head(model.out_norm(x)), cfg.output_logit_soft_cap)
+
+    res = []
+    for fn in (lambda f: model(f)[0], loop):
+        model.zero_grad()
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            logits = fn(feats)
+        logits.float().square().mean().backward()
+        res.append((logits.detach(), {n: p.grad.clone() for n, p in model.named_parameters()}))
+    (la, ga), (lb, gb) = res
+    assert torch.equal(la, lb)
+    for n in ga:
+        assert torch.equal(ga[n], gb[n]), n
+
+
 def test_xlstm_block_fused_equals_torch_path():
     """A whole xLSTM block under bf16 autocast: fused glue vs the torch path (glue disabled)."""
     from statecatcher_amd import xlstm
