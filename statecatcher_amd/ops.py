@@ -1370,12 +1370,13 @@ class AutocastLinearFn(torch.autograd.Function):
     The input gradient stays a library GEMM (NN form, TunableOp table)."""
 
     @staticmethod
-    def forward(ctx, x, w, b, cdt):
+    def forward(ctx, x, w, b, cdt, bias_from=0):
         xc = x.to(cdt)
         wc = w.to(cdt)
         y = torch.nn.functional.linear(xc, wc, None if b is None else b.to(cdt))
         ctx.save_for_backward(xc, wc)
         ctx.meta = (x.dtype, w.dtype, None if b is None else b.dtype)
+        ctx.bias_from = bias_from
         return y
 
     @staticmethod
@@ -1410,15 +1411,24 @@ class AutocastLinearFn(torch.autograd.Function):
                         dw = torch.cat([head, tail])
             dw = (dw if dw is not None else (dy2.t() @ x2).float()).to(wdt)
         if bdt is not None and ctx.needs_input_grad[2]:
-            db = colsum(dy2).to(bdt)
-        return dx, dw, db, None
+            f = ctx.bias_from
+            if f and f < N and (f * dy2.element_size()) % 16 == 0:
+                # bias entries before `f` are constant zero pieces (the xLSTM projection's
+                # q|k|v|o part): only the gate columns are summed over the B*T rows
+                db = torch.cat([torch.zeros(f, dtype=torch.float32, device=dy2.device),
+                                colsum(dy2[:, f:])]).to(bdt)
+            else:
+                db = colsum(dy2).to(bdt)
+        return dx, dw, db, None, None
 
 
-def autocast_linear(x, w, b=None):
-    """nn.Linear semantics under autocast (bf16 compute when enabled) through AutocastLinearFn."""
+def autocast_linear(x, w, b=None, bias_from=0):
+    """nn.Linear semantics under autocast (bf16 compute when enabled) through AutocastLinearFn.
+    bias_from: b[:bias_from] is a constant (its gradient is not summed; the returned gradient
+    there is 0)."""
     if x.is_cuda and torch.is_autocast_enabled("cuda"):
         cdt = torch.get_autocast_dtype("cuda")
     else:
         cdt = torch.promote_types(x.dtype, w.dtype)
     with torch.autocast("cuda", enabled=False):
-        return AutocastLinearFn.apply(x, w, b, cdt)
+        return AutocastLinearFn.apply(x, w, b, cdt, int(bias_from))

@@ -29,11 +29,12 @@ from . import ops
 from .ops import mlstm_chunkwise
 
 
-def _linear(x, w, b=None):
+def _linear(x, w, b=None, bias_from=0):
     """nn.Linear under autocast; on the GPU through ops.autocast_linear, whose backward takes the
-    weight gradient (a reduction over all B*T rows) from the MFMA split-L kernel."""
+    weight gradient (a reduction over all B*T rows) from the MFMA split-L kernel.  bias_from:
+    b[:bias_from] are constant zero pieces whose gradient is not summed."""
     if x.is_cuda:
-        return ops.autocast_linear(x, w, b)
+        return ops.autocast_linear(x, w, b, bias_from)
     return F.linear(x, w, b)
 
 
@@ -177,11 +178,16 @@ class mLSTMLayer(nn.Module):
         mods = self._mods()
         w = torch.cat([m.weight for m in mods])
         b = None
+        lead = 0   # leading bias columns that are cached zero pieces (no gradient to sum)
         if any(m.bias is not None for m in mods):
             b = torch.cat([m.bias if m.bias is not None else
                            _zeros(m.weight.shape[0], m.weight.dtype, m.weight.device)
                            for m in mods])
-        return _linear(x, w, b)
+            for m in mods:
+                if m.bias is not None:
+                    break
+                lead += m.weight.shape[0]
+        return _linear(x, w, b, lead)
 
     def projections(self, x):
         return self.projection(x).split([m.weight.shape[0] for m in self._mods()], -1)

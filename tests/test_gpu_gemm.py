@@ -210,3 +210,21 @@ def test_autocast_linear_wgrad_split_head():
     ref = dy.float().t() @ x
     err = (wr.grad - ref).abs().max().item() / ref.abs().max().item()
     assert err < 1e-5, err
+
+
+def test_autocast_linear_bias_from_sums_only_the_gate_columns():
+    """bias_from = 2304 (the xLSTM projection: q|k|v|o bias pieces are constant zeros): the bias
+    gradient of columns >= bias_from equals the full column sum, the leading part is 0."""
+    g = torch.Generator(device=DEV).manual_seed(12)
+    x = torch.randn(4096, 768, device=DEV, generator=g)
+    w = torch.randn(2312, 768, device=DEV, generator=g) * 0.02
+    b = torch.zeros(2312, device=DEV)
+    b[2304:] = torch.randn(8, device=DEV, generator=g)
+    dy = torch.randn(4096, 2312, device=DEV, generator=g).to(torch.bfloat16)
+    bq = b.clone().requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = ops().autocast_linear(x, w, bq, 2304)
+    y.backward(dy)
+    ref = dy.float().sum(0)
+    assert bool((bq.grad[:2304] == 0).all())
+    torch.testing.assert_close(bq.grad[2304:], ref[2304:], rtol=1e-5, atol=1e-4)
