@@ -949,6 +949,7 @@ class MLSTMFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, q, k, v, igate, fgate, c0, n0, m0, eps):
         require_device(q, k, v, igate, fgate)
+        ctx.set_materialize_grads(False)   # detached carried states: no zero-filled gradients
         B, NH, T, DQ = q.shape
         DV = v.shape[-1]
         cdt = q.dtype if q.dtype in (torch.bfloat16, torch.float16) else torch.bfloat16
@@ -993,6 +994,8 @@ class MLSTMFn(torch.autograd.Function):
         B, NH, T, DQ, DV, eps, qdt, kdt, vdt, has_c0, has_n0 = ctx.meta
         BH, nc = B * NH, T // 64
         dev = qc.device
+        if dh is None:
+            dh = torch.zeros(B, NH, T, DV, dtype=qc.dtype, device=dev)
         dhc = dh.to(qc.dtype).contiguous().view(BH, T, DV)
         dcTc = None if dcT is None else dcT.float().contiguous()
         dnTc = None if dnT is None else dnT.float().contiguous()
@@ -1048,6 +1051,7 @@ class MLSTMCoreFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, a, c0, n0, m0, w_mh, NH, DQ, DV, cap, eps, eps_mh):
         require_device(a)
+        ctx.set_materialize_grads(False)   # detached carried states: no zero-filled gradients
         B, T, N = a.shape
         lib = _lib.load()
         qo, ko, vo = 0, NH * DQ, 2 * NH * DQ
@@ -1107,6 +1111,8 @@ class MLSTMCoreFn(torch.autograd.Function):
         esz = a.element_size()
         base = a.data_ptr()
         stream = stream_of(a)
+        if dy is None:
+            dy = torch.zeros(B, T, NH * DV, dtype=torch.bfloat16, device=dev)
         dyc = dy.to(torch.bfloat16)
         if dyc.stride(2) != 1 or dyc.stride(0) != T * dyc.stride(1) or dyc.stride(1) % 4:
             dyc = dyc.contiguous()
