@@ -1387,45 +1387,99 @@ class AutocastLinearFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        xc, wc = ctx.saved_tensors
-        xdt, wdt, bdt = ctx.meta
-        N, K = wc.shape
-        dy2 = dy.reshape(-1, N).to(wc.dtype)
-        x2 = xc.reshape(-1, K)
-        dx = dw = db = None
-        if ctx.needs_input_grad[0]:
-            dx = (dy2 @ wc).view(*dy.shape[:-1], K).to(xdt)
-        if ctx.needs_input_grad[1]:
-            dw = None
-            if dy2.is_cuda and dy2.dtype == torch.bfloat16:
-                dyc, xcc = dy2.contiguous(), x2.contiguous()
-                dw = wgrad_mfma(dyc, xcc)
-                n0 = N - N % 256
-                if dw is None and 256 <= n0 < N:
-                    # e.g. the xLSTM q|k|v|o|i|f projection (N = 2312 at C4): the first N0 rows
-                    # of dW on the MFMA kernel (dy's row stride 2312 is a multiple of 8), the
-                    # gate rows that remain as a small library GEMM
-                    head = wgrad_mfma(dyc[:, :n0], xcc)
-                    if head is not None:
-                        # the tail rows from the MFMA kernel too, over the last 256-row window
-                        # (a 16-byte aligned view when N % 8 == 0; its first rows repeat the
-                        # head's): an M = 8, K = 48000 library GEMM took 130 us at C4, the
-                        # window ~30 us
-                        win = wgrad_mfma(dyc[:, N - 256:], xcc)
-                        tail = win[256 - (N - n0):] if win is not None else \
-                            _mm_f32(dyc[:, n0:].t(), xcc)
-                        dw = torch.cat([head, tail])
-            dw = (dw if dw is not None else (dy2.t() @ x2).float()).to(wdt)
-        if bdt is not None and ctx.needs_input_grad[2]:
-            f = ctx.bias_from
-            if f and f < N and (f * dy2.element_size()) % 16 == 0:
-                # bias entries before `f` are constant zero pieces (the xLSTM projection's
-                # q|k|v|o part): only the gate columns are summed over the B*T rows
-                db = torch.cat([torch.zeros(f, dtype=torch.float32, device=dy2.device),
-                                colsum(dy2[:, f:])]).to(bdt)
-            else:
-                db = colsum(dy2).to(bdt)
+        dx, dw, db = _linear_grads(ctx, dy, *ctx.needs_input_grad[:3])
         return dx, dw, db, None, None
+
+
+def _linear_grads(ctx, dy, need_x, need_w, need_b):
+    """(dx, dW, db) of AutocastLinearFn / FusedLinearFn from the saved (xc, wc), ctx.meta and
+    ctx.bias_from."""
+    xc, wc = ctx.saved_tensors
+    xdt, wdt, bdt = ctx.meta
+    N, K = wc.shape
+    dy2 = dy.reshape(-1, N).to(wc.dtype)
+    x2 = xc.reshape(-1, K)
+    dx = dw = db = None
+    if need_x:
+        dx = (dy2 @ wc).view(*dy.shape[:-1], K).to(xdt)
+    if need_w:
+        dw = None
+        if dy2.is_cuda and dy2.dtype == torch.bfloat16:
+            dyc, xcc = dy2.contiguous(), x2.contiguous()
+            dw = wgrad_mfma(dyc, xcc)
+            n0 = N - N % 256
+            if dw is None and 256 <= n0 < N:
+                # e.g. the xLSTM q|k|v|o|i|f projection (N = 2312 at C4): the first N0 rows
+                # of dW on the MFMA kernel (dy's row stride 2312 is a multiple of 8), the
+                # gate rows that remain as a small library GEMM
+                head = wgrad_mfma(dyc[:, :n0], xcc)
+                if head is not None:
+                    # the tail rows from the MFMA kernel too, over the last 256-row window
+                    # (a 16-byte aligned view when N % 8 == 0; its first rows repeat the
+                    # head's): an M = 8, K = 48000 library GEMM took 130 us at C4, the
+                    # window ~30 us
+                    win = wgrad_mfma(dyc[:, N - 256:], xcc)
+                    tail = win[256 - (N - n0):] if win is not None else \
+                        _mm_f32(dyc[:, n0:].t(), xcc)
+                    dw = torch.cat([head, tail])
+        dw = (dw if dw is not None else (dy2.t() @ x2).float()).to(wdt)
+    if bdt is not None and need_b:
+        f = ctx.bias_from
+        if f and f < N and (f * dy2.element_size()) % 16 == 0:
+            # bias entries before `f` are constant zero pieces (the xLSTM projection's
+            # q|k|v|o part): only the gate columns are summed over the B*T rows
+            db = torch.cat([torch.zeros(f, dtype=torch.float32, device=dy2.device),
+                            colsum(dy2[:, f:])]).to(bdt)
+        else:
+            db = colsum(dy2).to(bdt)
+    return dx, dw, db
+
+
+class FusedLinearFn(torch.autograd.Function):
+    """AutocastLinearFn over the row-concatenation of several fp32 weights (the xLSTM fused
+    projections) without materialising the fp32 concatenation: the bf16 image [sum rows, K] is
+    written by ONE sc_weight_images launch (cast and concatenation together), and the weight
+    gradient is split back into one gradient per weight.  Same roundings as cat -> cast."""
+
+    @staticmethod
+    def forward(ctx, x, b, cdt, bias_from, *ws):
+        rows = [w.shape[0] for w in ws]
+        K = ws[0].shape[1]
+        wc = torch.empty(sum(rows), K, dtype=cdt, device=x.device)
+        jobs, off = [], 0
+        for w, r in zip(ws, rows):
+            jobs.append(_lib.ImageJob(w.data_ptr(), wc[off].data_ptr(), None, r, K, K, w.stride(0), 0))
+            off += r
+        _image_jobs(jobs, list(ws))
+        xc = x.to(cdt)
+        y = torch.nn.functional.linear(xc, wc, None if b is None else b.to(cdt))
+        ctx.save_for_backward(xc, wc)
+        ctx.meta = (x.dtype, ws[0].dtype, None if b is None else b.dtype)
+        ctx.bias_from = bias_from
+        ctx.rows = rows
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        need = ctx.needs_input_grad
+        dx, dw, db = _linear_grads(ctx, dy, need[0], any(need[4:]), need[1])
+        dws = dw.split(ctx.rows) if dw is not None else [None] * len(ctx.rows)
+        return (dx, db, None, None) + tuple(dws)
+
+
+def fused_linear_ok(x, ws):
+    """FusedLinearFn's preconditions: bf16 autocast on a ROCm device, fp32 weights with unit
+    column stride and one common K."""
+    return (x.is_cuda and torch.is_autocast_enabled("cuda")
+            and torch.get_autocast_dtype("cuda") == torch.bfloat16
+            and all(w.is_cuda and w.dtype == torch.float32 and w.dim() == 2 and w.stride(1) == 1
+                    and w.shape[1] == ws[0].shape[1] for w in ws))
+
+
+def fused_linear(x, ws, b=None, bias_from=0):
+    """nn.Linear under bf16 autocast with weight = torch.cat(ws) (FusedLinearFn)."""
+    with torch.autocast("cuda", enabled=False):
+        return FusedLinearFn.apply(x, b, torch.bfloat16, int(bias_from), *ws)
 
 
 def autocast_linear(x, w, b=None, bias_from=0):

@@ -137,11 +137,14 @@ class FeedForward(nn.Module):
         # proj_up_gate and proj_up as ONE GEMM over the concatenated weight (parameters and
         # state_dict unchanged): one read and one autocast cast of x instead of two
         up = self.proj_up.weight.shape[0]
-        w = torch.cat([self.proj_up_gate.weight, self.proj_up.weight])
+        ws = [self.proj_up_gate.weight, self.proj_up.weight]
         b = None
         if self.proj_up.bias is not None:
             b = torch.cat([self.proj_up_gate.bias, self.proj_up.bias])
-        a = _linear(x, w, b)
+        if ops.fused_linear_ok(x, ws):   # the bf16 image of the concatenation in one launch
+            a = ops.fused_linear(x, ws, b)
+        else:
+            a = _linear(x, torch.cat(ws), b)
         if a.is_cuda and a.dtype == torch.bfloat16 and up % 4 == 0:
             # one HIP pass, one [dg | du] gradient
             return _linear(ops.swiglu(a), self.proj_down.weight, self.proj_down.bias)
@@ -176,7 +179,7 @@ class mLSTMLayer(nn.Module):
         times, and the two NH-wide gate projections (4 output columns each at C4) stop being
         GEMMs of their own."""
         mods = self._mods()
-        w = torch.cat([m.weight for m in mods])
+        ws = [m.weight for m in mods]
         b = None
         lead = 0   # leading bias columns that are cached zero pieces (no gradient to sum)
         if any(m.bias is not None for m in mods):
@@ -187,7 +190,9 @@ class mLSTMLayer(nn.Module):
                 if m.bias is not None:
                     break
                 lead += m.weight.shape[0]
-        return _linear(x, w, b, lead)
+        if ops.fused_linear_ok(x, ws):   # the bf16 image of the concatenation in one launch
+            return ops.fused_linear(x, ws, b, lead)
+        return _linear(x, torch.cat(ws), b, lead)
 
     def projections(self, x):
         return self.projection(x).split([m.weight.shape[0] for m in self._mods()], -1)

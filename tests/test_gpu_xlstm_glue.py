@@ -215,3 +215,27 @@ def test_mlstm_core_equals_composed_ops(with_state, monkeypatch):
                    ([sti[0].grad, sti[1].grad] if sti else []))
     for i, (u, v) in enumerate(zip(*res)):
         assert torch.equal(u, v), i
+
+
+def test_fused_linear_bitwise_vs_cat_then_linear():
+    """FusedLinearFn (bf16 image of the row-concatenated weights in one sc_weight_images launch,
+    weight gradient split back per weight) against torch.cat -> AutocastLinearFn: the same
+    roundings, so output and every gradient are bitwise equal."""
+    g = torch.Generator(device=DEV).manual_seed(21)
+    x = torch.randn(3, 640, 768, device=DEV, generator=g).to(torch.bfloat16)
+    ws = [torch.randn(n, 768, device=DEV, generator=g) * 0.02 for n in (384, 384, 768, 768, 4, 4)]
+    b = torch.cat([torch.zeros(2304, device=DEV), torch.randn(8, device=DEV, generator=g)])
+    dy = torch.randn(3, 640, 2312, device=DEV, generator=g).to(torch.bfloat16)
+    res = []
+    for fused in (True, False):
+        xi = x.clone().requires_grad_(True)
+        wi = [w.clone().requires_grad_(True) for w in ws]
+        bi = b.clone().requires_grad_(True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            assert ops().fused_linear_ok(xi, wi)
+            y = (ops().fused_linear(xi, wi, bi, 2304) if fused
+                 else ops().autocast_linear(xi, torch.cat(wi), bi, 2304))
+        y.backward(dy)
+        res.append([y.detach(), xi.grad, bi.grad] + [w.grad for w in wi])
+    for a, c in zip(*res):
+        assert torch.equal(a, c)
