@@ -243,6 +243,255 @@ __global__ void __launch_bounds__(512) tn_kernel(TnArgs a) {
   if (st_done < NST) store_some(NST);
 }
 
+// ------------------------------------------------------------------------------------------
+// 256 x 256 tiles, four-phase quadrant schedule (the default since round 3).
+//
+// A K-tile (64 columns) of the 256 x 256 output tile is four PHASES; in each, all 8 waves compute
+// one 128 x 128 QUADRANT of the tile (per wave 64 rows x 32 columns: 4 x 2 fragments, 16
+// v_mfma_f32_16x16x32_bf16) in the order (0,0) (0,1) (1,1) (1,0), so each phase needs ONE new
+// operand half (A rows 0-127 / 128-255 = "A0" / "A1", B rows likewise "B0" / "B1") and reuses
+// the other from registers:
+//   phase 1: A0 x B0   (A0, B0 read from LDS in phase 4 of the previous K-tile)
+//   phase 2: A0 x B1   (B1 read in phase 1)
+//   phase 3: A1 x B1   (A1 read in phase 2)
+//   phase 4: A1 x B0   (B0 read again in phase 3; A0, B0 of the next K-tile are read here)
+// LDS holds two K-tiles (2 x 4 halves x 16 KiB = 128 KiB).  Each half of K-tile g + 2 is
+// restaged into buffer g % 2 by LDS-DMA one phase after its last fragment read in K-tile g
+// (A0 in phase 1, B1 in 2, A1 in 3, B0 in 4): three halves (6 DMA instructions per thread) stay
+// in flight, and ONE counted wait per K-tile -- vmcnt(6) at the end of phase 3, which retires
+// B0 of the NEXT K-tile and everything older -- orders every fragment read after its DMA.  One
+// LDS-only barrier per phase; the MFMA cluster of a phase is bracketed by s_setprio so hipcc keeps
+// it between its barriers (cdna_hip_programming.md T5).
+// Epilogue: a quadrant's accumulators are final one phase after its last MFMAs; it is packed to
+// bf16 and stored in a later phase (q00 in phase 2 and q01 in phase 4 of the tile's last K-tile,
+// q11 in phase 1 and q10 in phase 2 of the next tile's first K-tile) -- the output stream runs
+// beside the MFMAs and no registers are held across tiles.  Buffer stores: rows >= M fall
+// outside the descriptor's range and are dropped.  Stores are never issued in phase 3 and are
+// younger than the B0 DMA the phase-3 wait targets, so they only inflate that count (loads
+// complete in order among themselves): the wait stays exact.
+constexpr int kHalfB = 128 * kRowB;   // one operand half: 128 rows x 128 B
+
+// MFMA fragment sets of one operand half, named (static indexing only: rule 20)
+struct FragA { i4v v[4][2]; };   // 4 row fragments (x rows) x 2 k-steps
+struct FragB { i4v v[2][2]; };   // 2 column fragments (W rows) x 2 k-steps
+
+__global__ void __launch_bounds__(512, 1) tn256_kernel(TnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const int lane = threadIdx.x & 63;
+  const int w = uniform(threadIdx.x >> 6);
+  const int wm = w >> 2, wn = w & 3;
+  const int l15 = lane & 15, l4 = lane >> 4;
+
+  const int G = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid % 8, qq = G / 8, rr = G % 8;
+  const int lid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + bid / 8;
+  const int nkt = a.K / kBK;
+  const int ntw = lid < a.tiles ? (a.tiles - lid + G - 1) / G : 0;
+  const int NG = ntw * nkt;
+  const uint32_t lds0 = lds_addr(lds);
+
+  // ---- DMA: wave w stages rows 16 w .. 16 w + 15 of a half (two 1-KiB pieces of 8 rows) ----
+  int drow[2];
+  uint32_t dcol[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int r = 8 * (2 * w + q) + (lane >> 3);
+    drow[q] = r;
+    dcol[q] = 8u * (uint32_t)((lane & 7) ^ swz(r));
+  }
+  // cursor of the DMA stream: K-tile dg of this workgroup's sequence
+  int dg = 0, dkt = 0, dtile = lid;
+  int dm0 = (dtile / a.ntn) * 256, dn0 = (dtile % a.ntn) * 256;
+  auto dma_half = [&](int h) __attribute__((always_inline)) {   // half h of K-tile dg
+    const uint32_t dst = lds0 + (uint32_t)(((dg & 1) * 4 + h) * kHalfB + 2 * w * 1024);
+    const uint32_t k0 = (uint32_t)dkt * kBK;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      if (h < 2) {
+        const uint32_t row = (uint32_t)min(dm0 + h * 128 + drow[q], a.M - 1);
+        dma_to_lds_s<16>(a.A, (row * a.lda + k0 + dcol[q]) * 2u, dst + q * 1024);
+      } else {
+        const uint32_t row = (uint32_t)(dn0 + (h - 2) * 128 + drow[q]);
+        dma_to_lds_s<16>(a.B, (row * a.ldb + k0 + dcol[q]) * 2u, dst + q * 1024);
+      }
+    }
+  };
+  auto dma_next = [&]() __attribute__((always_inline)) {   // advance the cursor one K-tile
+    ++dg;
+    if (++dkt == nkt) {
+      dkt = 0;
+      dtile += G;
+      dm0 = (dtile / a.ntn) * 256;
+      dn0 = (dtile % a.ntn) * 256;
+    }
+  };
+
+  // ---- fragment reads (byte offsets within a half; k-step kk flips address bit 6) ----
+  uint32_t offA[4], offB[2];
+#pragma unroll
+  for (int mf = 0; mf < 4; ++mf) {
+    const int r = wm * 64 + mf * 16 + l15;
+    offA[mf] = (uint32_t)(r * kRowB + 16 * (l4 ^ swz(r)));
+  }
+#pragma unroll
+  for (int nf = 0; nf < 2; ++nf) {
+    // W row for MFMA row i = l15 of column fragment nf: the lane's 2 x 4 accumulator values
+    // then hold output columns wn*32 + l4*8 + 0..7 (one 16-byte store per row fragment)
+    const int r = wn * 32 + (l15 >> 2) * 8 + nf * 4 + (l15 & 3);
+    offB[nf] = (uint32_t)(r * kRowB + 16 * (l4 ^ swz(r)));
+  }
+  auto half_base = [&](int buf, int h) __attribute__((always_inline)) {
+    return lds0 + (uint32_t)((buf * 4 + h) * kHalfB);
+  };
+  auto read_A = [&](int buf, int qm, FragA& f) __attribute__((always_inline)) {
+    const uint32_t hb = half_base(buf, qm);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int mf = 0; mf < 4; ++mf) f.v[mf][kk] = lds_read16(hb + (offA[mf] ^ (64u * kk)));
+  };
+  auto read_B = [&](int buf, int qn, FragB& f) __attribute__((always_inline)) {
+    const uint32_t hb = half_base(buf, 2 + qn);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int nf = 0; nf < 2; ++nf) f.v[nf][kk] = lds_read16(hb + (offB[nf] ^ (64u * kk)));
+  };
+
+  f4v acc[4][4][2];   // [quadrant (0,0) (0,1) (1,1) (1,0)][row frag][col frag]
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int mf = 0; mf < 4; ++mf)
+#pragma unroll
+      for (int nf = 0; nf < 2; ++nf) acc[q][mf][nf] = f4v{0.f, 0.f, 0.f, 0.f};
+  auto quad = [&](f4v (&c)[4][2], const FragA& fa, const FragB& fb) __attribute__((always_inline)) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int mf = 0; mf < 4; ++mf)
+#pragma unroll
+        for (int nf = 0; nf < 2; ++nf) {
+          if (SC_TN_ABL & 1)
+            c[mf][nf][0] += (float)(fb.v[nf][kk][0] ^ fa.v[mf][kk][1]);
+          else
+            c[mf][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                __builtin_bit_cast(b8v, fb.v[nf][kk]), __builtin_bit_cast(b8v, fa.v[mf][kk]),
+                c[mf][nf], 0, 0, 0);
+        }
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  // ---- epilogue: one quadrant (4 row fragments x one 16-byte store), then zeroed ----
+  const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(a.C, 0, a.cbytes, 0x00020000);
+  auto store_quad = [&](f4v (&c)[4][2], int m0, int n0, int qm, int qn) __attribute__((always_inline)) {
+    const uint32_t row = (uint32_t)(m0 + qm * 128 + wm * 64 + l15);
+    const uint32_t col = (uint32_t)(n0 + qn * 128 + wn * 32 + l4 * 8);
+#pragma unroll
+    for (int mf = 0; mf < 4; ++mf) {
+      i4v v;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const int nf = d >> 1, j = 2 * (d & 1);
+        const b2v p = {(__bf16)c[mf][nf][j], (__bf16)c[mf][nf][j + 1]};
+        v[d] = __builtin_bit_cast(int, p);
+      }
+      __builtin_amdgcn_raw_buffer_store_b128(v, crs, ((row + 16u * mf) * a.ldc + col) * 2u, 0, 0);
+#pragma unroll
+      for (int nf = 0; nf < 2; ++nf) c[mf][nf] = f4v{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+
+  if (NG == 0) return;
+  // ---- prologue: K-tiles 0 and 1 (halves in the steady-state issue order A0 B1 A1 B0) ----
+#pragma unroll
+  for (int g0 = 0; g0 < 2; ++g0)
+    if (dg < NG) {
+      dma_half(0); dma_half(3); dma_half(1); dma_half(2);
+      dma_next();
+    }
+  if (NG > 1) dma_wait_younger<8>(); else dma_wait();
+  lds_barrier();
+  // B fragment sets X / Y alternate roles between K-tiles (static names: the K-tile loop is
+  // unrolled by two): B0 is read twice per K-tile (phases 4 of the previous and 3 of this one)
+  // instead of living in registers through all four phases -- 16 registers fewer, no spills
+  FragA fa0, fa1;
+  FragB fbX, fbY;
+  read_A(0, 0, fa0);
+  read_B(0, 0, fbX);
+  lds_read_wait();
+
+  int kt = 0, tile = lid, pm0 = 0, pn0 = 0;
+  int m0 = (tile / a.ntn) * 256, n0 = (tile % a.ntn) * 256;
+  auto ktile = [&](int g, FragB& X, FragB& Y) __attribute__((always_inline)) {
+    const int buf = g & 1;
+    const bool first = kt == 0, last = kt == nkt - 1;
+    const bool more = dg < NG;   // K-tile g + 2 exists
+    // phase 1: quadrant (0,0) = A0 x B0 (X)
+    if (first && g > 0) store_quad(acc[2], pm0, pn0, 1, 1);
+    if (more && !(SC_TN_ABL & 2)) dma_half(0);
+    read_B(buf, 1, Y);
+    quad(acc[0], fa0, X);
+    lds_read_wait();
+    lds_barrier();
+    // phase 2: quadrant (0,1) = A0 x B1 (Y)
+    if (first && g > 0) store_quad(acc[3], pm0, pn0, 1, 0);
+    if (last) store_quad(acc[0], m0, n0, 0, 0);
+    if (more && !(SC_TN_ABL & 2)) dma_half(3);
+    read_A(buf, 1, fa1);
+    quad(acc[1], fa0, Y);
+    lds_read_wait();
+    lds_barrier();
+    // phase 3: quadrant (1,1) = A1 x B1 (Y); B0 read again into X; then retire B0 of K-tile
+    // g + 1 (and all older DMA)
+    if (more && !(SC_TN_ABL & 2)) dma_half(1);
+    read_B(buf, 0, X);
+    quad(acc[2], fa1, Y);
+    lds_read_wait();
+    if (more) dma_wait_younger<6>(); else dma_wait();
+    lds_barrier();
+    // phase 4: quadrant (1,0) = A1 x B0 (X); A0, B0 of K-tile g + 1 come out of LDS (into Y)
+    if (last) store_quad(acc[1], m0, n0, 0, 1);
+    if (more && !(SC_TN_ABL & 2)) dma_half(2);
+    if (more) dma_next();
+    if (g + 1 < NG) {
+      read_A(buf ^ 1, 0, fa0);
+      read_B(buf ^ 1, 0, Y);
+    }
+    quad(acc[3], fa1, X);
+    lds_read_wait();
+    lds_barrier();
+    if (++kt == nkt) {
+      kt = 0;
+      pm0 = m0;
+      pn0 = n0;
+      tile += G;
+      m0 = (tile / a.ntn) * 256;
+      n0 = (tile % a.ntn) * 256;
+    }
+  };
+  int g = 0;
+  for (; g + 1 < NG; g += 2) {
+    ktile(g, fbX, fbY);
+    ktile(g + 1, fbY, fbX);
+  }
+  if (g < NG) ktile(g, fbX, fbY);
+  store_quad(acc[2], pm0, pn0, 1, 1);
+  store_quad(acc[3], pm0, pn0, 1, 0);
+}
+
+int launch_tn256(const TnArgs& a, hipStream_t st) {
+  constexpr size_t lds = 2 * 4 * (size_t)kHalfB;   // 128 KiB
+  static const bool ok = hipFuncSetAttribute((const void*)tn256_kernel,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             (int)lds) == hipSuccess;
+  (void)ok;
+  const int grid = a.tiles < 256 ? a.tiles : 256;
+  hipLaunchKernelGGL(tn256_kernel, dim3(grid), dim3(512), lds, st, a);
+  return 0;
+}
+
 template <int MF, int SPI>
 int launch_tn(const TnArgs& a, hipStream_t st) {
   auto kern = tn_kernel<MF, SPI>;
@@ -268,8 +517,8 @@ extern "C" int sc_gemm_tn_bf16(const void* A, int64_t lda, const void* B, int64_
   SC_REQUIRE(M > 0 && N > 0 && K > 0, "sc_gemm_tn_bf16: empty shape M=%d N=%d K=%d", M, N, K);
   SC_REQUIRE(K % kBK == 0, "sc_gemm_tn_bf16: K=%d must be a multiple of 64 (zero-pad it)", K);
   SC_REQUIRE(N % kTN == 0, "sc_gemm_tn_bf16: N=%d must be a multiple of 256", N);
-  SC_REQUIRE(tile_m == 0 || tile_m == 128 || tile_m == 192,
-             "sc_gemm_tn_bf16: tile_m=%d must be 0 (default 192), 128 or 192", tile_m);
+  SC_REQUIRE(tile_m == 0 || tile_m == 128 || tile_m == 192 || tile_m == 256,
+             "sc_gemm_tn_bf16: tile_m=%d must be 0 (default 192), 128, 192 or 256", tile_m);
   SC_REQUIRE(lda >= K && ldb >= K && ldc >= N && lda % 8 == 0 && ldb % 8 == 0 && ldc % 8 == 0,
              "sc_gemm_tn_bf16: leading dimensions must cover the rows in 16-byte pieces");
   SC_REQUIRE((uintptr_t)A % 16 == 0 && (uintptr_t)B % 16 == 0 && (uintptr_t)C % 16 == 0,
@@ -284,6 +533,10 @@ extern "C" int sc_gemm_tn_bf16(const void* A, int64_t lda, const void* B, int64_
   TnArgs a{(const __bf16*)A, (const __bf16*)B, (__bf16*)C, M, N, K, ntn, (int)tiles,
            (uint32_t)lda, (uint32_t)ldb, (uint32_t)ldc, (uint32_t)((int64_t)M * ldc * 2)};
   hipStream_t st = (hipStream_t)stream;
+  if (tm == 256) {
+    launch_tn256(a, st);
+    return launch_status("sc_gemm_tn_bf16");
+  }
   // stores per stage: a tile's 2 MF stores must be issued within the next tile's K / 64 stages
   const int nks = K / kBK, nst = 2 * (tm / 32);
   const int spi = (nst + nks - 1) / nks;

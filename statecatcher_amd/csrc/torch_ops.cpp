@@ -121,12 +121,15 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> lucy_scan_fwd_meta(const Tensor& gate
           at::empty({need_ckpt ? sc_lucy_scan_ckpt_numel(B, T, D) : 0}, opt.dtype(at::kFloat))};
 }
 
-std::tuple<Tensor, Tensor, Tensor, Tensor> lucy_scan_bwd_hip(const Tensor& gates, const Tensor& ckpt,
+std::tuple<Tensor, Tensor, Tensor, Tensor> lucy_scan_bwd_hip(const Tensor& gates_in, const Tensor& ckpt,
                                                              const Tensor& dout_in,
                                                              const optional<Tensor>& ds_last,
                                                              const optional<Tensor>& bias,
                                                              bool want_dbias) {
-  c10::DeviceGuard guard(gates.device());
+  c10::DeviceGuard guard(gates_in.device());
+  // the same layouts the forward accepts: a [B,T,7,D] view strided in D is made contiguous
+  Tensor gates = gates_in;
+  if (gates.dim() == 4 && gates.size(2) == 7 && gates.stride(3) != 1) gates = gates.contiguous();
   const GateLayout L = gate_layout(gates);
   TORCH_CHECK(ckpt.numel() == sc_lucy_scan_ckpt_numel(L.B, L.T, L.D) && ckpt.scalar_type() == at::kFloat,
               "statecatcher::lucy_scan_bwd: ckpt is not the forward's checkpoint (run the forward "

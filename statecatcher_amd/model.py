@@ -94,8 +94,8 @@ def compute_loss(mode: str, criterion: nn.Module, model: nn.Module, feats: torch
         predictor_input = torch.cat([blank_prefix, tokens], dim=1)
         use_compact = bool(getattr(args, "compact_rnnt", False)) if args is not None else compact
         jm = getattr(use_rnnt_joiner, "module", use_rnnt_joiner)   # DDP-wrapped or not
-        if isinstance(criterion, RNNTLoss) and enc_out.is_cuda and \
-                rnnt_joint_supported(jm.joiner.in_features, jm.joiner.out_features):
+        if isinstance(criterion, RNNTLoss) and enc_out.is_cuda and criterion.use_fused_joint() \
+                and rnnt_joint_supported(jm.joiner.in_features, jm.joiner.out_features):
             # fused joiner + log_softmax + lattice (rnnt.hip joint_*): the (B, T, U+1, V) logits
             # are never materialised; same value as the compact and dense paths below
             enc_p, pred_p, W, bias = (use_rnnt_joiner(enc_out, predictor_input, in_lens, tgt_lens,
@@ -130,11 +130,21 @@ class RNNTLoss(nn.Module):
     the reference assigns the class itself as criterion, so its call constructs a module instead
     of computing a loss; this is the intended loss (warp_rnnt.rnnt_loss, reduction 'mean')."""
 
-    def __init__(self, blank=0, reduction="mean", average_frames=False):
+    def __init__(self, blank=0, reduction="mean", average_frames=False, fused_joint=None):
         super().__init__()
         self.blank = blank
         self.reduction = reduction
         self.average_frames = average_frames
+        # fused joiner + loss (ops.RNNTJointFn) rounds W and tanh(enc + pred) to bf16 before its
+        # MFMAs.  None: only where the step already computes in a 16-bit autocast dtype; fp32
+        # training keeps the reference's fp32 logits (materialised path).  True / False force it.
+        self.fused_joint = fused_joint
+
+    def use_fused_joint(self):
+        if self.fused_joint is not None:
+            return bool(self.fused_joint)
+        return (torch.is_autocast_enabled("cuda")
+                and torch.get_autocast_dtype("cuda") in (torch.bfloat16, torch.float16))
 
     def forward(self, log_probs, labels, frames_lengths, labels_lengths, blank_id=None,
                 compact=False, gather=True):
@@ -259,12 +269,15 @@ class ASRModel(nn.Module):
         return logits, new_states
 
 
-def build_xlstm_config(feat_dim, vocab_size, num_heads=2, num_blocks=3, embedding_dim=None):
+def build_xlstm_config(feat_dim, vocab_size, num_heads=2, num_blocks=3, embedding_dim=None,
+                       autocast_kernel_dtype="bfloat16"):
     """model.py:214-229: the xLSTM config train.py builds (embedding_dim = input_dim = feat_dim
-    in the reference; C4 uses a 768-wide model behind the input projection)."""
+    in the reference; C4 uses a 768-wide model behind the input projection).  The reference
+    passes autocast_kernel_dtype="float16" (model.py:227): the mLSTM cell then computes in fp16."""
     return xLSTMLargeConfig(embedding_dim=embedding_dim or feat_dim, input_dim=feat_dim,
                             num_heads=num_heads, num_blocks=num_blocks, vocab_size=vocab_size,
-                            return_last_states=True, mode="train")
+                            return_last_states=True, mode="train",
+                            autocast_kernel_dtype=autocast_kernel_dtype)
 
 
 def build_lucyrnn_config(input_dim, hidden_size, num_layers, vocab_size, is_training=True):

@@ -272,6 +272,29 @@ def pad_cols(x, k, dtype):
 from torch.utils.weak import WeakIdKeyDictionary  # noqa: E402
 
 _IMAGES = WeakIdKeyDictionary()
+# STATECATCHER_CHECK_IMAGES=1: on every cache hit, compare a few elements of the image with the
+# weight (one host sync per weight; a debugging aid for writes that bypass the version counter)
+_CHECK_IMAGES = os.environ.get("STATECATCHER_CHECK_IMAGES", "0") == "1"
+
+
+def invalidate_weight_images(params=None):
+    """Drop the cached bf16 images (of ``params``, or of every weight).  Needed only after a
+    write that bypasses the parameter's version counter -- ``p.data.copy_(...)`` or
+    ``p.data = ...`` (e.g. an EMA / averaged-weight swap): in-place updates through the parameter
+    itself (optimizers, ``load_state_dict``, ``with torch.no_grad(): p.copy_(...)``) are seen."""
+    if params is None:
+        _IMAGES.clear()
+        return
+    for p in params:
+        _IMAGES.pop(p, None)
+
+
+def _image_stale(w, img):
+    """Debug check: the first / last element of the image against the weight's bf16 value."""
+    flat = w.detach().reshape(-1)
+    probe = torch.stack([flat[0], flat[-1]]).to(torch.bfloat16).float()
+    return not torch.equal(probe, torch.stack([img.reshape(-1)[0], img.reshape(-1)[-1]]).float()) \
+        if img.dim() == 1 or img.shape[-1] == w.shape[-1] else False
 
 
 def weight_images(specs):
@@ -285,6 +308,9 @@ def weight_images(specs):
         key = (w._version, w.data_ptr(), rows, cols, bd, kp, bool(want_t))
         hit = _IMAGES.get(w)
         if hit is not None and hit[0] == key:
+            if _CHECK_IMAGES and bd == 0 and _image_stale(w, hit[1][0]):
+                raise RuntimeError("stale bf16 weight image: the weight was written through "
+                                   "p.data; call ops.invalidate_weight_images()")
             out[i] = hit[1]
             continue
         img = torch.empty(rows, kp, dtype=torch.bfloat16, device=w.device)

@@ -94,7 +94,7 @@ def clip_and_adam_step(optimizer, clip_params, max_norm):
         raise RuntimeError("clip_and_adam_step: optimizer not supported by the HIP Adam path "
                            "(hip_adam_eligible is False)")
     lib = _lib.load()
-    decoupled = 1 if type(optimizer) is torch.optim.AdamW else 0
+    default_decoupled = type(optimizer) is torch.optim.AdamW
     clip_ids = {id(p) for p in clip_params}
     groups, keep = [], []
     clip_entries = []
@@ -129,6 +129,9 @@ def clip_and_adam_step(optimizer, clip_params, max_norm):
         beta1, beta2 = g["betas"]
         wd = g.get("weight_decay", 0.0)
         lr = g["lr"]
+        # torch.optim.Adam(..., decoupled_weight_decay=True) is AdamW's update (torch >= 2.6
+        # stores the flag per group; AdamW sets it too): p *= 1 - lr wd instead of g += wd p
+        decoupled = 1 if g.get("decoupled_weight_decay", default_decoupled) else 0
         # parameters of one group share a step count unless added mid-training: one launch per
         # (clipped?, step) class
         classes = {}

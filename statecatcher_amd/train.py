@@ -74,14 +74,20 @@ class SegmentTrainer:
                  blank_id: int = 0, accumulation_steps: int = 1, max_grad_norm: float = 50.0,
                  amp_dtype: Optional[torch.dtype] = None, bucket_cap_mb: float = 50.0,
                  save_every_n_updates: Optional[int] = None, model_dir: Optional[str] = None,
-                 joiner: Optional[nn.Module] = None, compact_rnnt: bool = False):
+                 joiner: Optional[nn.Module] = None, compact_rnnt: bool = False,
+                 ddp: Optional[bool] = None):
         if mode == "rnnt" and joiner is None:
             raise ValueError("mode='rnnt' needs the joiner module (train.py:144-146 builds it)")
         self.model = model
         self.joiner = joiner
         self.compact_rnnt = compact_rnnt
         self.world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
-        if self.world > 1:
+        # ddp=None: wrap whenever the job has more than one rank; True: wrap at any world size
+        # (an initialised process group is required), e.g. a 1-rank RCCL group
+        self.ddp = self.world > 1 if ddp is None else bool(ddp)
+        if self.ddp and not (dist.is_available() and dist.is_initialized()):
+            raise ValueError("ddp=True needs an initialised torch.distributed process group")
+        if self.ddp:
             dev = next(model.parameters()).device
             self.net = nn.parallel.DistributedDataParallel(
                 model, device_ids=[dev.index] if dev.type == "cuda" else None,
@@ -153,7 +159,7 @@ class SegmentTrainer:
         """One segment (train.py:508-581).  Returns the (un-divided) loss tensor."""
         stepping = self._steps_now()
         sync = contextlib.ExitStack()
-        if not (stepping or self.world == 1):
+        if not (stepping or not self.ddp):
             sync.enter_context(self.net.no_sync())
             if self.joiner_net is not None:
                 sync.enter_context(self.joiner_net.no_sync())

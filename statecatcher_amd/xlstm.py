@@ -201,10 +201,11 @@ class mLSTMLayer(nn.Module):
         B, T, _ = x.shape
         NH = self.cfg.num_heads
         mh = self.multihead_norm
+        kdt = getattr(torch, self.cfg.autocast_kernel_dtype)
         if x.is_cuda and mh.bias is None and mh.force_float32_reductions:
             a = self.projection(x)
             DQ, DV = self.qk_dim // NH, self.v_dim // NH
-            if ops.mlstm_core_supported(a, NH, DQ, DV):
+            if ops.mlstm_core_supported(a, NH, DQ, DV) and kdt == a.dtype:
                 # split -> soft caps -> mLSTM cell -> gated head norm as one node reading q / k /
                 # v / o in place from the projection (ops.MLSTMCoreFn); same math and roundings
                 c0, n0, m0 = (None, None, None) if state is None else state
@@ -214,15 +215,20 @@ class mLSTMLayer(nn.Module):
             q, k, v, o, ig, fg = a.split([m.weight.shape[0] for m in self._mods()], -1)
         else:
             q, k, v, o, ig, fg = self.projections(x)
-        q = q.reshape(B, T, NH, -1).transpose(1, 2)
-        k = k.reshape(B, T, NH, -1).transpose(1, 2)
-        v = v.reshape(B, T, NH, -1).transpose(1, 2)
+        # the cell runs in autocast_kernel_dtype (the reference passes float16, model.py:227):
+        # q, k, v are cast to it as the xlstm fork's kernels cast their inputs
+        cell_dt = kdt if x.is_cuda and kdt in (torch.bfloat16, torch.float16) else q.dtype
+        q = q.reshape(B, T, NH, -1).transpose(1, 2).to(cell_dt)
+        k = k.reshape(B, T, NH, -1).transpose(1, 2).to(cell_dt)
+        v = v.reshape(B, T, NH, -1).transpose(1, 2).to(cell_dt)
         ig = soft_cap(ig, self.cfg.gate_soft_cap).transpose(1, 2)
         fg = soft_cap(fg, self.cfg.gate_soft_cap).transpose(1, 2)
         c0, n0, m0 = (None, None, None) if state is None else state
         h, new_state = mlstm_chunkwise(q, k, v, ig, fg, c0, n0, m0, return_last_states=True,
                                        eps=self.cfg.eps)
         mh = self.multihead_norm
+        if h.dtype != o.dtype and o.dtype == torch.bfloat16:
+            h = h.to(o.dtype)   # fp16 cell output back to the step's bf16 activations
         if (mh.bias is None and mh.force_float32_reductions and o.dtype == torch.bfloat16
                 and ops.gated_head_norm_supported(h)):
             # sigmoid(o) * MultiHeadLayerNorm(h) in one HIP pass on the cell's [B,NH,T,DH] layout

@@ -48,4 +48,4 @@ def assert_ref_parity(got, ref32, ref64, rtol=1e-3, afrac=1e-4, frac_ok=0.95):
     assert err64 <= 2 * noise + afrac * scale, (err64, noise)
     ok = np.abs(got - ref32) <= rtol * np.abs(ref32) + afrac * scale
     assert ok.mean() >= frac_ok, (ok.mean(), float(np.abs(got - ref32).max()))
-    return err64, noise
+    return err64, noise, float(ok.mean())

@@ -1,0 +1,201 @@
+"""Config C4 on the GPU: the xLSTM encoder at the bench's size (12 blocks x 768, 4 heads -> DQ 96,
+DV 192, FFN 2048) + CTC, T = 1500 (padded to 1536 inside ASRModel, model.py:341-347), B = 2.
+
+* One bf16-autocast training step (fwd + CTC + bwd + clip + Adam through SegmentTrainer):
+  finite, and bitwise identical when repeated from the same initial weights.
+* The same step with the mLSTM cell in fp16, as the reference configures it
+  (autocast_kernel_dtype="float16", /root/reference/model.py:227): finite, deterministic, and
+  consistent with the bf16-cell step (stated bounds below).
+* A 2-block, 768-wide slice (embedding Linear -> 2 xLSTM blocks -> out RMSNorm -> lm_head ->
+  soft cap 30) against the composition of transformers' own xLSTMBlock / xLSTMRMSNorm in fp64
+  (transformers 5.15.0 modeling_xlstm.py, the package tests/golden/gen_mlstm.py pins the cell
+  with; run at test time with the SAME weights) -- bf16 and fp16 cells.  Tolerance: at most 2x
+  the error of transformers' own composition run under the same bf16 autocast (or a floor).
+
+Parity w.r.t. the reference's own xLSTM fork is unpinned.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0") if torch.cuda.is_available() else None
+
+V, F = 1024, 80
+
+
+def sc():
+    import statecatcher_amd as s
+    return s
+
+
+def rel_err(got, ref):
+    got = got.detach().double().cpu()
+    ref = ref.detach().double().cpu()
+    return float((got - ref).norm() / max(float(ref.norm()), 1e-30))
+
+
+def close(got, ref, frac):
+    r = rel_err(got, ref)
+    assert r <= frac, f"relative Frobenius error {r:.3e} > {frac}"
+    g = got.detach().double().cpu().numpy()
+    rf = ref.detach().double().cpu().numpy()
+    np.testing.assert_allclose(g, rf, rtol=0.1, atol=0.1 * max(float(np.abs(rf).max()), 1e-30))
+    return r
+
+
+def c4_model(kernel_dtype, blocks=12, seed=0):
+    from statecatcher_amd.model import build_xlstm_config
+    torch.manual_seed(seed)
+    cfg = build_xlstm_config(F, V, num_heads=4, num_blocks=blocks, embedding_dim=768,
+                             autocast_kernel_dtype=kernel_dtype)
+    return sc().ASRModel(None, cfg, vocab_size=V, feat_dim=F, proj_dim=-1).to(DEV)
+
+
+def c4_batch(B=2, T=1500, seed=1):
+    g = torch.Generator().manual_seed(seed)
+    feats = torch.randn(B, T, F, generator=g)
+    U = torch.randint(50, 151, (B,), generator=g)
+    tok = torch.randint(1, V, (B, 150), generator=g)
+    for b in range(B):
+        tok[b, U[b]:] = 0
+    return (feats.to(DEV), torch.ones(B, T, dtype=torch.bool, device=DEV), tok.to(DEV),
+            [T] * B, U.tolist())
+
+
+def one_step(kernel_dtype, init_state=None):
+    """One SegmentTrainer step (bf16 autocast, HIP clip + Adam).  Returns (loss, {name: grad},
+    {name: param after the step}, state dict of the carried mLSTM states)."""
+    from statecatcher_amd.train import SegmentTrainer
+    model = c4_model(kernel_dtype)
+    if init_state is not None:
+        model.load_state_dict(init_state)
+    opt = torch.optim.Adam(model.parameters(), lr=3e-4)
+    tr = SegmentTrainer(model, sc().CTCLoss(blank=0, zero_infinity=True), opt,
+                        amp_dtype=torch.bfloat16, max_grad_norm=50.0)
+    grads = {}
+    hooks = [p.register_post_accumulate_grad_hook(
+        lambda p, n=n: grads.__setitem__(n, p.grad.detach().clone()))
+        for n, p in model.named_parameters()]
+    feats, masks, tok, il, tl = c4_batch()
+    loss = tr.train_segment(feats, masks, tok, il, tl)
+    torch.cuda.synchronize()
+    for h in hooks:
+        h.remove()
+    params = {n: p.detach().clone() for n, p in model.named_parameters()}
+    return float(loss.detach()), grads, params, tr.encoder_state
+
+
+@pytest.mark.parametrize("kernel_dtype", ["bfloat16", "float16"])
+def test_c4_training_step_finite_and_deterministic(kernel_dtype):
+    init = {k: v.detach().clone() for k, v in c4_model(kernel_dtype).state_dict().items()}
+    runs = [one_step(kernel_dtype, init) for _ in range(2)]
+    (l0, g0, p0, st0), (l1, g1, p1, st1) = runs
+    print(f"C4 {kernel_dtype} cell: loss {l0:.4f}, {len(g0)} gradients")
+    assert np.isfinite(l0) and l0 == l1
+    assert set(g0) == {n for n, _ in c4_model(kernel_dtype).named_parameters()}
+    for n in g0:
+        assert torch.isfinite(g0[n]).all(), n
+        assert torch.equal(g0[n], g1[n]), f"gradient of {n} not bitwise reproducible"
+        assert torch.equal(p0[n], p1[n]), f"parameter {n} after Adam not bitwise reproducible"
+    assert len(st0) == 12
+    for i in st0:
+        for a, b in zip(st0[i], st1[i]):
+            assert torch.isfinite(a).all() and torch.equal(a, b)
+
+
+def test_c4_fp16_cell_consistent_with_bf16_cell():
+    """The reference's fp16 cell against the bf16 cell on identical weights and batch: the two
+    differ only in the rounding of the cell's q / k / v and intermediate tiles (fp16 keeps 3
+    more mantissa bits), i.e. by the bf16 cell's own rounding noise.  Bounds: loss to 1e-3
+    relative (measured 2.1e-4), every gradient tensor cosine >= 0.97 and norm within 5%
+    (measured worst: block 11's out_proj weight, cosine 0.984, ratio 0.984)."""
+    init = {k: v.detach().clone() for k, v in c4_model("bfloat16").state_dict().items()}
+    lb, gb, _, _ = one_step("bfloat16", init)
+    lh, gh, _, _ = one_step("float16", init)
+    print(f"C4 loss bf16 cell {lb:.5f} fp16 cell {lh:.5f}")
+    assert abs(lb - lh) <= 1e-3 * abs(lb)
+    worst = (1.0, "")
+    for n in gb:
+        a, b = gb[n].double().flatten(), gh[n].double().flatten()
+        cos = float(a @ b / max(float(a.norm() * b.norm()), 1e-300))
+        ratio = float(b.norm() / max(float(a.norm()), 1e-300))
+        worst = min(worst, (cos, n))
+        assert cos >= 0.97 and 0.95 <= ratio <= 1.05, (n, cos, ratio)
+    print(f"C4 fp16 vs bf16 cell: worst gradient cosine {worst[0]:.5f} ({worst[1]})")
+
+
+def _hf_slice(blocks, state):
+    """transformers' xLSTMBlock x blocks + xLSTMRMSNorm in fp64 with our weights; embedding and
+    lm_head as plain fp64 linears; logits soft-capped at 30 (xLSTMForCausalLM)."""
+    from transformers import xLSTMConfig
+    from transformers.models.xlstm import modeling_xlstm as M
+    cfg = xLSTMConfig(hidden_size=768, embedding_dim=768, num_heads=4, num_blocks=blocks,
+                      vocab_size=V, mode="train", chunkwise_kernel="chunkwise--native_autograd",
+                      autocast_kernel_dtype="float32", return_last_states=True)
+    hf = torch.nn.ModuleList([M.xLSTMBlock(cfg) for _ in range(blocks)]).double()
+    hf.load_state_dict({k[len("encoder.blocks."):]: v.double() for k, v in state.items()
+                        if k.startswith("encoder.blocks.")})
+    norm = M.xLSTMRMSNorm(768, eps=cfg.norm_eps).double()
+    norm.load_state_dict({"weight": state["encoder.out_norm.weight"].double()})
+    return hf, norm
+
+
+def _slice_ref(state, x, R, device, autocast):
+    """(logits, dx, d q.weight of block 0, d proj_down.weight of block 1) of the transformers
+    composition, fp64 (autocast=False) or fp32 weights under bf16 autocast on `device`."""
+    hf, norm = _hf_slice(2, state)
+    dt = torch.float64 if not autocast else torch.float32
+    hf, norm = hf.to(device, dt), norm.to(device, dt)
+    W_e = state["encoder.embedding.weight"].to(device, dt)
+    b_e = state["encoder.embedding.bias"].to(device, dt)
+    W_l = state["encoder.lm_head.weight"].to(device, dt)
+    xr = x.to(device, dt).requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16, enabled=autocast):
+        h = torch.nn.functional.linear(xr, W_e, b_e)
+        for blk in hf:
+            h, _ = blk(h)
+        ref = torch.nn.functional.linear(norm(h), W_l)
+    ref = 30.0 * torch.tanh(ref.to(dt) / 30.0)
+    (ref * R.to(device, dt)).sum().backward()
+    return [t.detach().double().cpu() for t in
+            (ref, xr.grad, hf[0].mlstm_layer.q.weight.grad, hf[1].ffn.proj_down.weight.grad)]
+
+
+@pytest.mark.parametrize("kernel_dtype", ["bfloat16", "float16"])
+def test_c4_two_block_slice_vs_hf(kernel_dtype):
+    """Ours under bf16 autocast against transformers' fp64 composition, with the tolerance set by
+    the reference algorithm's own bf16 noise: the same transformers composition run under bf16
+    autocast on the GPU.  Each of logits, d input, d q.weight (block 0) and d proj_down.weight
+    (block 1) must be at most 2x as far from fp64 as transformers' own bf16 run (or within the
+    floor: 2e-2 logits, 5e-2 gradients)."""
+    B, T = 1, 256
+    model = c4_model(kernel_dtype, blocks=2, seed=3)
+    with torch.no_grad():   # a trained-like spread: random norms / gate biases, lm_head scaled
+        for n, p in model.named_parameters():
+            if "norm" in n:
+                p.normal_(1.0, 0.1)
+            elif n.endswith("gate_preact.bias"):
+                p.normal_(0.0, 1.0)
+        model.encoder.lm_head.weight.mul_(4.0)
+    state = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+    g = torch.Generator().manual_seed(9)
+    x = torch.randn(B, T, F, generator=g)
+    R = torch.randn(B, T, V, generator=g)
+    xd = x.to(DEV).requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        logits, st = model(xd, None)
+    (logits.float() * R.to(DEV)).sum().backward()
+    ours = [logits.detach().double().cpu(), xd.grad.double().cpu(),
+            model.encoder.blocks[0].mlstm_layer.q.weight.grad.double().cpu(),
+            model.encoder.blocks[1].ffn.proj_down.weight.grad.double().cpu()]
+    exact = _slice_ref(state, x, R, DEV, autocast=False)
+    hf16 = _slice_ref(state, x, R, DEV, autocast=True)
+    names = ["logits", "dx", "d q.weight (block 0)", "d ffn.proj_down.weight (block 1)"]
+    floors = [2e-2, 5e-2, 5e-2, 5e-2]
+    lines = []
+    for name, o, e, h, fl in zip(names, ours, exact, hf16, floors):
+        r_ours, r_hf = rel_err(o, e), rel_err(h, e)
+        lines.append(f"{name} ours {r_ours:.2e} / transformers-bf16 {r_hf:.2e}")
+        assert r_ours <= max(2.0 * r_hf, fl), (name, r_ours, r_hf)
+    print(f"C4 2-block slice, {kernel_dtype} cell, rel. Frobenius error vs fp64: " + "; ".join(lines))

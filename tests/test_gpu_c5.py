@@ -1,0 +1,126 @@
+"""Config C5 on the GPU against the oracle: the full LucyRNN 6 x 512 + RNN-T training step at the
+C5 lattice (T = 1500, U = 150, V = 1024; B = 2 so the oracle finishes in seconds).
+
+The step is model.py:73-105 (blank-prefixed predictor input, RNNTPredictorJoiner(V, 64, 64, V)
+as train.py:368-375 builds it, log_softmax, warp_rnnt 'mean', gather=True) over the drop-in
+LucyRNNtriton encoder.  The checker is oracle/lucy_step.rnnt_step: the numpy encoder of the C2
+step oracle + the joint and transducer lattice in fp64 (oracle.rnnt, pinned by brute-force
+alignment sums).  warp_rnnt itself is absent: parity w.r.t. it is unpinned.
+
+* fp32 (no autocast): compute_loss keeps the reference's fp32 joiner logits (the materialised
+  sc_rnnt_* path).  Loss to 1e-4 relative; every encoder and joiner gradient to 6e-3 in norm
+  (measured 2.0e-3 ... 5.1e-3, largest at layer 0: like CTC, an fp32 log-space lattice over
+  T = 1500 carries ~1e-3 of absolute error into the alignment posteriors; the oracle's lattice
+  is fp64).  The encoder's backward alone -- the oracle fed the GPU's own d loss / d enc_out --
+  to 1e-3.
+* The fused joiner (RNNTLoss(fused_joint=True), what the bench runs): against the oracle with
+  the fused kernels' bf16 rounding of W and tanh(enc + pred): loss 1e-4, gradients 1e-2 in norm.
+* The bench's arithmetic (bf16 autocast, fused joiner) against the fp32 oracle: loss 1e-3;
+  per tensor gradient cosine >= 0.999 and norm within 1% (measured >= 0.9999, 0.25%).
+"""
+import numpy as np
+import pytest
+import torch
+
+from tests.test_gpu_parity_step import (D512, DIN, L6, V1024, model_from, oracle_key,
+                                        oracle_params, to_np)
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0") if torch.cuda.is_available() else None
+B, T, U = 2, 1500, 150
+JKEYS = {"embedding.weight": "emb", "enc_proj.weight": "We", "enc_proj.bias": "be",
+         "pred_proj.weight": "Wp", "pred_proj.bias": "bp", "joiner.weight": "Wj",
+         "joiner.bias": "bj"}
+
+
+def sc():
+    import statecatcher_amd as s
+    return s
+
+
+def setup(seed=21):
+    p = oracle_params()
+    model = model_from(p)
+    torch.manual_seed(seed)
+    joiner = sc().RNNTPredictorJoiner(V1024, 64, 64, V1024).to(DEV)
+    with torch.no_grad():   # the encoder's logits are O(1): spread the joint a little
+        joiner.enc_proj.weight.mul_(4.0)
+        joiner.joiner.weight.mul_(3.0)
+    jp = {JKEYS[k]: v.detach().cpu().numpy().astype(np.float32) for k, v in joiner.named_parameters()}
+    rng = np.random.default_rng(seed)
+    feats = rng.standard_normal((B, T, DIN)).astype(np.float32)
+    tok = rng.integers(1, V1024, (B, U))
+    return p, model, joiner, jp, feats, tok
+
+
+def gpu_step(model, joiner, feats, tok, crit, autocast):
+    enc_out_holder = []
+    with torch.autocast("cuda", dtype=torch.bfloat16, enabled=autocast):
+        loss, _, enc_out, _ = sc().compute_loss(
+            "rnnt", crit, model, torch.from_numpy(feats).to(DEV),
+            torch.ones(B, T, dtype=torch.bool, device=DEV), torch.from_numpy(tok).to(DEV),
+            [T] * B, [U] * B, 0, use_rnnt_joiner=joiner)
+    enc_out.retain_grad()
+    enc_out_holder.append(enc_out)
+    loss.backward()
+    grads = {oracle_key(k): to_np(v.grad) for k, v in model.named_parameters()}
+    jgrads = {JKEYS[k]: to_np(v.grad) for k, v in joiner.named_parameters()}
+    return float(loss.detach()), grads, jgrads, to_np(enc_out.grad)
+
+
+def rel(a, b):
+    b = np.asarray(b, np.float64)
+    return float(np.linalg.norm(np.asarray(a, np.float64) - b) / max(np.linalg.norm(b), 1e-300))
+
+
+def test_c5_step_fp32_vs_oracle():
+    from oracle import lucy_step
+    p, model, joiner, jp, feats, tok = setup()
+    loss, grads, jgrads, dlog = gpu_step(model, joiner, feats, tok, sc().RNNTLoss(blank=0), False)
+    ref_loss, ref_g, ref_jg = lucy_step.rnnt_step(p, jp, feats, tok, [T] * B, [U] * B, L6, D512)
+    print(f"C5 fp32 loss {loss:.6f} oracle {ref_loss:.6f}")
+    np.testing.assert_allclose(loss, ref_loss, rtol=1e-4)
+    errs = {k: rel(grads[k], ref_g[k]) for k in ref_g}
+    errs.update({"joiner." + k: rel(jgrads[k], ref_jg[k]) for k in ref_jg})
+    print("C5 fp32 grads rel: " + " ".join(f"{k} {v:.1e}" for k, v in errs.items()))
+    assert max(errs.values()) < 6e-3, errs
+    # the encoder's backward on its own: the oracle fed the GPU's d loss / d enc_out
+    logits, _, x, (caches, h, s) = lucy_step.forward(p, feats, L6, D512)
+    enc_g = lucy_step.encoder_backward(p, dlog.astype(np.float32), x, caches, h, s, L6, D512)
+    e2 = {k: rel(grads[k], enc_g[k]) for k in enc_g}
+    print("C5 encoder backward (GPU dlogits) rel: " + " ".join(f"{k} {v:.1e}" for k, v in e2.items()))
+    assert max(e2.values()) < 1e-3, e2
+
+
+def test_c5_step_fused_joiner_vs_oracle_bf16_joint():
+    from oracle import lucy_step
+    p, model, joiner, jp, feats, tok = setup()
+    loss, grads, jgrads, _ = gpu_step(model, joiner, feats, tok,
+                                      sc().RNNTLoss(blank=0, fused_joint=True), False)
+    ref_loss, ref_g, ref_jg = lucy_step.rnnt_step(p, jp, feats, tok, [T] * B, [U] * B, L6, D512,
+                                                  round_bf16=True)
+    print(f"C5 fused loss {loss:.6f} oracle(bf16 joint) {ref_loss:.6f}")
+    np.testing.assert_allclose(loss, ref_loss, rtol=1e-4)
+    errs = {k: rel(grads[k], ref_g[k]) for k in ref_g}
+    errs.update({"joiner." + k: rel(jgrads[k], ref_jg[k]) for k in ref_jg})
+    print("C5 fused grads rel: " + " ".join(f"{k} {v:.1e}" for k, v in errs.items()))
+    assert max(errs.values()) < 1e-2, errs
+
+
+def test_c5_step_bf16_autocast_vs_fp32_oracle():
+    """The bench's arithmetic (bf16 autocast GEMMs and gates, fp32 state, fused bf16 joiner)."""
+    from oracle import lucy_step
+    p, model, joiner, jp, feats, tok = setup()
+    loss, grads, jgrads, _ = gpu_step(model, joiner, feats, tok, sc().RNNTLoss(blank=0), True)
+    ref_loss, ref_g, ref_jg = lucy_step.rnnt_step(p, jp, feats, tok, [T] * B, [U] * B, L6, D512)
+    print(f"C5 bf16 loss {loss:.6f} oracle {ref_loss:.6f}")
+    np.testing.assert_allclose(loss, ref_loss, rtol=1e-3)   # measured 3e-5
+    allg = {**grads, **{"joiner." + k: v for k, v in jgrads.items()}}
+    allr = {**ref_g, **{"joiner." + k: v for k, v in ref_jg.items()}}
+    for k in allr:
+        g, r = allg[k].ravel(), np.asarray(allr[k], np.float64).ravel()
+        cos = float(g @ r / max(np.linalg.norm(g) * np.linalg.norm(r), 1e-300))
+        ratio = float(np.linalg.norm(g) / max(np.linalg.norm(r), 1e-300))
+        print(f"C5 bf16 grad {k}: cos {cos:.4f} norm ratio {ratio:.4f}")
+        # measured: cosine >= 0.9999 and ratio 0.9975 ... 0.9999 for every tensor
+        assert cos >= 0.999 and abs(ratio - 1.0) <= 0.01, (k, cos, ratio)

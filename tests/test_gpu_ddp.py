@@ -1,0 +1,100 @@
+"""RCCL readiness on the leased GPU: SegmentTrainer wrapped in DistributedDataParallel over a
+1-rank "nccl" (= RCCL) process group, with the HIP ops and the HIP clip + Adam underneath.
+
+The reference trains single-process (/root/reference/train.py:85-89, :460-581); data-parallel
+training is this build's addition.  A 1-GPU lease cannot run a multi-rank
+collective, so this runs the real RCCL communicator at world size 1: DDP's bucket hooks fire over
+LucyCellFn's fused bias gradient, gradient_as_bucket_view buckets meet optim.clip_and_adam_step,
+and every bucket is all-reduced through RCCL.  The 2-rank sharding semantics are covered on the CPU
+by tests/test_train_ddp.py (gloo).  Parameters after 2 segments (state carried) must be BITWISE
+equal to the same training without DDP.
+"""
+import os
+
+import pytest
+import torch
+import torch.distributed as dist
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0") if torch.cuda.is_available() else None
+
+
+def sc():
+    import statecatcher_amd as s
+    return s
+
+
+@pytest.fixture(scope="module")
+def rccl_group():
+    import socket
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=DEV)
+    assert dist.get_backend() == "nccl"
+    yield
+    dist.destroy_process_group()
+
+
+def _build(mode, seed=0):
+    from statecatcher_amd.model import (ASRModel, CTCLoss, RNNTLoss, RNNTPredictorJoiner,
+                                        build_lucyrnn_config)
+    torch.manual_seed(seed)
+    V = 256
+    model = ASRModel(None, build_lucyrnn_config(80, 256, 3, V), vocab_size=V, feat_dim=80,
+                     proj_dim=-1).to(DEV)
+    with torch.no_grad():
+        model.encoder.output_proj.weight.normal_(0, 0.02)
+    if mode == "rnnt":
+        joiner = RNNTPredictorJoiner(V, 64, 64, V).to(DEV)
+        return model, joiner, RNNTLoss(blank=0), list(model.parameters()) + list(joiner.parameters())
+    return model, None, CTCLoss(blank=0, zero_infinity=True), list(model.parameters())
+
+
+def _train(mode, ddp):
+    from statecatcher_amd.train import SegmentTrainer
+    model, joiner, crit, params = _build(mode)
+    opt = torch.optim.Adam(params, lr=3e-4)
+    kw = dict(mode=mode, joiner=joiner) if mode == "rnnt" else {}
+    tr = SegmentTrainer(model, crit, opt, amp_dtype=torch.bfloat16, max_grad_norm=50.0,
+                        bucket_cap_mb=1.0, ddp=ddp, **kw)
+    if ddp:
+        assert isinstance(tr.net, torch.nn.parallel.DistributedDataParallel)
+    g = torch.Generator().manual_seed(5)
+    B, T = 4, 300
+    tr.begin_batch()
+    losses = []
+    for _ in range(2):   # two segments, encoder state carried (detached) between them
+        feats = torch.randn(B, T, 80, generator=g).to(DEV)
+        tok = torch.randint(1, 256, (B, 20), generator=g).to(DEV)
+        loss = tr.train_segment(feats, torch.ones(B, T, dtype=torch.bool, device=DEV), tok,
+                                [T] * B, [20, 17, 12, 20])
+        losses.append(float(loss.detach()))
+    torch.cuda.synchronize()
+    return losses, [p.detach().clone() for p in params]
+
+
+@pytest.mark.parametrize("mode", ["ctc", "rnnt"])
+def test_ddp_over_rccl_equals_single_process(rccl_group, mode):
+    l_ref, p_ref = _train(mode, ddp=False)
+    l_ddp, p_ddp = _train(mode, ddp=True)
+    print(f"{mode}: losses {l_ref} (plain) {l_ddp} (DDP over RCCL)")
+    assert l_ref == l_ddp
+    for a, b in zip(p_ref, p_ddp):
+        assert torch.equal(a, b)
+    # the parameters moved: the all-reduced gradients reached the HIP Adam
+    _, _, _, p0 = _build(mode)
+    assert any(not torch.equal(a, b) for a, b in zip(p_ref, p0))
+
+
+def test_rccl_allreduce_of_a_gradient_sized_buffer(rccl_group):
+    """The collective DDP issues, on its own: an fp32 all-reduce of the C2 gradient volume
+    (10.0 M parameters) through RCCL at world size 1 is the identity."""
+    x = torch.randn(10_013_696, device=DEV)
+    y = x.clone()
+    dist.all_reduce(y)
+    torch.cuda.synchronize()
+    assert torch.equal(x, y)

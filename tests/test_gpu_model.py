@@ -252,3 +252,32 @@ def test_colsum_vs_torch(dtype, M, N, perm):
     tol = 1e-5 * max(1.0, float(np.sqrt(max(M, 1))))
     torch.testing.assert_close(got.double().cpu(), ref, rtol=1e-5, atol=tol)
     assert torch.equal(got, colsum(x.to(DEV), perm))
+
+
+def test_weight_image_cache_and_data_writes():
+    """The bf16 weight images (ops.weight_images) follow in-place updates through the parameter
+    (version counter); a write through p.data bypasses it, and ops.invalidate_weight_images()
+    (or STATECATCHER_CHECK_IMAGES=1, which raises) is the documented remedy."""
+    from statecatcher_amd import ops
+    m = make_model().to(DEV)
+    x = torch.randn(2, 64, 24, device=DEV)
+    fresh = copy.deepcopy(m)
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+        m(x)                                             # images cached
+        for p in m.parameters():
+            p.mul_(0.5)                                  # in place through the parameter: seen
+        for p in fresh.parameters():
+            p.data.mul_(0.5)
+        ops.invalidate_weight_images(list(fresh.parameters()))
+        a, _ = m(x)
+        b, _ = fresh(x)
+        assert torch.equal(a, b)
+        for p in m.parameters():
+            p.data.mul_(2.0)                             # bypasses the version counter
+        ops.invalidate_weight_images()
+        c, _ = m(x)
+        for p in fresh.parameters():
+            p.data.mul_(2.0)
+        ops.invalidate_weight_images(list(fresh.parameters()))
+        d, _ = fresh(x)
+        assert torch.equal(c, d) and not torch.equal(a, c)

@@ -53,6 +53,8 @@ SHAPES = [(3584, 512), (1024,), (7,), (5, 13), (3, 1), (1024, 512)]
     ("adam", {}),
     ("adam", {"weight_decay": 0.01, "betas": (0.9, 0.98), "eps": 1e-6}),
     ("adamw", {"weight_decay": 0.05}),
+    # torch.optim.Adam with AdamW's update (a per-group flag since torch 2.6)
+    ("adam", {"weight_decay": 0.05, "decoupled_weight_decay": True}),
 ])
 @pytest.mark.parametrize("unaligned", [False, True])
 def test_clip_adam_matches_torch(kind, kw, unaligned):

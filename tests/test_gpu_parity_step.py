@@ -10,8 +10,9 @@
 Tolerances (stated per element class; both sides fp32 unless noted):
   module goldens: tests.conftest.assert_ref_parity -- the GPU is at most 2x as far from the
   reference's fp64 run as the reference's own fp32 run is (measured noise: h up to 1.9e-3 after
-  two segments at the reference init), and >= 95% of elements are within 1e-3 relative (floor
-  1e-4 x max) of the reference fp32 output.  The gate normaliser x / sqrt(x^2 + 1e-6) has slope
+  two segments at the reference init), and the fraction of elements within 1e-3 relative (floor
+  1e-4 x max) of the reference fp32 output is pinned per tensor (MODULE_FRAC_OK: measured 1.0
+  everywhere except d40_proj's first-segment logits, 0.963).  The gate normaliser x / sqrt(x^2 + 1e-6) has slope
   ~1e3 at 0, so rounding-order differences of a gate near zero are amplified.
   C2 step (well-conditioned init, see oracle_params -- the reference init is chaotic at C2
   depth even between the reference math's own fp32 and fp64 runs): loss 1e-4 relative;
@@ -67,6 +68,13 @@ def load_module_case(z, name):
     return m.to(DEV), L
 
 
+# fraction of elements within 1e-3 relative of the reference's fp32 output, per (case, segment,
+# tensor): measured on MI355X (profiles/r3_parity_measured.md) and pinned 0.005 below (the
+# kernels are deterministic; the margin covers a change of GEMM accumulation order)
+MODULE_FRAC_OK = {("d40_proj", 0, "logits"): 0.958}   # measured 0.9630; every other tensor 1.0000
+MODULE_FRAC_DEFAULT = 0.995
+
+
 @pytest.mark.parametrize("name", ["d64_init", "d64_proj", "d40_proj"])
 def test_lucyrnn_triton_vs_reference_module_goldens_fp32(name):
     z = load_golden("module")
@@ -78,8 +86,11 @@ def test_lucyrnn_triton_vs_reference_module_goldens_fp32(name):
             logits, (fh, fs) = m(x, state) if state is not None else m(x)
             pre = f"{name}/seg{seg}/"
             for got, key in [(logits, "logits"), (torch.stack(fh[0]), "h"), (torch.stack(fs[0]), "s")]:
-                e64, noise = assert_ref_parity(to_np(got), z[pre + key], z[pre + key + "64"])
-                print(f"{name} seg{seg} {key}: |gpu - ref64| {e64:.2e}, reference fp32 noise {noise:.2e}")
+                floor = MODULE_FRAC_OK.get((name, seg, key), MODULE_FRAC_DEFAULT)
+                e64, noise, frac = assert_ref_parity(to_np(got), z[pre + key], z[pre + key + "64"],
+                                                     frac_ok=floor)
+                print(f"{name} seg{seg} {key}: |gpu - ref64| {e64:.2e}, reference fp32 noise "
+                      f"{noise:.2e}, within 1e-3 of ref fp32: {frac:.4f} (pinned >= {floor})")
             assert fh[0][0].dtype == torch.float32 and fh[0][0].is_contiguous()
             state = (fh, fs)
 
@@ -212,6 +223,14 @@ def test_c2_training_step_fp32_vs_oracle():
         print(f"fp32 grad {k}: rel {rels[k]:.2e} norm {np.linalg.norm(rg):.3e} "
               f"max-err/max {np.abs(g - rg).max() / np.abs(rg).max():.2e}")
     assert max(rels.values()) < 6e-3, rels
+    # the encoder's backward on its own, free of CTC-lattice noise: the oracle fed the GPU's own
+    # d loss / d logits must give every encoder gradient to 1e-3 (north_star tolerance)
+    _, _, x_o, (caches_o, h_o, s_o) = lucy_step.forward(p0, feats, L6, D512)   # pre-Adam weights
+    enc_g = lucy_step.encoder_backward(p0, hip.astype(np.float32), x_o, caches_o, h_o, s_o, L6, D512)
+    e_enc = {k: np.linalg.norm(grads[k] - enc_g[k]) / np.linalg.norm(enc_g[k]) for k in enc_g}
+    print("fp32 encoder backward on the GPU's dlogits, rel: " +
+          " ".join(f"{k} {v:.1e}" for k, v in e_enc.items()))
+    assert max(e_enc.values()) < 1e-3, e_enc
     # clip + Adam step 1, restated on OUR gradients, equals the fused step exactly; and where the
     # gradient is far above Adam's eps (update ~ lr sign(g)) it equals the oracle's update
     tot = np.sqrt(sum(float((g ** 2).sum()) for g in grads.values()))
@@ -236,9 +255,43 @@ def test_c2_training_step_fp32_vs_oracle():
         assert same.all(), (k, int((~same).sum()))
 
 
+# bf16 step vs the fp32 oracle, measured on MI355X (profiles/r3_parity_measured.md): per tensor
+# (gradient cosine, norm ratio).  The kernels are deterministic, so these repeat exactly; the
+# bounds below leave 0.006 of cosine and 0.02 of norm ratio for a change of GEMM accumulation
+# order (which moves bf16 rounding points), and catch a regression larger than that.
+BF16_MEASURED = {
+    "encoder.tracks.0.0.linear.weight": (0.9999, 1.0005),
+    "encoder.tracks.0.0.linear.bias": (0.9886, 0.9710),
+    "encoder.tracks.0.1.linear.weight": (0.9808, 0.9508),
+    "encoder.tracks.0.1.linear.bias": (0.9809, 0.9503),
+    "encoder.tracks.0.2.linear.weight": (0.9754, 0.9456),
+    "encoder.tracks.0.2.linear.bias": (0.9754, 0.9461),
+    "encoder.tracks.0.3.linear.weight": (0.9732, 0.9687),
+    "encoder.tracks.0.3.linear.bias": (0.9732, 0.9688),
+    "encoder.tracks.0.4.linear.weight": (0.9771, 0.9620),
+    "encoder.tracks.0.4.linear.bias": (0.9771, 0.9619),
+    "encoder.tracks.0.5.linear.weight": (0.9761, 0.9803),
+    "encoder.tracks.0.5.linear.bias": (0.9762, 0.9808),
+    "encoder.norms.0.0.weight": (0.9968, 0.9895),
+    "encoder.norms.0.0.bias": (0.9971, 0.9863),
+    "encoder.norms.0.1.weight": (0.9856, 0.9573),
+    "encoder.norms.0.1.bias": (0.9855, 0.9604),
+    "encoder.norms.0.2.weight": (0.9730, 0.9857),
+    "encoder.norms.0.2.bias": (0.9724, 0.9825),
+    "encoder.norms.0.3.weight": (0.9761, 0.9532),
+    "encoder.norms.0.3.bias": (0.9762, 0.9569),
+    "encoder.norms.0.4.weight": (0.9768, 0.9778),
+    "encoder.norms.0.4.bias": (0.9773, 0.9764),
+    "encoder.output_proj.weight": (0.9755, 0.9746),
+    "encoder.output_proj.bias": (0.9754, 0.9747),
+}
+BF16_COS_MARGIN, BF16_RATIO_MARGIN = 0.006, 0.02
+
+
 def test_c2_training_step_bf16_vs_oracle():
     """The bench's arithmetic (bf16 autocast GEMMs, bf16 gates, fp32 state): loss within 1e-2
-    relative of the fp32 oracle; per tensor gradient cosine >= 0.97 and norm within 10%."""
+    relative of the fp32 oracle; per tensor, gradient cosine and norm ratio within the margins
+    above of their measured values (BF16_MEASURED)."""
     from oracle import lucy_step
     B, T = 2, 1500
     p = oracle_params()
@@ -259,7 +312,9 @@ def test_c2_training_step_bf16_vs_oracle():
         cos = float(g @ rg / (np.linalg.norm(g) * np.linalg.norm(rg)))
         ratio = float(np.linalg.norm(g) / np.linalg.norm(rg))
         print(f"bf16 grad {k}: cos {cos:.4f} norm ratio {ratio:.4f}")
-        assert cos >= 0.97 and 0.9 <= ratio <= 1.1, (k, cos, ratio)
+        mc, mr = BF16_MEASURED[k]
+        assert cos >= mc - BF16_COS_MARGIN and abs(ratio - mr) <= BF16_RATIO_MARGIN, \
+            (k, cos, ratio, (mc, mr))
 
 
 def test_four_segment_bf16_carry_vs_fp32_oracle():

@@ -139,10 +139,24 @@ def test_fused_joint_c5_size_vs_materialised_path():
         assert r < 2e-2, (name, r)
 
 
+def _count_fused(monkeypatch):
+    import statecatcher_amd.model as m
+    calls = []
+    orig = m.rnnt_joint_loss
+
+    def counted(*a, **k):
+        calls.append(1)
+        return orig(*a, **k)
+    monkeypatch.setattr(m, "rnnt_joint_loss", counted)
+    return calls
+
+
 @pytest.mark.parametrize("compact", [False, True])
-def test_compute_loss_rnnt_uses_fused_path(compact):
-    """compute_loss(mode='rnnt') with statecatcher RNNTLoss: the fused path, equal to the
-    materialised joiner + criterion.forward_logits (the reference's data flow)."""
+@pytest.mark.parametrize("mode", ["bf16-autocast", "forced"])
+def test_compute_loss_rnnt_uses_fused_path(compact, mode, monkeypatch):
+    """compute_loss(mode='rnnt') with statecatcher RNNTLoss takes the fused path under a 16-bit
+    autocast (or when forced), equal to the materialised joiner + criterion.forward_logits (the
+    reference's data flow) on the same bf16-rounded joiner operands."""
     B, T, Umax, V = 2, 50, 6, 64
     Cls = sc().RNNTCompactPredictorJoiner if compact else sc().RNNTPredictorJoiner
     torch.manual_seed(3)
@@ -155,9 +169,12 @@ def test_compute_loss_rnnt_uses_fused_path(compact):
     class Enc(torch.nn.Module):
         def forward(self, feats, masks, states=None):
             return feats, None
-    crit = sc().RNNTLoss(blank=0)
-    loss, _, _, _ = sc().compute_loss("rnnt", crit, Enc(), enc, None, tokens, in_lens, tgt_lens, 0,
-                                      use_rnnt_joiner=joiner, compact=compact)
+    calls = _count_fused(monkeypatch)
+    crit = sc().RNNTLoss(blank=0, fused_joint=True if mode == "forced" else None)
+    with torch.autocast("cuda", dtype=torch.bfloat16, enabled=mode != "forced"):
+        loss, _, _, _ = sc().compute_loss("rnnt", crit, Enc(), enc, None, tokens, in_lens, tgt_lens,
+                                          0, use_rnnt_joiner=joiner, compact=compact)
+    assert calls, "the fused joiner path was not taken"
     loss.backward()
     g_fused = [p.grad.clone() for p in joiner.parameters()]
     joiner.zero_grad()
@@ -168,6 +185,37 @@ def test_compute_loss_rnnt_uses_fused_path(compact):
         logits = joiner(enc, prefix)
     ref = crit.forward_logits(logits, tokens, in_lens, tgt_lens, blank_id=0, compact=compact)
     ref.backward()
+    print(f"{mode} compact={compact}: loss {loss.item():.6f} vs {ref.item():.6f}; grad rel "
+          + " ".join(f"{rel(gf, p.grad):.2e}" for gf, p in zip(g_fused, joiner.parameters())))
     np.testing.assert_allclose(loss.item(), ref.item(), rtol=2e-3)
     for gf, p in zip(g_fused, joiner.parameters()):
         assert rel(gf, p.grad) < 3e-2
+
+
+@pytest.mark.parametrize("compact", [False, True])
+def test_compute_loss_rnnt_fp32_keeps_fp32_logits(compact, monkeypatch):
+    """Plain fp32 training (no autocast): compute_loss keeps the reference's fp32 joiner logits
+    (materialised path, no bf16 rounding of W or z) -- bitwise the same as building the logits
+    and calling criterion.forward_logits directly."""
+    B, T, Umax, V = 2, 40, 5, 64
+    Cls = sc().RNNTCompactPredictorJoiner if compact else sc().RNNTPredictorJoiner
+    torch.manual_seed(4)
+    joiner = Cls(V, 16, 64, V).to(DEV)
+    enc = torch.randn(B, T, V, device=DEV)
+    tokens = torch.randint(1, V, (B, Umax), device=DEV)
+    in_lens, tgt_lens = [T, 33], [Umax, 3]
+    tokens[1, 3:] = 0
+
+    class Enc(torch.nn.Module):
+        def forward(self, feats, masks, states=None):
+            return feats, None
+    calls = _count_fused(monkeypatch)
+    crit = sc().RNNTLoss(blank=0)
+    loss, _, _, _ = sc().compute_loss("rnnt", crit, Enc(), enc, None, tokens, in_lens, tgt_lens, 0,
+                                      use_rnnt_joiner=joiner, compact=compact)
+    assert not calls, "fp32 training must not take the bf16 fused joiner"
+    prefix = torch.cat([torch.zeros(B, 1, dtype=torch.long, device=DEV), tokens], 1)
+    logits = joiner(enc, prefix, in_lens, tgt_lens) if compact else joiner(enc, prefix)
+    assert logits.dtype == torch.float32
+    ref = crit.forward_logits(logits, tokens, in_lens, tgt_lens, blank_id=0, compact=compact)
+    assert torch.equal(loss.detach(), ref.detach())

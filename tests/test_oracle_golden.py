@@ -238,3 +238,59 @@ def test_lucy_step_forward_vs_reference_module(name):
         assert_ref_parity(np.stack(h), z[pre + "h"], z[pre + "h64"])
         assert_ref_parity(np.stack(s), z[pre + "s"], z[pre + "s64"])
         state = (h, s)
+
+
+@pytest.mark.parametrize("T,U", [(1, 0), (4, 0), (1, 3), (7, 5), (23, 11)])
+def test_rnnt_vectorised_lattice_vs_loop_oracle(T, U):
+    """oracle.lucy_step.rnnt_lattice (anti-diagonal form, used by the C5 step oracle) against
+    oracle.rnnt.rnnt_single (pinned by brute-force alignment sums)."""
+    from oracle import lucy_step, rnnt
+    rng = np.random.default_rng(T * 31 + U)
+    V = 9
+    lp = torch.from_numpy(rng.standard_normal((T, U + 1, V))).log_softmax(-1).numpy()
+    y = rng.integers(1, V, U)
+    nll_ref, g = rnnt.rnnt_single(lp, y, 0)
+    nll, gb, gy = lucy_step.rnnt_lattice(lp[:, :, 0], lp[:, np.arange(U), y] if U else np.zeros((T, 0)))
+    np.testing.assert_allclose(nll, nll_ref, rtol=1e-12)
+    np.testing.assert_allclose(gb, g[:, :, 0], atol=1e-12)
+    for u in range(U):
+        gref = g[:, u, y[u]] - (g[:, u, 0] if y[u] == 0 else 0)
+        np.testing.assert_allclose(gy[:, u], gref, atol=1e-12)
+
+
+@pytest.mark.parametrize("round_bf16", [False, True])
+def test_rnnt_joint_oracle_grads_vs_autograd(round_bf16):
+    """oracle.lucy_step.rnnt_joint_loss_grad (the C5 joiner + lattice oracle) against torch
+    autograd through the same joint in fp64 with the lattice gradient injected at the log-probs
+    (the lattice itself is pinned above): ragged lengths, U = 0 included."""
+    from oracle import lucy_step, rnnt
+    rng = np.random.default_rng(5)
+    B, T, U, J, V = 3, 11, 4, 8, 12
+    enc_p = rng.standard_normal((B, T, J))
+    pred_p = rng.standard_normal((B, U + 1, J))
+    W = rng.standard_normal((V, J)).astype(np.float32)
+    bias = rng.standard_normal(V)
+    labels = rng.integers(1, V, (B, U))
+    fl, ll = [11, 6, 9], [4, 2, 0]
+    nll, de, dp, dW, db = lucy_step.rnnt_joint_loss_grad(enc_p, pred_p, W, bias, labels, fl, ll, 0,
+                                                         round_bf16=round_bf16, t_chunk=4)
+    e = torch.tensor(enc_p, requires_grad=True)
+    pp = torch.tensor(pred_p, requires_grad=True)
+    w = torch.tensor(W.astype(np.float64), requires_grad=True)
+    b = torch.tensor(bias, requires_grad=True)
+    z = torch.tanh(e.unsqueeze(2) + pp.unsqueeze(1))
+    if round_bf16:
+        z = z + (z.to(torch.bfloat16).double() - z).detach()
+        w = w + (w.to(torch.bfloat16).double() - w).detach()
+    lp = (z @ w.t() + b).log_softmax(-1)
+    glp = torch.zeros_like(lp)
+    ref = []
+    for i in range(B):
+        n, g = rnnt.rnnt_single(lp[i, :fl[i], :ll[i] + 1].detach().numpy(), labels[i, :ll[i]], 0)
+        ref.append(n)
+        glp[i, :fl[i], :ll[i] + 1] = torch.from_numpy(g)
+    lp.backward(glp)
+    np.testing.assert_allclose(nll, ref, rtol=1e-12)
+    wg = w.grad if not round_bf16 else None
+    for got, r in [(de, e.grad), (dp, pp.grad), (db, b.grad)] + ([(dW, wg)] if wg is not None else []):
+        np.testing.assert_allclose(got, r.numpy(), rtol=1e-9, atol=1e-12)
