@@ -402,17 +402,24 @@ int sc_fbank(const float* audio, int B, int64_t n_samples, int64_t audio_stride,
 /* 1 if the mLSTM kernels are compiled for this compute dtype (bf16/f16) and head dims. */
 int sc_mlstm_supported(int dtype, int DQ, int DV);
 
-/* Floats of the chunk-start state buffer (and of its gradient): BH * (T/64 + 1) * DQ * DV. */
+/* Floats of the chunk-boundary gradient buffer dstates_C: BH * (T/64 + 1) * DQ * DV. */
 int64_t sc_mlstm_state_numel(int BH, int T, int DQ, int DV);
+
+/* Elements of the forward's chunk-start state image states_C: BH * (T/64) * DQ * DV. */
+int64_t sc_mlstm_chunk_state_numel(int BH, int T, int DQ, int DV);
 
 /*
  * mLSTM cell forward over BH = batch x heads independent sequences, chunkwise (chunk 64,
  * T % 64 == 0).  q, k [BH][T][DQ], v [BH][T][DV] of dtype (bf16 or f16; MFMA with fp32
  * accumulation); igate, fgate fp32 [BH][T] pre-activations; optional initial state c0 fp32
  * [BH][DQ][DV], n0 [BH][DQ], m0 [BH] (NULL = zeros).  Outputs: h [BH][T][DV] (dtype);
- * states_C/n/m = the stabilised state at every chunk boundary (index T/64 is the final state:
- * [BH][T/64+1][DQ][DV], [BH][T/64+1][DQ], [BH][T/64+1]); m_rows, den_rows fp32 [BH][T] (the
- * row stabiliser and normaliser, consumed by the backward).  h_t = q~_t C_t / (max(|q~_t n_t|,
+ * states_C = the stabilised state C~_k at every chunk START k < T/64, in dtype ([BH][T/64][DQ]
+ * [DV]: exactly the operand the forward's q C~_k MFMA consumes; the backward's dq reads it);
+ * states_n / states_m fp32 at every chunk boundary ([BH][T/64+1][DQ], [BH][T/64+1]; index T/64
+ * is the final state); c_last fp32 [BH][DQ][DV] the final state C~ (the carried segment state);
+ * m_rows, den_rows fp32 [BH][T] (the row stabiliser and normaliser, consumed by the backward).
+ * One launch: each (sequence, 64-column block of C~) walks its chunks with the state in MFMA
+ * accumulators (the fp32 chunk states are never written to HBM).  h_t = q~_t C_t / (max(|q~_t n_t|,
  * e^{-m_t}) + eps) with q~ = q DQ^-1/2.
  * layout (optional, 7 int64): {NH, qb, qh, qt, vb, vh, vt} element strides of q / k (and dq /
  * dk) and v (dv) with sequence bh = b NH + h at step t at (bh / NH) qb + (bh % NH) qh + t qt:
@@ -422,9 +429,9 @@ int64_t sc_mlstm_state_numel(int BH, int T, int DQ, int DV);
  */
 int sc_mlstm_fwd(const void* q, const void* k, const void* v, int dtype, const float* igate,
                  const float* fgate, const float* c0, const float* n0, const float* m0, int BH,
-                 int T, int DQ, int DV, float eps, void* h, float* states_C, float* states_n,
-                 float* states_m, float* m_rows, float* den_rows, const int64_t* layout,
-                 void* stream);
+                 int T, int DQ, int DV, float eps, void* h, void* states_C, float* states_n,
+                 float* states_m, float* c_last, float* m_rows, float* den_rows,
+                 const int64_t* layout, void* stream);
 
 /*
  * Backward of sc_mlstm_fwd given dh (dtype, [BH][T][DV]) and optional gradients of the final
@@ -436,7 +443,7 @@ int sc_mlstm_fwd(const void* q, const void* k, const void* v, int dtype, const f
  */
 int sc_mlstm_bwd(const void* q, const void* k, const void* v, int dtype, const float* igate,
                  const float* fgate, const void* h, const void* dh, const float* dcT,
-                 const float* dnT, const float* states_C, const float* states_n,
+                 const float* dnT, const void* states_C, const float* states_n,
                  const float* states_m, const float* m_rows, const float* den_rows, int BH, int T,
                  int DQ, int DV, float eps, float* dstates_C, float* dstates_n, void* dq,
                  void* dk, void* dv, float* qdq, float* kdk, const int64_t* layout,

@@ -59,9 +59,10 @@ _SIGS = {
                                  _fp, _fp, _vp, _fp, _i32, _i32, _vp]),
     "sc_mlstm_supported": (_i32, [_i32, _i32, _i32]),
     "sc_mlstm_state_numel": (_i64, [_i32, _i32, _i32, _i32]),
+    "sc_mlstm_chunk_state_numel": (_i64, [_i32, _i32, _i32, _i32]),
     "sc_mlstm_fwd": (_i32, [_vp, _vp, _vp, _i32, _fp, _fp, _fp, _fp, _fp, _i32, _i32, _i32, _i32,
-                           _c.c_float, _vp, _fp, _fp, _fp, _fp, _fp, _vp, _vp]),
-    "sc_mlstm_bwd": (_i32, [_vp, _vp, _vp, _i32, _fp, _fp, _vp, _vp, _fp, _fp, _fp, _fp, _fp, _fp,
+                           _c.c_float, _vp, _vp, _fp, _fp, _fp, _fp, _fp, _vp, _vp]),
+    "sc_mlstm_bwd": (_i32, [_vp, _vp, _vp, _i32, _fp, _fp, _vp, _vp, _fp, _fp, _vp, _fp, _fp, _fp,
                            _fp, _i32, _i32, _i32, _i32, _c.c_float, _fp, _fp, _vp, _vp, _vp, _fp,
                            _fp, _vp, _vp]),
     "sc_xlstm_part_rows": (_i32, [_i64]),

@@ -12,11 +12,11 @@
 //           den_t = sum_{s<=t} W_ts (q_t.k_s)     + s e^{b_t + m_k - m_t} q_t.n~_k
 //           h_t = num_t / (max(|den_t|, e^{-m_t}) + eps)
 // Kernels (one 4-wave workgroup each; 16x16x32 bf16/f16 MFMA, fp32 accumulation, fp32 state):
-//   mlstm_fw_C   per (b,h, 64-column block of C~): walks the chunks in order, the state block
-//                lives in MFMA accumulators, stores every chunk-start state (C~_k, n~_k, m_k)
-//   mlstm_fw_H   per (b,h,chunk, 64-column block): S = Q K^T, causal decay mask,
-//                H[:, block] = M V[:, block] + Q~ C~_k[:, block], normaliser (S, the normaliser
-//                recomputed per block); keeps m_t and den_t for the backward
+//   mlstm_fw_walk per (b,h, 64-column block of C~): walks the chunks in order with the state
+//                block in MFMA accumulators; per chunk S = Q K^T, causal decay mask,
+//                H[:, block] = M V[:, block] + Q~ C~_k[:, block], normaliser (S and the
+//                normaliser recomputed per block), then the state update.  Keeps m_t, den_t and
+//                the compute-dtype image of every chunk-start state for the backward.
 //   mlstm_bw_dC  per (b,h): reverse walk, dC~_k = e^{g+m_k-m_{k+1}} dC~_{k+1} + Q~^T dnum
 //   mlstm_bw_dQ / _dK / _dV  per (b,h,chunk): the three input gradients (intra-chunk terms
 //                through dA = W o (dnum V^T + dden), inter-chunk terms through C~_k / dC~_{k+1})
@@ -63,7 +63,9 @@ struct MArgs {
   const float* c0;  // [BH][DQ][DV] or NULL
   const float* n0;  // [BH][DQ] or NULL
   const float* m0;  // [BH] or NULL
-  float* Cs;        // [BH][nc+1][DQ][DV] chunk-start states (fp32)
+  void* Cs;         // [BH][nc][DQ][DV] chunk-start states C~_0 .. C~_{nc-1} in the compute
+                    // dtype: the bf16 / f16 image the forward's Q~ C~_k MFMA consumes
+  float* c_last;    // [BH][DQ][DV] final state C~_nc (fp32: the carried segment state)
   float* ns;        // [BH][nc+1][DQ]
   float* ms;        // [BH][nc+1]
   void* h;          // [BH][T][DV]
@@ -200,28 +202,38 @@ __device__ __forceinline__ float sum16(float x) {
   return x;
 }
 
-// ------------------------------------------------------------------------- forward: states --
 // Column block of the state: C~'s columns evolve independently (C~ += K^T diag(f) V), so each
-// workgroup owns kCB = 64 columns of one (b,h) — DV/64 x BH workgroups instead of BH; n~ and m
+// workgroup owns kCB = 64 columns of one (b,h) -- DV/64 x BH workgroups instead of BH; n~ and m
 // are recomputed by every block (they need K and the gates only) and stored by block 0.
 constexpr int kCB = 64;
 
+// ------------------------------------------------------------------------- forward: walk ----
+// One workgroup per (b,h, 64-column block of C~) walks the chunks in order and does both halves
+// of the chunkwise forward for its columns: the chunk's outputs H[:, block] (S = Q K^T, causal
+// decay mask, M V + Q~ C~_k, normaliser) and the state update C~_{k+1}[:, block].  The state block
+// never leaves the MFMA accumulators: only its bf16 / f16 image (what the Q~ C~_k MFMA consumes,
+// kept for the backward's dq) and n~, m go to HBM -- no fp32 state stream and no re-read of it.
 template <int DT, int DQ, int DV>
-__global__ void __launch_bounds__(256) mlstm_fw_C(MArgs a) {
+__global__ void __launch_bounds__(256, 2) mlstm_fw_walk(MArgs a) {
   using M = MF<DT>;
   using T = typename M::T;
   using V8 = typename M::v8;
   constexpr int TJ = kCB / 16, NT = (DQ / 16) * TJ, PW = NT / 4;
   static_assert(NT % 4 == 0, "tile count must split over 4 waves");
   const int cb = blockIdx.x, bh = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int cj0 = cb * kCB;   // first state column of this block
+  const int cj0 = cb * kCB;
+  __shared__ __attribute__((aligned(16))) T Qs[kL * (DQ + kPad)];
+  __shared__ __attribute__((aligned(16))) T Ks[kL * (DQ + kPad)];
   __shared__ __attribute__((aligned(16))) T KT[DQ * (kL + kPad)];
   __shared__ __attribute__((aligned(16))) T VT[kCB * (kL + kPad)];
-  __shared__ float sb[kL], si[kL], fs[kL], scal[2];
+  __shared__ __attribute__((aligned(16))) T Ms[kL * (kL + kPad)];
+  __shared__ __attribute__((aligned(16))) T CT[kCB * (DQ + kPad)];
+  __shared__ float sb[kL], si[kL], mt[kL], rowf[kL], fs[kL], dsum[kL], qn[kL], nk[DQ], scal[2];
+  const T* Q = (const T*)a.q + qrow(a, bh, 0);
   const T* K = (const T*)a.k + qrow(a, bh, 0);
   const T* V = (const T*)a.v + vrow(a, bh, 0);
+  T* H = (T*)a.h + (int64_t)bh * a.T * DV;
   f32x4 acc[PW];
-  // tile q = w + 4p: rows i in [16 (q / TJ), +16), cols j in cj0 + [16 (q % TJ), +16)
 #pragma unroll
   for (int p = 0; p < PW; ++p) {
     const int q = w + 4 * p, i0 = 16 * (q / TJ), j0 = cj0 + 16 * (q % TJ);
@@ -233,27 +245,39 @@ __global__ void __launch_bounds__(256) mlstm_fw_C(MArgs a) {
   }
   float n = (tid < DQ && a.n0) ? a.n0[(int64_t)bh * DQ + tid] : 0.0f;
   float m = a.m0 ? a.m0[bh] : 0.0f;
-  auto store_state = [&](int k) {
-    float* C = a.Cs + ((int64_t)bh * (a.nc + 1) + k) * DQ * DV;
+  for (int k = 0; k < a.nc; ++k) {
+    const int64_t t0 = (int64_t)k * kL;
+    load_rows<T, DQ>(Qs, Q + t0 * a.qt, a.qt, tid);
+    load_rows<T, DQ>(Ks, K + t0 * a.qt, a.qt, tid);
+    load_rows_t<T, DQ>(KT, K + t0 * a.qt, a.qt, tid);
+    load_cols_t<T, DV, kCB>(VT, V + t0 * a.vt, a.vt, cj0, tid);
+    chunk_gates(a, bh, k, sb, si, tid);
+    // the state at the chunk start: its MFMA image (transposed, [j][i]) and the backward's copy
+    T* Cs = (T*)a.Cs + ((int64_t)bh * a.nc + k) * DQ * DV;
 #pragma unroll
     for (int p = 0; p < PW; ++p) {
-      const int q = w + 4 * p, i0 = 16 * (q / TJ), j0 = cj0 + 16 * (q % TJ);
+      const int q = w + 4 * p, i0 = 16 * (q / TJ), j0 = 16 * (q % TJ);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) C[(i0 + 4 * (lane >> 4) + r) * DV + j0 + (lane & 15)] = acc[p][r];
+      for (int r = 0; r < 4; ++r) {
+        const int i = i0 + 4 * (lane >> 4) + r, j = j0 + (lane & 15);
+        const T c = (T)acc[p][r];
+        CT[j * (DQ + kPad) + i] = c;
+        Cs[(int64_t)i * DV + cj0 + j] = c;
+      }
     }
-    if (cb == 0) {
-      if (tid < DQ) a.ns[((int64_t)bh * (a.nc + 1) + k) * DQ + tid] = n;
-      if (tid == 0) a.ms[(int64_t)bh * (a.nc + 1) + k] = m;
+    if (tid < DQ) {
+      nk[tid] = n;
+      if (cb == 0) a.ns[((int64_t)bh * (a.nc + 1) + k) * DQ + tid] = n;
     }
-  };
-  for (int k = 0; k < a.nc; ++k) {
-    store_state(k);
-    load_rows_t<T, DQ>(KT, K + (int64_t)k * kL * a.qt, a.qt, tid);
-    load_cols_t<T, DV, kCB>(VT, V + (int64_t)k * kL * a.vt, a.vt, cj0, tid);
-    chunk_gates(a, bh, k, sb, si, tid);
-    if (tid < 64) {
-      const float g = __shfl(sb[63], 0);   // sb written by this wave; LDS in order
-      const float as = g - sb[tid] + si[tid];
+    if (cb == 0 && tid == 0) a.ms[(int64_t)bh * (a.nc + 1) + k] = m;
+    if (tid < 64) {   // wave 0: row stabilisers, output scale, state-update key weights
+      const float bt = sb[tid];
+      const float mi = bt + wave_prefix_max(si[tid] - bt, tid);
+      const float m_t = fmaxf(bt + m, mi);
+      mt[tid] = m_t;
+      rowf[tid] = a.scale * expf(bt + m - m_t);
+      const float g = __shfl(bt, 63);
+      const float as = g - bt + si[tid];
       const float mn = fmaxf(g + m, wave_max(as));
       fs[tid] = expf(as - mn);
       if (tid == 0) {
@@ -262,6 +286,70 @@ __global__ void __launch_bounds__(256) mlstm_fw_C(MArgs a) {
       }
     }
     __syncthreads();
+    // q_t . n~_k (4 threads per row)
+    {
+      const int t = tid >> 2, part = tid & 3;
+      float qa = 0.0f;
+      for (int i = part; i < DQ; i += 4) qa += (float)Qs[t * (DQ + kPad) + i] * nk[i];
+      qa += __shfl_xor(qa, 1);
+      qa += __shfl_xor(qa, 2);
+      if (part == 0) qn[t] = qa;
+    }
+    // S = Q K^T for row block w, causal column blocks; M = S o W into LDS, row sums
+    {
+      float rs[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int ct = 0; ct < 4; ++ct) {
+        f32x4 s4 = {0.f, 0.f, 0.f, 0.f};
+        if (ct <= w) {
+#pragma unroll
+          for (int kk = 0; kk < DQ / 32; ++kk)
+            s4 = M::mma(frag<V8, T>(Qs, DQ + kPad, 16 * w, 32 * kk, lane),
+                        frag<V8, T>(Ks, DQ + kPad, 16 * ct, 32 * kk, lane), s4);
+        }
+        const int s = 16 * ct + (lane & 15);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int t = 16 * w + 4 * (lane >> 4) + r;
+          const float mv = (s <= t) ? s4[r] * a.scale * expf(sb[t] - sb[s] + si[s] - mt[t]) : 0.0f;
+          rs[r] += mv;
+          Ms[t * (kL + kPad) + s] = (T)mv;
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float tot = sum16(rs[r]);
+        if ((lane & 15) == 0) dsum[16 * w + 4 * (lane >> 4) + r] = tot;
+      }
+    }
+    __syncthreads();
+    // H = M V + (rowf Q) C~_k for row block w; normalise and store
+    {
+      const float rf = rowf[16 * w + (lane & 15)];
+      const int kin = (16 * (w + 1) + 31) / 32;
+      for (int cj = 0; cj < TJ; ++cj) {
+        f32x4 h4 = {0.f, 0.f, 0.f, 0.f};
+        for (int kk = 0; kk < kin; ++kk)
+          h4 = M::mma(frag<V8, T>(Ms, kL + kPad, 16 * w, 32 * kk, lane),
+                      frag<V8, T>(VT, kL + kPad, 16 * cj, 32 * kk, lane), h4);
+#pragma unroll
+        for (int kk = 0; kk < DQ / 32; ++kk)
+          h4 = M::mma(frag_rs<V8, T>(Qs, DQ + kPad, 16 * w, 32 * kk, lane, rf),
+                      frag<V8, T>(CT, DQ + kPad, 16 * cj, 32 * kk, lane), h4);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int t = 16 * w + 4 * (lane >> 4) + r;
+          const float dn = dsum[t] + rowf[t] * qn[t];
+          const float z = fmaxf(fabsf(dn), expf(-mt[t])) + a.eps;
+          H[(t0 + t) * DV + cj0 + 16 * cj + (lane & 15)] = (T)(h4[r] / z);
+        }
+      }
+      if (cb == 0 && tid < kL) {
+        const float dn = dsum[tid] + rowf[tid] * qn[tid];
+        a.mrow[(int64_t)bh * a.T + t0 + tid] = mt[tid];
+        a.den[(int64_t)bh * a.T + t0 + tid] = dn;
+      }
+    }
+    // state update: C~ <- decay C~ + (fs K)^T V[:, block];  n~ likewise
     const float decay = scal[0];
 #pragma unroll
     for (int p = 0; p < PW; ++p) {
@@ -281,108 +369,17 @@ __global__ void __launch_bounds__(256) mlstm_fw_C(MArgs a) {
     m = scal[1];
     __syncthreads();
   }
-  store_state(a.nc);
-}
-
-// ------------------------------------------------------------------------- forward: outputs -
-template <int DT, int DQ, int DV>
-__global__ void __launch_bounds__(256) mlstm_fw_H(MArgs a) {
-  using M = MF<DT>;
-  using T = typename M::T;
-  using V8 = typename M::v8;
-  constexpr int TJ = kCB / 16;   // output column tiles of this block
-  const int k = blockIdx.x, bh = blockIdx.y, cb = blockIdx.z, tid = threadIdx.x, lane = tid & 63,
-            w = tid >> 6;
-  const int cj0 = cb * kCB;
-  __shared__ __attribute__((aligned(16))) T Qs[kL * (DQ + kPad)];
-  __shared__ __attribute__((aligned(16))) T Ks[kL * (DQ + kPad)];
-  __shared__ __attribute__((aligned(16))) T VT[kCB * (kL + kPad)];
-  __shared__ __attribute__((aligned(16))) T Ms[kL * (kL + kPad)];
-  __shared__ __attribute__((aligned(16))) T CT[kCB * (DQ + kPad)];
-  __shared__ float sb[kL], si[kL], mt[kL], rowf[kL], dsum[kL], qn[kL], nk[DQ];
-  const int64_t t0 = (int64_t)k * kL;
-  const T* Q = (const T*)a.q + qrow(a, bh, t0);
-  load_rows<T, DQ>(Qs, Q, a.qt, tid);
-  load_rows<T, DQ>(Ks, (const T*)a.k + qrow(a, bh, t0), a.qt, tid);
-  load_cols_t<T, DV, kCB>(VT, (const T*)a.v + vrow(a, bh, t0), a.vt, cj0, tid);
-  const int64_t st = (int64_t)bh * (a.nc + 1) + k;
-  const float* Ck = a.Cs + st * DQ * DV;
-  for (int e = tid; e < DQ * kCB; e += 256) {   // C~_k[:, block] transposed to [j][i] (B of Q C)
-    const int i = e / kCB, j = e % kCB;
-    CT[j * (DQ + kPad) + i] = (T)Ck[(int64_t)i * DV + cj0 + j];
-  }
-  if (tid < DQ) nk[tid] = a.ns[st * DQ + tid];
-  const float mk = a.ms[st];
-  chunk_gates(a, bh, k, sb, si, tid);
-  if (tid < 64) {
-    const float bt = sb[tid];
-    const float mi = bt + wave_prefix_max(si[tid] - bt, tid);
-    const float m_t = fmaxf(bt + mk, mi);
-    mt[tid] = m_t;
-    rowf[tid] = a.scale * expf(bt + mk - m_t);
-  }
-  __syncthreads();
-  // q_t . n~_k (4 threads per row)
-  {
-    const int t = tid >> 2, part = tid & 3;
-    float acc = 0.0f;
-    for (int i = part; i < DQ; i += 4) acc += (float)Qs[t * (DQ + kPad) + i] * nk[i];
-    acc += __shfl_xor(acc, 1);
-    acc += __shfl_xor(acc, 2);
-    if (part == 0) qn[t] = acc;
-  }
-  // S = Q K^T for row block w, causal column blocks; M = S o W (bf16 into LDS), row sums
-  {
-    float rs[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int ct = 0; ct < 4; ++ct) {
-      f32x4 s4 = {0.f, 0.f, 0.f, 0.f};
-      if (ct <= w) {
+  // final state: fp32 (the carried segment state) + n~, m
 #pragma unroll
-        for (int kk = 0; kk < DQ / 32; ++kk)
-          s4 = M::mma(frag<V8, T>(Qs, DQ + kPad, 16 * w, 32 * kk, lane),
-                      frag<V8, T>(Ks, DQ + kPad, 16 * ct, 32 * kk, lane), s4);
-      }
-      const int s = 16 * ct + (lane & 15);
+  for (int p = 0; p < PW; ++p) {
+    const int q = w + 4 * p, i0 = 16 * (q / TJ), j0 = cj0 + 16 * (q % TJ);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int t = 16 * w + 4 * (lane >> 4) + r;
-        const float mv = (s <= t) ? s4[r] * a.scale * expf(sb[t] - sb[s] + si[s] - mt[t]) : 0.0f;
-        rs[r] += mv;
-        Ms[t * (kL + kPad) + s] = (T)mv;
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float tot = sum16(rs[r]);
-      if ((lane & 15) == 0) dsum[16 * w + 4 * (lane >> 4) + r] = tot;
-    }
+    for (int r = 0; r < 4; ++r)
+      a.c_last[((int64_t)bh * DQ + i0 + 4 * (lane >> 4) + r) * DV + j0 + (lane & 15)] = acc[p][r];
   }
-  __syncthreads();
-  // H = M V + (rowf Q) C~_k for row block w; normalise and store
-  const float rf = rowf[16 * w + (lane & 15)];
-  const int kin = (16 * (w + 1) + 31) / 32;   // non-zero k blocks of M's causal rows
-  T* H = (T*)a.h + ((int64_t)bh * a.T + t0) * DV;
-  for (int cj = 0; cj < TJ; ++cj) {
-    f32x4 h4 = {0.f, 0.f, 0.f, 0.f};
-    for (int kk = 0; kk < kin; ++kk)
-      h4 = M::mma(frag<V8, T>(Ms, kL + kPad, 16 * w, 32 * kk, lane),
-                  frag<V8, T>(VT, kL + kPad, 16 * cj, 32 * kk, lane), h4);
-#pragma unroll
-    for (int kk = 0; kk < DQ / 32; ++kk)
-      h4 = M::mma(frag_rs<V8, T>(Qs, DQ + kPad, 16 * w, 32 * kk, lane, rf),
-                  frag<V8, T>(CT, DQ + kPad, 16 * cj, 32 * kk, lane), h4);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int t = 16 * w + 4 * (lane >> 4) + r;
-      const float dn = dsum[t] + rowf[t] * qn[t];
-      const float z = fmaxf(fabsf(dn), expf(-mt[t])) + a.eps;
-      H[t * DV + cj0 + 16 * cj + (lane & 15)] = (T)(h4[r] / z);
-    }
-  }
-  if (cb == 0 && tid < kL) {
-    const float dn = dsum[tid] + rowf[tid] * qn[tid];
-    a.mrow[(int64_t)bh * a.T + t0 + tid] = mt[tid];
-    a.den[(int64_t)bh * a.T + t0 + tid] = dn;
+  if (cb == 0) {
+    if (tid < DQ) a.ns[((int64_t)bh * (a.nc + 1) + a.nc) * DQ + tid] = n;
+    if (tid == 0) a.ms[(int64_t)bh * (a.nc + 1) + a.nc] = m;
   }
 }
 
@@ -548,8 +545,11 @@ __global__ void __launch_bounds__(256) mlstm_bw_dQ(MArgs a) {
   load_rows<T, DV>(Vs, (const T*)a.v + vrow(a, bh, t0), a.vt, tid);
   load_rows_t<T, DQ>(KT, (const T*)a.k + qrow(a, bh, t0), a.qt, tid);
   const int64_t st = (int64_t)bh * (a.nc + 1) + k;
-  const float* Ck = a.Cs + st * DQ * DV;
-  for (int e = tid; e < DQ * DV; e += 256) Cm[(e / DV) * (DV + kPad) + e % DV] = (T)Ck[e];
+  const T* Ck = (const T*)a.Cs + ((int64_t)bh * a.nc + k) * DQ * DV;
+  for (int e = tid; e < DQ * DV / 8; e += 256) {   // 16-byte pieces of the [DQ][DV] image
+    const int i = (8 * e) / DV, j = (8 * e) % DV;
+    *(uint4*)(Cm + i * (DV + kPad) + j) = *(const uint4*)(Ck + 8 * e);
+  }
   if (tid < DQ) nk[tid] = a.ns[st * DQ + tid];
   chunk_dnum<T, DV>(a, bh, t0, Dn, (T*)nullptr, dden, tid);
   chunk_rows(a, bh, k, sb, si, mt, rowf, nullptr, tid);
@@ -705,8 +705,7 @@ __global__ void __launch_bounds__(256) mlstm_bw_dV(MArgs a) {
 
 template <int DT, int DQ, int DV>
 void launch_fwd(const MArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL((mlstm_fw_C<DT, DQ, DV>), dim3(DV / kCB, a.BH), dim3(256), 0, st, a);
-  hipLaunchKernelGGL((mlstm_fw_H<DT, DQ, DV>), dim3(a.nc, a.BH, DV / kCB), dim3(256), 0, st, a);
+  hipLaunchKernelGGL((mlstm_fw_walk<DT, DQ, DV>), dim3(DV / kCB, a.BH), dim3(256), 0, st, a);
 }
 template <int DT, int DQ, int DV>
 void launch_bwd(const MArgs& a, hipStream_t st) {
@@ -779,11 +778,16 @@ extern "C" int64_t sc_mlstm_state_numel(int BH, int T, int DQ, int DV) {
   return (int64_t)BH * (T / kL + 1) * DQ * DV;
 }
 
+extern "C" int64_t sc_mlstm_chunk_state_numel(int BH, int T, int DQ, int DV) {
+  if (BH <= 0 || T <= 0 || DQ <= 0 || DV <= 0) return 0;
+  return (int64_t)BH * (T / kL) * DQ * DV;
+}
+
 extern "C" int sc_mlstm_fwd(const void* q, const void* k, const void* v, int dtype,
                             const float* igate, const float* fgate, const float* c0,
                             const float* n0, const float* m0, int BH, int T, int DQ, int DV,
-                            float eps, void* h, float* states_C, float* states_n,
-                            float* states_m, float* m_rows, float* den_rows,
+                            float eps, void* h, void* states_C, float* states_n,
+                            float* states_m, float* c_last, float* m_rows, float* den_rows,
                             const int64_t* layout, void* stream) {
   clear_error();
   SC_REQUIRE(dtype == SC_BF16 || dtype == SC_F16, "sc_mlstm_fwd: dtype %d (bf16/f16 only)", dtype);
@@ -791,12 +795,13 @@ extern "C" int sc_mlstm_fwd(const void* q, const void* k, const void* v, int dty
   SC_REQUIRE(T % kL == 0, "sc_mlstm_fwd: T=%d is not a multiple of the chunk length %d", T, kL);
   SC_REQUIRE(dims_supported(DQ, DV), "sc_mlstm_fwd: head dims (%d, %d) not compiled in", DQ, DV);
   if (BH == 0 || T == 0) return 0;
-  SC_REQUIRE(q && k && v && igate && fgate && h && states_C && states_n && states_m && m_rows &&
-                 den_rows,
+  SC_REQUIRE(q && k && v && igate && fgate && h && states_C && states_n && states_m && c_last &&
+                 m_rows && den_rows,
              "sc_mlstm_fwd: null pointer");
   MArgs a{};
   a.q = q; a.k = k; a.v = v; a.ig = igate; a.fg = fgate; a.c0 = c0; a.n0 = n0; a.m0 = m0;
-  a.Cs = states_C; a.ns = states_n; a.ms = states_m; a.h = h; a.mrow = m_rows; a.den = den_rows;
+  a.Cs = states_C; a.ns = states_n; a.ms = states_m; a.c_last = c_last; a.h = h; a.mrow = m_rows;
+  a.den = den_rows;
   a.BH = BH; a.T = T; a.nc = T / kL; a.eps = eps; a.scale = 1.0f / sqrtf((float)DQ);
   if (int rc = set_layout(a, layout, DQ, DV, "sc_mlstm_fwd", {q, k, v})) return rc;
   hipStream_t st = (hipStream_t)stream;
@@ -808,7 +813,7 @@ extern "C" int sc_mlstm_fwd(const void* q, const void* k, const void* v, int dty
 extern "C" int sc_mlstm_bwd(const void* q, const void* k, const void* v, int dtype,
                             const float* igate, const float* fgate, const void* h,
                             const void* dh, const float* dcT, const float* dnT,
-                            const float* states_C, const float* states_n, const float* states_m,
+                            const void* states_C, const float* states_n, const float* states_m,
                             const float* m_rows, const float* den_rows, int BH, int T, int DQ,
                             int DV, float eps, float* dstates_C, float* dstates_n, void* dq,
                             void* dk, void* dv, float* qdq, float* kdk, const int64_t* layout,
@@ -823,7 +828,7 @@ extern "C" int sc_mlstm_bwd(const void* q, const void* k, const void* v, int dty
              "sc_mlstm_bwd: null pointer");
   MArgs a{};
   a.q = q; a.k = k; a.v = v; a.ig = igate; a.fg = fgate; a.h = (void*)h; a.dh = dh;
-  a.dcT = dcT; a.dnT = dnT; a.Cs = (float*)states_C; a.ns = (float*)states_n;
+  a.dcT = dcT; a.dnT = dnT; a.Cs = (void*)states_C; a.ns = (float*)states_n;
   a.ms = (float*)states_m; a.mrow = (float*)m_rows; a.den = (float*)den_rows;
   a.dCs = dstates_C; a.dns = dstates_n; a.dq = dq; a.dk = dk; a.dv = dv; a.qdq = qdq; a.kdk = kdk;
   a.BH = BH; a.T = T; a.nc = T / kL; a.eps = eps; a.scale = 1.0f / sqrtf((float)DQ);

@@ -232,7 +232,7 @@ def proj_fwd(x, w):
     K = 80 padded to 128: 116 vs 128 us); at K = 512 the library's 256 x 192 tiles win (157 vs
     246 us; csrc/tn_gemm.hip header)."""
     if x.shape[1] <= 128 and tn_ok(x, w):
-        return gemm_tn(x, w)
+        return gemm_tn(x, w, 256)   # 256 x 256 four-phase kernel: 114 us vs 120 (192-row tiles)
     return torch.matmul(x, w.t())
 
 
@@ -993,22 +993,22 @@ class MLSTMFn(torch.autograd.Function):
         m0c = None if m0 is None else m0.float().contiguous()
         dev = q.device
         h = torch.empty(BH, T, DV, dtype=cdt, device=dev)
-        Cs = torch.empty(BH, nc + 1, DQ, DV, dtype=torch.float32, device=dev)
+        Cs = torch.empty(BH, nc, DQ, DV, dtype=cdt, device=dev)   # chunk-start state images
+        cT = torch.empty(B, NH, DQ, DV, dtype=torch.float32, device=dev)
         ns = torch.empty(BH, nc + 1, DQ, dtype=torch.float32, device=dev)
         ms = torch.empty(BH, nc + 1, dtype=torch.float32, device=dev)
         mrow = torch.empty(BH, T, dtype=torch.float32, device=dev)
         den = torch.empty(BH, T, dtype=torch.float32, device=dev)
-        st_b = BH * (nc + 1) * (DQ * DV + DQ + 1) * 4
-        fwd_b = BH * T * ((2 * DQ + 2 * DV) * qc.element_size() + 4 * 4) + st_b   # q k v h, 4 rows
+        fwd_b = BH * T * (2 * DQ + 2 * DV) * qc.element_size()   # algorithmic: q k v in, h out
         with _timed("mlstm_fwd", qc, fwd_b):
             rc = lib.sc_mlstm_fwd(ptr(qc), ptr(kc), ptr(vc), dtype_code(qc), ptr(ig), ptr(fg), ptr(c0c),
                                   ptr(n0c), ptr(m0c), BH, T, DQ, DV, float(eps), ptr(h), ptr(Cs),
-                                  ptr(ns), ptr(ms), ptr(mrow), ptr(den), None, stream_of(qc))
+                                  ptr(ns), ptr(ms), ptr(cT), ptr(mrow), ptr(den), None,
+                                  stream_of(qc))
         check(rc, "sc_mlstm_fwd")
         ctx.save_for_backward(qc, kc, vc, ig, fg, h, Cs, ns, ms, mrow, den)
         ctx.meta = (B, NH, T, DQ, DV, float(eps), q.dtype, k.dtype, v.dtype, c0 is not None,
                     n0 is not None)
-        cT = Cs[:, nc].view(B, NH, DQ, DV).clone()
         nT = ns[:, nc].view(B, NH, DQ).clone()
         mT = ms[:, nc].view(B, NH, 1).clone()
         ctx.mark_non_differentiable(mT)
@@ -1025,16 +1025,15 @@ class MLSTMFn(torch.autograd.Function):
         dhc = dh.to(qc.dtype).contiguous().view(BH, T, DV)
         dcTc = None if dcT is None else dcT.float().contiguous()
         dnTc = None if dnT is None else dnT.float().contiguous()
-        dCs = torch.empty_like(Cs)
+        dCs = torch.empty(BH, nc + 1, DQ, DV, dtype=torch.float32, device=dev)
         dns = torch.empty_like(ns)
         dq = torch.empty_like(qc)
         dk = torch.empty_like(kc)
         dv = torch.empty_like(vc)
         qdq = torch.empty(BH, T, dtype=torch.float32, device=dev)
         kdk = torch.empty(BH, T, dtype=torch.float32, device=dev)
-        st_b = BH * (nc + 1) * (DQ * DV + DQ + 1) * 4
-        # reads q k v h dh + 4 fp32 rows + states; writes dq dk dv + 2 rows + state gradients
-        bwd_b = BH * T * ((4 * DQ + 4 * DV) * qc.element_size() + 6 * 4) + 2 * st_b
+        # algorithmic: reads q k v h dh, writes dq dk dv
+        bwd_b = BH * T * (4 * DQ + 4 * DV) * qc.element_size()
         with _timed("mlstm_bwd", qc, bwd_b):
             rc = _lib.load().sc_mlstm_bwd(
                 ptr(qc), ptr(kc), ptr(vc), dtype_code(qc), ptr(ig), ptr(fg), ptr(h), ptr(dhc),
@@ -1095,18 +1094,18 @@ class MLSTMCoreFn(torch.autograd.Function):
         base = a.data_ptr()
         lay = (ctypes.c_int64 * 7)(NH, T * N, DQ, N, T * N, DV, N)
         h = torch.empty(BH, T, DV, dtype=a.dtype, device=dev)
-        Cs = torch.empty(BH, nc + 1, DQ, DV, dtype=torch.float32, device=dev)
+        Cs = torch.empty(BH, nc, DQ, DV, dtype=a.dtype, device=dev)   # chunk-start state images
+        cT = torch.empty(B, NH, DQ, DV, dtype=torch.float32, device=dev)
         ns = torch.empty(BH, nc + 1, DQ, dtype=torch.float32, device=dev)
         ms = torch.empty(BH, nc + 1, dtype=torch.float32, device=dev)
         mrow = torch.empty(BH, T, dtype=torch.float32, device=dev)
         den = torch.empty(BH, T, dtype=torch.float32, device=dev)
-        st_b = BH * (nc + 1) * (DQ * DV + DQ + 1) * 4
-        fwd_b = BH * T * ((2 * DQ + 2 * DV) * esz + 4 * 4) + st_b
+        fwd_b = BH * T * (2 * DQ + 2 * DV) * esz   # algorithmic: q k v in, h out
         stream = stream_of(a)
         with _timed("mlstm_fwd", a, fwd_b):
             rc = lib.sc_mlstm_fwd(base + qo * esz, base + ko * esz, base + vo * esz, dtype_code(a),
                                   ptr(ig), ptr(fg), ptr(c0c), ptr(n0c), ptr(m0c), BH, T, DQ, DV,
-                                  float(eps), ptr(h), ptr(Cs), ptr(ns), ptr(ms), ptr(mrow),
+                                  float(eps), ptr(h), ptr(Cs), ptr(ns), ptr(ms), ptr(cT), ptr(mrow),
                                   ptr(den), lay, stream)
         check(rc, "sc_mlstm_fwd")
         wf = w_mh.detach().float().contiguous()
@@ -1117,7 +1116,6 @@ class MLSTMCoreFn(torch.autograd.Function):
                                    B, T, NH, DV, float(eps_mh), stream), "sc_mhln_gate_fwd")
         ctx.save_for_backward(a, ig, fg, h, Cs, ns, ms, mrow, den, wf, mean, rstd)
         ctx.meta = (NH, DQ, DV, cap, float(eps), c0 is not None, n0 is not None, w_mh.dtype)
-        cT = Cs[:, nc].view(B, NH, DQ, DV).clone()
         nT = ns[:, nc].view(B, NH, DQ).clone()
         mT = ms[:, nc].view(B, NH, 1).clone()
         ctx.mark_non_differentiable(mT)
@@ -1151,13 +1149,12 @@ class MLSTMCoreFn(torch.autograd.Function):
                                    B, T, NH, DV, stream), "sc_mhln_gate_bwd")
         dcTc = None if dcT is None else dcT.float().contiguous()
         dnTc = None if dnT is None else dnT.float().contiguous()
-        dCs = torch.empty_like(Cs)
+        dCs = torch.empty(BH, nc + 1, DQ, DV, dtype=torch.float32, device=dev)
         dns = torch.empty_like(ns)
         qdq = torch.empty(BH, T, dtype=torch.float32, device=dev)
         kdk = torch.empty(BH, T, dtype=torch.float32, device=dev)
         lay = (ctypes.c_int64 * 7)(NH, T * N, DQ, N, T * N, DV, N)
-        st_b = BH * (nc + 1) * (DQ * DV + DQ + 1) * 4
-        bwd_b = BH * T * ((4 * DQ + 4 * DV) * esz + 6 * 4) + 2 * st_b
+        bwd_b = BH * T * (4 * DQ + 4 * DV) * esz   # algorithmic: q k v h dh in, dq dk dv out
         with _timed("mlstm_bwd", a, bwd_b):
             rc = lib.sc_mlstm_bwd(
                 base + qo * esz, base + ko * esz, base + vo * esz, dtype_code(a), ptr(ig), ptr(fg),
