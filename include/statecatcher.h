@@ -402,7 +402,8 @@ int sc_fbank(const float* audio, int B, int64_t n_samples, int64_t audio_stride,
 /* 1 if the mLSTM kernels are compiled for this compute dtype (bf16/f16) and head dims. */
 int sc_mlstm_supported(int dtype, int DQ, int DV);
 
-/* Floats of the chunk-boundary gradient buffer dstates_C: BH * (T/64 + 1) * DQ * DV. */
+/* Floats of BH * (T/64 + 1) * DQ * DV (a chunk-boundary state buffer; kept for callers that
+ * size one, e.g. a per-chunk state dump). */
 int64_t sc_mlstm_state_numel(int BH, int T, int DQ, int DV);
 
 /* Elements of the forward's chunk-start state image states_C: BH * (T/64) * DQ * DV. */
@@ -413,8 +414,9 @@ int64_t sc_mlstm_chunk_state_numel(int BH, int T, int DQ, int DV);
  * T % 64 == 0).  q, k [BH][T][DQ], v [BH][T][DV] of dtype (bf16 or f16; MFMA with fp32
  * accumulation); igate, fgate fp32 [BH][T] pre-activations; optional initial state c0 fp32
  * [BH][DQ][DV], n0 [BH][DQ], m0 [BH] (NULL = zeros).  Outputs: h [BH][T][DV] (dtype);
- * states_C = the stabilised state C~_k at every chunk START k < T/64, in dtype ([BH][T/64][DQ]
- * [DV]: exactly the operand the forward's q C~_k MFMA consumes; the backward's dq reads it);
+ * states_C = the stabilised state C~_k at every chunk START k < T/64, in dtype and TRANSPOSED
+ * ([BH][T/64][DV][DQ]: exactly the operand image the forward's q C~_k MFMA consumes; the
+ * backward's dq reads it);
  * states_n / states_m fp32 at every chunk boundary ([BH][T/64+1][DQ], [BH][T/64+1]; index T/64
  * is the final state); c_last fp32 [BH][DQ][DV] the final state C~ (the carried segment state);
  * m_rows, den_rows fp32 [BH][T] (the row stabiliser and normaliser, consumed by the backward).
@@ -436,7 +438,9 @@ int sc_mlstm_fwd(const void* q, const void* k, const void* v, int dtype, const f
 /*
  * Backward of sc_mlstm_fwd given dh (dtype, [BH][T][DV]) and optional gradients of the final
  * state (dcT fp32 [BH][DQ][DV], dnT [BH][DQ]; NULL = zero).  Outputs dq, dk, dv (dtype),
- * dstates_C/n (gradient w.r.t. every chunk-start state; index 0 = the initial state), and the
+ * dstates_C / dstates_n fp32 [BH][DQ][DV] / [BH][DQ] = the gradient w.r.t. the INITIAL state
+ * (c0, n0; the per-chunk state gradients never leave the chip: one 8-wave workgroup per
+ * sequence walks the chunks in reverse with dC~ in MFMA accumulators), and the
  * per-step gate terms qdq = q_t.dq_t, kdk = k_t.dk_t (fp32 [BH][T]): d igate = kdk,
  * d fgate_t = sigmoid(-f_t) sum_{r>=t} (qdq_r - kdk_r).  The stabiliser is not differentiated.
  * layout: as sc_mlstm_fwd's; dq / dk / dv are written with the same strides as q / k / v.

@@ -37,6 +37,9 @@ constexpr int kL = 64;    // chunk length
 constexpr int kPad = 8;   // LDS row padding (elements): 16 bytes, breaks bank conflicts
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+// 16-byte register piece (a native vector: HIP's u32x4 class defeats scalar replacement of
+// register arrays, which then live in scratch)
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 template <int DT> struct MF;
 template <> struct MF<SC_BF16> {
@@ -63,8 +66,8 @@ struct MArgs {
   const float* c0;  // [BH][DQ][DV] or NULL
   const float* n0;  // [BH][DQ] or NULL
   const float* m0;  // [BH] or NULL
-  void* Cs;         // [BH][nc][DQ][DV] chunk-start states C~_0 .. C~_{nc-1} in the compute
-                    // dtype: the bf16 / f16 image the forward's Q~ C~_k MFMA consumes
+  void* Cs;         // [BH][nc][DV][DQ] chunk-start states C~_0 .. C~_{nc-1}, transposed, in
+                    // the compute dtype: the bf16 / f16 image the forward's Q~ C~_k MFMA reads
   float* c_last;    // [BH][DQ][DV] final state C~_nc (fp32: the carried segment state)
   float* ns;        // [BH][nc+1][DQ]
   float* ms;        // [BH][nc+1]
@@ -126,42 +129,6 @@ __device__ __forceinline__ V8 frag_ks(const T* tile, int ld, int r0, int k0, int
   return x;
 }
 
-// Chunk rows [t0, t0+64) of a [T][D] matrix into LDS, row-major [64][D+kPad] or transposed
-// [D][64+kPad], 16-byte global loads (D % 8 == 0).
-template <typename T, int D>
-__device__ __forceinline__ void load_rows(T* dst, const T* src, int64_t ld, int tid) {
-  for (int e = tid; e < kL * D / 8; e += 256) {
-    const int r = e / (D / 8), c = (e % (D / 8)) * 8;
-    *(uint4*)(dst + r * (D + kPad) + c) = *(const uint4*)(src + (int64_t)r * ld + c);
-  }
-}
-// (transposing loaders: consecutive lanes take consecutive ROWS of one 8-column piece, so each
-// of the eight 2-byte LDS stores per piece hits consecutive addresses across the wave; with
-// lanes along the columns every store of a wave landed in one bank, 32-way)
-template <typename T, int D>
-__device__ __forceinline__ void load_rows_t(T* dst, const T* src, int64_t ld, int tid) {
-  for (int e = tid; e < kL * D / 8; e += 256) {
-    const int r = e % kL, c = (e / kL) * 8;
-    const uint4 raw = *(const uint4*)(src + (int64_t)r * ld + c);
-    const T* x = (const T*)&raw;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) dst[(c + j) * (kL + kPad) + r] = x[j];
-  }
-}
-
-// columns [c0, c0 + W) of chunk rows [t0, t0+64) of a [T][D] matrix, transposed into LDS
-// [W][64+kPad] (16-byte global loads; W % 8 == 0)
-template <typename T, int D, int W>
-__device__ __forceinline__ void load_cols_t(T* dst, const T* src, int64_t ld, int c0, int tid) {
-  for (int e = tid; e < kL * W / 8; e += 256) {
-    const int r = e % kL, c = (e / kL) * 8;
-    const uint4 raw = *(const uint4*)(src + (int64_t)r * ld + c0 + c);
-    const T* x = (const T*)&raw;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) dst[(c + j) * (kL + kPad) + r] = x[j];
-  }
-}
-
 // Gate prefix quantities of one chunk, computed by wave 0 (lane = step s) into LDS:
 // sb[s] = b_s (inclusive cumulative logsig f), si[s] = i_s; returns g = b_{L-1} in every lane
 // of wave 0 (others get 0).
@@ -220,7 +187,8 @@ __global__ void __launch_bounds__(256, 2) mlstm_fw_walk(MArgs a) {
   using V8 = typename M::v8;
   constexpr int TJ = kCB / 16, NT = (DQ / 16) * TJ, PW = NT / 4;
   static_assert(NT % 4 == 0, "tile count must split over 4 waves");
-  const int cb = blockIdx.x, bh = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int cb = blockIdx.x, bh = blockIdx.y, w = threadIdx.x >> 6;
+  int tid = threadIdx.x, lane = tid & 63;
   const int cj0 = cb * kCB;
   __shared__ __attribute__((aligned(16))) T Qs[kL * (DQ + kPad)];
   __shared__ __attribute__((aligned(16))) T Ks[kL * (DQ + kPad)];
@@ -245,25 +213,75 @@ __global__ void __launch_bounds__(256, 2) mlstm_fw_walk(MArgs a) {
   }
   float n = (tid < DQ && a.n0) ? a.n0[(int64_t)bh * DQ + tid] : 0.0f;
   float m = a.m0 ? a.m0[bh] : 0.0f;
+  // chunk inputs are prefetched into registers one chunk ahead: the loads of chunk k + 1 are
+  // issued right after chunk k's are written to LDS and land while chunk k computes (issued
+  // and waited per loader loop they cost a full memory latency each, four times per chunk)
+  constexpr int NQP = kL * DQ / 8 / 256, NVP = kL * kCB / 8 / 256;
+  static_assert(NQP * 256 * 8 == kL * DQ && NVP * 256 * 8 == kL * kCB, "piece split");
+  u32x4 pq[NQP], pk[NQP], pv[NVP];
+  float pig = 0.0f, pfg = 0.0f;
+  auto prefetch = [&](int kc) __attribute__((always_inline)) {
+    const int64_t tb = (int64_t)kc * kL;
+#pragma unroll
+    for (int u = 0; u < NQP; ++u) {
+      const int e = tid + 256 * u, r = e / (DQ / 8), c = (e % (DQ / 8)) * 8;
+      pq[u] = *(const u32x4*)(Q + (tb + r) * a.qt + c);
+      pk[u] = *(const u32x4*)(K + (tb + r) * a.qt + c);
+    }
+#pragma unroll
+    for (int u = 0; u < NVP; ++u) {
+      const int e = tid + 256 * u, r = e % kL, c = (e / kL) * 8;
+      pv[u] = *(const u32x4*)(V + (tb + r) * a.vt + cj0 + c);
+    }
+    if (tid < 64) {
+      const int64_t o = (int64_t)bh * a.T + tb + tid;
+      pig = a.ig[o];
+      pfg = a.fg[o];
+    }
+  };
+  prefetch(0);
   for (int k = 0; k < a.nc; ++k) {
     const int64_t t0 = (int64_t)k * kL;
-    load_rows<T, DQ>(Qs, Q + t0 * a.qt, a.qt, tid);
-    load_rows<T, DQ>(Ks, K + t0 * a.qt, a.qt, tid);
-    load_rows_t<T, DQ>(KT, K + t0 * a.qt, a.qt, tid);
-    load_cols_t<T, DV, kCB>(VT, V + t0 * a.vt, a.vt, cj0, tid);
-    chunk_gates(a, bh, k, sb, si, tid);
-    // the state at the chunk start: its MFMA image (transposed, [j][i]) and the backward's copy
-    T* Cs = (T*)a.Cs + ((int64_t)bh * a.nc + k) * DQ * DV;
+    // re-derive the lane-dependent addresses every chunk instead of holding dozens of them in
+    // VGPRs across the loop (hoisted, they pushed the prefetch registers out to scratch)
+    asm volatile("" : "+v"(tid), "+v"(lane));
+#pragma unroll
+    for (int u = 0; u < NQP; ++u) {
+      const int e = tid + 256 * u, r = e / (DQ / 8), c = (e % (DQ / 8)) * 8;
+      *(u32x4*)(Qs + r * (DQ + kPad) + c) = pq[u];
+      *(u32x4*)(Ks + r * (DQ + kPad) + c) = pk[u];
+      const V8 x = __builtin_bit_cast(V8, pk[u]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) KT[(c + j) * (kL + kPad) + r] = x[j];
+    }
+#pragma unroll
+    for (int u = 0; u < NVP; ++u) {
+      const int e = tid + 256 * u, r = e % kL, c = (e / kL) * 8;
+      const V8 x = __builtin_bit_cast(V8, pv[u]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) VT[(c + j) * (kL + kPad) + r] = x[j];
+    }
+    if (tid < 64) {   // chunk_gates on the prefetched pre-activations
+      float b = logsig(pfg);
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const float u = __shfl_up(b, d);
+        if (tid >= d) b += u;
+      }
+      sb[tid] = b;
+      si[tid] = pig;
+    }
+    if (k + 1 < a.nc) prefetch(k + 1);
+    // the state at the chunk start: its MFMA image, transposed ([j][i]); a lane's four
+    // accumulator rows are consecutive i, so each tile is one 8-byte LDS store
 #pragma unroll
     for (int p = 0; p < PW; ++p) {
       const int q = w + 4 * p, i0 = 16 * (q / TJ), j0 = 16 * (q % TJ);
+      typedef T v4 __attribute__((ext_vector_type(4)));
+      v4 c;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int i = i0 + 4 * (lane >> 4) + r, j = j0 + (lane & 15);
-        const T c = (T)acc[p][r];
-        CT[j * (DQ + kPad) + i] = c;
-        Cs[(int64_t)i * DV + cj0 + j] = c;
-      }
+      for (int r = 0; r < 4; ++r) c[r] = (T)acc[p][r];
+      *(v4*)(CT + (j0 + (lane & 15)) * (DQ + kPad) + i0 + 4 * (lane >> 4)) = c;
     }
     if (tid < DQ) {
       nk[tid] = n;
@@ -286,11 +304,30 @@ __global__ void __launch_bounds__(256, 2) mlstm_fw_walk(MArgs a) {
       }
     }
     __syncthreads();
-    // q_t . n~_k (4 threads per row)
+    // the backward's copy of the chunk-start state: CT's rows as they are, [j][i] (16-byte stores)
     {
+      T* Cs = (T*)a.Cs + (((int64_t)bh * a.nc + k) * DV + cj0) * DQ;
+      constexpr int NCP = kCB * DQ / 8 / 256;
+      static_assert(NCP * 256 * 8 == kCB * DQ, "state image split");
+#pragma unroll
+      for (int u = 0; u < NCP; ++u) {
+        const int e = tid + 256 * u, j = e / (DQ / 8), c = (e % (DQ / 8)) * 8;
+        *(u32x4*)(Cs + j * DQ + c) = *(const u32x4*)(CT + j * (DQ + kPad) + c);
+      }
+    }
+    // From here to the state update every wave touches only its own 16 rows of Ms / qn / dsum
+    // (rows 16 w ..): no barrier between the S and H phases.
+    // q_t . n~_k (4 threads per row, DQ / 4 consecutive i each)
+    {
+      constexpr int QP = DQ / 4;
       const int t = tid >> 2, part = tid & 3;
       float qa = 0.0f;
-      for (int i = part; i < DQ; i += 4) qa += (float)Qs[t * (DQ + kPad) + i] * nk[i];
+#pragma unroll
+      for (int u = 0; u < QP / 8; ++u) {
+        const V8 x = *(const V8*)(Qs + t * (DQ + kPad) + part * QP + 8 * u);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) qa += (float)x[e] * nk[part * QP + 8 * u + e];
+      }
       qa += __shfl_xor(qa, 1);
       qa += __shfl_xor(qa, 2);
       if (part == 0) qn[t] = qa;
@@ -298,14 +335,13 @@ __global__ void __launch_bounds__(256, 2) mlstm_fw_walk(MArgs a) {
     // S = Q K^T for row block w, causal column blocks; M = S o W into LDS, row sums
     {
       float rs[4] = {0.f, 0.f, 0.f, 0.f};
-      for (int ct = 0; ct < 4; ++ct) {
+#pragma unroll 1
+      for (int ct = 0; ct <= w; ++ct) {
         f32x4 s4 = {0.f, 0.f, 0.f, 0.f};
-        if (ct <= w) {
 #pragma unroll
-          for (int kk = 0; kk < DQ / 32; ++kk)
-            s4 = M::mma(frag<V8, T>(Qs, DQ + kPad, 16 * w, 32 * kk, lane),
-                        frag<V8, T>(Ks, DQ + kPad, 16 * ct, 32 * kk, lane), s4);
-        }
+        for (int kk = 0; kk < DQ / 32; ++kk)
+          s4 = M::mma(frag<V8, T>(Qs, DQ + kPad, 16 * w, 32 * kk, lane),
+                      frag<V8, T>(Ks, DQ + kPad, 16 * ct, 32 * kk, lane), s4);
         const int s = 16 * ct + (lane & 15);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -315,17 +351,32 @@ __global__ void __launch_bounds__(256, 2) mlstm_fw_walk(MArgs a) {
           Ms[t * (kL + kPad) + s] = (T)mv;
         }
       }
+      // the column blocks right of the diagonal: zero (the H MFMA reads them)
+      for (int ct = w + 1; ct < 4; ++ct) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          Ms[(16 * w + 4 * (lane >> 4) + r) * (kL + kPad) + 16 * ct + (lane & 15)] = (T)0.0f;
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const float tot = sum16(rs[r]);
         if ((lane & 15) == 0) dsum[16 * w + 4 * (lane >> 4) + r] = tot;
       }
     }
-    __syncthreads();
-    // H = M V + (rowf Q) C~_k for row block w; normalise and store
+    // H = M V + (rowf Q) C~_k for row block w, normalised; staged in the wave's own Ms rows
+    // (every cj has read them first) and stored as 16-byte rows
     {
       const float rf = rowf[16 * w + (lane & 15)];
       const int kin = (16 * (w + 1) + 31) / 32;
+      float zi[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int t = 16 * w + 4 * (lane >> 4) + r;
+        const float dn = dsum[t] + rowf[t] * qn[t];
+        zi[r] = 1.0f / (fmaxf(fabsf(dn), expf(-mt[t])) + a.eps);
+      }
+      f32x4 hv[TJ];
+#pragma unroll
       for (int cj = 0; cj < TJ; ++cj) {
         f32x4 h4 = {0.f, 0.f, 0.f, 0.f};
         for (int kk = 0; kk < kin; ++kk)
@@ -335,18 +386,25 @@ __global__ void __launch_bounds__(256, 2) mlstm_fw_walk(MArgs a) {
         for (int kk = 0; kk < DQ / 32; ++kk)
           h4 = M::mma(frag_rs<V8, T>(Qs, DQ + kPad, 16 * w, 32 * kk, lane, rf),
                       frag<V8, T>(CT, DQ + kPad, 16 * cj, 32 * kk, lane), h4);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int t = 16 * w + 4 * (lane >> 4) + r;
-          const float dn = dsum[t] + rowf[t] * qn[t];
-          const float z = fmaxf(fabsf(dn), expf(-mt[t])) + a.eps;
-          H[(t0 + t) * DV + cj0 + 16 * cj + (lane & 15)] = (T)(h4[r] / z);
-        }
+        hv[cj] = h4;
+        __builtin_amdgcn_sched_barrier(0);
       }
-      if (cb == 0 && tid < kL) {
-        const float dn = dsum[tid] + rowf[tid] * qn[tid];
-        a.mrow[(int64_t)bh * a.T + t0 + tid] = mt[tid];
-        a.den[(int64_t)bh * a.T + t0 + tid] = dn;
+#pragma unroll
+      for (int cj = 0; cj < TJ; ++cj) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          Ms[(16 * w + 4 * (lane >> 4) + r) * (kL + kPad) + 16 * cj + (lane & 15)] =
+              (T)(hv[cj][r] * zi[r]);
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {   // 16 rows x 128 bytes = 128 pieces over 64 lanes
+        const int e = lane + 64 * u, t = 16 * w + (e >> 3), c = (e & 7) * 8;
+        *(u32x4*)(H + (t0 + t) * DV + cj0 + c) = *(const u32x4*)(Ms + t * (kL + kPad) + c);
+      }
+      if (cb == 0 && lane < 16) {   // the wave's own rows
+        const int t = 16 * w + lane;
+        a.mrow[(int64_t)bh * a.T + t0 + t] = mt[t];
+        a.den[(int64_t)bh * a.T + t0 + t] = dsum[t] + rowf[t] * qn[t];
       }
     }
     // state update: C~ <- decay C~ + (fs K)^T V[:, block];  n~ likewise
@@ -360,10 +418,16 @@ __global__ void __launch_bounds__(256, 2) mlstm_fw_walk(MArgs a) {
         c = M::mma(frag_ks<V8, T>(KT, kL + kPad, i0, 32 * kk, lane, fs),
                    frag<V8, T>(VT, kL + kPad, j0, 32 * kk, lane), c);
       acc[p] = c;
+      __builtin_amdgcn_sched_barrier(0);
     }
     if (tid < DQ) {
       float sacc = 0.0f;
-      for (int s = 0; s < kL; ++s) sacc += fs[s] * (float)KT[tid * (kL + kPad) + s];
+#pragma unroll
+      for (int u = 0; u < kL / 8; ++u) {
+        const V8 x = *(const V8*)(KT + tid * (kL + kPad) + 8 * u);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) sacc += fs[8 * u + e] * (float)x[e];
+      }
       n = decay * n + sacc;
     }
     m = scal[1];
@@ -383,55 +447,73 @@ __global__ void __launch_bounds__(256, 2) mlstm_fw_walk(MArgs a) {
   }
 }
 
-// dnum_t = dh_t / Z_t and dden_t for the 64 rows of a chunk (4 threads per row): dnum rows go
-// to LDS row-major ([t][j]) and/or transposed ([j][t]); dden, Z into LDS arrays.
-template <typename T, int DV>
-__device__ __forceinline__ void chunk_dnum(const MArgs& a, int bh, int64_t t0, T* dn_rm, T* dn_t,
-                                           float* dden, int tid) {
-  const int t = tid >> 2, part = tid & 3;
-  const T* dh = (const T*)a.dh + ((int64_t)bh * a.T + t0 + t) * DV;
-  const T* h = (const T*)a.h + ((int64_t)bh * a.T + t0 + t) * DV;
-  const float m_t = a.mrow[(int64_t)bh * a.T + t0 + t];
-  const float dn = a.den[(int64_t)bh * a.T + t0 + t];
-  const float z = fmaxf(fabsf(dn), expf(-m_t)) + a.eps;
-  float dot = 0.0f;
-  for (int j = part * 8; j < DV; j += 32) {
-    const uint4 rd = *(const uint4*)(dh + j), rh = *(const uint4*)(h + j);
-    const T* xd = (const T*)&rd;
-    const T* xh = (const T*)&rh;
+// ------------------------------------------------------------------------- backward: walk ----
+// One 8-wave workgroup per sequence (b,h) walks the chunks in REVERSE with the state gradient
+// dC~ [DQ][DV] (fp32) in MFMA accumulators, and per chunk computes all three input gradients:
+//   dq_t = sum_s dA_ts k_s + rowf_t dnum_t C~_k^T + rowf_t dden_t n~_k
+//   dk_s = sum_t dA_ts q_t + es_s v_s dC~_{k+1}^T + es_s dn~_{k+1}
+//   dv_s = sum_t A_ts dnum_t + es_s k_s dC~_{k+1}
+//   dC~_k = decay dC~_{k+1} + (rowf q)^T dnum,   dn~_k = decay dn~_{k+1} + sum_t rowf_t dden_t q_t
+// (dA_ts = W_ts (dnum_t . v_s + dden_t), A_ts = W_ts q_t . k_s, W_ts = s e^{b_t - b_s + i_s - m_t},
+// s <= t).  Every operand lives in LDS once, row-major; MFMA fragments that run along a column
+// come out through ds_read_b64_tr_b16 (transposed reads), so no transposed copies are stored.
+// C~_k is the forward's compute-dtype image; dC~_{k+1}'s image replaces it in LDS once the dq
+// terms are done.  Nothing of size T x DQ x DV goes to HBM: the chunk states of the gradient
+// stay on chip (the gradient w.r.t. the initial state is the only state output).
+template <typename T>
+__device__ __forceinline__ uint32_t lds_off(const T* base, int row, int ld, int col) {
+  return (uint32_t)(size_t)(const __attribute__((address_space(3))) T*)(base + row * ld + col);
+}
+__device__ __forceinline__ int2 tr_read16(uint32_t byte) {
+  typedef short s4v __attribute__((ext_vector_type(4)));
+  return __builtin_bit_cast(int2, __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                                      (s4v __attribute__((address_space(3)))*)(size_t)byte));
+}
+// fragment (8 consecutive k for index n = n0 + (l & 15)) of an image stored [k][n] (row-major
+// in k): two transposed reads of 4 k-rows x 16 n-columns per 16-lane group
+template <typename V8, typename T>
+__device__ __forceinline__ V8 frag_t(const T* img, int ld, int k0, int n0, int lane) {
+  const int r = k0 + 8 * (lane >> 4) + ((lane & 15) >> 2), c = n0 + 4 * (lane & 3);
+  const int2 lo = tr_read16(lds_off(img, r, ld, c)), hi = tr_read16(lds_off(img, r + 4, ld, c));
+  return __builtin_bit_cast(V8, u32x4{(uint32_t)lo.x, (uint32_t)lo.y, (uint32_t)hi.x, (uint32_t)hi.y});
+}
+// same, element e scaled by fk[k0 + 8 (l >> 4) + e]
+template <typename V8, typename T>
+__device__ __forceinline__ V8 frag_t_ks(const T* img, int ld, int k0, int n0, int lane,
+                                        const float* fk) {
+  V8 x = frag_t<V8, T>(img, ld, k0, n0, lane);
+  const float* f = fk + k0 + 8 * (lane >> 4);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float d = (float)xd[e];
-      dot += d * (float)xh[e];
-      const T v = (T)(d / z);
-      if (dn_rm) dn_rm[t * (DV + kPad) + j + e] = v;
-      if (dn_t) dn_t[(j + e) * (kL + kPad) + t] = v;
-    }
-  }
-  dot += __shfl_xor(dot, 1);
-  dot += __shfl_xor(dot, 2);
-  if (part == 0) {
-    // den enters through max(|den|, e^{-m}): only the |den| branch carries a gradient
-    const float live = fabsf(dn) >= expf(-m_t) ? 1.0f : 0.0f;
-    dden[t] = -dot / z * (dn >= 0.0f ? 1.0f : -1.0f) * live;
-  }
+  for (int e = 0; e < 8; ++e) x[e] = (T)((float)x[e] * f[e]);
+  return x;
 }
 
-// ------------------------------------------------------------------------- backward: dC~ ----
 template <int DT, int DQ, int DV>
-__global__ void __launch_bounds__(256) mlstm_bw_dC(MArgs a) {
+__global__ void __launch_bounds__(512, 1) mlstm_bw_walk(MArgs a) {
   using M = MF<DT>;
   using T = typename M::T;
   using V8 = typename M::v8;
-  constexpr int TJ = DV / 16, NT = (DQ / 16) * TJ, PW = NT / 4;
-  const int bh = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  __shared__ __attribute__((aligned(16))) T QT[DQ * (kL + kPad)];
-  __shared__ __attribute__((aligned(16))) T DnT[DV * (kL + kPad)];
-  __shared__ float sb[kL], si[kL], rowf[kL], dden[kL], scal[1];
-  f32x4 acc[PW];
+  constexpr int LQ = DQ + kPad, LV = DV + kPad, LL = kL + kPad;
+  constexpr int NI = DQ / 16, NJ = DV / 16;       // tile counts along DQ, DV
+  constexpr int NC = NI * NJ;                     // state tiles
+  static_assert(NC % 8 == 0, "state tiles must split over 8 waves");
+  constexpr int PC = NC / 8;
+  const int bh = blockIdx.x, w = threadIdx.x >> 6;
+  int tid = threadIdx.x, lane = tid & 63;
+  __shared__ __attribute__((aligned(16))) T Qs[kL * LQ];
+  __shared__ __attribute__((aligned(16))) T Ks[kL * LQ];
+  __shared__ __attribute__((aligned(16))) T Vs[kL * LV];
+  __shared__ __attribute__((aligned(16))) T Dn[kL * LV];
+  __shared__ __attribute__((aligned(16))) T CS[DV * LQ];   // C~_k, then dC~_{k+1}, [j][i]
+  __shared__ __attribute__((aligned(16))) T dA[kL * LL];
+  __shared__ __attribute__((aligned(16))) T Am[kL * LL];
+  __shared__ float sb[kL], si[kL], mt[kL], rowf[kL], es[kL], dden[kL], nk[DQ], dnk[DQ];
+  __shared__ float qpart[NI * kL], kpart[NI * kL], scal[1];
+  // dC~ tiles q = w + 8 p: rows i0 = 16 (q / NJ), cols j0 = 16 (q % NJ)
+  f32x4 acc[PC];
 #pragma unroll
-  for (int p = 0; p < PW; ++p) {
-    const int q = w + 4 * p, i0 = 16 * (q / TJ), j0 = 16 * (q % TJ);
+  for (int p = 0; p < PC; ++p) {
+    const int q = w + 8 * p, i0 = 16 * (q / NJ), j0 = 16 * (q % NJ);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int i = i0 + 4 * (lane >> 4) + r, j = j0 + (lane & 15);
@@ -439,268 +521,273 @@ __global__ void __launch_bounds__(256) mlstm_bw_dC(MArgs a) {
     }
   }
   float dn = (tid < DQ && a.dnT) ? a.dnT[(int64_t)bh * DQ + tid] : 0.0f;
-  auto store = [&](int k) {
-    float* C = a.dCs + ((int64_t)bh * (a.nc + 1) + k) * DQ * DV;
-#pragma unroll
-    for (int p = 0; p < PW; ++p) {
-      const int q = w + 4 * p, i0 = 16 * (q / TJ), j0 = 16 * (q % TJ);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) C[(i0 + 4 * (lane >> 4) + r) * DV + j0 + (lane & 15)] = acc[p][r];
-    }
-    if (tid < DQ) a.dns[((int64_t)bh * (a.nc + 1) + k) * DQ + tid] = dn;
-  };
+  const T* Qg = (const T*)a.q + qrow(a, bh, 0);
+  const T* Kg = (const T*)a.k + qrow(a, bh, 0);
+  const T* Vg = (const T*)a.v + vrow(a, bh, 0);
+  T* dQg = (T*)a.dq + qrow(a, bh, 0);
+  T* dKg = (T*)a.dk + qrow(a, bh, 0);
+  T* dVg = (T*)a.dv + vrow(a, bh, 0);
   for (int k = a.nc - 1; k >= 0; --k) {
-    store(k + 1);
     const int64_t t0 = (int64_t)k * kL;
-    load_rows_t<T, DQ>(QT, (const T*)a.q + qrow(a, bh, t0), a.qt, tid);
-    chunk_dnum<T, DV>(a, bh, t0, (T*)nullptr, DnT, dden, tid);
+    asm volatile("" : "+v"(tid), "+v"(lane));   // see mlstm_fw_walk
+    // ---- chunk inputs: every global load of the chunk issued before any LDS store (one
+    // memory latency per chunk, not one per operand) ----
+    {
+      constexpr int NQ8 = kL * DQ / 8, NV8 = kL * DV / 8, NC8 = DQ * DV / 8;
+      constexpr int UQ = (NQ8 + 511) / 512, UV = (NV8 + 511) / 512, UC = (NC8 + 511) / 512;
+      constexpr int UH = DV / 64;   // dh / h pieces per thread (8 threads per row)
+      u32x4 rq[UQ], rk[UQ], rv[UV], rc[UC], rd[UH], rh[UH];
+      const T* Ck = (const T*)a.Cs + ((int64_t)bh * a.nc + k) * DQ * DV;
+      const int t = tid >> 3, part = tid & 7;
+      const int64_t ro = (int64_t)bh * a.T + t0 + t;
+      const T* dh = (const T*)a.dh + ro * DV;
+      const T* h = (const T*)a.h + ro * DV;
+#pragma unroll
+      for (int u = 0; u < UQ; ++u) {
+        const int e = tid + 512 * u, r = e / (DQ / 8), c = (e % (DQ / 8)) * 8;
+        if (e < NQ8) {
+          rq[u] = *(const u32x4*)(Qg + (t0 + r) * a.qt + c);
+          rk[u] = *(const u32x4*)(Kg + (t0 + r) * a.qt + c);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < UV; ++u) {
+        const int e = tid + 512 * u, r = e / (DV / 8), c = (e % (DV / 8)) * 8;
+        if (e < NV8) rv[u] = *(const u32x4*)(Vg + (t0 + r) * a.vt + c);
+      }
+#pragma unroll
+      for (int u = 0; u < UC; ++u) {
+        const int e = tid + 512 * u;
+        if (e < NC8) rc[u] = *(const u32x4*)(Ck + 8 * e);
+      }
+#pragma unroll
+      for (int u = 0; u < UH; ++u) {
+        rd[u] = *(const u32x4*)(dh + part * 8 + 64 * u);
+        rh[u] = *(const u32x4*)(h + part * 8 + 64 * u);
+      }
+      const float m_t = a.mrow[ro], dv_ = a.den[ro];
+#pragma unroll
+      for (int u = 0; u < UQ; ++u) {
+        const int e = tid + 512 * u, r = e / (DQ / 8), c = (e % (DQ / 8)) * 8;
+        if (e < NQ8) {
+          *(u32x4*)(Qs + r * LQ + c) = rq[u];
+          *(u32x4*)(Ks + r * LQ + c) = rk[u];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < UV; ++u) {
+        const int e = tid + 512 * u, r = e / (DV / 8), c = (e % (DV / 8)) * 8;
+        if (e < NV8) *(u32x4*)(Vs + r * LV + c) = rv[u];
+      }
+#pragma unroll
+      for (int u = 0; u < UC; ++u) {
+        const int e = tid + 512 * u;
+        if (e < NC8) {
+          const int j = (8 * e) / DQ, i = (8 * e) % DQ;
+          *(u32x4*)(CS + j * LQ + i) = rc[u];
+        }
+      }
+      // dnum = dh / z and dden (8 threads per row)
+      const float z = fmaxf(fabsf(dv_), expf(-m_t)) + a.eps;
+      float dot = 0.0f;
+#pragma unroll
+      for (int u = 0; u < UH; ++u) {
+        const V8 xd = __builtin_bit_cast(V8, rd[u]);
+        const V8 xh = __builtin_bit_cast(V8, rh[u]);
+        V8 o;
+#pragma unroll
+        for (int e2 = 0; e2 < 8; ++e2) {
+          const float d = (float)xd[e2];
+          dot += d * (float)xh[e2];
+          o[e2] = (T)(d / z);
+        }
+        *(V8*)(Dn + t * LV + part * 8 + 64 * u) = o;
+      }
+      dot += __shfl_xor(dot, 1);
+      dot += __shfl_xor(dot, 2);
+      dot += __shfl_xor(dot, 4);
+      if (part == 0) {
+        const float live = fabsf(dv_) >= expf(-m_t) ? 1.0f : 0.0f;
+        dden[t] = -dot / z * (dv_ >= 0.0f ? 1.0f : -1.0f) * live;
+        mt[t] = m_t;
+      }
+    }
+    if (tid < DQ) {
+      nk[tid] = a.ns[((int64_t)bh * (a.nc + 1) + k) * DQ + tid];
+      dnk[tid] = dn;
+    }
     chunk_gates(a, bh, k, sb, si, tid);
-    if (tid < 64) {
+    if (tid < 64) {   // wave 0 wrote sb / si; mt comes from the row threads (a barrier below)
       const int64_t st = (int64_t)bh * (a.nc + 1) + k;
       const float mk = a.ms[st], mk1 = a.ms[st + 1];
+      const float g = __shfl(sb[tid], 63);
       const float m_t = a.mrow[(int64_t)bh * a.T + t0 + tid];
       rowf[tid] = a.scale * expf(sb[tid] + mk - m_t);
-      if (tid == 0) scal[0] = expf(sb[63] + mk - mk1);
+      es[tid] = expf(g - sb[tid] + si[tid] - mk1);
+      if (tid == 0) scal[0] = expf(g + mk - mk1);
     }
     __syncthreads();
+    // ---- A = W o (Q K^T) and dA = W o (Dn V^T + dden): 10 causal tiles each, 20 jobs ----
+#pragma unroll 1
+    for (int jb = w; jb < 20; jb += 8) {
+      const bool isA = jb < 10;
+      const int idx = isA ? jb : jb - 10;
+      // idx -> (tr, tc), tc <= tr: 0 (0,0) 1 (1,0) 2 (1,1) 3 (2,0) 4 (2,1) 5 (2,2) 6.. (3,*)
+      const int tr = idx < 1 ? 0 : idx < 3 ? 1 : idx < 6 ? 2 : 3;
+      const int tc = idx - tr * (tr + 1) / 2;
+      f32x4 c4 = {0.f, 0.f, 0.f, 0.f};
+      if (isA) {
+#pragma unroll
+        for (int kk = 0; kk < DQ / 32; ++kk)
+          c4 = M::mma(frag<V8, T>(Qs, LQ, 16 * tr, 32 * kk, lane),
+                      frag<V8, T>(Ks, LQ, 16 * tc, 32 * kk, lane), c4);
+      } else {
+#pragma unroll
+        for (int kk = 0; kk < DV / 32; ++kk)
+          c4 = M::mma(frag<V8, T>(Dn, LV, 16 * tr, 32 * kk, lane),
+                      frag<V8, T>(Vs, LV, 16 * tc, 32 * kk, lane), c4);
+      }
+      const int s = 16 * tc + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int t = 16 * tr + 4 * (lane >> 4) + r;
+        const float wts = (s <= t) ? a.scale * expf(sb[t] - sb[s] + si[s] - mt[t]) : 0.0f;
+        if (isA) Am[t * LL + s] = (T)(c4[r] * wts);
+        else dA[t * LL + s] = (T)((c4[r] + dden[t]) * wts);
+      }
+    }
+    // zero the strictly upper tiles (tc > tr) of A and dA once (they stay zero across chunks)
+    if (k == a.nc - 1) {
+      for (int e = tid; e < kL * kL; e += 512) {
+        const int t = e / kL, s = e % kL;
+        if ((s >> 4) > (t >> 4)) {
+          Am[t * LL + s] = (T)0.0f;
+          dA[t * LL + s] = (T)0.0f;
+        }
+      }
+    }
+    __syncthreads();
+    // ---- dq = dA K + rowf (Dn C~_k^T) + rowf dden n~_k: 4 x NI tiles ----
+#pragma unroll 1
+    for (int jb = w; jb < 4 * NI; jb += 8) {
+      const int tr = jb / NI, ci = jb % NI;
+      f32x4 d4 = {0.f, 0.f, 0.f, 0.f};
+      for (int kk = 0; kk <= (16 * tr + 15) / 32; ++kk)   // causal: s <= t
+        d4 = M::mma(frag<V8, T>(dA, LL, 16 * tr, 32 * kk, lane),
+                    frag_t<V8, T>(Ks, LQ, 32 * kk, 16 * ci, lane), d4);
+      const float rf = rowf[16 * tr + (lane & 15)];
+#pragma unroll
+      for (int kk = 0; kk < DV / 32; ++kk)
+        d4 = M::mma(frag_rs<V8, T>(Dn, LV, 16 * tr, 32 * kk, lane, rf),
+                    frag_t<V8, T>(CS, LQ, 32 * kk, 16 * ci, lane), d4);
+      const int i = 16 * ci + (lane & 15);
+      float qd[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int t = 16 * tr + 4 * (lane >> 4) + r;
+        const float v = d4[r] + rowf[t] * dden[t] * nk[i];
+        dQg[(t0 + t) * a.qt + i] = (T)v;
+        qd[r] = sum16(v * (float)Qs[t * LQ + i]);
+      }
+      if ((lane & 15) == 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) qpart[ci * kL + 16 * tr + 4 * (lane >> 4) + r] = qd[r];
+      }
+    }
+    __syncthreads();
+    // ---- dC~_{k+1} image replaces C~_k ----
+#pragma unroll
+    for (int p = 0; p < PC; ++p) {
+      const int q = w + 8 * p, i0 = 16 * (q / NJ), j0 = 16 * (q % NJ);
+      typedef T v4 __attribute__((ext_vector_type(4)));
+      v4 c;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) c[r] = (T)acc[p][r];
+      *(v4*)(CS + (j0 + (lane & 15)) * LQ + i0 + 4 * (lane >> 4)) = c;
+    }
+    if (tid < kL) {
+      float sq = 0.0f;
+#pragma unroll
+      for (int ci = 0; ci < NI; ++ci) sq += qpart[ci * kL + tid];
+      a.qdq[(int64_t)bh * a.T + t0 + tid] = sq;
+    }
+    __syncthreads();
+    // ---- dk = dA^T Q + es (V dC~^T) + es dn~: 4 x NI tiles; dv = A^T Dn + es (K dC~): 4 x NJ ----
+#pragma unroll 1
+    for (int jb = w; jb < 4 * NI + 4 * NJ; jb += 8) {
+      f32x4 d4 = {0.f, 0.f, 0.f, 0.f};
+      if (jb < 4 * NI) {
+        const int sr = jb / NI, ci = jb % NI;
+        for (int kk = (16 * sr) / 32; kk < kL / 32; ++kk)   // causal: t >= s
+          d4 = M::mma(frag_t<V8, T>(dA, LL, 32 * kk, 16 * sr, lane),
+                      frag_t<V8, T>(Qs, LQ, 32 * kk, 16 * ci, lane), d4);
+        const float ef = es[16 * sr + (lane & 15)];
+#pragma unroll
+        for (int kk = 0; kk < DV / 32; ++kk)
+          d4 = M::mma(frag_rs<V8, T>(Vs, LV, 16 * sr, 32 * kk, lane, ef),
+                      frag_t<V8, T>(CS, LQ, 32 * kk, 16 * ci, lane), d4);
+        const int i = 16 * ci + (lane & 15);
+        float kd[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int s = 16 * sr + 4 * (lane >> 4) + r;
+          const float v = d4[r] + es[s] * dnk[i];
+          dKg[(t0 + s) * a.qt + i] = (T)v;
+          kd[r] = sum16(v * (float)Ks[s * LQ + i]);
+        }
+        if ((lane & 15) == 0) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) kpart[ci * kL + 16 * sr + 4 * (lane >> 4) + r] = kd[r];
+        }
+      } else {
+        const int jv = jb - 4 * NI, sr = jv / NJ, cj = jv % NJ;
+        for (int kk = (16 * sr) / 32; kk < kL / 32; ++kk)
+          d4 = M::mma(frag_t<V8, T>(Am, LL, 32 * kk, 16 * sr, lane),
+                      frag_t<V8, T>(Dn, LV, 32 * kk, 16 * cj, lane), d4);
+        const float ef = es[16 * sr + (lane & 15)];
+#pragma unroll
+        for (int kk = 0; kk < DQ / 32; ++kk)
+          d4 = M::mma(frag_rs<V8, T>(Ks, LQ, 16 * sr, 32 * kk, lane, ef),
+                      frag<V8, T>(CS, LQ, 16 * cj, 32 * kk, lane), d4);
+        const int j = 16 * cj + (lane & 15);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dVg[(t0 + 16 * sr + 4 * (lane >> 4) + r) * a.vt + j] = (T)d4[r];
+      }
+    }
+    // ---- state gradient to the chunk start: dC~_k = decay dC~_{k+1} + (rowf Q)^T Dn ----
     const float decay = scal[0];
 #pragma unroll
-    for (int p = 0; p < PW; ++p) {
-      const int q = w + 4 * p, i0 = 16 * (q / TJ), j0 = 16 * (q % TJ);
+    for (int p = 0; p < PC; ++p) {
+      const int q = w + 8 * p, i0 = 16 * (q / NJ), j0 = 16 * (q % NJ);
       f32x4 c = acc[p] * decay;
 #pragma unroll
       for (int kk = 0; kk < kL / 32; ++kk)
-        c = M::mma(frag_ks<V8, T>(QT, kL + kPad, i0, 32 * kk, lane, rowf),
-                   frag<V8, T>(DnT, kL + kPad, j0, 32 * kk, lane), c);
+        c = M::mma(frag_t_ks<V8, T>(Qs, LQ, 32 * kk, i0, lane, rowf),
+                   frag_t<V8, T>(Dn, LV, 32 * kk, j0, lane), c);
       acc[p] = c;
     }
     if (tid < DQ) {
       float sacc = 0.0f;
-      for (int t = 0; t < kL; ++t) sacc += rowf[t] * dden[t] * (float)QT[tid * (kL + kPad) + t];
+      for (int t = 0; t < kL; ++t) sacc += rowf[t] * dden[t] * (float)Qs[t * LQ + tid];
       dn = decay * dn + sacc;
     }
     __syncthreads();
-  }
-  store(0);
-}
-
-// Shared by the dQ and dK kernels: dA_ts = W_ts (dnum_t . v_s + dden_t) for row block w
-// (t), causal column blocks, from LDS dnum [t][j] and V [s][j]; written to LDS row-major
-// (dQ) or transposed (dK).
-template <typename M, int DV, bool TRANS>
-__device__ __forceinline__ void chunk_dA(const typename M::T* Dn, const typename M::T* Vs,
-                                         typename M::T* out, const float* sb, const float* si,
-                                         const float* mt, const float* dden, float scale, int w,
-                                         int lane) {
-  using T = typename M::T;
-  using V8 = typename M::v8;
-  for (int ct = 0; ct < 4; ++ct) {
-    f32x4 p4 = {0.f, 0.f, 0.f, 0.f};
-    if (ct <= w) {
+    if (tid < kL) {
+      float sk = 0.0f;
 #pragma unroll
-      for (int kk = 0; kk < DV / 32; ++kk)
-        p4 = M::mma(frag<V8, T>(Dn, DV + kPad, 16 * w, 32 * kk, lane),
-                    frag<V8, T>(Vs, DV + kPad, 16 * ct, 32 * kk, lane), p4);
-    }
-    const int s = 16 * ct + (lane & 15);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int t = 16 * w + 4 * (lane >> 4) + r;
-      const float v = (s <= t) ? (p4[r] + dden[t]) * scale * expf(sb[t] - sb[s] + si[s] - mt[t]) : 0.0f;
-      if (TRANS) out[s * (kL + kPad) + t] = (T)v;
-      else out[t * (kL + kPad) + s] = (T)v;
+      for (int ci = 0; ci < NI; ++ci) sk += kpart[ci * kL + tid];
+      a.kdk[(int64_t)bh * a.T + t0 + tid] = sk;
     }
   }
-}
-
-// gate prefix + per-row m_t, rowf_t (= s e^{b_t + m_k - m_t}) and per-key es_s (= e^{a_s - m_{k+1}})
-__device__ __forceinline__ void chunk_rows(const MArgs& a, int bh, int k, float* sb, float* si,
-                                           float* mt, float* rowf, float* es, int tid) {
-  chunk_gates(a, bh, k, sb, si, tid);
-  if (tid < 64) {
-    const int64_t st = (int64_t)bh * (a.nc + 1) + k;
-    const float mk = a.ms[st], mk1 = a.ms[st + 1];
-    const float m_t = a.mrow[(int64_t)bh * a.T + (int64_t)k * kL + tid];
-    const float g = __shfl(sb[63], 0);
-    mt[tid] = m_t;
-    if (rowf) rowf[tid] = a.scale * expf(sb[tid] + mk - m_t);
-    if (es) es[tid] = expf(g - sb[tid] + si[tid] - mk1);
+  // gradient w.r.t. the initial state
+#pragma unroll
+  for (int p = 0; p < PC; ++p) {
+    const int q = w + 8 * p, i0 = 16 * (q / NJ), j0 = 16 * (q % NJ);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      a.dCs[((int64_t)bh * DQ + i0 + 4 * (lane >> 4) + r) * DV + j0 + (lane & 15)] = acc[p][r];
   }
-}
-
-// ------------------------------------------------------------------------- backward: dQ -----
-template <int DT, int DQ, int DV>
-__global__ void __launch_bounds__(256) mlstm_bw_dQ(MArgs a) {
-  using M = MF<DT>;
-  using T = typename M::T;
-  using V8 = typename M::v8;
-  const int k = blockIdx.x, bh = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  __shared__ __attribute__((aligned(16))) T Dn[kL * (DV + kPad)];
-  __shared__ __attribute__((aligned(16))) T Vs[kL * (DV + kPad)];
-  __shared__ __attribute__((aligned(16))) T dA[kL * (kL + kPad)];
-  __shared__ __attribute__((aligned(16))) T KT[DQ * (kL + kPad)];
-  __shared__ __attribute__((aligned(16))) T Cm[DQ * (DV + kPad)];
-  __shared__ float sb[kL], si[kL], mt[kL], rowf[kL], dden[kL], nk[DQ];
-  const int64_t t0 = (int64_t)k * kL;
-  load_rows<T, DV>(Vs, (const T*)a.v + vrow(a, bh, t0), a.vt, tid);
-  load_rows_t<T, DQ>(KT, (const T*)a.k + qrow(a, bh, t0), a.qt, tid);
-  const int64_t st = (int64_t)bh * (a.nc + 1) + k;
-  const T* Ck = (const T*)a.Cs + ((int64_t)bh * a.nc + k) * DQ * DV;
-  for (int e = tid; e < DQ * DV / 8; e += 256) {   // 16-byte pieces of the [DQ][DV] image
-    const int i = (8 * e) / DV, j = (8 * e) % DV;
-    *(uint4*)(Cm + i * (DV + kPad) + j) = *(const uint4*)(Ck + 8 * e);
-  }
-  if (tid < DQ) nk[tid] = a.ns[st * DQ + tid];
-  chunk_dnum<T, DV>(a, bh, t0, Dn, (T*)nullptr, dden, tid);
-  chunk_rows(a, bh, k, sb, si, mt, rowf, nullptr, tid);
-  __syncthreads();
-  chunk_dA<M, DV, false>(Dn, Vs, dA, sb, si, mt, dden, a.scale, w, lane);
-  __syncthreads();
-  const float rf = rowf[16 * w + (lane & 15)];
-  const int kin = (16 * (w + 1) + 31) / 32;
-  const T* Q = (const T*)a.q + qrow(a, bh, t0);
-  T* dQ = (T*)a.dq + qrow(a, bh, t0);
-  float qd[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int ci = 0; ci < DQ / 16; ++ci) {
-    f32x4 d4 = {0.f, 0.f, 0.f, 0.f};
-    for (int kk = 0; kk < kin; ++kk)
-      d4 = M::mma(frag<V8, T>(dA, kL + kPad, 16 * w, 32 * kk, lane),
-                  frag<V8, T>(KT, kL + kPad, 16 * ci, 32 * kk, lane), d4);
-#pragma unroll
-    for (int kk = 0; kk < DV / 32; ++kk)
-      d4 = M::mma(frag_rs<V8, T>(Dn, DV + kPad, 16 * w, 32 * kk, lane, rf),
-                  frag<V8, T>(Cm, DV + kPad, 16 * ci, 32 * kk, lane), d4);
-    const int i = 16 * ci + (lane & 15);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int t = 16 * w + 4 * (lane >> 4) + r;
-      const float v = d4[r] + rowf[t] * dden[t] * nk[i];
-      dQ[t * a.qt + i] = (T)v;
-      qd[r] += v * (float)Q[t * a.qt + i];
-    }
-  }
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const float tot = sum16(qd[r]);
-    if ((lane & 15) == 0) a.qdq[(int64_t)bh * a.T + t0 + 16 * w + 4 * (lane >> 4) + r] = tot;
-  }
-}
-
-// ------------------------------------------------------------------------- backward: dK -----
-template <int DT, int DQ, int DV>
-__global__ void __launch_bounds__(256) mlstm_bw_dK(MArgs a) {
-  using M = MF<DT>;
-  using T = typename M::T;
-  using V8 = typename M::v8;
-  const int k = blockIdx.x, bh = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  __shared__ __attribute__((aligned(16))) T Dn[kL * (DV + kPad)];
-  __shared__ __attribute__((aligned(16))) T Vs[kL * (DV + kPad)];
-  __shared__ __attribute__((aligned(16))) T dAT[kL * (kL + kPad)];
-  __shared__ __attribute__((aligned(16))) T QT[DQ * (kL + kPad)];
-  __shared__ __attribute__((aligned(16))) T dCm[DQ * (DV + kPad)];
-  __shared__ float sb[kL], si[kL], mt[kL], es[kL], dden[kL], dnk[DQ];
-  const int64_t t0 = (int64_t)k * kL;
-  load_rows<T, DV>(Vs, (const T*)a.v + vrow(a, bh, t0), a.vt, tid);
-  load_rows_t<T, DQ>(QT, (const T*)a.q + qrow(a, bh, t0), a.qt, tid);
-  const int64_t st1 = (int64_t)bh * (a.nc + 1) + k + 1;
-  const float* dC = a.dCs + st1 * DQ * DV;
-  for (int e = tid; e < DQ * DV; e += 256) dCm[(e / DV) * (DV + kPad) + e % DV] = (T)dC[e];
-  if (tid < DQ) dnk[tid] = a.dns[st1 * DQ + tid];
-  chunk_dnum<T, DV>(a, bh, t0, Dn, (T*)nullptr, dden, tid);
-  chunk_rows(a, bh, k, sb, si, mt, nullptr, es, tid);
-  __syncthreads();
-  chunk_dA<M, DV, true>(Dn, Vs, dAT, sb, si, mt, dden, a.scale, w, lane);
-  __syncthreads();
-  // row block w holds keys s in [16w, 16w+16): intra sums over t >= s
-  const float ef = es[16 * w + (lane & 15)];
-  const int k0 = (16 * w) / 32;
-  const T* K = (const T*)a.k + qrow(a, bh, t0);
-  T* dK = (T*)a.dk + qrow(a, bh, t0);
-  float kd[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int ci = 0; ci < DQ / 16; ++ci) {
-    f32x4 d4 = {0.f, 0.f, 0.f, 0.f};
-    for (int kk = k0; kk < kL / 32; ++kk)
-      d4 = M::mma(frag<V8, T>(dAT, kL + kPad, 16 * w, 32 * kk, lane),
-                  frag<V8, T>(QT, kL + kPad, 16 * ci, 32 * kk, lane), d4);
-#pragma unroll
-    for (int kk = 0; kk < DV / 32; ++kk)
-      d4 = M::mma(frag_rs<V8, T>(Vs, DV + kPad, 16 * w, 32 * kk, lane, ef),
-                  frag<V8, T>(dCm, DV + kPad, 16 * ci, 32 * kk, lane), d4);
-    const int i = 16 * ci + (lane & 15);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int s = 16 * w + 4 * (lane >> 4) + r;
-      const float v = d4[r] + es[s] * dnk[i];
-      dK[s * a.qt + i] = (T)v;
-      kd[r] += v * (float)K[s * a.qt + i];
-    }
-  }
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const float tot = sum16(kd[r]);
-    if ((lane & 15) == 0) a.kdk[(int64_t)bh * a.T + t0 + 16 * w + 4 * (lane >> 4) + r] = tot;
-  }
-}
-
-// ------------------------------------------------------------------------- backward: dV -----
-template <int DT, int DQ, int DV>
-__global__ void __launch_bounds__(256) mlstm_bw_dV(MArgs a) {
-  using M = MF<DT>;
-  using T = typename M::T;
-  using V8 = typename M::v8;
-  const int k = blockIdx.x, bh = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  __shared__ __attribute__((aligned(16))) T Qs[kL * (DQ + kPad)];
-  __shared__ __attribute__((aligned(16))) T Ks[kL * (DQ + kPad)];
-  __shared__ __attribute__((aligned(16))) T AT[kL * (kL + kPad)];
-  __shared__ __attribute__((aligned(16))) T DnT[DV * (kL + kPad)];
-  __shared__ __attribute__((aligned(16))) T dCT[DV * (DQ + kPad)];
-  __shared__ float sb[kL], si[kL], mt[kL], es[kL], dden[kL];
-  const int64_t t0 = (int64_t)k * kL;
-  load_rows<T, DQ>(Qs, (const T*)a.q + qrow(a, bh, t0), a.qt, tid);
-  load_rows<T, DQ>(Ks, (const T*)a.k + qrow(a, bh, t0), a.qt, tid);
-  const int64_t st1 = (int64_t)bh * (a.nc + 1) + k + 1;
-  const float* dC = a.dCs + st1 * DQ * DV;
-  for (int e = tid; e < DQ * DV; e += 256) {
-    const int i = e / DV, j = e % DV;
-    dCT[j * (DQ + kPad) + i] = (T)dC[e];
-  }
-  chunk_dnum<T, DV>(a, bh, t0, (T*)nullptr, DnT, dden, tid);
-  chunk_rows(a, bh, k, sb, si, mt, nullptr, es, tid);
-  __syncthreads();
-  // A_ts = W_ts S_ts, transposed into LDS [s][t]
-  for (int ct = 0; ct < 4; ++ct) {
-    f32x4 s4 = {0.f, 0.f, 0.f, 0.f};
-    if (ct <= w) {
-#pragma unroll
-      for (int kk = 0; kk < DQ / 32; ++kk)
-        s4 = M::mma(frag<V8, T>(Qs, DQ + kPad, 16 * w, 32 * kk, lane),
-                    frag<V8, T>(Ks, DQ + kPad, 16 * ct, 32 * kk, lane), s4);
-    }
-    const int s = 16 * ct + (lane & 15);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int t = 16 * w + 4 * (lane >> 4) + r;
-      const float v = (s <= t) ? s4[r] * a.scale * expf(sb[t] - sb[s] + si[s] - mt[t]) : 0.0f;
-      AT[s * (kL + kPad) + t] = (T)v;
-    }
-  }
-  __syncthreads();
-  const float ef = es[16 * w + (lane & 15)];
-  const int k0 = (16 * w) / 32;
-  T* dV = (T*)a.dv + vrow(a, bh, t0);
-  for (int cj = 0; cj < DV / 16; ++cj) {
-    f32x4 d4 = {0.f, 0.f, 0.f, 0.f};
-    for (int kk = k0; kk < kL / 32; ++kk)
-      d4 = M::mma(frag<V8, T>(AT, kL + kPad, 16 * w, 32 * kk, lane),
-                  frag<V8, T>(DnT, kL + kPad, 16 * cj, 32 * kk, lane), d4);
-#pragma unroll
-    for (int kk = 0; kk < DQ / 32; ++kk)
-      d4 = M::mma(frag_rs<V8, T>(Ks, DQ + kPad, 16 * w, 32 * kk, lane, ef),
-                  frag<V8, T>(dCT, DQ + kPad, 16 * cj, 32 * kk, lane), d4);
-    const int j = 16 * cj + (lane & 15);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) dV[(16 * w + 4 * (lane >> 4) + r) * a.vt + j] = (T)d4[r];
-  }
+  if (tid < DQ) a.dns[(int64_t)bh * DQ + tid] = dn;
 }
 
 template <int DT, int DQ, int DV>
@@ -709,10 +796,7 @@ void launch_fwd(const MArgs& a, hipStream_t st) {
 }
 template <int DT, int DQ, int DV>
 void launch_bwd(const MArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL((mlstm_bw_dC<DT, DQ, DV>), dim3(a.BH), dim3(256), 0, st, a);
-  hipLaunchKernelGGL((mlstm_bw_dQ<DT, DQ, DV>), dim3(a.nc, a.BH), dim3(256), 0, st, a);
-  hipLaunchKernelGGL((mlstm_bw_dK<DT, DQ, DV>), dim3(a.nc, a.BH), dim3(256), 0, st, a);
-  hipLaunchKernelGGL((mlstm_bw_dV<DT, DQ, DV>), dim3(a.nc, a.BH), dim3(256), 0, st, a);
+  hipLaunchKernelGGL((mlstm_bw_walk<DT, DQ, DV>), dim3(a.BH), dim3(512), 0, st, a);
 }
 
 // head dimensions compiled in (DQ, DV): the xLSTM-large defaults qk = v/2 at 64..192 wide heads

@@ -481,6 +481,210 @@ __global__ void __launch_bounds__(512, 1) tn256_kernel(TnArgs a) {
   store_quad(acc[3], pm0, pn0, 1, 0);
 }
 
+// ------------------------------------------------------------------------------------------
+// 256 x 256 tiles, PING-PONG schedule (tile_m = 257 selects it; measured against tn256 above).
+//
+// The two waves that share a SIMD (w and w + 4) alternate roles every segment: while one runs a
+// 16-MFMA compute segment, the other issues its next fragment reads (and its share of the
+// LDS-DMA stream) -- the SIMD's matrix pipe is fed by one wave while the other waits on LDS.
+// Waves 4-7 start one barrier late and stay offset by one segment (MI355X_MICROARCH.md "Two
+// waves per SIMD", cdna_hip_programming.md §5 8-phase template).
+//   * wave w: output rows 128 (w >> 2) + [0, 128) (its own A half), columns 64 (w & 3) + [0, 64);
+//     per K-tile four quadrants of 64 x 32 in the order (0,0) (0,1) (1,1) (1,0): load segments
+//     L1 (A rows 0-63, B cols 0-31), L2 (B cols 32-63), L3 (A rows 64-127), L4 (B cols 0-31).
+//   * LDS: two K-tile buffers (4 halves x 16 KiB each).  K-tile j + 1 is staged into buffer
+//     (j + 1) % 2 during K-tile j (wave w DMAs 8 of its 64 1-KiB pieces, 4 in L1 and 4 in L2);
+//     its last readers (K-tile j - 1) finished a barrier earlier.  Every wave retires its own
+//     pieces with vmcnt(0) at the end of its L4 -- four segments after the last one was issued
+//     and one barrier before the first read of K-tile j + 1.
+//   * epilogue: a finished tile's four quadrants are packed and stored in L1 of the next tile's
+//     first K-tile, BEFORE that segment's DMA (so the K-tile's single vmcnt(0) also covers them,
+//     six segments later); buffer stores drop rows >= M.
+struct FragA1 { i4v v[4][2]; };   // one quadrant: 4 row fragments x 2 k-steps
+struct FragB1 { i4v v[2][2]; };   // 2 column fragments x 2 k-steps
+
+__global__ void __launch_bounds__(512, 1) tnpp_kernel(TnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const int lane = threadIdx.x & 63;
+  const int w = uniform(threadIdx.x >> 6);
+  const int hf = w >> 2, wq = w & 3;
+  const int l15 = lane & 15, l4 = lane >> 4;
+
+  const int G = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid % 8, qq = G / 8, rr = G % 8;
+  const int lid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + bid / 8;
+  const int nkt = a.K / kBK;
+  const int ntw = lid < a.tiles ? (a.tiles - lid + G - 1) / G : 0;
+  const int NG = ntw * nkt;
+  const uint32_t lds0 = lds_addr(lds);
+
+  // ---- DMA: wave w stages rows 64 (w & 1) + [0, 64) of half w >> 1 (8 pieces of 8 rows) ----
+  const int dh = w >> 1;                 // 0, 1: A halves; 2, 3: B halves
+  uint32_t dvo[8];                       // lane byte offset within the operand, per piece
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int r = 64 * (w & 1) + 8 * q + (lane >> 3);
+    dvo[q] = (uint32_t)(r) * 0u + 16u * (uint32_t)((lane & 7) ^ swz(r));   // chunk part
+  }
+  int dg = 0, dkt = 0, dtile = lid;
+  int dm0 = (dtile / a.ntn) * 256, dn0 = (dtile % a.ntn) * 256;
+  auto dma_pieces = [&](int q0) __attribute__((always_inline)) {   // pieces q0 .. q0 + 3
+    const uint32_t dst = lds0 + (uint32_t)(((dg & 1) * 4 + dh) * kHalfB + 64 * (w & 1) * kRowB);
+    const uint32_t kb = (uint32_t)dkt * kBK * 2u;
+#pragma unroll
+    for (int q = q0; q < q0 + 4; ++q) {
+      const int r = 64 * (w & 1) + 8 * q + (lane >> 3);
+      if (dh < 2) {
+        const uint32_t row = (uint32_t)min(dm0 + dh * 128 + r, a.M - 1);
+        dma_to_lds_s<16>(a.A, row * a.lda * 2u + kb + dvo[q], dst + q * 1024);
+      } else {
+        const uint32_t row = (uint32_t)(dn0 + (dh - 2) * 128 + r);
+        dma_to_lds_s<16>(a.B, row * a.ldb * 2u + kb + dvo[q], dst + q * 1024);
+      }
+    }
+  };
+  auto dma_next = [&]() __attribute__((always_inline)) {
+    ++dg;
+    if (++dkt == nkt) {
+      dkt = 0;
+      dtile += G;
+      dm0 = (dtile / a.ntn) * 256;
+      dn0 = (dtile % a.ntn) * 256;
+    }
+  };
+
+  // ---- fragment offsets within a half ----
+  uint32_t offA[2][4], offB[2][2];
+#pragma unroll
+  for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+    for (int mf = 0; mf < 4; ++mf) {
+      const int r = mq * 64 + mf * 16 + l15;
+      offA[mq][mf] = (uint32_t)(r * kRowB + 16 * (l4 ^ swz(r)));
+    }
+#pragma unroll
+  for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+    for (int nf = 0; nf < 2; ++nf) {
+      const int r = (wq & 1) * 64 + nq * 32 + (l15 >> 2) * 8 + nf * 4 + (l15 & 3);
+      offB[nq][nf] = (uint32_t)(r * kRowB + 16 * (l4 ^ swz(r)));
+    }
+  auto read_A = [&](int buf, int mq, FragA1& f) __attribute__((always_inline)) {
+    const uint32_t hb = lds0 + (uint32_t)((buf * 4 + hf) * kHalfB);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int mf = 0; mf < 4; ++mf) f.v[mf][kk] = lds_read16(hb + (offA[mq][mf] ^ (64u * kk)));
+  };
+  auto read_B = [&](int buf, int nq, FragB1& f) __attribute__((always_inline)) {
+    const uint32_t hb = lds0 + (uint32_t)((buf * 4 + 2 + (wq >> 1)) * kHalfB);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int nf = 0; nf < 2; ++nf) f.v[nf][kk] = lds_read16(hb + (offB[nq][nf] ^ (64u * kk)));
+  };
+
+  f4v acc[4][4][2];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int mf = 0; mf < 4; ++mf)
+#pragma unroll
+      for (int nf = 0; nf < 2; ++nf) acc[q][mf][nf] = f4v{0.f, 0.f, 0.f, 0.f};
+  auto quad = [&](f4v (&c)[4][2], const FragA1& fa, const FragB1& fb) __attribute__((always_inline)) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int mf = 0; mf < 4; ++mf)
+#pragma unroll
+        for (int nf = 0; nf < 2; ++nf)
+          c[mf][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              __builtin_bit_cast(b8v, fb.v[nf][kk]), __builtin_bit_cast(b8v, fa.v[mf][kk]),
+              c[mf][nf], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(a.C, 0, a.cbytes, 0x00020000);
+  auto store_quad = [&](f4v (&c)[4][2], int m0, int n0, int mq, int nq) __attribute__((always_inline)) {
+    const uint32_t row = (uint32_t)(m0 + hf * 128 + mq * 64 + l15);
+    const uint32_t col = (uint32_t)(n0 + wq * 64 + nq * 32 + l4 * 8);
+#pragma unroll
+    for (int mf = 0; mf < 4; ++mf) {
+      i4v v;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const int nf = d >> 1, j = 2 * (d & 1);
+        const b2v p = {(__bf16)c[mf][nf][j], (__bf16)c[mf][nf][j + 1]};
+        v[d] = __builtin_bit_cast(int, p);
+      }
+      __builtin_amdgcn_raw_buffer_store_b128(v, crs, ((row + 16u * mf) * a.ldc + col) * 2u, 0, 0);
+#pragma unroll
+      for (int nf = 0; nf < 2; ++nf) c[mf][nf] = f4v{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto store_tile = [&](int m0, int n0) __attribute__((always_inline)) {
+    store_quad(acc[0], m0, n0, 0, 0);
+    store_quad(acc[1], m0, n0, 0, 1);
+    store_quad(acc[2], m0, n0, 1, 1);
+    store_quad(acc[3], m0, n0, 1, 0);
+  };
+
+  if (NG == 0) return;
+  // prologue: K-tile 0 (all 8 pieces of this wave), retired before the first reads
+  dma_pieces(0);
+  dma_pieces(4);
+  dma_next();
+  dma_wait();
+  lds_barrier();
+  if (hf == 1) __builtin_amdgcn_s_barrier();   // waves 4-7: one segment behind
+
+  FragA1 fa;
+  FragB1 fb;
+  int kt = 0, tile = lid, pm0 = 0, pn0 = 0;
+  int m0 = (tile / a.ntn) * 256, n0 = (tile % a.ntn) * 256;
+  for (int j = 0; j < NG; ++j) {
+    const int buf = j & 1;
+    const bool more = dg < NG;   // K-tile j + 1 to stage
+    // L1: previous tile's stores (older than this K-tile's DMA), DMA pieces 0-3, A(mq 0), B(nq 0)
+    if (kt == 0 && j > 0) store_tile(pm0, pn0);
+    if (more) dma_pieces(0);
+    read_A(buf, 0, fa);
+    read_B(buf, 0, fb);
+    lds_read_wait();
+    __builtin_amdgcn_s_barrier();
+    quad(acc[0], fa, fb);                              // C1: (0,0)
+    __builtin_amdgcn_s_barrier();
+    if (more) dma_pieces(4);                           // L2
+    read_B(buf, 1, fb);
+    lds_read_wait();
+    __builtin_amdgcn_s_barrier();
+    quad(acc[1], fa, fb);                              // C2: (0,1)
+    __builtin_amdgcn_s_barrier();
+    read_A(buf, 1, fa);                                // L3
+    lds_read_wait();
+    __builtin_amdgcn_s_barrier();
+    quad(acc[2], fa, fb);                              // C3: (1,1)
+    __builtin_amdgcn_s_barrier();
+    read_B(buf, 0, fb);                                // L4; this wave's DMA of K-tile j + 1 lands
+    lds_read_wait();
+    dma_wait();
+    if (more) dma_next();
+    __builtin_amdgcn_s_barrier();
+    quad(acc[3], fa, fb);                              // C4: (1,0)
+    __builtin_amdgcn_s_barrier();
+    if (++kt == nkt) {
+      kt = 0;
+      pm0 = m0;
+      pn0 = n0;
+      tile += G;
+      m0 = (tile / a.ntn) * 256;
+      n0 = (tile % a.ntn) * 256;
+    }
+  }
+  store_tile(pm0, pn0);
+  if (hf == 0) __builtin_amdgcn_s_barrier();   // same barrier count in both halves
+}
+
 int launch_tn256(const TnArgs& a, hipStream_t st) {
   constexpr size_t lds = 2 * 4 * (size_t)kHalfB;   // 128 KiB
   static const bool ok = hipFuncSetAttribute((const void*)tn256_kernel,
@@ -489,6 +693,17 @@ int launch_tn256(const TnArgs& a, hipStream_t st) {
   (void)ok;
   const int grid = a.tiles < 256 ? a.tiles : 256;
   hipLaunchKernelGGL(tn256_kernel, dim3(grid), dim3(512), lds, st, a);
+  return 0;
+}
+
+int launch_tnpp(const TnArgs& a, hipStream_t st) {
+  constexpr size_t lds = 2 * 4 * (size_t)kHalfB;   // 128 KiB
+  static const bool ok = hipFuncSetAttribute((const void*)tnpp_kernel,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             (int)lds) == hipSuccess;
+  (void)ok;
+  const int grid = a.tiles < 256 ? a.tiles : 256;
+  hipLaunchKernelGGL(tnpp_kernel, dim3(grid), dim3(512), lds, st, a);
   return 0;
 }
 
@@ -517,8 +732,9 @@ extern "C" int sc_gemm_tn_bf16(const void* A, int64_t lda, const void* B, int64_
   SC_REQUIRE(M > 0 && N > 0 && K > 0, "sc_gemm_tn_bf16: empty shape M=%d N=%d K=%d", M, N, K);
   SC_REQUIRE(K % kBK == 0, "sc_gemm_tn_bf16: K=%d must be a multiple of 64 (zero-pad it)", K);
   SC_REQUIRE(N % kTN == 0, "sc_gemm_tn_bf16: N=%d must be a multiple of 256", N);
-  SC_REQUIRE(tile_m == 0 || tile_m == 128 || tile_m == 192 || tile_m == 256,
-             "sc_gemm_tn_bf16: tile_m=%d must be 0 (default 192), 128, 192 or 256", tile_m);
+  SC_REQUIRE(tile_m == 0 || tile_m == 128 || tile_m == 192 || tile_m == 256 || tile_m == 257,
+             "sc_gemm_tn_bf16: tile_m=%d must be 0 (default 192), 128, 192, 256 or 257 (256, "
+             "ping-pong schedule)", tile_m);
   SC_REQUIRE(lda >= K && ldb >= K && ldc >= N && lda % 8 == 0 && ldb % 8 == 0 && ldc % 8 == 0,
              "sc_gemm_tn_bf16: leading dimensions must cover the rows in 16-byte pieces");
   SC_REQUIRE((uintptr_t)A % 16 == 0 && (uintptr_t)B % 16 == 0 && (uintptr_t)C % 16 == 0,
@@ -526,13 +742,17 @@ extern "C" int sc_gemm_tn_bf16(const void* A, int64_t lda, const void* B, int64_
   SC_REQUIRE((int64_t)M * lda * 2 < (1ll << 32) && (int64_t)N * ldb * 2 < (1ll << 32) &&
                  ((int64_t)M + 256) * ldc * 2 < (1ll << 32),
              "sc_gemm_tn_bf16: operands must be smaller than 4 GiB");
-  const int tm = tile_m ? tile_m : 192;
+  const int tm = tile_m == 257 ? 256 : tile_m ? tile_m : 192;
   const int ntn = N / kTN;
   const int64_t tiles = (int64_t)((M + tm - 1) / tm) * ntn;
   SC_REQUIRE(tiles < (1 << 30), "sc_gemm_tn_bf16: too many tiles");
   TnArgs a{(const __bf16*)A, (const __bf16*)B, (__bf16*)C, M, N, K, ntn, (int)tiles,
            (uint32_t)lda, (uint32_t)ldb, (uint32_t)ldc, (uint32_t)((int64_t)M * ldc * 2)};
   hipStream_t st = (hipStream_t)stream;
+  if (tile_m == 257) {
+    launch_tnpp(a, st);
+    return launch_status("sc_gemm_tn_bf16");
+  }
   if (tm == 256) {
     launch_tn256(a, st);
     return launch_status("sc_gemm_tn_bf16");

@@ -14,6 +14,8 @@
 //   layer_norm_*    nn.LayerNorm(D) between layers                 lucyrnn_triton.py:96-97, :136-137
 //   ctc_fwd/_bwd    nn.CTCLoss(blank, zero_infinity) on log_softmax  train.py:142, model.py:60-71
 //   ctc_greedy_decode  decoder.py:3-30
+//   mlstm_fwd/_bwd  the xLSTM encoder's mLSTM cell (fork mlstm_kernels)  model.py:214-229
+//   rnnt_joint_fwd/_bwd  RNNTPredictorJoiner + log_softmax + warp_rnnt   model.py:73-145, train.py:38-42
 // There is no CPU kernel: calling an op on CPU tensors raises (no silent fallback).
 
 #include <ATen/ATen.h>
@@ -394,6 +396,218 @@ std::tuple<Tensor, Tensor> ctc_greedy_decode_meta(const Tensor& lp, const Tensor
   return {at::empty({lp.size(0), lp.size(1)}, io), at::empty({lp.size(0)}, io)};
 }
 
+// ------------------------------------------------------------------------------ mLSTM --------
+// q, k [B,NH,T,DQ], v [B,NH,T,DV] (bf16 / f16, contiguous), igate / fgate fp32 [B,NH,T]: the
+// chunkwise cell of the xLSTM encoder (model.py:214-229; the fork's mlstm_kernels).
+struct MlstmDims { int64_t B, NH, T, DQ, DV; };
+
+MlstmDims check_mlstm(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& ig,
+                      const Tensor& fg) {
+  TORCH_CHECK(q.dim() == 4 && k.sizes() == q.sizes() && v.dim() == 4 &&
+                  v.sizes().slice(0, 3) == q.sizes().slice(0, 3),
+              "statecatcher::mlstm: q, k [B,NH,T,DQ] and v [B,NH,T,DV]");
+  TORCH_CHECK(q.scalar_type() == k.scalar_type() && q.scalar_type() == v.scalar_type() &&
+                  (q.scalar_type() == at::kBFloat16 || q.scalar_type() == at::kHalf),
+              "statecatcher::mlstm: q, k, v must share a bf16 / f16 dtype");
+  TORCH_CHECK(ig.sizes() == q.sizes().slice(0, 3) && fg.sizes() == ig.sizes(),
+              "statecatcher::mlstm: igate / fgate must be [B,NH,T]");
+  const MlstmDims d{q.size(0), q.size(1), q.size(2), q.size(3), v.size(3)};
+  TORCH_CHECK(d.T % 64 == 0, "statecatcher::mlstm: T=", d.T, " must be a multiple of 64");
+  TORCH_CHECK(sc_mlstm_supported(dtype_code(q), (int)d.DQ, (int)d.DV),
+              "statecatcher::mlstm: head dims (", d.DQ, ", ", d.DV, ") not compiled in");
+  return d;
+}
+
+std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> mlstm_fwd_hip(
+    const Tensor& q_in, const Tensor& k_in, const Tensor& v_in, const Tensor& ig_in,
+    const Tensor& fg_in, const optional<Tensor>& c0, const optional<Tensor>& n0,
+    const optional<Tensor>& m0, double eps) {
+  c10::DeviceGuard guard(q_in.device());
+  const MlstmDims d = check_mlstm(q_in, k_in, v_in, ig_in, fg_in);
+  Tensor q = q_in.contiguous(), k = k_in.contiguous(), v = v_in.contiguous();
+  Tensor ig = f32c(ig_in), fg = f32c(fg_in);
+  optional<Tensor> c0c, n0c, m0c;
+  if (c0 && c0->defined()) c0c = f32c(*c0);
+  if (n0 && n0->defined()) n0c = f32c(*n0);
+  if (m0 && m0->defined()) m0c = f32c(*m0);
+  const int64_t BH = d.B * d.NH, nc = d.T / 64;
+  auto fo = q.options().dtype(at::kFloat);
+  Tensor h = at::empty({d.B, d.NH, d.T, d.DV}, q.options());
+  Tensor c_last = at::empty({d.B, d.NH, d.DQ, d.DV}, fo);
+  Tensor ns = at::empty({BH, nc + 1, d.DQ}, fo), ms = at::empty({BH, nc + 1}, fo);
+  Tensor cs = at::empty({BH, nc, d.DV, d.DQ}, q.options());
+  Tensor mrow = at::empty({BH, d.T}, fo), den = at::empty({BH, d.T}, fo);
+  sc_check(sc_mlstm_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), dtype_code(q), ig.data_ptr<float>(),
+                        fg.data_ptr<float>(), (const float*)opt_ptr(c0c), (const float*)opt_ptr(n0c),
+                        (const float*)opt_ptr(m0c), (int)BH, (int)d.T, (int)d.DQ, (int)d.DV, (float)eps,
+                        h.data_ptr(), cs.data_ptr(), ns.data_ptr<float>(), ms.data_ptr<float>(),
+                        c_last.data_ptr<float>(), mrow.data_ptr<float>(), den.data_ptr<float>(),
+                        nullptr, stream_for(q)),
+           "statecatcher::mlstm_fwd");
+  return {h, c_last, ns, ms, cs, mrow, den};
+}
+
+std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> mlstm_fwd_meta(
+    const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& ig, const Tensor& fg,
+    const optional<Tensor>& c0, const optional<Tensor>& n0, const optional<Tensor>& m0, double eps) {
+  const MlstmDims d = check_mlstm(q, k, v, ig, fg);
+  const int64_t BH = d.B * d.NH, nc = d.T / 64;
+  auto fo = q.options().dtype(at::kFloat);
+  return {at::empty({d.B, d.NH, d.T, d.DV}, q.options()), at::empty({d.B, d.NH, d.DQ, d.DV}, fo),
+          at::empty({BH, nc + 1, d.DQ}, fo), at::empty({BH, nc + 1}, fo),
+          at::empty({BH, nc, d.DV, d.DQ}, q.options()), at::empty({BH, d.T}, fo),
+          at::empty({BH, d.T}, fo)};
+}
+
+std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> mlstm_bwd_hip(
+    const Tensor& q_in, const Tensor& k_in, const Tensor& v_in, const Tensor& ig_in,
+    const Tensor& fg_in, const Tensor& h, const Tensor& dh_in, const optional<Tensor>& dcT,
+    const optional<Tensor>& dnT, const Tensor& cs, const Tensor& ns, const Tensor& ms,
+    const Tensor& mrow, const Tensor& den, double eps) {
+  c10::DeviceGuard guard(q_in.device());
+  const MlstmDims d = check_mlstm(q_in, k_in, v_in, ig_in, fg_in);
+  Tensor q = q_in.contiguous(), k = k_in.contiguous(), v = v_in.contiguous();
+  Tensor ig = f32c(ig_in), fg = f32c(fg_in);
+  Tensor dh = dh_in.to(q.scalar_type()).contiguous(), hc = h.contiguous();
+  TORCH_CHECK(dh.sizes() == hc.sizes() && hc.sizes() == v.sizes(),
+              "statecatcher::mlstm_bwd: h / dh must be [B,NH,T,DV]");
+  const int64_t BH = d.B * d.NH, nc = d.T / 64;
+  TORCH_CHECK(cs.numel() == BH * nc * d.DQ * d.DV && cs.scalar_type() == q.scalar_type(),
+              "statecatcher::mlstm_bwd: c_states is not mlstm_fwd's");
+  optional<Tensor> dcc, dnc;
+  if (dcT && dcT->defined()) dcc = f32c(*dcT);
+  if (dnT && dnT->defined()) dnc = f32c(*dnT);
+  auto fo = q.options().dtype(at::kFloat);
+  Tensor dq = at::empty_like(q), dk = at::empty_like(k), dv = at::empty_like(v);
+  Tensor dc0 = at::empty({d.B, d.NH, d.DQ, d.DV}, fo), dn0 = at::empty({d.B, d.NH, d.DQ}, fo);
+  Tensor qdq = at::empty({d.B, d.NH, d.T}, fo), kdk = at::empty({d.B, d.NH, d.T}, fo);
+  sc_check(sc_mlstm_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), dtype_code(q), ig.data_ptr<float>(),
+                        fg.data_ptr<float>(), hc.data_ptr(), dh.data_ptr(),
+                        (const float*)opt_ptr(dcc), (const float*)opt_ptr(dnc), cs.data_ptr(),
+                        ns.data_ptr<float>(), ms.data_ptr<float>(), mrow.data_ptr<float>(),
+                        den.data_ptr<float>(), (int)BH, (int)d.T, (int)d.DQ, (int)d.DV, (float)eps,
+                        dc0.data_ptr<float>(), dn0.data_ptr<float>(), dq.data_ptr(), dk.data_ptr(),
+                        dv.data_ptr(), qdq.data_ptr<float>(), kdk.data_ptr<float>(), nullptr,
+                        stream_for(q)),
+           "statecatcher::mlstm_bwd");
+  return {dq, dk, dv, dc0, dn0, qdq, kdk};
+}
+
+std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> mlstm_bwd_meta(
+    const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& ig, const Tensor& fg,
+    const Tensor& h, const Tensor& dh, const optional<Tensor>& dcT, const optional<Tensor>& dnT,
+    const Tensor& cs, const Tensor& ns, const Tensor& ms, const Tensor& mrow, const Tensor& den,
+    double eps) {
+  const MlstmDims d = check_mlstm(q, k, v, ig, fg);
+  auto fo = q.options().dtype(at::kFloat);
+  return {at::empty(q.sizes(), q.options()), at::empty(k.sizes(), k.options()),
+          at::empty(v.sizes(), v.options()), at::empty({d.B, d.NH, d.DQ, d.DV}, fo),
+          at::empty({d.B, d.NH, d.DQ}, fo), at::empty({d.B, d.NH, d.T}, fo),
+          at::empty({d.B, d.NH, d.T}, fo)};
+}
+
+// ------------------------------------------------------------------- fused RNN-T joiner ------
+// enc_p [B,T,J], pred_p [B,U+1,J] (the joiner's enc_proj / pred_proj outputs), W [V,J], bias
+// [V]: RNNTPredictorJoiner's joint + log_softmax + warp_rnnt's gathered lattice
+// (model.py:73-145) without the (B,T,U+1,V) logits.
+void check_joint(const Tensor& enc, const Tensor& pred, const Tensor& W, const Tensor& bias,
+                 const Tensor& labels) {
+  TORCH_CHECK(enc.dim() == 3 && pred.dim() == 3 && pred.size(0) == enc.size(0) &&
+                  pred.size(2) == enc.size(2) && W.dim() == 2 && W.size(1) == enc.size(2) &&
+                  bias.dim() == 1 && bias.size(0) == W.size(0),
+              "statecatcher::rnnt_joint: enc_p [B,T,J], pred_p [B,U+1,J], W [V,J], bias [V]");
+  TORCH_CHECK(labels.dim() == 2 && labels.size(0) == enc.size(0) && labels.size(1) >= pred.size(1) - 1,
+              "statecatcher::rnnt_joint: labels must be padded [B, >= U]");
+}
+
+std::tuple<Tensor, Tensor> rnnt_joint_fwd_hip(const Tensor& enc_in, const Tensor& pred_in,
+                                              const Tensor& W_in, const Tensor& bias_in,
+                                              const Tensor& labels_in, const Tensor& flen_in,
+                                              const Tensor& llen_in, int64_t blank) {
+  c10::DeviceGuard guard(enc_in.device());
+  check_joint(enc_in, pred_in, W_in, bias_in, labels_in);
+  Tensor enc = f32c(enc_in), pred = f32c(pred_in), bias = f32c(bias_in);
+  Tensor W = W_in.to(at::kBFloat16).contiguous();
+  const int64_t B = enc.size(0), T = enc.size(1), J = enc.size(2), U = pred.size(1) - 1, V = W.size(0);
+  Tensor labels = labels_in.to(at::kLong).narrow(1, 0, U).contiguous();
+  Tensor flen = flen_in.to(at::kLong).contiguous(), llen = llen_in.to(at::kLong).contiguous();
+  const int64_t wsb = (int64_t)sc_rnnt_workspace_bytes((int)B, (int)std::max<int64_t>(T, 1), (int)U);
+  Tensor ws = at::empty({wsb}, enc.options().dtype(at::kByte));
+  Tensor nll = at::empty({B}, enc.options());
+  if (T == 0 || B == 0) {
+    nll.fill_(std::numeric_limits<double>::infinity());
+    return {nll, ws};
+  }
+  sc_check(sc_rnnt_joint_fwd(enc.data_ptr<float>(), pred.data_ptr<float>(), W.data_ptr(),
+                             bias.data_ptr<float>(), (int)B, (int)T, (int)U, (int)V, (int)J,
+                             labels.data_ptr<int64_t>(), U ? labels.stride(0) : 0,
+                             flen.data_ptr<int64_t>(), llen.data_ptr<int64_t>(), (int)blank,
+                             nll.data_ptr<float>(), ws.data_ptr(), (size_t)wsb, stream_for(enc)),
+           "statecatcher::rnnt_joint_fwd");
+  return {nll, ws};
+}
+
+std::tuple<Tensor, Tensor> rnnt_joint_fwd_meta(const Tensor& enc, const Tensor& pred, const Tensor& W,
+                                               const Tensor& bias, const Tensor& labels,
+                                               const Tensor& flen, const Tensor& llen, int64_t blank) {
+  check_joint(enc, pred, W, bias, labels);
+  const int64_t wsb = (int64_t)sc_rnnt_workspace_bytes(
+      (int)enc.size(0), (int)std::max<int64_t>(enc.size(1), 1), (int)(pred.size(1) - 1));
+  return {at::empty({enc.size(0)}, enc.options().dtype(at::kFloat)),
+          at::empty({wsb}, enc.options().dtype(at::kByte))};
+}
+
+Tensor colsum_rows(const Tensor& x2d) {   // fixed-order fp32 column sums (sc_colsum)
+  const int64_t M = x2d.size(0), N = x2d.size(1);
+  Tensor out = at::empty({N}, x2d.options().dtype(at::kFloat));
+  const size_t wsb = sc_colsum_workspace_bytes((int)M, (int)N);
+  Tensor ws = at::empty({(int64_t)wsb}, x2d.options().dtype(at::kByte));
+  sc_check(sc_colsum(x2d.data_ptr(), dtype_code(x2d), (int)M, (int)N, x2d.stride(0), 1, 1,
+                     out.data_ptr<float>(), ws.data_ptr(), wsb, stream_for(x2d)),
+           "statecatcher::colsum");
+  return out;
+}
+
+std::tuple<Tensor, Tensor, Tensor, Tensor> rnnt_joint_bwd_hip(
+    const Tensor& enc_in, const Tensor& pred_in, const Tensor& W_in, const Tensor& bias_in,
+    const Tensor& labels_in, const Tensor& flen_in, const Tensor& llen_in, const Tensor& ws,
+    const Tensor& scale_in, int64_t blank) {
+  c10::DeviceGuard guard(enc_in.device());
+  check_joint(enc_in, pred_in, W_in, bias_in, labels_in);
+  Tensor enc = f32c(enc_in), pred = f32c(pred_in), bias = f32c(bias_in);
+  Tensor W = W_in.to(at::kBFloat16).contiguous();
+  const int64_t B = enc.size(0), T = enc.size(1), J = enc.size(2), U = pred.size(1) - 1, V = W.size(0);
+  Tensor labels = labels_in.to(at::kLong).narrow(1, 0, U).contiguous();
+  Tensor flen = flen_in.to(at::kLong).contiguous(), llen = llen_in.to(at::kLong).contiguous();
+  auto fo = enc.options();
+  if (T == 0 || B == 0)
+    return {at::zeros_like(enc), at::zeros_like(pred), at::zeros({V, J}, fo), at::zeros({V}, fo)};
+  int ntb = 0, nus = 0, S = 0;
+  sc_check(sc_rnnt_joint_geometry((int)B, (int)T, (int)U, (int)V, &ntb, &nus, &S),
+           "statecatcher::rnnt_joint_geometry");
+  Tensor d_enc = at::empty({nus, B, T, J}, fo), d_pred = at::zeros({B, ntb, U + 1, J}, fo);
+  Tensor dW = at::empty({S, V, J}, fo), db = at::empty({S, V}, fo);
+  Tensor scale = f32c(scale_in.expand({B}));
+  sc_check(sc_rnnt_joint_bwd(enc.data_ptr<float>(), pred.data_ptr<float>(), W.data_ptr(),
+                             bias.data_ptr<float>(), (int)B, (int)T, (int)U, (int)V, (int)J,
+                             labels.data_ptr<int64_t>(), U ? labels.stride(0) : 0,
+                             flen.data_ptr<int64_t>(), llen.data_ptr<int64_t>(), (int)blank,
+                             scale.data_ptr<float>(), d_enc.data_ptr<float>(), d_pred.data_ptr<float>(),
+                             dW.data_ptr<float>(), db.data_ptr<float>(), ws.data_ptr(),
+                             (size_t)ws.numel(), stream_for(enc)),
+           "statecatcher::rnnt_joint_bwd");
+  return {d_enc.sum(0), d_pred.sum(1), colsum_rows(dW.view({S, V * J})).view({V, J}), colsum_rows(db)};
+}
+
+std::tuple<Tensor, Tensor, Tensor, Tensor> rnnt_joint_bwd_meta(
+    const Tensor& enc, const Tensor& pred, const Tensor& W, const Tensor& bias, const Tensor& labels,
+    const Tensor& flen, const Tensor& llen, const Tensor& ws, const Tensor& scale, int64_t blank) {
+  check_joint(enc, pred, W, bias, labels);
+  auto fo = enc.options().dtype(at::kFloat);
+  return {at::empty(enc.sizes(), fo), at::empty(pred.sizes(), fo), at::empty(W.sizes(), fo),
+          at::empty(bias.sizes(), fo)};
+}
+
 }  // namespace
 
 TORCH_LIBRARY(statecatcher, m) {
@@ -417,6 +631,18 @@ TORCH_LIBRARY(statecatcher, m) {
   m.def("ctc_mean(Tensor nll, Tensor tgt_lens) -> (Tensor loss, Tensor factor)");
   m.def("ctc_greedy_decode(Tensor log_probs, Tensor lengths, int blank=0)"
         " -> (Tensor tokens, Tensor counts)");
+  m.def("mlstm_fwd(Tensor q, Tensor k, Tensor v, Tensor igate, Tensor fgate, Tensor? c0=None, "
+        "Tensor? n0=None, Tensor? m0=None, float eps=1e-6) -> (Tensor h, Tensor c_last, "
+        "Tensor n_states, Tensor m_states, Tensor c_states, Tensor m_rows, Tensor den_rows)");
+  m.def("mlstm_bwd(Tensor q, Tensor k, Tensor v, Tensor igate, Tensor fgate, Tensor h, Tensor dh, "
+        "Tensor? dc_last, Tensor? dn_last, Tensor c_states, Tensor n_states, Tensor m_states, "
+        "Tensor m_rows, Tensor den_rows, float eps=1e-6) -> (Tensor dq, Tensor dk, Tensor dv, "
+        "Tensor dc0, Tensor dn0, Tensor qdq, Tensor kdk)");
+  m.def("rnnt_joint_fwd(Tensor enc_p, Tensor pred_p, Tensor W, Tensor bias, Tensor labels, "
+        "Tensor frames_lengths, Tensor labels_lengths, int blank=0) -> (Tensor nll, Tensor workspace)");
+  m.def("rnnt_joint_bwd(Tensor enc_p, Tensor pred_p, Tensor W, Tensor bias, Tensor labels, "
+        "Tensor frames_lengths, Tensor labels_lengths, Tensor workspace, Tensor scale, int blank=0)"
+        " -> (Tensor d_enc, Tensor d_pred, Tensor dW, Tensor dbias)");
 }
 
 TORCH_LIBRARY_IMPL(statecatcher, CUDA, m) {
@@ -430,6 +656,10 @@ TORCH_LIBRARY_IMPL(statecatcher, CUDA, m) {
   m.impl("ctc_bwd", &ctc_bwd_hip);
   m.impl("ctc_mean", &ctc_mean_hip);
   m.impl("ctc_greedy_decode", &ctc_greedy_decode_hip);
+  m.impl("mlstm_fwd", &mlstm_fwd_hip);
+  m.impl("mlstm_bwd", &mlstm_bwd_hip);
+  m.impl("rnnt_joint_fwd", &rnnt_joint_fwd_hip);
+  m.impl("rnnt_joint_bwd", &rnnt_joint_bwd_hip);
 }
 
 TORCH_LIBRARY_IMPL(statecatcher, Meta, m) {
@@ -443,4 +673,8 @@ TORCH_LIBRARY_IMPL(statecatcher, Meta, m) {
   m.impl("ctc_bwd", &ctc_bwd_meta);
   m.impl("ctc_mean", &ctc_mean_meta);
   m.impl("ctc_greedy_decode", &ctc_greedy_decode_meta);
+  m.impl("mlstm_fwd", &mlstm_fwd_meta);
+  m.impl("mlstm_bwd", &mlstm_bwd_meta);
+  m.impl("rnnt_joint_fwd", &rnnt_joint_fwd_meta);
+  m.impl("rnnt_joint_bwd", &rnnt_joint_bwd_meta);
 }

@@ -993,7 +993,7 @@ class MLSTMFn(torch.autograd.Function):
         m0c = None if m0 is None else m0.float().contiguous()
         dev = q.device
         h = torch.empty(BH, T, DV, dtype=cdt, device=dev)
-        Cs = torch.empty(BH, nc, DQ, DV, dtype=cdt, device=dev)   # chunk-start state images
+        Cs = torch.empty(BH, nc, DV, DQ, dtype=cdt, device=dev)   # chunk-start state images [j][i]
         cT = torch.empty(B, NH, DQ, DV, dtype=torch.float32, device=dev)
         ns = torch.empty(BH, nc + 1, DQ, dtype=torch.float32, device=dev)
         ms = torch.empty(BH, nc + 1, dtype=torch.float32, device=dev)
@@ -1025,8 +1025,8 @@ class MLSTMFn(torch.autograd.Function):
         dhc = dh.to(qc.dtype).contiguous().view(BH, T, DV)
         dcTc = None if dcT is None else dcT.float().contiguous()
         dnTc = None if dnT is None else dnT.float().contiguous()
-        dCs = torch.empty(BH, nc + 1, DQ, DV, dtype=torch.float32, device=dev)
-        dns = torch.empty_like(ns)
+        dCs = torch.empty(BH, DQ, DV, dtype=torch.float32, device=dev)   # d initial state
+        dns = torch.empty(BH, DQ, dtype=torch.float32, device=dev)
         dq = torch.empty_like(qc)
         dk = torch.empty_like(kc)
         dv = torch.empty_like(vc)
@@ -1047,8 +1047,8 @@ class MLSTMFn(torch.autograd.Function):
         shp = (B, NH, T)
         return (dq.view(B, NH, T, DQ).to(qdt), dk.view(B, NH, T, DQ).to(kdt),
                 dv.view(B, NH, T, DV).to(vdt), kdk.view(shp), dfg.view(shp),
-                dCs[:, 0].view(B, NH, DQ, DV) if has_c0 else None,
-                dns[:, 0].view(B, NH, DQ) if has_n0 else None, None, None)
+                dCs.view(B, NH, DQ, DV) if has_c0 else None,
+                dns.view(B, NH, DQ) if has_n0 else None, None, None)
 
 
 def _soft_cap(x, cap):
@@ -1094,7 +1094,7 @@ class MLSTMCoreFn(torch.autograd.Function):
         base = a.data_ptr()
         lay = (ctypes.c_int64 * 7)(NH, T * N, DQ, N, T * N, DV, N)
         h = torch.empty(BH, T, DV, dtype=a.dtype, device=dev)
-        Cs = torch.empty(BH, nc, DQ, DV, dtype=a.dtype, device=dev)   # chunk-start state images
+        Cs = torch.empty(BH, nc, DV, DQ, dtype=a.dtype, device=dev)   # chunk-start state images [j][i]
         cT = torch.empty(B, NH, DQ, DV, dtype=torch.float32, device=dev)
         ns = torch.empty(BH, nc + 1, DQ, dtype=torch.float32, device=dev)
         ms = torch.empty(BH, nc + 1, dtype=torch.float32, device=dev)
@@ -1149,8 +1149,8 @@ class MLSTMCoreFn(torch.autograd.Function):
                                    B, T, NH, DV, stream), "sc_mhln_gate_bwd")
         dcTc = None if dcT is None else dcT.float().contiguous()
         dnTc = None if dnT is None else dnT.float().contiguous()
-        dCs = torch.empty(BH, nc + 1, DQ, DV, dtype=torch.float32, device=dev)
-        dns = torch.empty_like(ns)
+        dCs = torch.empty(BH, DQ, DV, dtype=torch.float32, device=dev)   # d initial state
+        dns = torch.empty(BH, DQ, dtype=torch.float32, device=dev)
         qdq = torch.empty(BH, T, dtype=torch.float32, device=dev)
         kdk = torch.empty(BH, T, dtype=torch.float32, device=dev)
         lay = (ctypes.c_int64 * 7)(NH, T * N, DQ, N, T * N, DV, N)
@@ -1169,8 +1169,8 @@ class MLSTMCoreFn(torch.autograd.Function):
         dfg_c = dfg.transpose(1, 2).to(a.dtype)
         da[..., io:io + NH] = _soft_cap_bwd(dig_c, a[..., io:io + NH], cap)
         da[..., fo:fo + NH] = _soft_cap_bwd(dfg_c, a[..., fo:fo + NH], cap)
-        return (da, dCs[:, 0].view(B, NH, DQ, DV) if has_c0 else None,
-                dns[:, 0].view(B, NH, DQ) if has_n0 else None, None,
+        return (da, dCs.view(B, NH, DQ, DV) if has_c0 else None,
+                dns.view(B, NH, DQ) if has_n0 else None, None,
                 _part_sum(part).to(wdt), None, None, None, None, None, None)
 
 

@@ -15,6 +15,8 @@ Reference interfaces (what a ``train.py`` user swaps in):
   ctc_loss    <- nn.CTCLoss(blank, reduction='mean', zero_infinity)  train.py:142 (on model.py:70's
                  log_softmax, fused here when is_logits)
   ctc_greedy_decode <- decoder.py:3-30
+  mlstm       <- the xLSTM encoder's mLSTM cell (fork mlstm_kernels)  model.py:214-229
+  rnnt_joint_nll <- RNNTPredictorJoiner + log_softmax + warp_rnnt      model.py:73-145
 """
 import os
 
@@ -22,7 +24,8 @@ import torch
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_torch_ops.so")
 OPS = ("abi_version", "lucy_scan_fwd", "lucy_scan_bwd", "decay_scan_fwd", "decay_scan_bwd",
-       "layer_norm_fwd", "layer_norm_bwd", "ctc_fwd", "ctc_bwd", "ctc_mean", "ctc_greedy_decode")
+       "layer_norm_fwd", "layer_norm_bwd", "ctc_fwd", "ctc_bwd", "ctc_mean", "ctc_greedy_decode",
+       "mlstm_fwd", "mlstm_bwd", "rnnt_joint_fwd", "rnnt_joint_bwd")
 
 _LOADED = False
 
@@ -119,6 +122,48 @@ def _mean_backward(ctx, grad_loss, grad_factor):
     return (factor * grad_loss if grad_loss is not None else None), None
 
 
+def _mlstm_setup(ctx, inputs, output):
+    q, k, v, ig, fg, c0, n0, m0, eps = inputs
+    h, c_last, ns, ms, cs, mrow, den = output
+    ctx.save_for_backward(q, k, v, ig, fg, h, cs, ns, ms, mrow, den)
+    ctx.eps = eps
+    ctx.has = (c0 is not None, n0 is not None)
+    ctx.nc = ns.shape[1] - 1
+
+
+def _mlstm_backward(ctx, dh, dc_last, dns, dms, dcs, dmrow, dden):
+    """Gradients of (h, final C, final n) -- the n / m state outputs beyond the final chunk are
+    internal (their gradients are ignored, as the stabiliser is not differentiated)."""
+    q, k, v, ig, fg, h, cs, ns, ms, mrow, den = ctx.saved_tensors
+    if dh is None:
+        dh = torch.zeros_like(h)
+    dn_last = None if dns is None else dns[:, ctx.nc].reshape(q.shape[0], q.shape[1], -1)
+    dq, dk, dv, dc0, dn0, qdq, kdk = torch.ops.statecatcher.mlstm_bwd(
+        q, k, v, ig, fg, h, dh, dc_last, dn_last, cs, ns, ms, mrow, den, ctx.eps)
+    # d igate_s = k_s.dk_s ; d fgate_t = sigmoid(-f_t) sum_{r >= t} (q_r.dq_r - k_r.dk_r)
+    dfg = torch.sigmoid(-fg.float()) * (qdq - kdk).flip(-1).cumsum(-1).flip(-1)
+    has_c0, has_n0 = ctx.has
+    return (dq, dk, dv, kdk.to(ig.dtype), dfg.to(fg.dtype), dc0 if has_c0 else None,
+            dn0 if has_n0 else None, None, None)
+
+
+def _joint_setup(ctx, inputs, output):
+    enc, pred, W, bias, labels, flen, llen, blank = inputs
+    ctx.save_for_backward(enc, pred, W, bias, labels, flen, llen, output[1])
+    ctx.blank = blank
+    ctx.dtypes = (enc.dtype, pred.dtype, W.dtype, bias.dtype)
+
+
+def _joint_backward(ctx, grad_nll, grad_ws):
+    enc, pred, W, bias, labels, flen, llen, ws = ctx.saved_tensors
+    if grad_nll is None:
+        return (None,) * 8
+    de, dp, dW, db = torch.ops.statecatcher.rnnt_joint_bwd(enc, pred, W, bias, labels, flen, llen,
+                                                           ws, grad_nll, ctx.blank)
+    ed, pd, wd, bd = ctx.dtypes
+    return de.to(ed), dp.to(pd), dW.to(wd), db.to(bd), None, None, None, None
+
+
 def _register_autograd():
     reg = torch.library.register_autograd
     reg("statecatcher::lucy_scan_fwd", _scan_backward, setup_context=_scan_setup)
@@ -126,6 +171,8 @@ def _register_autograd():
     reg("statecatcher::layer_norm_fwd", _ln_backward, setup_context=_ln_setup)
     reg("statecatcher::ctc_fwd", _ctc_backward, setup_context=_ctc_setup)
     reg("statecatcher::ctc_mean", _mean_backward, setup_context=_mean_setup)
+    reg("statecatcher::mlstm_fwd", _mlstm_backward, setup_context=_mlstm_setup)
+    reg("statecatcher::rnnt_joint_fwd", _joint_backward, setup_context=_joint_setup)
 
 
 # ------------------------------------------------------------------------------- functions ----
@@ -165,3 +212,19 @@ def ctc_loss(x, targets, in_lens, tgt_lens, blank=0, is_logits=True):
 def ctc_greedy_decode(log_probs, lengths, blank=0):
     """(tokens int32 [B,T], counts int32 [B]) of decoder.py's greedy CTC decode."""
     return load().ctc_greedy_decode(log_probs, lengths, blank)
+
+
+def mlstm(q, k, v, igate, fgate, c0=None, n0=None, m0=None, eps=1e-6):
+    """transformers' mlstm_chunkwise(return_last_states=True) on the HIP walk kernels:
+    (h [B,NH,T,DV], (C [B,NH,DQ,DV], n [B,NH,DQ], m [B,NH,1])).  q, k, v bf16 / f16, gates fp32
+    [B,NH,T]; differentiable in q, k, v, the gates, c0 and n0."""
+    h, c_last, ns, ms, _, _, _ = load().mlstm_fwd(q, k, v, igate, fgate, c0, n0, m0, eps)
+    B, NH = q.shape[:2]
+    return h, (c_last, ns[:, -1].reshape(B, NH, -1), ms[:, -1].reshape(B, NH, 1))
+
+
+def rnnt_joint_nll(enc_p, pred_p, W, bias, labels, frames_lengths, labels_lengths, blank=0):
+    """Per-sequence RNN-T nll [B] of the fused joiner (RNNTPredictorJoiner's joint, log_softmax,
+    warp_rnnt's gathered lattice) without materialising the (B, T, U+1, V) logits."""
+    return load().rnnt_joint_fwd(enc_p, pred_p, W, bias, labels, frames_lengths, labels_lengths,
+                                 blank)[0]

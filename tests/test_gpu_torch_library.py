@@ -187,3 +187,51 @@ def test_torch_compile_fullgraph_matches_eager():
     compiled = run(torch.compile(f, fullgraph=True, backend="aot_eager"))
     for a, b in zip(eager, compiled):
         torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
+
+
+def test_mlstm_op_bitwise_vs_ctypes_path_and_opcheck():
+    """torch.ops.statecatcher.mlstm_fwd / _bwd launch the walk kernels the ctypes node
+    (ops.MLSTMFn) launches: h, the final state and every gradient bitwise equal."""
+    tl, ops = _tl(), _ops()
+    g = torch.Generator().manual_seed(3)
+    B, NH, T, DQ, DV = 2, 2, 192, 64, 128
+    q, k = (torch.randn(B, NH, T, DQ, generator=g).to(DEV, torch.bfloat16) for _ in range(2))
+    v = torch.randn(B, NH, T, DV, generator=g).to(DEV, torch.bfloat16)
+    ig = (torch.randn(B, NH, T, generator=g) * 3).to(DEV)
+    fg = (torch.randn(B, NH, T, generator=g) * 2 + 3).to(DEV)
+    c0 = (torch.randn(B, NH, DQ, DV, generator=g) * 0.3).to(DEV)
+    n0 = (torch.randn(B, NH, DQ, generator=g) * 0.3).to(DEV)
+    R = torch.randn(B, NH, T, DV, generator=g).to(DEV)
+    outs = []
+    for fn in (lambda *a: tl.mlstm(*a), lambda *a: ops.mlstm_chunkwise(*a, return_last_states=True)):
+        leaves = [t.clone().requires_grad_() for t in (q, k, v, ig, fg, c0, n0)]
+        h, (c, n, m) = fn(*leaves)
+        ((h.float() * R).sum() + c.sum() + n.sum()).backward()
+        outs.append([h, c, n, m] + [t.grad for t in leaves])
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    torch.library.opcheck(torch.ops.statecatcher.mlstm_fwd.default,
+                          (q, k, v, ig, fg, c0, n0, None, 1e-6),
+                          test_utils=("test_schema", "test_faketensor"))
+
+
+def test_rnnt_joint_op_bitwise_vs_ctypes_path():
+    tl, ops = _tl(), _ops()
+    g = torch.Generator().manual_seed(4)
+    B, T, U, V, J = 2, 37, 7, 96, 64
+    enc = torch.randn(B, T, J, generator=g).to(DEV)
+    pred = torch.randn(B, U + 1, J, generator=g).to(DEV)
+    W = (torch.randn(V, J, generator=g) * 0.3).to(DEV)
+    bias = torch.randn(V, generator=g).to(DEV)
+    lab = torch.randint(1, V, (B, U), generator=g).to(DEV)
+    fl = torch.tensor([T, 20], device=DEV)
+    ll = torch.tensor([U, 3], device=DEV)
+    outs = []
+    for fn in (lambda *a: tl.rnnt_joint_nll(*a, lab, fl, ll, 0),
+               lambda *a: ops.RNNTJointFn.apply(*a, lab, fl, ll, 0)):
+        leaves = [t.clone().requires_grad_() for t in (enc, pred, W, bias)]
+        nll = fn(*leaves)
+        nll.mean().backward()
+        outs.append([nll] + [t.grad for t in leaves])
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)

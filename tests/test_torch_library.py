@@ -111,3 +111,45 @@ def test_cpu_tensors_are_refused(sc):
     h = torch.zeros(1, 64)
     with pytest.raises(NotImplementedError):
         sc.lucy_scan_fwd(g, h, h, None, False)
+
+
+def test_mlstm_and_rnnt_joint_meta_and_autograd_trace(sc):
+    """The P1 ops (mlstm_*, rnnt_*): Meta shapes, and their autograd formulas trace
+    into the backward ops."""
+    B, NH, T, DQ, DV = 2, 4, 128, 96, 192
+    q = torch.empty(B, NH, T, DQ, device=META, dtype=torch.bfloat16, requires_grad=True)
+    k = torch.empty(B, NH, T, DQ, device=META, dtype=torch.bfloat16, requires_grad=True)
+    v = torch.empty(B, NH, T, DV, device=META, dtype=torch.bfloat16, requires_grad=True)
+    ig = torch.empty(B, NH, T, device=META, requires_grad=True)
+    fg = torch.empty(B, NH, T, device=META, requires_grad=True)
+    h, (c, n, m) = tl.mlstm(q, k, v, ig, fg)
+    assert h.shape == (B, NH, T, DV) and h.dtype == torch.bfloat16
+    assert c.shape == (B, NH, DQ, DV) and c.dtype == torch.float32
+    assert n.shape == (B, NH, DQ) and m.shape == (B, NH, 1)
+
+    def f_ml(q, k, v, ig, fg):
+        h, (c, n, m) = tl.mlstm(q, k, v, ig, fg)
+        return torch.autograd.grad(h.float().sum() + c.sum(), (q, k, v, ig, fg))
+    gm = make_fx(f_ml)(q, k, v, ig, fg)
+    names = [str(x.target) for x in gm.graph.nodes if "statecatcher" in str(x.target)]
+    assert "statecatcher.mlstm_fwd.default" in names and "statecatcher.mlstm_bwd.default" in names
+
+    T2, U, V, J = 40, 6, 64, 64
+    enc = torch.empty(B, T2, J, device=META, requires_grad=True)
+    pred = torch.empty(B, U + 1, J, device=META, requires_grad=True)
+    W = torch.empty(V, J, device=META, requires_grad=True)
+    bias = torch.empty(V, device=META, requires_grad=True)
+    lab = torch.empty(B, U, device=META, dtype=torch.long)
+    ln = torch.empty(B, device=META, dtype=torch.long)
+    nll = tl.rnnt_joint_nll(enc, pred, W, bias, lab, ln, ln)
+    assert nll.shape == (B,) and nll.dtype == torch.float32
+
+    def f_j(enc, pred, W, bias):
+        return torch.autograd.grad(tl.rnnt_joint_nll(enc, pred, W, bias, lab, ln, ln).sum(),
+                                   (enc, pred, W, bias))
+    gm = make_fx(f_j)(enc, pred, W, bias)
+    names = [str(x.target) for x in gm.graph.nodes if "statecatcher" in str(x.target)]
+    assert "statecatcher.rnnt_joint_fwd.default" in names
+    assert "statecatcher.rnnt_joint_bwd.default" in names
+    with pytest.raises(RuntimeError, match="multiple of 64"):
+        sc.mlstm_fwd(q[:, :, :100], k[:, :, :100], v[:, :, :100], ig[:, :, :100], fg[:, :, :100])

@@ -2,7 +2,7 @@
 """Frame-major projection GEMMs at the C2 shapes: the persistent MFMA kernel (tn_gemm.hip)
 against the library GEMM torch.matmul picks (TunableOp table on), interleaved rounds in one
 process, HIP-event timing over rotating random inputs.
-usage: python tools/tn_bench.py [--tm 128|192]"""
+usage: python tools/tn_bench.py [--tm 128|192|256|257]"""
 import os
 import sys
 
@@ -20,7 +20,7 @@ if os.path.exists(tab):
     tun.read_file(tab)
 
 dev = "cuda"
-TMS = [int(sys.argv[sys.argv.index("--tm") + 1])] if "--tm" in sys.argv else [192, 128]
+TMS = [int(sys.argv[sys.argv.index("--tm") + 1])] if "--tm" in sys.argv else [257, 256]
 
 
 def timeit(fn, n=10):
@@ -54,7 +54,7 @@ for name, M, N, K in SHAPES:
         for k, f in arms.items():
             res[k].append(timeit(f))
     ref = As[0].float() @ Bs[0].float().t()
-    err = ((ops.gemm_tn(As[0], Bs[0]).float() - ref).abs().max() / ref.abs().max()).item()
+    err = ((ops.gemm_tn(As[0], Bs[0], TMS[0]).float() - ref).abs().max() / ref.abs().max()).item()
     line = " | ".join(f"{k} med {sorted(v)[2]:6.1f} min {min(v):6.1f} us "
                       f"({F / sorted(v)[2] / 1e6:6.1f} TF/s)" for k, v in res.items())
     out_gbs = M * N * 2 / (min(res[f"tn{TMS[0]}"]) * 1e-6) / 1e9
