@@ -11,15 +11,15 @@
 //           num_t = sum_{s<=t} W_ts (q_t.k_s) v_s + s e^{b_t + m_k - m_t} q_t C~_k
 //           den_t = sum_{s<=t} W_ts (q_t.k_s)     + s e^{b_t + m_k - m_t} q_t.n~_k
 //           h_t = num_t / (max(|den_t|, e^{-m_t}) + eps)
-// Kernels (one 4-wave workgroup each; 16x16x32 bf16/f16 MFMA, fp32 accumulation, fp32 state):
-//   mlstm_fw_walk per (b,h, 64-column block of C~): walks the chunks in order with the state
-//                block in MFMA accumulators; per chunk S = Q K^T, causal decay mask,
+// Kernels (16x16x32 bf16/f16 MFMA, fp32 accumulation, fp32 state):
+//   mlstm_fw_walk per (b,h, 64-column block of C~), 4 waves: walks the chunks in order with the
+//                state block in MFMA accumulators; per chunk S = Q K^T, causal decay mask,
 //                H[:, block] = M V[:, block] + Q~ C~_k[:, block], normaliser (S and the
 //                normaliser recomputed per block), then the state update.  Keeps m_t, den_t and
 //                the compute-dtype image of every chunk-start state for the backward.
-//   mlstm_bw_dC  per (b,h): reverse walk, dC~_k = e^{g+m_k-m_{k+1}} dC~_{k+1} + Q~^T dnum
-//   mlstm_bw_dQ / _dK / _dV  per (b,h,chunk): the three input gradients (intra-chunk terms
-//                through dA = W o (dnum V^T + dden), inter-chunk terms through C~_k / dC~_{k+1})
+//   mlstm_bw_walk per (b,h), 8 waves: walks the chunks in reverse with dC~ in MFMA accumulators
+//                and computes the chunk's three input gradients on the way (intra-chunk terms
+//                through dA = W o (dnum V^T + dden), inter-chunk terms through C~_k / dC~_{k+1}).
 // The stabiliser m is treated as a constant in the backward (it cancels in h up to the eps
 // term), as the chunkwise kernels of the mlstm_kernels family do.  Gate gradients follow from
 // the pair identities  di_s = k_s.dk_s  and  dF_t = q_t.dq_t - k_t.dk_t  (F = cumulative
@@ -28,6 +28,14 @@
 #include <initializer_list>
 
 #include "sc_common.h"
+
+// SC_ML_ABL: timing ablations (tools/mlstm_abl.sh; results are garbage).  Forward walk: 1 no S
+// MFMAs, 2 no H MFMAs, 4 no state-update MFMAs, 8 no global stores, 16 no LDS fill.  Backward
+// walk: 32 no A/dA phase, 64 no dq phase, 128 no dk/dv phase, 256 no dC update, 512 no loads.
+#ifndef SC_ML_ABL
+#define SC_ML_ABL 0
+#endif
+#define ML_ABL(b) ((SC_ML_ABL & (b)) != 0)
 
 namespace sc {
 
@@ -129,337 +137,66 @@ __device__ __forceinline__ V8 frag_ks(const T* tile, int ld, int r0, int k0, int
   return x;
 }
 
-// Gate prefix quantities of one chunk, computed by wave 0 (lane = step s) into LDS:
-// sb[s] = b_s (inclusive cumulative logsig f), si[s] = i_s; returns g = b_{L-1} in every lane
-// of wave 0 (others get 0).
-__device__ __forceinline__ void chunk_gates(const MArgs& a, int bh, int k, float* sb, float* si,
-                                            int tid) {
-  if (tid < 64) {
-    const int64_t o = (int64_t)bh * a.T + k * kL + tid;
-    const float i = a.ig[o];
-    float b = logsig(a.fg[o]);
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const float u = __shfl_up(b, d);
-      if (tid >= d) b += u;
-    }
-    sb[tid] = b;
-    si[tid] = i;
-  }
+// ---- cross-lane helpers on DPP (VALU lane moves; __shfl_* would be an LDS permute round trip
+// each, and the walks' per-chunk chains are latency-bound) ----
+// lane moves within 16-lane rows; lanes whose source is out of the row keep `old`
+template <int CTRL>
+__device__ __forceinline__ float dppf(float old, float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, old),
+                                                               __builtin_bit_cast(int, x), CTRL,
+                                                               0xf, 0xf, false));
 }
-
-// inclusive prefix max over the 64 lanes of a wave
-__device__ __forceinline__ float wave_prefix_max(float x, int lane) {
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const float u = __shfl_up(x, d);
-    if (lane >= d) x = fmaxf(x, u);
-  }
-  return x;
+__device__ __forceinline__ float rdlane(float x, int l) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), l));
 }
-__device__ __forceinline__ float wave_max(float x) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) x = fmaxf(x, __shfl_xor(x, o));
-  return x;
+constexpr int kQuadX1 = 0xB1, kQuadX2 = 0x4E, kHalfMirror = 0x141, kRowMirror = 0x140;
+constexpr int kRowShr1 = 0x111, kRowShr2 = 0x112, kRowShr4 = 0x114, kRowShr8 = 0x118;
+// sums over aligned groups of 4 / 8 / 16 lanes (every lane of the group gets the total)
+__device__ __forceinline__ float sum4(float x) {
+  x += dppf<kQuadX1>(0.0f, x);
+  return x + dppf<kQuadX2>(0.0f, x);
+}
+__device__ __forceinline__ float sum8(float x) {
+  x = sum4(x);
+  return x + dppf<kHalfMirror>(0.0f, x);
 }
 // sum over the 16 lanes that share (lane >> 4) — the columns of one accumulator row group
 __device__ __forceinline__ float sum16(float x) {
-#pragma unroll
-  for (int o = 1; o < 16; o <<= 1) x += __shfl_xor(x, o);
-  return x;
+  x = sum8(x);
+  return x + dppf<kRowMirror>(0.0f, x);
+}
+__device__ __forceinline__ float wave_max(float x) {
+  x = fmaxf(x, dppf<kQuadX1>(x, x));
+  x = fmaxf(x, dppf<kQuadX2>(x, x));
+  x = fmaxf(x, dppf<kHalfMirror>(x, x));
+  x = fmaxf(x, dppf<kRowMirror>(x, x));
+  return fmaxf(fmaxf(rdlane(x, 0), rdlane(x, 16)), fmaxf(rdlane(x, 32), rdlane(x, 48)));
+}
+// inclusive prefix sum / max over the 64 lanes of a wave: Hillis-Steele within each 16-lane row,
+// then the row totals (read as scalars) carried into the rows above
+__device__ __forceinline__ float wave_prefix_sum(float x, int lane) {
+  x += dppf<kRowShr1>(0.0f, x);
+  x += dppf<kRowShr2>(0.0f, x);
+  x += dppf<kRowShr4>(0.0f, x);
+  x += dppf<kRowShr8>(0.0f, x);
+  const float r1 = rdlane(x, 15), r2 = rdlane(x, 31), r3 = rdlane(x, 47);
+  const int row = lane >> 4;
+  const float o12 = r1 + r2;
+  return x + (row == 0 ? 0.0f : row == 1 ? r1 : row == 2 ? o12 : o12 + r3);
+}
+__device__ __forceinline__ float wave_prefix_max(float x, int lane) {
+  constexpr float ninf = -__builtin_huge_valf();
+  x = fmaxf(x, dppf<kRowShr1>(ninf, x));
+  x = fmaxf(x, dppf<kRowShr2>(ninf, x));
+  x = fmaxf(x, dppf<kRowShr4>(ninf, x));
+  x = fmaxf(x, dppf<kRowShr8>(ninf, x));
+  const float r1 = rdlane(x, 15), r2 = rdlane(x, 31), r3 = rdlane(x, 47);
+  const int row = lane >> 4;
+  const float o12 = fmaxf(r1, r2);
+  return fmaxf(x, row == 0 ? ninf : row == 1 ? r1 : row == 2 ? o12 : fmaxf(o12, r3));
 }
 
-// Column block of the state: C~'s columns evolve independently (C~ += K^T diag(f) V), so each
-// workgroup owns kCB = 64 columns of one (b,h) -- DV/64 x BH workgroups instead of BH; n~ and m
-// are recomputed by every block (they need K and the gates only) and stored by block 0.
-constexpr int kCB = 64;
-
-// ------------------------------------------------------------------------- forward: walk ----
-// One workgroup per (b,h, 64-column block of C~) walks the chunks in order and does both halves
-// of the chunkwise forward for its columns: the chunk's outputs H[:, block] (S = Q K^T, causal
-// decay mask, M V + Q~ C~_k, normaliser) and the state update C~_{k+1}[:, block].  The state block
-// never leaves the MFMA accumulators: only its bf16 / f16 image (what the Q~ C~_k MFMA consumes,
-// kept for the backward's dq) and n~, m go to HBM -- no fp32 state stream and no re-read of it.
-template <int DT, int DQ, int DV>
-__global__ void __launch_bounds__(256, 2) mlstm_fw_walk(MArgs a) {
-  using M = MF<DT>;
-  using T = typename M::T;
-  using V8 = typename M::v8;
-  constexpr int TJ = kCB / 16, NT = (DQ / 16) * TJ, PW = NT / 4;
-  static_assert(NT % 4 == 0, "tile count must split over 4 waves");
-  const int cb = blockIdx.x, bh = blockIdx.y, w = threadIdx.x >> 6;
-  int tid = threadIdx.x, lane = tid & 63;
-  const int cj0 = cb * kCB;
-  __shared__ __attribute__((aligned(16))) T Qs[kL * (DQ + kPad)];
-  __shared__ __attribute__((aligned(16))) T Ks[kL * (DQ + kPad)];
-  __shared__ __attribute__((aligned(16))) T KT[DQ * (kL + kPad)];
-  __shared__ __attribute__((aligned(16))) T VT[kCB * (kL + kPad)];
-  __shared__ __attribute__((aligned(16))) T Ms[kL * (kL + kPad)];
-  __shared__ __attribute__((aligned(16))) T CT[kCB * (DQ + kPad)];
-  __shared__ float sb[kL], si[kL], mt[kL], rowf[kL], fs[kL], dsum[kL], qn[kL], nk[DQ], scal[2];
-  const T* Q = (const T*)a.q + qrow(a, bh, 0);
-  const T* K = (const T*)a.k + qrow(a, bh, 0);
-  const T* V = (const T*)a.v + vrow(a, bh, 0);
-  T* H = (T*)a.h + (int64_t)bh * a.T * DV;
-  f32x4 acc[PW];
-#pragma unroll
-  for (int p = 0; p < PW; ++p) {
-    const int q = w + 4 * p, i0 = 16 * (q / TJ), j0 = cj0 + 16 * (q % TJ);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int i = i0 + 4 * (lane >> 4) + r, j = j0 + (lane & 15);
-      acc[p][r] = a.c0 ? a.c0[((int64_t)bh * DQ + i) * DV + j] : 0.0f;
-    }
-  }
-  float n = (tid < DQ && a.n0) ? a.n0[(int64_t)bh * DQ + tid] : 0.0f;
-  float m = a.m0 ? a.m0[bh] : 0.0f;
-  // chunk inputs are prefetched into registers one chunk ahead: the loads of chunk k + 1 are
-  // issued right after chunk k's are written to LDS and land while chunk k computes (issued
-  // and waited per loader loop they cost a full memory latency each, four times per chunk)
-  constexpr int NQP = kL * DQ / 8 / 256, NVP = kL * kCB / 8 / 256;
-  static_assert(NQP * 256 * 8 == kL * DQ && NVP * 256 * 8 == kL * kCB, "piece split");
-  u32x4 pq[NQP], pk[NQP], pv[NVP];
-  float pig = 0.0f, pfg = 0.0f;
-  auto prefetch = [&](int kc) __attribute__((always_inline)) {
-    const int64_t tb = (int64_t)kc * kL;
-#pragma unroll
-    for (int u = 0; u < NQP; ++u) {
-      const int e = tid + 256 * u, r = e / (DQ / 8), c = (e % (DQ / 8)) * 8;
-      pq[u] = *(const u32x4*)(Q + (tb + r) * a.qt + c);
-      pk[u] = *(const u32x4*)(K + (tb + r) * a.qt + c);
-    }
-#pragma unroll
-    for (int u = 0; u < NVP; ++u) {
-      const int e = tid + 256 * u, r = e % kL, c = (e / kL) * 8;
-      pv[u] = *(const u32x4*)(V + (tb + r) * a.vt + cj0 + c);
-    }
-    if (tid < 64) {
-      const int64_t o = (int64_t)bh * a.T + tb + tid;
-      pig = a.ig[o];
-      pfg = a.fg[o];
-    }
-  };
-  prefetch(0);
-  for (int k = 0; k < a.nc; ++k) {
-    const int64_t t0 = (int64_t)k * kL;
-    // re-derive the lane-dependent addresses every chunk instead of holding dozens of them in
-    // VGPRs across the loop (hoisted, they pushed the prefetch registers out to scratch)
-    asm volatile("" : "+v"(tid), "+v"(lane));
-#pragma unroll
-    for (int u = 0; u < NQP; ++u) {
-      const int e = tid + 256 * u, r = e / (DQ / 8), c = (e % (DQ / 8)) * 8;
-      *(u32x4*)(Qs + r * (DQ + kPad) + c) = pq[u];
-      *(u32x4*)(Ks + r * (DQ + kPad) + c) = pk[u];
-      const V8 x = __builtin_bit_cast(V8, pk[u]);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) KT[(c + j) * (kL + kPad) + r] = x[j];
-    }
-#pragma unroll
-    for (int u = 0; u < NVP; ++u) {
-      const int e = tid + 256 * u, r = e % kL, c = (e / kL) * 8;
-      const V8 x = __builtin_bit_cast(V8, pv[u]);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) VT[(c + j) * (kL + kPad) + r] = x[j];
-    }
-    if (tid < 64) {   // chunk_gates on the prefetched pre-activations
-      float b = logsig(pfg);
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const float u = __shfl_up(b, d);
-        if (tid >= d) b += u;
-      }
-      sb[tid] = b;
-      si[tid] = pig;
-    }
-    if (k + 1 < a.nc) prefetch(k + 1);
-    // the state at the chunk start: its MFMA image, transposed ([j][i]); a lane's four
-    // accumulator rows are consecutive i, so each tile is one 8-byte LDS store
-#pragma unroll
-    for (int p = 0; p < PW; ++p) {
-      const int q = w + 4 * p, i0 = 16 * (q / TJ), j0 = 16 * (q % TJ);
-      typedef T v4 __attribute__((ext_vector_type(4)));
-      v4 c;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) c[r] = (T)acc[p][r];
-      *(v4*)(CT + (j0 + (lane & 15)) * (DQ + kPad) + i0 + 4 * (lane >> 4)) = c;
-    }
-    if (tid < DQ) {
-      nk[tid] = n;
-      if (cb == 0) a.ns[((int64_t)bh * (a.nc + 1) + k) * DQ + tid] = n;
-    }
-    if (cb == 0 && tid == 0) a.ms[(int64_t)bh * (a.nc + 1) + k] = m;
-    if (tid < 64) {   // wave 0: row stabilisers, output scale, state-update key weights
-      const float bt = sb[tid];
-      const float mi = bt + wave_prefix_max(si[tid] - bt, tid);
-      const float m_t = fmaxf(bt + m, mi);
-      mt[tid] = m_t;
-      rowf[tid] = a.scale * expf(bt + m - m_t);
-      const float g = __shfl(bt, 63);
-      const float as = g - bt + si[tid];
-      const float mn = fmaxf(g + m, wave_max(as));
-      fs[tid] = expf(as - mn);
-      if (tid == 0) {
-        scal[0] = expf(g + m - mn);
-        scal[1] = mn;
-      }
-    }
-    __syncthreads();
-    // the backward's copy of the chunk-start state: CT's rows as they are, [j][i] (16-byte stores)
-    {
-      T* Cs = (T*)a.Cs + (((int64_t)bh * a.nc + k) * DV + cj0) * DQ;
-      constexpr int NCP = kCB * DQ / 8 / 256;
-      static_assert(NCP * 256 * 8 == kCB * DQ, "state image split");
-#pragma unroll
-      for (int u = 0; u < NCP; ++u) {
-        const int e = tid + 256 * u, j = e / (DQ / 8), c = (e % (DQ / 8)) * 8;
-        *(u32x4*)(Cs + j * DQ + c) = *(const u32x4*)(CT + j * (DQ + kPad) + c);
-      }
-    }
-    // From here to the state update every wave touches only its own 16 rows of Ms / qn / dsum
-    // (rows 16 w ..): no barrier between the S and H phases.
-    // q_t . n~_k (4 threads per row, DQ / 4 consecutive i each)
-    {
-      constexpr int QP = DQ / 4;
-      const int t = tid >> 2, part = tid & 3;
-      float qa = 0.0f;
-#pragma unroll
-      for (int u = 0; u < QP / 8; ++u) {
-        const V8 x = *(const V8*)(Qs + t * (DQ + kPad) + part * QP + 8 * u);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) qa += (float)x[e] * nk[part * QP + 8 * u + e];
-      }
-      qa += __shfl_xor(qa, 1);
-      qa += __shfl_xor(qa, 2);
-      if (part == 0) qn[t] = qa;
-    }
-    // S = Q K^T for row block w, causal column blocks; M = S o W into LDS, row sums
-    {
-      float rs[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 1
-      for (int ct = 0; ct <= w; ++ct) {
-        f32x4 s4 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int kk = 0; kk < DQ / 32; ++kk)
-          s4 = M::mma(frag<V8, T>(Qs, DQ + kPad, 16 * w, 32 * kk, lane),
-                      frag<V8, T>(Ks, DQ + kPad, 16 * ct, 32 * kk, lane), s4);
-        const int s = 16 * ct + (lane & 15);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int t = 16 * w + 4 * (lane >> 4) + r;
-          const float mv = (s <= t) ? s4[r] * a.scale * expf(sb[t] - sb[s] + si[s] - mt[t]) : 0.0f;
-          rs[r] += mv;
-          Ms[t * (kL + kPad) + s] = (T)mv;
-        }
-      }
-      // the column blocks right of the diagonal: zero (the H MFMA reads them)
-      for (int ct = w + 1; ct < 4; ++ct) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          Ms[(16 * w + 4 * (lane >> 4) + r) * (kL + kPad) + 16 * ct + (lane & 15)] = (T)0.0f;
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float tot = sum16(rs[r]);
-        if ((lane & 15) == 0) dsum[16 * w + 4 * (lane >> 4) + r] = tot;
-      }
-    }
-    // H = M V + (rowf Q) C~_k for row block w, normalised; staged in the wave's own Ms rows
-    // (every cj has read them first) and stored as 16-byte rows
-    {
-      const float rf = rowf[16 * w + (lane & 15)];
-      const int kin = (16 * (w + 1) + 31) / 32;
-      float zi[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int t = 16 * w + 4 * (lane >> 4) + r;
-        const float dn = dsum[t] + rowf[t] * qn[t];
-        zi[r] = 1.0f / (fmaxf(fabsf(dn), expf(-mt[t])) + a.eps);
-      }
-      f32x4 hv[TJ];
-#pragma unroll
-      for (int cj = 0; cj < TJ; ++cj) {
-        f32x4 h4 = {0.f, 0.f, 0.f, 0.f};
-        for (int kk = 0; kk < kin; ++kk)
-          h4 = M::mma(frag<V8, T>(Ms, kL + kPad, 16 * w, 32 * kk, lane),
-                      frag<V8, T>(VT, kL + kPad, 16 * cj, 32 * kk, lane), h4);
-#pragma unroll
-        for (int kk = 0; kk < DQ / 32; ++kk)
-          h4 = M::mma(frag_rs<V8, T>(Qs, DQ + kPad, 16 * w, 32 * kk, lane, rf),
-                      frag<V8, T>(CT, DQ + kPad, 16 * cj, 32 * kk, lane), h4);
-        hv[cj] = h4;
-        __builtin_amdgcn_sched_barrier(0);
-      }
-#pragma unroll
-      for (int cj = 0; cj < TJ; ++cj) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          Ms[(16 * w + 4 * (lane >> 4) + r) * (kL + kPad) + 16 * cj + (lane & 15)] =
-              (T)(hv[cj][r] * zi[r]);
-      }
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {   // 16 rows x 128 bytes = 128 pieces over 64 lanes
-        const int e = lane + 64 * u, t = 16 * w + (e >> 3), c = (e & 7) * 8;
-        *(u32x4*)(H + (t0 + t) * DV + cj0 + c) = *(const u32x4*)(Ms + t * (kL + kPad) + c);
-      }
-      if (cb == 0 && lane < 16) {   // the wave's own rows
-        const int t = 16 * w + lane;
-        a.mrow[(int64_t)bh * a.T + t0 + t] = mt[t];
-        a.den[(int64_t)bh * a.T + t0 + t] = dsum[t] + rowf[t] * qn[t];
-      }
-    }
-    // state update: C~ <- decay C~ + (fs K)^T V[:, block];  n~ likewise
-    const float decay = scal[0];
-#pragma unroll
-    for (int p = 0; p < PW; ++p) {
-      const int q = w + 4 * p, i0 = 16 * (q / TJ), j0 = 16 * (q % TJ);
-      f32x4 c = acc[p] * decay;
-#pragma unroll
-      for (int kk = 0; kk < kL / 32; ++kk)
-        c = M::mma(frag_ks<V8, T>(KT, kL + kPad, i0, 32 * kk, lane, fs),
-                   frag<V8, T>(VT, kL + kPad, j0, 32 * kk, lane), c);
-      acc[p] = c;
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if (tid < DQ) {
-      float sacc = 0.0f;
-#pragma unroll
-      for (int u = 0; u < kL / 8; ++u) {
-        const V8 x = *(const V8*)(KT + tid * (kL + kPad) + 8 * u);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) sacc += fs[8 * u + e] * (float)x[e];
-      }
-      n = decay * n + sacc;
-    }
-    m = scal[1];
-    __syncthreads();
-  }
-  // final state: fp32 (the carried segment state) + n~, m
-#pragma unroll
-  for (int p = 0; p < PW; ++p) {
-    const int q = w + 4 * p, i0 = 16 * (q / TJ), j0 = cj0 + 16 * (q % TJ);
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-      a.c_last[((int64_t)bh * DQ + i0 + 4 * (lane >> 4) + r) * DV + j0 + (lane & 15)] = acc[p][r];
-  }
-  if (cb == 0) {
-    if (tid < DQ) a.ns[((int64_t)bh * (a.nc + 1) + a.nc) * DQ + tid] = n;
-    if (tid == 0) a.ms[(int64_t)bh * (a.nc + 1) + a.nc] = m;
-  }
-}
-
-// ------------------------------------------------------------------------- backward: walk ----
-// One 8-wave workgroup per sequence (b,h) walks the chunks in REVERSE with the state gradient
-// dC~ [DQ][DV] (fp32) in MFMA accumulators, and per chunk computes all three input gradients:
-//   dq_t = sum_s dA_ts k_s + rowf_t dnum_t C~_k^T + rowf_t dden_t n~_k
-//   dk_s = sum_t dA_ts q_t + es_s v_s dC~_{k+1}^T + es_s dn~_{k+1}
-//   dv_s = sum_t A_ts dnum_t + es_s k_s dC~_{k+1}
-//   dC~_k = decay dC~_{k+1} + (rowf q)^T dnum,   dn~_k = decay dn~_{k+1} + sum_t rowf_t dden_t q_t
-// (dA_ts = W_ts (dnum_t . v_s + dden_t), A_ts = W_ts q_t . k_s, W_ts = s e^{b_t - b_s + i_s - m_t},
-// s <= t).  Every operand lives in LDS once, row-major; MFMA fragments that run along a column
-// come out through ds_read_b64_tr_b16 (transposed reads), so no transposed copies are stored.
-// C~_k is the forward's compute-dtype image; dC~_{k+1}'s image replaces it in LDS once the dq
-// terms are done.  Nothing of size T x DQ x DV goes to HBM: the chunk states of the gradient
-// stay on chip (the gradient w.r.t. the initial state is the only state output).
+// ---- transposed LDS fragment reads (ds_read_b64_tr_b16) ----
 template <typename T>
 __device__ __forceinline__ uint32_t lds_off(const T* base, int row, int ld, int col) {
   return (uint32_t)(size_t)(const __attribute__((address_space(3))) T*)(base + row * ld + col);
@@ -488,11 +225,337 @@ __device__ __forceinline__ V8 frag_t_ks(const T* img, int ld, int k0, int n0, in
   return x;
 }
 
+// Column block of the state: C~'s columns evolve independently (C~ += K^T diag(f) V), so each
+// workgroup owns kCB = 64 columns of one (b,h) -- DV/64 x BH workgroups instead of BH; n~ and m
+// are recomputed by every block (they need K and the gates only) and stored by block 0.
+constexpr int kCB = 64;
+
+// ------------------------------------------------------------------------- forward: walk ----
+// Gate quantities of one chunk for the lane's step s = lane, computed by every wave from the same
+// 64 pre-activations (identical results in every wave: no LDS round trip for the values a lane
+// needs itself, and the stabiliser m stays a per-wave register).
+struct ChunkGates {
+  float b;      // b_s: inclusive cumulative logsig(f) within the chunk
+  float i;      // i_s
+  float mt;     // m_t: the row stabiliser (t = lane)
+  float rowf;   // s e^{b_t + m_k - m_t}: weight of the inter-chunk term of row t
+  float fs;     // e^{g - b_s + i_s - m_{k+1}}: weight of key s in the state update
+  float decay;  // e^{g + m_k - m_{k+1}}
+  float mn;     // m_{k+1}
+};
+__device__ __forceinline__ ChunkGates chunk_gate_math(float ig, float fg, float m, float scale,
+                                                      int lane) {
+  ChunkGates G;
+  const float b = wave_prefix_sum(logsig(fg), lane);
+  G.b = b;
+  G.i = ig;
+  G.mt = fmaxf(b + m, b + wave_prefix_max(ig - b, lane));
+  G.rowf = scale * expf(b + m - G.mt);
+  const float g = rdlane(b, 63);
+  const float as = g - b + ig;
+  G.mn = fmaxf(g + m, wave_max(as));
+  G.fs = expf(as - G.mn);
+  G.decay = expf(g + m - G.mn);
+  return G;
+}
+
+// One workgroup per (b,h, 64-column block of C~) walks the chunks in order and does both halves
+// of the chunkwise forward for its columns: the chunk's outputs H[:, block] (S = Q K^T, causal
+// decay mask, M V + Q~ C~_k, normaliser) and the state update C~_{k+1}[:, block].  The state block
+// and n~ never leave the MFMA accumulators: only the state's bf16 / f16 image (what the Q~ C~_k
+// MFMA consumes, kept for the backward's dq) and n~, m go to HBM.
+// LDS holds every operand row-major as loaded (16-byte stores); the operands that run along a
+// column (K^T in the state update, V in M V) come out through transposed reads.  Per-row weights
+// scale the accumulators, per-k weights are folded into one scaled copy Kf = diag(fs) K written
+// with the fill: no VALU work between a fragment read and its MFMA.
+template <int DT, int DQ, int DV>
+__global__ void __launch_bounds__(256, 2) mlstm_fw_walk(MArgs a) {
+  using M = MF<DT>;
+  using T = typename M::T;
+  using V8 = typename M::v8;
+  typedef T v4t __attribute__((ext_vector_type(4)));
+  constexpr int LQ = DQ + kPad, LC = kCB + kPad;
+  constexpr int TJ = kCB / 16, NI = DQ / 16, NT = NI * TJ, PW = NT / 4;
+  static_assert(NT % 4 == 0, "tile count must split over 4 waves");
+  const int cb = blockIdx.x, bh = blockIdx.y, w = threadIdx.x >> 6;
+  int tid = threadIdx.x, lane = tid & 63;
+  const int cj0 = cb * kCB;
+  __shared__ __attribute__((aligned(16))) T Qs[kL * LQ];
+  __shared__ __attribute__((aligned(16))) T Ks[kL * LQ];
+  __shared__ __attribute__((aligned(16))) T Kf[kL * LQ];
+  __shared__ __attribute__((aligned(16))) T Vs[kL * LC];
+  __shared__ __attribute__((aligned(16))) T Ms[kL * LC];   // M = S o W, then H staging
+  __shared__ __attribute__((aligned(16))) T CT[kCB * LQ];  // C~_k[:, block], [j][i]
+  __shared__ float sb[kL], si[kL], mts[kL], rowfs[kL], dsum[kL], qn[kL], fsv[kL], nk[DQ], np2[2 * DQ];
+  const T* Q = (const T*)a.q + qrow(a, bh, 0);
+  const T* K = (const T*)a.k + qrow(a, bh, 0);
+  const T* V = (const T*)a.v + vrow(a, bh, 0);
+  T* H = (T*)a.h + (int64_t)bh * a.T * DV;
+  f32x4 acc[PW];   // C~ tiles q = w + 4 p: rows i0 = 16 (q / TJ), block columns 16 (q % TJ)
+#pragma unroll
+  for (int p = 0; p < PW; ++p) {
+    const int q = w + 4 * p, i0 = 16 * (q / TJ), j0 = cj0 + 16 * (q % TJ);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = i0 + 4 * (lane >> 4) + r, j = j0 + (lane & 15);
+      acc[p][r] = a.c0 ? a.c0[((int64_t)bh * DQ + i) * DV + j] : 0.0f;
+    }
+  }
+  // n~ (fp32: the normaliser's q.n~ can cancel, and bf16 products in its sum showed) on thread
+  // i < DQ; its chunk increment sum_s fs_s k_s[i] comes as two half sums from threads i, DQ + i
+  float n = (tid < DQ && a.n0) ? a.n0[(int64_t)bh * DQ + tid] : 0.0f;
+  float decay = 1.0f;
+  float m = a.m0 ? a.m0[bh] : 0.0f;
+  // chunk inputs are prefetched into registers one chunk ahead: the loads of chunk k + 1 are
+  // issued right after chunk k's are written to LDS and land while chunk k computes
+  constexpr int NQP = kL * DQ / 8 / 256, NVP = kL * kCB / 8 / 256;
+  static_assert(NQP * 256 * 8 == kL * DQ && NVP * 256 * 8 == kL * kCB, "piece split");
+  u32x4 pq[NQP], pk[NQP], pv[NVP];
+  float pig, pfg;
+  auto prefetch = [&](int kc) __attribute__((always_inline)) {
+    const int64_t tb = (int64_t)kc * kL;
+#pragma unroll
+    for (int u = 0; u < NQP; ++u) {
+      const int e = tid + 256 * u, r = e / (DQ / 8), c = (e % (DQ / 8)) * 8;
+      pq[u] = *(const u32x4*)(Q + (tb + r) * a.qt + c);
+      pk[u] = *(const u32x4*)(K + (tb + r) * a.qt + c);
+    }
+#pragma unroll
+    for (int u = 0; u < NVP; ++u) {
+      const int e = tid + 256 * u, r = e / (kCB / 8), c = (e % (kCB / 8)) * 8;
+      pv[u] = *(const u32x4*)(V + (tb + r) * a.vt + cj0 + c);
+    }
+    const int64_t o = (int64_t)bh * a.T + tb + lane;
+    pig = a.ig[o];
+    pfg = a.fg[o];
+  };
+  prefetch(0);
+  for (int k = 0; k < a.nc; ++k) {
+    const int64_t t0 = (int64_t)k * kL;
+    // re-derive the lane-dependent addresses every chunk instead of holding dozens of them in
+    // VGPRs across the loop (hoisted, they pushed the prefetch registers out to scratch)
+    asm volatile("" : "+v"(tid), "+v"(lane));
+    const ChunkGates G = chunk_gate_math(pig, pfg, m, a.scale, lane);
+    if (k > 0 && tid < DQ) n = decay * n + np2[tid] + np2[DQ + tid];   // previous chunk's update
+    decay = G.decay;
+    if (!ML_ABL(16)) {
+#pragma unroll
+      for (int u = 0; u < NQP; ++u) {
+        const int e = tid + 256 * u, r = e / (DQ / 8), c = (e % (DQ / 8)) * 8;
+        *(u32x4*)(Qs + r * LQ + c) = pq[u];
+        *(u32x4*)(Ks + r * LQ + c) = pk[u];
+        const float f = __shfl(G.fs, r);
+        const V8 x = __builtin_bit_cast(V8, pk[u]);
+        V8 y;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) y[j] = (T)((float)x[j] * f);
+        *(V8*)(Kf + r * LQ + c) = y;
+      }
+#pragma unroll
+      for (int u = 0; u < NVP; ++u) {
+        const int e = tid + 256 * u, r = e / (kCB / 8), c = (e % (kCB / 8)) * 8;
+        *(u32x4*)(Vs + r * LC + c) = pv[u];
+      }
+    }
+    if (w == 0) {
+      sb[lane] = G.b;
+      si[lane] = G.i;
+      mts[lane] = G.mt;
+      rowfs[lane] = G.rowf;
+      fsv[lane] = G.fs;
+    }
+    if (k + 1 < a.nc) prefetch(k + 1);
+    // the state at the chunk start: its MFMA image, transposed ([j][i]); a lane's four
+    // accumulator rows are consecutive i, so each tile is one 8-byte LDS store
+#pragma unroll
+    for (int p = 0; p < PW; ++p) {
+      const int q = w + 4 * p, i0 = 16 * (q / TJ), j0 = 16 * (q % TJ);
+      v4t c;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) c[r] = (T)acc[p][r];
+      *(v4t*)(CT + (j0 + (lane & 15)) * LQ + i0 + 4 * (lane >> 4)) = c;
+    }
+    if (tid < DQ) {
+      nk[tid] = n;
+      if (cb == 0) a.ns[((int64_t)bh * (a.nc + 1) + k) * DQ + tid] = n;
+    }
+    if (cb == 0 && tid == 0) a.ms[(int64_t)bh * (a.nc + 1) + k] = m;
+    __syncthreads();
+    // the backward's copy of the chunk-start state: CT's rows as they are, [j][i] (16-byte stores)
+    {
+      T* Cs = (T*)a.Cs + (((int64_t)bh * a.nc + k) * DV + cj0) * DQ;
+      constexpr int NCP = kCB * DQ / 8 / 256;
+      static_assert(NCP * 256 * 8 == kCB * DQ, "state image split");
+#pragma unroll
+      for (int u = 0; u < NCP; ++u) {
+        const int e = tid + 256 * u, j = e / (DQ / 8), c = (e % (DQ / 8)) * 8;
+        if (!ML_ABL(8)) *(u32x4*)(Cs + j * DQ + c) = *(const u32x4*)(CT + j * LQ + c);
+      }
+    }
+    // From here to the state update every wave touches only its own 16 rows of Ms / qn / dsum
+    // (rows 16 w ..): no barrier between the S and H phases.
+    // q_t . n~_k (4 threads per row, DQ / 4 consecutive i each)
+    {
+      constexpr int QP = DQ / 4;
+      const int t = tid >> 2, part = tid & 3;
+      float qa = 0.0f;
+#pragma unroll
+      for (int u = 0; u < QP / 8; ++u) {
+        const V8 x = *(const V8*)(Qs + t * LQ + part * QP + 8 * u);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) qa += (float)x[e] * nk[part * QP + 8 * u + e];
+      }
+      qa = sum4(qa);
+      if (part == 0) qn[t] = qa;
+    }
+    // the row block's Q fragments (S and the inter-chunk term of H)
+    V8 qa[DQ / 32];
+#pragma unroll
+    for (int kk = 0; kk < DQ / 32; ++kk) qa[kk] = frag<V8, T>(Qs, LQ, 16 * w, 32 * kk, lane);
+    // S = Q K^T for row block w, causal column blocks; M = S o W into LDS, row sums
+    {
+      float rs[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+      for (int ct = 0; ct <= w; ++ct) {
+        V8 kb[DQ / 32];
+#pragma unroll
+        for (int kk = 0; kk < DQ / 32; ++kk) kb[kk] = frag<V8, T>(Ks, LQ, 16 * ct, 32 * kk, lane);
+        f32x4 s4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < (ML_ABL(1) ? 0 : DQ / 32); ++kk) s4 = M::mma(qa[kk], kb[kk], s4);
+        const int s = 16 * ct + (lane & 15);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int t = 16 * w + 4 * (lane >> 4) + r;
+          const float mv = (s <= t) ? s4[r] * a.scale * expf(sb[t] - sb[s] + si[s] - mts[t]) : 0.0f;
+          rs[r] += mv;
+          Ms[t * LC + s] = (T)mv;
+        }
+      }
+      // the column blocks right of the diagonal: zero (the H MFMA reads them)
+      for (int ct = w + 1; ct < 4; ++ct) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Ms[(16 * w + 4 * (lane >> 4) + r) * LC + 16 * ct + (lane & 15)] = (T)0.0f;
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float tot = sum16(rs[r]);
+        if ((lane & 15) == 0) dsum[16 * w + 4 * (lane >> 4) + r] = tot;
+      }
+    }
+    // H = M V + rowf (Q C~_k) for row block w, normalised; staged in the wave's own Ms rows
+    // (every cj has read them first) and stored as 16-byte rows
+    {
+      float zi[4], rf[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int t = 16 * w + 4 * (lane >> 4) + r;
+        rf[r] = rowfs[t];
+        const float dn = dsum[t] + rf[r] * qn[t];
+        zi[r] = 1.0f / (fmaxf(fabsf(dn), expf(-mts[t])) + a.eps);
+      }
+      f32x4 hv[TJ];
+#pragma unroll
+      for (int cj = 0; cj < TJ; ++cj) {
+        // both k-steps of M V always (M is zero right of the diagonal block), fragments first
+        V8 ma[2], vb[2], cb2[DQ / 32];
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          ma[kk] = frag<V8, T>(Ms, LC, 16 * w, 32 * kk, lane);
+          vb[kk] = frag_t<V8, T>(Vs, LC, 32 * kk, 16 * cj, lane);
+        }
+#pragma unroll
+        for (int kk = 0; kk < DQ / 32; ++kk) cb2[kk] = frag<V8, T>(CT, LQ, 16 * cj, 32 * kk, lane);
+        f32x4 h4 = {0.f, 0.f, 0.f, 0.f}, e4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < (ML_ABL(2) ? 0 : 2); ++kk) h4 = M::mma(ma[kk], vb[kk], h4);
+#pragma unroll
+        for (int kk = 0; kk < (ML_ABL(2) ? 0 : DQ / 32); ++kk) e4 = M::mma(qa[kk], cb2[kk], e4);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) hv[cj][r] = (h4[r] + rf[r] * e4[r]) * zi[r];
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int cj = 0; cj < TJ; ++cj) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          Ms[(16 * w + 4 * (lane >> 4) + r) * LC + 16 * cj + (lane & 15)] = (T)hv[cj][r];
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {   // 16 rows x 128 bytes = 128 pieces over 64 lanes
+        const int e = lane + 64 * u, t = 16 * w + (e >> 3), c = (e & 7) * 8;
+        if (!ML_ABL(8)) *(u32x4*)(H + (t0 + t) * DV + cj0 + c) = *(const u32x4*)(Ms + t * LC + c);
+      }
+      if (cb == 0 && lane < 16) {   // the wave's own rows
+        const int t = 16 * w + lane;
+        a.mrow[(int64_t)bh * a.T + t0 + t] = mts[t];
+        a.den[(int64_t)bh * a.T + t0 + t] = dsum[t] + rowfs[t] * qn[t];
+      }
+    }
+    // state update: C~ <- decay C~ + Kf^T V[:, block];  n~ <- decay n~ + Kf^T 1
+#pragma unroll
+    for (int p = 0; p < PW; ++p) {
+      const int q = w + 4 * p, i0 = 16 * (q / TJ), j0 = 16 * (q % TJ);
+      f32x4 c = acc[p] * G.decay;
+#pragma unroll
+      for (int kk = 0; kk < (ML_ABL(4) ? 0 : kL / 32); ++kk)
+        c = M::mma(frag_t<V8, T>(Kf, LQ, 32 * kk, i0, lane),
+                   frag_t<V8, T>(Vs, LC, 32 * kk, j0, lane), c);
+      acc[p] = c;
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (tid < 2 * DQ) {   // n~ increment: half sums over s (fp32 weights, bf16 keys)
+      const int i = tid % DQ, s0 = (tid / DQ) * (kL / 2);
+      float sacc = 0.0f;
+#pragma unroll 8
+      for (int s2 = 0; s2 < kL / 2; ++s2) sacc += fsv[s0 + s2] * (float)Ks[(s0 + s2) * LQ + i];
+      np2[tid] = sacc;
+    }
+    m = G.mn;
+    __syncthreads();
+  }
+  // final state: fp32 (the carried segment state) + n~, m
+#pragma unroll
+  for (int p = 0; p < PW; ++p) {
+    const int q = w + 4 * p, i0 = 16 * (q / TJ), j0 = cj0 + 16 * (q % TJ);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      a.c_last[((int64_t)bh * DQ + i0 + 4 * (lane >> 4) + r) * DV + j0 + (lane & 15)] = acc[p][r];
+  }
+  if (tid < DQ) n = decay * n + np2[tid] + np2[DQ + tid];
+  if (cb == 0) {
+    if (tid < DQ) a.ns[((int64_t)bh * (a.nc + 1) + a.nc) * DQ + tid] = n;
+    if (tid == 0) a.ms[(int64_t)bh * (a.nc + 1) + a.nc] = m;
+  }
+}
+
+// ------------------------------------------------------------------------- backward: walk ----
+// One 8-wave workgroup per sequence (b,h) walks the chunks in REVERSE with the state gradient
+// dC~ [DQ][DV] (fp32) in MFMA accumulators, and per chunk computes all three input gradients:
+//   dq_t = sum_s dA_ts k_s + rowf_t (dnum_t C~_k^T + dden_t n~_k)
+//   dk_s = sum_t dA_ts q_t + es_s (v_s dC~_{k+1}^T + dn~_{k+1})
+//   dv_s = sum_t A_ts dnum_t + es_s k_s dC~_{k+1}
+//   dC~_k = decay dC~_{k+1} + (rowf q)^T dnum,   dn~_k = decay dn~_{k+1} + sum_t rowf_t dden_t q_t
+// (dA_ts = W_ts (dnum_t . v_s + dden_t), A_ts = W_ts q_t . k_s, W_ts = s e^{b_t - b_s + i_s - m_t},
+// s <= t).  Every operand lives in LDS once, row-major as loaded; MFMA fragments that run along
+// a column come out through transposed reads.  The per-row weights rowf / es scale the
+// accumulators (a second accumulator per job for the weighted term); the one per-k weight,
+// rowf in the state update, is folded into a scaled copy Qr = diag(rowf) Q written with the fill.
+// C~_k is the forward's compute-dtype image; dC~_{k+1}'s image replaces it in LDS once the dq
+// terms are done.  Nothing of size T x DQ x DV goes to HBM: the chunk states of the gradient stay
+// on chip (the gradient w.r.t. the initial state is the only state output).
+// f16 range: dh of a trained-from-scratch model sits far below f16's normal range (~1e-6 against
+// 6e-5), where its images would keep 3-4 significant bits.  The f16 walk therefore scales each
+// chunk by a power of two S_k = 2^-e with max |dh| S_k in [0.5, 1) (dnum, dden, dA and the dC~
+// image all carry S_k; the fp32 dC~ / dn~ carry is rescaled exactly when S changes) and divides
+// every output by S_k.  bf16 has the exponent range of fp32 and runs unscaled.
 template <int DT, int DQ, int DV>
 __global__ void __launch_bounds__(512, 1) mlstm_bw_walk(MArgs a) {
   using M = MF<DT>;
   using T = typename M::T;
   using V8 = typename M::v8;
+  typedef T v4t __attribute__((ext_vector_type(4)));
+  constexpr bool kScale = DT == SC_F16;
   constexpr int LQ = DQ + kPad, LV = DV + kPad, LL = kL + kPad;
   constexpr int NI = DQ / 16, NJ = DV / 16;       // tile counts along DQ, DV
   constexpr int NC = NI * NJ;                     // state tiles
@@ -501,6 +564,7 @@ __global__ void __launch_bounds__(512, 1) mlstm_bw_walk(MArgs a) {
   const int bh = blockIdx.x, w = threadIdx.x >> 6;
   int tid = threadIdx.x, lane = tid & 63;
   __shared__ __attribute__((aligned(16))) T Qs[kL * LQ];
+  __shared__ __attribute__((aligned(16))) T Qr[kL * LQ];   // diag(rowf) Q
   __shared__ __attribute__((aligned(16))) T Ks[kL * LQ];
   __shared__ __attribute__((aligned(16))) T Vs[kL * LV];
   __shared__ __attribute__((aligned(16))) T Dn[kL * LV];
@@ -508,7 +572,7 @@ __global__ void __launch_bounds__(512, 1) mlstm_bw_walk(MArgs a) {
   __shared__ __attribute__((aligned(16))) T dA[kL * LL];
   __shared__ __attribute__((aligned(16))) T Am[kL * LL];
   __shared__ float sb[kL], si[kL], mt[kL], rowf[kL], es[kL], dden[kL], nk[DQ], dnk[DQ];
-  __shared__ float qpart[NI * kL], kpart[NI * kL], scal[1];
+  __shared__ float qpart[NI * kL], kpart[NI * kL], dnp[4 * DQ], smax[16];
   // dC~ tiles q = w + 8 p: rows i0 = 16 (q / NJ), cols j0 = 16 (q % NJ)
   f32x4 acc[PC];
 #pragma unroll
@@ -521,6 +585,7 @@ __global__ void __launch_bounds__(512, 1) mlstm_bw_walk(MArgs a) {
     }
   }
   float dn = (tid < DQ && a.dnT) ? a.dnT[(int64_t)bh * DQ + tid] : 0.0f;
+  float S = 1.0f, decay = 1.0f;   // S: the current chunk's gradient scale (f16)
   const T* Qg = (const T*)a.q + qrow(a, bh, 0);
   const T* Kg = (const T*)a.k + qrow(a, bh, 0);
   const T* Vg = (const T*)a.v + vrow(a, bh, 0);
@@ -530,65 +595,147 @@ __global__ void __launch_bounds__(512, 1) mlstm_bw_walk(MArgs a) {
   for (int k = a.nc - 1; k >= 0; --k) {
     const int64_t t0 = (int64_t)k * kL;
     asm volatile("" : "+v"(tid), "+v"(lane));   // see mlstm_fw_walk
+    // dn~_{k+1}: the previous chunk's four partial sums (after its closing barrier)
+    if (k < a.nc - 1 && tid < DQ)
+      dn = decay * dn + dnp[tid] + dnp[DQ + tid] + dnp[2 * DQ + tid] + dnp[3 * DQ + tid];
     // ---- chunk inputs: every global load of the chunk issued before any LDS store (one
     // memory latency per chunk, not one per operand) ----
-    {
-      constexpr int NQ8 = kL * DQ / 8, NV8 = kL * DV / 8, NC8 = DQ * DV / 8;
-      constexpr int UQ = (NQ8 + 511) / 512, UV = (NV8 + 511) / 512, UC = (NC8 + 511) / 512;
-      constexpr int UH = DV / 64;   // dh / h pieces per thread (8 threads per row)
-      u32x4 rq[UQ], rk[UQ], rv[UV], rc[UC], rd[UH], rh[UH];
-      const T* Ck = (const T*)a.Cs + ((int64_t)bh * a.nc + k) * DQ * DV;
-      const int t = tid >> 3, part = tid & 7;
-      const int64_t ro = (int64_t)bh * a.T + t0 + t;
-      const T* dh = (const T*)a.dh + ro * DV;
-      const T* h = (const T*)a.h + ro * DV;
+    constexpr int NQ8 = kL * DQ / 8, NV8 = kL * DV / 8, NC8 = DQ * DV / 8;
+    constexpr int UQ = (NQ8 + 511) / 512, UV = (NV8 + 511) / 512, UC = (NC8 + 511) / 512;
+    constexpr int UH = DV / 64;   // dh / h pieces per thread (8 threads per row)
+    u32x4 rq[UQ] = {}, rk[UQ] = {}, rv[UV] = {}, rc[UC] = {}, rd[UH] = {}, rh[UH] = {};
+    const T* Ck = (const T*)a.Cs + ((int64_t)bh * a.nc + k) * DQ * DV;
+    const int t = tid >> 3, part = tid & 7;
+    const int64_t ro = (int64_t)bh * a.T + t0 + t;
+    const T* dh = (const T*)a.dh + ro * DV;
+    const T* h = (const T*)a.h + ro * DV;
+    const int64_t st = (int64_t)bh * (a.nc + 1) + k;
+    const float mk = a.ms[st], mk1 = a.ms[st + 1];
+    const int64_t og = (int64_t)bh * a.T + t0 + lane;
+    const float g_i = a.ig[og], g_f = a.fg[og], g_m = a.mrow[og];
+    const float n_k = tid < DQ ? a.ns[st * DQ + tid] : 0.0f;
 #pragma unroll
-      for (int u = 0; u < UQ; ++u) {
-        const int e = tid + 512 * u, r = e / (DQ / 8), c = (e % (DQ / 8)) * 8;
-        if (e < NQ8) {
-          rq[u] = *(const u32x4*)(Qg + (t0 + r) * a.qt + c);
-          rk[u] = *(const u32x4*)(Kg + (t0 + r) * a.qt + c);
-        }
+    for (int u = 0; u < UQ; ++u) {
+      const int e = tid + 512 * u, r = e / (DQ / 8), c = (e % (DQ / 8)) * 8;
+      if (e < NQ8 && !ML_ABL(512)) {
+        rq[u] = *(const u32x4*)(Qg + (t0 + r) * a.qt + c);
+        rk[u] = *(const u32x4*)(Kg + (t0 + r) * a.qt + c);
       }
+    }
 #pragma unroll
-      for (int u = 0; u < UV; ++u) {
-        const int e = tid + 512 * u, r = e / (DV / 8), c = (e % (DV / 8)) * 8;
-        if (e < NV8) rv[u] = *(const u32x4*)(Vg + (t0 + r) * a.vt + c);
-      }
+    for (int u = 0; u < UV; ++u) {
+      const int e = tid + 512 * u, r = e / (DV / 8), c = (e % (DV / 8)) * 8;
+      if (e < NV8 && !ML_ABL(512)) rv[u] = *(const u32x4*)(Vg + (t0 + r) * a.vt + c);
+    }
 #pragma unroll
-      for (int u = 0; u < UC; ++u) {
-        const int e = tid + 512 * u;
-        if (e < NC8) rc[u] = *(const u32x4*)(Ck + 8 * e);
-      }
+    for (int u = 0; u < UC; ++u) {
+      const int e = tid + 512 * u;
+      if (e < NC8 && !ML_ABL(512)) rc[u] = *(const u32x4*)(Ck + 8 * e);
+    }
 #pragma unroll
-      for (int u = 0; u < UH; ++u) {
+    for (int u = 0; u < UH; ++u) {
+      if (!ML_ABL(512)) {
         rd[u] = *(const u32x4*)(dh + part * 8 + 64 * u);
         rh[u] = *(const u32x4*)(h + part * 8 + 64 * u);
       }
-      const float m_t = a.mrow[ro], dv_ = a.den[ro];
+    }
+    const float m_t = a.mrow[ro], dv_ = a.den[ro];
+    // gate quantities (every wave, lane = step)
+    const float b = wave_prefix_sum(logsig(g_f), lane);
+    const float g = rdlane(b, 63);
+    const float rowf_l = a.scale * expf(b + mk - g_m);
+    decay = expf(g + mk - mk1);
+    if (w == 0) {
+      sb[lane] = b;
+      si[lane] = g_i;
+      rowf[lane] = rowf_l;
+      es[lane] = expf(g - b + g_i - mk1);
+    }
 #pragma unroll
-      for (int u = 0; u < UQ; ++u) {
-        const int e = tid + 512 * u, r = e / (DQ / 8), c = (e % (DQ / 8)) * 8;
-        if (e < NQ8) {
-          *(u32x4*)(Qs + r * LQ + c) = rq[u];
-          *(u32x4*)(Ks + r * LQ + c) = rk[u];
-        }
-      }
+    for (int u = 0; u < UQ; ++u) {
+      const int e = tid + 512 * u, r = e / (DQ / 8), c = (e % (DQ / 8)) * 8;
+      const float f = __shfl(rowf_l, r & 63);
+      if (e < NQ8) {
+        *(u32x4*)(Qs + r * LQ + c) = rq[u];
+        *(u32x4*)(Ks + r * LQ + c) = rk[u];
+        const V8 x = __builtin_bit_cast(V8, rq[u]);
+        V8 y;
 #pragma unroll
-      for (int u = 0; u < UV; ++u) {
-        const int e = tid + 512 * u, r = e / (DV / 8), c = (e % (DV / 8)) * 8;
-        if (e < NV8) *(u32x4*)(Vs + r * LV + c) = rv[u];
+        for (int j = 0; j < 8; ++j) y[j] = (T)((float)x[j] * f);
+        *(V8*)(Qr + r * LQ + c) = y;
       }
+    }
 #pragma unroll
-      for (int u = 0; u < UC; ++u) {
-        const int e = tid + 512 * u;
-        if (e < NC8) {
-          const int j = (8 * e) / DQ, i = (8 * e) % DQ;
-          *(u32x4*)(CS + j * LQ + i) = rc[u];
-        }
+    for (int u = 0; u < UV; ++u) {
+      const int e = tid + 512 * u, r = e / (DV / 8), c = (e % (DV / 8)) * 8;
+      if (e < NV8) *(u32x4*)(Vs + r * LV + c) = rv[u];
+    }
+#pragma unroll
+    for (int u = 0; u < UC; ++u) {
+      const int e = tid + 512 * u;
+      if (e < NC8) {
+        const int j = (8 * e) / DQ, i = (8 * e) % DQ;
+        *(u32x4*)(CS + j * LQ + i) = rc[u];
       }
-      // dnum = dh / z and dden (8 threads per row)
-      const float z = fmaxf(fabsf(dv_), expf(-m_t)) + a.eps;
+    }
+    if (tid < DQ) {
+      nk[tid] = n_k;
+    }
+    const float z = fmaxf(fabsf(dv_), expf(-m_t)) + a.eps;
+    // the chunk's gradient scale (f16): dnum = dh / z to [0.5, 1) and the carried dC~ below 2^10
+    // (z can be ~1e-6, so it is dnum, not dh, that must fit)
+    float Sk = 1.0f;
+    if constexpr (kScale) {
+      float mx = 0.0f, mc = 0.0f;
+#pragma unroll
+      for (int u = 0; u < UH; ++u) {
+        const V8 xd = __builtin_bit_cast(V8, rd[u]);
+#pragma unroll
+        for (int e2 = 0; e2 < 8; ++e2) mx = fmaxf(mx, fabsf((float)xd[e2]));
+      }
+      mx /= z;
+#pragma unroll
+      for (int p = 0; p < PC; ++p)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) mc = fmaxf(mc, fabsf(acc[p][r]));
+      mx = wave_max(mx);
+      mc = wave_max(mc);
+      if (lane == 0) {
+        smax[w] = mx;
+        smax[8 + w] = mc;
+      }
+      __syncthreads();
+      mx = smax[0];
+      mc = smax[8];
+#pragma unroll
+      for (int v = 1; v < 8; ++v) {
+        mx = fmaxf(mx, smax[v]);
+        mc = fmaxf(mc, smax[8 + v]);
+      }
+      mc /= S;   // in true units
+      float s1 = 3.0e38f, s2 = 3.0e38f;
+      int ex;
+      if (mx > 0.0f && mx < 3.0e38f) {
+        frexpf(mx, &ex);
+        s1 = ldexpf(1.0f, -ex);
+      }
+      if (mc > 0.0f && mc < 3.0e38f) {
+        frexpf(mc, &ex);
+        s2 = ldexpf(1.0f, 10 - ex);
+      }
+      Sk = fminf(s1, s2);
+      if (!(Sk < 3.0e38f)) Sk = S;   // nothing to scale by: keep the previous chunk's
+      // the carried gradients move to this chunk's scale (powers of two: exact)
+      const float rs = Sk / S;
+#pragma unroll
+      for (int p = 0; p < PC; ++p) acc[p] *= rs;
+      dn *= rs;
+      S = Sk;
+    }
+    if (tid < DQ) dnk[tid] = dn;
+    // dnum = dh S / z and dden S (8 threads per row)
+    {
+      const float zs = Sk / z;
       float dot = 0.0f;
 #pragma unroll
       for (int u = 0; u < UH; ++u) {
@@ -599,37 +746,21 @@ __global__ void __launch_bounds__(512, 1) mlstm_bw_walk(MArgs a) {
         for (int e2 = 0; e2 < 8; ++e2) {
           const float d = (float)xd[e2];
           dot += d * (float)xh[e2];
-          o[e2] = (T)(d / z);
+          o[e2] = (T)(d * zs);
         }
         *(V8*)(Dn + t * LV + part * 8 + 64 * u) = o;
       }
-      dot += __shfl_xor(dot, 1);
-      dot += __shfl_xor(dot, 2);
-      dot += __shfl_xor(dot, 4);
+      dot = sum8(dot);
       if (part == 0) {
         const float live = fabsf(dv_) >= expf(-m_t) ? 1.0f : 0.0f;
-        dden[t] = -dot / z * (dv_ >= 0.0f ? 1.0f : -1.0f) * live;
+        dden[t] = -dot * zs * (dv_ >= 0.0f ? 1.0f : -1.0f) * live;
         mt[t] = m_t;
       }
-    }
-    if (tid < DQ) {
-      nk[tid] = a.ns[((int64_t)bh * (a.nc + 1) + k) * DQ + tid];
-      dnk[tid] = dn;
-    }
-    chunk_gates(a, bh, k, sb, si, tid);
-    if (tid < 64) {   // wave 0 wrote sb / si; mt comes from the row threads (a barrier below)
-      const int64_t st = (int64_t)bh * (a.nc + 1) + k;
-      const float mk = a.ms[st], mk1 = a.ms[st + 1];
-      const float g = __shfl(sb[tid], 63);
-      const float m_t = a.mrow[(int64_t)bh * a.T + t0 + tid];
-      rowf[tid] = a.scale * expf(sb[tid] + mk - m_t);
-      es[tid] = expf(g - sb[tid] + si[tid] - mk1);
-      if (tid == 0) scal[0] = expf(g + mk - mk1);
     }
     __syncthreads();
     // ---- A = W o (Q K^T) and dA = W o (Dn V^T + dden): 10 causal tiles each, 20 jobs ----
 #pragma unroll 1
-    for (int jb = w; jb < 20; jb += 8) {
+    for (int jb = w; jb < (ML_ABL(32) ? 0 : 20); jb += 8) {
       const bool isA = jb < 10;
       const int idx = isA ? jb : jb - 10;
       // idx -> (tr, tc), tc <= tr: 0 (0,0) 1 (1,0) 2 (1,1) 3 (2,0) 4 (2,1) 5 (2,2) 6.. (3,*)
@@ -637,57 +768,76 @@ __global__ void __launch_bounds__(512, 1) mlstm_bw_walk(MArgs a) {
       const int tc = idx - tr * (tr + 1) / 2;
       f32x4 c4 = {0.f, 0.f, 0.f, 0.f};
       if (isA) {
+        V8 fa[DQ / 32], fb[DQ / 32];
 #pragma unroll
-        for (int kk = 0; kk < DQ / 32; ++kk)
-          c4 = M::mma(frag<V8, T>(Qs, LQ, 16 * tr, 32 * kk, lane),
-                      frag<V8, T>(Ks, LQ, 16 * tc, 32 * kk, lane), c4);
+        for (int kk = 0; kk < DQ / 32; ++kk) {
+          fa[kk] = frag<V8, T>(Qs, LQ, 16 * tr, 32 * kk, lane);
+          fb[kk] = frag<V8, T>(Ks, LQ, 16 * tc, 32 * kk, lane);
+        }
+#pragma unroll
+        for (int kk = 0; kk < DQ / 32; ++kk) c4 = M::mma(fa[kk], fb[kk], c4);
       } else {
+        V8 fa[DV / 32], fb[DV / 32];
 #pragma unroll
-        for (int kk = 0; kk < DV / 32; ++kk)
-          c4 = M::mma(frag<V8, T>(Dn, LV, 16 * tr, 32 * kk, lane),
-                      frag<V8, T>(Vs, LV, 16 * tc, 32 * kk, lane), c4);
+        for (int kk = 0; kk < DV / 32; ++kk) {
+          fa[kk] = frag<V8, T>(Dn, LV, 16 * tr, 32 * kk, lane);
+          fb[kk] = frag<V8, T>(Vs, LV, 16 * tc, 32 * kk, lane);
+        }
+#pragma unroll
+        for (int kk = 0; kk < DV / 32; ++kk) c4 = M::mma(fa[kk], fb[kk], c4);
       }
       const int s = 16 * tc + (lane & 15);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int t = 16 * tr + 4 * (lane >> 4) + r;
-        const float wts = (s <= t) ? a.scale * expf(sb[t] - sb[s] + si[s] - mt[t]) : 0.0f;
-        if (isA) Am[t * LL + s] = (T)(c4[r] * wts);
-        else dA[t * LL + s] = (T)((c4[r] + dden[t]) * wts);
+        const int tt = 16 * tr + 4 * (lane >> 4) + r;
+        const float wts = (s <= tt) ? a.scale * expf(sb[tt] - sb[s] + si[s] - mt[tt]) : 0.0f;
+        if (isA) Am[tt * LL + s] = (T)(c4[r] * wts);
+        else dA[tt * LL + s] = (T)((c4[r] + dden[tt]) * wts);
       }
     }
     // zero the strictly upper tiles (tc > tr) of A and dA once (they stay zero across chunks)
     if (k == a.nc - 1) {
       for (int e = tid; e < kL * kL; e += 512) {
-        const int t = e / kL, s = e % kL;
-        if ((s >> 4) > (t >> 4)) {
-          Am[t * LL + s] = (T)0.0f;
-          dA[t * LL + s] = (T)0.0f;
+        const int tt = e / kL, s = e % kL;
+        if ((s >> 4) > (tt >> 4)) {
+          Am[tt * LL + s] = (T)0.0f;
+          dA[tt * LL + s] = (T)0.0f;
         }
       }
     }
     __syncthreads();
-    // ---- dq = dA K + rowf (Dn C~_k^T) + rowf dden n~_k: 4 x NI tiles ----
+    const float inv = 1.0f / S;
+    // ---- dq = dA K + rowf (Dn C~_k^T + dden n~_k): 4 x NI tiles ----
 #pragma unroll 1
-    for (int jb = w; jb < 4 * NI; jb += 8) {
+    for (int jb = w; jb < (ML_ABL(64) ? 0 : 4 * NI); jb += 8) {
       const int tr = jb / NI, ci = jb % NI;
-      f32x4 d4 = {0.f, 0.f, 0.f, 0.f};
-      for (int kk = 0; kk <= (16 * tr + 15) / 32; ++kk)   // causal: s <= t
-        d4 = M::mma(frag<V8, T>(dA, LL, 16 * tr, 32 * kk, lane),
-                    frag_t<V8, T>(Ks, LQ, 32 * kk, 16 * ci, lane), d4);
-      const float rf = rowf[16 * tr + (lane & 15)];
+      // every fragment of the job is read before its first MFMA (the two causal k-steps always:
+      // dA's tiles above the diagonal are zero), so the LDS latency is paid once per job
+      V8 fa[2], fb[2], ga[DV / 32], gb[DV / 32];
 #pragma unroll
-      for (int kk = 0; kk < DV / 32; ++kk)
-        d4 = M::mma(frag_rs<V8, T>(Dn, LV, 16 * tr, 32 * kk, lane, rf),
-                    frag_t<V8, T>(CS, LQ, 32 * kk, 16 * ci, lane), d4);
+      for (int kk = 0; kk < 2; ++kk) {
+        fa[kk] = frag<V8, T>(dA, LL, 16 * tr, 32 * kk, lane);
+        fb[kk] = frag_t<V8, T>(Ks, LQ, 32 * kk, 16 * ci, lane);
+      }
+#pragma unroll
+      for (int kk = 0; kk < DV / 32; ++kk) {
+        ga[kk] = frag<V8, T>(Dn, LV, 16 * tr, 32 * kk, lane);
+        gb[kk] = frag_t<V8, T>(CS, LQ, 32 * kk, 16 * ci, lane);
+      }
+      f32x4 d4 = {0.f, 0.f, 0.f, 0.f}, e4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) d4 = M::mma(fa[kk], fb[kk], d4);
+#pragma unroll
+      for (int kk = 0; kk < DV / 32; ++kk) e4 = M::mma(ga[kk], gb[kk], e4);
       const int i = 16 * ci + (lane & 15);
+      const float nki = nk[i];
       float qd[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int t = 16 * tr + 4 * (lane >> 4) + r;
-        const float v = d4[r] + rowf[t] * dden[t] * nk[i];
-        dQg[(t0 + t) * a.qt + i] = (T)v;
-        qd[r] = sum16(v * (float)Qs[t * LQ + i]);
+        const int tt = 16 * tr + 4 * (lane >> 4) + r;
+        const float v = d4[r] + rowf[tt] * (e4[r] + dden[tt] * nki);
+        dQg[(t0 + tt) * a.qt + i] = (T)(v * inv);
+        qd[r] = sum16(v * (float)Qs[tt * LQ + i]);
       }
       if ((lane & 15) == 0) {
 #pragma unroll
@@ -699,40 +849,47 @@ __global__ void __launch_bounds__(512, 1) mlstm_bw_walk(MArgs a) {
 #pragma unroll
     for (int p = 0; p < PC; ++p) {
       const int q = w + 8 * p, i0 = 16 * (q / NJ), j0 = 16 * (q % NJ);
-      typedef T v4 __attribute__((ext_vector_type(4)));
-      v4 c;
+      v4t c;
 #pragma unroll
       for (int r = 0; r < 4; ++r) c[r] = (T)acc[p][r];
-      *(v4*)(CS + (j0 + (lane & 15)) * LQ + i0 + 4 * (lane >> 4)) = c;
+      *(v4t*)(CS + (j0 + (lane & 15)) * LQ + i0 + 4 * (lane >> 4)) = c;
     }
     if (tid < kL) {
       float sq = 0.0f;
 #pragma unroll
       for (int ci = 0; ci < NI; ++ci) sq += qpart[ci * kL + tid];
-      a.qdq[(int64_t)bh * a.T + t0 + tid] = sq;
+      a.qdq[(int64_t)bh * a.T + t0 + tid] = sq * inv;
     }
     __syncthreads();
-    // ---- dk = dA^T Q + es (V dC~^T) + es dn~: 4 x NI tiles; dv = A^T Dn + es (K dC~): 4 x NJ ----
+    // ---- dk = dA^T Q + es (V dC~^T + dn~): 4 x NI tiles; dv = A^T Dn + es (K dC~): 4 x NJ ----
 #pragma unroll 1
-    for (int jb = w; jb < 4 * NI + 4 * NJ; jb += 8) {
-      f32x4 d4 = {0.f, 0.f, 0.f, 0.f};
+    for (int jb = w; jb < (ML_ABL(128) ? 0 : 4 * NI + 4 * NJ); jb += 8) {
+      f32x4 d4 = {0.f, 0.f, 0.f, 0.f}, e4 = {0.f, 0.f, 0.f, 0.f};
       if (jb < 4 * NI) {
         const int sr = jb / NI, ci = jb % NI;
-        for (int kk = (16 * sr) / 32; kk < kL / 32; ++kk)   // causal: t >= s
-          d4 = M::mma(frag_t<V8, T>(dA, LL, 32 * kk, 16 * sr, lane),
-                      frag_t<V8, T>(Qs, LQ, 32 * kk, 16 * ci, lane), d4);
-        const float ef = es[16 * sr + (lane & 15)];
+        V8 fa[2], fb[2], ga[DV / 32], gb[DV / 32];   // (as the dq job)
 #pragma unroll
-        for (int kk = 0; kk < DV / 32; ++kk)
-          d4 = M::mma(frag_rs<V8, T>(Vs, LV, 16 * sr, 32 * kk, lane, ef),
-                      frag_t<V8, T>(CS, LQ, 32 * kk, 16 * ci, lane), d4);
+        for (int kk = 0; kk < 2; ++kk) {
+          fa[kk] = frag_t<V8, T>(dA, LL, 32 * kk, 16 * sr, lane);
+          fb[kk] = frag_t<V8, T>(Qs, LQ, 32 * kk, 16 * ci, lane);
+        }
+#pragma unroll
+        for (int kk = 0; kk < DV / 32; ++kk) {
+          ga[kk] = frag<V8, T>(Vs, LV, 16 * sr, 32 * kk, lane);
+          gb[kk] = frag_t<V8, T>(CS, LQ, 32 * kk, 16 * ci, lane);
+        }
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) d4 = M::mma(fa[kk], fb[kk], d4);
+#pragma unroll
+        for (int kk = 0; kk < DV / 32; ++kk) e4 = M::mma(ga[kk], gb[kk], e4);
         const int i = 16 * ci + (lane & 15);
+        const float dni = dnk[i];
         float kd[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int s = 16 * sr + 4 * (lane >> 4) + r;
-          const float v = d4[r] + es[s] * dnk[i];
-          dKg[(t0 + s) * a.qt + i] = (T)v;
+          const float v = d4[r] + es[s] * (e4[r] + dni);
+          dKg[(t0 + s) * a.qt + i] = (T)(v * inv);
           kd[r] = sum16(v * (float)Ks[s * LQ + i]);
         }
         if ((lane & 15) == 0) {
@@ -741,53 +898,71 @@ __global__ void __launch_bounds__(512, 1) mlstm_bw_walk(MArgs a) {
         }
       } else {
         const int jv = jb - 4 * NI, sr = jv / NJ, cj = jv % NJ;
-        for (int kk = (16 * sr) / 32; kk < kL / 32; ++kk)
-          d4 = M::mma(frag_t<V8, T>(Am, LL, 32 * kk, 16 * sr, lane),
-                      frag_t<V8, T>(Dn, LV, 32 * kk, 16 * cj, lane), d4);
-        const float ef = es[16 * sr + (lane & 15)];
+        V8 fa[2], fb[2], ga[DQ / 32], gb[DQ / 32];
 #pragma unroll
-        for (int kk = 0; kk < DQ / 32; ++kk)
-          d4 = M::mma(frag_rs<V8, T>(Ks, LQ, 16 * sr, 32 * kk, lane, ef),
-                      frag<V8, T>(CS, LQ, 16 * cj, 32 * kk, lane), d4);
+        for (int kk = 0; kk < 2; ++kk) {
+          fa[kk] = frag_t<V8, T>(Am, LL, 32 * kk, 16 * sr, lane);
+          fb[kk] = frag_t<V8, T>(Dn, LV, 32 * kk, 16 * cj, lane);
+        }
+#pragma unroll
+        for (int kk = 0; kk < DQ / 32; ++kk) {
+          ga[kk] = frag<V8, T>(Ks, LQ, 16 * sr, 32 * kk, lane);
+          gb[kk] = frag<V8, T>(CS, LQ, 16 * cj, 32 * kk, lane);
+        }
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) d4 = M::mma(fa[kk], fb[kk], d4);
+#pragma unroll
+        for (int kk = 0; kk < DQ / 32; ++kk) e4 = M::mma(ga[kk], gb[kk], e4);
         const int j = 16 * cj + (lane & 15);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) dVg[(t0 + 16 * sr + 4 * (lane >> 4) + r) * a.vt + j] = (T)d4[r];
+        for (int r = 0; r < 4; ++r) {
+          const int s = 16 * sr + 4 * (lane >> 4) + r;
+          dVg[(t0 + s) * a.vt + j] = (T)((d4[r] + es[s] * e4[r]) * inv);
+        }
       }
     }
-    // ---- state gradient to the chunk start: dC~_k = decay dC~_{k+1} + (rowf Q)^T Dn ----
-    const float decay = scal[0];
+    // ---- state gradient to the chunk start: dC~_k = decay dC~_{k+1} + Qr^T Dn ----
 #pragma unroll
     for (int p = 0; p < PC; ++p) {
       const int q = w + 8 * p, i0 = 16 * (q / NJ), j0 = 16 * (q % NJ);
       f32x4 c = acc[p] * decay;
 #pragma unroll
-      for (int kk = 0; kk < kL / 32; ++kk)
-        c = M::mma(frag_t_ks<V8, T>(Qs, LQ, 32 * kk, i0, lane, rowf),
+      for (int kk = 0; kk < (ML_ABL(256) ? 0 : kL / 32); ++kk)
+        c = M::mma(frag_t<V8, T>(Qr, LQ, 32 * kk, i0, lane),
                    frag_t<V8, T>(Dn, LV, 32 * kk, j0, lane), c);
       acc[p] = c;
+      __builtin_amdgcn_sched_barrier(0);
     }
-    if (tid < DQ) {
+    // dn~ partial sums sum_t dden_t Qr[t][i] over four 16-step quarters (combined next chunk)
+    if (tid < 4 * DQ) {
+      const int i = tid % DQ, qt4 = tid / DQ;
       float sacc = 0.0f;
-      for (int t = 0; t < kL; ++t) sacc += rowf[t] * dden[t] * (float)Qs[t * LQ + tid];
-      dn = decay * dn + sacc;
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int tt = 16 * qt4 + u;
+        sacc += dden[tt] * (float)Qr[tt * LQ + i];
+      }
+      dnp[qt4 * DQ + i] = sacc;
     }
     __syncthreads();
-    if (tid < kL) {
+    if (tid < kL) {   // (kpart comes from every wave's dk jobs: after the barrier)
       float sk = 0.0f;
 #pragma unroll
       for (int ci = 0; ci < NI; ++ci) sk += kpart[ci * kL + tid];
-      a.kdk[(int64_t)bh * a.T + t0 + tid] = sk;
+      a.kdk[(int64_t)bh * a.T + t0 + tid] = sk * inv;
     }
   }
-  // gradient w.r.t. the initial state
+  // gradient w.r.t. the initial state (unscaled)
+  if (tid < DQ) dn = decay * dn + dnp[tid] + dnp[DQ + tid] + dnp[2 * DQ + tid] + dnp[3 * DQ + tid];
+  const float inv = 1.0f / S;
 #pragma unroll
   for (int p = 0; p < PC; ++p) {
     const int q = w + 8 * p, i0 = 16 * (q / NJ), j0 = 16 * (q % NJ);
 #pragma unroll
     for (int r = 0; r < 4; ++r)
-      a.dCs[((int64_t)bh * DQ + i0 + 4 * (lane >> 4) + r) * DV + j0 + (lane & 15)] = acc[p][r];
+      a.dCs[((int64_t)bh * DQ + i0 + 4 * (lane >> 4) + r) * DV + j0 + (lane & 15)] = acc[p][r] * inv;
   }
-  if (tid < DQ) a.dns[(int64_t)bh * DQ + tid] = dn;
+  if (tid < DQ) a.dns[(int64_t)bh * DQ + tid] = dn * inv;
 }
 
 template <int DT, int DQ, int DV>

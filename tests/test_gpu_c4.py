@@ -104,26 +104,94 @@ def test_c4_training_step_finite_and_deterministic(kernel_dtype):
             assert torch.isfinite(a).all() and torch.equal(a, b)
 
 
+# the parameters between the last mLSTM cell and the loss
+ABOVE_LAST_CELL = ("encoder.blocks.11.mlstm_layer.out_proj.", "encoder.blocks.11.ffn.",
+                   "encoder.blocks.11.mlstm_layer.multihead_norm.",
+                   "encoder.blocks.11.norm_ffn.", "encoder.out_norm.", "encoder.lm_head.")
+
+
 def test_c4_fp16_cell_consistent_with_bf16_cell():
-    """The reference's fp16 cell against the bf16 cell on identical weights and batch: the two
-    differ only in the rounding of the cell's q / k / v and intermediate tiles (fp16 keeps 3
-    more mantissa bits), i.e. by the bf16 cell's own rounding noise.  Bounds: loss to 1e-3
-    relative (measured 2.1e-4), every gradient tensor cosine >= 0.88 and norm within 5%
-    (measured worst: block 11's q weight, cosine 0.901, ratio 0.973; the 2-block slice test
-    shows transformers' own bf16 run 12% (Frobenius) from fp64 on the q-weight gradient)."""
+    """The reference's fp16 cell against the bf16 cell on identical weights and batch.  Loss to
+    1e-3 relative (measured 9e-5); every gradient finite; the gradients of the parameters above
+    the last cell (block 11's out_proj and FFN, the output norm, lm_head) cosine >= 0.95 and norm
+    within 5%.  Deeper gradients are not compared: at this initialisation the encoder's backward
+    amplifies rounding -- the per-block gradient norm grows ~20x from block 11 to block 0 --
+    so that transformers' own bf16 composition is 50-110% (Frobenius) away from its fp64 run on
+    the q / k / out_proj weight gradients of blocks 0-10, as are both of our cells
+    (tools/c4_hf_diag.py, profiles/r3_c4_hf_diag.txt).  The cell is pinned per dtype by
+    test_c4_last_cell_gradients_vs_fp64 and the 2-block slice tests."""
     init = {k: v.detach().clone() for k, v in c4_model("bfloat16").state_dict().items()}
     lb, gb, _, _ = one_step("bfloat16", init)
     lh, gh, _, _ = one_step("float16", init)
     print(f"C4 loss bf16 cell {lb:.5f} fp16 cell {lh:.5f}")
     assert abs(lb - lh) <= 1e-3 * abs(lb)
-    worst = (1.0, "")
+    stats = []
     for n in gb:
+        assert torch.isfinite(gh[n]).all() and torch.isfinite(gb[n]).all(), n
+        if not n.startswith(ABOVE_LAST_CELL):
+            continue
         a, b = gb[n].double().flatten(), gh[n].double().flatten()
         cos = float(a @ b / max(float(a.norm() * b.norm()), 1e-300))
         ratio = float(b.norm() / max(float(a.norm()), 1e-300))
-        worst = min(worst, (cos, n))
-        assert cos >= 0.88 and 0.95 <= ratio <= 1.05, (n, cos, ratio)
-    print(f"C4 fp16 vs bf16 cell: worst gradient cosine {worst[0]:.5f} ({worst[1]})")
+        stats.append((cos, ratio, n))
+    assert len(stats) >= 6
+    stats.sort()
+    print("C4 fp16 vs bf16 cell above the last cell: " +
+          "; ".join(f"{n} {c:.4f} (norm ratio {r:.3f})" for c, r, n in stats))
+    for cos, ratio, n in stats:
+        assert cos >= 0.95 and 0.95 <= ratio <= 1.05, (n, cos, ratio)
+
+
+@pytest.mark.parametrize("kernel_dtype", ["bfloat16", "float16"])
+def test_c4_last_cell_gradients_vs_fp64(kernel_dtype):
+    """The last block's mLSTM cell inside the C4 step (B = 2, T = 1536, DQ 96, DV 192, the
+    step's own q / k / v / gates and incoming dh, captured): every input gradient against
+    tests/torch_ref.mlstm64 in fp64 on the same rounded inputs.  dq / dk / dv to 1e-2
+    (relative Frobenius), the per-step input / forget gate gradients to cosine >= 0.999 and
+    5e-2 (the forget gate's is a reverse cumulative sum over the 1536 steps of q.dq - k.dk).
+    fp16 runs with the walk's per-chunk power-of-two gradient scaling (dh ~ 1e-6 here, below
+    f16's normal range)."""
+    from statecatcher_amd import ops, xlstm
+    from tests.torch_ref import mlstm64
+    orig_cell, orig_core = xlstm.mlstm_chunkwise, ops.mlstm_core_supported
+    cap = []
+
+    def capturing_cell(q, k, v, ig, fg, c0, n0, m0, **kw):
+        leaves = [t.detach().clone().requires_grad_(True) for t in (q, k, v, ig, fg)]
+        h, _ = orig_cell(*leaves, c0, n0, m0, **kw)
+        rec = {"in": leaves, "h": h, "state": (c0, n0, m0)}
+        cap.append(rec)
+        h2, st2 = orig_cell(q, k, v, ig, fg, c0, n0, m0, **kw)
+        h2.register_hook(lambda g, rec=rec: rec.__setitem__("dh", g.detach().clone()))
+        return h2, st2
+
+    init = {k: v.detach().clone() for k, v in c4_model(kernel_dtype).state_dict().items()}
+    xlstm.mlstm_chunkwise, ops.mlstm_core_supported = capturing_cell, (lambda *a: False)
+    try:
+        one_step(kernel_dtype, init)
+    finally:
+        xlstm.mlstm_chunkwise, ops.mlstm_core_supported = orig_cell, orig_core
+    rec = cap[-1]
+    assert all(t is None for t in rec["state"])
+    got = torch.autograd.grad(rec["h"], rec["in"], rec["dh"])
+    ref = [t.detach().double().requires_grad_(True) for t in rec["in"]]
+    q = ref[0]
+    B, NH, _, DQ = q.shape
+    z = dict(device=q.device, dtype=torch.float64)
+    rh, _ = mlstm64(*ref, torch.zeros(B, NH, DQ, ref[2].shape[-1], **z),
+                    torch.zeros(B, NH, DQ, **z), torch.zeros(B, NH, 1, **z))
+    (rh * rec["dh"].double()).sum().backward()
+    lines = []
+    for name, g, r in zip(["dq", "dk", "dv", "d igate", "d fgate"], got, ref):
+        gd, rd = g.double(), r.grad
+        rel = float((gd - rd).norm() / max(float(rd.norm()), 1e-300))
+        cos = float((gd * rd).sum() / max(float(gd.norm() * rd.norm()), 1e-300))
+        lines.append(f"{name} rel {rel:.2e} cos {cos:.5f}")
+        if name in ("dq", "dk", "dv"):
+            assert rel <= 1e-2, (name, rel)
+        else:
+            assert cos >= 0.999 and rel <= 5e-2, (name, rel, cos)
+    print(f"C4 last cell ({kernel_dtype}) vs fp64: " + "; ".join(lines))
 
 
 def _hf_slice(blocks, state):
