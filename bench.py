@@ -145,7 +145,8 @@ def build_workload(args, device):
         cfg = build_xlstm_config(args.feat, args.vocab, num_heads=4, num_blocks=12, embedding_dim=768)
         model = ASRModel(None, cfg, vocab_size=args.vocab, feat_dim=args.feat, proj_dim=-1).to(device)
         conf = {"workload": "xLSTM 12x768 (mLSTM, 4 heads) + CTC training step, stateful "
-                            f"{args.segments}-segment carry", "blocks": 12, "embedding_dim": 768}
+                            f"{args.segments}-segment carry", "blocks": 12, "embedding_dim": 768,
+                "mlstm_cell_dtype": cfg.autocast_kernel_dtype}   # float16 as model.py:227
         return model, CTCLoss(blank=0, zero_infinity=True), list(model.parameters()), \
             dict(mode="ctc"), conf
     cfg = build_lucyrnn_config(args.feat, args.hidden, args.layers, args.vocab)

@@ -453,6 +453,26 @@ int sc_mlstm_bwd(const void* q, const void* k, const void* v, int dtype, const f
                  void* dk, void* dv, float* qdq, float* kdk, const int64_t* layout,
                  void* stream);
 
+/*
+ * sc_mlstm_fwd / sc_mlstm_bwd with the operands in another dtype than the cell computes in:
+ * io_dtype is the dtype of q, k, v, h (and dh, dq, dk, dv); dtype the cell's MFMA dtype and the
+ * chunk-state image's.  Supported pairs: (bf16, bf16), (f16, f16), and (f16, bf16) -- the
+ * reference's float16 cell (autocast_kernel_dtype, model.py:227) reading a bf16-autocast
+ * model's projection in place, each operand rounded to f16 on load as .to(float16) would.
+ */
+int sc_mlstm_fwd_io(const void* q, const void* k, const void* v, int dtype, int io_dtype,
+                    const float* igate, const float* fgate, const float* c0, const float* n0,
+                    const float* m0, int BH, int T, int DQ, int DV, float eps, void* h,
+                    void* states_C, float* states_n, float* states_m, float* c_last,
+                    float* m_rows, float* den_rows, const int64_t* layout, void* stream);
+int sc_mlstm_bwd_io(const void* q, const void* k, const void* v, int dtype, int io_dtype,
+                    const float* igate, const float* fgate, const void* h, const void* dh,
+                    const float* dcT, const float* dnT, const void* states_C,
+                    const float* states_n, const float* states_m, const float* m_rows,
+                    const float* den_rows, int BH, int T, int DQ, int DV, float eps,
+                    float* dstates_C, float* dstates_n, void* dq, void* dk, void* dv,
+                    float* qdq, float* kdk, const int64_t* layout, void* stream);
+
 /* ---------------------------------------------------------------- RNN-T ----------------- */
 
 /* Workspace bytes for sc_rnnt_fwd / sc_rnnt_bwd (gathered log-probs, alpha, beta, offsets). */

@@ -65,6 +65,28 @@ template <> struct MF<SC_F16> {
   }
 };
 
+// 8 packed 16-bit elements of dtype IO as the compute type's fragment (a no-op when equal):
+// the f16 cell reads the bf16 projection in place, rounding as a .to(float16) would
+// an fp32 result stored as IO through the compute dtype's rounding first (f16 cell on bf16
+// operands: the value leaves the cell as f16 and is then cast, as the split path's
+// h.to(bfloat16) and autograd's gradient cast do; a no-op round trip when IO == DT)
+template <int DT, int IO>
+__device__ __forceinline__ typename MF<IO>::T out16(float x) {
+  return (typename MF<IO>::T)(float)(typename MF<DT>::T)x;
+}
+template <int DT, int IO>
+__device__ __forceinline__ typename MF<DT>::v8 cvt8(u32x4 x) {
+  if constexpr (DT == IO) {
+    return __builtin_bit_cast(typename MF<DT>::v8, x);
+  } else {
+    const typename MF<IO>::v8 y = __builtin_bit_cast(typename MF<IO>::v8, x);
+    typename MF<DT>::v8 r;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) r[e] = (typename MF<DT>::T)(float)y[e];
+    return r;
+  }
+}
+
 struct MArgs {
   const void* q;   // [BH][T][DQ]
   const void* k;   // [BH][T][DQ]
@@ -268,11 +290,12 @@ __device__ __forceinline__ ChunkGates chunk_gate_math(float ig, float fg, float 
 // column (K^T in the state update, V in M V) come out through transposed reads.  Per-row weights
 // scale the accumulators, per-k weights are folded into one scaled copy Kf = diag(fs) K written
 // with the fill: no VALU work between a fragment read and its MFMA.
-template <int DT, int DQ, int DV>
+template <int DT, int IO, int DQ, int DV>
 __global__ void __launch_bounds__(256, 2) mlstm_fw_walk(MArgs a) {
   using M = MF<DT>;
   using T = typename M::T;
   using V8 = typename M::v8;
+  using TI = typename MF<IO>::T;   // q / k / v / h in HBM
   typedef T v4t __attribute__((ext_vector_type(4)));
   constexpr int LQ = DQ + kPad, LC = kCB + kPad;
   constexpr int TJ = kCB / 16, NI = DQ / 16, NT = NI * TJ, PW = NT / 4;
@@ -342,10 +365,10 @@ __global__ void __launch_bounds__(256, 2) mlstm_fw_walk(MArgs a) {
 #pragma unroll
       for (int u = 0; u < NQP; ++u) {
         const int e = tid + 256 * u, r = e / (DQ / 8), c = (e % (DQ / 8)) * 8;
-        *(u32x4*)(Qs + r * LQ + c) = pq[u];
-        *(u32x4*)(Ks + r * LQ + c) = pk[u];
+        *(V8*)(Qs + r * LQ + c) = cvt8<DT, IO>(pq[u]);
+        const V8 x = cvt8<DT, IO>(pk[u]);
+        *(V8*)(Ks + r * LQ + c) = x;
         const float f = __shfl(G.fs, r);
-        const V8 x = __builtin_bit_cast(V8, pk[u]);
         V8 y;
 #pragma unroll
         for (int j = 0; j < 8; ++j) y[j] = (T)((float)x[j] * f);
@@ -354,7 +377,7 @@ __global__ void __launch_bounds__(256, 2) mlstm_fw_walk(MArgs a) {
 #pragma unroll
       for (int u = 0; u < NVP; ++u) {
         const int e = tid + 256 * u, r = e / (kCB / 8), c = (e % (kCB / 8)) * 8;
-        *(u32x4*)(Vs + r * LC + c) = pv[u];
+        *(V8*)(Vs + r * LC + c) = cvt8<DT, IO>(pv[u]);
       }
     }
     if (w == 0) {
@@ -479,7 +502,7 @@ __global__ void __launch_bounds__(256, 2) mlstm_fw_walk(MArgs a) {
       for (int cj = 0; cj < TJ; ++cj) {
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          Ms[(16 * w + 4 * (lane >> 4) + r) * LC + 16 * cj + (lane & 15)] = (T)hv[cj][r];
+          ((TI*)Ms)[(16 * w + 4 * (lane >> 4) + r) * LC + 16 * cj + (lane & 15)] = out16<DT, IO>(hv[cj][r]);
       }
 #pragma unroll
       for (int u = 0; u < 2; ++u) {   // 16 rows x 128 bytes = 128 pieces over 64 lanes
@@ -549,11 +572,13 @@ __global__ void __launch_bounds__(256, 2) mlstm_fw_walk(MArgs a) {
 // chunk by a power of two S_k = 2^-e with max |dh| S_k in [0.5, 1) (dnum, dden, dA and the dC~
 // image all carry S_k; the fp32 dC~ / dn~ carry is rescaled exactly when S changes) and divides
 // every output by S_k.  bf16 has the exponent range of fp32 and runs unscaled.
-template <int DT, int DQ, int DV>
+template <int DT, int IO, int DQ, int DV>
 __global__ void __launch_bounds__(512, 1) mlstm_bw_walk(MArgs a) {
   using M = MF<DT>;
   using T = typename M::T;
   using V8 = typename M::v8;
+  using TI = typename MF<IO>::T;   // q / k / v / h / dh and the gradients in HBM
+  using V8I = typename MF<IO>::v8;
   typedef T v4t __attribute__((ext_vector_type(4)));
   constexpr bool kScale = DT == SC_F16;
   constexpr int LQ = DQ + kPad, LV = DV + kPad, LL = kL + kPad;
@@ -589,9 +614,9 @@ __global__ void __launch_bounds__(512, 1) mlstm_bw_walk(MArgs a) {
   const T* Qg = (const T*)a.q + qrow(a, bh, 0);
   const T* Kg = (const T*)a.k + qrow(a, bh, 0);
   const T* Vg = (const T*)a.v + vrow(a, bh, 0);
-  T* dQg = (T*)a.dq + qrow(a, bh, 0);
-  T* dKg = (T*)a.dk + qrow(a, bh, 0);
-  T* dVg = (T*)a.dv + vrow(a, bh, 0);
+  TI* dQg = (TI*)a.dq + qrow(a, bh, 0);
+  TI* dKg = (TI*)a.dk + qrow(a, bh, 0);
+  TI* dVg = (TI*)a.dv + vrow(a, bh, 0);
   for (int k = a.nc - 1; k >= 0; --k) {
     const int64_t t0 = (int64_t)k * kL;
     asm volatile("" : "+v"(tid), "+v"(lane));   // see mlstm_fw_walk
@@ -656,9 +681,9 @@ __global__ void __launch_bounds__(512, 1) mlstm_bw_walk(MArgs a) {
       const int e = tid + 512 * u, r = e / (DQ / 8), c = (e % (DQ / 8)) * 8;
       const float f = __shfl(rowf_l, r & 63);
       if (e < NQ8) {
-        *(u32x4*)(Qs + r * LQ + c) = rq[u];
-        *(u32x4*)(Ks + r * LQ + c) = rk[u];
-        const V8 x = __builtin_bit_cast(V8, rq[u]);
+        const V8 x = cvt8<DT, IO>(rq[u]);
+        *(V8*)(Qs + r * LQ + c) = x;
+        *(V8*)(Ks + r * LQ + c) = cvt8<DT, IO>(rk[u]);
         V8 y;
 #pragma unroll
         for (int j = 0; j < 8; ++j) y[j] = (T)((float)x[j] * f);
@@ -668,7 +693,7 @@ __global__ void __launch_bounds__(512, 1) mlstm_bw_walk(MArgs a) {
 #pragma unroll
     for (int u = 0; u < UV; ++u) {
       const int e = tid + 512 * u, r = e / (DV / 8), c = (e % (DV / 8)) * 8;
-      if (e < NV8) *(u32x4*)(Vs + r * LV + c) = rv[u];
+      if (e < NV8) *(V8*)(Vs + r * LV + c) = cvt8<DT, IO>(rv[u]);
     }
 #pragma unroll
     for (int u = 0; u < UC; ++u) {
@@ -689,7 +714,7 @@ __global__ void __launch_bounds__(512, 1) mlstm_bw_walk(MArgs a) {
       float mx = 0.0f, mc = 0.0f;
 #pragma unroll
       for (int u = 0; u < UH; ++u) {
-        const V8 xd = __builtin_bit_cast(V8, rd[u]);
+        const V8I xd = __builtin_bit_cast(V8I, rd[u]);
 #pragma unroll
         for (int e2 = 0; e2 < 8; ++e2) mx = fmaxf(mx, fabsf((float)xd[e2]));
       }
@@ -739,8 +764,8 @@ __global__ void __launch_bounds__(512, 1) mlstm_bw_walk(MArgs a) {
       float dot = 0.0f;
 #pragma unroll
       for (int u = 0; u < UH; ++u) {
-        const V8 xd = __builtin_bit_cast(V8, rd[u]);
-        const V8 xh = __builtin_bit_cast(V8, rh[u]);
+        const V8I xd = __builtin_bit_cast(V8I, rd[u]);
+        const V8I xh = __builtin_bit_cast(V8I, rh[u]);
         V8 o;
 #pragma unroll
         for (int e2 = 0; e2 < 8; ++e2) {
@@ -836,7 +861,7 @@ __global__ void __launch_bounds__(512, 1) mlstm_bw_walk(MArgs a) {
       for (int r = 0; r < 4; ++r) {
         const int tt = 16 * tr + 4 * (lane >> 4) + r;
         const float v = d4[r] + rowf[tt] * (e4[r] + dden[tt] * nki);
-        dQg[(t0 + tt) * a.qt + i] = (T)(v * inv);
+        dQg[(t0 + tt) * a.qt + i] = out16<DT, IO>(v * inv);
         qd[r] = sum16(v * (float)Qs[tt * LQ + i]);
       }
       if ((lane & 15) == 0) {
@@ -889,7 +914,7 @@ __global__ void __launch_bounds__(512, 1) mlstm_bw_walk(MArgs a) {
         for (int r = 0; r < 4; ++r) {
           const int s = 16 * sr + 4 * (lane >> 4) + r;
           const float v = d4[r] + es[s] * (e4[r] + dni);
-          dKg[(t0 + s) * a.qt + i] = (T)(v * inv);
+          dKg[(t0 + s) * a.qt + i] = out16<DT, IO>(v * inv);
           kd[r] = sum16(v * (float)Ks[s * LQ + i]);
         }
         if ((lane & 15) == 0) {
@@ -917,7 +942,7 @@ __global__ void __launch_bounds__(512, 1) mlstm_bw_walk(MArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int s = 16 * sr + 4 * (lane >> 4) + r;
-          dVg[(t0 + s) * a.vt + j] = (T)((d4[r] + es[s] * e4[r]) * inv);
+          dVg[(t0 + s) * a.vt + j] = out16<DT, IO>((d4[r] + es[s] * e4[r]) * inv);
         }
       }
     }
@@ -965,29 +990,42 @@ __global__ void __launch_bounds__(512, 1) mlstm_bw_walk(MArgs a) {
   if (tid < DQ) a.dns[(int64_t)bh * DQ + tid] = dn * inv;
 }
 
-template <int DT, int DQ, int DV>
+template <int DT, int IO, int DQ, int DV>
 void launch_fwd(const MArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL((mlstm_fw_walk<DT, DQ, DV>), dim3(DV / kCB, a.BH), dim3(256), 0, st, a);
+  hipLaunchKernelGGL((mlstm_fw_walk<DT, IO, DQ, DV>), dim3(DV / kCB, a.BH), dim3(256), 0, st, a);
 }
-template <int DT, int DQ, int DV>
+template <int DT, int IO, int DQ, int DV>
 void launch_bwd(const MArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL((mlstm_bw_walk<DT, DQ, DV>), dim3(a.BH), dim3(512), 0, st, a);
+  hipLaunchKernelGGL((mlstm_bw_walk<DT, IO, DQ, DV>), dim3(a.BH), dim3(512), 0, st, a);
 }
 
 // head dimensions compiled in (DQ, DV): the xLSTM-large defaults qk = v/2 at 64..192 wide heads
 #define SC_MLSTM_DIMS(X) X(32, 64) X(64, 64) X(64, 128) X(96, 192)
 
-template <int DT>
+template <int DT, int IO>
 bool dispatch(const MArgs& a, int DQ, int DV, bool bwd, hipStream_t st) {
 #define SC_CASE(q, v)                                    \
   if (DQ == q && DV == v) {                              \
-    if (bwd) launch_bwd<DT, q, v>(a, st);                \
-    else launch_fwd<DT, q, v>(a, st);                    \
+    if (bwd) launch_bwd<DT, IO, q, v>(a, st);            \
+    else launch_fwd<DT, IO, q, v>(a, st);                \
     return true;                                         \
   }
   SC_MLSTM_DIMS(SC_CASE)
 #undef SC_CASE
   return false;
+}
+
+// (compute dtype, operand dtype) pairs: bf16 / bf16, f16 / f16, and the reference's f16 cell on
+// a bf16-autocast model's projection (f16 compute, bf16 in HBM)
+bool io_supported(int dtype, int io_dtype) {
+  return (dtype == SC_BF16 && io_dtype == SC_BF16) || (dtype == SC_F16 && io_dtype == SC_F16) ||
+         (dtype == SC_F16 && io_dtype == SC_BF16);
+}
+void dispatch_io(const MArgs& a, int dtype, int io_dtype, int DQ, int DV, bool bwd,
+                 hipStream_t st) {
+  if (dtype == SC_BF16) dispatch<SC_BF16, SC_BF16>(a, DQ, DV, bwd, st);
+  else if (io_dtype == SC_F16) dispatch<SC_F16, SC_F16>(a, DQ, DV, bwd, st);
+  else dispatch<SC_F16, SC_BF16>(a, DQ, DV, bwd, st);
 }
 
 bool dims_supported(int DQ, int DV) {
@@ -1042,14 +1080,17 @@ extern "C" int64_t sc_mlstm_chunk_state_numel(int BH, int T, int DQ, int DV) {
   return (int64_t)BH * (T / kL) * DQ * DV;
 }
 
-extern "C" int sc_mlstm_fwd(const void* q, const void* k, const void* v, int dtype,
+extern "C" int sc_mlstm_fwd_io(const void* q, const void* k, const void* v, int dtype,
+                               int io_dtype,
                             const float* igate, const float* fgate, const float* c0,
                             const float* n0, const float* m0, int BH, int T, int DQ, int DV,
                             float eps, void* h, void* states_C, float* states_n,
                             float* states_m, float* c_last, float* m_rows, float* den_rows,
                             const int64_t* layout, void* stream) {
   clear_error();
-  SC_REQUIRE(dtype == SC_BF16 || dtype == SC_F16, "sc_mlstm_fwd: dtype %d (bf16/f16 only)", dtype);
+  SC_REQUIRE(io_supported(dtype, io_dtype),
+             "sc_mlstm_fwd: dtype %d / operand dtype %d (bf16/bf16, f16/f16, f16/bf16 only)", dtype,
+             io_dtype);
   SC_REQUIRE(BH >= 0 && T >= 0, "sc_mlstm_fwd: bad shape");
   SC_REQUIRE(T % kL == 0, "sc_mlstm_fwd: T=%d is not a multiple of the chunk length %d", T, kL);
   SC_REQUIRE(dims_supported(DQ, DV), "sc_mlstm_fwd: head dims (%d, %d) not compiled in", DQ, DV);
@@ -1064,12 +1105,22 @@ extern "C" int sc_mlstm_fwd(const void* q, const void* k, const void* v, int dty
   a.BH = BH; a.T = T; a.nc = T / kL; a.eps = eps; a.scale = 1.0f / sqrtf((float)DQ);
   if (int rc = set_layout(a, layout, DQ, DV, "sc_mlstm_fwd", {q, k, v})) return rc;
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == SC_BF16) dispatch<SC_BF16>(a, DQ, DV, false, st);
-  else dispatch<SC_F16>(a, DQ, DV, false, st);
+  dispatch_io(a, dtype, io_dtype, DQ, DV, false, st);
   return launch_status("sc_mlstm_fwd");
 }
 
-extern "C" int sc_mlstm_bwd(const void* q, const void* k, const void* v, int dtype,
+extern "C" int sc_mlstm_fwd(const void* q, const void* k, const void* v, int dtype,
+                            const float* igate, const float* fgate, const float* c0,
+                            const float* n0, const float* m0, int BH, int T, int DQ, int DV,
+                            float eps, void* h, void* states_C, float* states_n,
+                            float* states_m, float* c_last, float* m_rows, float* den_rows,
+                            const int64_t* layout, void* stream) {
+  return sc_mlstm_fwd_io(q, k, v, dtype, dtype, igate, fgate, c0, n0, m0, BH, T, DQ, DV, eps, h,
+                         states_C, states_n, states_m, c_last, m_rows, den_rows, layout, stream);
+}
+
+extern "C" int sc_mlstm_bwd_io(const void* q, const void* k, const void* v, int dtype,
+                               int io_dtype,
                             const float* igate, const float* fgate, const void* h,
                             const void* dh, const float* dcT, const float* dnT,
                             const void* states_C, const float* states_n, const float* states_m,
@@ -1078,7 +1129,9 @@ extern "C" int sc_mlstm_bwd(const void* q, const void* k, const void* v, int dty
                             void* dk, void* dv, float* qdq, float* kdk, const int64_t* layout,
                             void* stream) {
   clear_error();
-  SC_REQUIRE(dtype == SC_BF16 || dtype == SC_F16, "sc_mlstm_bwd: dtype %d (bf16/f16 only)", dtype);
+  SC_REQUIRE(io_supported(dtype, io_dtype),
+             "sc_mlstm_bwd: dtype %d / operand dtype %d (bf16/bf16, f16/f16, f16/bf16 only)", dtype,
+             io_dtype);
   SC_REQUIRE(T % kL == 0, "sc_mlstm_bwd: T=%d is not a multiple of the chunk length %d", T, kL);
   SC_REQUIRE(dims_supported(DQ, DV), "sc_mlstm_bwd: head dims (%d, %d) not compiled in", DQ, DV);
   if (BH == 0 || T == 0) return 0;
@@ -1093,7 +1146,19 @@ extern "C" int sc_mlstm_bwd(const void* q, const void* k, const void* v, int dty
   a.BH = BH; a.T = T; a.nc = T / kL; a.eps = eps; a.scale = 1.0f / sqrtf((float)DQ);
   if (int rc = set_layout(a, layout, DQ, DV, "sc_mlstm_bwd", {q, k, v, dq, dk, dv})) return rc;
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == SC_BF16) dispatch<SC_BF16>(a, DQ, DV, true, st);
-  else dispatch<SC_F16>(a, DQ, DV, true, st);
+  dispatch_io(a, dtype, io_dtype, DQ, DV, true, st);
   return launch_status("sc_mlstm_bwd");
+}
+
+extern "C" int sc_mlstm_bwd(const void* q, const void* k, const void* v, int dtype,
+                            const float* igate, const float* fgate, const void* h,
+                            const void* dh, const float* dcT, const float* dnT,
+                            const void* states_C, const float* states_n, const float* states_m,
+                            const float* m_rows, const float* den_rows, int BH, int T, int DQ,
+                            int DV, float eps, float* dstates_C, float* dstates_n, void* dq,
+                            void* dk, void* dv, float* qdq, float* kdk, const int64_t* layout,
+                            void* stream) {
+  return sc_mlstm_bwd_io(q, k, v, dtype, dtype, igate, fgate, h, dh, dcT, dnT, states_C,
+                         states_n, states_m, m_rows, den_rows, BH, T, DQ, DV, eps, dstates_C,
+                         dstates_n, dq, dk, dv, qdq, kdk, layout, stream);
 }

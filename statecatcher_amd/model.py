@@ -270,10 +270,11 @@ class ASRModel(nn.Module):
 
 
 def build_xlstm_config(feat_dim, vocab_size, num_heads=2, num_blocks=3, embedding_dim=None,
-                       autocast_kernel_dtype="bfloat16"):
+                       autocast_kernel_dtype="float16"):
     """model.py:214-229: the xLSTM config train.py builds (embedding_dim = input_dim = feat_dim
     in the reference; C4 uses a 768-wide model behind the input projection).  The reference
-    passes autocast_kernel_dtype="float16" (model.py:227): the mLSTM cell then computes in fp16."""
+    passes autocast_kernel_dtype="float16" (model.py:227), and so does this builder by default:
+    the mLSTM cell then computes in fp16 (on the bf16 projection, ops.MLSTMCoreFn)."""
     return xLSTMLargeConfig(embedding_dim=embedding_dim or feat_dim, input_dim=feat_dim,
                             num_heads=num_heads, num_blocks=num_blocks, vocab_size=vocab_size,
                             return_last_states=True, mode="train",

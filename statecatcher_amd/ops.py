@@ -1071,10 +1071,14 @@ class MLSTMCoreFn(torch.autograd.Function):
     q, k, v and o are read in place from a (sc_mlstm_* layout strides, the gated norm's row
     stride): no split copies or head transposes.  The backward writes dq / dk / dv / do / di / df
     straight into ONE gradient tensor of a's shape: no concatenation of six slice gradients.
-    Same kernels and roundings as MLSTMFn + GatedHeadNormFn + the torch soft caps."""
+    Same kernels and roundings as MLSTMFn + GatedHeadNormFn + the torch soft caps.
+    cell_dtype: the cell's compute dtype -- bf16, or float16 as the reference configures it
+    (autocast_kernel_dtype, model.py:227): q / k / v are then rounded to f16 on load inside the
+    kernels (sc_mlstm_*_io), as the split path's .to(float16) rounds them, and h / dq / dk / dv
+    stay bf16 in HBM."""
 
     @staticmethod
-    def forward(ctx, a, c0, n0, m0, w_mh, NH, DQ, DV, cap, eps, eps_mh):
+    def forward(ctx, a, c0, n0, m0, w_mh, NH, DQ, DV, cap, eps, eps_mh, cell_dtype=torch.bfloat16):
         require_device(a)
         ctx.set_materialize_grads(False)   # detached carried states: no zero-filled gradients
         B, T, N = a.shape
@@ -1094,7 +1098,8 @@ class MLSTMCoreFn(torch.autograd.Function):
         base = a.data_ptr()
         lay = (ctypes.c_int64 * 7)(NH, T * N, DQ, N, T * N, DV, N)
         h = torch.empty(BH, T, DV, dtype=a.dtype, device=dev)
-        Cs = torch.empty(BH, nc, DV, DQ, dtype=a.dtype, device=dev)   # chunk-start state images [j][i]
+        Cs = torch.empty(BH, nc, DV, DQ, dtype=cell_dtype, device=dev)   # state images [j][i]
+        cdc = dtype_code(Cs)
         cT = torch.empty(B, NH, DQ, DV, dtype=torch.float32, device=dev)
         ns = torch.empty(BH, nc + 1, DQ, dtype=torch.float32, device=dev)
         ms = torch.empty(BH, nc + 1, dtype=torch.float32, device=dev)
@@ -1103,10 +1108,10 @@ class MLSTMCoreFn(torch.autograd.Function):
         fwd_b = BH * T * (2 * DQ + 2 * DV) * esz   # algorithmic: q k v in, h out
         stream = stream_of(a)
         with _timed("mlstm_fwd", a, fwd_b):
-            rc = lib.sc_mlstm_fwd(base + qo * esz, base + ko * esz, base + vo * esz, dtype_code(a),
-                                  ptr(ig), ptr(fg), ptr(c0c), ptr(n0c), ptr(m0c), BH, T, DQ, DV,
-                                  float(eps), ptr(h), ptr(Cs), ptr(ns), ptr(ms), ptr(cT), ptr(mrow),
-                                  ptr(den), lay, stream)
+            rc = lib.sc_mlstm_fwd_io(base + qo * esz, base + ko * esz, base + vo * esz, cdc,
+                                     dtype_code(a), ptr(ig), ptr(fg), ptr(c0c), ptr(n0c), ptr(m0c),
+                                     BH, T, DQ, DV, float(eps), ptr(h), ptr(Cs), ptr(ns), ptr(ms),
+                                     ptr(cT), ptr(mrow), ptr(den), lay, stream)
         check(rc, "sc_mlstm_fwd")
         wf = w_mh.detach().float().contiguous()
         y = torch.empty(B, T, NH * DV, dtype=torch.bfloat16, device=dev)
@@ -1156,9 +1161,9 @@ class MLSTMCoreFn(torch.autograd.Function):
         lay = (ctypes.c_int64 * 7)(NH, T * N, DQ, N, T * N, DV, N)
         bwd_b = BH * T * (4 * DQ + 4 * DV) * esz   # algorithmic: q k v h dh in, dq dk dv out
         with _timed("mlstm_bwd", a, bwd_b):
-            rc = lib.sc_mlstm_bwd(
-                base + qo * esz, base + ko * esz, base + vo * esz, dtype_code(a), ptr(ig), ptr(fg),
-                ptr(h), ptr(dh), ptr(dcTc), ptr(dnTc), ptr(Cs), ptr(ns), ptr(ms), ptr(mrow),
+            rc = lib.sc_mlstm_bwd_io(
+                base + qo * esz, base + ko * esz, base + vo * esz, dtype_code(Cs), dtype_code(a),
+                ptr(ig), ptr(fg), ptr(h), ptr(dh), ptr(dcTc), ptr(dnTc), ptr(Cs), ptr(ns), ptr(ms), ptr(mrow),
                 ptr(den), BH, T, DQ, DV, eps, ptr(dCs), ptr(dns), dbase + qo * esz,
                 dbase + ko * esz, dbase + vo * esz, ptr(qdq), ptr(kdk), lay, stream)
         check(rc, "sc_mlstm_bwd")
@@ -1171,7 +1176,7 @@ class MLSTMCoreFn(torch.autograd.Function):
         da[..., fo:fo + NH] = _soft_cap_bwd(dfg_c, a[..., fo:fo + NH], cap)
         return (da, dCs.view(B, NH, DQ, DV) if has_c0 else None,
                 dns.view(B, NH, DQ) if has_n0 else None, None,
-                _part_sum(part).to(wdt), None, None, None, None, None, None)
+                _part_sum(part).to(wdt), None, None, None, None, None, None, None)
 
 
 def mlstm_core_supported(a, NH, DQ, DV):

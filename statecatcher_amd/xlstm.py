@@ -205,12 +205,12 @@ class mLSTMLayer(nn.Module):
         if x.is_cuda and mh.bias is None and mh.force_float32_reductions:
             a = self.projection(x)
             DQ, DV = self.qk_dim // NH, self.v_dim // NH
-            if ops.mlstm_core_supported(a, NH, DQ, DV) and kdt == a.dtype:
+            if ops.mlstm_core_supported(a, NH, DQ, DV) and kdt in (torch.bfloat16, torch.float16):
                 # split -> soft caps -> mLSTM cell -> gated head norm as one node reading q / k /
                 # v / o in place from the projection (ops.MLSTMCoreFn); same math and roundings
                 c0, n0, m0 = (None, None, None) if state is None else state
                 y, c, n, m = ops.MLSTMCoreFn.apply(a, c0, n0, m0, mh.weight, NH, DQ, DV,
-                                                   self.cfg.gate_soft_cap, self.cfg.eps, mh.eps)
+                                                   self.cfg.gate_soft_cap, self.cfg.eps, mh.eps, kdt)
                 return _linear(y, self.out_proj.weight, self.out_proj.bias), (c, n, m)
             q, k, v, o, ig, fg = a.split([m.weight.shape[0] for m in self._mods()], -1)
         else:
