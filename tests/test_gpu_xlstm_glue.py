@@ -188,9 +188,10 @@ def test_mlstm_core_equals_composed_ops(with_state, kernel_dtype, monkeypatch):
     GatedHeadNormFn, autograd's concatenation): same kernels and roundings, so the layer output,
     the final state and every gradient are bit-identical.  With the reference's float16 cell the
     core path reads the bf16 projection and rounds to f16 on load (sc_mlstm_*_io) where the split
-    path casts; the loss is scaled so that dh lies in f16's normal range, where the split path's
-    f16 cast of the bf16 dh is exact (below it the core path, which reads dh as bf16, is the more
-    accurate one)."""
+    path casts: the forward is still bit-identical; in the backward the split path also casts
+    the bf16 dh to f16, which is exact only in f16's normal range, while the core path reads dh
+    as bf16 -- so there the gradients agree to 1e-2 (relative Frobenius; measured ~1e-3, from
+    the |dh| < 6e-5 elements) and the core path's are the more accurate."""
     from statecatcher_amd import xlstm
     cfg = xlstm.xLSTMLargeConfig(embedding_dim=256, num_heads=4, num_blocks=1, vocab_size=64,
                                  autocast_kernel_dtype=kernel_dtype)
@@ -216,11 +217,15 @@ def test_mlstm_core_equals_composed_ops(with_state, kernel_dtype, monkeypatch):
         sti = None if st is None else tuple(t.clone().requires_grad_(i < 2) for i, t in enumerate(st))
         with torch.autocast("cuda", dtype=torch.bfloat16):
             y, (c, n, m) = layer(xi, sti)
-        (4096.0 * y.float().square().mean() + c.square().mean() + n.mean()).backward()
+        (y.float().square().mean() + c.square().mean() + n.mean()).backward()
         res.append([y, c, n, m, xi.grad] + [p.grad for p in layer.parameters()] +
                    ([sti[0].grad, sti[1].grad] if sti else []))
     for i, (u, v) in enumerate(zip(*res)):
-        assert torch.equal(u, v), i
+        if kernel_dtype == "bfloat16" or i < 4:
+            assert torch.equal(u, v), i
+        else:
+            rel = float((u.double() - v.double()).norm() / max(float(v.double().norm()), 1e-30))
+            assert rel <= 1e-2, (i, rel)
 
 
 def test_fused_linear_bitwise_vs_cat_then_linear():
