@@ -190,8 +190,9 @@ def test_mlstm_core_equals_composed_ops(with_state, kernel_dtype, monkeypatch):
     core path reads the bf16 projection and rounds to f16 on load (sc_mlstm_*_io) where the split
     path casts: the forward is still bit-identical; in the backward the split path also casts
     the bf16 dh to f16, which is exact only in f16's normal range, while the core path reads dh
-    as bf16 -- so there the gradients agree to 1e-2 (relative Frobenius; measured ~1e-3, from
-    the |dh| < 6e-5 elements) and the core path's are the more accurate."""
+    as bf16 -- so there the gradients agree to 1e-2 (relative Frobenius, with the loss scaled so
+    that most of dh is in f16's normal range; the |dh| < 6e-5 elements differ) and the core
+    path's are the more accurate (unscaled, the split path's f16 dh costs 7% on q.weight)."""
     from statecatcher_amd import xlstm
     cfg = xlstm.xLSTMLargeConfig(embedding_dim=256, num_heads=4, num_blocks=1, vocab_size=64,
                                  autocast_kernel_dtype=kernel_dtype)
@@ -217,7 +218,8 @@ def test_mlstm_core_equals_composed_ops(with_state, kernel_dtype, monkeypatch):
         sti = None if st is None else tuple(t.clone().requires_grad_(i < 2) for i, t in enumerate(st))
         with torch.autocast("cuda", dtype=torch.bfloat16):
             y, (c, n, m) = layer(xi, sti)
-        (y.float().square().mean() + c.square().mean() + n.mean()).backward()
+        # (scaled: dh mostly inside f16's normal range, see above)
+        (4096.0 * y.float().square().mean() + c.square().mean() + n.mean()).backward()
         res.append([y, c, n, m, xi.grad] + [p.grad for p in layer.parameters()] +
                    ([sti[0].grad, sti[1].grad] if sti else []))
     for i, (u, v) in enumerate(zip(*res)):
