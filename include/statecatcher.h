@@ -375,6 +375,15 @@ int sc_mhln_gate_fwd(const void* h, const void* o, int64_t ldo, const float* w, 
 int sc_mhln_gate_bwd(const void* h, const void* o, int64_t ldo, const float* w, const float* mean,
                      const float* rstd, const void* dy, int64_t ldy, void* dh, void* dgo,
                      int64_t lddo, float* part, int B, int T, int NH, int DH, void* stream);
+/* The same with h in f16 (an f16 mLSTM cell's output), each element rounded to bf16 on load as
+ * h.to(bfloat16) would; dh is written in bf16. */
+int sc_mhln_gate_fwd_h16(const void* h, const void* o, int64_t ldo, const float* w, void* out,
+                         float* mean, float* rstd, int B, int T, int NH, int DH, float eps,
+                         void* stream);
+int sc_mhln_gate_bwd_h16(const void* h, const void* o, int64_t ldo, const float* w,
+                         const float* mean, const float* rstd, const void* dy, int64_t ldy,
+                         void* dh, void* dgo, int64_t lddo, float* part, int B, int T, int NH,
+                         int DH, void* stream);
 int sc_swiglu_fwd(const void* a, void* y, int64_t rows, int F, void* stream);
 int sc_swiglu_bwd(const void* a, const void* dy, void* da, int64_t rows, int F, void* stream);
 
@@ -455,10 +464,11 @@ int sc_mlstm_bwd(const void* q, const void* k, const void* v, int dtype, const f
 
 /*
  * sc_mlstm_fwd / sc_mlstm_bwd with the operands in another dtype than the cell computes in:
- * io_dtype is the dtype of q, k, v, h (and dh, dq, dk, dv); dtype the cell's MFMA dtype and the
- * chunk-state image's.  Supported pairs: (bf16, bf16), (f16, f16), and (f16, bf16) -- the
+ * io_dtype is the dtype of q, k, v (and dh, dq, dk, dv); dtype the cell's MFMA dtype and that of h
+ * and the chunk-state image.  Supported pairs: (bf16, bf16), (f16, f16), and (f16, bf16) -- the
  * reference's float16 cell (autocast_kernel_dtype, model.py:227) reading a bf16-autocast
- * model's projection in place, each operand rounded to f16 on load as .to(float16) would.
+ * model's projection in place, each operand rounded to f16 on load as .to(float16) would, and
+ * the gradients rounded through f16 to bf16 as the split path's casts are.
  */
 int sc_mlstm_fwd_io(const void* q, const void* k, const void* v, int dtype, int io_dtype,
                     const float* igate, const float* fgate, const float* c0, const float* n0,

@@ -79,6 +79,10 @@ _SIGS = {
                                 _c.c_float, _vp]),
     "sc_mhln_gate_bwd": (_i32, [_vp, _vp, _i64, _fp, _fp, _fp, _vp, _i64, _vp, _vp, _i64, _fp,
                                 _i32, _i32, _i32, _i32, _vp]),
+    "sc_mhln_gate_fwd_h16": (_i32, [_vp, _vp, _i64, _fp, _vp, _fp, _fp, _i32, _i32, _i32, _i32,
+                                _c.c_float, _vp]),
+    "sc_mhln_gate_bwd_h16": (_i32, [_vp, _vp, _i64, _fp, _fp, _fp, _vp, _i64, _vp, _vp, _i64, _fp,
+                                _i32, _i32, _i32, _i32, _vp]),
     "sc_swiglu_fwd": (_i32, [_vp, _vp, _i64, _i32, _vp]),
     "sc_swiglu_bwd": (_i32, [_vp, _vp, _vp, _i64, _i32, _vp]),
     "sc_adam_parts": (_i64, [_vp, _i32]),

@@ -295,7 +295,6 @@ __global__ void __launch_bounds__(256, 2) mlstm_fw_walk(MArgs a) {
   using M = MF<DT>;
   using T = typename M::T;
   using V8 = typename M::v8;
-  using TI = typename MF<IO>::T;   // q / k / v / h in HBM
   typedef T v4t __attribute__((ext_vector_type(4)));
   constexpr int LQ = DQ + kPad, LC = kCB + kPad;
   constexpr int TJ = kCB / 16, NI = DQ / 16, NT = NI * TJ, PW = NT / 4;
@@ -502,7 +501,7 @@ __global__ void __launch_bounds__(256, 2) mlstm_fw_walk(MArgs a) {
       for (int cj = 0; cj < TJ; ++cj) {
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          ((TI*)Ms)[(16 * w + 4 * (lane >> 4) + r) * LC + 16 * cj + (lane & 15)] = out16<DT, IO>(hv[cj][r]);
+          Ms[(16 * w + 4 * (lane >> 4) + r) * LC + 16 * cj + (lane & 15)] = (T)hv[cj][r];
       }
 #pragma unroll
       for (int u = 0; u < 2; ++u) {   // 16 rows x 128 bytes = 128 pieces over 64 lanes
@@ -577,7 +576,7 @@ __global__ void __launch_bounds__(512, 1) mlstm_bw_walk(MArgs a) {
   using M = MF<DT>;
   using T = typename M::T;
   using V8 = typename M::v8;
-  using TI = typename MF<IO>::T;   // q / k / v / h / dh and the gradients in HBM
+  using TI = typename MF<IO>::T;   // q / k / v / dh and the gradients in HBM (h: compute dtype)
   using V8I = typename MF<IO>::v8;
   typedef T v4t __attribute__((ext_vector_type(4)));
   constexpr bool kScale = DT == SC_F16;
@@ -765,7 +764,7 @@ __global__ void __launch_bounds__(512, 1) mlstm_bw_walk(MArgs a) {
 #pragma unroll
       for (int u = 0; u < UH; ++u) {
         const V8I xd = __builtin_bit_cast(V8I, rd[u]);
-        const V8I xh = __builtin_bit_cast(V8I, rh[u]);
+        const V8 xh = __builtin_bit_cast(V8, rh[u]);
         V8 o;
 #pragma unroll
         for (int e2 = 0; e2 < 8; ++e2) {

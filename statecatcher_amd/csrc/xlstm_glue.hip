@@ -39,6 +39,13 @@ __device__ __forceinline__ void ld4(const u16* p, float (&v)[4]) {
   v[2] = __uint_as_float(q.y << 16);
   v[3] = __uint_as_float(q.y & 0xffff0000u);
 }
+// 4 f16 rounded to bf16 (an f16 mLSTM cell's h as the split path's h.to(bfloat16) sees it)
+__device__ __forceinline__ void ld4_h16(const u16* p, float (&v)[4]) {
+  typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+  const h4 q = *(const h4*)p;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) v[k] = rbf((float)q[k]);
+}
 __device__ __forceinline__ void st4(u16* p, const float (&v)[4]) {
   uint2 q;
   q.x = (uint32_t)tobf(v[0]) | ((uint32_t)tobf(v[1]) << 16);
@@ -175,6 +182,7 @@ struct MhArgs {
   int B, T, NH;
   int64_t ldo, ldy, lddo;
   float eps;
+  int h16;   // h is f16 (read rounded to bf16), else bf16
 };
 
 template <int CH>
@@ -190,7 +198,8 @@ __global__ void __launch_bounds__(256) mhln_fwd_kernel(MhArgs a) {
   float s = 0.0f;
 #pragma unroll
   for (int c = 0; c < CH; ++c) {
-    ld4(hp + (c * 16 + sub) * 4, v[c]);
+    if (a.h16) ld4_h16(hp + (c * 16 + sub) * 4, v[c]);
+    else ld4(hp + (c * 16 + sub) * 4, v[c]);
 #pragma unroll
     for (int k = 0; k < 4; ++k) s += v[c][k];
   }
@@ -245,7 +254,8 @@ __global__ void __launch_bounds__(256) mhln_bwd_kernel(MhArgs a) {
     for (int c = 0; c < CH; ++c) {
       const int col = n * DH + (c * 16 + sub) * 4;
       float hv[4], ov[4], dv[4], dov[4];
-      ld4(a.h + hrow + (c * 16 + sub) * 4, hv);
+      if (a.h16) ld4_h16(a.h + hrow + (c * 16 + sub) * 4, hv);
+      else ld4(a.h + hrow + (c * 16 + sub) * 4, hv);
       ld4(a.o + m * a.ldo + col, ov);
       ld4(a.dy + m * a.ldy + col, dv);
       const float4 wq = *(const float4*)(a.w + col);
@@ -415,9 +425,9 @@ static int mh_check(int B, int T, int NH, int DH, const char* who) {
   return 0;
 }
 
-extern "C" int sc_mhln_gate_fwd(const void* h, const void* o, int64_t ldo, const float* w, void* out,
-                                float* mean, float* rstd, int B, int T, int NH, int DH, float eps,
-                                void* stream) {
+static int mhln_fwd(const void* h, int h16, const void* o, int64_t ldo, const float* w,
+                    void* out, float* mean, float* rstd, int B, int T, int NH, int DH, float eps,
+                    void* stream) {
   clear_error();
   if (int rc = mh_check(B, T, NH, DH, "sc_mhln_gate_fwd")) return rc;
   SC_REQUIRE(h && o && w && out && mean && rstd, "sc_mhln_gate_fwd: null pointer");
@@ -425,7 +435,7 @@ extern "C" int sc_mhln_gate_fwd(const void* h, const void* o, int64_t ldo, const
   const int64_t M = (int64_t)B * T;
   if (M == 0) return 0;
   MhArgs a{(const u16*)h, (const u16*)o, w, (u16*)out, mean, rstd, nullptr, nullptr, nullptr,
-           nullptr, B, T, NH, ldo, 0, 0, eps};
+           nullptr, B, T, NH, ldo, 0, 0, eps, h16};
   const dim3 g((unsigned)((M + 3) / 4));
   hipStream_t st = (hipStream_t)stream;
   switch (DH / 64) {
@@ -436,11 +446,21 @@ extern "C" int sc_mhln_gate_fwd(const void* h, const void* o, int64_t ldo, const
   }
   return launch_status("sc_mhln_gate_fwd");
 }
+extern "C" int sc_mhln_gate_fwd(const void* h, const void* o, int64_t ldo, const float* w, void* out,
+                                float* mean, float* rstd, int B, int T, int NH, int DH, float eps,
+                                void* stream) {
+  return mhln_fwd(h, 0, o, ldo, w, out, mean, rstd, B, T, NH, DH, eps, stream);
+}
+extern "C" int sc_mhln_gate_fwd_h16(const void* h, const void* o, int64_t ldo, const float* w,
+                                    void* out, float* mean, float* rstd, int B, int T, int NH,
+                                    int DH, float eps, void* stream) {
+  return mhln_fwd(h, 1, o, ldo, w, out, mean, rstd, B, T, NH, DH, eps, stream);
+}
 
-extern "C" int sc_mhln_gate_bwd(const void* h, const void* o, int64_t ldo, const float* w,
-                                const float* mean, const float* rstd, const void* dy, int64_t ldy,
-                                void* dh, void* dgo, int64_t lddo, float* part, int B, int T,
-                                int NH, int DH, void* stream) {
+static int mhln_bwd(const void* h, int h16, const void* o, int64_t ldo, const float* w,
+                    const float* mean, const float* rstd, const void* dy, int64_t ldy, void* dh,
+                    void* dgo, int64_t lddo, float* part, int B, int T, int NH, int DH,
+                    void* stream) {
   clear_error();
   if (int rc = mh_check(B, T, NH, DH, "sc_mhln_gate_bwd")) return rc;
   SC_REQUIRE(h && o && w && mean && rstd && dy && dh && dgo && part, "sc_mhln_gate_bwd: null pointer");
@@ -449,7 +469,7 @@ extern "C" int sc_mhln_gate_bwd(const void* h, const void* o, int64_t ldo, const
   if (M == 0) return 0;
   MhArgs a{(const u16*)h, (const u16*)o, w, nullptr, const_cast<float*>(mean),
            const_cast<float*>(rstd), (const u16*)dy, (u16*)dh, (u16*)dgo, part, B, T, NH, ldo,
-           ldy, lddo, 0.0f};
+           ldy, lddo, 0.0f, h16};
   const dim3 g((unsigned)part_rows(M));
   const size_t lds = (size_t)4 * NH * DH * sizeof(float);
   hipStream_t st = (hipStream_t)stream;
@@ -460,6 +480,18 @@ extern "C" int sc_mhln_gate_bwd(const void* h, const void* o, int64_t ldo, const
     default: hipLaunchKernelGGL(mhln_bwd_kernel<4>, g, dim3(256), lds, st, a); break;
   }
   return launch_status("sc_mhln_gate_bwd");
+}
+extern "C" int sc_mhln_gate_bwd(const void* h, const void* o, int64_t ldo, const float* w,
+                                const float* mean, const float* rstd, const void* dy, int64_t ldy,
+                                void* dh, void* dgo, int64_t lddo, float* part, int B, int T,
+                                int NH, int DH, void* stream) {
+  return mhln_bwd(h, 0, o, ldo, w, mean, rstd, dy, ldy, dh, dgo, lddo, part, B, T, NH, DH, stream);
+}
+extern "C" int sc_mhln_gate_bwd_h16(const void* h, const void* o, int64_t ldo, const float* w,
+                                    const float* mean, const float* rstd, const void* dy,
+                                    int64_t ldy, void* dh, void* dgo, int64_t lddo, float* part,
+                                    int B, int T, int NH, int DH, void* stream) {
+  return mhln_bwd(h, 1, o, ldo, w, mean, rstd, dy, ldy, dh, dgo, lddo, part, B, T, NH, DH, stream);
 }
 
 extern "C" int sc_swiglu_fwd(const void* a, void* y, int64_t rows, int F, void* stream) {

@@ -1097,7 +1097,7 @@ class MLSTMCoreFn(torch.autograd.Function):
         esz = a.element_size()
         base = a.data_ptr()
         lay = (ctypes.c_int64 * 7)(NH, T * N, DQ, N, T * N, DV, N)
-        h = torch.empty(BH, T, DV, dtype=a.dtype, device=dev)
+        h = torch.empty(BH, T, DV, dtype=cell_dtype, device=dev)   # the cell's output dtype
         Cs = torch.empty(BH, nc, DV, DQ, dtype=cell_dtype, device=dev)   # state images [j][i]
         cdc = dtype_code(Cs)
         cT = torch.empty(B, NH, DQ, DV, dtype=torch.float32, device=dev)
@@ -1117,8 +1117,10 @@ class MLSTMCoreFn(torch.autograd.Function):
         y = torch.empty(B, T, NH * DV, dtype=torch.bfloat16, device=dev)
         mean = torch.empty(B * T, NH, dtype=torch.float32, device=dev)
         rstd = torch.empty_like(mean)
-        check(lib.sc_mhln_gate_fwd(ptr(h), base + oo * esz, N, ptr(wf), ptr(y), ptr(mean), ptr(rstd),
-                                   B, T, NH, DV, float(eps_mh), stream), "sc_mhln_gate_fwd")
+        # (an f16 h is read rounded to bf16: the split path's h.to(bfloat16))
+        mh_fwd = lib.sc_mhln_gate_fwd_h16 if h.dtype == torch.float16 else lib.sc_mhln_gate_fwd
+        check(mh_fwd(ptr(h), base + oo * esz, N, ptr(wf), ptr(y), ptr(mean), ptr(rstd),
+                     B, T, NH, DV, float(eps_mh), stream), "sc_mhln_gate_fwd")
         ctx.save_for_backward(a, ig, fg, h, Cs, ns, ms, mrow, den, wf, mean, rstd)
         ctx.meta = (NH, DQ, DV, cap, float(eps), c0 is not None, n0 is not None, w_mh.dtype)
         nT = ns[:, nc].view(B, NH, DQ).clone()
@@ -1147,11 +1149,12 @@ class MLSTMCoreFn(torch.autograd.Function):
             dyc = dyc.contiguous()
         da = torch.empty_like(a)
         dbase = da.data_ptr()
-        dh = torch.empty_like(h)
+        dh = torch.empty(h.shape, dtype=a.dtype, device=dev)   # bf16 (f16 cell: not cast)
         part = torch.empty(lib.sc_xlstm_part_rows(B * T), NH * DV, dtype=torch.float32, device=dev)
-        check(lib.sc_mhln_gate_bwd(ptr(h), base + oo * esz, N, ptr(wf), ptr(mean), ptr(rstd),
-                                   ptr(dyc), dyc.stride(1), ptr(dh), dbase + oo * esz, N, ptr(part),
-                                   B, T, NH, DV, stream), "sc_mhln_gate_bwd")
+        mh_bwd = lib.sc_mhln_gate_bwd_h16 if h.dtype == torch.float16 else lib.sc_mhln_gate_bwd
+        check(mh_bwd(ptr(h), base + oo * esz, N, ptr(wf), ptr(mean), ptr(rstd),
+                     ptr(dyc), dyc.stride(1), ptr(dh), dbase + oo * esz, N, ptr(part),
+                     B, T, NH, DV, stream), "sc_mhln_gate_bwd")
         dcTc = None if dcT is None else dcT.float().contiguous()
         dnTc = None if dnT is None else dnT.float().contiguous()
         dCs = torch.empty(BH, DQ, DV, dtype=torch.float32, device=dev)   # d initial state
