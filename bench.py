@@ -412,6 +412,23 @@ def main():
         roofline = {"bound": "hbm", "kernel": dom, "achieved": kd["achieved_GBs"],
                     "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": kd["frac_of_peak"],
                     "traffic": traffic}
+    # C5: the fused joiner owns half the step and is MFMA work.  Per launch (one segment of B
+    # sequences, all T = seq frames, U + 1 = 151 label positions): N = B T (U+1) lattice nodes,
+    # joint_fwd 2 N V J flops (the logits once), joint_bwd 3 x 2 N V J (logits recomputed, dW,
+    # dZ); J = 64.  Peak: bf16 dense MFMA (MI355X_MICROARCH.md).
+    if args.workload == "rnnt":
+        nodes = args.batch * args.seq * 151
+        for name, mult in (("rnnt_joint_fwd", 1), ("rnnt_joint_bwd", 3)):
+            if name in kernels:
+                fl = mult * 2.0 * nodes * args.vocab * 64
+                tfs = fl / (kernels[name]["avg_us"] * 1e-6) / 1e12
+                kernels[name].update({"flops_per_launch": fl, "achieved_TFLOPs": round(tfs, 1),
+                                      "frac_of_peak": round(tfs / PEAK_BF16_TFLOPS, 4)})
+        if "rnnt_joint_bwd" in kernels:
+            kj = kernels["rnnt_joint_bwd"]
+            roofline = {"bound": "mfma", "kernel": "rnnt_joint_bwd", "achieved": kj["achieved_TFLOPs"],
+                        "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": kj["frac_of_peak"],
+                        "traffic": None}
 
     frames = world * args.batch * args.seq * args.steps
     value = frames / dt
