@@ -778,7 +778,9 @@ __global__ void __launch_bounds__(512) joint_fwd_kernel(JointArgs a) {
 #define SC_JOINT_BF 0
 #endif
 constexpr int kVbWg = 16;   // vocab blocks (of 32) per workgroup
-constexpr int kVbW = 4;     // per wave
+constexpr int kJW = 8;      // waves per workgroup: two per SIMD, so one wave's exp / pack /
+                            // transpose work runs beside the other's MFMAs (<= 256 registers each)
+constexpr int kVbW = kVbWg / kJW;   // vocab blocks per wave
 
 struct NodeLd {   // the loads of node_weights, issued one column ahead
   double lp2, oA, oB, be_b, be_y;
@@ -825,42 +827,43 @@ struct BwdLds {   // byte offsets of the LDS regions
   static constexpr int kDeP = 36;                       // d enc partial row pitch (floats)
   static constexpr int kW = 0;                          // W half image [512][128 B]
   static constexpr int kBias = kW + kVbWg * 32 * 128;   // [512] fp32, x log2(e)
-  static constexpr int kZ = kBias + kVbWg * 32 * 4;     // z bf16 image [32][128 B]
-  static constexpr int kZ32 = kZ + 32 * 128;            // 1 - z^2 fp32 [32][64]
-  static constexpr int kEnc = kZ32 + 32 * 64 * 4;       // the task's enc rows fp32 [32][64]
-  static constexpr int kNs = kEnc + 32 * 64 * 4;        // node scalars: c, wb, wy [3][32]
-  static constexpr int kP = kNs + 3 * 32 * 4;           // per-wave p image [4][32][128 B]
-  static constexpr int kRed = kP + 4 * 32 * 128;        // d pred partials [4][64]
-  static constexpr int kDe = kRed + 4 * 64 * 4;         // per-wave d enc partials [4][64 j][36]
-  static constexpr int kEnd = kDe + 4 * 64 * kDeP * 4;
+  // column operands, two buffers (column u + 1 is staged while u computes):
+  static constexpr int kZ = kBias + kVbWg * 32 * 4;     // z bf16 image [2][32][128 B]
+  static constexpr int kZ32 = kZ + 2 * 32 * 128;        // 1 - z^2 fp32 [2][32][64]
+  static constexpr int kNs = kZ32 + 2 * 32 * 64 * 4;    // node scalars: c, wb, wy [2][3][32]
+  static constexpr int kRed = kNs + 2 * 3 * 32 * 4;     // d pred partials [2][8][64]
+  static constexpr int kEnc = kRed + 2 * kJW * 64 * 4;  // the task's enc rows fp32 [32][64]
+  static constexpr int kP = kEnc + 32 * 64 * 4;         // per-wave p image [8][32][128 B]
+  static constexpr int kDe = kP;                        // d enc partials [4][64 j][36], at the
+                                                        // task's end: over the p images
+  static constexpr int kEnd = kP + (kJW * 32 * 128 > 4 * 64 * kDeP * 4 ? kJW * 32 * 128
+                                                                        : 4 * 64 * kDeP * 4);
 };
 
-__global__ void __launch_bounds__(256) joint_bwd_kernel(JointArgs a) {
+__global__ void __launch_bounds__(64 * kJW) joint_bwd_kernel(JointArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const RnntArgs& r = a.r;
   const int nvb = r.V / 32, VS = a.vs;
   const int vh = blockIdx.x % VS, slot = blockIdx.x / VS, nslot = gridDim.x / VS;
   const int vb0 = vh * kVbWg, nvw = min(kVbWg, nvb - vb0);   // this workgroup's vocab blocks
-  const int th = threadIdx.x, lane = th & 63, w = uniform(th >> 6), h = lane >> 5;
-  const int g1 = (lane >> 4) & 1;
+  const int w = uniform(threadIdx.x >> 6);
+  int th = threadIdx.x, lane = th & 63, h = lane >> 5;
+  int g1 = (lane >> 4) & 1;
   unsigned char* wl = lds + BwdLds::kW;
   float* bias_l = (float*)(lds + BwdLds::kBias);
-  unsigned char* zimg = lds + BwdLds::kZ;
-  float* z32 = (float*)(lds + BwdLds::kZ32);   // 1 - z^2
+  unsigned char* const zimg0 = lds + BwdLds::kZ;
+  float* const z320 = (float*)(lds + BwdLds::kZ32);   // 1 - z^2
   float* encl = (float*)(lds + BwdLds::kEnc);
-  float* ns_c = (float*)(lds + BwdLds::kNs);
-  float* ns_wb = ns_c + 32;
-  float* ns_wy = ns_c + 64;
+  float* const ns0 = (float*)(lds + BwdLds::kNs);   // [2][c | wb | wy][32]
   unsigned char* pimg = lds + BwdLds::kP + w * 32 * 128;
-  float* red = (float*)(lds + BwdLds::kRed);
-  float* dep = (float*)(lds + BwdLds::kDe);              // [4][64][kDeP]
-  float* dew = dep + w * 64 * BwdLds::kDeP;
+  float* const red0 = (float*)(lds + BwdLds::kRed);   // [2][8][64]
+  float* dep = (float*)(lds + BwdLds::kDe);              // [4][64][kDeP]: waves w, w + 4
   // this half of W and its bias (x log2 e)
-  for (int i = th; i < nvw * 32 * 8; i += 256) {
+  for (int i = th; i < nvw * 32 * 8; i += 64 * kJW) {
     const int v = i >> 3, c = i & 7;
     *(uint4*)(wl + wimg(v, c)) = *(const uint4*)(a.W + (int64_t)(vb0 * 32 + v) * kJ + 8 * c);
   }
-  for (int i = th; i < nvw * 32; i += 256) bias_l[i] = a.bias[vb0 * 32 + i] * kLog2e;
+  for (int i = th; i < nvw * 32; i += 64 * kJW) bias_l[i] = a.bias[vb0 * 32 + i] * kLog2e;
 
   jf16 acc[kVbW][2];
   float dbs[kVbW];
@@ -874,7 +877,8 @@ __global__ void __launch_bounds__(256) joint_bwd_kernel(JointArgs a) {
   }
   const int ntbp = VS * a.ntb;   // t-block rows of the d pred / g partial layouts
   const int64_t ntask = (int64_t)r.B * a.ntb * a.nus;
-  const int zn = th >> 3, jg = th & 7;   // staging: node zn, j = 8 jg .. 8 jg + 7
+  const int zn = (th >> 3) & 31, jg = th & 7;   // staging (threads < 256): node zn, j = 8 jg ..
+  const bool stager = th < 256;
   for (int64_t task = slot; task < ntask; task += nslot) {
     const int b = (int)(task / ((int64_t)a.ntb * a.nus));
     const int tb = (int)((task / a.nus) % a.ntb), us = (int)(task % a.nus);
@@ -885,7 +889,14 @@ __global__ void __launch_bounds__(256) joint_bwd_kernel(JointArgs a) {
     const int ue = tb * 32 < Tb ? min((int)((int64_t)(us + 1) * r.U1 / a.nus), Ub + 1) : ua;
     const bool zok = tb * 32 + zn < Tb;
     lds_barrier();   // the previous task's reads of encl / d enc partials are done
-    if (ua < ue) {
+    // d enc of the task: this wave's partial over its vocab blocks, in registers across u
+    // (Y's layout: [jb][q] = node (q & 3) + 8 (q >> 2) + 4 h, j = jb 32 + (lane & 31))
+    float dacc[2][16];
+#pragma unroll
+    for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) dacc[jb][q] = 0.0f;
+    if (ua < ue && stager) {
       const float* ep = a.enc + ((int64_t)b * r.T + (zok ? tb * 32 + zn : Tb - 1)) * kJ + 8 * jg;
       *(float4*)(encl + zn * 64 + 8 * jg) = *(const float4*)ep;
       *(float4*)(encl + zn * 64 + 8 * jg + 4) = *(const float4*)(ep + 4);
@@ -895,68 +906,69 @@ __global__ void __launch_bounds__(256) joint_bwd_kernel(JointArgs a) {
     NodeLd nd{};
     if (th < 32 && ua < ue) nd = node_load(r, b, tb * 32 + th, ua, Tb, Ub);
     float4 pn0 = make_float4(0.f, 0.f, 0.f, 0.f), pn1 = pn0;
-    if (ua < ue) {
+    if (ua < ue && stager) {
       const float* pp = a.pred + ((int64_t)b * r.U1 + ua) * kJ + 8 * jg;
       pn0 = *(const float4*)pp;
       pn1 = *(const float4*)(pp + 4);
     }
-    for (int u = ua; u < ue; ++u) {
-      lds_barrier();   // the previous column's LDS reads are done
-      if (u > ua && th < 64) {   // d pred of the previous column: the 4 wave partials
-        const float s = red[th] + red[64 + th] + red[128 + th] + red[192 + th];
-        a.d_pred[(((int64_t)b * ntbp + vh * a.ntb + tb) * r.U1 + u - 1) * kJ + th] = s;
+    // stage column uu into buffer bf: z (bf16 image + fp32 1 - z^2), node scalars; the loads of
+    // the column after it are issued here and land while this one computes
+    auto stage = [&](int uu, int bf) __attribute__((always_inline)) {
+      if (!stager) return;
+      const float4 e0 = *(const float4*)(encl + zn * 64 + 8 * jg);
+      const float4 e1 = *(const float4*)(encl + zn * 64 + 8 * jg + 4);
+      const float xs[8] = {e0.x + pn0.x, e0.y + pn0.y, e0.z + pn0.z, e0.w + pn0.w,
+                           e1.x + pn1.x, e1.y + pn1.y, e1.z + pn1.z, e1.w + pn1.w};
+      if (uu + 1 < ue) {
+        const float* pp = a.pred + ((int64_t)b * r.U1 + uu + 1) * kJ + 8 * jg;
+        pn0 = *(const float4*)pp;
+        pn1 = *(const float4*)(pp + 4);
       }
-      {   // stage column u: z (bf16 image + fp32), node scalars
-        const float4 e0 = *(const float4*)(encl + zn * 64 + 8 * jg);
-        const float4 e1 = *(const float4*)(encl + zn * 64 + 8 * jg + 4);
-        const float xs[8] = {e0.x + pn0.x, e0.y + pn0.y, e0.z + pn0.z, e0.w + pn0.w,
-                             e1.x + pn1.x, e1.y + pn1.y, e1.z + pn1.z, e1.w + pn1.w};
-        if (u + 1 < ue) {
-          const float* pp = a.pred + ((int64_t)b * r.U1 + u + 1) * kJ + 8 * jg;
-          pn0 = *(const float4*)pp;
-          pn1 = *(const float4*)(pp + 4);
-        }
-        float zf[8];
-        jbf8 zb;
+      float zf[8];
+      jbf8 zb;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          zf[e] = zok ? tanh_(xs[e]) : 0.0f;
-          zb[e] = (__bf16)zf[e];
-        }
-        *(jbf8*)(zimg + wimg(zn, jg)) = zb;
-        // tanh' = 1 - z^2, once per element (every wave scales its dZ partial by it)
-        *(float4*)(z32 + zn * 64 + 8 * jg) = make_float4(1.0f - zf[0] * zf[0], 1.0f - zf[1] * zf[1],
-                                                         1.0f - zf[2] * zf[2], 1.0f - zf[3] * zf[3]);
-        *(float4*)(z32 + zn * 64 + 8 * jg + 4) = make_float4(1.0f - zf[4] * zf[4], 1.0f - zf[5] * zf[5],
-                                                             1.0f - zf[6] * zf[6], 1.0f - zf[7] * zf[7]);
-        if (th < 32) {
-          float wb, wy, l2;
-          node_finish(nd, tb * 32 + th, u, Tb, Ub, wb, wy, l2);
-          const float an = wb + wy;
-          // p = a exp2(x log2e + b log2e - l2) = exp2(x log2e + b log2e + c), c = log2 a - l2
-          ns_c[th] = an > 0.0f ? log2_(an) - l2 : -1e30f;
-          ns_wb[th] = wb;
-          ns_wy[th] = wy;
-          if (u + 1 < ue) nd = node_load(r, b, tb * 32 + th, u + 1, Tb, Ub);   // in flight
-        }
+      for (int e = 0; e < 8; ++e) {
+        zf[e] = zok ? tanh_(xs[e]) : 0.0f;
+        zb[e] = (__bf16)zf[e];
       }
-      lds_barrier();
+      *(jbf8*)(zimg0 + bf * 32 * 128 + wimg(zn, jg)) = zb;
+      // tanh' = 1 - z^2, once per element (every wave scales its dZ partial by it)
+      float* zz = z320 + bf * 32 * 64 + zn * 64 + 8 * jg;
+      *(float4*)zz = make_float4(1.0f - zf[0] * zf[0], 1.0f - zf[1] * zf[1],
+                                 1.0f - zf[2] * zf[2], 1.0f - zf[3] * zf[3]);
+      *(float4*)(zz + 4) = make_float4(1.0f - zf[4] * zf[4], 1.0f - zf[5] * zf[5],
+                                       1.0f - zf[6] * zf[6], 1.0f - zf[7] * zf[7]);
+      if (th < 32) {
+        float wb, wy, l2;
+        node_finish(nd, tb * 32 + th, uu, Tb, Ub, wb, wy, l2);
+        const float an = wb + wy;
+        // p = a exp2(x log2e + b log2e - l2) = exp2(x log2e + b log2e + c), c = log2 a - l2
+        float* ns = ns0 + bf * 96;
+        ns[th] = an > 0.0f ? log2_(an) - l2 : -1e30f;
+        ns[32 + th] = wb;
+        ns[64 + th] = wy;
+        if (uu + 1 < ue) nd = node_load(r, b, tb * 32 + th, uu + 1, Tb, Ub);   // in flight
+      }
+    };
+    if (ua < ue) stage(ua, 0);
+    lds_barrier();
+    for (int u = ua; u < ue; ++u) {
+      // lane-dependent addresses re-derived per column, not held across it (register budget of
+      // two waves per SIMD)
+      asm volatile("" : "+v"(th), "+v"(lane), "+v"(h), "+v"(g1));
+      const int cb = (u - ua) & 1;
+      const unsigned char* zimg = zimg0 + cb * 32 * 128;
+      const float* z32 = z320 + cb * 32 * 64;
+      const float* ns_c = ns0 + cb * 96;
+      const float* ns_wb = ns_c + 32;
+      const float* ns_wy = ns_c + 64;
+      float* red = red0 + cb * kJW * 64;
+      if (u + 1 < ue) stage(u + 1, cb ^ 1);   // into the other buffer (read two columns ago)
       // column operands: z rows (logits A operand), z^T (dW B operand), node terms per register
-      jbf8 zA[4], zT[2][2];
+      jbf8 zA[4];
 #pragma unroll
       for (int s = 0; s < 4; ++s) zA[s] = lds_b128(zimg, wimg(lane & 31, 2 * s + h));
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-        for (int jb = 0; jb < 2; ++jb)
-          zT[s2][jb] = cat8(tr_rd(zimg, 16 * s2 + 4 * h, jb * 32 + 16 * g1, lane),
-                            tr_rd(zimg, 16 * s2 + 8 + 4 * h, jb * 32 + 16 * g1, lane));
-      float cq[16];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float4 cv = *(const float4*)(ns_c + 8 * q + 4 * h);
-        cq[4 * q] = cv.x; cq[4 * q + 1] = cv.y; cq[4 * q + 2] = cv.z; cq[4 * q + 3] = cv.w;
-      }
+
       jf16 Y[2];
 #pragma unroll
       for (int jb = 0; jb < 2; ++jb)
@@ -965,7 +977,7 @@ __global__ void __launch_bounds__(256) joint_bwd_kernel(JointArgs a) {
       const int yl = u < Ub ? label_at(r, b, u) : r.blank;
       // logits of vocab block k (W rows of a block past the vocabulary: block 0, p forced to 0)
       auto logits_blk = [&](int k) __attribute__((always_inline)) {
-        const int lvb = w + 4 * k;
+        const int lvb = w + kJW * k;
         const int vl = (lvb < nvw ? lvb : 0) * 32 + (lane & 31);
         jf16 x;
 #pragma unroll
@@ -974,22 +986,26 @@ __global__ void __launch_bounds__(256) joint_bwd_kernel(JointArgs a) {
         for (int s = 0; s < 4; ++s) x = mfma32(zA[s], lds_b128(wl, wimg(vl, 2 * s + h)), x);
         return x;
       };
-      // software pipeline: block k+1's W reads and logits MFMAs are issued before block k's
-      // exp / transpose work, so their latency overlaps it (one wave per SIMD hides nothing)
-      jf16 xnext = logits_blk(0);
+      // (no software pipeline across the wave's blocks: the other wave on the SIMD covers the
+      // logits' latency, and its registers are the two-waves-per-SIMD budget)
 #pragma unroll
       for (int k = 0; k < kVbW; ++k) {
         // every wave runs all kVbW blocks (no early exit: its PHIs cost a copy of Y)
-        const int lvb = w + 4 * k;
+        const int lvb = w + kJW * k;
         const bool vok = lvb < nvw;
         const int lvc = vok ? lvb : 0;   // (the W rows read for a block past the vocabulary)
         const int vl = lvc * 32 + (lane & 31);
-        const jf16 x = xnext;
-        if (k + 1 < kVbW) xnext = logits_blk(k + 1);
+        const jf16 x = logits_blk(k);
         const float bl = vok ? bias_l[vl] : -1e30f;
         float p[16], ps = 0.0f;
 #pragma unroll
-        for (int q = 0; q < 16; ++q) p[q] = exp2_(fmaf(x[q], kLog2e, bl + cq[q]));
+        for (int g = 0; g < 4; ++g) {   // node terms c_n (re-read per block: registers)
+          const float4 cv = *(const float4*)(ns_c + 8 * g + 4 * h);
+          p[4 * g] = exp2_(fmaf(x[4 * g], kLog2e, bl + cv.x));
+          p[4 * g + 1] = exp2_(fmaf(x[4 * g + 1], kLog2e, bl + cv.y));
+          p[4 * g + 2] = exp2_(fmaf(x[4 * g + 2], kLog2e, bl + cv.z));
+          p[4 * g + 3] = exp2_(fmaf(x[4 * g + 3], kLog2e, bl + cv.w));
+        }
         // the sparse arcs of the gathered lattice: dlogits[n][blank] -= wb_n, dlogits[n][y_u] -=
         // wy_n (one or two blocks per column), so dW, d bias and dZ all take them from p
         const int vg0 = (vb0 + lvb) * 32;
@@ -1018,7 +1034,11 @@ __global__ void __launch_bounds__(256) joint_bwd_kernel(JointArgs a) {
         for (int s2 = 0; s2 < 2; ++s2) {
           pf[s2] = pack8(p + 8 * s2);
 #pragma unroll
-          for (int jb = 0; jb < 2; ++jb) acc[k][jb] = mfma32(pf[s2], zT[s2][jb], acc[k][jb]);
+          for (int jb = 0; jb < 2; ++jb)   // z^T fragments re-read per block (registers)
+            acc[k][jb] = mfma32(pf[s2],
+                                cat8(tr_rd(zimg, 16 * s2 + 4 * h, jb * 32 + 16 * g1, lane),
+                                     tr_rd(zimg, 16 * s2 + 8 + 4 * h, jb * 32 + 16 * g1, lane)),
+                                acc[k][jb]);
         }
         // p^T through the wave's image: registers 4g..4g+3 are rows n = 8g + 4h .. +3 of column
         // v = lane & 31 -> 8 bytes at [v][8g + 4h] (whole packed dwords: element-wise bf16
@@ -1053,36 +1073,53 @@ __global__ void __launch_bounds__(256) joint_bwd_kernel(JointArgs a) {
         const int j = jb * 32 + (lane & 31);
         float sp = 0.0f;
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {   // nodes 8g + 4h .. +3 = registers 4g .. 4g+3
-          float* de4 = dew + j * BwdLds::kDeP + 8 * g + 4 * h;
-          float4 dv = u > ua ? *(const float4*)de4 : make_float4(0.f, 0.f, 0.f, 0.f);
-          float o[4];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int q = 4 * g + e, n = 8 * g + 4 * h + e;
-            o[e] = Y[jb][q] * z32[n * 64 + j];
-            sp += o[e];
-          }
-          dv.x += o[0];
-          dv.y += o[1];
-          dv.z += o[2];
-          dv.w += o[3];
-          *(float4*)de4 = dv;
+        for (int q = 0; q < 16; ++q) {   // register q = node (q & 3) + 8 (q >> 2) + 4 h
+          const int n = (q & 3) + 8 * (q >> 2) + 4 * h;
+          const float o = Y[jb][q] * z32[n * 64 + j];
+          dacc[jb][q] += o;
+          sp += o;
         }
         sp += __shfl_xor(sp, 32);
         if (h == 0) red[w * 64 + j] = sp;
       }
+      // the column's one barrier: its d pred partials and the next column's operands are
+      // complete, and this column's buffer is free for column u + 2
+      lds_barrier();
+      if (th < 64) {   // d pred of this column: the wave partials (red buffers alternate)
+        float s = 0.0f;
+#pragma unroll
+        for (int ww = 0; ww < kJW; ++ww) s += red[ww * 64 + th];
+        a.d_pred[(((int64_t)b * ntbp + vh * a.ntb + tb) * r.U1 + u) * kJ + th] = s;
+      }
     }
-    lds_barrier();
-    if (ua < ue && th < 64) {
-      const float s = red[th] + red[64 + th] + red[128 + th] + red[192 + th];
-      a.d_pred[(((int64_t)b * ntbp + vh * a.ntb + tb) * r.U1 + ue - 1) * kJ + th] = s;
+    // d enc of the task: the 8 waves' register partials meet in 4 LDS slots (waves w and w + 4
+    // share slot w & 3, in two rounds), then 8 values per thread, j fastest (coalesced)
+    float* slotp = dep + (w & 3) * 64 * BwdLds::kDeP;
+#pragma unroll
+    for (int rnd = 0; rnd < 2; ++rnd) {
+      if ((w >> 2) == rnd) {
+#pragma unroll
+        for (int jb = 0; jb < 2; ++jb) {
+          const int j = jb * 32 + (lane & 31);
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {   // nodes 8g + 4h .. +3 = registers 4g .. 4g+3
+            float4* de4 = (float4*)(slotp + j * BwdLds::kDeP + 8 * g + 4 * h);
+            float4 v = make_float4(dacc[jb][4 * g], dacc[jb][4 * g + 1], dacc[jb][4 * g + 2],
+                                   dacc[jb][4 * g + 3]);
+            if (rnd) {
+              const float4 o = *de4;
+              v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+            }
+            *de4 = v;
+          }
+        }
+      }
+      lds_barrier();
     }
-    // d enc of the task: the 4 waves' partials, 8 values per thread, j fastest (coalesced)
     float* dst = a.d_enc + ((int64_t)(vh * a.nus + us) * r.B + b) * r.T * kJ;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int e = th + 256 * i, n = e >> 6, j = e & 63;
+    for (int i = 0; i < 32 * 64 / (64 * kJW); ++i) {
+      const int e = th + 64 * kJW * i, n = e >> 6, j = e & 63;
       const int tq = tb * 32 + n;
       float s = 0.0f;
       if (ua < ue) {
@@ -1096,7 +1133,7 @@ __global__ void __launch_bounds__(256) joint_bwd_kernel(JointArgs a) {
   float* dw = a.dW + (int64_t)slot * r.V * kJ;
 #pragma unroll
   for (int k = 0; k < kVbW; ++k) {
-    const int lvb = w + 4 * k;
+    const int lvb = w + kJW * k;
     if (lvb >= nvw) continue;
     const int vbg = vb0 + lvb;
 #pragma unroll
@@ -1302,6 +1339,6 @@ extern "C" int sc_rnnt_joint_bwd(const float* enc, const float* pred, const void
   static const bool ok = joint_lds_attr(joint_bwd_kernel, joint_lds_bwd());
   SC_REQUIRE(ok, "sc_rnnt_joint_bwd: LDS attribute");
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(joint_bwd_kernel, dim3(j.S * j.vs), dim3(256), joint_lds_bwd(), st, j);
+  hipLaunchKernelGGL(joint_bwd_kernel, dim3(j.S * j.vs), dim3(64 * kJW), joint_lds_bwd(), st, j);
   return launch_status("sc_rnnt_joint_bwd");
 }
