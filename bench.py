@@ -167,6 +167,24 @@ def build_workload(args, device):
     return model, CTCLoss(blank=0, zero_infinity=True), list(model.parameters()), dict(mode="ctc"), conf
 
 
+def cpu_quota():
+    """This process's CPU allowance: the cgroup v2 quota (cpu.max "quota period" -> CPUs), the
+    affinity mask and OMP_NUM_THREADS, as a string for the cpu_baseline record."""
+    parts = []
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        parts.append("cgroup cpu.max " + ("unlimited" if q == "max" else
+                                          f"{int(q) / int(per):g} CPUs ({q}/{per})"))
+    except Exception:
+        parts.append("cgroup cpu.max unreadable")
+    try:
+        parts.append(f"affinity {len(os.sched_getaffinity(0))} CPUs")
+    except Exception:
+        pass
+    parts.append(f"OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS', 'unset')}")
+    return ", ".join(parts)
+
+
 def cpu_baseline(args):
     """Oracle (numpy port) of the same step on a bounded sample: B=32, T=args.cpu_seq."""
     from oracle import lucy_step
@@ -192,6 +210,7 @@ def cpu_baseline(args):
                       f"(U~[{T // 30},{T // 10}]), {args.layers}x{args.hidden}, 1 step, "
                       f"{dt:.1f} s on {model} (os.cpu_count={os.cpu_count()}, BLAS threads="
                       f"{threads} = this job's CPU share)",
+            "cpu_quota": cpu_quota(),
             "c1_nn_lstm": c1_lstm_baseline()}
 
 

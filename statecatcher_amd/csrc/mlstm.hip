@@ -597,11 +597,17 @@ __global__ void __launch_bounds__(512, 1) mlstm_bw_walk(MArgs a) {
   __shared__ __attribute__((aligned(16))) T Am[kL * LL];
   __shared__ float sb[kL], si[kL], mt[kL], rowf[kL], es[kL], dden[kL], nk[DQ], dnk[DQ];
   __shared__ float qpart[NI * kL], kpart[NI * kL], dnp[4 * DQ], smax[16];
-  // dC~ tiles q = w + 8 p: rows i0 = 16 (q / NJ), cols j0 = 16 (q % NJ)
+  // dC~ tiles: the waves form a 2 x 4 grid over the NI x NJ tiles, wave w owning the BI x BJ
+  // block (w >> 2, w & 3); tile p = a BJ + b is at rows 16 (BI (w >> 2) + a), cols 16 (BJ (w & 3)
+  // + b): per k-step the block's BI + BJ fragments feed BI BJ MFMAs
+  static_assert(NI % 2 == 0 && NJ % 4 == 0, "2 x 4 wave grid");
+  constexpr int BI = NI / 2, BJ = NJ / 4;
+  static_assert(BI * BJ == PC, "block = the wave's tiles");
+  const int ib0 = BI * (w >> 2), jb0 = BJ * (w & 3);
   f32x4 acc[PC];
 #pragma unroll
   for (int p = 0; p < PC; ++p) {
-    const int q = w + 8 * p, i0 = 16 * (q / NJ), j0 = 16 * (q % NJ);
+    const int i0 = 16 * (ib0 + p / BJ), j0 = 16 * (jb0 + p % BJ);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int i = i0 + 4 * (lane >> 4) + r, j = j0 + (lane & 15);
@@ -831,48 +837,52 @@ __global__ void __launch_bounds__(512, 1) mlstm_bw_walk(MArgs a) {
     }
     __syncthreads();
     const float inv = 1.0f / S;
-    // ---- dq = dA K + rowf (Dn C~_k^T + dden n~_k): 4 x NI tiles ----
-#pragma unroll 1
-    for (int jb = w; jb < (ML_ABL(64) ? 0 : 4 * NI); jb += 8) {
-      const int tr = jb / NI, ci = jb % NI;
-      // every fragment of the job is read before its first MFMA (the two causal k-steps always:
-      // dA's tiles above the diagonal are zero), so the LDS latency is paid once per job
-      V8 fa[2], fb[2], ga[DV / 32], gb[DV / 32];
+    // ---- dq = dA K + rowf (Dn C~_k^T + dden n~_k): 4 x NI tiles, wave w the row block
+    // tr = w >> 1 and NI / 2 column blocks: each A fragment feeds NI / 2 MFMAs.  (The causal
+    // chain always takes both k-steps: dA's tiles above the diagonal are zero.) ----
+    if (!ML_ABL(64)) {
+      constexpr int NC2 = NI / 2;
+      const int tr = w >> 1, c0 = (w & 1) * NC2;
+      f32x4 d4[NC2], e4[NC2];
+#pragma unroll
+      for (int c = 0; c < NC2; ++c) d4[c] = e4[c] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
-        fa[kk] = frag<V8, T>(dA, LL, 16 * tr, 32 * kk, lane);
-        fb[kk] = frag_t<V8, T>(Ks, LQ, 32 * kk, 16 * ci, lane);
+        const V8 fa = frag<V8, T>(dA, LL, 16 * tr, 32 * kk, lane);
+#pragma unroll
+        for (int c = 0; c < NC2; ++c)
+          d4[c] = M::mma(fa, frag_t<V8, T>(Ks, LQ, 32 * kk, 16 * (c0 + c), lane), d4[c]);
       }
 #pragma unroll
       for (int kk = 0; kk < DV / 32; ++kk) {
-        ga[kk] = frag<V8, T>(Dn, LV, 16 * tr, 32 * kk, lane);
-        gb[kk] = frag_t<V8, T>(CS, LQ, 32 * kk, 16 * ci, lane);
+        const V8 ga = frag<V8, T>(Dn, LV, 16 * tr, 32 * kk, lane);
+#pragma unroll
+        for (int c = 0; c < NC2; ++c)
+          e4[c] = M::mma(ga, frag_t<V8, T>(CS, LQ, 32 * kk, 16 * (c0 + c), lane), e4[c]);
       }
-      f32x4 d4 = {0.f, 0.f, 0.f, 0.f}, e4 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) d4 = M::mma(fa[kk], fb[kk], d4);
+      for (int c = 0; c < NC2; ++c) {
+        const int ci = c0 + c, i = 16 * ci + (lane & 15);
+        const float nki = nk[i];
+        float qd[4];
 #pragma unroll
-      for (int kk = 0; kk < DV / 32; ++kk) e4 = M::mma(ga[kk], gb[kk], e4);
-      const int i = 16 * ci + (lane & 15);
-      const float nki = nk[i];
-      float qd[4];
+        for (int r = 0; r < 4; ++r) {
+          const int tt = 16 * tr + 4 * (lane >> 4) + r;
+          const float v = d4[c][r] + rowf[tt] * (e4[c][r] + dden[tt] * nki);
+          dQg[(t0 + tt) * a.qt + i] = out16<DT, IO>(v * inv);
+          qd[r] = sum16(v * (float)Qs[tt * LQ + i]);
+        }
+        if ((lane & 15) == 0) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int tt = 16 * tr + 4 * (lane >> 4) + r;
-        const float v = d4[r] + rowf[tt] * (e4[r] + dden[tt] * nki);
-        dQg[(t0 + tt) * a.qt + i] = out16<DT, IO>(v * inv);
-        qd[r] = sum16(v * (float)Qs[tt * LQ + i]);
-      }
-      if ((lane & 15) == 0) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) qpart[ci * kL + 16 * tr + 4 * (lane >> 4) + r] = qd[r];
+          for (int r = 0; r < 4; ++r) qpart[ci * kL + 16 * tr + 4 * (lane >> 4) + r] = qd[r];
+        }
       }
     }
     __syncthreads();
     // ---- dC~_{k+1} image replaces C~_k ----
 #pragma unroll
     for (int p = 0; p < PC; ++p) {
-      const int q = w + 8 * p, i0 = 16 * (q / NJ), j0 = 16 * (q % NJ);
+      const int i0 = 16 * (ib0 + p / BJ), j0 = 16 * (jb0 + p % BJ);
       v4t c;
 #pragma unroll
       for (int r = 0; r < 4; ++r) c[r] = (T)acc[p][r];
@@ -885,77 +895,94 @@ __global__ void __launch_bounds__(512, 1) mlstm_bw_walk(MArgs a) {
       a.qdq[(int64_t)bh * a.T + t0 + tid] = sq * inv;
     }
     __syncthreads();
-    // ---- dk = dA^T Q + es (V dC~^T + dn~): 4 x NI tiles; dv = A^T Dn + es (K dC~): 4 x NJ ----
-#pragma unroll 1
-    for (int jb = w; jb < (ML_ABL(128) ? 0 : 4 * NI + 4 * NJ); jb += 8) {
-      f32x4 d4 = {0.f, 0.f, 0.f, 0.f}, e4 = {0.f, 0.f, 0.f, 0.f};
-      if (jb < 4 * NI) {
-        const int sr = jb / NI, ci = jb % NI;
-        V8 fa[2], fb[2], ga[DV / 32], gb[DV / 32];   // (as the dq job)
+    // ---- dk = dA^T Q + es (V dC~^T + dn~): 4 x NI tiles; dv = A^T Dn + es (K dC~): 4 x NJ.
+    // Wave w: key row block sr = w >> 1, NI / 2 dk column blocks, then NJ / 2 dv column blocks
+    // in passes of NI / 2 (register-blocked as the dq phase) ----
+    if (!ML_ABL(128)) {
+      constexpr int NC2 = NI / 2;
+      const int sr = w >> 1;
+      {
+        const int c0 = (w & 1) * NC2;
+        f32x4 d4[NC2], e4[NC2];
+#pragma unroll
+        for (int c = 0; c < NC2; ++c) d4[c] = e4[c] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
-          fa[kk] = frag_t<V8, T>(dA, LL, 32 * kk, 16 * sr, lane);
-          fb[kk] = frag_t<V8, T>(Qs, LQ, 32 * kk, 16 * ci, lane);
+          const V8 fa = frag_t<V8, T>(dA, LL, 32 * kk, 16 * sr, lane);
+#pragma unroll
+          for (int c = 0; c < NC2; ++c)
+            d4[c] = M::mma(fa, frag_t<V8, T>(Qs, LQ, 32 * kk, 16 * (c0 + c), lane), d4[c]);
         }
 #pragma unroll
         for (int kk = 0; kk < DV / 32; ++kk) {
-          ga[kk] = frag<V8, T>(Vs, LV, 16 * sr, 32 * kk, lane);
-          gb[kk] = frag_t<V8, T>(CS, LQ, 32 * kk, 16 * ci, lane);
+          const V8 ga = frag<V8, T>(Vs, LV, 16 * sr, 32 * kk, lane);
+#pragma unroll
+          for (int c = 0; c < NC2; ++c)
+            e4[c] = M::mma(ga, frag_t<V8, T>(CS, LQ, 32 * kk, 16 * (c0 + c), lane), e4[c]);
         }
 #pragma unroll
-        for (int kk = 0; kk < 2; ++kk) d4 = M::mma(fa[kk], fb[kk], d4);
+        for (int c = 0; c < NC2; ++c) {
+          const int ci = c0 + c, i = 16 * ci + (lane & 15);
+          const float dni = dnk[i];
+          float kd[4];
 #pragma unroll
-        for (int kk = 0; kk < DV / 32; ++kk) e4 = M::mma(ga[kk], gb[kk], e4);
-        const int i = 16 * ci + (lane & 15);
-        const float dni = dnk[i];
-        float kd[4];
+          for (int r = 0; r < 4; ++r) {
+            const int s = 16 * sr + 4 * (lane >> 4) + r;
+            const float v = d4[c][r] + es[s] * (e4[c][r] + dni);
+            dKg[(t0 + s) * a.qt + i] = out16<DT, IO>(v * inv);
+            kd[r] = sum16(v * (float)Ks[s * LQ + i]);
+          }
+          if ((lane & 15) == 0) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int s = 16 * sr + 4 * (lane >> 4) + r;
-          const float v = d4[r] + es[s] * (e4[r] + dni);
-          dKg[(t0 + s) * a.qt + i] = out16<DT, IO>(v * inv);
-          kd[r] = sum16(v * (float)Ks[s * LQ + i]);
+            for (int r = 0; r < 4; ++r) kpart[ci * kL + 16 * sr + 4 * (lane >> 4) + r] = kd[r];
+          }
         }
-        if ((lane & 15) == 0) {
+      }
+      constexpr int NV2 = NJ / 2;
+      static_assert(NV2 % NC2 == 0, "dv passes");
+#pragma unroll 1
+      for (int pass = 0; pass < NV2 / NC2; ++pass) {
+        const int c0 = (w & 1) * NV2 + pass * NC2;
+        f32x4 d4[NC2], e4[NC2];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) kpart[ci * kL + 16 * sr + 4 * (lane >> 4) + r] = kd[r];
-        }
-      } else {
-        const int jv = jb - 4 * NI, sr = jv / NJ, cj = jv % NJ;
-        V8 fa[2], fb[2], ga[DQ / 32], gb[DQ / 32];
+        for (int c = 0; c < NC2; ++c) d4[c] = e4[c] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
-          fa[kk] = frag_t<V8, T>(Am, LL, 32 * kk, 16 * sr, lane);
-          fb[kk] = frag_t<V8, T>(Dn, LV, 32 * kk, 16 * cj, lane);
+          const V8 fa = frag_t<V8, T>(Am, LL, 32 * kk, 16 * sr, lane);
+#pragma unroll
+          for (int c = 0; c < NC2; ++c)
+            d4[c] = M::mma(fa, frag_t<V8, T>(Dn, LV, 32 * kk, 16 * (c0 + c), lane), d4[c]);
         }
 #pragma unroll
         for (int kk = 0; kk < DQ / 32; ++kk) {
-          ga[kk] = frag<V8, T>(Ks, LQ, 16 * sr, 32 * kk, lane);
-          gb[kk] = frag<V8, T>(CS, LQ, 16 * cj, 32 * kk, lane);
+          const V8 ga = frag<V8, T>(Ks, LQ, 16 * sr, 32 * kk, lane);
+#pragma unroll
+          for (int c = 0; c < NC2; ++c)
+            e4[c] = M::mma(ga, frag<V8, T>(CS, LQ, 16 * (c0 + c), 32 * kk, lane), e4[c]);
         }
 #pragma unroll
-        for (int kk = 0; kk < 2; ++kk) d4 = M::mma(fa[kk], fb[kk], d4);
+        for (int c = 0; c < NC2; ++c) {
+          const int j = 16 * (c0 + c) + (lane & 15);
 #pragma unroll
-        for (int kk = 0; kk < DQ / 32; ++kk) e4 = M::mma(ga[kk], gb[kk], e4);
-        const int j = 16 * cj + (lane & 15);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int s = 16 * sr + 4 * (lane >> 4) + r;
-          dVg[(t0 + s) * a.vt + j] = out16<DT, IO>((d4[r] + es[s] * e4[r]) * inv);
+          for (int r = 0; r < 4; ++r) {
+            const int s = 16 * sr + 4 * (lane >> 4) + r;
+            dVg[(t0 + s) * a.vt + j] = out16<DT, IO>((d4[c][r] + es[s] * e4[c][r]) * inv);
+          }
         }
       }
     }
     // ---- state gradient to the chunk start: dC~_k = decay dC~_{k+1} + Qr^T Dn ----
 #pragma unroll
-    for (int p = 0; p < PC; ++p) {
-      const int q = w + 8 * p, i0 = 16 * (q / NJ), j0 = 16 * (q % NJ);
-      f32x4 c = acc[p] * decay;
+    for (int p = 0; p < PC; ++p) acc[p] *= decay;
 #pragma unroll
-      for (int kk = 0; kk < (ML_ABL(256) ? 0 : kL / 32); ++kk)
-        c = M::mma(frag_t<V8, T>(Qr, LQ, 32 * kk, i0, lane),
-                   frag_t<V8, T>(Dn, LV, 32 * kk, j0, lane), c);
-      acc[p] = c;
-      __builtin_amdgcn_sched_barrier(0);
+    for (int kk = 0; kk < (ML_ABL(256) ? 0 : kL / 32); ++kk) {
+      V8 fq[BI], fd[BJ];
+#pragma unroll
+      for (int x = 0; x < BI; ++x) fq[x] = frag_t<V8, T>(Qr, LQ, 32 * kk, 16 * (ib0 + x), lane);
+#pragma unroll
+      for (int y = 0; y < BJ; ++y) fd[y] = frag_t<V8, T>(Dn, LV, 32 * kk, 16 * (jb0 + y), lane);
+#pragma unroll
+      for (int p = 0; p < PC; ++p) acc[p] = M::mma(fq[p / BJ], fd[p % BJ], acc[p]);
     }
     // dn~ partial sums sum_t dden_t Qr[t][i] over four 16-step quarters (combined next chunk)
     if (tid < 4 * DQ) {
@@ -981,7 +1008,7 @@ __global__ void __launch_bounds__(512, 1) mlstm_bw_walk(MArgs a) {
   const float inv = 1.0f / S;
 #pragma unroll
   for (int p = 0; p < PC; ++p) {
-    const int q = w + 8 * p, i0 = 16 * (q / NJ), j0 = 16 * (q % NJ);
+    const int i0 = 16 * (ib0 + p / BJ), j0 = 16 * (jb0 + p % BJ);
 #pragma unroll
     for (int r = 0; r < 4; ++r)
       a.dCs[((int64_t)bh * DQ + i0 + 4 * (lane >> 4) + r) * DV + j0 + (lane & 15)] = acc[p][r] * inv;
