@@ -477,15 +477,16 @@ __global__ void __launch_bounds__(256, 2) mlstm_fw_walk(MArgs a) {
         zi[r] = 1.0f / (fmaxf(fabsf(dn), expf(-mts[t])) + a.eps);
       }
       f32x4 hv[TJ];
+      // both k-steps of M V always (M is zero right of the diagonal block); the row block's M
+      // fragments once for the TJ column blocks
+      V8 ma[2];
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) ma[kk] = frag<V8, T>(Ms, LC, 16 * w, 32 * kk, lane);
 #pragma unroll
       for (int cj = 0; cj < TJ; ++cj) {
-        // both k-steps of M V always (M is zero right of the diagonal block), fragments first
-        V8 ma[2], vb[2], cb2[DQ / 32];
+        V8 vb[2], cb2[DQ / 32];
 #pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
-          ma[kk] = frag<V8, T>(Ms, LC, 16 * w, 32 * kk, lane);
-          vb[kk] = frag_t<V8, T>(Vs, LC, 32 * kk, 16 * cj, lane);
-        }
+        for (int kk = 0; kk < 2; ++kk) vb[kk] = frag_t<V8, T>(Vs, LC, 32 * kk, 16 * cj, lane);
 #pragma unroll
         for (int kk = 0; kk < DQ / 32; ++kk) cb2[kk] = frag<V8, T>(CT, LQ, 16 * cj, 32 * kk, lane);
         f32x4 h4 = {0.f, 0.f, 0.f, 0.f}, e4 = {0.f, 0.f, 0.f, 0.f};
