@@ -70,6 +70,8 @@ _SIGS = {
     "sc_mlstm_bwd_io": (_i32, [_vp, _vp, _vp, _i32, _i32, _fp, _fp, _vp, _vp, _fp, _fp, _vp, _fp, _fp,
                               _fp, _fp, _i32, _i32, _i32, _i32, _c.c_float, _fp, _fp, _vp, _vp, _vp,
                               _fp, _fp, _vp, _vp]),
+    "sc_mlstm_gate_bwd": (_i32, [_fp, _fp, _fp, _i32, _i32, _fp, _vp, _vp, _i32, _i64, _i32, _i32,
+                                _c.c_float, _vp]),
     "sc_xlstm_part_rows": (_i32, [_i64]),
     "sc_rmsnorm_fwd": (_i32, [_vp, _fp, _vp, _fp, _i64, _i32, _c.c_float, _vp]),
     "sc_rmsnorm_bwd": (_i32, [_vp, _vp, _fp, _fp, _vp, _fp, _i64, _i32, _vp]),

@@ -1087,6 +1087,68 @@ int set_layout(MArgs& a, const int64_t* layout, int DQ, int DV, const char* what
   return 0;
 }
 
+// ----------------------------------------------------------------- gate gradients ----
+// d igate = kdk, d fgate_t = sigmoid(-f_t) sum_{r>=t} (qdq_r - kdk_r) for one sequence per wave
+// (lane = a contiguous T/64-step segment: segment suffix sums, then the suffix over the lanes
+// above).  mode 0 writes d fgate fp32 [BH][T] (MLSTMFn); mode 1 writes both gate gradients
+// through the soft cap's backward, in bf16 with the roundings of the torch chain it replaces
+// (x / cap, tanh, g cap, tanh_backward, / cap: each op's result rounded to bf16), into the
+// projection gradient at [b][t][io + h] / [b][t][fo + h] (MLSTMCoreFn).
+__device__ __forceinline__ float rbf16(float x) { return (float)(__bf16)x; }
+
+__device__ __forceinline__ float softcap_bwd_bf16(float g, float x, float cap) {
+  if (!(cap > 0.0f)) return g;
+  const float y = rbf16(tanhf(rbf16(x / cap)));
+  const float t1 = rbf16(g * cap);
+  const float t2 = rbf16(t1 * (1.0f - y * y));
+  return rbf16(t2 / cap);
+}
+
+struct GateArgs {
+  const float* qdq;
+  const float* kdk;
+  const float* fg;
+  float* dfg;             // mode 0
+  const __bf16* a;        // mode 1: raw pre-activations, [B][T][ld]
+  __bf16* da;             // mode 1
+  int BH, T, NH, io, fo;
+  int64_t ld;
+  float cap;
+};
+
+__global__ void __launch_bounds__(64) mlstm_gate_bwd_kernel(GateArgs g) {
+  const int bh = blockIdx.x, lane = threadIdx.x;
+  const int seg = g.T / 64, t0 = lane * seg;
+  const int64_t base = (int64_t)bh * g.T;
+  float tot = 0.0f;
+  for (int t = t0 + seg - 1; t >= t0; --t) tot += g.qdq[base + t] - g.kdk[base + t];
+  // suffix over the lanes above: inclusive prefix sum of the reversed lane order, minus own
+  float above = 0.0f;
+  {
+    float x = tot;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const float u = __shfl_down(x, d);
+      if (lane + d < 64) x += u;
+    }
+    above = x - tot;
+  }
+  const int b = bh / g.NH, h = bh % g.NH;
+  float run = above;
+  for (int t = t0 + seg - 1; t >= t0; --t) {
+    run += g.qdq[base + t] - g.kdk[base + t];
+    const float dfg = run / (1.0f + expf(g.fg[base + t]));   // sigmoid(-f) R, as 1 / (1 + e^f)
+    if (g.dfg) {
+      g.dfg[base + t] = dfg;
+    } else {
+      const int64_t row = ((int64_t)b * g.T + t) * g.ld;
+      const float xi = (float)g.a[row + g.io + h], xf = (float)g.a[row + g.fo + h];
+      g.da[row + g.io + h] = (__bf16)softcap_bwd_bf16(rbf16(g.kdk[base + t]), xi, g.cap);
+      g.da[row + g.fo + h] = (__bf16)softcap_bwd_bf16(rbf16(dfg), xf, g.cap);
+    }
+  }
+}
+
 }  // namespace
 
 }  // namespace sc
@@ -1188,4 +1250,22 @@ extern "C" int sc_mlstm_bwd(const void* q, const void* k, const void* v, int dty
   return sc_mlstm_bwd_io(q, k, v, dtype, dtype, igate, fgate, h, dh, dcT, dnT, states_C,
                          states_n, states_m, m_rows, den_rows, BH, T, DQ, DV, eps, dstates_C,
                          dstates_n, dq, dk, dv, qdq, kdk, layout, stream);
+}
+
+extern "C" int sc_mlstm_gate_bwd(const float* qdq, const float* kdk, const float* fgate, int BH,
+                                 int T, float* dfgate, const void* a, void* da, int NH,
+                                 int64_t ld, int io, int fo, float cap, void* stream) {
+  clear_error();
+  SC_REQUIRE(BH >= 0 && T >= 0 && T % 64 == 0, "sc_mlstm_gate_bwd: T=%d (a multiple of 64)", T);
+  if (BH == 0 || T == 0) return 0;
+  SC_REQUIRE(qdq && kdk && fgate, "sc_mlstm_gate_bwd: null input");
+  SC_REQUIRE((dfgate != nullptr) != (da != nullptr), "sc_mlstm_gate_bwd: exactly one output mode");
+  if (da) {
+    SC_REQUIRE(a && NH > 0 && BH % NH == 0 && io >= 0 && fo >= 0 && ld >= fo + NH && ld >= io + NH,
+               "sc_mlstm_gate_bwd: projection layout");
+  }
+  GateArgs g{qdq, kdk, fgate, dfgate, (const __bf16*)a, (__bf16*)da, BH, T, NH > 0 ? NH : 1,
+             io, fo, ld, cap};
+  hipLaunchKernelGGL(mlstm_gate_bwd_kernel, dim3(BH), dim3(64), 0, (hipStream_t)stream, g);
+  return launch_status("sc_mlstm_gate_bwd");
 }

@@ -1042,8 +1042,9 @@ class MLSTMFn(torch.autograd.Function):
                 stream_of(qc))
         check(rc, "sc_mlstm_bwd")
         # d igate_s = k_s.dk_s ; dF_t = q_t.dq_t - k_t.dk_t ; d fgate = sigmoid(-f) revcumsum(dF)
-        dF = qdq - kdk
-        dfg = torch.sigmoid(-fg) * dF.flip(-1).cumsum(-1).flip(-1)
+        dfg = torch.empty_like(kdk)
+        check(_lib.load().sc_mlstm_gate_bwd(ptr(qdq), ptr(kdk), ptr(fg), BH, T, ptr(dfg), None, None,
+                                            0, 0, 0, 0, 0.0, stream_of(qc)), "sc_mlstm_gate_bwd")
         shp = (B, NH, T)
         return (dq.view(B, NH, T, DQ).to(qdt), dk.view(B, NH, T, DQ).to(kdt),
                 dv.view(B, NH, T, DV).to(vdt), kdk.view(shp), dfg.view(shp),
@@ -1170,13 +1171,11 @@ class MLSTMCoreFn(torch.autograd.Function):
                 ptr(den), BH, T, DQ, DV, eps, ptr(dCs), ptr(dns), dbase + qo * esz,
                 dbase + ko * esz, dbase + vo * esz, ptr(qdq), ptr(kdk), lay, stream)
         check(rc, "sc_mlstm_bwd")
-        # gate gradients as MLSTMFn returns them, then through the soft caps in a's dtype
-        dF = (qdq - kdk).view(B, NH, T)
-        dfg = torch.sigmoid(-fg) * dF.flip(-1).cumsum(-1).flip(-1)
-        dig_c = kdk.view(B, NH, T).transpose(1, 2).to(a.dtype)
-        dfg_c = dfg.transpose(1, 2).to(a.dtype)
-        da[..., io:io + NH] = _soft_cap_bwd(dig_c, a[..., io:io + NH], cap)
-        da[..., fo:fo + NH] = _soft_cap_bwd(dfg_c, a[..., fo:fo + NH], cap)
+        # gate gradients as MLSTMFn returns them, then through the soft caps with the bf16
+        # roundings of the torch chain (_soft_cap_bwd), straight into da: one kernel
+        check(lib.sc_mlstm_gate_bwd(ptr(qdq), ptr(kdk), ptr(fg), BH, T, None, base, dbase, NH, N,
+                                    io, fo, float(cap) if cap is not None else 0.0, stream),
+              "sc_mlstm_gate_bwd")
         return (da, dCs.view(B, NH, DQ, DV) if has_c0 else None,
                 dns.view(B, NH, DQ) if has_n0 else None, None,
                 _part_sum(part).to(wdt), None, None, None, None, None, None, None)

@@ -252,3 +252,37 @@ def test_fused_linear_bitwise_vs_cat_then_linear():
         res.append([y.detach(), xi.grad, bi.grad] + [w.grad for w in wi])
     for a, c in zip(*res):
         assert torch.equal(a, c)
+
+
+@pytest.mark.parametrize("cap", [15.0, None])
+def test_mlstm_gate_bwd_kernel_vs_torch_chain(cap):
+    """sc_mlstm_gate_bwd against the torch chain it replaced in MLSTMFn / MLSTMCoreFn:
+    d fgate = sigmoid(-f) * flip(cumsum(flip(qdq - kdk))) (fp32; the kernel's suffix sums run in
+    another order: 1e-5 relative), and the soft-cap backward in bf16 (ops._soft_cap_bwd): the
+    input-gate gradient bitwise, the forget-gate one bitwise given the kernel's own fp32 d fgate."""
+    from statecatcher_amd import _lib
+    from statecatcher_amd.ops import _soft_cap_bwd, ptr
+    g = torch.Generator(device=DEV).manual_seed(4)
+    B, NH, T = 3, 4, 384
+    io, fo, N = 8, 20, 40
+    qdq = torch.randn(B * NH, T, device=DEV, generator=g)
+    kdk = torch.randn(B * NH, T, device=DEV, generator=g) * 0.5
+    fg = torch.randn(B * NH, T, device=DEV, generator=g) * 3 + 2
+    a = (torch.randn(B, T, N, device=DEV, generator=g) * 20).to(torch.bfloat16)
+    lib = _lib.load()
+    dfg = torch.empty_like(kdk)
+    assert lib.sc_mlstm_gate_bwd(ptr(qdq), ptr(kdk), ptr(fg), B * NH, T, ptr(dfg), None, None, 0, 0,
+                                 0, 0, 0.0, None) == 0
+    da = torch.zeros_like(a)
+    assert lib.sc_mlstm_gate_bwd(ptr(qdq), ptr(kdk), ptr(fg), B * NH, T, None, ptr(a), ptr(da), NH,
+                                 N, io, fo, cap or 0.0, None) == 0
+    torch.cuda.synchronize()
+    ref_dfg = torch.sigmoid(-fg) * (qdq - kdk).flip(-1).cumsum(-1).flip(-1)
+    torch.testing.assert_close(dfg, ref_dfg, rtol=1e-5, atol=1e-5 * float(ref_dfg.abs().max()))
+    dig_c = kdk.view(B, NH, T).transpose(1, 2).to(torch.bfloat16)
+    dfg_c = dfg.view(B, NH, T).transpose(1, 2).to(torch.bfloat16)
+    ref_i = _soft_cap_bwd(dig_c, a[..., io:io + NH], cap)
+    ref_f = _soft_cap_bwd(dfg_c, a[..., fo:fo + NH], cap)
+    assert torch.equal(da[..., io:io + NH], ref_i)
+    assert torch.equal(da[..., fo:fo + NH], ref_f)
+    assert not da[..., :io].any() and not da[..., io + NH:fo].any() and not da[..., fo + NH:].any()
