@@ -488,10 +488,10 @@ int sc_mlstm_bwd_io(const void* q, const void* k, const void* v, int dtype, int 
  * and the forget-gate pre-activations fgate (fp32 [BH][T], after any soft cap):
  *   d igate = kdk,  d fgate_t = sigmoid(-fgate_t) sum_{r >= t} (qdq_r - kdk_r).
  * Either dfgate != NULL (fp32 [BH][T]; d igate is kdk itself), or da != NULL: both gradients
- * through the xLSTM gate soft cap (cap > 0; cap <= 0 = none) in bf16, with the roundings of the
- * torch chain g * cap, tanh(x / cap), tanh_backward, / cap, written into the projection gradient
- * da at [b][t][io + h] and [b][t][fo + h] (row stride ld elements), a holding the raw bf16
- * pre-activations at the same positions; sequence bh = b NH + h.
+ * through the xLSTM gate soft cap (cap > 0; cap <= 0 = none): g (1 - tanh(x / cap)^2) in fp32,
+ * rounded once to bf16, written into the projection gradient da at [b][t][io + h] and
+ * [b][t][fo + h] (row stride ld elements), a holding the raw bf16 pre-activations at the same
+ * positions; sequence bh = b NH + h.
  */
 int sc_mlstm_gate_bwd(const float* qdq, const float* kdk, const float* fgate, int BH, int T,
                       float* dfgate, const void* a, void* da, int NH, int64_t ld, int io, int fo,

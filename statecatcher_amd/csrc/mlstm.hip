@@ -1091,17 +1091,16 @@ int set_layout(MArgs& a, const int64_t* layout, int DQ, int DV, const char* what
 // d igate = kdk, d fgate_t = sigmoid(-f_t) sum_{r>=t} (qdq_r - kdk_r) for one sequence per wave
 // (lane = a contiguous T/64-step segment: segment suffix sums, then the suffix over the lanes
 // above).  mode 0 writes d fgate fp32 [BH][T] (MLSTMFn); mode 1 writes both gate gradients
-// through the soft cap's backward, in bf16 with the roundings of the torch chain it replaces
-// (x / cap, tanh, g cap, tanh_backward, / cap: each op's result rounded to bf16), into the
-// projection gradient at [b][t][io + h] / [b][t][fo + h] (MLSTMCoreFn).
-__device__ __forceinline__ float rbf16(float x) { return (float)(__bf16)x; }
+// through the soft cap's backward into the projection gradient at [b][t][io + h] / [b][t][fo + h]
+// (MLSTMCoreFn).
 
-__device__ __forceinline__ float softcap_bwd_bf16(float g, float x, float cap) {
+// d/dx cap tanh(x / cap) = 1 - tanh(x / cap)^2, in fp32 on the fp32 gradient, one bf16 rounding
+// (the torch chain it replaces rounds each of its five ops to bf16; near saturation 1 - y^2 of a
+// bf16 y keeps only a few bits)
+__device__ __forceinline__ float softcap_bwd(float g, float x, float cap) {
   if (!(cap > 0.0f)) return g;
-  const float y = rbf16(tanhf(rbf16(x / cap)));
-  const float t1 = rbf16(g * cap);
-  const float t2 = rbf16(t1 * (1.0f - y * y));
-  return rbf16(t2 / cap);
+  const float y = tanhf(x / cap);
+  return g * (1.0f - y * y);
 }
 
 struct GateArgs {
@@ -1143,8 +1142,8 @@ __global__ void __launch_bounds__(64) mlstm_gate_bwd_kernel(GateArgs g) {
     } else {
       const int64_t row = ((int64_t)b * g.T + t) * g.ld;
       const float xi = (float)g.a[row + g.io + h], xf = (float)g.a[row + g.fo + h];
-      g.da[row + g.io + h] = (__bf16)softcap_bwd_bf16(rbf16(g.kdk[base + t]), xi, g.cap);
-      g.da[row + g.fo + h] = (__bf16)softcap_bwd_bf16(rbf16(dfg), xf, g.cap);
+      g.da[row + g.io + h] = (__bf16)softcap_bwd(g.kdk[base + t], xi, g.cap);
+      g.da[row + g.fo + h] = (__bf16)softcap_bwd(dfg, xf, g.cap);
     }
   }
 }

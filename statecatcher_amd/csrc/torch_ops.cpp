@@ -506,6 +506,28 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> mlstm_bwd_met
           at::empty({d.B, d.NH, d.T}, fo)};
 }
 
+// d fgate = sigmoid(-fgate) * (reverse cumulative sum of qdq - kdk) over the last dim [.., T]
+Tensor mlstm_gate_bwd_hip(const Tensor& qdq_in, const Tensor& kdk_in, const Tensor& fg_in) {
+  c10::DeviceGuard guard(qdq_in.device());
+  TORCH_CHECK(qdq_in.sizes() == kdk_in.sizes() && kdk_in.sizes() == fg_in.sizes() &&
+                  qdq_in.dim() >= 1 && qdq_in.size(-1) % 64 == 0,
+              "statecatcher::mlstm_gate_bwd: qdq / kdk / fgate [.., T], T % 64 == 0");
+  Tensor qdq = f32c(qdq_in), kdk = f32c(kdk_in), fg = f32c(fg_in);
+  Tensor dfg = at::empty_like(qdq);
+  const int64_t T = qdq.size(-1), BH = T ? qdq.numel() / T : 0;
+  sc_check(sc_mlstm_gate_bwd(qdq.data_ptr<float>(), kdk.data_ptr<float>(), fg.data_ptr<float>(),
+                             (int)BH, (int)T, dfg.data_ptr<float>(), nullptr, nullptr, 0, 0, 0, 0,
+                             0.0f, stream_for(qdq)),
+           "statecatcher::mlstm_gate_bwd");
+  return dfg;
+}
+
+Tensor mlstm_gate_bwd_meta(const Tensor& qdq, const Tensor& kdk, const Tensor& fg) {
+  TORCH_CHECK(qdq.sizes() == kdk.sizes() && kdk.sizes() == fg.sizes(),
+              "statecatcher::mlstm_gate_bwd: shapes");
+  return at::empty(qdq.sizes(), qdq.options().dtype(at::kFloat));
+}
+
 // ------------------------------------------------------------------- fused RNN-T joiner ------
 // enc_p [B,T,J], pred_p [B,U+1,J] (the joiner's enc_proj / pred_proj outputs), W [V,J], bias
 // [V]: RNNTPredictorJoiner's joint + log_softmax + warp_rnnt's gathered lattice
@@ -638,6 +660,7 @@ TORCH_LIBRARY(statecatcher, m) {
         "Tensor? dc_last, Tensor? dn_last, Tensor c_states, Tensor n_states, Tensor m_states, "
         "Tensor m_rows, Tensor den_rows, float eps=1e-6) -> (Tensor dq, Tensor dk, Tensor dv, "
         "Tensor dc0, Tensor dn0, Tensor qdq, Tensor kdk)");
+  m.def("mlstm_gate_bwd(Tensor qdq, Tensor kdk, Tensor fgate) -> Tensor");
   m.def("rnnt_joint_fwd(Tensor enc_p, Tensor pred_p, Tensor W, Tensor bias, Tensor labels, "
         "Tensor frames_lengths, Tensor labels_lengths, int blank=0) -> (Tensor nll, Tensor workspace)");
   m.def("rnnt_joint_bwd(Tensor enc_p, Tensor pred_p, Tensor W, Tensor bias, Tensor labels, "
@@ -658,6 +681,7 @@ TORCH_LIBRARY_IMPL(statecatcher, CUDA, m) {
   m.impl("ctc_greedy_decode", &ctc_greedy_decode_hip);
   m.impl("mlstm_fwd", &mlstm_fwd_hip);
   m.impl("mlstm_bwd", &mlstm_bwd_hip);
+  m.impl("mlstm_gate_bwd", &mlstm_gate_bwd_hip);
   m.impl("rnnt_joint_fwd", &rnnt_joint_fwd_hip);
   m.impl("rnnt_joint_bwd", &rnnt_joint_bwd_hip);
 }
@@ -675,6 +699,7 @@ TORCH_LIBRARY_IMPL(statecatcher, Meta, m) {
   m.impl("ctc_greedy_decode", &ctc_greedy_decode_meta);
   m.impl("mlstm_fwd", &mlstm_fwd_meta);
   m.impl("mlstm_bwd", &mlstm_bwd_meta);
+  m.impl("mlstm_gate_bwd", &mlstm_gate_bwd_meta);
   m.impl("rnnt_joint_fwd", &rnnt_joint_fwd_meta);
   m.impl("rnnt_joint_bwd", &rnnt_joint_bwd_meta);
 }

@@ -1171,8 +1171,8 @@ class MLSTMCoreFn(torch.autograd.Function):
                 ptr(den), BH, T, DQ, DV, eps, ptr(dCs), ptr(dns), dbase + qo * esz,
                 dbase + ko * esz, dbase + vo * esz, ptr(qdq), ptr(kdk), lay, stream)
         check(rc, "sc_mlstm_bwd")
-        # gate gradients as MLSTMFn returns them, then through the soft caps with the bf16
-        # roundings of the torch chain (_soft_cap_bwd), straight into da: one kernel
+        # gate gradients as MLSTMFn returns them, then through the soft caps (fp32, one bf16
+        # rounding; _soft_cap_bwd's torch chain rounds each op) straight into da: one kernel
         check(lib.sc_mlstm_gate_bwd(ptr(qdq), ptr(kdk), ptr(fg), BH, T, None, base, dbase, NH, N,
                                     io, fo, float(cap) if cap is not None else 0.0, stream),
               "sc_mlstm_gate_bwd")

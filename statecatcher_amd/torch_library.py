@@ -25,7 +25,7 @@ import torch
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_torch_ops.so")
 OPS = ("abi_version", "lucy_scan_fwd", "lucy_scan_bwd", "decay_scan_fwd", "decay_scan_bwd",
        "layer_norm_fwd", "layer_norm_bwd", "ctc_fwd", "ctc_bwd", "ctc_mean", "ctc_greedy_decode",
-       "mlstm_fwd", "mlstm_bwd", "rnnt_joint_fwd", "rnnt_joint_bwd")
+       "mlstm_fwd", "mlstm_bwd", "mlstm_gate_bwd", "rnnt_joint_fwd", "rnnt_joint_bwd")
 
 _LOADED = False
 
@@ -141,7 +141,7 @@ def _mlstm_backward(ctx, dh, dc_last, dns, dms, dcs, dmrow, dden):
     dq, dk, dv, dc0, dn0, qdq, kdk = torch.ops.statecatcher.mlstm_bwd(
         q, k, v, ig, fg, h, dh, dc_last, dn_last, cs, ns, ms, mrow, den, ctx.eps)
     # d igate_s = k_s.dk_s ; d fgate_t = sigmoid(-f_t) sum_{r >= t} (q_r.dq_r - k_r.dk_r)
-    dfg = torch.sigmoid(-fg.float()) * (qdq - kdk).flip(-1).cumsum(-1).flip(-1)
+    dfg = torch.ops.statecatcher.mlstm_gate_bwd(qdq, kdk, fg)
     has_c0, has_n0 = ctx.has
     return (dq, dk, dv, kdk.to(ig.dtype), dfg.to(fg.dtype), dc0 if has_c0 else None,
             dn0 if has_n0 else None, None, None)

@@ -185,8 +185,11 @@ def test_xlstm_block_fused_equals_torch_path():
 def test_mlstm_core_equals_composed_ops(with_state, kernel_dtype, monkeypatch):
     """ops.MLSTMCoreFn (q/k/v/o read in place from the fused projection, one gradient tensor
     written in place) against the composed path it replaces (split, soft caps, MLSTMFn,
-    GatedHeadNormFn, autograd's concatenation): same kernels and roundings, so the layer output,
-    the final state and every gradient are bit-identical.  With the reference's float16 cell the
+    GatedHeadNormFn, autograd's concatenation): the layer output and the final state are
+    bit-identical; the gradients agree to 1e-2 (relative Frobenius; measured ~1e-3): the core
+    path takes the gate gradients through the soft cap in fp32 with one bf16 rounding
+    (sc_mlstm_gate_bwd), the composed path through torch's five bf16 ops.  With the reference's
+    float16 cell the
     core path reads the bf16 projection and rounds to f16 on load (sc_mlstm_*_io) where the split
     path casts: the forward is still bit-identical; in the backward the split path also casts
     the bf16 dh to f16, which is exact only in f16's normal range, while the core path reads dh
@@ -223,7 +226,7 @@ def test_mlstm_core_equals_composed_ops(with_state, kernel_dtype, monkeypatch):
         res.append([y, c, n, m, xi.grad] + [p.grad for p in layer.parameters()] +
                    ([sti[0].grad, sti[1].grad] if sti else []))
     for i, (u, v) in enumerate(zip(*res)):
-        if kernel_dtype == "bfloat16" or i < 4:
+        if i < 4:
             assert torch.equal(u, v), i
         else:
             rel = float((u.double() - v.double()).norm() / max(float(v.double().norm()), 1e-30))
@@ -256,10 +259,11 @@ def test_fused_linear_bitwise_vs_cat_then_linear():
 
 @pytest.mark.parametrize("cap", [15.0, None])
 def test_mlstm_gate_bwd_kernel_vs_torch_chain(cap):
-    """sc_mlstm_gate_bwd against the torch chain it replaced in MLSTMFn / MLSTMCoreFn:
-    d fgate = sigmoid(-f) * flip(cumsum(flip(qdq - kdk))) (fp32; the kernel's suffix sums run in
-    another order: 1e-5 relative), and the soft-cap backward in bf16 (ops._soft_cap_bwd): the
-    input-gate gradient bitwise, the forget-gate one bitwise given the kernel's own fp32 d fgate."""
+    """sc_mlstm_gate_bwd against what it replaced in MLSTMFn / MLSTMCoreFn: d fgate =
+    sigmoid(-f) * flip(cumsum(flip(qdq - kdk))) in fp32 (the kernel's suffix sums run in another
+    order: 1e-5 relative), and the soft-cap backward: against fp64 g (1 - tanh(x / cap)^2) to
+    one bf16 rounding, and at least as close to it as the torch chain (ops._soft_cap_bwd, five
+    bf16 roundings).  Columns outside the two gate groups are untouched."""
     from statecatcher_amd import _lib
     from statecatcher_amd.ops import _soft_cap_bwd, ptr
     g = torch.Generator(device=DEV).manual_seed(4)
@@ -279,10 +283,13 @@ def test_mlstm_gate_bwd_kernel_vs_torch_chain(cap):
     torch.cuda.synchronize()
     ref_dfg = torch.sigmoid(-fg) * (qdq - kdk).flip(-1).cumsum(-1).flip(-1)
     torch.testing.assert_close(dfg, ref_dfg, rtol=1e-5, atol=1e-5 * float(ref_dfg.abs().max()))
-    dig_c = kdk.view(B, NH, T).transpose(1, 2).to(torch.bfloat16)
-    dfg_c = dfg.view(B, NH, T).transpose(1, 2).to(torch.bfloat16)
-    ref_i = _soft_cap_bwd(dig_c, a[..., io:io + NH], cap)
-    ref_f = _soft_cap_bwd(dfg_c, a[..., fo:fo + NH], cap)
-    assert torch.equal(da[..., io:io + NH], ref_i)
-    assert torch.equal(da[..., fo:fo + NH], ref_f)
+    for col, gr in ((io, kdk), (fo, dfg)):
+        gt = gr.view(B, NH, T).transpose(1, 2).double()
+        x = a[..., col:col + NH].double()
+        exact = gt if cap is None else gt * (1 - torch.tanh(x / cap) ** 2)
+        got = da[..., col:col + NH].double()
+        err = (got - exact).abs()
+        assert bool((err <= 2.0 ** -8 * exact.abs() + 1e-30).all())
+        chain = _soft_cap_bwd(gt.to(torch.bfloat16), a[..., col:col + NH], cap).double()
+        assert float(err.norm()) <= float((chain - exact).norm()) + 1e-30
     assert not da[..., :io].any() and not da[..., io + NH:fo].any() and not da[..., fo + NH:].any()
