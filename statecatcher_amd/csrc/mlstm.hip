@@ -623,41 +623,17 @@ __global__ void __launch_bounds__(512, 1) mlstm_bw_walk(MArgs a) {
   TI* dQg = (TI*)a.dq + qrow(a, bh, 0);
   TI* dKg = (TI*)a.dk + qrow(a, bh, 0);
   TI* dVg = (TI*)a.dv + vrow(a, bh, 0);
-  for (int k = a.nc - 1; k >= 0; --k) {
-    const int64_t t0 = (int64_t)k * kL;
-    asm volatile("" : "+v"(tid), "+v"(lane));   // see mlstm_fw_walk
-    // dn~_{k+1}: the previous chunk's four partial sums (after its closing barrier)
-    if (k < a.nc - 1 && tid < DQ)
-      dn = decay * dn + dnp[tid] + dnp[DQ + tid] + dnp[2 * DQ + tid] + dnp[3 * DQ + tid];
-    // ---- chunk inputs: every global load of the chunk issued before any LDS store (one
-    // memory latency per chunk, not one per operand) ----
-    constexpr int NQ8 = kL * DQ / 8, NV8 = kL * DV / 8, NC8 = DQ * DV / 8;
-    constexpr int UQ = (NQ8 + 511) / 512, UV = (NV8 + 511) / 512, UC = (NC8 + 511) / 512;
-    constexpr int UH = DV / 64;   // dh / h pieces per thread (8 threads per row)
-    u32x4 rq[UQ] = {}, rk[UQ] = {}, rv[UV] = {}, rc[UC] = {}, rd[UH] = {}, rh[UH] = {};
-    const T* Ck = (const T*)a.Cs + ((int64_t)bh * a.nc + k) * DQ * DV;
-    const int t = tid >> 3, part = tid & 7;
-    const int64_t ro = (int64_t)bh * a.T + t0 + t;
+  constexpr int NQ8 = kL * DQ / 8, NV8 = kL * DV / 8, NC8 = DQ * DV / 8;
+  constexpr int UQ = (NQ8 + 511) / 512, UV = (NV8 + 511) / 512, UC = (NC8 + 511) / 512;
+  constexpr int UH = DV / 64;   // dh / h pieces per thread (8 threads per row)
+  u32x4 rq[UQ] = {}, rk[UQ] = {}, rv[UV] = {}, rc[UC] = {}, rd[UH] = {}, rh[UH] = {};
+  float mk = 0.f, mk1 = 0.f, g_i = 0.f, g_f = 0.f, g_m = 0.f, n_k = 0.f, m_t = 0.f, dv_ = 0.f;
+  auto load_state = [&](int kc) __attribute__((always_inline)) {
+    const int64_t tb = (int64_t)kc * kL;
+    const T* Ck = (const T*)a.Cs + ((int64_t)bh * a.nc + kc) * DQ * DV;
+    const int64_t ro = (int64_t)bh * a.T + tb + (tid >> 3);
     const T* dh = (const T*)a.dh + ro * DV;
     const T* h = (const T*)a.h + ro * DV;
-    const int64_t st = (int64_t)bh * (a.nc + 1) + k;
-    const float mk = a.ms[st], mk1 = a.ms[st + 1];
-    const int64_t og = (int64_t)bh * a.T + t0 + lane;
-    const float g_i = a.ig[og], g_f = a.fg[og], g_m = a.mrow[og];
-    const float n_k = tid < DQ ? a.ns[st * DQ + tid] : 0.0f;
-#pragma unroll
-    for (int u = 0; u < UQ; ++u) {
-      const int e = tid + 512 * u, r = e / (DQ / 8), c = (e % (DQ / 8)) * 8;
-      if (e < NQ8 && !ML_ABL(512)) {
-        rq[u] = *(const u32x4*)(Qg + (t0 + r) * a.qt + c);
-        rk[u] = *(const u32x4*)(Kg + (t0 + r) * a.qt + c);
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < UV; ++u) {
-      const int e = tid + 512 * u, r = e / (DV / 8), c = (e % (DV / 8)) * 8;
-      if (e < NV8 && !ML_ABL(512)) rv[u] = *(const u32x4*)(Vg + (t0 + r) * a.vt + c);
-    }
 #pragma unroll
     for (int u = 0; u < UC; ++u) {
       const int e = tid + 512 * u;
@@ -666,11 +642,51 @@ __global__ void __launch_bounds__(512, 1) mlstm_bw_walk(MArgs a) {
 #pragma unroll
     for (int u = 0; u < UH; ++u) {
       if (!ML_ABL(512)) {
-        rd[u] = *(const u32x4*)(dh + part * 8 + 64 * u);
-        rh[u] = *(const u32x4*)(h + part * 8 + 64 * u);
+        rd[u] = *(const u32x4*)(dh + (tid & 7) * 8 + 64 * u);
+        rh[u] = *(const u32x4*)(h + (tid & 7) * 8 + 64 * u);
       }
     }
-    const float m_t = a.mrow[ro], dv_ = a.den[ro];
+    m_t = a.mrow[ro];
+    dv_ = a.den[ro];
+  };
+  auto load_qkv = [&](int kc) __attribute__((always_inline)) {
+    const int64_t tb = (int64_t)kc * kL;
+    const int64_t st = (int64_t)bh * (a.nc + 1) + kc;
+    mk = a.ms[st];
+    mk1 = a.ms[st + 1];
+    const int64_t og = (int64_t)bh * a.T + tb + lane;
+    g_i = a.ig[og];
+    g_f = a.fg[og];
+    g_m = a.mrow[og];
+    n_k = tid < DQ ? a.ns[st * DQ + tid] : 0.0f;
+#pragma unroll
+    for (int u = 0; u < UQ; ++u) {
+      const int e = tid + 512 * u, r = e / (DQ / 8), c = (e % (DQ / 8)) * 8;
+      if (e < NQ8 && !ML_ABL(512)) {
+        rq[u] = *(const u32x4*)(Qg + (tb + r) * a.qt + c);
+        rk[u] = *(const u32x4*)(Kg + (tb + r) * a.qt + c);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < UV; ++u) {
+      const int e = tid + 512 * u, r = e / (DV / 8), c = (e % (DV / 8)) * 8;
+      if (e < NV8 && !ML_ABL(512)) rv[u] = *(const u32x4*)(Vg + (tb + r) * a.vt + c);
+    }
+  };
+  for (int k = a.nc - 1; k >= 0; --k) {
+    const int64_t t0 = (int64_t)k * kL;
+    asm volatile("" : "+v"(tid), "+v"(lane));   // see mlstm_fw_walk
+    // dn~_{k+1}: the previous chunk's four partial sums (after its closing barrier)
+    if (k < a.nc - 1 && tid < DQ)
+      dn = decay * dn + dnp[tid] + dnp[DQ + tid] + dnp[2 * DQ + tid] + dnp[3 * DQ + tid];
+    // ---- chunk inputs, loaded during the previous (later) chunk: the C~_k image, dh and h rows
+    // are issued after that chunk's dq phase, q / k / v and the chunk scalars after its dk / dv
+    // phase, so both land while it computes (the first chunk loads here) ----
+    if (k == a.nc - 1) {
+      load_state(k);
+      load_qkv(k);
+    }
+    const int t = tid >> 3, part = tid & 7;
     // gate quantities (every wave, lane = step)
     const float b = wave_prefix_sum(logsig(g_f), lane);
     const float g = rdlane(b, 63);
@@ -789,6 +805,7 @@ __global__ void __launch_bounds__(512, 1) mlstm_bw_walk(MArgs a) {
       }
     }
     __syncthreads();
+    if (k > 0) load_state(k - 1);   // every register of this chunk's inputs is consumed
     // ---- A = W o (Q K^T) and dA = W o (Dn V^T + dden): 10 causal tiles each, 20 jobs ----
 #pragma unroll 1
     for (int jb = w; jb < (ML_ABL(32) ? 0 : 20); jb += 8) {
@@ -896,6 +913,7 @@ __global__ void __launch_bounds__(512, 1) mlstm_bw_walk(MArgs a) {
       a.qdq[(int64_t)bh * a.T + t0 + tid] = sq * inv;
     }
     __syncthreads();
+    if (k > 0) load_qkv(k - 1);
     // ---- dk = dA^T Q + es (V dC~^T + dn~): 4 x NI tiles; dv = A^T Dn + es (K dC~): 4 x NJ.
     // Wave w: key row block sr = w >> 1, NI / 2 dk column blocks, then NJ / 2 dv column blocks
     // in passes of NI / 2 (register-blocked as the dq phase) ----

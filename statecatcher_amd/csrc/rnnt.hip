@@ -531,8 +531,20 @@ struct JointArgs {
   float* db;           // [S][V]
 };
 
-__device__ __forceinline__ uint32_t wimg(int row, int chunk) {   // [row][8 x 16 B], XOR-swizzled
-  return (uint32_t)(row * 128 + 16 * (chunk ^ (row & 7)));
+// [row][8 x 16 B] images, the chunk XOR-swizzled by s(row) = ((row >> 1) & 1) << 2 | (row >> 2) & 3.
+// A 256-B bank row holds two image rows, so a slot is (row & 1) 8 + (chunk ^ s(row)): the 16 rows
+// of a ds_read_b128 lane group (distinct row & 15, one chunk) and the 4 aligned rows x 4 aligned
+// chunks of a ds_read_b64_tr_b16 half both land on 16 distinct slots (row & 7 as the swizzle left
+// both 2-way: rows r and r + 2 of a transposed read, r and r + 8 of a row read shared a slot)
+__device__ __forceinline__ uint32_t wswz(int row) { return (((row >> 1) & 1) << 2) | ((row >> 2) & 3); }
+__device__ __forceinline__ uint32_t wimg(int row, int chunk) {
+  return (uint32_t)(row * 128 + 16 * (chunk ^ wswz(row)));
+}
+// the joint backward's p image: as wimg, and the two 8-byte halves of a chunk swapped on odd rows,
+// so that the 16 rows of a ds_write_b64 lane group (one chunk, one half) take the 16 distinct
+// 8-byte places of a 128-B write bank window; col is an element index, a multiple of 4
+__device__ __forceinline__ uint32_t pimg_off(int row, int col) {
+  return wimg(row, col >> 3) + 8 * (((col >> 2) & 1) ^ (row & 1));
 }
 
 __device__ __forceinline__ jbf8 lds_b128(const unsigned char* lds, uint32_t off) {
@@ -541,10 +553,11 @@ __device__ __forceinline__ jbf8 lds_b128(const unsigned char* lds, uint32_t off)
 
 // ds_read_b64_tr_b16: group lane 4q+p addresses row R0+q, columns C0+4p..+3 of the image; lane i
 // of the group receives column C0+i of rows R0..R0+3
+template <bool P = false>
 __device__ __forceinline__ js4 tr_rd(const unsigned char* lds, int R0, int C0, int lane) {
   const int i = lane & 15, q = i >> 2, p = i & 3;
   const int row = R0 + q, col = C0 + 4 * p;
-  const uint32_t off = wimg(row, col >> 3) + 8 * ((col >> 2) & 1);
+  const uint32_t off = P ? pimg_off(row, col) : wimg(row, col >> 3) + 8 * ((col >> 2) & 1);
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
       (js4 __attribute__((address_space(3)))*)(size_t)(lds_addr(lds) + off));
 }
@@ -777,6 +790,12 @@ __global__ void __launch_bounds__(512) joint_fwd_kernel(JointArgs a) {
 #ifndef SC_JOINT_BF
 #define SC_JOINT_BF 0
 #endif
+// SC_JOINT_ABL: ablation bits for tools timing only (never set in a shipped build; wrong results):
+//   1 the column epilogue without the 1 - z^2 factor, 2 no column epilogue, 4 no exponentials,
+//   8 no p transpose / dZ MFMAs
+#ifndef SC_JOINT_ABL
+#define SC_JOINT_ABL 0
+#endif
 constexpr int kVbWg = 16;   // vocab blocks (of 32) per workgroup
 constexpr int kJW = 8;      // waves per workgroup: two per SIMD, so one wave's exp / pack /
                             // transpose work runs beside the other's MFMAs (<= 256 registers each)
@@ -829,8 +848,9 @@ struct BwdLds {   // byte offsets of the LDS regions
   static constexpr int kBias = kW + kVbWg * 32 * 128;   // [512] fp32, x log2(e)
   // column operands, two buffers (column u + 1 is staged while u computes):
   static constexpr int kZ = kBias + kVbWg * 32 * 4;     // z bf16 image [2][32][128 B]
-  static constexpr int kZ32 = kZ + 2 * 32 * 128;        // 1 - z^2 fp32 [2][32][64]
-  static constexpr int kNs = kZ32 + 2 * 32 * 64 * 4;    // node scalars: c, wb, wy [2][3][32]
+  static constexpr int kZP = 36;                        // 1 - z^2 row pitch (floats)
+  static constexpr int kZ32 = kZ + 2 * 32 * 128;        // 1 - z^2 fp32 [2][64 j][kZP], node fastest
+  static constexpr int kNs = kZ32 + 2 * 64 * kZP * 4;   // node scalars: c, wb, wy [2][3][32]
   static constexpr int kRed = kNs + 2 * 3 * 32 * 4;     // d pred partials [2][8][64]
   static constexpr int kEnc = kRed + 2 * kJW * 64 * 4;  // the task's enc rows fp32 [32][64]
   static constexpr int kP = kEnc + 32 * 64 * 4;         // per-wave p image [8][32][128 B]
@@ -933,11 +953,10 @@ __global__ void __launch_bounds__(64 * kJW) joint_bwd_kernel(JointArgs a) {
       }
       *(jbf8*)(zimg0 + bf * 32 * 128 + wimg(zn, jg)) = zb;
       // tanh' = 1 - z^2, once per element (every wave scales its dZ partial by it)
-      float* zz = z320 + bf * 32 * 64 + zn * 64 + 8 * jg;
-      *(float4*)zz = make_float4(1.0f - zf[0] * zf[0], 1.0f - zf[1] * zf[1],
-                                 1.0f - zf[2] * zf[2], 1.0f - zf[3] * zf[3]);
-      *(float4*)(zz + 4) = make_float4(1.0f - zf[4] * zf[4], 1.0f - zf[5] * zf[5],
-                                       1.0f - zf[6] * zf[6], 1.0f - zf[7] * zf[7]);
+      // ([j][n]: the epilogue reads a lane's four consecutive nodes as one 16-byte piece)
+      float* zz = z320 + bf * 64 * BwdLds::kZP + 8 * jg * BwdLds::kZP + zn;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) zz[e * BwdLds::kZP] = 1.0f - zf[e] * zf[e];
       if (th < 32) {
         float wb, wy, l2;
         node_finish(nd, tb * 32 + th, uu, Tb, Ub, wb, wy, l2);
@@ -958,7 +977,7 @@ __global__ void __launch_bounds__(64 * kJW) joint_bwd_kernel(JointArgs a) {
       asm volatile("" : "+v"(th), "+v"(lane), "+v"(h), "+v"(g1));
       const int cb = (u - ua) & 1;
       const unsigned char* zimg = zimg0 + cb * 32 * 128;
-      const float* z32 = z320 + cb * 32 * 64;
+      const float* z32 = z320 + cb * 64 * BwdLds::kZP;
       const float* ns_c = ns0 + cb * 96;
       const float* ns_wb = ns_c + 32;
       const float* ns_wy = ns_c + 64;
@@ -1001,10 +1020,17 @@ __global__ void __launch_bounds__(64 * kJW) joint_bwd_kernel(JointArgs a) {
 #pragma unroll
         for (int g = 0; g < 4; ++g) {   // node terms c_n (re-read per block: registers)
           const float4 cv = *(const float4*)(ns_c + 8 * g + 4 * h);
-          p[4 * g] = exp2_(fmaf(x[4 * g], kLog2e, bl + cv.x));
-          p[4 * g + 1] = exp2_(fmaf(x[4 * g + 1], kLog2e, bl + cv.y));
-          p[4 * g + 2] = exp2_(fmaf(x[4 * g + 2], kLog2e, bl + cv.z));
-          p[4 * g + 3] = exp2_(fmaf(x[4 * g + 3], kLog2e, bl + cv.w));
+          if (SC_JOINT_ABL & 4) {
+            p[4 * g] = fmaf(x[4 * g], kLog2e, bl + cv.x);
+            p[4 * g + 1] = fmaf(x[4 * g + 1], kLog2e, bl + cv.y);
+            p[4 * g + 2] = fmaf(x[4 * g + 2], kLog2e, bl + cv.z);
+            p[4 * g + 3] = fmaf(x[4 * g + 3], kLog2e, bl + cv.w);
+          } else {
+            p[4 * g] = exp2_(fmaf(x[4 * g], kLog2e, bl + cv.x));
+            p[4 * g + 1] = exp2_(fmaf(x[4 * g + 1], kLog2e, bl + cv.y));
+            p[4 * g + 2] = exp2_(fmaf(x[4 * g + 2], kLog2e, bl + cv.z));
+            p[4 * g + 3] = exp2_(fmaf(x[4 * g + 3], kLog2e, bl + cv.w));
+          }
         }
         // the sparse arcs of the gathered lattice: dlogits[n][blank] -= wb_n, dlogits[n][y_u] -=
         // wy_n (one or two blocks per column), so dW, d bias and dZ all take them from p
@@ -1045,15 +1071,19 @@ __global__ void __launch_bounds__(64 * kJW) joint_bwd_kernel(JointArgs a) {
         // extraction from the vector miscompiles into a broadcast of one element)
         typedef int ji2 __attribute__((ext_vector_type(2)));
         typedef int ji4 __attribute__((ext_vector_type(4)));
+        if (SC_JOINT_ABL & 8) {
+          asm volatile("" :: "v"(pf[0]), "v"(pf[1]));
+          continue;
+        }
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const ji4 d = __builtin_bit_cast(ji4, pf[g >> 1]);
-          *(ji2*)(pimg + wimg(lane & 31, g) + 8 * h) = ji2{d[2 * (g & 1)], d[2 * (g & 1) + 1]};
+          *(ji2*)(pimg + pimg_off(lane & 31, 8 * g + 4 * h)) = ji2{d[2 * (g & 1)], d[2 * (g & 1) + 1]};
         }
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
-          const jbf8 pt = cat8(tr_rd(pimg, 16 * s2 + 4 * h, 16 * g1, lane),
-                               tr_rd(pimg, 16 * s2 + 8 + 4 * h, 16 * g1, lane));
+          const jbf8 pt = cat8(tr_rd<true>(pimg, 16 * s2 + 4 * h, 16 * g1, lane),
+                               tr_rd<true>(pimg, 16 * s2 + 8 + 4 * h, 16 * g1, lane));
 #pragma unroll
           for (int jb = 0; jb < 2; ++jb) {
             const jbf8 wt = cat8(tr_rd(wl, lvc * 32 + 16 * s2 + 4 * h, jb * 32 + 16 * g1, lane),
@@ -1068,20 +1098,32 @@ __global__ void __launch_bounds__(64 * kJW) joint_bwd_kernel(JointArgs a) {
       // Y[jb][q] = this wave's part of dZ[node n_q][j = jb*32 + (lane & 31)],
       // n_q = (q & 3) + 8 (q >> 2) + 4 h: d pre = dZ (1 - z^2) into the wave's d enc partial
       // (LDS, [j][n]) and d pred (over n)
+      // (registers 4g .. 4g+3 are the consecutive nodes 8g + 4h .. +3: one conflict-free 16-byte
+      // read of [j][n] per g, and packed fp32 products / sums over register pairs)
+      typedef float jf2 __attribute__((ext_vector_type(2)));
 #pragma unroll
-      for (int jb = 0; jb < 2; ++jb) {
+      for (int jb = 0; jb < ((SC_JOINT_ABL & 2) ? 0 : 2); ++jb) {
         const int j = jb * 32 + (lane & 31);
-        float sp = 0.0f;
+        jf2 sp2 = {0.0f, 0.0f};
 #pragma unroll
-        for (int q = 0; q < 16; ++q) {   // register q = node (q & 3) + 8 (q >> 2) + 4 h
-          const int n = (q & 3) + 8 * (q >> 2) + 4 * h;
-          const float o = Y[jb][q] * z32[n * 64 + j];
-          dacc[jb][q] += o;
-          sp += o;
+        for (int g = 0; g < 4; ++g) {
+          const float4 zz = (SC_JOINT_ABL & 1) ? make_float4(1.f, 1.f, 1.f, 1.f)
+                                               : *(const float4*)(z32 + j * BwdLds::kZP + 8 * g + 4 * h);
+          const jf2 o0 = jf2{Y[jb][4 * g], Y[jb][4 * g + 1]} * jf2{zz.x, zz.y};
+          const jf2 o1 = jf2{Y[jb][4 * g + 2], Y[jb][4 * g + 3]} * jf2{zz.z, zz.w};
+          const jf2 a0 = jf2{dacc[jb][4 * g], dacc[jb][4 * g + 1]} + o0;
+          const jf2 a1 = jf2{dacc[jb][4 * g + 2], dacc[jb][4 * g + 3]} + o1;
+          dacc[jb][4 * g] = a0.x;
+          dacc[jb][4 * g + 1] = a0.y;
+          dacc[jb][4 * g + 2] = a1.x;
+          dacc[jb][4 * g + 3] = a1.y;
+          sp2 += o0 + o1;
         }
+        float sp = sp2.x + sp2.y;
         sp += __shfl_xor(sp, 32);
         if (h == 0) red[w * 64 + j] = sp;
       }
+      if (SC_JOINT_ABL & 2) asm volatile("" :: "v"(Y[0]), "v"(Y[1]));
       // the column's one barrier: its d pred partials and the next column's operands are
       // complete, and this column's buffer is free for column u + 2
       lds_barrier();
