@@ -17,9 +17,10 @@
 //                H[:, block] = M V[:, block] + Q~ C~_k[:, block], normaliser (S and the
 //                normaliser recomputed per block), then the state update.  Keeps m_t, den_t and
 //                the compute-dtype image of every chunk-start state for the backward.
-//   mlstm_bw_walk per (b,h), 8 waves: walks the chunks in reverse with dC~ in MFMA accumulators
-//                and computes the chunk's three input gradients on the way (intra-chunk terms
-//                through dA = W o (dnum V^T + dden), inter-chunk terms through C~_k / dC~_{k+1}).
+//   mlstm_bw_walk per (b,h), 8 waves, two roles: a walk through the chunks in reverse with dC~ in
+//                MFMA accumulators, computing dk and dv on the way (intra-chunk terms through
+//                A / dA = W o (dnum V^T + dden), inter-chunk terms through dC~_{k+1}), and beside
+//                it a workgroup computing dq of every chunk from the forward's C~_k (no carry).
 // The stabiliser m is treated as a constant in the backward (it cancels in h up to the eps
 // term), as the chunkwise kernels of the mlstm_kernels family do.  Gate gradients follow from
 // the pair identities  di_s = k_s.dk_s  and  dF_t = q_t.dq_t - k_t.dk_t  (F = cumulative
@@ -553,25 +554,30 @@ __global__ void __launch_bounds__(256, 2) mlstm_fw_walk(MArgs a) {
 }
 
 // ------------------------------------------------------------------------- backward: walk ----
-// One 8-wave workgroup per sequence (b,h) walks the chunks in REVERSE with the state gradient
-// dC~ [DQ][DV] (fp32) in MFMA accumulators, and per chunk computes all three input gradients:
-//   dq_t = sum_s dA_ts k_s + rowf_t (dnum_t C~_k^T + dden_t n~_k)
+// Two workgroup roles in one launch of 2 BH 8-wave workgroups.
+// Workgroups 0 .. BH-1 walk one sequence (b,h) through the chunks in REVERSE with the state
+// gradient dC~ [DQ][DV] (fp32) in MFMA accumulators and compute per chunk
 //   dk_s = sum_t dA_ts q_t + es_s (v_s dC~_{k+1}^T + dn~_{k+1})
 //   dv_s = sum_t A_ts dnum_t + es_s k_s dC~_{k+1}
 //   dC~_k = decay dC~_{k+1} + (rowf q)^T dnum,   dn~_k = decay dn~_{k+1} + sum_t rowf_t dden_t q_t
+// Workgroups BH .. 2BH-1 compute, for sequence bh - BH and each chunk independently,
+//   dq_t = sum_s dA_ts k_s + rowf_t (dnum_t C~_k^T + dden_t n~_k)
+// which reads the forward's states C~_k, n~_k and no carried gradient, so it leaves the serial
+// walk (whose chunk then has three barriers instead of five) and runs beside it on the CUs the
+// walks leave free (one workgroup per CU: 2 BH = 256 at C4).
 // (dA_ts = W_ts (dnum_t . v_s + dden_t), A_ts = W_ts q_t . k_s, W_ts = s e^{b_t - b_s + i_s - m_t},
 // s <= t).  Every operand lives in LDS once, row-major as loaded; MFMA fragments that run along
 // a column come out through transposed reads.  The per-row weights rowf / es scale the
 // accumulators (a second accumulator per job for the weighted term); the one per-k weight,
 // rowf in the state update, is folded into a scaled copy Qr = diag(rowf) Q written with the fill.
-// C~_k is the forward's compute-dtype image; dC~_{k+1}'s image replaces it in LDS once the dq
-// terms are done.  Nothing of size T x DQ x DV goes to HBM: the chunk states of the gradient stay
-// on chip (the gradient w.r.t. the initial state is the only state output).
+// Nothing of size T x DQ x DV goes to HBM: the chunk states of the gradient stay on chip (the
+// gradient w.r.t. the initial state is the only state output).
 // f16 range: dh of a trained-from-scratch model sits far below f16's normal range (~1e-6 against
-// 6e-5), where its images would keep 3-4 significant bits.  The f16 walk therefore scales each
-// chunk by a power of two S_k = 2^-e with max |dh| S_k in [0.5, 1) (dnum, dden, dA and the dC~
-// image all carry S_k; the fp32 dC~ / dn~ carry is rescaled exactly when S changes) and divides
-// every output by S_k.  bf16 has the exponent range of fp32 and runs unscaled.
+// 6e-5), where its images would keep 3-4 significant bits.  The f16 kernels therefore scale each
+// chunk by a power of two S_k = 2^-e (max |dh / z| S_k in [0.5, 1), and in the walk the carried
+// dC~ below 2^10): dnum, dden, dA and the dC~ image carry S_k, the fp32 dC~ / dn~ carry is
+// rescaled exactly when S changes, and every output is divided by S_k.  bf16 has the exponent
+// range of fp32 and runs unscaled.
 template <int DT, int IO, int DQ, int DV>
 __global__ void __launch_bounds__(512, 1) mlstm_bw_walk(MArgs a) {
   using M = MF<DT>;
@@ -586,18 +592,299 @@ __global__ void __launch_bounds__(512, 1) mlstm_bw_walk(MArgs a) {
   constexpr int NC = NI * NJ;                     // state tiles
   static_assert(NC % 8 == 0, "state tiles must split over 8 waves");
   constexpr int PC = NC / 8;
-  const int bh = blockIdx.x, w = threadIdx.x >> 6;
+  const int w = threadIdx.x >> 6;
   int tid = threadIdx.x, lane = tid & 63;
   __shared__ __attribute__((aligned(16))) T Qs[kL * LQ];
   __shared__ __attribute__((aligned(16))) T Qr[kL * LQ];   // diag(rowf) Q
   __shared__ __attribute__((aligned(16))) T Ks[kL * LQ];
   __shared__ __attribute__((aligned(16))) T Vs[kL * LV];
   __shared__ __attribute__((aligned(16))) T Dn[kL * LV];
-  __shared__ __attribute__((aligned(16))) T CS[DV * LQ];   // C~_k, then dC~_{k+1}, [j][i]
+  __shared__ __attribute__((aligned(16))) T CS[DV * LQ];   // walk: dC~_{k+1}; dq: C~_k ([j][i])
   __shared__ __attribute__((aligned(16))) T dA[kL * LL];
   __shared__ __attribute__((aligned(16))) T Am[kL * LL];
   __shared__ float sb[kL], si[kL], mt[kL], rowf[kL], es[kL], dden[kL], nk[DQ], dnk[DQ];
-  __shared__ float qpart[NI * kL], kpart[NI * kL], dnp[4 * DQ], smax[16];
+  __shared__ float part[NI * kL], dnp[4 * DQ], smax[16];
+  constexpr int NQ8 = kL * DQ / 8, NV8 = kL * DV / 8, NC8 = DQ * DV / 8;
+  constexpr int UQ = (NQ8 + 511) / 512, UV = (NV8 + 511) / 512, UC = (NC8 + 511) / 512;
+  constexpr int UH = DV / 64;   // dh / h pieces per thread (8 threads per row)
+  const bool walk = (int)blockIdx.x < a.BH;
+  const int bh = walk ? blockIdx.x : blockIdx.x - a.BH;
+  const T* Qg = (const T*)a.q + qrow(a, bh, 0);
+  const T* Kg = (const T*)a.k + qrow(a, bh, 0);
+  const T* Vg = (const T*)a.v + vrow(a, bh, 0);
+  // zero the strictly upper tiles (tc > tr) of A and dA once (they stay zero across chunks;
+  // ordered before any read by the first chunk's barrier)
+  for (int e = tid; e < kL * kL; e += 512) {
+    const int tt = e / kL, s = e % kL;
+    if ((s >> 4) > (tt >> 4)) {
+      Am[tt * LL + s] = (T)0.0f;
+      dA[tt * LL + s] = (T)0.0f;
+    }
+  }
+
+  // ---- pieces shared by the two roles ----
+  // chunk inputs in registers (issued ahead of their use)
+  u32x4 rq[UQ] = {}, rk[UQ] = {}, rv[UV] = {}, rd[UH] = {}, rh[UH] = {};
+  float mk = 0.f, mk1 = 0.f, g_i = 0.f, g_f = 0.f, g_m = 0.f, m_t = 0.f, dv_ = 0.f;
+  auto load_rows = [&](int kc) __attribute__((always_inline)) {   // dh, h, m_t, den of the rows
+    const int64_t ro = (int64_t)bh * a.T + (int64_t)kc * kL + (tid >> 3);
+    const T* dh = (const T*)a.dh + ro * DV;
+    const T* h = (const T*)a.h + ro * DV;
+#pragma unroll
+    for (int u = 0; u < UH; ++u) {
+      if (!ML_ABL(512)) {
+        rd[u] = *(const u32x4*)(dh + (tid & 7) * 8 + 64 * u);
+        rh[u] = *(const u32x4*)(h + (tid & 7) * 8 + 64 * u);
+      }
+    }
+    m_t = a.mrow[ro];
+    dv_ = a.den[ro];
+  };
+  auto load_qkv = [&](int kc) __attribute__((always_inline)) {   // q, k, v and the chunk scalars
+    const int64_t tb = (int64_t)kc * kL;
+    const int64_t st = (int64_t)bh * (a.nc + 1) + kc;
+    mk = a.ms[st];
+    mk1 = a.ms[st + 1];
+    const int64_t og = (int64_t)bh * a.T + tb + lane;
+    g_i = a.ig[og];
+    g_f = a.fg[og];
+    g_m = a.mrow[og];
+#pragma unroll
+    for (int u = 0; u < UQ; ++u) {
+      const int e = tid + 512 * u, r = e / (DQ / 8), c = (e % (DQ / 8)) * 8;
+      if (e < NQ8 && !ML_ABL(512)) {
+        rq[u] = *(const u32x4*)(Qg + (tb + r) * a.qt + c);
+        rk[u] = *(const u32x4*)(Kg + (tb + r) * a.qt + c);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < UV; ++u) {
+      const int e = tid + 512 * u, r = e / (DV / 8), c = (e % (DV / 8)) * 8;
+      if (e < NV8 && !ML_ABL(512)) rv[u] = *(const u32x4*)(Vg + (tb + r) * a.vt + c);
+    }
+  };
+  // gate quantities (every wave, lane = step) and the Q / K (/ Qr) / V fill; returns g = b_{L-1}
+  auto fill_chunk = [&](bool with_qr) __attribute__((always_inline)) {
+    const float b = wave_prefix_sum(logsig(g_f), lane);
+    const float rowf_l = a.scale * expf(b + mk - g_m);
+    if (w == 0) {
+      sb[lane] = b;
+      si[lane] = g_i;
+      rowf[lane] = rowf_l;
+    }
+#pragma unroll
+    for (int u = 0; u < UQ; ++u) {
+      const int e = tid + 512 * u, r = e / (DQ / 8), c = (e % (DQ / 8)) * 8;
+      const float f = __shfl(rowf_l, r & 63);
+      if (e < NQ8) {
+        const V8 x = cvt8<DT, IO>(rq[u]);
+        *(V8*)(Qs + r * LQ + c) = x;
+        *(V8*)(Ks + r * LQ + c) = cvt8<DT, IO>(rk[u]);
+        if (with_qr) {
+          V8 y;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) y[j] = (T)((float)x[j] * f);
+          *(V8*)(Qr + r * LQ + c) = y;
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < UV; ++u) {
+      const int e = tid + 512 * u, r = e / (DV / 8), c = (e % (DV / 8)) * 8;
+      if (e < NV8) *(V8*)(Vs + r * LV + c) = cvt8<DT, IO>(rv[u]);
+    }
+    return b;
+  };
+  // the chunk's gradient scale (f16): dnum = dh / z to [0.5, 1) and the carried dC~ (largest
+  // magnitude mc, in units of the previous scale S) below 2^10; z can be ~1e-6, so it is dnum,
+  // not dh, that must fit.  Keeps S when nothing sets a scale.
+  auto chunk_scale = [&](float z, float mc, float S) __attribute__((always_inline)) {
+    float mx = 0.0f;
+#pragma unroll
+    for (int u = 0; u < UH; ++u) {
+      const V8I xd = __builtin_bit_cast(V8I, rd[u]);
+#pragma unroll
+      for (int e2 = 0; e2 < 8; ++e2) mx = fmaxf(mx, fabsf((float)xd[e2]));
+    }
+    mx /= z;
+    mx = wave_max(mx);
+    mc = wave_max(mc);
+    if (lane == 0) {
+      smax[w] = mx;
+      smax[8 + w] = mc;
+    }
+    __syncthreads();
+    mx = smax[0];
+    mc = smax[8];
+#pragma unroll
+    for (int v = 1; v < 8; ++v) {
+      mx = fmaxf(mx, smax[v]);
+      mc = fmaxf(mc, smax[8 + v]);
+    }
+    mc /= S;   // in true units
+    float s1 = 3.0e38f, s2 = 3.0e38f;
+    int ex;
+    if (mx > 0.0f && mx < 3.0e38f) {
+      frexpf(mx, &ex);
+      s1 = ldexpf(1.0f, -ex);
+    }
+    if (mc > 0.0f && mc < 3.0e38f) {
+      frexpf(mc, &ex);
+      s2 = ldexpf(1.0f, 10 - ex);
+    }
+    const float Sk = fminf(s1, s2);
+    return Sk < 3.0e38f ? Sk : S;
+  };
+  // dnum = dh S / z and dden S (8 threads per row)
+  auto fill_dn = [&](float z, float Sk) __attribute__((always_inline)) {
+    const int t = tid >> 3, pt = tid & 7;
+    const float zs = Sk / z;
+    float dot = 0.0f;
+#pragma unroll
+    for (int u = 0; u < UH; ++u) {
+      const V8I xd = __builtin_bit_cast(V8I, rd[u]);
+      const V8 xh = __builtin_bit_cast(V8, rh[u]);
+      V8 o;
+#pragma unroll
+      for (int e2 = 0; e2 < 8; ++e2) {
+        const float d = (float)xd[e2];
+        dot += d * (float)xh[e2];
+        o[e2] = (T)(d * zs);
+      }
+      *(V8*)(Dn + t * LV + pt * 8 + 64 * u) = o;
+    }
+    dot = sum8(dot);
+    if (pt == 0) {
+      const float live = fabsf(dv_) >= expf(-m_t) ? 1.0f : 0.0f;
+      dden[t] = -dot * zs * (dv_ >= 0.0f ? 1.0f : -1.0f) * live;
+      mt[t] = m_t;
+    }
+  };
+  // one causal 16 x 16 tile of A = W o (Q K^T) (isA) or dA = W o (Dn V^T + dden)
+  auto a_job = [&](int idx, bool isA) __attribute__((always_inline)) {
+    // idx -> (tr, tc), tc <= tr: 0 (0,0) 1 (1,0) 2 (1,1) 3 (2,0) 4 (2,1) 5 (2,2) 6.. (3,*)
+    const int tr = idx < 1 ? 0 : idx < 3 ? 1 : idx < 6 ? 2 : 3;
+    const int tc = idx - tr * (tr + 1) / 2;
+    f32x4 c4 = {0.f, 0.f, 0.f, 0.f};
+    if (isA) {
+      V8 fa[DQ / 32], fb[DQ / 32];
+#pragma unroll
+      for (int kk = 0; kk < DQ / 32; ++kk) {
+        fa[kk] = frag<V8, T>(Qs, LQ, 16 * tr, 32 * kk, lane);
+        fb[kk] = frag<V8, T>(Ks, LQ, 16 * tc, 32 * kk, lane);
+      }
+#pragma unroll
+      for (int kk = 0; kk < DQ / 32; ++kk) c4 = M::mma(fa[kk], fb[kk], c4);
+    } else {
+      V8 fa[DV / 32], fb[DV / 32];
+#pragma unroll
+      for (int kk = 0; kk < DV / 32; ++kk) {
+        fa[kk] = frag<V8, T>(Dn, LV, 16 * tr, 32 * kk, lane);
+        fb[kk] = frag<V8, T>(Vs, LV, 16 * tc, 32 * kk, lane);
+      }
+#pragma unroll
+      for (int kk = 0; kk < DV / 32; ++kk) c4 = M::mma(fa[kk], fb[kk], c4);
+    }
+    const int s = 16 * tc + (lane & 15);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int tt = 16 * tr + 4 * (lane >> 4) + r;
+      const float wts = (s <= tt) ? a.scale * expf(sb[tt] - sb[s] + si[s] - mt[tt]) : 0.0f;
+      if (isA) Am[tt * LL + s] = (T)(c4[r] * wts);
+      else dA[tt * LL + s] = (T)((c4[r] + dden[tt]) * wts);
+    }
+  };
+
+  if (!walk) {
+    // ================= dq role: every chunk of sequence bh, independently =================
+    TI* dQg = (TI*)a.dq + qrow(a, bh, 0);
+#pragma unroll 1
+    for (int k = 0; k < a.nc; ++k) {
+      const int64_t t0 = (int64_t)k * kL;
+      asm volatile("" : "+v"(tid), "+v"(lane));   // see mlstm_fw_walk
+      u32x4 rc[UC] = {};
+      const T* Ck = (const T*)a.Cs + ((int64_t)bh * a.nc + k) * DQ * DV;
+#pragma unroll
+      for (int u = 0; u < UC; ++u) {
+        const int e = tid + 512 * u;
+        if (e < NC8 && !ML_ABL(512)) rc[u] = *(const u32x4*)(Ck + 8 * e);
+      }
+      const float n_k = tid < DQ ? a.ns[((int64_t)bh * (a.nc + 1) + k) * DQ + tid] : 0.0f;
+      load_qkv(k);
+      load_rows(k);
+      fill_chunk(false);
+#pragma unroll
+      for (int u = 0; u < UC; ++u) {
+        const int e = tid + 512 * u;
+        if (e < NC8) {
+          const int j = (8 * e) / DQ, i = (8 * e) % DQ;
+          *(u32x4*)(CS + j * LQ + i) = rc[u];
+        }
+      }
+      if (tid < DQ) nk[tid] = n_k;
+      const float z = fmaxf(fabsf(dv_), expf(-m_t)) + a.eps;
+      float Sk = 1.0f;
+      if constexpr (kScale) Sk = chunk_scale(z, 0.0f, 1.0f);
+      fill_dn(z, Sk);
+      __syncthreads();
+      // ---- dA = W o (Dn V^T + dden): 10 causal tiles ----
+#pragma unroll 1
+      for (int jb = w; jb < (ML_ABL(32) ? 0 : 10); jb += 8) a_job(jb, false);
+      __syncthreads();
+      const float inv = 1.0f / Sk;
+      // ---- dq = dA K + rowf (Dn C~_k^T + dden n~_k): 4 x NI tiles, wave w the row block
+      // tr = w >> 1 and NI / 2 column blocks: each A fragment feeds NI / 2 MFMAs.  (The causal
+      // chain always takes both k-steps: dA's tiles above the diagonal are zero.) ----
+      if (!ML_ABL(64)) {
+        constexpr int NC2 = NI / 2;
+        const int tr = w >> 1, c0 = (w & 1) * NC2;
+        f32x4 d4[NC2], e4[NC2];
+#pragma unroll
+        for (int c = 0; c < NC2; ++c) d4[c] = e4[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          const V8 fa = frag<V8, T>(dA, LL, 16 * tr, 32 * kk, lane);
+#pragma unroll
+          for (int c = 0; c < NC2; ++c)
+            d4[c] = M::mma(fa, frag_t<V8, T>(Ks, LQ, 32 * kk, 16 * (c0 + c), lane), d4[c]);
+        }
+#pragma unroll
+        for (int kk = 0; kk < DV / 32; ++kk) {
+          const V8 ga = frag<V8, T>(Dn, LV, 16 * tr, 32 * kk, lane);
+#pragma unroll
+          for (int c = 0; c < NC2; ++c)
+            e4[c] = M::mma(ga, frag_t<V8, T>(CS, LQ, 32 * kk, 16 * (c0 + c), lane), e4[c]);
+        }
+#pragma unroll
+        for (int c = 0; c < NC2; ++c) {
+          const int ci = c0 + c, i = 16 * ci + (lane & 15);
+          const float nki = nk[i];
+          float qd[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int tt = 16 * tr + 4 * (lane >> 4) + r;
+            const float v = d4[c][r] + rowf[tt] * (e4[c][r] + dden[tt] * nki);
+            dQg[(t0 + tt) * a.qt + i] = out16<DT, IO>(v * inv);
+            qd[r] = sum16(v * (float)Qs[tt * LQ + i]);
+          }
+          if ((lane & 15) == 0) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) part[ci * kL + 16 * tr + 4 * (lane >> 4) + r] = qd[r];
+          }
+        }
+      }
+      __syncthreads();
+      if (tid < kL) {
+        float sq = 0.0f;
+#pragma unroll
+        for (int ci = 0; ci < NI; ++ci) sq += part[ci * kL + tid];
+        a.qdq[(int64_t)bh * a.T + t0 + tid] = sq * inv;
+      }
+    }
+    return;
+  }
+
+  // ================= walk role =================
   // dC~ tiles: the waves form a 2 x 4 grid over the NI x NJ tiles, wave w owning the BI x BJ
   // block (w >> 2, w & 3); tile p = a BJ + b is at rows 16 (BI (w >> 2) + a), cols 16 (BJ (w & 3)
   // + b): per k-step the block's BI + BJ fragments feed BI BJ MFMAs
@@ -617,161 +904,34 @@ __global__ void __launch_bounds__(512, 1) mlstm_bw_walk(MArgs a) {
   }
   float dn = (tid < DQ && a.dnT) ? a.dnT[(int64_t)bh * DQ + tid] : 0.0f;
   float S = 1.0f, decay = 1.0f;   // S: the current chunk's gradient scale (f16)
-  const T* Qg = (const T*)a.q + qrow(a, bh, 0);
-  const T* Kg = (const T*)a.k + qrow(a, bh, 0);
-  const T* Vg = (const T*)a.v + vrow(a, bh, 0);
-  TI* dQg = (TI*)a.dq + qrow(a, bh, 0);
   TI* dKg = (TI*)a.dk + qrow(a, bh, 0);
   TI* dVg = (TI*)a.dv + vrow(a, bh, 0);
-  constexpr int NQ8 = kL * DQ / 8, NV8 = kL * DV / 8, NC8 = DQ * DV / 8;
-  constexpr int UQ = (NQ8 + 511) / 512, UV = (NV8 + 511) / 512, UC = (NC8 + 511) / 512;
-  constexpr int UH = DV / 64;   // dh / h pieces per thread (8 threads per row)
-  u32x4 rq[UQ] = {}, rk[UQ] = {}, rv[UV] = {}, rc[UC] = {}, rd[UH] = {}, rh[UH] = {};
-  float mk = 0.f, mk1 = 0.f, g_i = 0.f, g_f = 0.f, g_m = 0.f, n_k = 0.f, m_t = 0.f, dv_ = 0.f;
-  auto load_state = [&](int kc) __attribute__((always_inline)) {
-    const int64_t tb = (int64_t)kc * kL;
-    const T* Ck = (const T*)a.Cs + ((int64_t)bh * a.nc + kc) * DQ * DV;
-    const int64_t ro = (int64_t)bh * a.T + tb + (tid >> 3);
-    const T* dh = (const T*)a.dh + ro * DV;
-    const T* h = (const T*)a.h + ro * DV;
-#pragma unroll
-    for (int u = 0; u < UC; ++u) {
-      const int e = tid + 512 * u;
-      if (e < NC8 && !ML_ABL(512)) rc[u] = *(const u32x4*)(Ck + 8 * e);
-    }
-#pragma unroll
-    for (int u = 0; u < UH; ++u) {
-      if (!ML_ABL(512)) {
-        rd[u] = *(const u32x4*)(dh + (tid & 7) * 8 + 64 * u);
-        rh[u] = *(const u32x4*)(h + (tid & 7) * 8 + 64 * u);
-      }
-    }
-    m_t = a.mrow[ro];
-    dv_ = a.den[ro];
-  };
-  auto load_qkv = [&](int kc) __attribute__((always_inline)) {
-    const int64_t tb = (int64_t)kc * kL;
-    const int64_t st = (int64_t)bh * (a.nc + 1) + kc;
-    mk = a.ms[st];
-    mk1 = a.ms[st + 1];
-    const int64_t og = (int64_t)bh * a.T + tb + lane;
-    g_i = a.ig[og];
-    g_f = a.fg[og];
-    g_m = a.mrow[og];
-    n_k = tid < DQ ? a.ns[st * DQ + tid] : 0.0f;
-#pragma unroll
-    for (int u = 0; u < UQ; ++u) {
-      const int e = tid + 512 * u, r = e / (DQ / 8), c = (e % (DQ / 8)) * 8;
-      if (e < NQ8 && !ML_ABL(512)) {
-        rq[u] = *(const u32x4*)(Qg + (tb + r) * a.qt + c);
-        rk[u] = *(const u32x4*)(Kg + (tb + r) * a.qt + c);
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < UV; ++u) {
-      const int e = tid + 512 * u, r = e / (DV / 8), c = (e % (DV / 8)) * 8;
-      if (e < NV8 && !ML_ABL(512)) rv[u] = *(const u32x4*)(Vg + (tb + r) * a.vt + c);
-    }
-  };
   for (int k = a.nc - 1; k >= 0; --k) {
     const int64_t t0 = (int64_t)k * kL;
     asm volatile("" : "+v"(tid), "+v"(lane));   // see mlstm_fw_walk
     // dn~_{k+1}: the previous chunk's four partial sums (after its closing barrier)
     if (k < a.nc - 1 && tid < DQ)
       dn = decay * dn + dnp[tid] + dnp[DQ + tid] + dnp[2 * DQ + tid] + dnp[3 * DQ + tid];
-    // ---- chunk inputs, loaded during the previous (later) chunk: the C~_k image, dh and h rows
-    // are issued after that chunk's dq phase, q / k / v and the chunk scalars after its dk / dv
-    // phase, so both land while it computes (the first chunk loads here) ----
+    // ---- chunk inputs, loaded during the previous (later) chunk: the dh and h rows are issued
+    // after its first barrier, q / k / v and the chunk scalars after its A / dA phase, so both
+    // land while it computes (the first chunk loads here) ----
     if (k == a.nc - 1) {
-      load_state(k);
+      load_rows(k);
       load_qkv(k);
     }
-    const int t = tid >> 3, part = tid & 7;
-    // gate quantities (every wave, lane = step)
-    const float b = wave_prefix_sum(logsig(g_f), lane);
+    const float b = fill_chunk(true);
     const float g = rdlane(b, 63);
-    const float rowf_l = a.scale * expf(b + mk - g_m);
     decay = expf(g + mk - mk1);
-    if (w == 0) {
-      sb[lane] = b;
-      si[lane] = g_i;
-      rowf[lane] = rowf_l;
-      es[lane] = expf(g - b + g_i - mk1);
-    }
-#pragma unroll
-    for (int u = 0; u < UQ; ++u) {
-      const int e = tid + 512 * u, r = e / (DQ / 8), c = (e % (DQ / 8)) * 8;
-      const float f = __shfl(rowf_l, r & 63);
-      if (e < NQ8) {
-        const V8 x = cvt8<DT, IO>(rq[u]);
-        *(V8*)(Qs + r * LQ + c) = x;
-        *(V8*)(Ks + r * LQ + c) = cvt8<DT, IO>(rk[u]);
-        V8 y;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) y[j] = (T)((float)x[j] * f);
-        *(V8*)(Qr + r * LQ + c) = y;
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < UV; ++u) {
-      const int e = tid + 512 * u, r = e / (DV / 8), c = (e % (DV / 8)) * 8;
-      if (e < NV8) *(V8*)(Vs + r * LV + c) = cvt8<DT, IO>(rv[u]);
-    }
-#pragma unroll
-    for (int u = 0; u < UC; ++u) {
-      const int e = tid + 512 * u;
-      if (e < NC8) {
-        const int j = (8 * e) / DQ, i = (8 * e) % DQ;
-        *(u32x4*)(CS + j * LQ + i) = rc[u];
-      }
-    }
-    if (tid < DQ) {
-      nk[tid] = n_k;
-    }
+    if (w == 0) es[lane] = expf(g - b + g_i - mk1);
     const float z = fmaxf(fabsf(dv_), expf(-m_t)) + a.eps;
-    // the chunk's gradient scale (f16): dnum = dh / z to [0.5, 1) and the carried dC~ below 2^10
-    // (z can be ~1e-6, so it is dnum, not dh, that must fit)
     float Sk = 1.0f;
     if constexpr (kScale) {
-      float mx = 0.0f, mc = 0.0f;
-#pragma unroll
-      for (int u = 0; u < UH; ++u) {
-        const V8I xd = __builtin_bit_cast(V8I, rd[u]);
-#pragma unroll
-        for (int e2 = 0; e2 < 8; ++e2) mx = fmaxf(mx, fabsf((float)xd[e2]));
-      }
-      mx /= z;
+      float mc = 0.0f;
 #pragma unroll
       for (int p = 0; p < PC; ++p)
 #pragma unroll
         for (int r = 0; r < 4; ++r) mc = fmaxf(mc, fabsf(acc[p][r]));
-      mx = wave_max(mx);
-      mc = wave_max(mc);
-      if (lane == 0) {
-        smax[w] = mx;
-        smax[8 + w] = mc;
-      }
-      __syncthreads();
-      mx = smax[0];
-      mc = smax[8];
-#pragma unroll
-      for (int v = 1; v < 8; ++v) {
-        mx = fmaxf(mx, smax[v]);
-        mc = fmaxf(mc, smax[8 + v]);
-      }
-      mc /= S;   // in true units
-      float s1 = 3.0e38f, s2 = 3.0e38f;
-      int ex;
-      if (mx > 0.0f && mx < 3.0e38f) {
-        frexpf(mx, &ex);
-        s1 = ldexpf(1.0f, -ex);
-      }
-      if (mc > 0.0f && mc < 3.0e38f) {
-        frexpf(mc, &ex);
-        s2 = ldexpf(1.0f, 10 - ex);
-      }
-      Sk = fminf(s1, s2);
-      if (!(Sk < 3.0e38f)) Sk = S;   // nothing to scale by: keep the previous chunk's
+      Sk = chunk_scale(z, mc, S);
       // the carried gradients move to this chunk's scale (powers of two: exact)
       const float rs = Sk / S;
 #pragma unroll
@@ -780,124 +940,8 @@ __global__ void __launch_bounds__(512, 1) mlstm_bw_walk(MArgs a) {
       S = Sk;
     }
     if (tid < DQ) dnk[tid] = dn;
-    // dnum = dh S / z and dden S (8 threads per row)
-    {
-      const float zs = Sk / z;
-      float dot = 0.0f;
-#pragma unroll
-      for (int u = 0; u < UH; ++u) {
-        const V8I xd = __builtin_bit_cast(V8I, rd[u]);
-        const V8 xh = __builtin_bit_cast(V8, rh[u]);
-        V8 o;
-#pragma unroll
-        for (int e2 = 0; e2 < 8; ++e2) {
-          const float d = (float)xd[e2];
-          dot += d * (float)xh[e2];
-          o[e2] = (T)(d * zs);
-        }
-        *(V8*)(Dn + t * LV + part * 8 + 64 * u) = o;
-      }
-      dot = sum8(dot);
-      if (part == 0) {
-        const float live = fabsf(dv_) >= expf(-m_t) ? 1.0f : 0.0f;
-        dden[t] = -dot * zs * (dv_ >= 0.0f ? 1.0f : -1.0f) * live;
-        mt[t] = m_t;
-      }
-    }
-    __syncthreads();
-    if (k > 0) load_state(k - 1);   // every register of this chunk's inputs is consumed
-    // ---- A = W o (Q K^T) and dA = W o (Dn V^T + dden): 10 causal tiles each, 20 jobs ----
-#pragma unroll 1
-    for (int jb = w; jb < (ML_ABL(32) ? 0 : 20); jb += 8) {
-      const bool isA = jb < 10;
-      const int idx = isA ? jb : jb - 10;
-      // idx -> (tr, tc), tc <= tr: 0 (0,0) 1 (1,0) 2 (1,1) 3 (2,0) 4 (2,1) 5 (2,2) 6.. (3,*)
-      const int tr = idx < 1 ? 0 : idx < 3 ? 1 : idx < 6 ? 2 : 3;
-      const int tc = idx - tr * (tr + 1) / 2;
-      f32x4 c4 = {0.f, 0.f, 0.f, 0.f};
-      if (isA) {
-        V8 fa[DQ / 32], fb[DQ / 32];
-#pragma unroll
-        for (int kk = 0; kk < DQ / 32; ++kk) {
-          fa[kk] = frag<V8, T>(Qs, LQ, 16 * tr, 32 * kk, lane);
-          fb[kk] = frag<V8, T>(Ks, LQ, 16 * tc, 32 * kk, lane);
-        }
-#pragma unroll
-        for (int kk = 0; kk < DQ / 32; ++kk) c4 = M::mma(fa[kk], fb[kk], c4);
-      } else {
-        V8 fa[DV / 32], fb[DV / 32];
-#pragma unroll
-        for (int kk = 0; kk < DV / 32; ++kk) {
-          fa[kk] = frag<V8, T>(Dn, LV, 16 * tr, 32 * kk, lane);
-          fb[kk] = frag<V8, T>(Vs, LV, 16 * tc, 32 * kk, lane);
-        }
-#pragma unroll
-        for (int kk = 0; kk < DV / 32; ++kk) c4 = M::mma(fa[kk], fb[kk], c4);
-      }
-      const int s = 16 * tc + (lane & 15);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int tt = 16 * tr + 4 * (lane >> 4) + r;
-        const float wts = (s <= tt) ? a.scale * expf(sb[tt] - sb[s] + si[s] - mt[tt]) : 0.0f;
-        if (isA) Am[tt * LL + s] = (T)(c4[r] * wts);
-        else dA[tt * LL + s] = (T)((c4[r] + dden[tt]) * wts);
-      }
-    }
-    // zero the strictly upper tiles (tc > tr) of A and dA once (they stay zero across chunks)
-    if (k == a.nc - 1) {
-      for (int e = tid; e < kL * kL; e += 512) {
-        const int tt = e / kL, s = e % kL;
-        if ((s >> 4) > (tt >> 4)) {
-          Am[tt * LL + s] = (T)0.0f;
-          dA[tt * LL + s] = (T)0.0f;
-        }
-      }
-    }
-    __syncthreads();
-    const float inv = 1.0f / S;
-    // ---- dq = dA K + rowf (Dn C~_k^T + dden n~_k): 4 x NI tiles, wave w the row block
-    // tr = w >> 1 and NI / 2 column blocks: each A fragment feeds NI / 2 MFMAs.  (The causal
-    // chain always takes both k-steps: dA's tiles above the diagonal are zero.) ----
-    if (!ML_ABL(64)) {
-      constexpr int NC2 = NI / 2;
-      const int tr = w >> 1, c0 = (w & 1) * NC2;
-      f32x4 d4[NC2], e4[NC2];
-#pragma unroll
-      for (int c = 0; c < NC2; ++c) d4[c] = e4[c] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        const V8 fa = frag<V8, T>(dA, LL, 16 * tr, 32 * kk, lane);
-#pragma unroll
-        for (int c = 0; c < NC2; ++c)
-          d4[c] = M::mma(fa, frag_t<V8, T>(Ks, LQ, 32 * kk, 16 * (c0 + c), lane), d4[c]);
-      }
-#pragma unroll
-      for (int kk = 0; kk < DV / 32; ++kk) {
-        const V8 ga = frag<V8, T>(Dn, LV, 16 * tr, 32 * kk, lane);
-#pragma unroll
-        for (int c = 0; c < NC2; ++c)
-          e4[c] = M::mma(ga, frag_t<V8, T>(CS, LQ, 32 * kk, 16 * (c0 + c), lane), e4[c]);
-      }
-#pragma unroll
-      for (int c = 0; c < NC2; ++c) {
-        const int ci = c0 + c, i = 16 * ci + (lane & 15);
-        const float nki = nk[i];
-        float qd[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int tt = 16 * tr + 4 * (lane >> 4) + r;
-          const float v = d4[c][r] + rowf[tt] * (e4[c][r] + dden[tt] * nki);
-          dQg[(t0 + tt) * a.qt + i] = out16<DT, IO>(v * inv);
-          qd[r] = sum16(v * (float)Qs[tt * LQ + i]);
-        }
-        if ((lane & 15) == 0) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) qpart[ci * kL + 16 * tr + 4 * (lane >> 4) + r] = qd[r];
-        }
-      }
-    }
-    __syncthreads();
-    // ---- dC~_{k+1} image replaces C~_k ----
+    fill_dn(z, Sk);
+    // ---- dC~_{k+1} image (the dk / dv operand) ----
 #pragma unroll
     for (int p = 0; p < PC; ++p) {
       const int i0 = 16 * (ib0 + p / BJ), j0 = 16 * (jb0 + p % BJ);
@@ -906,17 +950,17 @@ __global__ void __launch_bounds__(512, 1) mlstm_bw_walk(MArgs a) {
       for (int r = 0; r < 4; ++r) c[r] = (T)acc[p][r];
       *(v4t*)(CS + (j0 + (lane & 15)) * LQ + i0 + 4 * (lane >> 4)) = c;
     }
-    if (tid < kL) {
-      float sq = 0.0f;
-#pragma unroll
-      for (int ci = 0; ci < NI; ++ci) sq += qpart[ci * kL + tid];
-      a.qdq[(int64_t)bh * a.T + t0 + tid] = sq * inv;
-    }
+    __syncthreads();
+    if (k > 0) load_rows(k - 1);   // dh / h of this chunk are consumed
+    // ---- A = W o (Q K^T) and dA = W o (Dn V^T + dden): 10 causal tiles each, 20 jobs ----
+#pragma unroll 1
+    for (int jb = w; jb < (ML_ABL(32) ? 0 : 20); jb += 8) a_job(jb < 10 ? jb : jb - 10, jb < 10);
     __syncthreads();
     if (k > 0) load_qkv(k - 1);
+    const float inv = 1.0f / S;
     // ---- dk = dA^T Q + es (V dC~^T + dn~): 4 x NI tiles; dv = A^T Dn + es (K dC~): 4 x NJ.
     // Wave w: key row block sr = w >> 1, NI / 2 dk column blocks, then NJ / 2 dv column blocks
-    // in passes of NI / 2 (register-blocked as the dq phase) ----
+    // in passes of NI / 2 (register-blocked: each A fragment feeds NI / 2 MFMAs) ----
     if (!ML_ABL(128)) {
       constexpr int NC2 = NI / 2;
       const int sr = w >> 1;
@@ -953,7 +997,7 @@ __global__ void __launch_bounds__(512, 1) mlstm_bw_walk(MArgs a) {
           }
           if ((lane & 15) == 0) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) kpart[ci * kL + 16 * sr + 4 * (lane >> 4) + r] = kd[r];
+            for (int r = 0; r < 4; ++r) part[ci * kL + 16 * sr + 4 * (lane >> 4) + r] = kd[r];
           }
         }
       }
@@ -1015,10 +1059,10 @@ __global__ void __launch_bounds__(512, 1) mlstm_bw_walk(MArgs a) {
       dnp[qt4 * DQ + i] = sacc;
     }
     __syncthreads();
-    if (tid < kL) {   // (kpart comes from every wave's dk jobs: after the barrier)
+    if (tid < kL) {   // (part comes from every wave's dk jobs: after the barrier)
       float sk = 0.0f;
 #pragma unroll
-      for (int ci = 0; ci < NI; ++ci) sk += kpart[ci * kL + tid];
+      for (int ci = 0; ci < NI; ++ci) sk += part[ci * kL + tid];
       a.kdk[(int64_t)bh * a.T + t0 + tid] = sk * inv;
     }
   }
@@ -1041,7 +1085,8 @@ void launch_fwd(const MArgs& a, hipStream_t st) {
 }
 template <int DT, int IO, int DQ, int DV>
 void launch_bwd(const MArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL((mlstm_bw_walk<DT, IO, DQ, DV>), dim3(a.BH), dim3(512), 0, st, a);
+  // workgroups 0 .. BH-1 walk, BH .. 2BH-1 take the dq terms
+  hipLaunchKernelGGL((mlstm_bw_walk<DT, IO, DQ, DV>), dim3(2 * a.BH), dim3(512), 0, st, a);
 }
 
 // head dimensions compiled in (DQ, DV): the xLSTM-large defaults qk = v/2 at 64..192 wide heads
