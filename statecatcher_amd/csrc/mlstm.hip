@@ -26,6 +26,7 @@
 // the pair identities  di_s = k_s.dk_s  and  dF_t = q_t.dq_t - k_t.dk_t  (F = cumulative
 // logsig(f)): the kernels emit the two dot products, the host turns dF into df by a reverse
 // cumulative sum times sigmoid(-f).
+#include <cstdlib>
 #include <initializer_list>
 
 #include "sc_common.h"
@@ -291,7 +292,7 @@ __device__ __forceinline__ ChunkGates chunk_gate_math(float ig, float fg, float 
 // column (K^T in the state update, V in M V) come out through transposed reads.  Per-row weights
 // scale the accumulators, per-k weights are folded into one scaled copy Kf = diag(fs) K written
 // with the fill: no VALU work between a fragment read and its MFMA.
-template <int DT, int IO, int DQ, int DV>
+template <int DT, int IO, int DQ, int DV, int MODE>
 __global__ void __launch_bounds__(256, 2) mlstm_fw_walk(MArgs a) {
   using M = MF<DT>;
   using T = typename M::T;
@@ -300,7 +301,14 @@ __global__ void __launch_bounds__(256, 2) mlstm_fw_walk(MArgs a) {
   constexpr int LQ = DQ + kPad, LC = kCB + kPad;
   constexpr int TJ = kCB / 16, NI = DQ / 16, NT = NI * TJ, PW = NT / 4;
   static_assert(NT % 4 == 0, "tile count must split over 4 waves");
-  const int cb = blockIdx.x, bh = blockIdx.y, w = threadIdx.x >> 6;
+  // MODE 0: the whole walk.  MODE 1: the state walk alone (gates, C~ / n~ / m and the state
+  // image; no outputs).  MODE 2: one chunk's outputs per workgroup (blockIdx.y = bh nc + k), from
+  // the state image, n~_k and m_k the state walk left in HBM -- every chunk at once.
+  constexpr bool kState = MODE != 2, kOut = MODE != 1;
+  const int cb = blockIdx.x, w = threadIdx.x >> 6;
+  const int bh = MODE == 2 ? (int)blockIdx.y / a.nc : (int)blockIdx.y;
+  const int k_begin = MODE == 2 ? (int)blockIdx.y % a.nc : 0;
+  const int k_end = MODE == 2 ? k_begin + 1 : a.nc;
   int tid = threadIdx.x, lane = tid & 63;
   const int cj0 = cb * kCB;
   __shared__ __attribute__((aligned(16))) T Qs[kL * LQ];
@@ -316,7 +324,7 @@ __global__ void __launch_bounds__(256, 2) mlstm_fw_walk(MArgs a) {
   T* H = (T*)a.h + (int64_t)bh * a.T * DV;
   f32x4 acc[PW];   // C~ tiles q = w + 4 p: rows i0 = 16 (q / TJ), block columns 16 (q % TJ)
 #pragma unroll
-  for (int p = 0; p < PW; ++p) {
+  for (int p = 0; p < (kState ? PW : 0); ++p) {
     const int q = w + 4 * p, i0 = 16 * (q / TJ), j0 = cj0 + 16 * (q % TJ);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -329,6 +337,10 @@ __global__ void __launch_bounds__(256, 2) mlstm_fw_walk(MArgs a) {
   float n = (tid < DQ && a.n0) ? a.n0[(int64_t)bh * DQ + tid] : 0.0f;
   float decay = 1.0f;
   float m = a.m0 ? a.m0[bh] : 0.0f;
+  if constexpr (MODE == 2) {
+    n = tid < DQ ? a.ns[((int64_t)bh * (a.nc + 1) + k_begin) * DQ + tid] : 0.0f;
+    m = a.ms[(int64_t)bh * (a.nc + 1) + k_begin];
+  }
   // chunk inputs are prefetched into registers one chunk ahead: the loads of chunk k + 1 are
   // issued right after chunk k's are written to LDS and land while chunk k computes
   constexpr int NQP = kL * DQ / 8 / 256, NVP = kL * kCB / 8 / 256;
@@ -340,7 +352,7 @@ __global__ void __launch_bounds__(256, 2) mlstm_fw_walk(MArgs a) {
 #pragma unroll
     for (int u = 0; u < NQP; ++u) {
       const int e = tid + 256 * u, r = e / (DQ / 8), c = (e % (DQ / 8)) * 8;
-      pq[u] = *(const u32x4*)(Q + (tb + r) * a.qt + c);
+      if (kOut) pq[u] = *(const u32x4*)(Q + (tb + r) * a.qt + c);
       pk[u] = *(const u32x4*)(K + (tb + r) * a.qt + c);
     }
 #pragma unroll
@@ -352,27 +364,29 @@ __global__ void __launch_bounds__(256, 2) mlstm_fw_walk(MArgs a) {
     pig = a.ig[o];
     pfg = a.fg[o];
   };
-  prefetch(0);
-  for (int k = 0; k < a.nc; ++k) {
+  prefetch(k_begin);
+  for (int k = k_begin; k < k_end; ++k) {
     const int64_t t0 = (int64_t)k * kL;
     // re-derive the lane-dependent addresses every chunk instead of holding dozens of them in
     // VGPRs across the loop (hoisted, they pushed the prefetch registers out to scratch)
     asm volatile("" : "+v"(tid), "+v"(lane));
     const ChunkGates G = chunk_gate_math(pig, pfg, m, a.scale, lane);
-    if (k > 0 && tid < DQ) n = decay * n + np2[tid] + np2[DQ + tid];   // previous chunk's update
+    if (kState && k > 0 && tid < DQ) n = decay * n + np2[tid] + np2[DQ + tid];   // previous chunk's update
     decay = G.decay;
     if (!ML_ABL(16)) {
 #pragma unroll
       for (int u = 0; u < NQP; ++u) {
         const int e = tid + 256 * u, r = e / (DQ / 8), c = (e % (DQ / 8)) * 8;
-        *(V8*)(Qs + r * LQ + c) = cvt8<DT, IO>(pq[u]);
+        if (kOut) *(V8*)(Qs + r * LQ + c) = cvt8<DT, IO>(pq[u]);
         const V8 x = cvt8<DT, IO>(pk[u]);
         *(V8*)(Ks + r * LQ + c) = x;
-        const float f = __shfl(G.fs, r);
-        V8 y;
+        if constexpr (kState) {
+          const float f = __shfl(G.fs, r);
+          V8 y;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) y[j] = (T)((float)x[j] * f);
-        *(V8*)(Kf + r * LQ + c) = y;
+          for (int j = 0; j < 8; ++j) y[j] = (T)((float)x[j] * f);
+          *(V8*)(Kf + r * LQ + c) = y;
+        }
       }
 #pragma unroll
       for (int u = 0; u < NVP; ++u) {
@@ -387,11 +401,20 @@ __global__ void __launch_bounds__(256, 2) mlstm_fw_walk(MArgs a) {
       rowfs[lane] = G.rowf;
       fsv[lane] = G.fs;
     }
-    if (k + 1 < a.nc) prefetch(k + 1);
+    if (kState && k + 1 < a.nc) prefetch(k + 1);
+    if constexpr (MODE == 2) {   // the state walk's image of C~_k[:, block], rows [j][i] as stored
+      const T* Cs = (const T*)a.Cs + (((int64_t)bh * a.nc + k) * DV + cj0) * DQ;
+      constexpr int NCP = kCB * DQ / 8 / 256;
+#pragma unroll
+      for (int u = 0; u < NCP; ++u) {
+        const int e = tid + 256 * u, j = e / (DQ / 8), c = (e % (DQ / 8)) * 8;
+        *(u32x4*)(CT + j * LQ + c) = *(const u32x4*)(Cs + j * DQ + c);
+      }
+    }
     // the state at the chunk start: its MFMA image, transposed ([j][i]); a lane's four
     // accumulator rows are consecutive i, so each tile is one 8-byte LDS store
 #pragma unroll
-    for (int p = 0; p < PW; ++p) {
+    for (int p = 0; p < (kState ? PW : 0); ++p) {
       const int q = w + 4 * p, i0 = 16 * (q / TJ), j0 = 16 * (q % TJ);
       v4t c;
 #pragma unroll
@@ -400,12 +423,12 @@ __global__ void __launch_bounds__(256, 2) mlstm_fw_walk(MArgs a) {
     }
     if (tid < DQ) {
       nk[tid] = n;
-      if (cb == 0) a.ns[((int64_t)bh * (a.nc + 1) + k) * DQ + tid] = n;
+      if (kState && cb == 0) a.ns[((int64_t)bh * (a.nc + 1) + k) * DQ + tid] = n;
     }
-    if (cb == 0 && tid == 0) a.ms[(int64_t)bh * (a.nc + 1) + k] = m;
+    if (kState && cb == 0 && tid == 0) a.ms[(int64_t)bh * (a.nc + 1) + k] = m;
     __syncthreads();
     // the backward's copy of the chunk-start state: CT's rows as they are, [j][i] (16-byte stores)
-    {
+    if constexpr (kState) {
       T* Cs = (T*)a.Cs + (((int64_t)bh * a.nc + k) * DV + cj0) * DQ;
       constexpr int NCP = kCB * DQ / 8 / 256;
       static_assert(NCP * 256 * 8 == kCB * DQ, "state image split");
@@ -417,6 +440,7 @@ __global__ void __launch_bounds__(256, 2) mlstm_fw_walk(MArgs a) {
     }
     // From here to the state update every wave touches only its own 16 rows of Ms / qn / dsum
     // (rows 16 w ..): no barrier between the S and H phases.
+    if constexpr (kOut) {
     // q_t . n~_k (4 threads per row, DQ / 4 consecutive i each)
     {
       constexpr int QP = DQ / 4;
@@ -516,6 +540,8 @@ __global__ void __launch_bounds__(256, 2) mlstm_fw_walk(MArgs a) {
         a.den[(int64_t)bh * a.T + t0 + t] = dsum[t] + rowfs[t] * qn[t];
       }
     }
+    }   // kOut
+    if constexpr (!kState) break;
     // state update: C~ <- decay C~ + Kf^T V[:, block];  n~ <- decay n~ + Kf^T 1
 #pragma unroll
     for (int p = 0; p < PW; ++p) {
@@ -538,6 +564,7 @@ __global__ void __launch_bounds__(256, 2) mlstm_fw_walk(MArgs a) {
     m = G.mn;
     __syncthreads();
   }
+  if constexpr (!kState) return;
   // final state: fp32 (the carried segment state) + n~, m
 #pragma unroll
   for (int p = 0; p < PW; ++p) {
@@ -1079,9 +1106,23 @@ __global__ void __launch_bounds__(512, 1) mlstm_bw_walk(MArgs a) {
   if (tid < DQ) a.dns[(int64_t)bh * DQ + tid] = dn * inv;
 }
 
+// SC_MLSTM_SPLIT=0 (environment, read per launch): the forward as one walk that also computes
+// the outputs (A/B timing, and the bitwise split-vs-walk test); default: the state walk, then
+// every chunk's outputs in parallel
+bool fwd_split() {
+  const char* e = getenv("SC_MLSTM_SPLIT");
+  return !(e && e[0] == '0');
+}
 template <int DT, int IO, int DQ, int DV>
 void launch_fwd(const MArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL((mlstm_fw_walk<DT, IO, DQ, DV>), dim3(DV / kCB, a.BH), dim3(256), 0, st, a);
+  if (!fwd_split()) {
+    hipLaunchKernelGGL((mlstm_fw_walk<DT, IO, DQ, DV, 0>), dim3(DV / kCB, a.BH), dim3(256), 0, st, a);
+    return;
+  }
+  hipLaunchKernelGGL((mlstm_fw_walk<DT, IO, DQ, DV, 1>), dim3(DV / kCB, a.BH), dim3(256), 0, st, a);
+  if (a.nc > 0)
+    hipLaunchKernelGGL((mlstm_fw_walk<DT, IO, DQ, DV, 2>), dim3(DV / kCB, a.BH * a.nc), dim3(256), 0,
+                       st, a);
 }
 template <int DT, int IO, int DQ, int DV>
 void launch_bwd(const MArgs& a, hipStream_t st) {

@@ -585,37 +585,6 @@ __device__ __forceinline__ jbf8 pack8(const float* p) {
   return r;
 }
 
-// the two arcs' occupancies of node (b, t, u) x the sequence's loss scale (as rnnt_grad_kernel;
-// both <= 0 there, returned here as positive weights wb, wy)
-__device__ __forceinline__ void node_weights(const RnntArgs& a, int b, int t, int u, int Tb, int Ub,
-                                             float& wb, float& wy) {
-  wb = 0.0f;
-  wy = 0.0f;
-  const double lp2 = a.ws.logp2[b];
-  const float sc = a.scale[b];
-  const int n = t + u;
-  const int64_t base = (int64_t)b * a.ND * a.U1p;
-  const int per = 2 * a.kh, nd = Tb + Ub;
-  const double oA = a.ws.offA[(int64_t)b * a.ND + (n + 1) / per];
-  const double oB = a.ws.offB[(int64_t)b * a.ND + (nd - n - 1) / per];
-  const double al = (double)a.ws.alpha[base + (int64_t)n * a.U1p + u] + oA;
-  const float eb = a.ws.lpb[base + (int64_t)n * a.U1p + u];
-  if (t + 1 < Tb) {
-    const double be = (double)a.ws.beta[base + (int64_t)(n + 1) * a.U1p + u] + oB;
-    wb = exp2_((float)(al + eb + be - lp2));
-  } else if (u == Ub) {
-    wb = exp2_((float)(al + eb - lp2));
-  }
-  if (u < Ub) {
-    const float ey = a.ws.lpy[base + (int64_t)n * a.U1p + u];
-    const double be = (double)a.ws.beta[base + (int64_t)(n + 1) * a.U1p + u + 1] + oB;
-    wy = exp2_((float)(al + ey + be - lp2));
-  }
-  const bool live = lp2 > -1e300 && sc != 0.0f;   // infeasible sequence or no gradient: zero
-  wb = live ? wb * sc : 0.0f;
-  wy = live ? wy * sc : 0.0f;
-}
-
 // cooperative copy of W (bf16 [V][64]) and bias into the LDS images
 __device__ __forceinline__ void load_w(const JointArgs& a, unsigned char* lds) {
   const int V = a.r.V;
@@ -796,50 +765,74 @@ __global__ void __launch_bounds__(512) joint_fwd_kernel(JointArgs a) {
 #ifndef SC_JOINT_ABL
 #define SC_JOINT_ABL 0
 #endif
+// SC_JOINT_PRIO: s_setprio 1 on waves 4-7 for the whole kernel (MI355X_MICROARCH.md, "Two waves
+// per SIMD", item 4: the second-dispatched half loses every arbitration to its older partner).
+// Measured (tools/joint_probe.py, C5 B=32, A/B in one process): 6.80-6.87 -> 6.20-6.26 ms.
+#ifndef SC_JOINT_PRIO
+#define SC_JOINT_PRIO 1
+#endif
+#ifndef SC_JOINT_ST8   // 1: column staging on all 8 waves (0: waves 0-3, A/B in tools only)
+#define SC_JOINT_ST8 1
+#endif
 constexpr int kVbWg = 16;   // vocab blocks (of 32) per workgroup
 constexpr int kJW = 8;      // waves per workgroup: two per SIMD, so one wave's exp / pack /
                             // transpose work runs beside the other's MFMAs (<= 256 registers each)
 constexpr int kVbW = kVbWg / kJW;   // vocab blocks per wave
 
-struct NodeLd {   // the loads of node_weights, issued one column ahead
-  double lp2, oA, oB, be_b, be_y;
-  float al, eb, ey, sc, lse;
-  bool ok;
-};
-
-__device__ __forceinline__ NodeLd node_load(const RnntArgs& a, int b, int t, int u, int Tb, int Ub) {
-  NodeLd d;
-  d.ok = t < Tb && u <= Ub;
-  const int tc = d.ok ? t : 0, uc = d.ok ? u : 0;
-  d.lp2 = a.ws.logp2[b];
-  d.sc = a.scale[b];
+// Node scalars of a column (the arcs' occupancies need alpha, beta, the emissions, lse and the
+// fp64 offsets) and its pred row come into LDS by LDS-DMA one column ahead (wave 0; lanes 0..31 =
+// the column's 32 nodes), not into VGPRs: a register prefetch held 24 registers across the
+// column (the kernel spilled at 256) and was drained by the first scratch reload's or label
+// load's vmcnt(0), one column early.  Field f of node i sits at [f][i].
+constexpr int kNF = 11;   // alpha, lpb, lpy, beta(t+1), beta(u+1), lse, offA lo/hi, offB lo/hi, label
+__device__ __forceinline__ void node_dma(const RnntArgs& a, int b, int t, int u, int Tb, int Ub,
+                                         uint32_t dst) {
+  const bool ok = t < Tb && u <= Ub;
+  const int tc = ok ? t : 0, uc = ok ? u : 0;
   const int n = tc + uc;
   const int64_t base = (int64_t)b * a.ND * a.U1p;
   const int per = 2 * a.kh, nd = Tb + Ub;
-  d.oA = a.ws.offA[(int64_t)b * a.ND + (n + 1) / per];
-  d.oB = a.ws.offB[(int64_t)b * a.ND + max(nd - n - 1, 0) / per];
-  d.al = a.ws.alpha[base + (int64_t)n * a.U1p + uc];
-  d.eb = a.ws.lpb[base + (int64_t)n * a.U1p + uc];
-  d.ey = a.ws.lpy[base + (int64_t)n * a.U1p + uc];
-  d.be_b = a.ws.beta[base + (int64_t)(n + 1) * a.U1p + uc];
-  d.be_y = a.ws.beta[base + (int64_t)(n + 1) * a.U1p + min(uc + 1, a.U1p - 1)];
-  d.lse = a.ws.lse[((int64_t)b * a.T + tc) * a.U1 + uc];
-  return d;
+  dma_to_lds<4>(a.ws.alpha + base + (int64_t)n * a.U1p + uc, dst);
+  dma_to_lds<4>(a.ws.lpb + base + (int64_t)n * a.U1p + uc, dst + 128);
+  dma_to_lds<4>(a.ws.lpy + base + (int64_t)n * a.U1p + uc, dst + 2 * 128);
+  // (row n + 1 = ND for the lattice's last node of the last sequence: the workspace's next
+  // region, read and never used)
+  dma_to_lds<4>(a.ws.beta + base + (int64_t)(n + 1) * a.U1p + uc, dst + 3 * 128);
+  dma_to_lds<4>(a.ws.beta + base + (int64_t)(n + 1) * a.U1p + min(uc + 1, a.U1p - 1), dst + 4 * 128);
+  dma_to_lds<4>(a.ws.lse + ((int64_t)b * a.T + tc) * a.U1 + uc, dst + 5 * 128);
+  const double* oa = a.ws.offA + (int64_t)b * a.ND + (n + 1) / per;
+  const double* ob = a.ws.offB + (int64_t)b * a.ND + max(nd - n - 1, 0) / per;
+  dma_to_lds<4>(oa, dst + 6 * 128);
+  dma_to_lds<4>((const char*)oa + 4, dst + 7 * 128);
+  dma_to_lds<4>(ob, dst + 8 * 128);
+  dma_to_lds<4>((const char*)ob + 4, dst + 9 * 128);
+  // the column's label (low dword of the int64; every lane the same address)
+  if (Ub > 0) dma_to_lds<4>(a.lab + (int64_t)b * a.labs + min(u, Ub - 1), dst + 10 * 128);
 }
 
-// (wb, wy, lse2) of a loaded node, as node_weights computes them
-__device__ __forceinline__ void node_finish(const NodeLd& d, int t, int u, int Tb, int Ub, float& wb,
-                                            float& wy, float& l2) {
+__device__ __forceinline__ float f_at(const uint32_t* f, int k, int i) {
+  return __uint_as_float(f[k * 32 + i]);
+}
+__device__ __forceinline__ double d_at(const uint32_t* f, int k, int i) {
+  return __hiloint2double((int)f[(k + 1) * 32 + i], (int)f[k * 32 + i]);
+}
+
+// (wb, wy, lse2) of node i of a column whose fields landed at f: the two arcs' occupancies x the
+// sequence's loss scale (as rnnt_grad_kernel; both <= 0 there, returned here as positive weights)
+__device__ __forceinline__ void node_finish(const uint32_t* f, int i, double lp2, float sc, int t,
+                                            int u, int Tb, int Ub, float& wb, float& wy, float& l2) {
+  const bool ok = t < Tb && u <= Ub;
   wb = 0.0f;
   wy = 0.0f;
-  const double al = (double)d.al + d.oA;
-  if (t + 1 < Tb) wb = exp2_((float)(al + d.eb + ((double)d.be_b + d.oB) - d.lp2));
-  else if (u == Ub) wb = exp2_((float)(al + d.eb - d.lp2));
-  if (u < Ub) wy = exp2_((float)(al + d.ey + ((double)d.be_y + d.oB) - d.lp2));
-  const bool live = d.ok && d.lp2 > -1e300 && d.sc != 0.0f;
-  wb = live ? wb * d.sc : 0.0f;
-  wy = live ? wy * d.sc : 0.0f;
-  l2 = d.ok ? d.lse * kLog2e : 1e30f;
+  const double al = (double)f_at(f, 0, i) + d_at(f, 6, i);
+  const double oB = d_at(f, 8, i);
+  if (t + 1 < Tb) wb = exp2_((float)(al + f_at(f, 1, i) + ((double)f_at(f, 3, i) + oB) - lp2));
+  else if (u == Ub) wb = exp2_((float)(al + f_at(f, 1, i) - lp2));
+  if (u < Ub) wy = exp2_((float)(al + f_at(f, 2, i) + ((double)f_at(f, 4, i) + oB) - lp2));
+  const bool live = ok && lp2 > -1e300 && sc != 0.0f;
+  wb = live ? wb * sc : 0.0f;
+  wy = live ? wy * sc : 0.0f;
+  l2 = ok ? f_at(f, 5, i) * kLog2e : 1e30f;
 }
 
 struct BwdLds {   // byte offsets of the LDS regions
@@ -850,14 +843,17 @@ struct BwdLds {   // byte offsets of the LDS regions
   static constexpr int kZ = kBias + kVbWg * 32 * 4;     // z bf16 image [2][32][128 B]
   static constexpr int kZP = 36;                        // 1 - z^2 row pitch (floats)
   static constexpr int kZ32 = kZ + 2 * 32 * 128;        // 1 - z^2 fp32 [2][64 j][kZP], node fastest
-  static constexpr int kNs = kZ32 + 2 * 64 * kZP * 4;   // node scalars: c, wb, wy [2][3][32]
-  static constexpr int kRed = kNs + 2 * 3 * 32 * 4;     // d pred partials [2][8][64]
+  static constexpr int kNs = kZ32 + 2 * 64 * kZP * 4;   // node scalars: c, wb, wy, label [2][4][32]
+  static constexpr int kRed = kNs + 2 * 4 * 32 * 4;     // d pred partials [2][8][64]
   static constexpr int kEnc = kRed + 2 * kJW * 64 * 4;  // the task's enc rows fp32 [32][64]
   static constexpr int kP = kEnc + 32 * 64 * 4;         // per-wave p image [8][32][128 B]
   static constexpr int kDe = kP;                        // d enc partials [4][64 j][36], at the
                                                         // task's end: over the p images
-  static constexpr int kEnd = kP + (kJW * 32 * 128 > 4 * 64 * kDeP * 4 ? kJW * 32 * 128
-                                                                        : 4 * 64 * kDeP * 4);
+  static constexpr int kPr = kP + (kJW * 32 * 128 > 4 * 64 * kDeP * 4 ? kJW * 32 * 128
+                                                                       : 4 * 64 * kDeP * 4);
+  // LDS-DMA landing zones, one column ahead: pred rows [2][64] fp32, node fields [2][kNF][32]
+  static constexpr int kNd = kPr + 2 * 64 * 4;
+  static constexpr int kEnd = kNd + 2 * kNF * 32 * 4;
 };
 
 __global__ void __launch_bounds__(64 * kJW) joint_bwd_kernel(JointArgs a) {
@@ -897,8 +893,21 @@ __global__ void __launch_bounds__(64 * kJW) joint_bwd_kernel(JointArgs a) {
   }
   const int ntbp = VS * a.ntb;   // t-block rows of the d pred / g partial layouts
   const int64_t ntask = (int64_t)r.B * a.ntb * a.nus;
+#if SC_JOINT_ST8
+  // staging spread over all 8 waves (node zn, j = 4 jq ..): each wave's share of the column's
+  // serial work (tanh, node scalars, DMA issue, d pred) stays small, so the barrier does not wait
+  // on one loaded wave; the roles: node DMA wave 6, pred DMA wave 5, node_finish wave 7, d pred
+  // wave 4
+  const int zn = th >> 4, jg = th & 15;
+  constexpr bool stager = true;
+  constexpr int kWn = 6, kWp = 5, kWf = 7, kWd = 4;
+#else
   const int zn = (th >> 3) & 31, jg = th & 7;   // staging (threads < 256): node zn, j = 8 jg ..
   const bool stager = th < 256;
+  constexpr int kWn = 0, kWp = 0, kWf = 0, kWd = 0;
+#endif
+  constexpr int kSE = SC_JOINT_ST8 ? 4 : 8;   // staged elements per thread
+  if (SC_JOINT_PRIO && w >= 4) __builtin_amdgcn_s_setprio(1);
   for (int64_t task = slot; task < ntask; task += nslot) {
     const int b = (int)(task / ((int64_t)a.ntb * a.nus));
     const int tb = (int)((task / a.nus) % a.ntb), us = (int)(task % a.nus);
@@ -917,59 +926,90 @@ __global__ void __launch_bounds__(64 * kJW) joint_bwd_kernel(JointArgs a) {
 #pragma unroll
       for (int q = 0; q < 16; ++q) dacc[jb][q] = 0.0f;
     if (ua < ue && stager) {
-      const float* ep = a.enc + ((int64_t)b * r.T + (zok ? tb * 32 + zn : Tb - 1)) * kJ + 8 * jg;
-      *(float4*)(encl + zn * 64 + 8 * jg) = *(const float4*)ep;
-      *(float4*)(encl + zn * 64 + 8 * jg + 4) = *(const float4*)(ep + 4);
+      const float* ep = a.enc + ((int64_t)b * r.T + (zok ? tb * 32 + zn : Tb - 1)) * kJ + kSE * jg;
+#pragma unroll
+      for (int e = 0; e < kSE; e += 4)
+        *(float4*)(encl + zn * 64 + kSE * jg + e) = *(const float4*)(ep + e);
     }
-    // node loads and pred row of the first column (then one column ahead; barriers are LDS-only,
-    // so no load is drained before its use)
-    NodeLd nd{};
-    if (th < 32 && ua < ue) nd = node_load(r, b, tb * 32 + th, ua, Tb, Ub);
-    float4 pn0 = make_float4(0.f, 0.f, 0.f, 0.f), pn1 = pn0;
-    if (ua < ue && stager) {
-      const float* pp = a.pred + ((int64_t)b * r.U1 + ua) * kJ + 8 * jg;
-      pn0 = *(const float4*)pp;
-      pn1 = *(const float4*)(pp + 4);
-    }
-    // stage column uu into buffer bf: z (bf16 image + fp32 1 - z^2), node scalars; the loads of
-    // the column after it are issued here and land while this one computes
+    // the column operands that come from HBM (pred row, node scalars, label) land in LDS one
+    // column ahead by LDS-DMA from wave 0 (node_dma), retired by wave 0's dma_wait() before the
+    // column's barrier; no VGPR holds them and no compiler-visible load sits in the column loop
+    uint32_t* const ndl0 = (uint32_t*)(lds + BwdLds::kNd);   // [2][kNF][32]
+    float* const prl0 = (float*)(lds + BwdLds::kPr);          // [2][64]
+    const double lp2 = r.ws.logp2[b];
+    const float lsc = r.scale[b];
+    auto col_dma = [&](int uu, int bf) __attribute__((always_inline)) {
+      if (w == kWp)
+        dma_to_lds<4>(a.pred + ((int64_t)b * r.U1 + uu) * kJ + lane, lds_addr(prl0 + bf * 64));
+      if (w == kWn && lane < 32)
+        node_dma(r, b, tb * 32 + lane, uu, Tb, Ub, lds_addr(ndl0 + bf * kNF * 32));
+    };
+    auto col_dma_wait = [&]() __attribute__((always_inline)) {
+      if (w == kWp || w == kWn) dma_wait();
+    };
+    // stage column uu into buffer bf: z (bf16 image + fp32 1 - z^2), node scalars, label; the
+    // DMA of the column after it is issued here and lands while this one computes
     auto stage = [&](int uu, int bf) __attribute__((always_inline)) {
       if (!stager) return;
-      const float4 e0 = *(const float4*)(encl + zn * 64 + 8 * jg);
-      const float4 e1 = *(const float4*)(encl + zn * 64 + 8 * jg + 4);
-      const float xs[8] = {e0.x + pn0.x, e0.y + pn0.y, e0.z + pn0.z, e0.w + pn0.w,
-                           e1.x + pn1.x, e1.y + pn1.y, e1.z + pn1.z, e1.w + pn1.w};
-      if (uu + 1 < ue) {
-        const float* pp = a.pred + ((int64_t)b * r.U1 + uu + 1) * kJ + 8 * jg;
-        pn0 = *(const float4*)pp;
-        pn1 = *(const float4*)(pp + 4);
-      }
-      float zf[8];
-      jbf8 zb;
+      const float* pr = prl0 + bf * 64 + kSE * jg;
+      const float* el = encl + zn * 64 + kSE * jg;
+      float xs[kSE];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
+      for (int e = 0; e < kSE; e += 4) {
+        const float4 pv = *(const float4*)(pr + e), ev = *(const float4*)(el + e);
+        xs[e] = ev.x + pv.x;
+        xs[e + 1] = ev.y + pv.y;
+        xs[e + 2] = ev.z + pv.z;
+        xs[e + 3] = ev.w + pv.w;
+      }
+      float zf[kSE];
+      __bf16 zb[kSE];
+#pragma unroll
+      for (int e = 0; e < kSE; ++e) {
         zf[e] = zok ? tanh_(xs[e]) : 0.0f;
         zb[e] = (__bf16)zf[e];
       }
-      *(jbf8*)(zimg0 + bf * 32 * 128 + wimg(zn, jg)) = zb;
+      if constexpr (kSE == 8) {
+        jbf8 z8;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) z8[e] = zb[e];
+        *(jbf8*)(zimg0 + bf * 32 * 128 + wimg(zn, jg)) = z8;
+      } else {
+        typedef __bf16 jbf4 __attribute__((ext_vector_type(4)));
+        *(jbf4*)(zimg0 + bf * 32 * 128 + wimg(zn, jg >> 1) + 8 * (jg & 1)) =
+            jbf4{zb[0], zb[1], zb[2], zb[3]};
+      }
       // tanh' = 1 - z^2, once per element (every wave scales its dZ partial by it)
       // ([j][n]: the epilogue reads a lane's four consecutive nodes as one 16-byte piece)
-      float* zz = z320 + bf * 64 * BwdLds::kZP + 8 * jg * BwdLds::kZP + zn;
+      float* zz = z320 + bf * 64 * BwdLds::kZP + kSE * jg * BwdLds::kZP + zn;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) zz[e * BwdLds::kZP] = 1.0f - zf[e] * zf[e];
-      if (th < 32) {
+      for (int e = 0; e < kSE; ++e) zz[e * BwdLds::kZP] = 1.0f - zf[e] * zf[e];
+      if (w == kWf && lane < 32) {
+        const int th = lane;
+        const uint32_t* nf = ndl0 + bf * kNF * 32;
         float wb, wy, l2;
-        node_finish(nd, tb * 32 + th, uu, Tb, Ub, wb, wy, l2);
+        node_finish(nf, th, lp2, lsc, tb * 32 + th, uu, Tb, Ub, wb, wy, l2);
         const float an = wb + wy;
         // p = a exp2(x log2e + b log2e - l2) = exp2(x log2e + b log2e + c), c = log2 a - l2
-        float* ns = ns0 + bf * 96;
+        float* ns = ns0 + bf * 128;
         ns[th] = an > 0.0f ? log2_(an) - l2 : -1e30f;
         ns[32 + th] = wb;
         ns[64 + th] = wy;
-        if (uu + 1 < ue) nd = node_load(r, b, tb * 32 + th, uu + 1, Tb, Ub);   // in flight
+        if (th == 0) {
+          const int lab = (int)nf[10 * 32];
+          ((int*)ns)[96] = uu < Ub ? (lab < 0 ? 0 : (lab >= r.V ? r.V - 1 : lab)) : r.blank;
+        }
       }
+      // (every read of DMA buffer bf ^ 1 happened before the barrier that ended column uu - 2)
+      if (uu + 1 < ue) col_dma(uu + 1, bf ^ 1);
     };
-    if (ua < ue) stage(ua, 0);
+    if (ua < ue) {
+      col_dma(ua, 0);
+      col_dma_wait();
+      lds_barrier();   // the first column's DMA has landed
+      stage(ua, 0);
+    }
+    col_dma_wait();
     lds_barrier();
     for (int u = ua; u < ue; ++u) {
       // lane-dependent addresses re-derived per column, not held across it (register budget of
@@ -978,7 +1018,7 @@ __global__ void __launch_bounds__(64 * kJW) joint_bwd_kernel(JointArgs a) {
       const int cb = (u - ua) & 1;
       const unsigned char* zimg = zimg0 + cb * 32 * 128;
       const float* z32 = z320 + cb * 64 * BwdLds::kZP;
-      const float* ns_c = ns0 + cb * 96;
+      const float* ns_c = ns0 + cb * 128;
       const float* ns_wb = ns_c + 32;
       const float* ns_wy = ns_c + 64;
       float* red = red0 + cb * kJW * 64;
@@ -993,7 +1033,7 @@ __global__ void __launch_bounds__(64 * kJW) joint_bwd_kernel(JointArgs a) {
       for (int jb = 0; jb < 2; ++jb)
 #pragma unroll
         for (int q = 0; q < 16; ++q) Y[jb][q] = 0.0f;
-      const int yl = u < Ub ? label_at(r, b, u) : r.blank;
+      const int yl = uniform(((const int*)ns_c)[96]);
       // logits of vocab block k (W rows of a block past the vocabulary: block 0, p forced to 0)
       auto logits_blk = [&](int k) __attribute__((always_inline)) {
         const int lvb = w + kJW * k;
@@ -1125,13 +1165,15 @@ __global__ void __launch_bounds__(64 * kJW) joint_bwd_kernel(JointArgs a) {
       }
       if (SC_JOINT_ABL & 2) asm volatile("" :: "v"(Y[0]), "v"(Y[1]));
       // the column's one barrier: its d pred partials and the next column's operands are
-      // complete, and this column's buffer is free for column u + 2
+      // complete (wave 0's DMA of column u + 2 included), and this column's buffer is free for
+      // column u + 2
+      col_dma_wait();
       lds_barrier();
-      if (th < 64) {   // d pred of this column: the wave partials (red buffers alternate)
+      if (w == kWd) {   // d pred of this column: the wave partials (red buffers alternate)
         float s = 0.0f;
 #pragma unroll
-        for (int ww = 0; ww < kJW; ++ww) s += red[ww * 64 + th];
-        a.d_pred[(((int64_t)b * ntbp + vh * a.ntb + tb) * r.U1 + u) * kJ + th] = s;
+        for (int ww = 0; ww < kJW; ++ww) s += red[ww * 64 + lane];
+        a.d_pred[(((int64_t)b * ntbp + vh * a.ntb + tb) * r.U1 + u) * kJ + lane] = s;
       }
     }
     // d enc of the task: the 8 waves' register partials meet in 4 LDS slots (waves w and w + 4

@@ -146,3 +146,37 @@ def test_xlstm_asr_ctc_training_step_runs_and_learns():
     assert isinstance(tr.encoder_state, dict) and len(tr.encoder_state) == 2
     assert np.isfinite(losses).all()
     assert np.mean(losses[-3:]) < 0.8 * np.mean(losses[:3])
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("DQ,DV,T", [(96, 192, 320), (32, 64, 192), (64, 128, 128)])
+def test_mlstm_fwd_split_bitwise_equals_walk(dtype, DQ, DV, T, monkeypatch):
+    """The forward as a state walk + chunk-parallel output kernel (default) is bitwise the single
+    walk (SC_MLSTM_SPLIT=0): same operations on the same state image, so h, the carried state
+    and every gradient (the backward reads the forward's state image, m and den) agree exactly,
+    with and without an initial state."""
+    g = torch.Generator(device=DEV).manual_seed(7)
+    BH = 6
+    q = torch.randn(1, BH, T, DQ, device=DEV, generator=g).to(dtype)
+    k = torch.randn(1, BH, T, DQ, device=DEV, generator=g).to(dtype)
+    v = torch.randn(1, BH, T, DV, device=DEV, generator=g).to(dtype)
+    ig = torch.randn(1, BH, T, device=DEV, generator=g) * 3
+    fg = torch.randn(1, BH, T, device=DEV, generator=g) * 2 + 3
+    c0 = torch.randn(1, BH, DQ, DV, device=DEV, generator=g) * 0.1
+    n0 = torch.randn(1, BH, DQ, device=DEV, generator=g) * 0.1
+    m0 = torch.randn(1, BH, 1, device=DEV, generator=g)
+    dh = torch.randn(1, BH, T, DV, device=DEV, generator=g).to(dtype)
+
+    def run(split, init):
+        monkeypatch.setenv("SC_MLSTM_SPLIT", "1" if split else "0")
+        leaves = [x.clone().requires_grad_(True) for x in (q, k, v, ig, fg)]
+        st = (c0, n0, m0) if init else (None, None, None)
+        h, (C, n, m) = ops().mlstm_chunkwise(*leaves, *st, return_last_states=True)
+        torch.autograd.backward([h, C.sum()], [dh, None])
+        torch.cuda.synchronize()
+        return [h, C, n, m] + [x.grad for x in leaves]
+
+    for init in (False, True):
+        a, b = run(True, init), run(False, init)
+        for i, (x, y) in enumerate(zip(a, b)):
+            assert torch.equal(x, y), (init, i)

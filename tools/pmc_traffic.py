@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Per-launch HBM traffic of the scan kernels from two rocprofv3 PMC passes.
+"""Per-launch HBM traffic of the scan and mLSTM kernels from two rocprofv3 PMC passes.
 
 usage: tools/pmc_traffic.py FETCH_counter_collection.csv WRITE_counter_collection.csv [out.json]
 
@@ -16,7 +16,10 @@ import sys
 from collections import defaultdict
 
 NAMES = {"lucy_scan_fwd_kernel": "lucy_scan_fwd", "lucy_scan_bwd_kernel": "lucy_scan_bwd",
-         "decay_scan_fwd_kernel": "decay_scan_fwd", "decay_scan_bwd_kernel": "decay_scan_bwd"}
+         "decay_scan_fwd_kernel": "decay_scan_fwd", "decay_scan_bwd_kernel": "decay_scan_bwd",
+         # the mLSTM walks read q / k / v / h / dh and the state image as 16-byte-per-lane rows
+         # (the same FETCH_SIZE calibration)
+         "mlstm_fw_walk": "mlstm_fwd", "mlstm_bw_walk": "mlstm_bwd"}
 
 
 def per_kernel(path, counter):
@@ -39,6 +42,14 @@ def main():
         w = sum(write[name]) / len(write[name])
         out[name] = {"hbm_bytes_per_launch": round(f + w), "fetch_bytes": round(f),
                      "write_bytes": round(w), "dispatches": len(fetch[name])}
+    if len(sys.argv) > 3:
+        # merge into an existing table (passes over different workloads fill different kernels)
+        try:
+            prev = json.load(open(sys.argv[3]))
+        except (OSError, ValueError):
+            prev = {}
+        prev.update(out)
+        out = prev
     txt = json.dumps(out, indent=1)
     if len(sys.argv) > 3:
         open(sys.argv[3], "w").write(txt + "\n")
