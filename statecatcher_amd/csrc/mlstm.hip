@@ -302,13 +302,11 @@ __global__ void __launch_bounds__(256, 2) mlstm_fw_walk(MArgs a) {
   constexpr int TJ = kCB / 16, NI = DQ / 16, NT = NI * TJ, PW = NT / 4;
   static_assert(NT % 4 == 0, "tile count must split over 4 waves");
   // MODE 0: the whole walk.  MODE 1: the state walk alone (gates, C~ / n~ / m and the state
-  // image; no outputs).  MODE 2: one chunk's outputs per workgroup (blockIdx.y = bh nc + k), from
-  // the state image, n~_k and m_k the state walk left in HBM -- every chunk at once.
-  constexpr bool kState = MODE != 2, kOut = MODE != 1;
+  // image; the outputs come from mlstm_fw_out).
+  static_assert(MODE == 0 || MODE == 1, "walk modes");
+  constexpr bool kOut = MODE == 0;
   const int cb = blockIdx.x, w = threadIdx.x >> 6;
-  const int bh = MODE == 2 ? (int)blockIdx.y / a.nc : (int)blockIdx.y;
-  const int k_begin = MODE == 2 ? (int)blockIdx.y % a.nc : 0;
-  const int k_end = MODE == 2 ? k_begin + 1 : a.nc;
+  const int bh = (int)blockIdx.y;
   int tid = threadIdx.x, lane = tid & 63;
   const int cj0 = cb * kCB;
   __shared__ __attribute__((aligned(16))) T Qs[kL * LQ];
@@ -324,7 +322,7 @@ __global__ void __launch_bounds__(256, 2) mlstm_fw_walk(MArgs a) {
   T* H = (T*)a.h + (int64_t)bh * a.T * DV;
   f32x4 acc[PW];   // C~ tiles q = w + 4 p: rows i0 = 16 (q / TJ), block columns 16 (q % TJ)
 #pragma unroll
-  for (int p = 0; p < (kState ? PW : 0); ++p) {
+  for (int p = 0; p < PW; ++p) {
     const int q = w + 4 * p, i0 = 16 * (q / TJ), j0 = cj0 + 16 * (q % TJ);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -337,10 +335,6 @@ __global__ void __launch_bounds__(256, 2) mlstm_fw_walk(MArgs a) {
   float n = (tid < DQ && a.n0) ? a.n0[(int64_t)bh * DQ + tid] : 0.0f;
   float decay = 1.0f;
   float m = a.m0 ? a.m0[bh] : 0.0f;
-  if constexpr (MODE == 2) {
-    n = tid < DQ ? a.ns[((int64_t)bh * (a.nc + 1) + k_begin) * DQ + tid] : 0.0f;
-    m = a.ms[(int64_t)bh * (a.nc + 1) + k_begin];
-  }
   // chunk inputs are prefetched into registers one chunk ahead: the loads of chunk k + 1 are
   // issued right after chunk k's are written to LDS and land while chunk k computes
   constexpr int NQP = kL * DQ / 8 / 256, NVP = kL * kCB / 8 / 256;
@@ -364,14 +358,14 @@ __global__ void __launch_bounds__(256, 2) mlstm_fw_walk(MArgs a) {
     pig = a.ig[o];
     pfg = a.fg[o];
   };
-  prefetch(k_begin);
-  for (int k = k_begin; k < k_end; ++k) {
+  prefetch(0);
+  for (int k = 0; k < a.nc; ++k) {
     const int64_t t0 = (int64_t)k * kL;
     // re-derive the lane-dependent addresses every chunk instead of holding dozens of them in
     // VGPRs across the loop (hoisted, they pushed the prefetch registers out to scratch)
     asm volatile("" : "+v"(tid), "+v"(lane));
     const ChunkGates G = chunk_gate_math(pig, pfg, m, a.scale, lane);
-    if (kState && k > 0 && tid < DQ) n = decay * n + np2[tid] + np2[DQ + tid];   // previous chunk's update
+    if (k > 0 && tid < DQ) n = decay * n + np2[tid] + np2[DQ + tid];   // previous chunk's update
     decay = G.decay;
     if (!ML_ABL(16)) {
 #pragma unroll
@@ -380,7 +374,7 @@ __global__ void __launch_bounds__(256, 2) mlstm_fw_walk(MArgs a) {
         if (kOut) *(V8*)(Qs + r * LQ + c) = cvt8<DT, IO>(pq[u]);
         const V8 x = cvt8<DT, IO>(pk[u]);
         *(V8*)(Ks + r * LQ + c) = x;
-        if constexpr (kState) {
+        {
           const float f = __shfl(G.fs, r);
           V8 y;
 #pragma unroll
@@ -395,26 +389,19 @@ __global__ void __launch_bounds__(256, 2) mlstm_fw_walk(MArgs a) {
       }
     }
     if (w == 0) {
-      sb[lane] = G.b;
-      si[lane] = G.i;
-      mts[lane] = G.mt;
-      rowfs[lane] = G.rowf;
+      if constexpr (kOut) {
+        sb[lane] = G.b;
+        si[lane] = G.i;
+        mts[lane] = G.mt;
+        rowfs[lane] = G.rowf;
+      }
       fsv[lane] = G.fs;
     }
-    if (kState && k + 1 < a.nc) prefetch(k + 1);
-    if constexpr (MODE == 2) {   // the state walk's image of C~_k[:, block], rows [j][i] as stored
-      const T* Cs = (const T*)a.Cs + (((int64_t)bh * a.nc + k) * DV + cj0) * DQ;
-      constexpr int NCP = kCB * DQ / 8 / 256;
-#pragma unroll
-      for (int u = 0; u < NCP; ++u) {
-        const int e = tid + 256 * u, j = e / (DQ / 8), c = (e % (DQ / 8)) * 8;
-        *(u32x4*)(CT + j * LQ + c) = *(const u32x4*)(Cs + j * DQ + c);
-      }
-    }
+    if (k + 1 < a.nc) prefetch(k + 1);
     // the state at the chunk start: its MFMA image, transposed ([j][i]); a lane's four
     // accumulator rows are consecutive i, so each tile is one 8-byte LDS store
 #pragma unroll
-    for (int p = 0; p < (kState ? PW : 0); ++p) {
+    for (int p = 0; p < PW; ++p) {
       const int q = w + 4 * p, i0 = 16 * (q / TJ), j0 = 16 * (q % TJ);
       v4t c;
 #pragma unroll
@@ -423,12 +410,12 @@ __global__ void __launch_bounds__(256, 2) mlstm_fw_walk(MArgs a) {
     }
     if (tid < DQ) {
       nk[tid] = n;
-      if (kState && cb == 0) a.ns[((int64_t)bh * (a.nc + 1) + k) * DQ + tid] = n;
+      if (cb == 0) a.ns[((int64_t)bh * (a.nc + 1) + k) * DQ + tid] = n;
     }
-    if (kState && cb == 0 && tid == 0) a.ms[(int64_t)bh * (a.nc + 1) + k] = m;
+    if (cb == 0 && tid == 0) a.ms[(int64_t)bh * (a.nc + 1) + k] = m;
     __syncthreads();
     // the backward's copy of the chunk-start state: CT's rows as they are, [j][i] (16-byte stores)
-    if constexpr (kState) {
+    {
       T* Cs = (T*)a.Cs + (((int64_t)bh * a.nc + k) * DV + cj0) * DQ;
       constexpr int NCP = kCB * DQ / 8 / 256;
       static_assert(NCP * 256 * 8 == kCB * DQ, "state image split");
@@ -541,7 +528,6 @@ __global__ void __launch_bounds__(256, 2) mlstm_fw_walk(MArgs a) {
       }
     }
     }   // kOut
-    if constexpr (!kState) break;
     // state update: C~ <- decay C~ + Kf^T V[:, block];  n~ <- decay n~ + Kf^T 1
 #pragma unroll
     for (int p = 0; p < PW; ++p) {
@@ -564,7 +550,6 @@ __global__ void __launch_bounds__(256, 2) mlstm_fw_walk(MArgs a) {
     m = G.mn;
     __syncthreads();
   }
-  if constexpr (!kState) return;
   // final state: fp32 (the carried segment state) + n~, m
 #pragma unroll
   for (int p = 0; p < PW; ++p) {
@@ -577,6 +562,181 @@ __global__ void __launch_bounds__(256, 2) mlstm_fw_walk(MArgs a) {
   if (cb == 0) {
     if (tid < DQ) a.ns[((int64_t)bh * (a.nc + 1) + a.nc) * DQ + tid] = n;
     if (tid == 0) a.ms[(int64_t)bh * (a.nc + 1) + a.nc] = m;
+  }
+}
+
+// Every chunk's outputs at once, after the state walk (mlstm_fw_walk MODE 1): one workgroup per
+// (b,h, chunk) computes S, the decay-masked M, q.n~_k and the normaliser ONCE and then H for every
+// 64-column block from the state image the walk stored (V / C~ blocks prefetched into registers
+// one block ahead).  The operations and their order are the walk's H phase: bitwise the same h.
+template <int DT, int IO, int DQ, int DV>
+__global__ void __launch_bounds__(256, 2) mlstm_fw_out(MArgs a) {
+  using M = MF<DT>;
+  using T = typename M::T;
+  using V8 = typename M::v8;
+  constexpr int LQ = DQ + kPad, LC = kCB + kPad;
+  constexpr int TJ = kCB / 16, NCB = DV / kCB;
+  constexpr int NQP = kL * DQ / 8 / 256, NVP = kL * kCB / 8 / 256, NCP = kCB * DQ / 8 / 256;
+  static_assert(NQP * 256 * 8 == kL * DQ && NVP * 256 * 8 == kL * kCB &&
+                NCP * 256 * 8 == kCB * DQ, "piece split");
+  const int bh = (int)blockIdx.x / a.nc, k = (int)blockIdx.x % a.nc, w = threadIdx.x >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  __shared__ __attribute__((aligned(16))) T Qs[kL * LQ];
+  __shared__ __attribute__((aligned(16))) T Ks[kL * LQ];
+  __shared__ __attribute__((aligned(16))) T Vs[kL * LC];
+  __shared__ __attribute__((aligned(16))) T Ms[kL * LC];
+  __shared__ __attribute__((aligned(16))) T Hs[kL * LC];
+  __shared__ __attribute__((aligned(16))) T CT[kCB * LQ];   // C~_k[:, block], [j][i]
+  __shared__ float sb[kL], si[kL], mts[kL], rowfs[kL], dsum[kL], qn[kL], nk[DQ];
+  const int64_t t0 = (int64_t)k * kL;
+  const T* Q = (const T*)a.q + qrow(a, bh, t0);
+  const T* K = (const T*)a.k + qrow(a, bh, t0);
+  const T* V = (const T*)a.v + vrow(a, bh, t0);
+  T* H = (T*)a.h + ((int64_t)bh * a.T + t0) * DV;
+  const T* Csb = (const T*)a.Cs + ((int64_t)bh * a.nc + k) * DV * DQ;
+  u32x4 pv[NVP], pc[NCP];
+  auto load_blk = [&](int c) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < NVP; ++u) {
+      const int e = tid + 256 * u, r = e / (kCB / 8), cc = (e % (kCB / 8)) * 8;
+      pv[u] = *(const u32x4*)(V + r * a.vt + c * kCB + cc);
+    }
+#pragma unroll
+    for (int u = 0; u < NCP; ++u) {
+      const int e = tid + 256 * u, j = e / (DQ / 8), cc = (e % (DQ / 8)) * 8;
+      pc[u] = *(const u32x4*)(Csb + (int64_t)(c * kCB + j) * DQ + cc);
+    }
+  };
+  auto store_blk = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < NVP; ++u) {
+      const int e = tid + 256 * u, r = e / (kCB / 8), cc = (e % (kCB / 8)) * 8;
+      *(V8*)(Vs + r * LC + cc) = cvt8<DT, IO>(pv[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < NCP; ++u) {
+      const int e = tid + 256 * u, j = e / (DQ / 8), cc = (e % (DQ / 8)) * 8;
+      *(u32x4*)(CT + j * LQ + cc) = pc[u];
+    }
+  };
+  load_blk(0);
+#pragma unroll
+  for (int u = 0; u < NQP; ++u) {
+    const int e = tid + 256 * u, r = e / (DQ / 8), c = (e % (DQ / 8)) * 8;
+    *(V8*)(Qs + r * LQ + c) = cvt8<DT, IO>(*(const u32x4*)(Q + r * a.qt + c));
+    *(V8*)(Ks + r * LQ + c) = cvt8<DT, IO>(*(const u32x4*)(K + r * a.qt + c));
+  }
+  const float m = a.ms[(int64_t)bh * (a.nc + 1) + k];
+  const int64_t o = (int64_t)bh * a.T + t0 + lane;
+  const ChunkGates G = chunk_gate_math(a.ig[o], a.fg[o], m, a.scale, lane);
+  if (w == 0) {
+    sb[lane] = G.b;
+    si[lane] = G.i;
+    mts[lane] = G.mt;
+    rowfs[lane] = G.rowf;
+  }
+  if (tid < DQ) nk[tid] = a.ns[((int64_t)bh * (a.nc + 1) + k) * DQ + tid];
+  store_blk();
+  if (NCB > 1) load_blk(1);
+  __syncthreads();
+  // every wave touches only its own 16 rows of Ms / Hs / qn / dsum from here on (as the walk)
+  {
+    constexpr int QP = DQ / 4;
+    const int t = tid >> 2, part = tid & 3;
+    float qa = 0.0f;
+#pragma unroll
+    for (int u = 0; u < QP / 8; ++u) {
+      const V8 x = *(const V8*)(Qs + t * LQ + part * QP + 8 * u);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) qa += (float)x[e] * nk[part * QP + 8 * u + e];
+    }
+    qa = sum4(qa);
+    if (part == 0) qn[t] = qa;
+  }
+  V8 qa[DQ / 32];
+#pragma unroll
+  for (int kk = 0; kk < DQ / 32; ++kk) qa[kk] = frag<V8, T>(Qs, LQ, 16 * w, 32 * kk, lane);
+  {
+    float rs[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+    for (int ct = 0; ct <= w; ++ct) {
+      V8 kb[DQ / 32];
+#pragma unroll
+      for (int kk = 0; kk < DQ / 32; ++kk) kb[kk] = frag<V8, T>(Ks, LQ, 16 * ct, 32 * kk, lane);
+      f32x4 s4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < DQ / 32; ++kk) s4 = M::mma(qa[kk], kb[kk], s4);
+      const int s = 16 * ct + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int t = 16 * w + 4 * (lane >> 4) + r;
+        const float mv = (s <= t) ? s4[r] * a.scale * expf(sb[t] - sb[s] + si[s] - mts[t]) : 0.0f;
+        rs[r] += mv;
+        Ms[t * LC + s] = (T)mv;
+      }
+    }
+    for (int ct = w + 1; ct < 4; ++ct) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Ms[(16 * w + 4 * (lane >> 4) + r) * LC + 16 * ct + (lane & 15)] = (T)0.0f;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float tot = sum16(rs[r]);
+      if ((lane & 15) == 0) dsum[16 * w + 4 * (lane >> 4) + r] = tot;
+    }
+  }
+  float zi[4], rf[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int t = 16 * w + 4 * (lane >> 4) + r;
+    rf[r] = rowfs[t];
+    const float dn = dsum[t] + rf[r] * qn[t];
+    zi[r] = 1.0f / (fmaxf(fabsf(dn), expf(-mts[t])) + a.eps);
+  }
+  V8 ma[2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) ma[kk] = frag<V8, T>(Ms, LC, 16 * w, 32 * kk, lane);
+#pragma unroll 1
+  for (int c = 0; c < NCB; ++c) {
+    f32x4 hv[TJ];
+#pragma unroll
+    for (int cj = 0; cj < TJ; ++cj) {
+      V8 vb[2], cb2[DQ / 32];
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) vb[kk] = frag_t<V8, T>(Vs, LC, 32 * kk, 16 * cj, lane);
+#pragma unroll
+      for (int kk = 0; kk < DQ / 32; ++kk) cb2[kk] = frag<V8, T>(CT, LQ, 16 * cj, 32 * kk, lane);
+      f32x4 h4 = {0.f, 0.f, 0.f, 0.f}, e4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) h4 = M::mma(ma[kk], vb[kk], h4);
+#pragma unroll
+      for (int kk = 0; kk < DQ / 32; ++kk) e4 = M::mma(qa[kk], cb2[kk], e4);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) hv[cj][r] = (h4[r] + rf[r] * e4[r]) * zi[r];
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int cj = 0; cj < TJ; ++cj) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        Hs[(16 * w + 4 * (lane >> 4) + r) * LC + 16 * cj + (lane & 15)] = (T)hv[cj][r];
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {   // the wave's 16 rows x 128 bytes
+      const int e = lane + 64 * u, t = 16 * w + (e >> 3), cc = (e & 7) * 8;
+      *(u32x4*)(H + (int64_t)t * DV + c * kCB + cc) = *(const u32x4*)(Hs + t * LC + cc);
+    }
+    if (c + 1 < NCB) {
+      __syncthreads();   // every wave has read block c's V / C~
+      store_blk();
+      if (c + 2 < NCB) load_blk(c + 2);
+      __syncthreads();
+    }
+  }
+  if (lane < 16) {
+    const int t = 16 * w + lane;
+    a.mrow[(int64_t)bh * a.T + t0 + t] = mts[t];
+    a.den[(int64_t)bh * a.T + t0 + t] = dsum[t] + rowfs[t] * qn[t];
   }
 }
 
@@ -1106,9 +1266,10 @@ __global__ void __launch_bounds__(512, 1) mlstm_bw_walk(MArgs a) {
   if (tid < DQ) a.dns[(int64_t)bh * DQ + tid] = dn * inv;
 }
 
-// SC_MLSTM_SPLIT=0 (environment, read per launch): the forward as one walk that also computes
-// the outputs (A/B timing, and the bitwise split-vs-walk test); default: the state walk, then
-// every chunk's outputs in parallel
+// The forward is the state walk (mlstm_fw_walk MODE 1), then every chunk's outputs at once
+// (mlstm_fw_out): 155-160 us at C4 against 180-184 us for the single walk that also computes
+// the outputs (tools/mlstm_bench.py, A/B in one process).  SC_MLSTM_SPLIT=0 (environment, read
+// per launch) runs the single walk: bitwise equal (tests/test_gpu_mlstm.py).
 bool fwd_split() {
   const char* e = getenv("SC_MLSTM_SPLIT");
   return !(e && e[0] == '0');
@@ -1121,8 +1282,7 @@ void launch_fwd(const MArgs& a, hipStream_t st) {
   }
   hipLaunchKernelGGL((mlstm_fw_walk<DT, IO, DQ, DV, 1>), dim3(DV / kCB, a.BH), dim3(256), 0, st, a);
   if (a.nc > 0)
-    hipLaunchKernelGGL((mlstm_fw_walk<DT, IO, DQ, DV, 2>), dim3(DV / kCB, a.BH * a.nc), dim3(256), 0,
-                       st, a);
+    hipLaunchKernelGGL((mlstm_fw_out<DT, IO, DQ, DV>), dim3(a.BH * a.nc), dim3(256), 0, st, a);
 }
 template <int DT, int IO, int DQ, int DV>
 void launch_bwd(const MArgs& a, hipStream_t st) {
