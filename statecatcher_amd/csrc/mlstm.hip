@@ -397,7 +397,8 @@ __global__ void __launch_bounds__(256, 2) mlstm_fw_walk(MArgs a) {
       }
       fsv[lane] = G.fs;
     }
-    if (k + 1 < a.nc) prefetch(k + 1);
+    // (MODE 0: the next chunk's loads go out here, beside the whole output phase)
+    if (kOut && k + 1 < a.nc) prefetch(k + 1);
     // the state at the chunk start: its MFMA image, transposed ([j][i]); a lane's four
     // accumulator rows are consecutive i, so each tile is one 8-byte LDS store
 #pragma unroll
@@ -407,6 +408,10 @@ __global__ void __launch_bounds__(256, 2) mlstm_fw_walk(MArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) c[r] = (T)acc[p][r];
       *(v4t*)(CT + (j0 + (lane & 15)) * LQ + i0 + 4 * (lane >> 4)) = c;
+      // the update's decay, applied now: with the next chunk's loads in flight, a packed multiply
+      // beside a register pair one of whose halves is a pending load waits for that load
+      acc[p] = acc[p] * G.decay;
+      asm volatile("" : "+v"(acc[p]));   // (kept here: the scheduler would sink it to its use)
     }
     if (tid < DQ) {
       nk[tid] = n;
@@ -425,6 +430,10 @@ __global__ void __launch_bounds__(256, 2) mlstm_fw_walk(MArgs a) {
         if (!ML_ABL(8)) *(u32x4*)(Cs + j * DQ + c) = *(const u32x4*)(CT + j * LQ + c);
       }
     }
+    // MODE 1: the next chunk's loads go out AFTER this chunk's stores.  vmcnt retires in order, so
+    // a wait the compiler places for a store's source registers (reused by the state update's
+    // fragments) then covers the stores alone, not loads issued a few hundred cycles earlier
+    if (!kOut && k + 1 < a.nc) prefetch(k + 1);
     // From here to the state update every wave touches only its own 16 rows of Ms / qn / dsum
     // (rows 16 w ..): no barrier between the S and H phases.
     if constexpr (kOut) {
@@ -532,7 +541,7 @@ __global__ void __launch_bounds__(256, 2) mlstm_fw_walk(MArgs a) {
 #pragma unroll
     for (int p = 0; p < PW; ++p) {
       const int q = w + 4 * p, i0 = 16 * (q / TJ), j0 = 16 * (q % TJ);
-      f32x4 c = acc[p] * G.decay;
+      f32x4 c = acc[p];
 #pragma unroll
       for (int kk = 0; kk < (ML_ABL(4) ? 0 : kL / 32); ++kk)
         c = M::mma(frag_t<V8, T>(Kf, LQ, 32 * kk, i0, lane),
@@ -619,23 +628,33 @@ __global__ void __launch_bounds__(256, 2) mlstm_fw_out(MArgs a) {
       *(u32x4*)(CT + j * LQ + cc) = pc[u];
     }
   };
-  load_blk(0);
+  // every load of the prologue in flight at once (the small ones first: vmcnt retires in order)
+  const float m = a.ms[(int64_t)bh * (a.nc + 1) + k];
+  const int64_t o = (int64_t)bh * a.T + t0 + lane;
+  const float igv = a.ig[o], fgv = a.fg[o];
+  const float nsv = tid < DQ ? a.ns[((int64_t)bh * (a.nc + 1) + k) * DQ + tid] : 0.0f;
+  u32x4 pq[NQP], pk[NQP];
 #pragma unroll
   for (int u = 0; u < NQP; ++u) {
     const int e = tid + 256 * u, r = e / (DQ / 8), c = (e % (DQ / 8)) * 8;
-    *(V8*)(Qs + r * LQ + c) = cvt8<DT, IO>(*(const u32x4*)(Q + r * a.qt + c));
-    *(V8*)(Ks + r * LQ + c) = cvt8<DT, IO>(*(const u32x4*)(K + r * a.qt + c));
+    pq[u] = *(const u32x4*)(Q + r * a.qt + c);
+    pk[u] = *(const u32x4*)(K + r * a.qt + c);
   }
-  const float m = a.ms[(int64_t)bh * (a.nc + 1) + k];
-  const int64_t o = (int64_t)bh * a.T + t0 + lane;
-  const ChunkGates G = chunk_gate_math(a.ig[o], a.fg[o], m, a.scale, lane);
+  load_blk(0);
+  const ChunkGates G = chunk_gate_math(igv, fgv, m, a.scale, lane);
   if (w == 0) {
     sb[lane] = G.b;
     si[lane] = G.i;
     mts[lane] = G.mt;
     rowfs[lane] = G.rowf;
   }
-  if (tid < DQ) nk[tid] = a.ns[((int64_t)bh * (a.nc + 1) + k) * DQ + tid];
+  if (tid < DQ) nk[tid] = nsv;
+#pragma unroll
+  for (int u = 0; u < NQP; ++u) {
+    const int e = tid + 256 * u, r = e / (DQ / 8), c = (e % (DQ / 8)) * 8;
+    *(V8*)(Qs + r * LQ + c) = cvt8<DT, IO>(pq[u]);
+    *(V8*)(Ks + r * LQ + c) = cvt8<DT, IO>(pk[u]);
+  }
   store_blk();
   if (NCB > 1) load_blk(1);
   __syncthreads();
