@@ -33,7 +33,8 @@
 
 // SC_ML_ABL: timing ablations (tools/mlstm_abl.sh; results are garbage).  Forward walk: 1 no S
 // MFMAs, 2 no H MFMAs, 4 no state-update MFMAs, 8 no global stores, 16 no LDS fill.  Backward
-// walk: 32 no A/dA phase, 64 no dq phase, 128 no dk/dv phase, 256 no dC update, 512 no loads.
+// walk: 32 no A/dA phase, 64 no dq phase, 128 no dk/dv phase, 256 no dC update, 512 no loads,
+// 1024 no dq role (its workgroups exit), 2048 no walk role.
 #ifndef SC_ML_ABL
 #define SC_ML_ABL 0
 #endif
@@ -1001,6 +1002,8 @@ __global__ void __launch_bounds__(512, 1) mlstm_bw_walk(MArgs a) {
     }
   };
 
+  if (ML_ABL(1024) && !walk) return;
+  if (ML_ABL(2048) && walk) return;
   if (!walk) {
     // ================= dq role: every chunk of sequence bh, independently =================
     TI* dQg = (TI*)a.dq + qrow(a, bh, 0);
