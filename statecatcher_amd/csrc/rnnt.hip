@@ -596,20 +596,36 @@ __device__ __forceinline__ void load_w(const JointArgs& a, unsigned char* lds) {
   for (int i = threadIdx.x; i < V; i += blockDim.x) bias[i] = a.bias[i];
 }
 
-// z of (b, t, u) at j = 16 s + 8 h + e (the B operand of the node-on-lane logits MFMA), bf16
-__device__ __forceinline__ void z_frags(const JointArgs& a, int b, int t, int u, bool ok, int h,
-                                        jbf8 (&zb)[4]) {
-  const float* ep = a.enc + ((int64_t)b * a.r.T + t) * kJ;
-  const float* pp = a.pred + ((int64_t)b * a.r.U1 + u) * kJ;
+// z of (b, t, u) at j = 16 s + 8 h + e (the B operand of the node-on-lane logits MFMA), bf16, for
+// the task's two columns u0, u0 + 1 (nc of them valid).  Every load is issued before the first
+// tanh: one exposed memory latency per task (per-s loads and uses had the compiler wait vmcnt(0)
+// eight times).
+__device__ __forceinline__ void z_frags2(const JointArgs& a, int b, int t, int u0, int nc, bool ok,
+                                         int h, jbf8 (&zb)[2][4]) {
+  const float* ep = a.enc + ((int64_t)b * a.r.T + t) * kJ + 8 * h;
+  const float* pp0 = a.pred + ((int64_t)b * a.r.U1 + u0) * kJ + 8 * h;
+  const float* pp1 = nc > 1 ? pp0 + kJ : pp0;
+  float4 e[8], p0[8], p1[8];
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
-    const int j0 = 16 * s + 8 * h;
-    const float4 e0 = *(const float4*)(ep + j0), e1 = *(const float4*)(ep + j0 + 4);
-    const float4 p0 = *(const float4*)(pp + j0), p1 = *(const float4*)(pp + j0 + 4);
-    const float x[8] = {e0.x + p0.x, e0.y + p0.y, e0.z + p0.z, e0.w + p0.w,
-                        e1.x + p1.x, e1.y + p1.y, e1.z + p1.z, e1.w + p1.w};
+    e[2 * s] = *(const float4*)(ep + 16 * s);
+    e[2 * s + 1] = *(const float4*)(ep + 16 * s + 4);
+    p0[2 * s] = *(const float4*)(pp0 + 16 * s);
+    p0[2 * s + 1] = *(const float4*)(pp0 + 16 * s + 4);
+    p1[2 * s] = *(const float4*)(pp1 + 16 * s);
+    p1[2 * s + 1] = *(const float4*)(pp1 + 16 * s + 4);
+  }
 #pragma unroll
-    for (int e = 0; e < 8; ++e) zb[s][e] = (__bf16)(ok ? tanh_(x[e]) : 0.0f);
+  for (int c = 0; c < 2; ++c) {
+    const float4* p = c ? p1 : p0;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const float4 e0 = e[2 * s], e1 = e[2 * s + 1], q0 = p[2 * s], q1 = p[2 * s + 1];
+      const float x[8] = {e0.x + q0.x, e0.y + q0.y, e0.z + q0.z, e0.w + q0.w,
+                          e1.x + q1.x, e1.y + q1.y, e1.z + q1.z, e1.w + q1.w};
+#pragma unroll
+      for (int k = 0; k < 8; ++k) zb[c][s][k] = (__bf16)(ok ? tanh_(x[k]) : 0.0f);
+    }
   }
 }
 
@@ -663,7 +679,8 @@ __global__ void __launch_bounds__(512) joint_fwd_kernel(JointArgs a) {
   const int lane = threadIdx.x & 63, h = lane >> 5;
   const int nup = (r.U1 + 1) / 2;
   const int64_t ntask = (int64_t)r.B * a.ntb * nup;
-  const int64_t wid = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 6), nwv = (int64_t)gridDim.x * 8;
+  // (wave-uniform in an SGPR: the per-task lengths and labels become scalar loads)
+  const int64_t wid = (int64_t)blockIdx.x * 8 + uniform(threadIdx.x >> 6), nwv = (int64_t)gridDim.x * 8;
   for (int64_t task = wid; task < ntask; task += nwv) {
     const int b = (int)(task / ((int64_t)a.ntb * nup));
     const int tb = (int)((task / nup) % a.ntb), up = (int)(task % nup);
@@ -675,9 +692,13 @@ __global__ void __launch_bounds__(512) joint_fwd_kernel(JointArgs a) {
     const int nc = (2 * up + 1 <= Ub) ? 2 : 1;
     jbf8 zb[2][4];
     float m[2], s[2];
+    // the two columns' labels, loaded beside z (used after the vocab loop)
+    int ylab[2];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) ylab[c] = 2 * up + c < Ub ? label_at(r, b, 2 * up + c) : r.blank;
+    z_frags2(a, b, tc, 2 * up, nc, tok, h, zb);
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
-      if (c < nc) z_frags(a, b, tc, 2 * up + c, tok, h, zb[c]);
       m[c] = -__builtin_huge_valf();
       s[c] = 0.0f;
     }
@@ -705,7 +726,7 @@ __global__ void __launch_bounds__(512) joint_fwd_kernel(JointArgs a) {
       const float M = fmaxf(m[c], mo);
       const float lse = M + flog(s[c] * exp2_((m[c] - M) * kLog2e) + so * exp2_((mo - M) * kLog2e));
       // blank and label logits: dot products over the lane's 32 j, halves combined
-      const int yl = u < Ub ? label_at(r, b, u) : r.blank;
+      const int yl = ylab[c];
       float lb = 0.0f, ly = 0.0f;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {

@@ -19,18 +19,23 @@ NAMES = {"lucy_scan_fwd_kernel": "lucy_scan_fwd", "lucy_scan_bwd_kernel": "lucy_
          "decay_scan_fwd_kernel": "decay_scan_fwd", "decay_scan_bwd_kernel": "decay_scan_bwd",
          # the mLSTM walks read q / k / v / h / dh and the state image as 16-byte-per-lane rows
          # (the same FETCH_SIZE calibration)
-         "mlstm_fw_walk": "mlstm_fwd", "mlstm_bw_walk": "mlstm_bwd"}
+         # a forward is the state walk plus the chunk-parallel output kernel: their per-dispatch
+         # averages add up to one launch of sc_mlstm_fwd
+         "mlstm_fw_walk": "mlstm_fwd", "mlstm_fw_out": "mlstm_fwd", "mlstm_bw_walk": "mlstm_bwd"}
 
 
 def per_kernel(path, counter):
-    acc = defaultdict(list)
+    """{name: (bytes per launch = sum over the name's kernels of their per-dispatch means,
+    dispatches of its first kernel)}"""
+    acc = defaultdict(lambda: defaultdict(list))
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] != counter:
             continue
         for frag, name in NAMES.items():
             if frag in r["Kernel_Name"]:
-                acc[name].append(float(r["Counter_Value"]) * 1024.0)
-    return acc
+                acc[name][frag].append(float(r["Counter_Value"]) * 1024.0)
+    return {name: (sum(sum(v) / len(v) for v in frags.values()), len(next(iter(frags.values()))))
+            for name, frags in acc.items()}
 
 
 def main():
@@ -38,10 +43,10 @@ def main():
     write = per_kernel(sys.argv[2], "WRITE_SIZE")
     out = {}
     for name in sorted(set(fetch) & set(write)):
-        f = 2.0 * sum(fetch[name]) / len(fetch[name])
-        w = sum(write[name]) / len(write[name])
+        f = 2.0 * fetch[name][0]
+        w = write[name][0]
         out[name] = {"hbm_bytes_per_launch": round(f + w), "fetch_bytes": round(f),
-                     "write_bytes": round(w), "dispatches": len(fetch[name])}
+                     "write_bytes": round(w), "dispatches": fetch[name][1]}
     if len(sys.argv) > 3:
         # merge into an existing table (passes over different workloads fill different kernels)
         try:

@@ -1,7 +1,12 @@
 set -e -o pipefail
-mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_mlstm.py -m gpu > gpurun_out/j4_test.log 2>&1
-: > gpurun_out/m4_bench.log
-for s in 1 0 1; do echo "== split $s" >> gpurun_out/m4_bench.log; SC_MLSTM_SPLIT=$s timeout -k 10 120 python3 -u tools/mlstm_bench.py --reps 10 >> gpurun_out/m4_bench.log 2>&1; done
-timeout -k 10 400 python3 -u bench.py --workload xlstm --steps 8 --warmup 4 > gpurun_out/b4_xlstm.json 2> gpurun_out/b4_xlstm.err
-echo done
+R=$GRAFT_REPO_ROOT
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_rnnt_joint.py -m gpu > gpurun_out/j7_test.log 2>&1
+bash tools/run_ab.sh j7_probe "python3 -u tools/joint_probe.py 32 3" fprio
+bash tools/round_run.sh r3c
+O=$R/gpurun_out/mpmc_r3c; mkdir -p $O
+cd /tmp && export TMPDIR=/tmp
+timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex mlstm_ -f csv -d $O/f -o run -- python3 $R/bench.py --workload xlstm --steps 2 --warmup 1 --cpu-baseline off > $O/f.log 2>&1
+timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex mlstm_ -f csv -d $O/w -o run -- python3 $R/bench.py --workload xlstm --steps 2 --warmup 1 --cpu-baseline off > $O/w.log 2>&1
+find $O -type f ! -name "*counter_collection.csv" -delete
+cd $R && bash tools/prof_workloads.sh
+echo alldone
