@@ -1,12 +1,3 @@
 set -e -o pipefail
-R=$GRAFT_REPO_ROOT
-timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_rnnt_joint.py -m gpu > gpurun_out/j7_test.log 2>&1
-bash tools/run_ab.sh j7_probe "python3 -u tools/joint_probe.py 32 3" fprio
-bash tools/round_run.sh r3c
-O=$R/gpurun_out/mpmc_r3c; mkdir -p $O
-cd /tmp && export TMPDIR=/tmp
-timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex mlstm_ -f csv -d $O/f -o run -- python3 $R/bench.py --workload xlstm --steps 2 --warmup 1 --cpu-baseline off > $O/f.log 2>&1
-timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex mlstm_ -f csv -d $O/w -o run -- python3 $R/bench.py --workload xlstm --steps 2 --warmup 1 --cpu-baseline off > $O/w.log 2>&1
-find $O -type f ! -name "*counter_collection.csv" -delete
-cd $R && bash tools/prof_workloads.sh
-echo alldone
+bash tools/run_ab.sh j10 "python3 -u tools/joint_probe.py 32 3" sb0 il ilsb0
+echo done
