@@ -22,8 +22,12 @@ timeout -k 10 500 rocprofv3 --pmc FETCH_SIZE -f csv --kernel-include-regex "scan
 echo "pmc write"
 timeout -k 10 500 rocprofv3 --pmc WRITE_SIZE -f csv --kernel-include-regex "scan" -d "$O/pmc_write_$TAG" -o run -- \
   python3 "$R/bench.py" --steps 2 --warmup 1 --cpu-baseline off > "$O/pmc_write_$TAG.log" 2>&1
+# the timed steps' dispatches of the hot kernels (bench --steps 5 --warmup 2, events in the last 2)
+python3 "$R/tools/trace_tail.py" "$O/prof_$TAG/run_kernel_trace.csv" 7 2 "lucy_scan|joint_|mlstm_" \
+  "$O/prof_$TAG/hot_dispatches.csv" > "$O/prof_$TAG/trace_tail.md" || echo "trace_tail failed"
 # keep only the summaries (gpurun copies back at most 64 MiB)
 find "$O/prof_$TAG" "$O/pmc_fetch_$TAG" "$O/pmc_write_$TAG" -type f \
-  ! -name "*kernel_stats.csv" ! -name "*counter_collection.csv" -delete
+  ! -name "*kernel_stats.csv" ! -name "*counter_collection.csv" ! -name "hot_dispatches.csv" \
+  ! -name "trace_tail.md" -delete
 du -sh "$O"
 echo done
