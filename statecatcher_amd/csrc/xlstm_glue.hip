@@ -46,6 +46,19 @@ __device__ __forceinline__ void ld4_h16(const u16* p, float (&v)[4]) {
 #pragma unroll
   for (int k = 0; k < 4; ++k) v[k] = rbf((float)q[k]);
 }
+// the same conversions from an 8-byte piece already in registers (loads issued a row ahead)
+__device__ __forceinline__ void cvt4(uint2 q, float (&v)[4]) {
+  v[0] = __uint_as_float(q.x << 16);
+  v[1] = __uint_as_float(q.x & 0xffff0000u);
+  v[2] = __uint_as_float(q.y << 16);
+  v[3] = __uint_as_float(q.y & 0xffff0000u);
+}
+__device__ __forceinline__ void cvt4_h16(uint2 q, float (&v)[4]) {
+  typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+  const h4 x = __builtin_bit_cast(h4, q);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) v[k] = rbf((float)x[k]);
+}
 __device__ __forceinline__ void st4(u16* p, const float (&v)[4]) {
   uint2 q;
   q.x = (uint32_t)tobf(v[0]) | ((uint32_t)tobf(v[1]) << 16);
@@ -123,15 +136,38 @@ __global__ void __launch_bounds__(256) rms_bwd_kernel(const u16* x, const u16* d
     const float4 q = *(const float4*)(w + (c * 64 + lane) * 4);
     wr[c][0] = q.x; wr[c][1] = q.y; wr[c][2] = q.z; wr[c][3] = q.w;
   }
-  for (int64_t row = (int64_t)blockIdx.x * 4 + wv; row < rows; row += (int64_t)gridDim.x * 4) {
-    const float rs = rstd[row];
+  // grid-stride rows with the next row's inputs loaded while this one computes (each wave
+  // walks ~rows / 2048 rows; a load-then-use loop paid a memory latency per row)
+  const int64_t rstep = (int64_t)gridDim.x * 4;
+  uint2 px[CH], pd[CH], pr[CH];
+  float prs = 0.0f;
+  auto load_row = [&](int64_t row) __attribute__((always_inline)) {
+    prs = rstd[row];
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      px[c] = *(const uint2*)(x + row * D + (c * 64 + lane) * 4);
+      pd[c] = *(const uint2*)(dy + row * D + (c * 64 + lane) * 4);
+      if constexpr (ADD) pr[c] = *(const uint2*)(dres + row * D + (c * 64 + lane) * 4);
+    }
+  };
+  if ((int64_t)blockIdx.x * 4 + wv < rows) load_row((int64_t)blockIdx.x * 4 + wv);
+  for (int64_t row = (int64_t)blockIdx.x * 4 + wv; row < rows; row += rstep) {
+    const float rs = prs;
+    uint2 cx[CH], cd[CH], cr[CH];
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      cx[c] = px[c];
+      cd[c] = pd[c];
+      cr[c] = pr[c];
+    }
+    if (row + rstep < rows) load_row(row + rstep);
     float xv[CH][4], gv[CH][4];
     float dot = 0.0f;
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
       float dv[4];
-      ld4(x + row * D + (c * 64 + lane) * 4, xv[c]);
-      ld4(dy + row * D + (c * 64 + lane) * 4, dv);
+      cvt4(cx[c], xv[c]);
+      cvt4(cd[c], dv);
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const float xh = xv[c][k] * rs;
@@ -149,7 +185,7 @@ __global__ void __launch_bounds__(256) rms_bwd_kernel(const u16* x, const u16* d
       for (int k = 0; k < 4; ++k) o[k] = rs * (gv[c][k] - xv[c][k] * dot);
       if constexpr (ADD) {
         float rv[4];
-        ld4(dres + row * D + (c * 64 + lane) * 4, rv);
+        cvt4(cr[c], rv);
 #pragma unroll
         for (int k = 0; k < 4; ++k) o[k] = rbf(o[k]) + rv[k];
       }
@@ -243,21 +279,48 @@ __global__ void __launch_bounds__(256) mhln_bwd_kernel(MhArgs a) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) dwp[c][k] = 0.0f;
   const bool hok = n < a.NH;
-  for (int64_t m = (int64_t)blockIdx.x * 4 + wv; m < M; m += (int64_t)gridDim.x * 4) {
+  // grid-stride rows with the next row's h / o / dy / statistics loaded while this one computes
+  // (a load-then-use loop paid one memory latency per row: 122 us at C4 for 375 MB)
+  const int64_t mstep = (int64_t)gridDim.x * 4;
+  uint2 ph[CH], po[CH], pd[CH];
+  float pmu = 0.0f, prs = 0.0f;
+  auto load_row = [&](int64_t m) __attribute__((always_inline)) {
+    const int b = (int)(m / a.T), t = (int)(m % a.T);
+    const int64_t hrow = (((int64_t)b * a.NH + n) * a.T + t) * DH;
+    pmu = a.mean[m * a.NH + n];
+    prs = a.rstd[m * a.NH + n];
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int col = n * DH + (c * 16 + sub) * 4;
+      ph[c] = *(const uint2*)(a.h + hrow + (c * 16 + sub) * 4);
+      po[c] = *(const uint2*)(a.o + m * a.ldo + col);
+      pd[c] = *(const uint2*)(a.dy + m * a.ldy + col);
+    }
+  };
+  if (hok && (int64_t)blockIdx.x * 4 + wv < M) load_row((int64_t)blockIdx.x * 4 + wv);
+  for (int64_t m = (int64_t)blockIdx.x * 4 + wv; m < M; m += mstep) {
     if (!hok) continue;
     const int b = (int)(m / a.T), t = (int)(m % a.T);
     const int64_t hrow = (((int64_t)b * a.NH + n) * a.T + t) * DH;
-    const float mu = a.mean[m * a.NH + n], rs = a.rstd[m * a.NH + n];
+    const float mu = pmu, rs = prs;
+    uint2 ch[CH], co[CH], cd[CH];
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      ch[c] = ph[c];
+      co[c] = po[c];
+      cd[c] = pd[c];
+    }
+    if (m + mstep < M) load_row(m + mstep);
     float xh[CH][4], g[CH][4];
     float s1 = 0.0f, s2 = 0.0f;
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
       const int col = n * DH + (c * 16 + sub) * 4;
       float hv[4], ov[4], dv[4], dov[4];
-      if (a.h16) ld4_h16(a.h + hrow + (c * 16 + sub) * 4, hv);
-      else ld4(a.h + hrow + (c * 16 + sub) * 4, hv);
-      ld4(a.o + m * a.ldo + col, ov);
-      ld4(a.dy + m * a.ldy + col, dv);
+      if (a.h16) cvt4_h16(ch[c], hv);
+      else cvt4(ch[c], hv);
+      cvt4(co[c], ov);
+      cvt4(cd[c], dv);
       const float4 wq = *(const float4*)(a.w + col);
       const float wk[4] = {wq.x, wq.y, wq.z, wq.w};
 #pragma unroll
