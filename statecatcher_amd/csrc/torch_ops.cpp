@@ -16,6 +16,9 @@
 //   ctc_greedy_decode  decoder.py:3-30
 //   mlstm_fwd/_bwd  the xLSTM encoder's mLSTM cell (fork mlstm_kernels)  model.py:214-229
 //   rnnt_joint_fwd/_bwd  RNNTPredictorJoiner + log_softmax + warp_rnnt   model.py:73-145, train.py:38-42
+//   gemm_tn         LinearSafe forward / input gradient GEMMs (bf16)  lucyrnn_triton.py:20-25, :107-109
+//   gemm_wgrad      LinearSafe / output_proj weight gradient           lucyrnn_triton.py:20-25, :107-109
+//   clip_adam_      clip_grad_norm_(params, max_norm) + optim.Adam/AdamW.step()  train.py:543-552
 // There is no CPU kernel: calling an op on CPU tensors raises (no silent fallback).
 
 #include <ATen/ATen.h>
@@ -24,6 +27,7 @@
 #include <torch/library.h>
 
 #include <tuple>
+#include <vector>
 
 #include "statecatcher.h"
 
@@ -630,7 +634,119 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> rnnt_joint_bwd_meta(
           at::empty(bias.sizes(), fo)};
 }
 
+// ------------------------------------------------------------------- projection GEMMs ------
+// C [M,N] bf16 = a [M,K] b [N,K]^T on the persistent MFMA kernel (sc_gemm_tn_bf16)
+Tensor gemm_tn_hip(const Tensor& a_in, const Tensor& b_in, int64_t tile_m) {
+  c10::DeviceGuard guard(a_in.device());
+  TORCH_CHECK(a_in.dim() == 2 && b_in.dim() == 2 && a_in.size(1) == b_in.size(1) &&
+                  a_in.scalar_type() == at::kBFloat16 && b_in.scalar_type() == at::kBFloat16,
+              "statecatcher::gemm_tn: a [M,K], b [N,K] bfloat16");
+  Tensor a = a_in.contiguous(), b = b_in.contiguous();
+  const int64_t M = a.size(0), N = b.size(0), K = a.size(1);
+  Tensor c = at::empty({M, N}, a.options());
+  if (M == 0 || N == 0) return c;
+  sc_check(sc_gemm_tn_bf16(a.data_ptr(), K, b.data_ptr(), K, c.data_ptr(), N, (int)M, (int)N,
+                           (int)K, (int)tile_m, stream_for(a)),
+           "statecatcher::gemm_tn");
+  return c;
+}
+
+Tensor gemm_tn_meta(const Tensor& a, const Tensor& b, int64_t tile_m) {
+  TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && a.size(1) == b.size(1), "statecatcher::gemm_tn: shapes");
+  return at::empty({a.size(0), b.size(0)}, a.options());
+}
+
+// dW [N,K] fp32 = dy [M,N]^T x [M,K] (bf16 operands): the split-L MFMA kernel
+// (sc_gemm_wgrad_bf16) and the fixed-order slab sum (sc_colsum); block_d = D > 0: dy's columns
+// are in step-blocked gate order and dW comes back in the reference's row order
+Tensor gemm_wgrad_hip(const Tensor& dy_in, const Tensor& x_in, int64_t block_d) {
+  c10::DeviceGuard guard(dy_in.device());
+  TORCH_CHECK(dy_in.dim() == 2 && x_in.dim() == 2 && dy_in.size(0) == x_in.size(0) &&
+                  dy_in.scalar_type() == at::kBFloat16 && x_in.scalar_type() == at::kBFloat16,
+              "statecatcher::gemm_wgrad: dy [M,N], x [M,K] bfloat16");
+  Tensor dy = dy_in.contiguous(), x = x_in.contiguous();
+  const int64_t M = dy.size(0), N = dy.size(1), K = x.size(1);
+  TORCH_CHECK(block_d == 0 || (N == 7 * block_d && block_d % 64 == 0),
+              "statecatcher::gemm_wgrad: block_d must be 0 or N / 7 (a multiple of 64)");
+  const int S = sc_gemm_wgrad_splits((int)M, (int)N, (int)K);
+  TORCH_CHECK(S > 0, "statecatcher::gemm_wgrad: shape [", M, ",", N, "] x [", M, ",", K,
+              "] outside the MFMA kernel's tiling (sc_gemm_wgrad_splits == 0)");
+  Tensor part = at::empty({S, N, K}, dy.options().dtype(at::kFloat));
+  void* st = stream_for(dy);
+  sc_check(sc_gemm_wgrad_bf16(dy.data_ptr(), N, x.data_ptr(), K, part.data_ptr<float>(), (int)M,
+                              (int)N, (int)K, S, st),
+           "statecatcher::gemm_wgrad");
+  Tensor dw = at::empty({N, K}, part.options());
+  const size_t wsb = sc_colsum_workspace_bytes(S, N * K);
+  Tensor ws = at::empty({(int64_t)wsb}, dy.options().dtype(at::kByte));
+  sc_check(sc_colsum(part.data_ptr(), SC_F32, S, N * K, N * K, block_d ? block_d / 64 : 1,
+                     block_d ? 7 : 1, dw.data_ptr<float>(), ws.data_ptr(), wsb, st),
+           "statecatcher::gemm_wgrad (slab sum)");
+  return dw;
+}
+
+Tensor gemm_wgrad_meta(const Tensor& dy, const Tensor& x, int64_t block_d) {
+  TORCH_CHECK(dy.dim() == 2 && x.dim() == 2 && dy.size(0) == x.size(0), "statecatcher::gemm_wgrad: shapes");
+  return at::empty({dy.size(1), x.size(1)}, dy.options().dtype(at::kFloat));
+}
+
+// --------------------------------------------------------------------- optimizer step ------
+// clip_grad_norm_(clipped tensors, max_norm) then Adam / AdamW on every tensor, in place on
+// params / exp_avgs / exp_avg_sqs (torch's own optimizer state); grads are read only.  The first
+// n_clip tensors form the clip set (the reference clips model.parameters() only).  Returns the
+// total norm clip_grad_norm_ reports (0-dim fp32; 0 when max_norm <= 0: no clipping).
+Tensor clip_adam_hip(at::TensorList params, at::TensorList grads, at::TensorList exp_avgs,
+                     at::TensorList exp_avg_sqs, int64_t n_clip, double max_norm, double lr,
+                     double beta1, double beta2, double eps, double weight_decay, bool decoupled,
+                     double step_size, double bc2_sqrt) {
+  const size_t nt = params.size();
+  TORCH_CHECK(nt > 0 && grads.size() == nt && exp_avgs.size() == nt && exp_avg_sqs.size() == nt,
+              "statecatcher::clip_adam_: equal-length tensor lists");
+  TORCH_CHECK(n_clip >= 0 && n_clip <= (int64_t)nt, "statecatcher::clip_adam_: n_clip");
+  c10::DeviceGuard guard(params[0].device());
+  std::vector<sc_adam_tensor> t(nt);
+  for (size_t i = 0; i < nt; ++i) {
+    for (const Tensor* x : {&params[i], &grads[i], &exp_avgs[i], &exp_avg_sqs[i]})
+      TORCH_CHECK(x->is_cuda() && x->scalar_type() == at::kFloat && x->is_contiguous() &&
+                      x->numel() == params[i].numel(),
+                  "statecatcher::clip_adam_: fp32 contiguous device tensors of equal size");
+    t[i] = sc_adam_tensor{params[i].data_ptr<float>(), grads[i].data_ptr<float>(),
+                          exp_avgs[i].data_ptr<float>(), exp_avg_sqs[i].data_ptr<float>(),
+                          params[i].numel()};
+  }
+  void* st = stream_for(params[0]);
+  Tensor norm = at::zeros({}, params[0].options());
+  Tensor part;
+  int64_t np = 0;
+  if (max_norm > 0.0 && n_clip > 0) {
+    np = sc_adam_parts(t.data(), (int)n_clip);
+    part = at::empty({np}, params[0].options());
+    sc_check(sc_adam_sumsq(t.data(), (int)n_clip, part.data_ptr<float>(), st),
+             "statecatcher::clip_adam_ (sum of squares)");
+  }
+  // the clipped tensors with the clip coefficient, then the rest unclipped
+  sc_check(sc_adam_step(t.data(), (int)n_clip, np ? part.data_ptr<float>() : nullptr, np,
+                        max_norm, lr, beta1, beta2, eps, weight_decay, decoupled ? 1 : 0,
+                        step_size, bc2_sqrt, np ? norm.data_ptr<float>() : nullptr, st),
+           "statecatcher::clip_adam_");
+  if ((int64_t)nt > n_clip)
+    sc_check(sc_adam_step(t.data() + n_clip, (int)(nt - n_clip), nullptr, 0, max_norm, lr, beta1,
+                          beta2, eps, weight_decay, decoupled ? 1 : 0, step_size, bc2_sqrt,
+                          nullptr, st),
+             "statecatcher::clip_adam_ (unclipped)");
+  return norm;
+}
+
+Tensor clip_adam_meta(at::TensorList params, at::TensorList grads, at::TensorList exp_avgs,
+                      at::TensorList exp_avg_sqs, int64_t n_clip, double max_norm, double lr,
+                      double beta1, double beta2, double eps, double weight_decay, bool decoupled,
+                      double step_size, double bc2_sqrt) {
+  TORCH_CHECK(!params.empty(), "statecatcher::clip_adam_: empty parameter list");
+  return at::empty({}, params[0].options());
+}
+
 }  // namespace
+
 
 TORCH_LIBRARY(statecatcher, m) {
   m.def("abi_version() -> int", []() -> int64_t { return sc_abi_version(); });
@@ -663,6 +779,11 @@ TORCH_LIBRARY(statecatcher, m) {
   m.def("mlstm_gate_bwd(Tensor qdq, Tensor kdk, Tensor fgate) -> Tensor");
   m.def("rnnt_joint_fwd(Tensor enc_p, Tensor pred_p, Tensor W, Tensor bias, Tensor labels, "
         "Tensor frames_lengths, Tensor labels_lengths, int blank=0) -> (Tensor nll, Tensor workspace)");
+  m.def("gemm_tn(Tensor a, Tensor b, int tile_m=0) -> Tensor");
+  m.def("gemm_wgrad(Tensor dy, Tensor x, int block_d=0) -> Tensor");
+  m.def("clip_adam_(Tensor(a!)[] params, Tensor[] grads, Tensor(b!)[] exp_avgs, "
+        "Tensor(c!)[] exp_avg_sqs, int n_clip, float max_norm, float lr, float beta1, float beta2, "
+        "float eps, float weight_decay, bool decoupled, float step_size, float bc2_sqrt) -> Tensor");
   m.def("rnnt_joint_bwd(Tensor enc_p, Tensor pred_p, Tensor W, Tensor bias, Tensor labels, "
         "Tensor frames_lengths, Tensor labels_lengths, Tensor workspace, Tensor scale, int blank=0)"
         " -> (Tensor d_enc, Tensor d_pred, Tensor dW, Tensor dbias)");
@@ -684,6 +805,9 @@ TORCH_LIBRARY_IMPL(statecatcher, CUDA, m) {
   m.impl("mlstm_gate_bwd", &mlstm_gate_bwd_hip);
   m.impl("rnnt_joint_fwd", &rnnt_joint_fwd_hip);
   m.impl("rnnt_joint_bwd", &rnnt_joint_bwd_hip);
+  m.impl("gemm_tn", &gemm_tn_hip);
+  m.impl("gemm_wgrad", &gemm_wgrad_hip);
+  m.impl("clip_adam_", &clip_adam_hip);
 }
 
 TORCH_LIBRARY_IMPL(statecatcher, Meta, m) {
@@ -702,4 +826,7 @@ TORCH_LIBRARY_IMPL(statecatcher, Meta, m) {
   m.impl("mlstm_gate_bwd", &mlstm_gate_bwd_meta);
   m.impl("rnnt_joint_fwd", &rnnt_joint_fwd_meta);
   m.impl("rnnt_joint_bwd", &rnnt_joint_bwd_meta);
+  m.impl("gemm_tn", &gemm_tn_meta);
+  m.impl("gemm_wgrad", &gemm_wgrad_meta);
+  m.impl("clip_adam_", &clip_adam_meta);
 }

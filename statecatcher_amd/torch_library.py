@@ -17,6 +17,9 @@ Reference interfaces (what a ``train.py`` user swaps in):
   ctc_greedy_decode <- decoder.py:3-30
   mlstm       <- the xLSTM encoder's mLSTM cell (fork mlstm_kernels)  model.py:214-229
   rnnt_joint_nll <- RNNTPredictorJoiner + log_softmax + warp_rnnt      model.py:73-145
+  gemm_tn     <- LinearSafe's forward / input-gradient GEMM (bf16)    lucyrnn_triton.py:20-25
+  gemm_wgrad  <- LinearSafe / output_proj weight gradient             lucyrnn_triton.py:20-25, :107-109
+  clip_adam_  <- clip_grad_norm_(params, 50) + optim.Adam/AdamW.step() train.py:543-552
 """
 import os
 
@@ -25,7 +28,8 @@ import torch
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_torch_ops.so")
 OPS = ("abi_version", "lucy_scan_fwd", "lucy_scan_bwd", "decay_scan_fwd", "decay_scan_bwd",
        "layer_norm_fwd", "layer_norm_bwd", "ctc_fwd", "ctc_bwd", "ctc_mean", "ctc_greedy_decode",
-       "mlstm_fwd", "mlstm_bwd", "mlstm_gate_bwd", "rnnt_joint_fwd", "rnnt_joint_bwd")
+       "mlstm_fwd", "mlstm_bwd", "mlstm_gate_bwd", "rnnt_joint_fwd", "rnnt_joint_bwd",
+       "gemm_tn", "gemm_wgrad", "clip_adam_")
 
 _LOADED = False
 
@@ -228,3 +232,32 @@ def rnnt_joint_nll(enc_p, pred_p, W, bias, labels, frames_lengths, labels_length
     warp_rnnt's gathered lattice) without materialising the (B, T, U+1, V) logits."""
     return load().rnnt_joint_fwd(enc_p, pred_p, W, bias, labels, frames_lengths, labels_lengths,
                                  blank)[0]
+
+
+def gemm_tn(a, b, tile_m=0):
+    """C [M,N] bf16 = a [M,K] b [N,K]^T on the persistent MFMA kernel (K % 64 == 0, N % 256 == 0;
+    include/statecatcher.h sc_gemm_tn_bf16).  Not differentiable: a building block of the
+    projection nodes' forward and input gradient."""
+    return load().gemm_tn(a, b, tile_m)
+
+
+def gemm_wgrad(dy, x, block_d=0):
+    """dW [N,K] fp32 = dy [M,N]^T x [M,K] (bf16 operands) on the split-L MFMA kernel plus the
+    fixed-order slab sum; block_d = D: dy's columns in step-blocked gate order, dW returned in
+    the reference's row order.  Raises outside the kernel's tiling (sc_gemm_wgrad_splits)."""
+    return load().gemm_wgrad(dy, x, block_d)
+
+
+def clip_adam_(params, grads, exp_avgs, exp_avg_sqs, n_clip, max_norm, lr, betas, eps,
+               weight_decay, decoupled, step):
+    """clip_grad_norm_(params[:n_clip], max_norm) then one Adam (decoupled=False) / AdamW step
+    at step count `step` on every tensor, in place (params, exp_avgs, exp_avg_sqs; grads read
+    only), as optim.clip_and_adam_step does for an optimizer.  Returns clip_grad_norm_'s total
+    norm (0-dim fp32 tensor; 0 without clipping)."""
+    import math
+    beta1, beta2 = betas
+    bc1, bc2 = 1.0 - beta1 ** step, 1.0 - beta2 ** step
+    return load().clip_adam_(list(params), list(grads), list(exp_avgs), list(exp_avg_sqs),
+                             int(n_clip), float(max_norm), float(lr), float(beta1), float(beta2),
+                             float(eps), float(weight_decay), bool(decoupled), lr / bc1,
+                             math.sqrt(bc2))

@@ -235,3 +235,35 @@ def test_rnnt_joint_op_bitwise_vs_ctypes_path():
         outs.append([nll] + [t.grad for t in leaves])
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+def test_gemm_and_adam_ops_bitwise_vs_ctypes_path():
+    """torch.ops.statecatcher.gemm_tn / gemm_wgrad / clip_adam_ run the same kernels as the
+    ctypes nodes (ops.gemm_tn, ops.wgrad_mfma, optim.clip_and_adam_step): bitwise equal."""
+    from statecatcher_amd import ops, optim
+    tl = _tl()
+    g = torch.Generator(device=DEV).manual_seed(3)
+    M, K, N = 8192, 512, 3584
+    a = torch.randn(M, K, device=DEV, generator=g).to(torch.bfloat16)
+    w = torch.randn(N, K, device=DEV, generator=g).to(torch.bfloat16)
+    assert torch.equal(tl.gemm_tn(a, w), ops.gemm_tn(a, w))
+    dy = torch.randn(M, N, device=DEV, generator=g).to(torch.bfloat16)
+    for bd in (0, 512):
+        assert torch.equal(tl.gemm_wgrad(dy, a, bd), ops.wgrad_mfma(dy, a, bd))
+    # one clipped Adam step on two parameters against the optimizer path
+    ps = [torch.randn(1000, device=DEV, generator=g), torch.randn(37, 5, device=DEV, generator=g)]
+    gs = [torch.randn_like(p) * 40 for p in ps]
+    q = [p.clone().requires_grad_(True) for p in ps]
+    for x, gr in zip(q, gs):
+        x.grad = gr.clone()
+    opt = torch.optim.Adam(q, lr=1e-3)
+    norm_ref = optim.clip_and_adam_step(opt, q, 50.0)
+    m = [torch.zeros_like(p) for p in ps]
+    v = [torch.zeros_like(p) for p in ps]
+    pc = [p.clone() for p in ps]
+    norm = tl.clip_adam_(pc, gs, m, v, 2, 50.0, 1e-3, (0.9, 0.999), 1e-8, 0.0, False, 1.0)
+    torch.cuda.synchronize()
+    assert torch.equal(norm.reshape(()), norm_ref.reshape(()))
+    for x, y, mm, vv in zip(pc, q, m, v):
+        assert torch.equal(x, y.detach())
+        assert torch.equal(mm, opt.state[y]["exp_avg"]) and torch.equal(vv, opt.state[y]["exp_avg_sq"])

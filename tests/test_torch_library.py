@@ -153,3 +153,27 @@ def test_mlstm_and_rnnt_joint_meta_and_autograd_trace(sc):
     assert "statecatcher.rnnt_joint_bwd.default" in names
     with pytest.raises(RuntimeError, match="multiple of 64"):
         sc.mlstm_fwd(q[:, :, :100], k[:, :, :100], v[:, :, :100], ig[:, :, :100], fg[:, :, :100])
+
+
+def test_gemm_and_adam_meta(sc):
+    """The projection GEMM, weight-gradient and optimizer ops: schemas and Meta shapes."""
+    a = torch.empty(4096, 512, device=META, dtype=torch.bfloat16)
+    w = torch.empty(3584, 512, device=META, dtype=torch.bfloat16)
+    c = sc.gemm_tn(a, w, 0)
+    assert c.shape == (4096, 3584) and c.dtype == torch.bfloat16
+    dy = torch.empty(4096, 3584, device=META, dtype=torch.bfloat16)
+    dw = sc.gemm_wgrad(dy, a, 512)
+    assert dw.shape == (3584, 512) and dw.dtype == torch.float32
+    p = [torch.empty(10, device=META), torch.empty(3, 4, device=META)]
+    n = sc.clip_adam_(p, p, p, p, 1, 50.0, 1e-3, 0.9, 0.999, 1e-8, 0.0, False, 1e-3, 0.03)
+    assert n.shape == () and n.dtype == torch.float32
+    s = str(torch.ops.statecatcher.clip_adam_.default._schema)
+    assert "Tensor(a!)[] params" in s and "Tensor(b!)[] exp_avgs" in s
+
+
+def test_gemm_ops_refuse_cpu(sc):
+    a = torch.zeros(256, 64, dtype=torch.bfloat16)
+    with pytest.raises((RuntimeError, NotImplementedError)):
+        sc.gemm_tn(a, a, 0)
+    with pytest.raises((RuntimeError, NotImplementedError)):
+        sc.gemm_wgrad(a, a, 0)
