@@ -191,10 +191,10 @@ def wgrad_splitk(dy, x, blocked_d=0):
     return colsum(part.view(S, N * K), perm).view(N, K)
 
 
-def wgrad_mfma(dy, x, blocked_d=0):
-    """dW = dy^T x in fp32 on the MFMA split-L kernel (sc_gemm_wgrad_bf16: gemm.hip) plus the
-    fixed-order slab sum (sc_colsum, which also un-permutes step-blocked rows), or None when the
-    shape is outside the kernel's tiling (the caller uses the library GEMM)."""
+def wgrad_mfma_slabs(dy, x):
+    """The split-L MFMA weight-gradient kernel alone (sc_gemm_wgrad_bf16: gemm.hip) on the
+    current stream: fp32 slabs [S, N, K] whose fixed-order sum is dW = dy^T x, or None when the
+    shape is outside the kernel's tiling."""
     M, N = dy.shape
     K = x.shape[1]
     lib = _lib.load()
@@ -206,8 +206,40 @@ def wgrad_mfma(dy, x, blocked_d=0):
     rc = lib.sc_gemm_wgrad_bf16(ptr(dy), dy.stride(0), ptr(x), x.stride(0), ptr(part), M, N, K, S,
                                 stream_of(dy))
     check(rc, "sc_gemm_wgrad_bf16")
+    return part
+
+
+def wgrad_slab_sum(part, blocked_d=0):
+    """dW [N, K] from wgrad_mfma_slabs' slabs: fixed-order sum (sc_colsum), un-permuting
+    step-blocked rows when blocked_d = D."""
+    S, N, K = part.shape
     perm = (blocked_d // 64, 7) if blocked_d else (1, 1)
     return colsum(part.view(S, N * K), perm).view(N, K)
+
+
+def wgrad_mfma(dy, x, blocked_d=0):
+    """dW = dy^T x in fp32 on the MFMA split-L kernel (sc_gemm_wgrad_bf16: gemm.hip) plus the
+    fixed-order slab sum (sc_colsum, which also un-permutes step-blocked rows), or None when the
+    shape is outside the kernel's tiling (the caller uses the library GEMM)."""
+    part = wgrad_mfma_slabs(dy, x)
+    return None if part is None else wgrad_slab_sum(part, blocked_d)
+
+
+# SC_WGRAD_STREAM=1 (A/B only): a cell's weight-gradient kernel on a side stream beside the
+# input-gradient GEMM, whose 376 tiles of 256 x 256 fill 1.5 waves of the 256 CUs, so that the
+# weight gradient's workgroups take the CUs its last wave leaves idle (slab sum and everything
+# after on the main stream; bitwise the same results).  Measured slower at C2 (5.13 vs 5.04 ms
+# per step): the persistent weight-gradient workgroups, started piecemeal, lose the per-XCD L2
+# sharing of their L-split (268 vs 165 us) and the library GEMM gets no faster.  Default off.
+USE_WGRAD_STREAM = os.environ.get("SC_WGRAD_STREAM", "0") == "1"
+_SIDE_STREAMS = {}
+
+
+def _side_stream(dev):
+    s = _SIDE_STREAMS.get(dev)
+    if s is None:
+        s = _SIDE_STREAMS[dev] = torch.cuda.Stream(device=dev)
+    return s
 
 
 # SC_TN=0 routes the projection GEMMs back to the library (A/B timing in tools/ only)
@@ -442,15 +474,34 @@ class LucyCellFn(torch.autograd.Function):
         dgates, dh0, ds0, dbias = _scan_bwd(gates, ckpt, dout, ds_last, ctx.needs_input_grad[2],
                                             bias)
         dg2 = dgates.view(xc.shape[0], -1)
+        bd = (dg2.shape[1] // 7) if ctx.blocked else 0
+        # the weight gradient's MFMA kernel on the side stream, beside the input gradient
+        part = None
+        if (USE_WGRAD_STREAM and ctx.needs_input_grad[0] and ctx.needs_input_grad[1]
+                and dg2.is_cuda and dg2.dtype == torch.bfloat16 and xc.dtype == torch.bfloat16):
+            main = torch.cuda.current_stream(dg2.device)
+            side = _side_stream(dg2.device)
+            side.wait_stream(main)   # dgates and x are complete
+            with torch.cuda.stream(side):
+                with _timed("gate_gemm_wgrad", dg2, 0):
+                    part = wgrad_mfma_slabs(dg2, xc)
+            if part is not None:
+                # (allocator: their blocks are not reused before the side stream's reads end)
+                dg2.record_stream(side)
+                xc.record_stream(side)
         dx = None
         if ctx.needs_input_grad[0]:
             with _timed("gate_gemm_dgrad", dg2, 0):
                 dx = torch.matmul(dg2, wt.t()) if wt is not None else proj_dgrad(dg2, wc)
             dx = dx.to(xdt)
         dw = None
-        if ctx.needs_input_grad[1]:
+        if part is not None:
+            main.wait_stream(side)
+            part.record_stream(main)
+            dw = wgrad_slab_sum(part, bd).to(wdt)
+        elif ctx.needs_input_grad[1]:
             with _timed("gate_gemm_wgrad", dg2, 0):
-                dw = wgrad_splitk(dg2, xc, blocked_d=(dg2.shape[1] // 7) if ctx.blocked else 0)
+                dw = wgrad_splitk(dg2, xc, blocked_d=bd)
             dw = dw.to(wdt)
         db = colsum(dbias.view(dbias.shape[0], -1)).to(wdt) if dbias is not None else None
         return dx, dw, db, dh0.to(hdt), ds0.to(sdt), None, None, None, None
