@@ -238,3 +238,31 @@ def test_autocast_linear_bias_from_sums_only_the_gate_columns():
     ref = dy.float().sum(0)
     assert bool((bq.grad[:2304] == 0).all())
     torch.testing.assert_close(bq.grad[2304:], ref[2304:], rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("din", [80, 512])
+def test_cell_side_stream_wgrad_bitwise(din, monkeypatch):
+    """ops.USE_WGRAD_STREAM (SC_WGRAD_STREAM=1): the cell's weight-gradient kernel on a side
+    stream beside the input gradient gives bitwise the same gradients as the one-stream order
+    (layer 0's Din = 80 takes the library weight gradient on the main stream either way)."""
+    o = ops()
+    g = torch.Generator(device="cuda").manual_seed(11)
+    B, T, D = 4, 200, 512
+    x = torch.randn(B, T, din, device="cuda", generator=g)
+    w = torch.randn(7 * D, din, device="cuda", generator=g) * 0.05
+    b = torch.randn(7 * D, device="cuda", generator=g) * 0.1
+    h0 = torch.zeros(B, D, device="cuda")
+    s0 = torch.zeros(B, D, device="cuda")
+    dout = torch.randn(B, T, D, device="cuda", generator=g).to(torch.bfloat16)
+
+    def run(side):
+        monkeypatch.setattr(o, "USE_WGRAD_STREAM", side)
+        leaves = [t.clone().requires_grad_(True) for t in (x, w, b)]
+        out, s_last, h_last = o.lucy_cell(leaves[0], leaves[1], leaves[2], h0, s0,
+                                          cdt=torch.bfloat16)
+        out.backward(dout)
+        torch.cuda.synchronize()
+        return [t.grad for t in leaves]
+
+    for a, c in zip(run(True), run(False)):
+        assert torch.equal(a, c)
