@@ -10,7 +10,13 @@
 //
 // Kernels (all on the caller's stream):
 //   ctc_emit_kernel   one wave per (b,t) row: log-sum-exp over V (logits only), then the
-//                     emission log-probs of the row's 2U+1 states, base 2, into lpe[b,t,:]
+//                     emission log-probs of the row's 2U+1 states, base 2, into lpe[b,t,:],
+//                     shifted by the row's largest one, c_t (kept in cst[b,t]).  Every path takes
+//                     exactly one emission per frame, so the shift moves every path by the same
+//                     sum_t c_t: exact, and it keeps the lattice's fp32 values near 0, where their
+//                     rounding is small (unshifted, a value ~ -10 bits per step away from its
+//                     re-centring carried 3e-3 of relative error into the T=1500 posteriors;
+//                     tools/ctc_precision.py)
 //   ctc_chain_kernel  per b: for every target position the next position with the same label,
 //                     so label occupancies are summed in a fixed order (deterministic, no atomics)
 //   ctc_ab_kernel     one workgroup per (sequence, direction): 2B workgroups run alpha forward
@@ -45,7 +51,8 @@ struct CtcWs {
   float* beta;    // [B,T,Sp]   base-2, relative to offB
   double* offA;   // [B,T]      base-2 offsets: entry n = offset after the n-th re-centring (at
   double* offB;   // [B,T]      step i = 2Kn - 1 of the direction), so step i has entry (i+1)/2K
-  double* nll64;  // [B]        natural log
+  float* cst;     // [B,T]      base-2 per-row emission shift c_t (lpe = log2 p - c_t)
+  double* ll2s;   // [B]        base-2 log-likelihood of the SHIFTED lattice (log2 p - sum_t c_t)
   int* chain;     // [B,Um]
   int* first;     // [B,Um]
 };
@@ -73,7 +80,8 @@ static size_t ws_layout(int B, int T, int Umax, CtcWs* w, void* base) {
   t.beta = (float*)take((size_t)B * T * Sp * 4);
   t.offA = (double*)take((size_t)B * T * 8);
   t.offB = (double*)take((size_t)B * T * 8);
-  t.nll64 = (double*)take((size_t)B * 8);
+  t.cst = (float*)take((size_t)B * T * 4);
+  t.ll2s = (double*)take((size_t)B * 8);
   t.chain = (int*)take((size_t)B * Um * 4);
   t.first = (int*)take((size_t)B * Um * 4);
   if (w) *w = t;
@@ -161,11 +169,15 @@ __global__ void __launch_bounds__(256) ctc_emit_kernel(CtcArgs a) {
   const int Sb = 2 * clampi(a.tgt_lens[b], 0, a.Umax) + 1;
   const int64_t* tg = a.tg + (int64_t)b * a.tgs;
   float* out = a.ws.lpe + row * a.Sp;
-  for (int s = lane; s < a.Sp; s += 64) {
-    float v = -1e30f;
-    if (s < Sb) v = fmaxf((E::ld(p[state_label(tg, s, a.blank, a.V)]) - lse) * kLog2e, -1e30f);
-    out[s] = v;
-  }
+  auto lp2 = [&](int s) {
+    return fmaxf((E::ld(p[state_label(tg, s, a.blank, a.V)]) - lse) * kLog2e, -1e30f);
+  };
+  float c = -1e30f;
+  for (int s = lane; s < Sb; s += 64) c = fmaxf(c, lp2(s));
+  c = wave_max_dpp(c);
+  if (!(c > -1e29f)) c = 0.0f;   // every state dead (or NaN): no shift, the sentinel stays
+  for (int s = lane; s < a.Sp; s += 64) out[s] = s < Sb ? fmaxf(lp2(s) - c, -1e30f) : -1e30f;
+  if (lane == 0) a.ws.cst[row] = c;
 }
 
 // ---------------------------------------------------------------------------- chains --------
@@ -445,6 +457,13 @@ __device__ __forceinline__ void ab_run(const CtcArgs& a, int b, int Tb, int Ub) 
     body(bufB, i0 + kAbP);
   }
   if (!BETA) {
+    // sum_t c_t, the emission shift of every path, in fp64 and a fixed order
+    __shared__ double csum[16];
+    double cs = 0.0;
+    for (int t = tid; t < Tb; t += blockDim.x) cs += (double)a.ws.cst[(int64_t)b * a.T + t];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) cs += __shfl_xor(cs, o);
+    if (lane == 0) csum[w] = cs;
     // log p = log2sum(alpha_{Tb-1}(2Ub), alpha_{Tb-1}(2Ub-1)) + off, gathered over the workgroup
     float c = lse2_live((own && p == Ub) ? vB : kDead, (own && p == Ub - 1) ? vL : kDead);
 #pragma unroll
@@ -458,13 +477,16 @@ __device__ __forceinline__ void ab_run(const CtcArgs& a, int b, int Tb, int Ub) 
     lds_barrier();
     if (tid == 0) {
       float cc = kDead;
+      double ctot = 0.0;
       for (int q = 0; q < nw; ++q) {
         const float m = fmaxf(cc, wmax[q]);
         cc = m + log2_(exp2_(cc - m) + exp2_(wmax[q] - m));
+        ctot += csum[q];
       }
-      const double nll = (cc < 0.5f * kDead) ? __builtin_huge_val() : -((double)cc + off) * (double)kLn2;
-      a.ws.nll64[b] = nll;
-      a.nll[b] = (float)nll;
+      const bool dead = cc < 0.5f * kDead;
+      const double ll2s = (double)cc + off;
+      a.ws.ll2s[b] = dead ? -__builtin_huge_val() : ll2s;
+      a.nll[b] = dead ? __builtin_huge_valf() : (float)(-(ll2s + ctot) * 0.6931471805599453);
     }
   }
 }
@@ -478,7 +500,7 @@ __global__ void __launch_bounds__(1024) ctc_ab_kernel(CtcArgs a) {
   if (Tb == 0) {
     if (!is_beta && threadIdx.x == 0) {
       a.nll[b] = (Ub == 0) ? 0.0f : __builtin_huge_valf();
-      a.ws.nll64[b] = (Ub == 0) ? 0.0 : __builtin_huge_val();
+      a.ws.ll2s[b] = (Ub == 0) ? 0.0 : -__builtin_huge_val();
     }
     return;
   }
@@ -546,11 +568,13 @@ __global__ void __launch_bounds__(256) ctc_grad_kernel(CtcArgs a) {
   wave_lds_sync();
   const float* al = a.ws.alpha + ((int64_t)b * a.T + t) * a.Sp;
   const float* be = a.ws.beta + ((int64_t)b * a.T + t) * a.Sp;
-  // exp(lcab + nll - lp) = 2^(lcab2 + offA + offB + nll*log2e - lp*log2e): fold offsets in fp64
+  // exp(lcab + nll - lp) = 2^(lcab2 + offA + offB + c_t - ll2s - lp*log2e): the lattice holds
+  // alpha_t - sum_{t'<=t} c and beta_t - sum_{t'>=t} c, so alpha + beta carries c_t once more than
+  // the shifted log-likelihood ll2s; offsets folded in fp64
   const int per = 2 * a.kh;   // steps per re-centring
   const float koff = (float)(a.ws.offA[(int64_t)b * a.T + (t + 1) / per] +
                              a.ws.offB[(int64_t)b * a.T + (Tb - t) / per] +
-                             a.ws.nll64[b] * (double)kLog2e);
+                             (double)a.ws.cst[(int64_t)b * a.T + t] - a.ws.ll2s[b]);
   const int* chain = a.ws.chain + (int64_t)b * Um;
   const int* first = a.ws.first + (int64_t)b * Um;
   float m = kNegInf, l = 0.0f;   // blank-label occupancy (base 2), per lane

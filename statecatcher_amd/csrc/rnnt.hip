@@ -6,6 +6,15 @@
 //                      logits: the log_softmax of model.py:93 is fused), then the node's blank
 //                      and label log-probs in base 2, stored DIAGONAL-MAJOR ([b][t+u][u]) so
 //                      that the wavefront below reads one coalesced row per step.
+//   rnnt_shift_kernel  one wave per diagonal row: subtracts from every blank log-prob of frame t
+//                      the frame's largest, cb[t], and from every label-u log-prob the largest
+//                      over t, cy[u] (both gathered by the emission producers with order-mapped
+//                      integer atomicMax, so they are exact and independent of order).  Every
+//                      path takes exactly one blank per frame and one emission of each label, so
+//                      the shift moves every path by the same sum cb + sum cy: exact, and it keeps
+//                      the fp32 lattice values near 0.  Unshifted, nodes of one diagonal lie
+//                      hundreds of bits apart and their rounding put ~1e-2 of relative error into
+//                      the arc occupancies at T=1500, U=150 (tools/ctc_precision.py --rnnt).
 //   rnnt_ab_kernel     one workgroup per (sequence, direction): alpha forward and beta backward
 //                      run concurrently.  Lane = label position u; the lattice is swept by
 //                      anti-diagonals n = t + u (all nodes of a diagonal are independent), the
@@ -33,8 +42,21 @@ struct RnntWs {
   float* beta;     // [B][ND][U1p]    base-2, relative to offB[b][t+u]
   double* offA;    // [B][ND]
   double* offB;    // [B][ND]
-  double* logp2;   // [B]             base-2 log P(y|x)
+  double* logp2;   // [B]             base-2 log P(y|x) of the SHIFTED lattice (log2 P - shifts)
+  unsigned* cmb;   // [B][T]          order-mapped max over u of the frame's blank log-probs
+  unsigned* cmy;   // [B][U1]         order-mapped max over t of label u's log-probs (follows cmb)
 };
+
+// float <-> unsigned key with the same order (0 is below every key: "no value")
+__device__ __forceinline__ unsigned fkey(float f) {
+  const unsigned u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+// the shift a key stands for: 0 when nothing live was seen (the sentinel must stay dead)
+__device__ __forceinline__ float kshift(unsigned k) {
+  const float f = __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+  return (k != 0u && f > -1e29f) ? f : 0.0f;
+}
 
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 int u1p_of(int Umax) { return 64 * ((Umax + 1 + 63) / 64); }
@@ -57,6 +79,8 @@ size_t ws_layout(int B, int T, int Umax, RnntWs* w, void* base) {
   t.offA = (double*)take((size_t)B * ND * 8);
   t.offB = (double*)take((size_t)B * ND * 8);
   t.logp2 = (double*)take((size_t)B * 8);
+  t.cmb = (unsigned*)take((size_t)B * (T + U1) * 4);
+  t.cmy = t.cmb + (size_t)B * T;
   if (w) *w = t;
   return off;
 }
@@ -152,8 +176,38 @@ __global__ void __launch_bounds__(256) rnnt_emit_kernel(RnntArgs a) {
   if (lane == 0) {
     const int64_t d = ((int64_t)b * a.ND + t + u) * a.U1p + u;
     a.ws.lse[node] = lse;
-    a.ws.lpb[d] = fmaxf((E::ld(p[a.blank]) - lse) * kLog2e, kDeadR);
-    a.ws.lpy[d] = u < Ub ? fmaxf((E::ld(p[label_at(a, b, u)]) - lse) * kLog2e, kDeadR) : kDeadR;
+    const float lb = fmaxf((E::ld(p[a.blank]) - lse) * kLog2e, kDeadR);
+    a.ws.lpb[d] = lb;
+    atomicMax(a.ws.cmb + (int64_t)b * a.T + t, fkey(lb));
+    if (u < Ub) {
+      const float ly = fmaxf((E::ld(p[label_at(a, b, u)]) - lse) * kLog2e, kDeadR);
+      a.ws.lpy[d] = ly;
+      atomicMax(a.ws.cmy + (int64_t)b * a.U1 + u, fkey(ly));
+    } else {
+      a.ws.lpy[d] = kDeadR;
+    }
+  }
+}
+
+// the emission shift (see the file header), in place, one wave per diagonal row (b, n)
+__global__ void __launch_bounds__(256) rnnt_shift_kernel(RnntArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= (int64_t)a.B * a.ND) return;
+  const int b = (int)(row / a.ND), n = (int)(row % a.ND);
+  const int Tb = clampr(a.flen[b], 0, a.T), Ub = clampr(a.llen[b], 0, a.Umax);
+  if (n >= Tb + Ub) return;
+  float* pb = a.ws.lpb + row * a.U1p;
+  float* py = a.ws.lpy + row * a.U1p;
+  for (int u = lane; u <= Ub; u += 64) {
+    const int t = n - u;
+    if (t < 0 || t >= Tb) continue;
+    const float vb = pb[u];
+    if (vb > -1e29f) pb[u] = fmaxf(vb - kshift(a.ws.cmb[(int64_t)b * a.T + t]), kDeadR);
+    if (u < Ub) {
+      const float vy = py[u];
+      if (vy > -1e29f) py[u] = fmaxf(vy - kshift(a.ws.cmy[(int64_t)b * a.U1 + u]), kDeadR);
+    }
   }
 }
 
@@ -286,10 +340,23 @@ __device__ __forceinline__ void ab_run(const RnntArgs& a, int b, int Tb, int Ub)
     load(ebA, eyA, i0 + 2 * kPf);
     body(ebB, eyB, i0 + kPf);
   }
-  if (!BETA && own && u == Ub) {   // log P = alpha(Tb-1, Ub) + its terminal blank
-    const double lp = (double)v + (double)lpb[(int64_t)(nd - 1) * a.U1p + Ub] + off;
-    a.ws.logp2[b] = lp;
-    a.nll[b] = (float)(-lp * (double)kLn2);
+  if (!BETA) {
+    // the emission shift of every path, sum_t cb[t] + sum_{u<Ub} cy[u], fp64 in a fixed order
+    __shared__ double csum[16];
+    double cs = 0.0;
+    for (int i = tid; i < Tb + Ub; i += blockDim.x)
+      cs += (double)kshift(i < Tb ? a.ws.cmb[(int64_t)b * a.T + i] : a.ws.cmy[(int64_t)b * a.U1 + i - Tb]);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) cs += __shfl_xor(cs, o);
+    if (lane == 0) csum[w] = cs;
+    lds_barrier();
+    if (own && u == Ub) {   // log P = alpha(Tb-1, Ub) + its terminal blank (+ the shift)
+      double ctot = 0.0;
+      for (int q = 0; q < nw; ++q) ctot += csum[q];
+      const double lp = (double)v + (double)lpb[(int64_t)(nd - 1) * a.U1p + Ub] + off;
+      a.ws.logp2[b] = lp;
+      a.nll[b] = (float)(-(lp + ctot) * 0.6931471805599453);
+    }
   }
 }
 
@@ -422,11 +489,23 @@ void launch_ab(const RnntArgs& a, hipStream_t st) {
   }
 }
 
+// the shift maxima start at key 0 ("nothing seen"); the emission producers raise them
+void clear_shift(const RnntArgs& a, hipStream_t st) {
+  (void)hipMemsetAsync(a.ws.cmb, 0, (size_t)a.B * (a.T + a.U1) * 4, st);
+}
+// shift the emissions, then alpha / beta
+void launch_lattice(const RnntArgs& a, hipStream_t st) {
+  const int64_t rows = (int64_t)a.B * a.ND;
+  hipLaunchKernelGGL(rnnt_shift_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, a);
+  launch_ab(a, st);
+}
+
 template <int DT>
 void launch_fwd(const RnntArgs& a, hipStream_t st) {
   const int64_t nodes = (int64_t)a.B * a.T * a.U1;
+  clear_shift(a, st);
   hipLaunchKernelGGL((rnnt_emit_kernel<DT>), dim3((unsigned)((nodes + 3) / 4)), dim3(256), 0, st, a);
-  launch_ab(a, st);
+  launch_lattice(a, st);
 }
 
 template <int DT, int GT>
@@ -744,13 +823,21 @@ __global__ void __launch_bounds__(512) joint_fwd_kernel(JointArgs a) {
       const float* bias = (const float*)(lds + kVmaxJ * 128);
       lb += bias[r.blank];
       ly += bias[yl];
+      const float lb2 = fmaxf((lb - lse) * kLog2e, kDeadR);
+      const float ly2 = u < Ub ? fmaxf((ly - lse) * kLog2e, kDeadR) : kDeadR;
       if (h == 0 && tok) {
         const int64_t node = ((int64_t)b * r.T + t) * r.U1 + u;
         const int64_t d = ((int64_t)b * r.ND + t + u) * r.U1p + u;
         r.ws.lse[node] = lse;
-        r.ws.lpb[d] = fmaxf((lb - lse) * kLog2e, kDeadR);
-        r.ws.lpy[d] = u < Ub ? fmaxf((ly - lse) * kLog2e, kDeadR) : kDeadR;
+        r.ws.lpb[d] = lb2;
+        r.ws.lpy[d] = ly2;
+        atomicMax(r.ws.cmb + (int64_t)b * r.T + t, fkey(lb2));
       }
+      // label u's max over the column's 32 frames first: one atomic per column
+      unsigned ky = (h == 0 && tok && u < Ub) ? fkey(ly2) : 0u;
+#pragma unroll
+      for (int o = 16; o > 0; o >>= 1) ky = max(ky, (unsigned)__shfl_xor((int)ky, o));
+      if (lane == 0 && u < Ub) atomicMax(r.ws.cmy + (int64_t)b * r.U1 + u, ky);
     }
   }
 }
@@ -1418,8 +1505,9 @@ extern "C" int sc_rnnt_joint_fwd(const float* enc, const float* pred, const void
   static const bool ok = joint_lds_attr(joint_fwd_kernel, joint_lds_fwd());
   SC_REQUIRE(ok, "sc_rnnt_joint_fwd: LDS attribute");
   hipStream_t st = (hipStream_t)stream;
+  clear_shift(j.r, st);
   hipLaunchKernelGGL(joint_fwd_kernel, dim3(256), dim3(512), joint_lds_fwd(), st, j);
-  launch_ab(j.r, st);
+  launch_lattice(j.r, st);
   return launch_status("sc_rnnt_joint_fwd");
 }
 

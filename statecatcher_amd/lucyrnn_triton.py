@@ -13,6 +13,8 @@ Differences from the reference, all deliberate:
   * s_last and the carried h (out[:, -1]) are returned in fp32 whatever the gate dtype, so a
     bf16-autocast run carries its state across segments unrounded, as the fp32 reference does.
 """
+import threading
+
 import torch
 import torch.nn as nn
 
@@ -49,6 +51,27 @@ class _LinearFn(torch.autograd.Function):
         dw = wgrad_splitk(dy, xc).to(wdt) if ctx.needs_input_grad[1] else None
         db = colsum(dy).to(wdt) if has_b and ctx.needs_input_grad[2] else None
         return dx, dw, db, None, None
+
+
+# compute_loss's request to hand the output projection to the loss (ops.CTCHeadFn): set, the next
+# LucyRNNtriton forward on this thread that can fuse stores (hidden, output_proj, images) here
+# and returns DEFERRED_LOGITS in place of the logits
+_HEAD = threading.local()
+DEFERRED_LOGITS = object()
+
+
+class defer_output_head:
+    """with defer_output_head() as h: ... model(...) ...; h.taken is (x, output_proj, images) when
+    the encoder deferred its output projection, else None."""
+
+    def __enter__(self):
+        self.taken = None
+        _HEAD.req = self
+        return self
+
+    def __exit__(self, *exc):
+        _HEAD.req = None
+        return False
 
 
 class LinearSafe(nn.Module):
@@ -216,7 +239,13 @@ class LucyRNNtriton(nn.Module):
             x = track_outputs[0]
         else:
             x = self.merge_proj(torch.cat(track_outputs, dim=-1))
-        logits = self.output_proj(x.contiguous(), out_imgs)
+        req = getattr(_HEAD, "req", None)
+        if req is not None and out_imgs is not None and out_imgs[1] is not None:
+            req.taken = (x, self.output_proj, out_imgs)
+            _HEAD.req = None
+            logits = DEFERRED_LOGITS
+        else:
+            logits = self.output_proj(x.contiguous(), out_imgs)
         if self.config.return_last_states:
             return logits, (final_h, final_s)
         return logits

@@ -12,9 +12,9 @@ import torch
 import torch.nn as nn
 
 from .lucyrnn_conf import LucyRNNConfig
-from .lucyrnn_triton import LucyRNNtriton
+from .lucyrnn_triton import DEFERRED_LOGITS, LucyRNNtriton, defer_output_head
 from .xlstm import xLSTMLarge, xLSTMLargeConfig
-from .ops import ctc_loss, rnnt_joint_loss, rnnt_joint_supported, rnnt_loss
+from .ops import ctc_head_loss, ctc_head_supported, ctc_loss, rnnt_joint_loss, rnnt_joint_supported, rnnt_loss
 
 
 def detach_states(states):
@@ -52,11 +52,17 @@ class CTCLoss(nn.Module):
     log_softmax that model.py:70 applies first and skips the transpose.
     """
 
-    def __init__(self, blank=0, reduction="mean", zero_infinity=True):
+    def __init__(self, blank=0, reduction="mean", zero_infinity=True, fused_head=False):
         super().__init__()
         self.blank = blank
         self.reduction = reduction
         self.zero_infinity = zero_infinity
+        # compute_loss under bf16 autocast: the encoder's output projection joins the loss
+        # (ops.CTCHeadFn, fp32 logits) when reduction is the training criterion's
+        self.fuse_output_head = fused_head
+
+    def fused_head(self):
+        return self.fuse_output_head and self.reduction == "mean" and self.zero_infinity
 
     def forward(self, log_probs, targets, input_lengths, target_lengths):
         return ctc_loss(log_probs.transpose(0, 1), targets, input_lengths, target_lengths,
@@ -78,7 +84,22 @@ def compute_loss(mode: str, criterion: nn.Module, model: nn.Module, feats: torch
         input_state = detach_states(input_state)
         if args is not None and getattr(args, "debug", False):
             assert_all_detached(input_state)
-    enc_out, output_state = model(feats, masks, input_state)
+    fuse_head = (mode == "ctc" and isinstance(criterion, CTCLoss) and criterion.fused_head()
+                 and feats.is_cuda and torch.is_autocast_enabled("cuda")
+                 and torch.get_autocast_dtype("cuda") == torch.bfloat16)
+    if fuse_head:
+        # the LucyRNNtriton encoder hands its output projection to the loss (ops.CTCHeadFn):
+        # fp32 logits into the lattice, a bf16 gradient straight into the projection backward
+        with defer_output_head() as head:
+            enc_out, output_state = model(feats, masks, input_state)
+        if enc_out is DEFERRED_LOGITS:
+            x, proj, imgs = head.taken
+            with torch.autocast("cuda", enabled=False):
+                loss, enc_out = ctc_head_loss(x, proj.weight, proj.bias, imgs, tokens, in_lens,
+                                              tgt_lens, blank=criterion.blank)
+            return loss, output_state, enc_out, output_state
+    else:
+        enc_out, output_state = model(feats, masks, input_state)
     if mode == "ctc":
         if isinstance(criterion, CTCLoss):
             loss = criterion.forward_logits(enc_out, tokens, in_lens, tgt_lens)
@@ -143,8 +164,10 @@ class RNNTLoss(nn.Module):
     def use_fused_joint(self):
         if self.fused_joint is not None:
             return bool(self.fused_joint)
-        return (torch.is_autocast_enabled("cuda")
-                and torch.get_autocast_dtype("cuda") in (torch.bfloat16, torch.float16))
+        # bf16 autocast only: the fused kernels round W and z to bf16, coarser than the 10-bit
+        # mantissa of a float16 autocast run (the reference's own training dtype, train.py:516),
+        # which keeps the materialised joiner in float16
+        return torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16
 
     def forward(self, log_probs, labels, frames_lengths, labels_lengths, blank_id=None,
                 compact=False, gather=True):

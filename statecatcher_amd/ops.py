@@ -692,6 +692,78 @@ class CTCMeanFn(torch.autograd.Function):
         return CTCFn.backward(ctx, ctx.factor * grad_loss)
 
 
+def _logits_fp32(x2, wc, b):
+    """x2 [M,K] bf16 @ wc [V,K]^T + b (fp32) -> fp32 [M,V]: the MFMA accumulator leaves the GEMM
+    unrounded (hipBLASLt with an fp32 D)."""
+    return torch.addmm(b, x2, wc.t(), out_dtype=torch.float32)
+
+
+class CTCHeadFn(torch.autograd.Function):
+    """output_proj (LinearSafe, lucyrnn_triton.py:107-109, :150) + log_softmax + nn.CTCLoss(
+    reduction='mean', zero_infinity=True) (model.py:68-71, train.py:142) as ONE node, for bf16
+    autocast training.  Returns (loss, logits).
+
+    Why: rounding the logits to bf16 before the lattice is what costs the bf16 C2 step 2-5% of
+    gradient direction against the fp32 oracle (tools/bf16_logits_diag.py reproduces the measured
+    cosines from that rounding alone).  Here the projection writes fp32 logits, which the lattice
+    reads, and the lattice's gradient is written in bf16 straight into the projection backward's
+    operand (a separate fp32 logits tensor would need an fp32 gradient and a cast pass, since
+    autograd casts a gradient to its input's dtype).  The logits output stays differentiable: a
+    gradient reaching it from elsewhere is added before the projection backward."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, wc, wt, targets, in_lens, tgt_lens, blank):
+        ctx.set_materialize_grads(False)
+        B, T, K = x.shape
+        V = w.shape[0]
+        x2 = x.reshape(-1, K)
+        logits = _logits_fp32(x2, wc, b).view(B, T, V)
+        loss = CTCMeanFn.forward(ctx, logits, targets, in_lens, tgt_lens, blank, True)
+        ctx.head = (x2, wt, x.shape, x.dtype)
+        return loss, logits
+
+    @staticmethod
+    def backward(ctx, g_loss, g_logits):
+        logits, targets, in_lens, tgt_lens, nll, ws = ctx.saved_tensors
+        blank, is_logits, umax, wsb = ctx.meta
+        x2, wt, xshape, xdt = ctx.head
+        B, T, V = logits.shape
+        dy = torch.empty(B, T, V, dtype=torch.bfloat16, device=logits.device)
+        if g_loss is None:
+            dy.zero_()
+        elif T > 0:
+            scale = (ctx.factor * g_loss).to(torch.float32).contiguous()
+            rc = _lib.load().sc_ctc_bwd(ptr(logits), dtype_code(logits), 1, B, T, V,
+                                        logits.stride(0), logits.stride(1), ptr(targets),
+                                        targets.stride(0) if umax else 0, umax, ptr(in_lens),
+                                        ptr(tgt_lens), blank, ptr(nll), ptr(scale), ptr(dy),
+                                        dtype_code(dy), ptr(ws), wsb, stream_of(logits))
+            check(rc, "sc_ctc_bwd")
+        if g_logits is not None:
+            dy = (dy.float() + g_logits).to(torch.bfloat16)
+        dy2 = dy.view(-1, V)
+        dx = torch.matmul(dy2, wt.t()).view(xshape).to(xdt) if ctx.needs_input_grad[0] else None
+        dw = wgrad_splitk(dy2, x2) if ctx.needs_input_grad[1] else None
+        db = colsum(dy2) if ctx.needs_input_grad[2] else None
+        return dx, dw, db, None, None, None, None, None, None
+
+
+def ctc_head_supported(x, w, b, imgs):
+    """CTCHeadFn applies: bf16 hidden on the GPU, fp32 projection with a bias, bf16 images of W
+    and W^T (LucyRNNtriton._weight_images under bf16 autocast)."""
+    return (imgs is not None and imgs[1] is not None and x.is_cuda and x.dtype == torch.bfloat16
+            and x.dim() == 3 and b is not None and w.dtype == torch.float32
+            and b.dtype == torch.float32)
+
+
+def ctc_head_loss(x, w, b, imgs, targets, in_lens, tgt_lens, blank=0):
+    """(loss, fp32 logits) of CTCHeadFn: x [B,T,D] bf16 hidden, w [V,D] / b [V] the fp32
+    output_proj parameters, imgs their (W, W^T) bf16 images."""
+    dev = x.device
+    return CTCHeadFn.apply(x.contiguous(), w, b, imgs[0], imgs[1], targets.to(dev),
+                           _as_len_tensor(in_lens, dev), _as_len_tensor(tgt_lens, dev), int(blank))
+
+
 def ctc_nll(x, targets, in_lens, tgt_lens, blank=0, is_logits=True):
     dev = x.device
     return CTCFn.apply(x, targets.to(dev), _as_len_tensor(in_lens, dev), _as_len_tensor(tgt_lens, dev),

@@ -8,13 +8,14 @@ step oracle + the joint and transducer lattice in fp64 (oracle.rnnt, pinned by b
 alignment sums).  warp_rnnt itself is absent: parity w.r.t. it is unpinned.
 
 * fp32 (no autocast): compute_loss keeps the reference's fp32 joiner logits (the materialised
-  sc_rnnt_* path).  Loss to 1e-4 relative; every encoder and joiner gradient to 6e-3 in norm
-  (measured 2.0e-3 ... 5.1e-3, largest at layer 0: like CTC, an fp32 log-space lattice over
-  T = 1500 carries ~1e-3 of absolute error into the alignment posteriors; the oracle's lattice
-  is fp64).  The encoder's backward alone -- the oracle fed the GPU's own d loss / d enc_out --
+  sc_rnnt_* path).  Loss to 1e-4 relative; every encoder and joiner gradient to 1e-3 in norm,
+  north_star's tolerance (measured 2e-6 ... 3.2e-5 with rnnt.hip's per-frame blank / per-label
+  emission shift; 2.0e-3 ... 5.1e-3 before it, when the nodes of one lattice diagonal sat hundreds
+  of bits apart in fp32).  The encoder's backward alone -- the oracle fed the GPU's own d loss / d enc_out --
   to 1e-3.
 * The fused joiner (RNNTLoss(fused_joint=True), what the bench runs): against the oracle with
-  the fused kernels' bf16 rounding of W and tanh(enc + pred): loss 1e-4, gradients 1e-2 in norm.
+  the fused kernels' bf16 rounding of W and tanh(enc + pred): loss 1e-4, gradients 1e-3 in norm
+  (measured 2.5e-4 ... 3.6e-4: the bf16 logits MFMA's own accumulation order).
 * The bench's arithmetic (bf16 autocast, fused joiner) against the fp32 oracle: loss 1e-3;
   per tensor gradient cosine >= 0.999 and norm within 1% (measured >= 0.9999, 0.25%).
 """
@@ -83,7 +84,7 @@ def test_c5_step_fp32_vs_oracle():
     errs = {k: rel(grads[k], ref_g[k]) for k in ref_g}
     errs.update({"joiner." + k: rel(jgrads[k], ref_jg[k]) for k in ref_jg})
     print("C5 fp32 grads rel: " + " ".join(f"{k} {v:.1e}" for k, v in errs.items()))
-    assert max(errs.values()) < 6e-3, errs
+    assert max(errs.values()) < 1e-3, errs
     # the encoder's backward on its own: the oracle fed the GPU's d loss / d enc_out
     logits, _, x, (caches, h, s) = lucy_step.forward(p, feats, L6, D512)
     enc_g = lucy_step.encoder_backward(p, dlog.astype(np.float32), x, caches, h, s, L6, D512)
@@ -104,7 +105,7 @@ def test_c5_step_fused_joiner_vs_oracle_bf16_joint():
     errs = {k: rel(grads[k], ref_g[k]) for k in ref_g}
     errs.update({"joiner." + k: rel(jgrads[k], ref_jg[k]) for k in ref_jg})
     print("C5 fused grads rel: " + " ".join(f"{k} {v:.1e}" for k, v in errs.items()))
-    assert max(errs.values()) < 1e-2, errs
+    assert max(errs.values()) < 1e-3, errs
 
 
 def test_c5_step_bf16_autocast_vs_fp32_oracle():

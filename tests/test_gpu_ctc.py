@@ -71,7 +71,10 @@ def test_ctc_full_size_vs_aten_cpu():
     ref = torch.nn.CTCLoss(blank=0, zero_infinity=True)(xr.log_softmax(-1).transpose(0, 1), tg, il, tl)
     ref.backward()
     np.testing.assert_allclose(loss.item(), ref.item(), rtol=1e-4)
-    np.testing.assert_allclose(x.grad.cpu().numpy(), xr.grad.numpy(), rtol=1e-2, atol=2e-6)
+    # the gradient to north_star's 1e-3 in norm (measured 3.3e-4 with the per-frame emission
+    # shift of ctc.hip; 2.5e-3 before it)
+    g64 = xr.grad.numpy()
+    assert np.linalg.norm(x.grad.cpu().numpy() - g64) / np.linalg.norm(g64) <= 1e-3
     # at least as accurate as the reference's own criterion in fp32 (ATen ctc_loss, CPU fp32)
     x32 = logits.clone().requires_grad_(True)
     torch.nn.CTCLoss(blank=0, zero_infinity=True)(x32.log_softmax(-1).transpose(0, 1), tg, il, tl).backward()
@@ -104,8 +107,12 @@ def test_ctc_long_targets_many_waves_vs_aten_cpu(U):
                                        reduction="none", zero_infinity=False)
     ref.sum().backward()
     np.testing.assert_allclose(nll.detach().cpu().numpy(), ref.detach().numpy(), rtol=1e-4)
-    # |grad| <= 1; fp32 log-space lattices over T = 2054 steps: 1e-4 absolute
-    np.testing.assert_allclose(x.grad.cpu().numpy(), xr.grad.numpy(), rtol=1e-2, atol=1e-4)
+    # |grad| <= 1: 1e-4 absolute per element, and 1e-3 in norm (north_star)
+    g, g64 = x.grad.cpu().numpy(), xr.grad.numpy()
+    np.testing.assert_allclose(g, g64, rtol=1e-2, atol=1e-4)
+    rel = np.linalg.norm(g - g64) / np.linalg.norm(g64)
+    print(f"U={U}: CTC grad rel err vs fp64 {rel:.2e}")
+    assert rel <= 1e-3
 
 
 def test_ctc_bf16_logits_vs_oracle():

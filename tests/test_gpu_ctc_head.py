@@ -1,0 +1,108 @@
+"""The fused output projection + CTC node (ops.CTCHeadFn) that compute_loss uses under bf16
+autocast: output_proj (lucyrnn_triton.py:107-109, :150) writes fp32 logits, the lattice
+(model.py:68-71, train.py:142: log_softmax + nn.CTCLoss(mean, zero_infinity)) reads them, and its
+gradient goes to the projection backward in bf16.
+
+* Against the same computation unfused on the same bf16 operands (fp32 logits from the bf16
+  GEMM, the fp32 HIP lattice, the projection's backward in fp32 torch): loss 1e-5 relative,
+  gradients 1e-2 in norm (the fused backward's bf16 dlogits and bf16 GEMMs).
+* The returned logits stay differentiable: a second loss on them adds its gradient.
+* compute_loss takes it exactly under bf16 autocast with CTCLoss(fused_head=True).
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0") if torch.cuda.is_available() else None
+
+
+def sc():
+    import statecatcher_amd as s
+    return s
+
+
+def rel(a, b):
+    return float((a.double() - b.double()).norm() / b.double().norm())
+
+
+def inputs(B=3, T=200, D=256, V=512, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    x = (torch.randn(B, T, D, generator=g) * 0.5).to(torch.bfloat16).to(DEV)
+    w = (torch.randn(V, D, generator=g) * 0.05).to(DEV)
+    b = (torch.randn(V, generator=g) * 0.1).to(DEV)
+    U = [20, 35, 0]
+    tg = torch.randint(1, V, (B, 35), generator=g)
+    for i, u in enumerate(U):
+        tg[i, u:] = 0
+    return x, w, b, tg.to(DEV), [T, T - 30, T - 7], U
+
+
+def test_ctc_head_vs_unfused():
+    x, w, b, tg, il, tl = inputs()
+    ops = sc().ops
+    wc, wt = w.to(torch.bfloat16), w.t().contiguous().to(torch.bfloat16)
+    x1 = x.clone().requires_grad_(True)
+    w1, b1 = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    loss, logits = ops.ctc_head_loss(x1, w1, b1, (wc, wt), tg, il, tl)
+    assert logits.dtype == torch.float32
+    loss.backward()
+    # unfused: fp32 logits of the same bf16 operands; w, b enter through an identity-gradient
+    # rounding so their gradients are d loss / d (bf16 W) as the fused node's are
+    x2 = x.float().requires_grad_(True)
+    w2, b2 = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    wq = w2 + (wc.float() - w2).detach()
+    ref_logits = x2 @ wq.t() + b2
+    ref = sc().ctc_loss(ref_logits, tg, il, tl)
+    ref.backward()
+    print(f"head: loss {loss.item():.6f} vs {ref.item():.6f}; logits {rel(logits, ref_logits):.1e}; "
+          f"dx {rel(x1.grad, x2.grad):.2e} dW {rel(w1.grad, w2.grad):.2e} db {rel(b1.grad, b2.grad):.2e}")
+    np.testing.assert_allclose(loss.item(), ref.item(), rtol=1e-5)
+    assert rel(logits, ref_logits) < 1e-5
+    for got, want in ((x1.grad, x2.grad), (w1.grad, w2.grad), (b1.grad, b2.grad)):
+        assert got.dtype == want.dtype or got.dtype == torch.bfloat16
+        assert rel(got, want) < 1e-2
+
+
+def test_ctc_head_logits_stay_differentiable():
+    x, w, b, tg, il, tl = inputs(seed=1)
+    wc, wt = w.to(torch.bfloat16), w.t().contiguous().to(torch.bfloat16)
+    w1 = w.clone().requires_grad_(True)
+    loss, logits = sc().ops.ctc_head_loss(x, w1, b, (wc, wt), tg, il, tl)
+    (loss + logits.square().sum()).backward()
+    g_both = w1.grad.clone()
+    w1.grad = None
+    loss, logits = sc().ops.ctc_head_loss(x, w1, b, (wc, wt), tg, il, tl)
+    loss.backward()
+    g_ctc = w1.grad.clone()
+    extra = 2.0 * (logits.detach().reshape(-1, w.shape[0]).t() @ x.float().reshape(-1, x.shape[2]))
+    assert rel(g_both - g_ctc, extra) < 2e-2
+
+
+def test_compute_loss_uses_head_under_bf16_autocast(monkeypatch):
+    import statecatcher_amd.model as m
+    calls = []
+    orig = m.ctc_head_loss
+    monkeypatch.setattr(m, "ctc_head_loss", lambda *a, **k: calls.append(1) or orig(*a, **k))
+    cfg = sc().build_lucyrnn_config(80, 128, 2, 256)
+    model = sc().ASRModel(None, cfg, vocab_size=256, feat_dim=80, proj_dim=-1).to(DEV)
+    with torch.no_grad():
+        model.encoder.output_proj.weight.normal_(0, 0.05)
+    feats = torch.randn(2, 64, 80, device=DEV)
+    masks = torch.ones(2, 64, dtype=torch.bool, device=DEV)
+    tok = torch.randint(1, 256, (2, 10), device=DEV)
+    crit = sc().CTCLoss(blank=0, zero_infinity=True, fused_head=True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        loss, _, enc_out, _ = sc().compute_loss("ctc", crit, model, feats, masks, tok, [64, 64],
+                                                [10, 10], 0)
+    assert calls and enc_out.dtype == torch.float32 and enc_out.shape == (2, 64, 256)
+    loss.backward()
+    assert model.encoder.output_proj.weight.grad is not None
+    # fp32 training and a non-fusing criterion keep the module's own logits
+    calls.clear()
+    loss, _, enc_out, _ = sc().compute_loss("ctc", crit, model, feats, masks, tok, [64, 64], [10, 10], 0)
+    assert not calls and enc_out.dtype == torch.float32
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        _, _, enc_out, _ = sc().compute_loss("ctc", sc().CTCLoss(blank=0, fused_head=False), model,
+                                             feats, masks, tok, [64, 64], [10, 10], 0)
+    assert not calls and enc_out.dtype == torch.bfloat16

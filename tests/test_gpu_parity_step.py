@@ -16,11 +16,11 @@ Tolerances (stated per element class; both sides fp32 unless noted):
   ~1e3 at 0, so rounding-order differences of a gate near zero are amplified.
   C2 step (well-conditioned init, see oracle_params -- the reference init is chaotic at C2
   depth even between the reference math's own fp32 and fp64 runs): loss 1e-4 relative;
-  gradients ||g - g_ref|| / ||g_ref|| <= 6e-3 per tensor (measured 2.0e-3 on output_proj,
-  growing to 4.2e-3 at layer 0).  The oracle runs CTC in fp64; any fp32 log-space lattice over
-  T=1500 carries ~1e-3 absolute error in alpha + beta - nll, i.e. relative error in the
-  alignment posteriors: ATen's own fp32 ctc_loss (the reference's criterion) is 3.7e-3 from
-  fp64 at this shape (tests/test_gpu_ctc.py measures both on the same input).
+  gradients ||g - g_ref|| / ||g_ref|| <= 1e-3 per tensor, north_star's tolerance (measured
+  1.2e-4 ... 1.6e-4, profiles/r4_parity_measured.md).  The oracle runs CTC in fp64; the HIP
+  lattice is fp32 in log space with every frame's emissions shifted by their maximum
+  (csrc/ctc.hip), which holds the posteriors' error at ~1e-4 (2.5e-3 without the shift; ATen's own
+  fp32 ctc_loss, the reference's criterion, is 5.2e-2 from fp64 on these logits).
   bf16: gradient cosine >= 0.97 and norm within 10% per tensor (bf16 logits move CTC's
   alignment posteriors by ~20% at T=1500 with an untrained, near-uniform output).
   Adam step 1: the post-step parameters equal clip + Adam restated on the GPU's own gradients
@@ -222,7 +222,7 @@ def test_c2_training_step_fp32_vs_oracle():
         rels[k] = np.linalg.norm(g - rg) / np.linalg.norm(rg)
         print(f"fp32 grad {k}: rel {rels[k]:.2e} norm {np.linalg.norm(rg):.3e} "
               f"max-err/max {np.abs(g - rg).max() / np.abs(rg).max():.2e}")
-    assert max(rels.values()) < 6e-3, rels
+    assert max(rels.values()) < 1e-3, rels
     # the encoder's backward on its own, free of CTC-lattice noise: the oracle fed the GPU's own
     # d loss / d logits must give every encoder gradient to 1e-3 (north_star tolerance)
     _, _, x_o, (caches_o, h_o, s_o) = lucy_step.forward(p0, feats, L6, D512)   # pre-Adam weights

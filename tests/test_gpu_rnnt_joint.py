@@ -93,6 +93,7 @@ def test_fused_joint_vs_fp64(B, T, Umax, V, Tb, Ub):
     for got, ref, name in [(enc_p.grad, ge, "enc"), (pred_p.grad, gp, "pred"), (W.grad, gw, "W"),
                            (bias.grad, gb, "bias")]:
         assert torch.isfinite(got).all(), name
+        print(f"fused joint B={B} T={T} U={Umax} V={V} {name}: rel {rel(got, ref):.2e}")
         assert rel(got, ref) < 1e-2, (name, rel(got, ref))
 
 
@@ -219,3 +220,24 @@ def test_compute_loss_rnnt_fp32_keeps_fp32_logits(compact, monkeypatch):
     assert logits.dtype == torch.float32
     ref = crit.forward_logits(logits, tokens, in_lens, tgt_lens, blank_id=0, compact=compact)
     assert torch.equal(loss.detach(), ref.detach())
+
+
+def test_compute_loss_rnnt_fp16_autocast_keeps_materialised_joiner(monkeypatch):
+    """Under float16 autocast (the reference's own training dtype, train.py:516) the automatic
+    choice keeps the materialised joiner: the fused kernels' bf16 rounding of W and z is coarser
+    than float16's."""
+    B, T, Umax, V = 2, 30, 4, 64
+    torch.manual_seed(5)
+    joiner = sc().RNNTPredictorJoiner(V, 16, 64, V).to(DEV)
+    enc = torch.randn(B, T, V, device=DEV)
+    tokens = torch.randint(1, V, (B, Umax), device=DEV)
+
+    class Enc(torch.nn.Module):
+        def forward(self, feats, masks, states=None):
+            return feats, None
+    calls = _count_fused(monkeypatch)
+    with torch.autocast("cuda", dtype=torch.float16):
+        loss, _, _, _ = sc().compute_loss("rnnt", sc().RNNTLoss(blank=0), Enc(), enc, None, tokens,
+                                          [T, T], [Umax, Umax], 0, use_rnnt_joiner=joiner)
+    assert not calls, "float16 autocast must not take the bf16 fused joiner"
+    assert torch.isfinite(loss)
