@@ -46,6 +46,10 @@ def parse():
     ap.add_argument("--feat", type=int, default=80)
     ap.add_argument("--segments", type=int, default=4)
     ap.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16")
+    ap.add_argument("--output-head", choices=["split", "bf16"], default="split",
+                    help="CTC workload under bf16: 'split' = the output projection as one bf16 GEMM "
+                         "on split-precision operands with fp32 logits (ops.CTCHeadFn: gradients "
+                         "match the fp32 oracle); 'bf16' = plain bf16 operands and logits")
     ap.add_argument("--bucket-mb", type=float, default=8.0,
                     help="DDP gradient bucket size: ~one layer (7.3 MB fp32) per bucket, so each "
                          "layer's all-reduce overlaps the backward of the layers below it")
@@ -164,7 +168,12 @@ def build_workload(args, device):
             dict(mode="rnnt", joiner=joiner), conf
     conf["workload"] = (f"LucyRNN {args.layers}x{args.hidden} + CTC training step, stateful "
                         f"{args.segments}-segment carry")
-    return model, CTCLoss(blank=0, zero_infinity=True), list(model.parameters()), dict(mode="ctc"), conf
+    split = args.output_head == "split"
+    if args.dtype == "bf16":
+        conf["output_projection"] = ("bf16 GEMM on split-precision operands, fp32 logits" if split
+                                     else "bf16 operands and logits")
+    return model, CTCLoss(blank=0, zero_infinity=True, fused_head=split), list(model.parameters()), \
+        dict(mode="ctc"), conf
 
 
 def cpu_quota():
@@ -308,13 +317,53 @@ def spawn_ranks(n, cmd, port=None):
     return rc
 
 
+def count_gpus_without_hip(topo="/sys/class/kfd/kfd/topology/nodes"):
+    """GPUs this process may use, counted WITHOUT touching HIP: the parent forks and execs the
+    rank processes, and HIP initialised before a fork/exec is unusable in the children (and on
+    this pool an exec after GPU initialisation takes the machine down).  torch.cuda.device_count()
+    tries amdsmi but falls back to hipGetDeviceCount, so it is not used here.  Sources, in order:
+    the KFD topology in sysfs (nodes with SIMDs are GPUs), then amdsmi; a HIP_VISIBLE_DEVICES /
+    ROCR_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES list caps the count.  None when neither source
+    answers."""
+    n = None
+    try:
+        n = 0
+        for node in os.listdir(topo):
+            with open(os.path.join(topo, node, "properties")) as f:
+                props = dict(line.split()[:2] for line in f if len(line.split()) >= 2)
+            if int(props.get("simd_count", "0")) > 0:
+                n += 1
+    except (OSError, ValueError):
+        n = None
+    if not n:
+        try:
+            import amdsmi
+            amdsmi.amdsmi_init()
+            try:
+                n = len(amdsmi.amdsmi_get_processor_handles())
+            finally:
+                amdsmi.amdsmi_shut_down()
+        except Exception:
+            n = None
+    if n is None:
+        return None
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip()]))
+    return n
+
+
 def main():
     args = parse()
     if args.gpus < 1:
         sys.exit(f"bench.py: --gpus must be >= 1, got {args.gpus}")
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         # plain `python bench.py --gpus N`: start N ranks ourselves (torchrun's environment)
-        ndev = torch.cuda.device_count()   # counts devices without initialising HIP
+        ndev = count_gpus_without_hip()
+        if ndev is None:
+            sys.exit("bench.py: cannot count GPUs without initialising HIP (no KFD topology in "
+                     "sysfs, no amdsmi); launch the ranks with torchrun instead")
         if ndev < args.gpus:
             sys.exit(f"bench.py: --gpus {args.gpus} but only {ndev} GPU(s) visible")
         sys.exit(spawn_ranks(args.gpus, [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]))

@@ -98,6 +98,20 @@ int sc_lucy_scan_fwd(const void* gates, int gates_dtype, const float* gate_bias,
                      void* stream);
 
 /*
+ * sc_lucy_scan_fwd plus two 16-bit planes with out's strides: out_dup (the rounded h again) and
+ * out_lo (h minus its rounding, rounded).  With out, out_dup, out_lo as the K blocks of one
+ * [B*T][3D] operand, a bf16 GEMM against [W_hi | W_lo | W_hi] gives x.W with the error of an fp32
+ * GEMM (the output projection before the CTC lattice, lucyrnn_triton.py:150 / model.py:70).
+ * gates_dtype must be bf16 or f16.
+ */
+int sc_lucy_scan_fwd_split(const void* gates, int gates_dtype, const float* gate_bias,
+                           const float* h0, const float* s0, void* out, void* out_dup, void* out_lo,
+                           float* s_out, float* h_out, int B, int T, int D,
+                           int64_t stride_g_bt, int64_t stride_g_td, int64_t stride_g_cd,
+                           int64_t stride_g_cb, int64_t stride_o_bt, int64_t stride_o_bd,
+                           float* ckpt, void* stream);
+
+/*
  * Backward scan.  Inputs: the forward's gates and ckpt, dout = dL/d out (same dtype as gates,
  * strides stride_d_bt/stride_d_bd), ds_last = dL/d s_out (fp32 [B,D], may be NULL = zero).
  * Outputs: dgates (gates_dtype, laid out like gates with strides stride_dg_*), dh0, ds0 (fp32
@@ -410,10 +424,6 @@ int sc_fbank(const float* audio, int B, int64_t n_samples, int64_t audio_stride,
 
 /* 1 if the mLSTM kernels are compiled for this compute dtype (bf16/f16) and head dims. */
 int sc_mlstm_supported(int dtype, int DQ, int DV);
-
-/* Floats of BH * (T/64 + 1) * DQ * DV (a chunk-boundary state buffer; kept for callers that
- * size one, e.g. a per-chunk state dump). */
-int64_t sc_mlstm_state_numel(int BH, int T, int DQ, int DV);
 
 /* Elements of the forward's chunk-start state image states_C: BH * (T/64) * DQ * DV. */
 int64_t sc_mlstm_chunk_state_numel(int BH, int T, int DQ, int DV);

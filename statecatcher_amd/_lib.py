@@ -18,7 +18,7 @@ _DTYPE = {torch.float32: SC_F32, torch.bfloat16: SC_BF16, torch.float16: SC_F16}
 
 _c = ctypes
 _i32, _i64, _vp, _fp = _c.c_int, _c.c_int64, _c.c_void_p, _c.c_void_p
-ABI_VERSION = 8  # include/statecatcher.h; bumped on any signature change
+ABI_VERSION = 9  # include/statecatcher.h; bumped on any signature change
 
 _SIGS = {
     "sc_abi_version": (_i32, []),
@@ -30,6 +30,8 @@ _SIGS = {
     "sc_lucy_scan_ckpt_numel": (_i64, [_i32, _i32, _i32]),
     "sc_lucy_scan_fwd": (_i32, [_vp, _i32, _fp, _fp, _fp, _vp, _fp, _fp, _i32, _i32, _i32,
                                _i64, _i64, _i64, _i64, _i64, _i64, _fp, _vp]),
+    "sc_lucy_scan_fwd_split": (_i32, [_vp, _i32, _fp, _fp, _fp, _vp, _vp, _vp, _fp, _fp, _i32, _i32,
+                                     _i32, _i64, _i64, _i64, _i64, _i64, _i64, _fp, _vp]),
     "sc_lucy_scan_bwd": (_i32, [_vp, _i32, _fp, _fp, _vp, _fp, _vp, _fp, _fp, _fp, _i32, _i32, _i32,
                                _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64,
                                _vp]),
@@ -58,7 +60,6 @@ _SIGS = {
     "sc_lucy_step_cell": (_i32, [_i32, _vp, _i32, _i64, _vp, _vp, _fp, _fp, _fp, _fp, _c.c_float,
                                  _fp, _fp, _vp, _fp, _i32, _i32, _vp]),
     "sc_mlstm_supported": (_i32, [_i32, _i32, _i32]),
-    "sc_mlstm_state_numel": (_i64, [_i32, _i32, _i32, _i32]),
     "sc_mlstm_chunk_state_numel": (_i64, [_i32, _i32, _i32, _i32]),
     "sc_mlstm_fwd": (_i32, [_vp, _vp, _vp, _i32, _fp, _fp, _fp, _fp, _fp, _i32, _i32, _i32, _i32,
                            _c.c_float, _vp, _vp, _fp, _fp, _fp, _fp, _fp, _vp, _vp]),

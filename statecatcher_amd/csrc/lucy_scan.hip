@@ -85,6 +85,11 @@ struct ScanFwdArgs {
   float* ckpt;
   int B, T, D, nsc;
   int64_t g_bt, g_td, g_cd, g_cb, o_bt, o_bd;
+  // optional split-precision planes (16-bit out only, same strides as out): out_dup = out again,
+  // out_lo = h - out in the same 16-bit type.  [out | out_dup | out_lo] against [Wh | Wl | Wh]
+  // is one bf16 GEMM with the error of an fp32 one (sc_lucy_scan_fwd_split)
+  void* out_dup;
+  void* out_lo;
 };
 
 struct ScanBwdArgs {
@@ -327,7 +332,7 @@ __device__ __forceinline__ float compose_prefix_sw(const float2 (*agg)[64], int 
 
 // ------------------------------------------------------------------------ forward ----------
 // FD: LDS slots per wave (fetch depth), ring by super-chunk index.
-template <int DT, int NW, int LC, int PW, int FD>
+template <int DT, int NW, int LC, int PW, int FD, bool SPLIT = false>
 __global__ void __launch_bounds__(NW * 64)
 lucy_scan_fwd_kernel(ScanFwdArgs a) {
   static_assert(NW * LC == kChunk, "super-chunk must be 64 steps");
@@ -358,6 +363,8 @@ lucy_scan_fwd_kernel(ScanFwdArgs a) {
 
   const T* gsrc = (const T*)a.gates + (int64_t)b * a.g_bt + (int64_t)blk * a.g_cb;
   const Buf<T> obuf((T*)a.out + (int64_t)b * a.o_bt);
+  const Buf<T> dbuf(SPLIT ? (T*)a.out_dup + (int64_t)b * a.o_bt : (T*)a.out);
+  const Buf<T> lbuf(SPLIT ? (T*)a.out_lo + (int64_t)b * a.o_bt : (T*)a.out);
   const uint32_t vo = (uint32_t)d * sizeof(T);
   const uint32_t otd = (uint32_t)(a.o_bd * sizeof(T));
   if (w == 0) {
@@ -495,7 +502,14 @@ lucy_scan_fwd_kernel(ScanFwdArgs a) {
     }
 #pragma unroll
     for (int j = 0; j < LC; ++j)
-      if (FULL || (dok && t0 + j < a.T)) obuf.st(E::st(hs[j]), vo, (uint32_t)(t0 + j) * otd);
+      if (FULL || (dok && t0 + j < a.T)) {
+        const T hi = E::st(hs[j]);
+        obuf.st(hi, vo, (uint32_t)(t0 + j) * otd);
+        if constexpr (SPLIT) {
+          dbuf.st(hi, vo, (uint32_t)(t0 + j) * otd);
+          lbuf.st(E::st(hs[j] - E::ld(hi)), vo, (uint32_t)(t0 + j) * otd);
+        }
+      }
   };
   const bool blk_full = (blk + 1) * 64 <= a.D;
   for (int k = 0; k < a.nsc; ++k) {
@@ -921,11 +935,11 @@ static bool set_lds_limit(K kernel, size_t bytes) {
                              (int)bytes) == hipSuccess;
 }
 
-template <int DT, int PW>
+template <int DT, int PW, bool SPLIT = false>
 static void launch_fwd(const ScanFwdArgs& a, hipStream_t st) {
   using T = typename Elem<DT>::T;
   constexpr int FD = (SC_FWD_FD >= 2 && LdsElem<T, PW>::BYTES == 2) ? 2 : 1;   // 2 x 56 KiB fit
-  auto kern = lucy_scan_fwd_kernel<DT, kNW, kLC, PW, FD>;
+  auto kern = lucy_scan_fwd_kernel<DT, kNW, kLC, PW, FD, SPLIT>;
   const size_t lds = (size_t)FD * kNW * kLC * 7 * 64 * LdsElem<T, PW>::BYTES;
   static const bool lds_ok = set_lds_limit(kern, lds);
   (void)lds_ok;
@@ -958,10 +972,17 @@ static bool wide_pieces(const void* p, int esize, int D, std::initializer_list<i
 
 template <int DT>
 static void dispatch_fwd(const ScanFwdArgs& a, hipStream_t st) {
-  if (wide_pieces(a.gates, sizeof(typename Elem<DT>::T), a.D, {a.g_bt, a.g_td, a.g_cd, a.g_cb}))
-    launch_fwd<DT, 16>(a, st);
-  else
-    launch_fwd<DT, (int)sizeof(typename Elem<DT>::T)>(a, st);
+  constexpr int es = (int)sizeof(typename Elem<DT>::T);
+  const bool wide = wide_pieces(a.gates, es, a.D, {a.g_bt, a.g_td, a.g_cd, a.g_cb});
+  if constexpr (es == 2) {
+    if (a.out_lo) {
+      if (wide) launch_fwd<DT, 16, true>(a, st);
+      else launch_fwd<DT, es, true>(a, st);
+      return;
+    }
+  }
+  if (wide) launch_fwd<DT, 16>(a, st);
+  else launch_fwd<DT, es>(a, st);
 }
 
 template <int DT>
@@ -991,14 +1012,11 @@ extern "C" int64_t sc_lucy_scan_ckpt_numel(int B, int T, int D) {
 
 static int check_dtype(int dt) { return dt == SC_F32 || dt == SC_BF16 || dt == SC_F16; }
 
-extern "C" int sc_lucy_scan_fwd(const void* gates, int gates_dtype, const float* gate_bias,
-                                const float* h0,
-                                const float* s0, void* out, float* s_out, float* h_out, int B,
-                                int T, int D,
-                                int64_t stride_g_bt, int64_t stride_g_td, int64_t stride_g_cd,
-                                int64_t stride_g_cb, int64_t stride_o_bt, int64_t stride_o_bd,
-                                float* ckpt, void* stream) {
-  clear_error();
+static int scan_fwd(const void* gates, int gates_dtype, const float* gate_bias, const float* h0,
+                    const float* s0, void* out, float* s_out, float* h_out, int B, int T, int D,
+                    int64_t stride_g_bt, int64_t stride_g_td, int64_t stride_g_cd,
+                    int64_t stride_g_cb, int64_t stride_o_bt, int64_t stride_o_bd, float* ckpt,
+                    void* out_dup, void* out_lo, void* stream) {
   SC_REQUIRE(check_dtype(gates_dtype), "sc_lucy_scan_fwd: unsupported gates dtype %d", gates_dtype);
   SC_REQUIRE(B >= 0 && T >= 0 && D >= 0, "sc_lucy_scan_fwd: negative shape B=%d T=%d D=%d", B, T, D);
   SC_REQUIRE(B <= 65535, "sc_lucy_scan_fwd: B=%d exceeds grid limit 65535", B);
@@ -1011,7 +1029,8 @@ extern "C" int sc_lucy_scan_fwd(const void* gates, int gates_dtype, const float*
   SC_REQUIRE((int64_t)T * stride_o_bd * 4 < (1ll << 31),
              "sc_lucy_scan_fwd: one batch row of out spans >= 2 GiB");
   ScanFwdArgs a{gates, gate_bias, h0, s0, out, s_out, h_out, ckpt, B, T, D, (T + kChunk - 1) / kChunk,
-                stride_g_bt, stride_g_td, stride_g_cd, stride_g_cb, stride_o_bt, stride_o_bd};
+                stride_g_bt, stride_g_td, stride_g_cd, stride_g_cb, stride_o_bt, stride_o_bd,
+                out_dup, out_lo};
   hipStream_t st = (hipStream_t)stream;
   switch (gates_dtype) {
     case SC_F32: dispatch_fwd<SC_F32>(a, st); break;
@@ -1019,6 +1038,35 @@ extern "C" int sc_lucy_scan_fwd(const void* gates, int gates_dtype, const float*
     default: dispatch_fwd<SC_F16>(a, st); break;
   }
   return launch_status("sc_lucy_scan_fwd");
+}
+
+extern "C" int sc_lucy_scan_fwd(const void* gates, int gates_dtype, const float* gate_bias,
+                                const float* h0,
+                                const float* s0, void* out, float* s_out, float* h_out, int B,
+                                int T, int D,
+                                int64_t stride_g_bt, int64_t stride_g_td, int64_t stride_g_cd,
+                                int64_t stride_g_cb, int64_t stride_o_bt, int64_t stride_o_bd,
+                                float* ckpt, void* stream) {
+  clear_error();
+  return scan_fwd(gates, gates_dtype, gate_bias, h0, s0, out, s_out, h_out, B, T, D, stride_g_bt,
+                  stride_g_td, stride_g_cd, stride_g_cb, stride_o_bt, stride_o_bd, ckpt, nullptr,
+                  nullptr, stream);
+}
+
+extern "C" int sc_lucy_scan_fwd_split(const void* gates, int gates_dtype, const float* gate_bias,
+                                      const float* h0, const float* s0, void* out, void* out_dup,
+                                      void* out_lo, float* s_out, float* h_out, int B, int T, int D,
+                                      int64_t stride_g_bt, int64_t stride_g_td,
+                                      int64_t stride_g_cd, int64_t stride_g_cb,
+                                      int64_t stride_o_bt, int64_t stride_o_bd, float* ckpt,
+                                      void* stream) {
+  clear_error();
+  SC_REQUIRE(gates_dtype == SC_BF16 || gates_dtype == SC_F16,
+             "sc_lucy_scan_fwd_split: the split planes need a 16-bit out (dtype %d)", gates_dtype);
+  SC_REQUIRE(T == 0 || (out_dup && out_lo), "sc_lucy_scan_fwd_split: null out_dup/out_lo");
+  return scan_fwd(gates, gates_dtype, gate_bias, h0, s0, out, s_out, h_out, B, T, D, stride_g_bt,
+                  stride_g_td, stride_g_cd, stride_g_cb, stride_o_bt, stride_o_bd, ckpt, out_dup,
+                  out_lo, stream);
 }
 
 extern "C" int sc_lucy_scan_bwd(const void* gates, int gates_dtype, const float* gate_bias,

@@ -111,8 +111,9 @@ struct MArgs {
   const void* dh;   // [BH][T][DV]
   const float* dcT;  // [BH][DQ][DV] or NULL (gradient w.r.t. the final state)
   const float* dnT;  // [BH][DQ] or NULL
-  float* dCs;       // [BH][nc+1][DQ][DV]: gradient w.r.t. C~_k (dCs[0] = dC0)
-  float* dns;       // [BH][nc+1][DQ]
+  float* dCs;       // [BH][DQ][DV]: gradient w.r.t. the initial state C~_0 (every later dC~_k
+                    // stays on chip)
+  float* dns;       // [BH][DQ]:     gradient w.r.t. n~_0
   void* dq;         // [BH][T][DQ]
   void* dk;
   void* dv;         // [BH][T][DV]
@@ -1442,11 +1443,6 @@ using namespace sc;
 
 extern "C" int sc_mlstm_supported(int dtype, int DQ, int DV) {
   return (dtype == SC_BF16 || dtype == SC_F16) && dims_supported(DQ, DV);
-}
-
-extern "C" int64_t sc_mlstm_state_numel(int BH, int T, int DQ, int DV) {
-  if (BH <= 0 || T <= 0 || DQ <= 0 || DV <= 0) return 0;
-  return (int64_t)BH * (T / kL + 1) * DQ * DV;
 }
 
 extern "C" int64_t sc_mlstm_chunk_state_numel(int BH, int T, int DQ, int DV) {

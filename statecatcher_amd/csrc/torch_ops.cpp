@@ -476,8 +476,21 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> mlstm_bwd_hip
   TORCH_CHECK(dh.sizes() == hc.sizes() && hc.sizes() == v.sizes(),
               "statecatcher::mlstm_bwd: h / dh must be [B,NH,T,DV]");
   const int64_t BH = d.B * d.NH, nc = d.T / 64;
-  TORCH_CHECK(cs.numel() == BH * nc * d.DQ * d.DV && cs.scalar_type() == q.scalar_type(),
+  TORCH_CHECK(cs.numel() == BH * nc * d.DQ * d.DV && cs.scalar_type() == q.scalar_type() &&
+                  cs.is_contiguous() && cs.device() == q.device(),
               "statecatcher::mlstm_bwd: c_states is not mlstm_fwd's");
+  // the other state images go to the kernel as raw pointers: shape, dtype, layout and device
+  // exactly as mlstm_fwd returns them
+  auto f32_state = [&](const Tensor& t, at::IntArrayRef shape, const char* name) {
+    TORCH_CHECK(t.sizes() == shape && t.scalar_type() == at::kFloat && t.is_contiguous() &&
+                    t.device() == q.device(),
+                "statecatcher::mlstm_bwd: ", name, " must be contiguous fp32 ", shape,
+                " on the device of q (mlstm_fwd's output), got ", t.sizes(), " ", t.scalar_type());
+  };
+  f32_state(ns, {BH, nc + 1, d.DQ}, "n_states");
+  f32_state(ms, {BH, nc + 1}, "m_states");
+  f32_state(mrow, {BH, d.T}, "m_rows");
+  f32_state(den, {BH, d.T}, "den_rows");
   optional<Tensor> dcc, dnc;
   if (dcT && dcT->defined()) dcc = f32c(*dcT);
   if (dnT && dnT->defined()) dnc = f32c(*dnT);
@@ -708,8 +721,9 @@ Tensor clip_adam_hip(at::TensorList params, at::TensorList grads, at::TensorList
   for (size_t i = 0; i < nt; ++i) {
     for (const Tensor* x : {&params[i], &grads[i], &exp_avgs[i], &exp_avg_sqs[i]})
       TORCH_CHECK(x->is_cuda() && x->scalar_type() == at::kFloat && x->is_contiguous() &&
-                      x->numel() == params[i].numel(),
-                  "statecatcher::clip_adam_: fp32 contiguous device tensors of equal size");
+                      x->numel() == params[i].numel() && x->device() == params[0].device(),
+                  "statecatcher::clip_adam_: fp32 contiguous tensors of equal size, all on the "
+                  "device of params[0]");
     t[i] = sc_adam_tensor{params[i].data_ptr<float>(), grads[i].data_ptr<float>(),
                           exp_avgs[i].data_ptr<float>(), exp_avg_sqs[i].data_ptr<float>(),
                           params[i].numel()};

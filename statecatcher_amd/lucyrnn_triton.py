@@ -54,15 +54,15 @@ class _LinearFn(torch.autograd.Function):
 
 
 # compute_loss's request to hand the output projection to the loss (ops.CTCHeadFn): set, the next
-# LucyRNNtriton forward on this thread that can fuse stores (hidden, output_proj, images) here
-# and returns DEFERRED_LOGITS in place of the logits
+# LucyRNNtriton forward on this thread that can fuse stores (hidden, output_proj, images, the
+# last scan's split-precision buffer or None) here and returns DEFERRED_LOGITS for the logits
 _HEAD = threading.local()
 DEFERRED_LOGITS = object()
 
 
 class defer_output_head:
-    """with defer_output_head() as h: ... model(...) ...; h.taken is (x, output_proj, images) when
-    the encoder deferred its output projection, else None."""
+    """with defer_output_head() as h: ... model(...) ...; h.taken is (x, output_proj, images,
+    wide) when the encoder deferred its output projection, else None."""
 
     def __enter__(self):
         self.taken = None
@@ -154,11 +154,12 @@ class LucyRNNCellTriton(nn.Module):
         out, s_out, _ = self.forward_with_h(x, h0, s0)
         return out, s_out
 
-    def forward_with_h(self, x, h0, s0, imgs=None):
+    def forward_with_h(self, x, h0, s0, imgs=None, split_sink=None):
         """(out, s_out, h_last): h_last = out[:, -1] in fp32, unrounded by a 16-bit out (the
         state LucyRNNtriton carries).  Projection GEMM + scan are one autograd node: the scan
         backward hands the bias gradient back from registers, the weight gradient runs on the
-        MFMA split-L kernel.  imgs: this layer's entry of ops.weight_images (bf16 only)."""
+        MFMA split-L kernel.  imgs: this layer's entry of ops.weight_images (bf16 only);
+        split_sink: ops.LucyCellFn's (the scan's split-precision output planes)."""
         w, b = self.linear.weight, self.linear.bias
         if x.is_cuda and torch.is_autocast_enabled("cuda"):
             cdt = torch.get_autocast_dtype("cuda")
@@ -169,7 +170,7 @@ class LucyRNNCellTriton(nn.Module):
         if imgs is not None and cdt != torch.bfloat16:
             imgs = None
         with torch.autocast("cuda", enabled=False):
-            return lucy_cell(x, w, b, h0, s0, cdt, imgs)
+            return lucy_cell(x, w, b, h0, s0, cdt, imgs, split_sink)
 
 
 class LucyRNNtriton(nn.Module):
@@ -218,6 +219,11 @@ class LucyRNNtriton(nn.Module):
             h, s = hidden_states
 
         cell_imgs, out_imgs = self._weight_images(x)
+        req = getattr(_HEAD, "req", None)
+        if req is not None and not (out_imgs is not None and out_imgs[1] is not None
+                                    and self.num_tracks == 1):
+            req = None
+        sink = [] if req is not None else None
         track_outputs, final_h, final_s = [], [], []
         for t in range(self.num_tracks):
             x_t = x
@@ -228,7 +234,8 @@ class LucyRNNtriton(nn.Module):
                 # h carry = out[:, -1] (lucyrnn_triton.py:135), taken in fp32 from the scan and
                 # contiguous
                 x_t, s_t[l], h_t[l] = layer.forward_with_h(
-                    x_t, h_t[l], s_t[l], cell_imgs.get((t, l)) if cell_imgs else None)
+                    x_t, h_t[l], s_t[l], cell_imgs.get((t, l)) if cell_imgs else None,
+                    sink if l == len(layers) - 1 else None)
                 if l < len(norms):
                     x_t = norms[l](x_t)
             track_outputs.append(x_t)
@@ -239,9 +246,9 @@ class LucyRNNtriton(nn.Module):
             x = track_outputs[0]
         else:
             x = self.merge_proj(torch.cat(track_outputs, dim=-1))
-        req = getattr(_HEAD, "req", None)
-        if req is not None and out_imgs is not None and out_imgs[1] is not None:
-            req.taken = (x, self.output_proj, out_imgs)
+        if req is not None:
+            # the last layer's scan wrote [x_hi | x_hi | x_lo] (sink) when its gates were bf16
+            req.taken = (x, self.output_proj, out_imgs, sink[0] if sink else None)
             _HEAD.req = None
             logits = DEFERRED_LOGITS
         else:

@@ -52,7 +52,7 @@ class CTCLoss(nn.Module):
     log_softmax that model.py:70 applies first and skips the transpose.
     """
 
-    def __init__(self, blank=0, reduction="mean", zero_infinity=True, fused_head=False):
+    def __init__(self, blank=0, reduction="mean", zero_infinity=True, fused_head=True):
         super().__init__()
         self.blank = blank
         self.reduction = reduction
@@ -93,10 +93,10 @@ def compute_loss(mode: str, criterion: nn.Module, model: nn.Module, feats: torch
         with defer_output_head() as head:
             enc_out, output_state = model(feats, masks, input_state)
         if enc_out is DEFERRED_LOGITS:
-            x, proj, imgs = head.taken
+            x, proj, imgs, wide = head.taken
             with torch.autocast("cuda", enabled=False):
                 loss, enc_out = ctc_head_loss(x, proj.weight, proj.bias, imgs, tokens, in_lens,
-                                              tgt_lens, blank=criterion.blank)
+                                              tgt_lens, blank=criterion.blank, wide=wide)
             return loss, output_state, enc_out, output_state
     else:
         enc_out, output_state = model(feats, masks, input_state)

@@ -51,7 +51,9 @@ def gate_layout(gates):
                      f"shape {tuple(gates.shape)} strides {gates.stride()}")
 
 
-def _scan_fwd(gates, h0, s0, need_ckpt, bias=None, want_h=False):
+def _scan_fwd(gates, h0, s0, need_ckpt, bias=None, want_h=False, split=False):
+    """split (16-bit gates): out is the first D columns of a [B,T,3D] buffer whose other two
+    blocks are out again and h - out (sc_lucy_scan_fwd_split), returned as the last element."""
     require_device(gates, h0, s0)
     if gates.dim() == 4 and gates.shape[2] == 7 and gates.stride(3) != 1:
         gates = gates.contiguous()
@@ -61,7 +63,9 @@ def _scan_fwd(gates, h0, s0, need_ckpt, bias=None, want_h=False):
     # the reference reads h0/s0 as contiguous even when handed a strided view
     h0c = h0.detach().to(torch.float32).contiguous()
     s0c = s0.detach().to(torch.float32).contiguous()
-    out = torch.empty(B, T, D, dtype=gates.dtype, device=gates.device)
+    split = split and gates.dtype in (torch.bfloat16, torch.float16)
+    wide = torch.empty(B, T, 3 * D, dtype=gates.dtype, device=gates.device) if split else None
+    out = wide[..., :D] if split else torch.empty(B, T, D, dtype=gates.dtype, device=gates.device)
     s_out = torch.empty(B, D, dtype=torch.float32, device=gates.device)
     h_out = torch.empty(B, D, dtype=torch.float32, device=gates.device) if want_h else None
     lib = _lib.load()
@@ -72,11 +76,19 @@ def _scan_fwd(gates, h0, s0, need_ckpt, bias=None, want_h=False):
     e = gates.element_size()
     nbytes = B * T * D * 8 * e + (ckpt.numel() * 4 if ckpt is not None else 0) + 4 * B * D * 4
     with _timed("lucy_scan_fwd", gates, nbytes):
-        rc = lib.sc_lucy_scan_fwd(ptr(gates), dtype_code(gates), ptr(bias), ptr(h0c), ptr(s0c),
-                                  ptr(out), ptr(s_out), ptr(h_out), B, T, D, *gs, out.stride(0),
-                                  out.stride(1), ptr(ckpt), stream_of(gates))
+        if split:
+            rc = lib.sc_lucy_scan_fwd_split(ptr(gates), dtype_code(gates), ptr(bias), ptr(h0c),
+                                            ptr(s0c), ptr(out), ptr(wide[..., D:2 * D]),
+                                            ptr(wide[..., 2 * D:]), ptr(s_out), ptr(h_out), B, T, D,
+                                            *gs, out.stride(0), out.stride(1), ptr(ckpt),
+                                            stream_of(gates))
+        else:
+            rc = lib.sc_lucy_scan_fwd(ptr(gates), dtype_code(gates), ptr(bias), ptr(h0c), ptr(s0c),
+                                      ptr(out), ptr(s_out), ptr(h_out), B, T, D, *gs, out.stride(0),
+                                      out.stride(1), ptr(ckpt), stream_of(gates))
     check(rc, "sc_lucy_scan_fwd")
-    return (gates, out, s_out, ckpt, h_out) if want_h else (gates, out, s_out, ckpt)
+    res = (gates, out, s_out, ckpt, h_out) if want_h else (gates, out, s_out, ckpt)
+    return res + (wide,) if split else res
 
 
 def _scan_bwd(gates, ckpt, dout, ds_last, want_dbias, bias=None):
@@ -419,7 +431,10 @@ class LucyCellFn(torch.autograd.Function):
     """
 
     @staticmethod
-    def forward(ctx, x2d, w, b, h0, s0, B, T, cdt, imgs=None):
+    def forward(ctx, x2d, w, b, h0, s0, B, T, cdt, imgs=None, split_sink=None):
+        """split_sink: a list; when given (bf16), the scan also writes the split-precision planes
+        of its output (sc_lucy_scan_fwd_split) and the [B,T,3D] buffer is appended to it (out is
+        its first D columns): the input of CTCHeadFn's one-GEMM fp32-accurate projection."""
         ctx.set_materialize_grads(False)   # unused state outputs: no zero-filled gradients
         D = w.shape[0] // 7
         blocked = D % 64 == 0
@@ -453,7 +468,10 @@ class LucyCellFn(torch.autograd.Function):
             gates = proj_fwd(xg, wg)
         gates = gates.view(B, T, D // 64, 7, 64) if blocked else gates.view(B, T, 7, D)
         need = any(ctx.needs_input_grad)
-        gates, out, s_out, ckpt, h_out = _scan_fwd(gates, h0, s0, need, bias, want_h=True)
+        res = _scan_fwd(gates, h0, s0, need, bias, want_h=True, split=split_sink is not None)
+        gates, out, s_out, ckpt, h_out = res[:5]
+        if len(res) > 5:
+            split_sink.append(res[5])
         if need:
             ctx.save_for_backward(xc, wc, wt, gates, ckpt, bias)
             ctx.dtypes = (x2d.dtype, w.dtype, h0.dtype, s0.dtype)
@@ -504,17 +522,17 @@ class LucyCellFn(torch.autograd.Function):
                 dw = wgrad_splitk(dg2, xc, blocked_d=bd)
             dw = dw.to(wdt)
         db = colsum(dbias.view(dbias.shape[0], -1)).to(wdt) if dbias is not None else None
-        return dx, dw, db, dh0.to(hdt), ds0.to(sdt), None, None, None, None
+        return dx, dw, db, dh0.to(hdt), ds0.to(sdt), None, None, None, None, None
 
 
-def lucy_cell(x, w, b, h0, s0, cdt=None, imgs=None):
+def lucy_cell(x, w, b, h0, s0, cdt=None, imgs=None, split_sink=None):
     """x [B,T,Din] -> (out [B,T,D], s_last [B,D] fp32, h_last [B,D] fp32) through projection
     + scan.  imgs: the (forward weight, transposed weight) images of cell_image_spec, or None
-    (the cell casts w itself)."""
+    (the cell casts w itself).  split_sink: see LucyCellFn.forward."""
     B, T, Din = x.shape
     if cdt is None:
         cdt = torch.promote_types(x.dtype, w.dtype)
-    return LucyCellFn.apply(x.reshape(B * T, Din), w, b, h0, s0, B, T, cdt, imgs)
+    return LucyCellFn.apply(x.reshape(B * T, Din), w, b, h0, s0, B, T, cdt, imgs, split_sink)
 
 
 # ----------------------------------------------------------------------------- LayerNorm -----
@@ -698,6 +716,26 @@ def _logits_fp32(x2, wc, b):
     return torch.addmm(b, x2, wc.t(), out_dtype=torch.float32)
 
 
+_SPLIT_W = WeakIdKeyDictionary()
+
+
+def split_weight_image(w):
+    """[W_hi | W_lo | W_hi] bf16 [V, 3K] of an fp32 w [V, K] (W_hi = bf16(w), W_lo = bf16(w -
+    W_hi)): against [x_hi | x_hi | x_lo] one bf16 GEMM gives x_hi W_hi + x_hi W_lo + x_lo W_hi,
+    i.e. x.W to ~2^-16 relative.  Cached per weight version (rebuilt once per optimizer step)."""
+    key = (w._version, w.data_ptr(), tuple(w.shape))
+    hit = _SPLIT_W.get(w)
+    if hit is not None and hit[0] == key:
+        return hit[1]
+    with torch.no_grad():
+        wd = w.detach()
+        hi = wd.to(torch.bfloat16)
+        lo = (wd - hi.float()).to(torch.bfloat16)
+        img = torch.cat([hi, lo, hi], 1)
+    _SPLIT_W[w] = (key, img)
+    return img
+
+
 class CTCHeadFn(torch.autograd.Function):
     """output_proj (LinearSafe, lucyrnn_triton.py:107-109, :150) + log_softmax + nn.CTCLoss(
     reduction='mean', zero_infinity=True) (model.py:68-71, train.py:142) as ONE node, for bf16
@@ -712,12 +750,15 @@ class CTCHeadFn(torch.autograd.Function):
     gradient reaching it from elsewhere is added before the projection backward."""
 
     @staticmethod
-    def forward(ctx, x, w, b, wc, wt, targets, in_lens, tgt_lens, blank):
+    def forward(ctx, x, w, b, wc, wt, targets, in_lens, tgt_lens, blank, wide=None):
         ctx.set_materialize_grads(False)
         B, T, K = x.shape
         V = w.shape[0]
         x2 = x.reshape(-1, K)
-        logits = _logits_fp32(x2, wc, b).view(B, T, V)
+        if wide is not None:   # [x_hi | x_hi | x_lo] from the scan: fp32-accurate logits
+            logits = _logits_fp32(wide.view(-1, 3 * K), split_weight_image(w), b).view(B, T, V)
+        else:
+            logits = _logits_fp32(x2, wc, b).view(B, T, V)
         loss = CTCMeanFn.forward(ctx, logits, targets, in_lens, tgt_lens, blank, True)
         ctx.head = (x2, wt, x.shape, x.dtype)
         return loss, logits
@@ -745,7 +786,7 @@ class CTCHeadFn(torch.autograd.Function):
         dx = torch.matmul(dy2, wt.t()).view(xshape).to(xdt) if ctx.needs_input_grad[0] else None
         dw = wgrad_splitk(dy2, x2) if ctx.needs_input_grad[1] else None
         db = colsum(dy2) if ctx.needs_input_grad[2] else None
-        return dx, dw, db, None, None, None, None, None, None
+        return dx, dw, db, None, None, None, None, None, None, None
 
 
 def ctc_head_supported(x, w, b, imgs):
@@ -756,12 +797,20 @@ def ctc_head_supported(x, w, b, imgs):
             and b.dtype == torch.float32)
 
 
-def ctc_head_loss(x, w, b, imgs, targets, in_lens, tgt_lens, blank=0):
+def ctc_head_loss(x, w, b, imgs, targets, in_lens, tgt_lens, blank=0, wide=None):
     """(loss, fp32 logits) of CTCHeadFn: x [B,T,D] bf16 hidden, w [V,D] / b [V] the fp32
-    output_proj parameters, imgs their (W, W^T) bf16 images."""
+    output_proj parameters, imgs their (W, W^T) bf16 images; wide: the scan's split-precision
+    [B,T,3D] buffer whose first D columns are x (LucyCellFn split_sink), or None."""
     dev = x.device
-    return CTCHeadFn.apply(x.contiguous(), w, b, imgs[0], imgs[1], targets.to(dev),
-                           _as_len_tensor(in_lens, dev), _as_len_tensor(tgt_lens, dev), int(blank))
+    if wide is not None and not (wide.is_contiguous() and wide.shape[:2] == x.shape[:2]
+                                 and wide.shape[2] == 3 * x.shape[2]
+                                 and x.data_ptr() == wide.data_ptr()):
+        raise ValueError("ctc_head_loss: wide must be the [B,T,3D] buffer x is the head of")
+    if wide is None:
+        x = x.contiguous()
+    return CTCHeadFn.apply(x, w, b, imgs[0], imgs[1], targets.to(dev),
+                           _as_len_tensor(in_lens, dev), _as_len_tensor(tgt_lens, dev), int(blank),
+                           wide)
 
 
 def ctc_nll(x, targets, in_lens, tgt_lens, blank=0, is_logits=True):

@@ -215,9 +215,12 @@ class mLSTMLayer(nn.Module):
             q, k, v, o, ig, fg = a.split([m.weight.shape[0] for m in self._mods()], -1)
         else:
             q, k, v, o, ig, fg = self.projections(x)
-        # the cell runs in autocast_kernel_dtype (the reference passes float16, model.py:227):
-        # q, k, v are cast to it as the xlstm fork's kernels cast their inputs
-        cell_dt = kdt if x.is_cuda and kdt in (torch.bfloat16, torch.float16) else q.dtype
+        # under autocast the cell runs in autocast_kernel_dtype (the reference passes float16,
+        # model.py:227): q, k, v are cast to it as the xlstm fork's kernels cast their inputs.
+        # Without autocast the dtype is the activations' own, as transformers' native chunkwise
+        # cell (modeling_xlstm.py:323) ignores autocast_kernel_dtype
+        cell_dt = (kdt if x.is_cuda and torch.is_autocast_enabled("cuda")
+                   and kdt in (torch.bfloat16, torch.float16) else q.dtype)
         q = q.reshape(B, T, NH, -1).transpose(1, 2).to(cell_dt)
         k = k.reshape(B, T, NH, -1).transpose(1, 2).to(cell_dt)
         v = v.reshape(B, T, NH, -1).transpose(1, 2).to(cell_dt)
@@ -227,8 +230,8 @@ class mLSTMLayer(nn.Module):
         h, new_state = mlstm_chunkwise(q, k, v, ig, fg, c0, n0, m0, return_last_states=True,
                                        eps=self.cfg.eps)
         mh = self.multihead_norm
-        if h.dtype != o.dtype and o.dtype == torch.bfloat16:
-            h = h.to(o.dtype)   # fp16 cell output back to the step's bf16 activations
+        if h.dtype != o.dtype:
+            h = h.to(o.dtype)   # the cell's output back to the step's activation dtype
         if (mh.bias is None and mh.force_float32_reductions and o.dtype == torch.bfloat16
                 and ops.gated_head_norm_supported(h)):
             # sigmoid(o) * MultiHeadLayerNorm(h) in one HIP pass on the cell's [B,NH,T,DH] layout

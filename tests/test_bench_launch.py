@@ -45,3 +45,36 @@ def test_bad_gpus_exits_nonzero(argv, env):
                        capture_output=True, text=True, timeout=120)
     assert p.returncode != 0
     assert "--gpus" in p.stderr
+
+
+def _fake_topology(root, simds):
+    for i, s in enumerate(simds):
+        d = root / str(i)
+        d.mkdir(parents=True)
+        (d / "properties").write_text(f"cpu_cores_count {0 if s else 64}\nsimd_count {s}\n"
+                                      f"gfx_target_version {90500 if s else 0}\n")
+
+
+def test_count_gpus_from_kfd_topology(tmp_path, monkeypatch):
+    """The parent counts GPUs from the KFD topology (CPU nodes have no SIMDs), capped by a
+    visible-devices list, and never initialises HIP doing so."""
+    import torch
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(var, raising=False)
+    _fake_topology(tmp_path, [0, 256, 256, 256, 256, 0, 256, 256, 256, 256])
+    assert bench.count_gpus_without_hip(str(tmp_path)) == 8
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0,3")
+    assert bench.count_gpus_without_hip(str(tmp_path)) == 2
+    assert not torch.cuda.is_initialized()
+
+
+def test_gpus_without_a_countable_device_exits_nonzero(tmp_path):
+    """No KFD topology and no working amdsmi (this container): --gpus 2 must fail loudly rather
+    than fall back to a HIP device query in the parent."""
+    if bench.count_gpus_without_hip() is not None:
+        pytest.skip("this machine exposes GPUs")
+    e = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"], env=e,
+                       capture_output=True, text=True, timeout=300)
+    assert p.returncode != 0
+    assert "cannot count GPUs" in p.stderr or "GPU(s) visible" in p.stderr

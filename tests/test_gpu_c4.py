@@ -268,3 +268,27 @@ def test_c4_two_block_slice_vs_hf(kernel_dtype):
         lines.append(f"{name} ours {r_ours:.2e} / transformers-bf16 {r_hf:.2e}")
         assert r_ours <= max(2.0 * r_hf, fl), (name, r_ours, r_hf)
     print(f"C4 2-block slice, {kernel_dtype} cell, rel. Frobenius error vs fp64: " + "; ".join(lines))
+
+
+def test_fp32_step_ignores_kernel_dtype_outside_autocast():
+    """Plain fp32 training (no autocast) with the builder's default autocast_kernel_dtype
+    (float16, as model.py:227): transformers' native chunkwise cell ignores that setting outside
+    autocast (modeling_xlstm.py:323), so the step must equal the float32-kernel-dtype model's
+    bitwise, and the gated head norm must see the activations' fp32 dtype."""
+    from statecatcher_amd.model import ASRModel, build_xlstm_config
+    g = torch.Generator().manual_seed(2)
+    B, T = 2, 128
+    feats = torch.randn(B, T, 80, generator=g).to(DEV)
+    out = {}
+    for kd in ("float16", "float32"):
+        torch.manual_seed(0)
+        cfg = build_xlstm_config(80, V, num_heads=4, num_blocks=2, embedding_dim=768,
+                                 autocast_kernel_dtype=kd)
+        model = ASRModel(None, cfg, vocab_size=V, feat_dim=80, proj_dim=-1).to(DEV)
+        logits, _ = model(feats, torch.ones(B, T, dtype=torch.bool, device=DEV))
+        logits.float().square().mean().backward()
+        out[kd] = (logits.detach(), {n: p.grad.detach().clone() for n, p in model.named_parameters()})
+    assert out["float16"][0].dtype == torch.float32
+    assert torch.equal(out["float16"][0], out["float32"][0])
+    for n, gr in out["float32"][1].items():
+        assert torch.equal(out["float16"][1][n], gr), n

@@ -106,3 +106,45 @@ def test_compute_loss_uses_head_under_bf16_autocast(monkeypatch):
         _, _, enc_out, _ = sc().compute_loss("ctc", sc().CTCLoss(blank=0, fused_head=False), model,
                                              feats, masks, tok, [64, 64], [10, 10], 0)
     assert not calls and enc_out.dtype == torch.bfloat16
+
+
+def test_split_scan_planes():
+    """sc_lucy_scan_fwd_split: out bitwise the plain scan's, out_dup == out, and out + out_lo is
+    the fp32 h to ~2^-16 (the same gates run through the fp32 scan)."""
+    ops = sc().ops
+    g = torch.Generator().manual_seed(3)
+    B, T, D = 2, 300, 128
+    gates = (torch.randn(B, T, 7, D, generator=g) * 0.5).to(torch.bfloat16).to(DEV)
+    h0 = torch.randn(B, D, generator=g).to(DEV)
+    s0 = torch.randn(B, D, generator=g).to(DEV)
+    _, out, s_out, _, wide = ops._scan_fwd(gates, h0, s0, False, split=True)
+    _, ref, s_ref, _ = ops._scan_fwd(gates, h0, s0, False)
+    assert torch.equal(out, ref) and torch.equal(s_out, s_ref)
+    assert torch.equal(wide[..., D:2 * D], out)
+    _, h32, _, _ = ops._scan_fwd(gates.float(), h0, s0, False)
+    hs = out.float() + wide[..., 2 * D:].float()
+    err = ((hs - h32).abs() / h32.abs().clamp_min(1e-3)).max().item()
+    print(f"split planes: max rel |hi + lo - h32| {err:.2e}")
+    assert err < 2 ** -15
+
+
+def test_ctc_head_split_logits_match_fp32():
+    """With the scan's [x_hi | x_hi | x_lo] buffer and [W_hi | W_lo | W_hi], the head's logits
+    are the fp32 x.W + b to ~1e-5 (one bf16 GEMM)."""
+    ops = sc().ops
+    g = torch.Generator().manual_seed(4)
+    B, T, D, V = 2, 128, 256, 512
+    x32 = torch.randn(B, T, D, generator=g).to(DEV)
+    hi = x32.to(torch.bfloat16)
+    wide = torch.cat([hi, hi, (x32 - hi.float()).to(torch.bfloat16)], -1).contiguous()
+    x = wide[..., :D]
+    w = (torch.randn(V, D, generator=g) * 0.05).to(DEV)
+    b = (torch.randn(V, generator=g) * 0.1).to(DEV)
+    tg = torch.randint(1, V, (B, 12), generator=g).to(DEV)
+    imgs = (w.to(torch.bfloat16), w.t().contiguous().to(torch.bfloat16))
+    _, logits = ops.ctc_head_loss(x, w, b, imgs, tg, [T, T], [12, 12], wide=wide)
+    ref = x32.double() @ w.double().t() + b.double()
+    _, l1 = ops.ctc_head_loss(x, w, b, imgs, tg, [T, T], [12, 12])
+    e_split, e_plain = rel(logits, ref), rel(l1, ref)
+    print(f"head logits rel err vs fp64: split {e_split:.2e}, bf16 operands {e_plain:.2e}")
+    assert e_split < 2e-5 < e_plain

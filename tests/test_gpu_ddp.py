@@ -7,7 +7,8 @@ collective, so this runs the real RCCL communicator at world size 1: DDP's bucke
 LucyCellFn's fused bias gradient, gradient_as_bucket_view buckets meet optim.clip_and_adam_step,
 and every bucket is all-reduced through RCCL.  The 2-rank sharding semantics are covered on the CPU
 by tests/test_train_ddp.py (gloo).  Parameters after 2 segments (state carried) must be BITWISE
-equal to the same training without DDP.
+equal to the same training without DDP -- on a small model, and on config C3's (6 x 512, V 1024,
+T 1500, 8 MB buckets, 4 carried segments, accumulation 1 and 2).
 """
 import os
 
@@ -88,6 +89,52 @@ def test_ddp_over_rccl_equals_single_process(rccl_group, mode):
     # the parameters moved: the all-reduced gradients reached the HIP Adam
     _, _, _, p0 = _build(mode)
     assert any(not torch.equal(a, b) for a, b in zip(p_ref, p0))
+
+
+@pytest.mark.parametrize("accumulation", [1, 2])
+def test_c3_model_ddp_over_rccl_equals_single_process(rccl_group, accumulation):
+    """Config C3's model and step as bench.py runs it: LucyRNN 6 x 512 + CTC, V = 1024, T = 1500,
+    bf16 autocast, the bench's 8 MB buckets (the 40 MB of gradients in 5+ buckets, each layer's
+    all-reduce overlapping the backward below it), 4 segments with the encoder state carried, and
+    gradient accumulation over 1 and 2 segments (no_sync on the accumulating ones); B = 2 per rank.
+    DDP over the RCCL communicator must leave every parameter bitwise where plain training does."""
+    from statecatcher_amd.model import ASRModel, CTCLoss, build_lucyrnn_config
+    from statecatcher_amd.train import SegmentTrainer
+    V, B, T, U = 1024, 2, 1500, 150
+
+    def run(ddp):
+        torch.manual_seed(11)
+        model = ASRModel(None, build_lucyrnn_config(80, 512, 6, V), vocab_size=V, feat_dim=80,
+                         proj_dim=-1).to(DEV)
+        with torch.no_grad():
+            model.encoder.output_proj.weight.normal_(0, 0.02)
+        params = list(model.parameters())
+        opt = torch.optim.Adam(params, lr=3e-4)
+        tr = SegmentTrainer(model, CTCLoss(blank=0, zero_infinity=True), opt,
+                            amp_dtype=torch.bfloat16, max_grad_norm=50.0, bucket_cap_mb=8.0,
+                            accumulation_steps=accumulation, ddp=ddp)
+        if ddp:   # the bench's bucket cap: 40 MB of gradients in 5+ all-reduces
+            assert tr.net.bucket_bytes_cap == 8 * 1024 * 1024
+        g = torch.Generator().manual_seed(7)
+        tr.begin_batch()
+        losses = []
+        for _ in range(4):
+            feats = torch.randn(B, T, 80, generator=g).to(DEV)
+            tok = torch.randint(1, V, (B, U), generator=g).to(DEV)
+            loss = tr.train_segment(feats, torch.ones(B, T, dtype=torch.bool, device=DEV), tok,
+                                    [T] * B, [U, 97])
+            losses.append(float(loss.detach()))
+        torch.cuda.synchronize()
+        state = [t.detach().clone() for t in tr.encoder_state[0][0] + tr.encoder_state[1][0]]
+        return losses, [p.detach().clone() for p in params], state
+
+    l_ref, p_ref, s_ref = run(False)
+    l_ddp, p_ddp, s_ddp = run(True)
+    print(f"C3 acc={accumulation}: losses {l_ref} (plain) {l_ddp} (DDP over RCCL)")
+    assert l_ref == l_ddp
+    assert all(torch.equal(a, b) for a, b in zip(p_ref, p_ddp))
+    assert all(torch.equal(a, b) for a, b in zip(s_ref, s_ddp))
+    assert all(torch.isfinite(torch.tensor(l_ref)))
 
 
 def test_rccl_allreduce_of_a_gradient_sized_buffer(rccl_group):

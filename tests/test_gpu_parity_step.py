@@ -21,8 +21,9 @@ Tolerances (stated per element class; both sides fp32 unless noted):
   lattice is fp32 in log space with every frame's emissions shifted by their maximum
   (csrc/ctc.hip), which holds the posteriors' error at ~1e-4 (2.5e-3 without the shift; ATen's own
   fp32 ctc_loss, the reference's criterion, is 5.2e-2 from fp64 on these logits).
-  bf16: gradient cosine >= 0.97 and norm within 10% per tensor (bf16 logits move CTC's
-  alignment posteriors by ~20% at T=1500 with an untrained, near-uniform output).
+  bf16 (the bench's arithmetic, split-precision output projection): gradient cosine >= 0.999 and
+  norm within 1% per tensor; with a plain bf16 output projection the measured 2-5% loss of
+  gradient direction is pinned per tensor (see BF16_MEASURED).
   Adam step 1: the post-step parameters equal clip + Adam restated on the GPU's own gradients
   (1e-4 relative, plus one fp32 ulp of the parameter), and wherever |g| >> Adam's eps (|g| > 1e-5,
   update ~ lr sign(g)) and >= 10x the tensor's rms gradient error they equal
@@ -255,10 +256,13 @@ def test_c2_training_step_fp32_vs_oracle():
         assert same.all(), (k, int((~same).sum()))
 
 
-# bf16 step vs the fp32 oracle, measured on MI355X (profiles/r3_parity_measured.md): per tensor
-# (gradient cosine, norm ratio).  The kernels are deterministic, so these repeat exactly; the
-# bounds below leave 0.006 of cosine and 0.02 of norm ratio for a change of GEMM accumulation
-# order (which moves bf16 rounding points), and catch a regression larger than that.
+# bf16 step vs the fp32 oracle with the output projection in plain bf16 (CTCLoss(fused_head=False):
+# bf16 operands, bf16 logits), measured on MI355X (profiles/r3_parity_measured.md): per tensor
+# (gradient cosine, norm ratio).  The 2-5% loss is the output projection's rounding alone -- of its
+# operands or of the logits -- which shifts CTC's alignment posteriors coherently over T = 1500
+# frames (tools/bf16_logits_diag.py reproduces these values on the CPU oracle; unbiased noise of
+# the same size costs nothing).  The kernels are deterministic, so these repeat exactly; the
+# bounds leave 0.006 of cosine and 0.02 of norm ratio for a change of GEMM accumulation order.
 BF16_MEASURED = {
     "encoder.tracks.0.0.linear.weight": (0.9999, 1.0005),
     "encoder.tracks.0.0.linear.bias": (0.9886, 0.9710),
@@ -288,33 +292,45 @@ BF16_MEASURED = {
 BF16_COS_MARGIN, BF16_RATIO_MARGIN = 0.006, 0.02
 
 
-def test_c2_training_step_bf16_vs_oracle():
+@pytest.mark.parametrize("fused_head", [True, False])
+def test_c2_training_step_bf16_vs_oracle(fused_head):
     """The bench's arithmetic (bf16 autocast GEMMs, bf16 gates, fp32 state): loss within 1e-2
-    relative of the fp32 oracle; per tensor, gradient cosine and norm ratio within the margins
-    above of their measured values (BF16_MEASURED)."""
+    relative of the fp32 oracle.  fused_head (the default, what the bench runs): the last scan
+    writes [x_hi | x_hi | x_lo] and the output projection is one bf16 GEMM against
+    [W_hi | W_lo | W_hi] with fp32 logits (ops.CTCHeadFn) -- every gradient's cosine >= 0.999 and
+    norm within 1% of the fp32 oracle (measured 1.0000 and <= 0.3%, profiles/r4_parity_measured.md).
+    Without it, per tensor within the margins of BF16_MEASURED."""
     from oracle import lucy_step
     B, T = 2, 1500
     p = oracle_params()
     model = model_from(p)
     feats, tok, U = step_inputs(B, T, 6)
     in_lens = np.full(B, T)
+    crit = sc().CTCLoss(blank=0, zero_infinity=True, fused_head=fused_head)
     with torch.autocast("cuda", dtype=torch.bfloat16):
-        loss, _, _, _ = sc().compute_loss("ctc", sc().CTCLoss(blank=0, zero_infinity=True), model,
+        loss, _, _, _ = sc().compute_loss("ctc", crit, model,
                                           torch.from_numpy(feats).to(DEV),
                                           torch.ones(B, T, dtype=torch.bool, device=DEV),
                                           torch.from_numpy(tok).to(DEV), in_lens.tolist(), U.tolist(), 0)
     loss.backward()
     ref_loss, _, ref_grads, _ = lucy_step.train_step(p, feats, tok, in_lens, U, L6, D512)
+    print(f"bf16 (fused_head={fused_head}) loss {loss.item():.6f} oracle {ref_loss:.6f}")
     np.testing.assert_allclose(loss.item(), ref_loss, rtol=1e-2)
+    bad = []
     for k, v in model.named_parameters():
         g = to_np(v.grad).ravel()
         rg = np.asarray(ref_grads[oracle_key(k)], np.float64).ravel()
         cos = float(g @ rg / (np.linalg.norm(g) * np.linalg.norm(rg)))
         ratio = float(np.linalg.norm(g) / np.linalg.norm(rg))
-        print(f"bf16 grad {k}: cos {cos:.4f} norm ratio {ratio:.4f}")
-        mc, mr = BF16_MEASURED[k]
-        assert cos >= mc - BF16_COS_MARGIN and abs(ratio - mr) <= BF16_RATIO_MARGIN, \
-            (k, cos, ratio, (mc, mr))
+        print(f"bf16 (fused_head={fused_head}) grad {k}: cos {cos:.4f} norm ratio {ratio:.4f}")
+        if fused_head:
+            ok = cos >= 0.999 and abs(ratio - 1.0) <= 0.01
+        else:
+            mc, mr = BF16_MEASURED[k]
+            ok = cos >= mc - BF16_COS_MARGIN and abs(ratio - mr) <= BF16_RATIO_MARGIN
+        if not ok:
+            bad.append((k, cos, ratio))
+    assert not bad, bad
 
 
 def test_four_segment_bf16_carry_vs_fp32_oracle():
