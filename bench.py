@@ -453,13 +453,14 @@ def main():
 
     # per-kernel average launch duration from the HIP events recorded on the launch stream
     kstats = {}
-    for name, e0, e1, nbytes in events:
-        k = kstats.setdefault(name, [0.0, 0, 0])
+    for name, e0, e1, nbytes, flops in events:
+        k = kstats.setdefault(name, [0.0, 0, 0, 0])
         k[0] += e0.elapsed_time(e1) * 1e-3
         k[1] += 1
         k[2] = nbytes
+        k[3] += flops
     kernels = {}
-    for name, (tsum, n, nbytes) in kstats.items():
+    for name, (tsum, n, nbytes, _) in kstats.items():
         avg = tsum / n
         tsteps = max(1, min(args.timing_steps, args.steps))
         kernels[name] = {"launches": n, "avg_us": round(avg * 1e6, 1),
@@ -484,6 +485,19 @@ def main():
     # sequences, all T = seq frames, U + 1 = 151 label positions): N = B T (U+1) lattice nodes,
     # joint_fwd 2 N V J flops (the logits once), joint_bwd 3 x 2 N V J (logits recomputed, dW,
     # dZ); J = 64.  Peak: bf16 dense MFMA (MI355X_MICROARCH.md).
+    # C4: the step belongs to its GEMMs (the xLSTM block linears: forward, input and weight
+    # gradients; profiles/r3d_prof_xlstm.md), so the roofline is theirs, as one class: the flops
+    # of every timed GEMM launch over their summed HIP-event time, against the bf16 MFMA peak
+    if args.workload == "xlstm" and "xlstm_gemm" in kstats:
+        tsum, n, _, fl = kstats["xlstm_gemm"]
+        tfs = fl / tsum / 1e12
+        kernels["xlstm_gemm"].update({"flops_per_step": fl / max(1, min(args.timing_steps, args.steps)),
+                                      "achieved_TFLOPs": round(tfs, 1),
+                                      "frac_of_peak": round(tfs / PEAK_BF16_TFLOPS, 4)})
+        roofline = {"bound": "mfma", "kernel": "xlstm_gemm (all block linears: fwd, dX, dW)",
+                    "achieved": round(tfs, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(tfs / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                    "mlstm": {k: kernels[k] for k in ("mlstm_fwd", "mlstm_bwd") if k in kernels}}
     if args.workload == "rnnt":
         nodes = args.batch * args.seq * 151
         for name, mult in (("rnnt_joint_fwd", 1), ("rnnt_joint_bwd", 3)):

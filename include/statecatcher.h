@@ -264,6 +264,32 @@ int sc_lucy_step_cell(int mode, const void* g, int dtype, int64_t g_stride, cons
                       const float* lnh_b, float eps, float* h, float* s, void* out,
                       const float* mask, int B, int D, void* stream);
 
+/*
+ * The same frame as a chain of fused kernels (csrc/lucy_frame.hip; no library GEMM, no separate
+ * LayerNorm launch).  Activations fp32; weights fp32 (fp32 MFMA, the reference's arithmetic) or
+ * bf16 (bf16 MFMA).  LayerNorm statistics travel as (n, mean, M2, -) float4 records, [nrec][B].
+ *
+ * sc_lucy_frame_gemm: y[b][j] = sum_k x~[b][k] w[j][k] + bias[j], x~ = x or, when ln_w is given,
+ *   LayerNorm(x) from the nst_in records of st_in (lucyrnn.py:45 layernorm_in).  epi:
+ *   0 plain; 1 plain + one statistics record of y per 64 columns into st_out ([N/64][B]);
+ *   2 unfused gates (N = 4D: z k v decay, lucyrnn.py:55-59): s' = sigmoid(decay) s + k v into s
+ *     (masked), y = x~ + s' ([B][D], K == D), z ([B][D]), records of z per 16 units into st_z;
+ *   3 fused gates (N = 5D: z k v h_pre decay; W_fused without its unused r rows, :47-53): s as
+ *     above, y = h_pre + s', z, records of y into st_out and of z into st_z ([D/16][B] each).
+ *   x 16-byte aligned with ldx % 4 == 0, K % 4 == 0; w 16-byte aligned with ldw % 8 == 0.
+ * sc_lucy_frame_cellb: h = (1 - sigmoid(LN_z z)) tanh(LN_h hp) + sigmoid(LN_z z) h (masked,
+ *   :61-68) in place, and out[b][:D] = h (the next layer's input).
+ */
+int sc_lucy_frame_gemm(int epi, const float* x, int64_t ldx, int K, const float* ln_w,
+                       const float* ln_b, const void* st_in, int nst_in, float eps, const void* w,
+                       int w_dtype, int64_t ldw, const float* bias, int B, int N, float* y,
+                       int64_t ldy, void* st_out, float* z, void* st_z, float* s,
+                       const float* mask, void* stream);
+int sc_lucy_frame_cellb(const float* z, const void* st_z, int nst_z, const float* hp,
+                        const void* st_h, int nst_h, const float* lnz_w, const float* lnz_b,
+                        const float* lnh_w, const float* lnh_b, float eps, float* h, float* out,
+                        int64_t ldo, const float* mask, int B, int D, void* stream);
+
 /* ---------------------------------------------------------------- column sums ----------- */
 
 /*

@@ -59,6 +59,10 @@ _SIGS = {
     "sc_lucy_step_ln": (_i32, [_vp, _i32, _fp, _fp, _c.c_float, _vp, _i32, _i32, _vp]),
     "sc_lucy_step_cell": (_i32, [_i32, _vp, _i32, _i64, _vp, _vp, _fp, _fp, _fp, _fp, _c.c_float,
                                  _fp, _fp, _vp, _fp, _i32, _i32, _vp]),
+    "sc_lucy_frame_gemm": (_i32, [_i32, _fp, _i64, _i32, _fp, _fp, _vp, _i32, _c.c_float, _vp, _i32,
+                                  _i64, _fp, _i32, _i32, _fp, _i64, _vp, _fp, _vp, _fp, _fp, _vp]),
+    "sc_lucy_frame_cellb": (_i32, [_fp, _vp, _i32, _fp, _vp, _i32, _fp, _fp, _fp, _fp, _c.c_float,
+                                   _fp, _fp, _i64, _fp, _i32, _i32, _vp]),
     "sc_mlstm_supported": (_i32, [_i32, _i32, _i32]),
     "sc_mlstm_chunk_state_numel": (_i64, [_i32, _i32, _i32, _i32]),
     "sc_mlstm_fwd": (_i32, [_vp, _vp, _vp, _i32, _fp, _fp, _fp, _fp, _fp, _i32, _i32, _i32, _i32,

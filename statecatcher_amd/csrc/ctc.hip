@@ -508,6 +508,193 @@ __global__ void __launch_bounds__(1024) ctc_ab_kernel(CtcArgs a) {
   else ab_run<K, false>(a, b, Tb, Ub);
 }
 
+// ONE WAVE per (sequence, direction) when the lattice's U + 1 state pairs fit PPL pairs per lane
+// (PPL <= 4: U <= 255; C2's U <= 150 takes PPL = 3).  Lane l holds pairs p = l PPL .. l PPL +
+// PPL - 1, so a step needs one DPP lane shift (alpha: the previous lane's last label state;
+// beta: the next lane's first pair) and 2 PPL independent log-sum-exps: no halo lanes, no LDS, no
+// barrier.  The recurrence's loop runs through PPL consecutive steps of one lane before it
+// crosses a lane, so the step's latency is one log-sum-exp plus a DPP every PPL steps, and the
+// 2 PPL chains of a step fill each other's issue gaps.  (The multi-wave kernel above spends a
+// workgroup barrier every K steps on its halo exchange and a third of its lanes on halo pairs.)
+// Re-centred on the wave max every kAb1R steps (fp64 offsets, stored per re-centring).
+constexpr int kAb1R = 32;
+constexpr int kAb1P = 16;   // emission prefetch depth (steps)
+
+template <int PPL, bool BETA>
+__device__ __forceinline__ void ab1_run(const CtcArgs& a, int b, int Tb, int Ub) {
+  const int lane = threadIdx.x;
+  const int64_t* tg = a.tg + (int64_t)b * a.tgs;
+  const int npairs = a.Sp / 2;            // pairs in a workspace row
+  bool skip[PPL];
+  uint32_t vo[PPL];                       // byte offset of pair p in a row (kDrop past it)
+  constexpr uint32_t kDrop = 0x80000000u;
+#pragma unroll
+  for (int j = 0; j < PPL; ++j) {
+    const int p = lane * PPL + j;
+    skip[j] = false;
+    if (p < Ub) {   // the label state 2p+1 is live
+      const int lab = (int)tg[p];
+      if (!BETA) {
+        skip[j] = p >= 1 && lab != a.blank && lab != (int)tg[p - 1];
+      } else if (p + 1 < Ub) {
+        const int l2 = (int)tg[p + 1];
+        skip[j] = l2 != a.blank && l2 != lab;
+      }
+    }
+    vo[j] = p < npairs ? (uint32_t)(8 * p) : kDrop;
+  }
+  const uint32_t rowb = (uint32_t)(a.Sp * 4);
+  const __amdgpu_buffer_rsrc_t ers = __builtin_amdgcn_make_buffer_rsrc(
+      a.ws.lpe + (int64_t)b * a.T * a.Sp, 0, (int)(rowb * (uint32_t)a.T), 0x00020000);
+  const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
+      (BETA ? a.ws.beta : a.ws.alpha) + (int64_t)b * a.T * a.Sp, 0, (int)(rowb * (uint32_t)a.T),
+      0x00020000);
+  double* offn = (BETA ? a.ws.offB : a.ws.offA) + (int64_t)b * a.T;
+  if (lane == 0) offn[0] = 0.0;
+  auto tstep = [&](int i) { return BETA ? Tb - 1 - i : i; };
+  f2v bufA[kAb1P][PPL], bufB[kAb1P][PPL];
+  auto load = [&](f2v (&buf)[kAb1P][PPL], int i0) {
+#pragma unroll
+    for (int s = 0; s < kAb1P; ++s) {
+      const uint32_t so = (uint32_t)tstep(min(i0 + s, Tb - 1)) * rowb;
+#pragma unroll
+      for (int j = 0; j < PPL; ++j)
+        buf[s][j] = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(ers, vo[j], so, 0));
+    }
+  };
+  float vB[PPL], vL[PPL];
+#pragma unroll
+  for (int j = 0; j < PPL; ++j) vB[j] = vL[j] = kDead;
+  double off = 0.0;
+  auto body = [&](const f2v (&buf)[kAb1P][PPL], int i0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int s = 0; s < kAb1P; ++s) {
+      const int i = i0 + s;
+      if (i >= Tb) break;
+      if (i == 0) {
+#pragma unroll
+        for (int j = 0; j < PPL; ++j) {
+          const int p = lane * PPL + j;
+          vB[j] = (p <= Ub && p == (BETA ? Ub : 0)) ? buf[s][j].x : kDead;
+          vL[j] = (p < Ub && p == (BETA ? Ub - 1 : 0)) ? buf[s][j].y : kDead;
+        }
+      } else if (!BETA) {
+        // pair p's predecessor label state 2p-1: pair p-1's, the previous lane's last for j = 0
+        float prevL[PPL];
+        prevL[0] = shr1(vL[PPL - 1]);   // lane 0: pair 0 has no predecessor (dead, not 0)
+#pragma unroll
+        for (int j = 1; j < PPL; ++j) prevL[j] = vL[j - 1];
+#pragma unroll
+        for (int j = 0; j < PPL; ++j) {
+          const f2v r = lse23(vB[j], prevL[j], vL[j], vB[j], skip[j] ? prevL[j] : kDead, buf[s][j]);
+          vB[j] = r.x;
+          vL[j] = r.y;
+        }
+      } else {
+        // pair p's successors 2p+2 (blank) and 2p+3 (label): pair p+1's, the next lane's first
+        float nB[PPL], nL[PPL];
+        nB[PPL - 1] = shl1(vB[0]);   // lane 63: no successor (dead, not 0)
+        nL[PPL - 1] = shl1(vL[0]);
+#pragma unroll
+        for (int j = 0; j + 1 < PPL; ++j) {
+          nB[j] = vB[j + 1];
+          nL[j] = vL[j + 1];
+        }
+#pragma unroll
+        for (int j = 0; j < PPL; ++j) {
+          const f2v r = lse23(vB[j], vL[j], vL[j], nB[j], skip[j] ? nL[j] : kDead, buf[s][j]);
+          vB[j] = r.x;
+          vL[j] = r.y;
+        }
+      }
+      if ((i + 1) % kAb1R == 0) {   // re-centre on the wave max
+        float m = kDead;
+#pragma unroll
+        for (int j = 0; j < PPL; ++j) m = vmax3(m, vB[j], vL[j]);
+        m = wave_max_dpp(m);
+        if (m > 0.5f * kDead) {   // all dead (infeasible): keep the sentinel
+#pragma unroll
+          for (int j = 0; j < PPL; ++j) {
+            vB[j] -= m;
+            vL[j] -= m;
+          }
+          off += (double)m;
+        }
+        if (lane == 0) offn[(i + 1) / kAb1R] = off;
+      }
+      const uint32_t so = (uint32_t)tstep(i) * rowb;
+#pragma unroll
+      for (int j = 0; j < PPL; ++j)
+        __builtin_amdgcn_raw_buffer_store_b64(
+            __builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, f2v{vB[j], vL[j]}),
+            ors, vo[j], so, 0);
+    }
+  };
+  load(bufA, 0);
+  for (int i0 = 0; i0 < Tb; i0 += 2 * kAb1P) {
+    load(bufB, i0 + kAb1P);
+    body(bufA, i0);
+    if (i0 + kAb1P >= Tb) break;
+    load(bufA, i0 + 2 * kAb1P);
+    body(bufB, i0 + kAb1P);
+  }
+  if (!BETA) {
+    // sum_t c_t in fp64, fixed order
+    double cs = 0.0;
+    for (int t = lane; t < Tb; t += 64) cs += (double)a.ws.cst[(int64_t)b * a.T + t];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) cs += __shfl_xor(cs, o);
+    // log p = log2sum(alpha_{Tb-1}(2Ub), alpha_{Tb-1}(2Ub-1)) + off
+    float c = kDead;
+#pragma unroll
+    for (int j = 0; j < PPL; ++j) {
+      const int p = lane * PPL + j;
+      if (p == Ub) c = lse2_live(c, vB[j]);
+      if (p == Ub - 1) c = lse2_live(c, vL[j]);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float co = __shfl_xor(c, o);
+      const float m = fmaxf(c, co);
+      c = m + log2_(exp2_(c - m) + exp2_(co - m));
+    }
+    if (lane == 0) {
+      const bool dead = c < 0.5f * kDead;
+      const double ll2s = (double)c + off;
+      a.ws.ll2s[b] = dead ? -__builtin_huge_val() : ll2s;
+      a.nll[b] = dead ? __builtin_huge_valf() : (float)(-(ll2s + cs) * 0.6931471805599453);
+    }
+  }
+}
+
+template <int PPL>
+__global__ void __launch_bounds__(64) ctc_ab1_kernel(CtcArgs a) {
+  const bool is_beta = blockIdx.x >= a.B;
+  const int b = is_beta ? blockIdx.x - a.B : blockIdx.x;
+  const int Tb = clampi(a.in_lens[b], 0, a.T);
+  const int Ub = clampi(a.tgt_lens[b], 0, a.Umax);
+  if (Tb == 0) {
+    if (!is_beta && threadIdx.x == 0) {
+      a.nll[b] = (Ub == 0) ? 0.0f : __builtin_huge_valf();
+      a.ws.ll2s[b] = (Ub == 0) ? 0.0 : -__builtin_huge_val();
+    }
+    return;
+  }
+  if (is_beta) ab1_run<PPL, true>(a, b, Tb, Ub);
+  else ab1_run<PPL, false>(a, b, Tb, Ub);
+}
+
+// pairs per lane of the one-wave lattice (0: the multi-wave kernel).  SC_CTC_AB1=0 in the
+// environment forces the multi-wave kernel (A/B timing in tools only).
+static int ab1_ppl(int Umax) {
+  static const bool on = [] {
+    const char* e = getenv("SC_CTC_AB1");
+    return !(e && e[0] == '0');
+  }();
+  const int ppl = (Umax + 1 + 63) / 64;
+  return (on && ppl <= 4) ? ppl : 0;
+}
+
 // K (steps between halo exchanges) so that ceil((Umax + 1) / (64 - K)) waves of state pairs fit
 // a 1024-thread group
 static int ab_halo_k(int Umax) {
@@ -644,6 +831,13 @@ static void launch_fwd(const CtcArgs& a, hipStream_t st) {
   hipLaunchKernelGGL((ctc_emit_kernel<DT>), dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, a);
   hipLaunchKernelGGL(ctc_chain_kernel, dim3(a.B, ((a.Umax > 0 ? a.Umax : 1) + 3) / 4), dim3(256), 0,
                      st, a);
+  switch (ab1_ppl(a.Umax)) {
+    case 1: hipLaunchKernelGGL((ctc_ab1_kernel<1>), dim3(2 * a.B), dim3(64), 0, st, a); return;
+    case 2: hipLaunchKernelGGL((ctc_ab1_kernel<2>), dim3(2 * a.B), dim3(64), 0, st, a); return;
+    case 3: hipLaunchKernelGGL((ctc_ab1_kernel<3>), dim3(2 * a.B), dim3(64), 0, st, a); return;
+    case 4: hipLaunchKernelGGL((ctc_ab1_kernel<4>), dim3(2 * a.B), dim3(64), 0, st, a); return;
+    default: break;
+  }
   const int K = a.kh;
   const int nw = (a.Umax + 1 + (64 - K) - 1) / (64 - K);
   const size_t sh = 2 * (size_t)nw * (64 - K) * sizeof(float2);
@@ -731,7 +925,9 @@ static CtcArgs make_args(const void* x, int is_logits, int B, int T, int V, int6
   a.S = 2 * umax + 1;
   a.Sp = 64 * states_per_lane(a.S);
   a.Umax = umax;
-  a.kh = ab_halo_k(umax);
+  // steps per re-centring / 2 (the gradient's offset index): the one-wave lattice re-centres
+  // every kAb1R steps, the multi-wave one at every second halo exchange
+  a.kh = ab1_ppl(umax) ? kAb1R / 2 : ab_halo_k(umax);
   a.blank = blank;
   a.sb = sb;
   a.stt = st;

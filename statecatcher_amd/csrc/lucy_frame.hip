@@ -1,0 +1,410 @@
+// Streaming frame of the native LucyRNN (infer mode) as a short chain of fused kernels — SURVEY
+// §8(f) row 2: the reference's per-frame loop lucyrnn.py:172-184, LucyRNNCell.forward
+// (lucyrnn.py:44-70) at T = 1, with the state resident in HBM in fp32 between calls.
+//
+// A frame of B streams is, per layer (u = LN_in(a) etc. as in lucyrnn.py:45-68):
+//   lucy_frame_gemm  PRO_NONE / EPI_STATS  a = x W_in^T + b_in, plus per-row LayerNorm partial
+//                                          statistics of a (one record per 64 output columns)
+//   lucy_frame_gemm  PRO_LN / EPI_CELL     g = LN_in(a) W_g^T + b_g, the workgroup owning 16 units
+//                                          of EVERY gate, so the cell's elementwise part runs in
+//                                          its epilogue: s' = sigmoid(dl) s + k v (state, masked),
+//                                          then unfused: y = u + s' (the input of W_h); fused:
+//                                          hp = h_pre + s'; z and hp with their row statistics
+//   lucy_frame_gemm  PRO_NONE / EPI_STATS  (unfused) hp = y W_h^T + b_h, statistics of hp
+//   lucy_frame_cellb                       h = (1 - sigmoid(LN_z z)) tanh(LN_h hp)
+//                                              + sigmoid(LN_z z) h_prev, masked; the next input
+// and after the last layer the output projection (lucy_frame_gemm PRO_NONE / EPI_PLAIN) and the
+// greedy step (sc_ctc_greedy_step, decode.hip).  The W_r rows are never computed: the reference
+// evaluates sigmoid(LN_r(W_r u)) and never uses it.
+//
+// LayerNorm (nn.LayerNorm: biased variance, eps inside the rsqrt) is split over the producing GEMM
+// and its consumer: every producer workgroup writes (n, mean, M2) of its columns per row, the
+// consumer combines the records (Chan's parallel formula) and normalises on load — no separate
+// LayerNorm launch and no second pass over the activations.
+//
+// GEMM tiling (B streams x N outputs x K, B <= a few hundred: skinny): one wave computes one 16 x 16
+// output tile over a K slice on MFMA — v_mfma_f32_16x16x4_f32 for fp32 weights (exact f32 products,
+// the reference's arithmetic), v_mfma_f32_16x16x32_bf16 for bf16 weights (activations rounded to
+// bf16 on load, fp32 accumulate); a workgroup holds NT tiles x KS K-slices, summed through LDS.
+// Activations between kernels are fp32.
+#include "sc_common.h"
+
+namespace sc {
+
+enum { FR_PLAIN = 0, FR_STATS = 1, FR_CELL_UNFUSED = 2, FR_CELL_FUSED = 3 };
+
+struct FrameGemmArgs {
+  const float* x;        // [B][ldx] fp32 activations (the A operand, before the prologue)
+  int64_t ldx;
+  int K;                 // reduction length
+  const float* ln_w;     // PRO_LN: LayerNorm weight / bias over K (NULL: no prologue)
+  const float* ln_b;
+  const float4* st_in;   // PRO_LN: [nst_in][B] (n, mean, M2, -) records of x's rows
+  int nst_in;
+  float eps;
+  const void* w;         // [N][ldw] weights (fp32 or bf16): output column j = row j
+  int64_t ldw;
+  const float* bias;     // [N]
+  int B, N;
+  int gstride;           // EPI_CELL: W row of gate g, unit d = g * gstride + d (gstride = D)
+  // outputs
+  float* y;              // PLAIN / STATS: [B][ldy]; CELL: y (unfused) or hp (fused) [B][D]
+  int64_t ldy;
+  float4* st_out;        // STATS: [N / (NT * 16)][B]; CELL: [D / 16][B] records of y/hp (fused)
+  float* z;              // CELL: raw z [B][D]
+  float4* st_z;          // CELL: [D / 16][B] records of z
+  float* s;              // CELL: fp32 state [B][D], in place
+  const float* mask;     // CELL: [B] or NULL
+};
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+// Chan's combination of (n, mean, M2) records -> (mean, rstd) of the full row
+__device__ __forceinline__ void combine_stats(const float4* rec, int nrec, int64_t stride,
+                                              float eps, float& mean, float& rstd) {
+  float n = 0.0f, sm = 0.0f;
+  for (int i = 0; i < nrec; ++i) {
+    const float4 r = rec[i * stride];
+    n += r.x;
+    sm += r.x * r.y;
+  }
+  mean = sm / n;
+  float m2 = 0.0f;
+  for (int i = 0; i < nrec; ++i) {
+    const float4 r = rec[i * stride];
+    const float d = r.y - mean;
+    m2 += r.z + r.x * d * d;
+  }
+  rstd = 1.0f / sqrtf(m2 / n + eps);
+}
+
+// (n, mean, M2) of 16 values held by the 16 lanes of a lane group (xor butterflies within it)
+__device__ __forceinline__ float4 stats16(float v) {
+  float sm = v;
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) sm += __shfl_xor(sm, o);
+  const float mean = sm * (1.0f / 16.0f);
+  float d = (v - mean) * (v - mean);
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) d += __shfl_xor(d, o);
+  return make_float4(16.0f, mean, d, 0.0f);
+}
+
+// One workgroup: rows r0 .. r0 + 15, NT output tiles x KS K-slices (one wave each).
+//   PLAIN / STATS: tile t = columns n0 + 16 t .. (n0 = blockIdx.x * 16 NT)
+//   CELL: tile t = gate t, units d0 .. d0 + 15 (d0 = 16 blockIdx.x), W rows t * gstride + d
+template <bool BF16W, bool LN, int EPI, int NT, int KS>
+__global__ void __launch_bounds__(64 * NT * KS) lucy_frame_gemm(FrameGemmArgs a) {
+  __shared__ float part[NT * KS][16][17];   // per-wave 16 x 16 partial sums (padded rows)
+  __shared__ float stat[16][2];             // PRO_LN: (mean, rstd) of the workgroup's rows
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int t = w % NT, ks = w / NT;
+  const int r0 = blockIdx.y * 16;
+  constexpr bool CELL = EPI == FR_CELL_UNFUSED || EPI == FR_CELL_FUSED;
+  const int cbase = CELL ? blockIdx.x * 16 + t * a.gstride : (blockIdx.x * NT + t) * 16;
+  // the row statistics of the prologue, once per workgroup
+  if (LN) {
+    if (threadIdx.x < 16) {
+      const int r = min(r0 + (int)threadIdx.x, a.B - 1);
+      float mean, rstd;
+      combine_stats(a.st_in + r, a.nst_in, a.B, a.eps, mean, rstd);
+      stat[threadIdx.x][0] = mean;
+      stat[threadIdx.x][1] = rstd;
+    }
+    __syncthreads();
+  }
+  const int arow = r0 + (lane & 15);
+  const bool rok = arow < a.B;
+  const float* xr = a.x + (int64_t)min(arow, a.B - 1) * a.ldx;
+  const int col = cbase + (lane & 15);
+  const bool cok = CELL || col < a.N;
+  const float mean = LN ? stat[lane & 15][0] : 0.0f, rstd = LN ? stat[lane & 15][1] : 1.0f;
+  // K slice of this wave, in steps of KSTEP
+  constexpr int KSTEP = BF16W ? 32 : 16;
+  const int nsteps = (a.K + KSTEP - 1) / KSTEP;
+  const int sb = (int)((int64_t)nsteps * ks / KS), se = (int)((int64_t)nsteps * (ks + 1) / KS);
+  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  const int q = lane >> 4;
+  // Every load of a chunk of up to SMAX steps is issued before its first MFMA (one exposed
+  // memory latency per chunk, not per step: the operands come from L2 / the Infinity Cache)
+  if constexpr (!BF16W) {
+    constexpr int SMAX = NT * KS > 8 ? 8 : 16;   // (10 waves: 3 per SIMD, <= 168 VGPRs)
+    const float* wr = (const float*)a.w + (int64_t)(cok ? col : 0) * a.ldw;
+    for (int c0 = sb; c0 < se; c0 += SMAX) {
+      float4 xa[SMAX], wb[SMAX];
+#pragma unroll
+      for (int i = 0; i < SMAX; ++i) {
+        const int k0 = (c0 + i) * 16 + 4 * q;   // this lane's 4 consecutive k of step c0 + i
+        const bool full = c0 + i < se && k0 + 3 < a.K && rok && cok;
+        xa[i] = full ? *(const float4*)(xr + k0) : make_float4(0.f, 0.f, 0.f, 0.f);
+        wb[i] = full ? *(const float4*)(wr + k0) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int i = 0; i < SMAX; ++i) {
+        if (c0 + i >= se) break;
+        const int k0 = (c0 + i) * 16 + 4 * q;
+        float av[4] = {xa[i].x, xa[i].y, xa[i].z, xa[i].w};
+        float bv[4] = {wb[i].x, wb[i].y, wb[i].z, wb[i].w};
+        if (!(k0 + 3 < a.K && rok && cok)) {   // a ragged K tail (layer 0: K = 80 x stack)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            av[j] = k0 + j < a.K && rok ? xr[k0 + j] : 0.0f;
+            bv[j] = k0 + j < a.K && cok ? wr[k0 + j] : 0.0f;
+          }
+        }
+        if (LN) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            av[j] = k0 + j < a.K ? (av[j] - mean) * rstd * a.ln_w[k0 + j] + a.ln_b[k0 + j] : 0.0f;
+        }
+        // k slot q of MFMA j is k0 + j for both operands: the sum runs over the same k set
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[0], bv[0], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[1], bv[1], acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[2], bv[2], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[3], bv[3], acc1, 0, 0, 0);
+      }
+    }
+  } else {
+    constexpr int SMAX = 8;
+    const __bf16* wr = (const __bf16*)a.w + (int64_t)(cok ? col : 0) * a.ldw;
+    for (int c0 = sb; c0 < se; c0 += SMAX) {
+      float4 x0[SMAX], x1[SMAX];
+      bf16x8 wb[SMAX];
+#pragma unroll
+      for (int i = 0; i < SMAX; ++i) {
+        const int k0 = (c0 + i) * 32 + 8 * q;   // this lane's 8 consecutive k of step c0 + i
+        const bool full = c0 + i < se && k0 + 7 < a.K && rok && cok;
+        x0[i] = full ? *(const float4*)(xr + k0) : make_float4(0.f, 0.f, 0.f, 0.f);
+        x1[i] = full ? *(const float4*)(xr + k0 + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+        if (full) wb[i] = *(const bf16x8*)(wr + k0);
+        else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) wb[i][j] = (__bf16)0.0f;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < SMAX; ++i) {
+        if (c0 + i >= se) break;
+        const int k0 = (c0 + i) * 32 + 8 * q;
+        float f[8] = {x0[i].x, x0[i].y, x0[i].z, x0[i].w, x1[i].x, x1[i].y, x1[i].z, x1[i].w};
+        bf16x8 bv = wb[i];
+        if (!(k0 + 7 < a.K && rok && cok)) {   // ragged K tail
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            f[j] = k0 + j < a.K && rok ? xr[k0 + j] : 0.0f;
+            bv[j] = k0 + j < a.K && cok ? wr[k0 + j] : (__bf16)0.0f;
+          }
+        }
+        bf16x8 av;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float v = LN && k0 + j < a.K ? (f[j] - mean) * rstd * a.ln_w[k0 + j] + a.ln_b[k0 + j]
+                                             : f[j];
+          av[j] = (__bf16)v;
+        }
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc0, 0, 0, 0);
+      }
+    }
+  }
+  // C layout: column lane & 15, rows 4 (lane >> 4) + i
+#pragma unroll
+  for (int i = 0; i < 4; ++i) part[w][4 * q + i][lane & 15] = acc0[i] + acc1[i];
+  __syncthreads();
+  // sum the K slices into slot t (waves ks = 0)
+  if (KS > 1 && ks == 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float v = part[t][4 * q + i][lane & 15];
+#pragma unroll
+      for (int s = 1; s < KS; ++s) v += part[t + s * NT][4 * q + i][lane & 15];
+      part[t][4 * q + i][lane & 15] = v;
+    }
+  }
+  if (KS > 1) __syncthreads();
+  if constexpr (!CELL) {
+    // tile t (waves w < NT): bias, store, row statistics over the workgroup's 16 NT columns
+    if (w < NT) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = r0 + 4 * q + i, c = cbase + (lane & 15);
+        const float v = part[w][4 * q + i][lane & 15] + (c < a.N ? a.bias[c] : 0.0f);
+        part[w][4 * q + i][lane & 15] = v;
+        if (r < a.B && c < a.N) a.y[(int64_t)r * a.ldy + c] = v;
+      }
+    }
+    if (EPI == FR_STATS) {
+      __syncthreads();
+      if (threadIdx.x < 16) {   // one lane per row: two passes over the 16 NT values
+        const int rr = threadIdx.x;
+        const int ncol = min(16 * NT, a.N - (int)blockIdx.x * 16 * NT);
+        float sm = 0.0f;
+        for (int c = 0; c < ncol; ++c) sm += part[c >> 4][rr][c & 15];
+        const float mn = sm / (float)ncol;
+        float m2 = 0.0f;
+        for (int c = 0; c < ncol; ++c) {
+          const float d = part[c >> 4][rr][c & 15] - mn;
+          m2 += d * d;
+        }
+        if (r0 + rr < a.B) a.st_out[(int64_t)blockIdx.x * a.B + r0 + rr] = make_float4((float)ncol, mn, m2, 0.0f);
+      }
+    }
+  } else {
+    // the cell's elementwise part for the 16 x 16 (row, unit) elements: one per lane of wave 0..3
+    if (w < 4) {
+      const int rr = 4 * w + q, r = r0 + rr, d = blockIdx.x * 16 + (lane & 15);
+      const int D = a.gstride;
+      const bool ok = r < a.B;
+      const int rc = ok ? r : a.B - 1;
+      auto gate = [&](int g) { return part[g][rr][lane & 15] + a.bias[g * a.gstride + d]; };
+      const float z = gate(0), k = gate(1), v = gate(2);
+      const float dl = gate(EPI == FR_CELL_FUSED ? 4 : 3);
+      const float m = a.mask ? a.mask[rc] : 1.0f;
+      const float sp = a.s[(int64_t)rc * D + d];
+      const float sn = (1.0f / (1.0f + expf(-dl))) * sp + k * v;
+      float o;
+      if (EPI == FR_CELL_FUSED) {
+        o = gate(3) + sn;                                   // hp = h_pre + s'
+      } else {
+        const float av = a.x[(int64_t)rc * a.ldx + d];      // u = LN_in(a), unit d
+        o = LN ? (av - stat[rr][0]) * stat[rr][1] * a.ln_w[d] + a.ln_b[d] : av;
+        o += sn;                                            // y = u + s'
+      }
+      const float4 sz = stats16(z), so = stats16(o);
+      if (ok) {
+        a.s[(int64_t)r * D + d] = m * sn + (1.0f - m) * sp;
+        a.z[(int64_t)r * D + d] = z;
+        a.y[(int64_t)r * D + d] = o;
+        if ((lane & 15) == 0) {
+          a.st_z[(int64_t)blockIdx.x * a.B + r] = sz;
+          if (a.st_out) a.st_out[(int64_t)blockIdx.x * a.B + r] = so;
+        }
+      }
+    }
+  }
+}
+
+// h = (1 - zg) c + zg h_prev (masked), zg = sigmoid(LN_z z), c = tanh(LN_h hp): one workgroup of
+// 256 threads per row
+struct FrameCellArgs {
+  const float* z;
+  const float4* st_z;   // [nst_z][B] or NULL (no LayerNorm)
+  int nst_z;
+  const float* hp;
+  const float4* st_h;   // [nst_h][B] or NULL
+  int nst_h;
+  const float *lnz_w, *lnz_b, *lnh_w, *lnh_b;
+  float eps;
+  float* h;             // fp32 state [B][D], in place
+  float* out;           // next layer input [B][ldo] fp32
+  int64_t ldo;
+  const float* mask;
+  int B, D;
+};
+
+__global__ void __launch_bounds__(256) lucy_frame_cellb(FrameCellArgs a) {
+  __shared__ float st[4];
+  const int r = blockIdx.x;
+  if (threadIdx.x == 0) {
+    float mz = 0.0f, rz = 1.0f, mh = 0.0f, rh = 1.0f;
+    if (a.lnz_w) combine_stats(a.st_z + r, a.nst_z, a.B, a.eps, mz, rz);
+    if (a.lnh_w) combine_stats(a.st_h + r, a.nst_h, a.B, a.eps, mh, rh);
+    st[0] = mz; st[1] = rz; st[2] = mh; st[3] = rh;
+  }
+  __syncthreads();
+  const float m = a.mask ? a.mask[r] : 1.0f;
+  for (int d = threadIdx.x; d < a.D; d += 256) {
+    const int64_t i = (int64_t)r * a.D + d;
+    float z = a.z[i], hp = a.hp[i];
+    if (a.lnz_w) z = (z - st[0]) * st[1] * a.lnz_w[d] + a.lnz_b[d];
+    if (a.lnh_w) hp = (hp - st[2]) * st[3] * a.lnh_w[d] + a.lnh_b[d];
+    const float zg = 1.0f / (1.0f + expf(-z));
+    const float hprev = a.h[i];
+    const float hv = (1.0f - zg) * tanhf(hp) + zg * hprev;
+    const float hn = m * hv + (1.0f - m) * hprev;
+    a.h[i] = hn;
+    a.out[(int64_t)r * a.ldo + d] = hn;
+  }
+}
+
+template <bool BF16W, bool LN, int EPI, int NT, int KS>
+static void launch_gemm(const FrameGemmArgs& a, int nblk, hipStream_t st) {
+  hipLaunchKernelGGL((lucy_frame_gemm<BF16W, LN, EPI, NT, KS>), dim3(nblk, (a.B + 15) / 16),
+                     dim3(64 * NT * KS), 0, st, a);
+}
+
+template <bool BF16W, bool LN>
+static void dispatch_gemm(int epi, int ngate, const FrameGemmArgs& a, hipStream_t st) {
+  switch (epi) {
+    case FR_PLAIN: launch_gemm<BF16W, LN, FR_PLAIN, 4, 2>(a, (a.N + 63) / 64, st); break;
+    case FR_STATS: launch_gemm<BF16W, LN, FR_STATS, 4, 2>(a, (a.N + 63) / 64, st); break;
+    case FR_CELL_UNFUSED:
+      launch_gemm<BF16W, LN, FR_CELL_UNFUSED, 4, 2>(a, a.gstride / 16, st); break;
+    default: launch_gemm<BF16W, LN, FR_CELL_FUSED, 5, 2>(a, a.gstride / 16, st); break;
+  }
+  (void)ngate;
+}
+
+}  // namespace sc
+
+using namespace sc;
+
+extern "C" int sc_lucy_frame_gemm(int epi, const float* x, int64_t ldx, int K, const float* ln_w,
+                                  const float* ln_b, const void* st_in, int nst_in, float eps,
+                                  const void* w, int w_dtype, int64_t ldw, const float* bias,
+                                  int B, int N, float* y, int64_t ldy, void* st_out, float* z,
+                                  void* st_z, float* s, const float* mask, void* stream) {
+  clear_error();
+  SC_REQUIRE(epi >= FR_PLAIN && epi <= FR_CELL_FUSED, "sc_lucy_frame_gemm: bad epilogue %d", epi);
+  SC_REQUIRE(w_dtype == SC_F32 || w_dtype == SC_BF16, "sc_lucy_frame_gemm: weights fp32 or bf16");
+  SC_REQUIRE(B >= 0 && K > 0 && N > 0, "sc_lucy_frame_gemm: bad shape B=%d K=%d N=%d", B, K, N);
+  if (B == 0) return 0;
+  SC_REQUIRE(x && w && bias && y, "sc_lucy_frame_gemm: null pointer");
+  SC_REQUIRE(ldx % 4 == 0 && ldw % 8 == 0 && K % 4 == 0 && (uintptr_t)x % 16 == 0 &&
+                 (uintptr_t)w % 16 == 0,
+             "sc_lucy_frame_gemm: rows must be 16-byte aligned (ldx %% 4, ldw %% 8, K %% 4)");
+  SC_REQUIRE((ln_w == nullptr) == (ln_b == nullptr) && (!ln_w || (st_in && nst_in > 0)),
+             "sc_lucy_frame_gemm: LayerNorm prologue needs weight, bias and statistics");
+  const bool cell = epi >= FR_CELL_UNFUSED;
+  const int ng = epi == FR_CELL_FUSED ? 5 : 4;
+  if (cell) {
+    SC_REQUIRE(N % (16 * ng) == 0, "sc_lucy_frame_gemm: N = %d gates x D, D a multiple of 16", N);
+    SC_REQUIRE(z && st_z && s, "sc_lucy_frame_gemm: cell outputs / state missing");
+    SC_REQUIRE(epi == FR_CELL_FUSED || K == N / ng, "sc_lucy_frame_gemm: unfused cell needs K == D");
+  } else {
+    SC_REQUIRE(epi == FR_PLAIN || st_out, "sc_lucy_frame_gemm: statistics output missing");
+  }
+  FrameGemmArgs a;
+  a.x = x; a.ldx = ldx; a.K = K; a.ln_w = ln_w; a.ln_b = ln_b; a.st_in = (const float4*)st_in;
+  a.nst_in = nst_in; a.eps = eps; a.w = w; a.ldw = ldw; a.bias = bias; a.B = B; a.N = N;
+  a.gstride = cell ? N / ng : 16;
+  a.y = y; a.ldy = ldy; a.st_out = (float4*)st_out; a.z = z; a.st_z = (float4*)st_z; a.s = s;
+  a.mask = mask;
+  hipStream_t st = (hipStream_t)stream;
+  if (w_dtype == SC_BF16) {
+    if (ln_w) dispatch_gemm<true, true>(epi, ng, a, st);
+    else dispatch_gemm<true, false>(epi, ng, a, st);
+  } else {
+    if (ln_w) dispatch_gemm<false, true>(epi, ng, a, st);
+    else dispatch_gemm<false, false>(epi, ng, a, st);
+  }
+  return launch_status("sc_lucy_frame_gemm");
+}
+
+extern "C" int sc_lucy_frame_cellb(const float* z, const void* st_z, int nst_z, const float* hp,
+                                   const void* st_h, int nst_h, const float* lnz_w,
+                                   const float* lnz_b, const float* lnh_w, const float* lnh_b,
+                                   float eps, float* h, float* out, int64_t ldo, const float* mask,
+                                   int B, int D, void* stream) {
+  clear_error();
+  SC_REQUIRE(B >= 0 && D > 0, "sc_lucy_frame_cellb: bad shape");
+  if (B == 0) return 0;
+  SC_REQUIRE(z && hp && h && out, "sc_lucy_frame_cellb: null pointer");
+  SC_REQUIRE((lnz_w == nullptr) == (lnz_b == nullptr) && (lnh_w == nullptr) == (lnh_b == nullptr) &&
+                 (!lnz_w || (st_z && nst_z > 0)) && (!lnh_w || (st_h && nst_h > 0)),
+             "sc_lucy_frame_cellb: LayerNorm needs weight, bias and statistics");
+  FrameCellArgs a{z, (const float4*)st_z, nst_z, hp, (const float4*)st_h, nst_h, lnz_w, lnz_b,
+                  lnh_w, lnh_b, eps, h, out, ldo, mask, B, D};
+  hipLaunchKernelGGL(lucy_frame_cellb, dim3(B), dim3(256), 0, (hipStream_t)stream, a);
+  return launch_status("sc_lucy_frame_cellb");
+}

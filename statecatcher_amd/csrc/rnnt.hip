@@ -360,6 +360,169 @@ __device__ __forceinline__ void ab_run(const RnntArgs& a, int b, int Tb, int Ub)
   }
 }
 
+// ONE WAVE per (sequence, direction) when U + 1 <= 64 PPL label positions (PPL <= 4; C5's U = 150
+// takes PPL = 3): lane l holds u = l PPL .. l PPL + PPL - 1, so a diagonal needs one DPP lane shift
+// (alpha: the previous lane's last u; beta: the next lane's first) and PPL independent
+// log-sum-exps -- no halo lanes, no LDS, no barrier (the multi-wave kernel above exchanges halos
+// through LDS with a workgroup barrier every K diagonals).  Re-centred on the wave max every
+// kAb1R diagonals (fp64 offsets, stored per re-centring; the gradient indexes them with kh =
+// kAb1R / 2).
+constexpr int kAb1R = 32;
+constexpr int kAb1P = 16;   // emission prefetch depth (diagonals)
+
+template <int PPL, bool BETA>
+__device__ __forceinline__ void ab1_run(const RnntArgs& a, int b, int Tb, int Ub) {
+  const int lane = threadIdx.x;
+  const int nd = Tb + Ub;
+  const int64_t base = (int64_t)b * a.ND * a.U1p;
+  constexpr uint32_t kDrop = 0x80000000u;
+  // byte offsets in a row: the node's own column (blank arc, stores) and its label arc's
+  // column (alpha: the arc from u - 1; beta: the arc from u itself)
+  uint32_t vb[PPL], vy[PPL];
+#pragma unroll
+  for (int j = 0; j < PPL; ++j) {
+    const int u = lane * PPL + j;
+    vb[j] = u <= Ub ? (uint32_t)(4 * u) : kDrop;
+    const int uy = BETA ? u : u - 1;
+    vy[j] = (uy >= 0 && uy < Ub && u <= Ub) ? (uint32_t)(4 * uy) : kDrop;
+  }
+  const uint32_t rowb = 4u * (uint32_t)a.U1p;
+  const int nbytes = (int)(rowb * (uint32_t)a.ND);
+  const __amdgpu_buffer_rsrc_t brs = __builtin_amdgcn_make_buffer_rsrc(a.ws.lpb + base, 0, nbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(a.ws.lpy + base, 0, nbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
+      (BETA ? a.ws.beta : a.ws.alpha) + base, 0, nbytes, 0x00020000);
+  double* offn = (BETA ? a.ws.offB : a.ws.offA) + (int64_t)b * a.ND;
+  if (lane == 0) offn[0] = 0.0;
+  // emissions of diagonal step i: alpha reads the arcs entering diagonal n = i from row n - 1,
+  // beta the arcs leaving row n = nd - 1 - i
+  auto row_of = [&](int i) {
+    const int r = BETA ? nd - 1 - min(i, nd - 1) : min(i, nd - 1) - 1;
+    return r < 0 ? 0 : r;
+  };
+  float ebA[kAb1P][PPL], eyA[kAb1P][PPL], ebB[kAb1P][PPL], eyB[kAb1P][PPL];
+  auto load = [&](float (&eb)[kAb1P][PPL], float (&ey)[kAb1P][PPL], int i0) {
+#pragma unroll
+    for (int s = 0; s < kAb1P; ++s) {
+      const uint32_t so = (uint32_t)row_of(i0 + s) * rowb;
+#pragma unroll
+      for (int j = 0; j < PPL; ++j) {
+        eb[s][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(brs, vb[j], so, 0));
+        ey[s][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(yrs, vy[j], so, 0));
+      }
+    }
+  };
+  float v[PPL];
+#pragma unroll
+  for (int j = 0; j < PPL; ++j) v[j] = kDeadR;
+  double off = 0.0;
+  auto body = [&](const float (&eb)[kAb1P][PPL], const float (&ey)[kAb1P][PPL], int i0)
+      __attribute__((always_inline)) {
+#pragma unroll
+    for (int s = 0; s < kAb1P; ++s) {
+      const int i = i0 + s;
+      if (i >= nd) break;
+      const int n = BETA ? nd - 1 - i : i;
+      float nb[PPL];   // the neighbour u -/+ 1 on the previous diagonal
+      if (!BETA) {
+        nb[0] = dpp_shr1(v[PPL - 1]);
+#pragma unroll
+        for (int j = 1; j < PPL; ++j) nb[j] = v[j - 1];
+      } else {
+        nb[PPL - 1] = dpp_shl1(v[0]);
+#pragma unroll
+        for (int j = 0; j + 1 < PPL; ++j) nb[j] = v[j + 1];
+      }
+#pragma unroll
+      for (int j = 0; j < PPL; ++j) {
+        const int u = lane * PPL + j;
+        const int t = n - u;
+        const bool valid = u <= Ub && t >= 0 && t < Tb;
+        float nv;
+        if (!BETA) {
+          nv = i == 0 ? (u == 0 ? 0.0f : kDeadR)
+                      : lse2_live(t >= 1 ? v[j] + eb[s][j] : kDeadR, u >= 1 ? nb[j] + ey[s][j] : kDeadR);
+        } else {
+          nv = i == 0 ? (u == Ub ? eb[s][j] : kDeadR)   // terminal blank of (Tb-1, Ub)
+                      : lse2_live(t + 1 < Tb ? v[j] + eb[s][j] : kDeadR, u < Ub ? nb[j] + ey[s][j] : kDeadR);
+        }
+        v[j] = valid ? fmaxf(nv, kDeadR) : kDeadR;
+      }
+      if ((i + 1) % kAb1R == 0) {   // re-centre on the wave max
+        float m = kDeadR;
+#pragma unroll
+        for (int j = 0; j < PPL; ++j) m = fmaxf(m, v[j]);
+        m = wave_max_dpp(m);
+        if (m > 0.5f * kDeadR) {   // all dead: keep the sentinel
+#pragma unroll
+          for (int j = 0; j < PPL; ++j) v[j] -= m;
+          off += (double)m;
+        }
+        if (lane == 0) offn[(i + 1) / kAb1R] = off;
+      }
+      const uint32_t so = (uint32_t)n * rowb;
+#pragma unroll
+      for (int j = 0; j < PPL; ++j) {
+        const int u = lane * PPL + j;
+        const int t = n - u;
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[j]), ors,
+                                              (u <= Ub && t >= 0 && t < Tb) ? vb[j] : kDrop, so, 0);
+      }
+    }
+  };
+  load(ebA, eyA, 0);
+  for (int i0 = 0; i0 < nd; i0 += 2 * kAb1P) {
+    load(ebB, eyB, i0 + kAb1P);
+    body(ebA, eyA, i0);
+    if (i0 + kAb1P >= nd) break;
+    load(ebA, eyA, i0 + 2 * kAb1P);
+    body(ebB, eyB, i0 + kAb1P);
+  }
+  if (!BETA) {
+    // the emission shift of every path, sum_t cb[t] + sum_{u<Ub} cy[u], fp64 in a fixed order
+    double cs = 0.0;
+    for (int i = lane; i < Tb + Ub; i += 64)
+      cs += (double)kshift(i < Tb ? a.ws.cmb[(int64_t)b * a.T + i] : a.ws.cmy[(int64_t)b * a.U1 + i - Tb]);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) cs += __shfl_xor(cs, o);
+#pragma unroll
+    for (int j = 0; j < PPL; ++j) {
+      if (lane * PPL + j == Ub) {   // log P = alpha(Tb-1, Ub) + its terminal blank (+ the shift)
+        const double lp = (double)v[j] + (double)a.ws.lpb[base + (int64_t)(nd - 1) * a.U1p + Ub] + off;
+        a.ws.logp2[b] = lp;
+        a.nll[b] = (float)(-(lp + cs) * 0.6931471805599453);
+      }
+    }
+  }
+}
+
+template <int PPL>
+__global__ void __launch_bounds__(64) rnnt_ab1_kernel(RnntArgs a) {
+  const bool is_beta = blockIdx.x >= a.B;
+  const int b = is_beta ? blockIdx.x - a.B : blockIdx.x;
+  const int Tb = clampr(a.flen[b], 0, a.T), Ub = clampr(a.llen[b], 0, a.Umax);
+  if (Tb == 0) {   // no frames: no alignment exists
+    if (!is_beta && threadIdx.x == 0) {
+      a.nll[b] = __builtin_huge_valf();
+      a.ws.logp2[b] = -__builtin_huge_val();
+    }
+    return;
+  }
+  if (is_beta) ab1_run<PPL, true>(a, b, Tb, Ub);
+  else ab1_run<PPL, false>(a, b, Tb, Ub);
+}
+
+// label positions per lane of the one-wave lattice (0: the multi-wave kernel).  SC_RNNT_AB1=0 in
+// the environment forces the multi-wave kernel (A/B timing in tools only).
+int ab1_ppl(int Umax) {
+  static const bool on = [] {
+    const char* e = getenv("SC_RNNT_AB1");
+    return !(e && e[0] == '0');
+  }();
+  const int ppl = (Umax + 1 + 63) / 64;
+  return (on && ppl <= 4) ? ppl : 0;
+}
+
 template <int K>
 __global__ void __launch_bounds__(1024) rnnt_ab_kernel(RnntArgs a) {
   const bool is_beta = blockIdx.x >= a.B;
@@ -477,6 +640,13 @@ __global__ void __launch_bounds__(256) rnnt_grad_kernel(RnntArgs a) {
 }
 
 void launch_ab(const RnntArgs& a, hipStream_t st) {
+  switch (ab1_ppl(a.Umax)) {
+    case 1: hipLaunchKernelGGL((rnnt_ab1_kernel<1>), dim3(2 * a.B), dim3(64), 0, st, a); return;
+    case 2: hipLaunchKernelGGL((rnnt_ab1_kernel<2>), dim3(2 * a.B), dim3(64), 0, st, a); return;
+    case 3: hipLaunchKernelGGL((rnnt_ab1_kernel<3>), dim3(2 * a.B), dim3(64), 0, st, a); return;
+    case 4: hipLaunchKernelGGL((rnnt_ab1_kernel<4>), dim3(2 * a.B), dim3(64), 0, st, a); return;
+    default: break;
+  }
   const int K = a.kh;
   const int nw = (a.U1 + (64 - K) - 1) / (64 - K);
   const size_t sh = 2 * (size_t)nw * (64 - K) * sizeof(float);
@@ -560,7 +730,8 @@ RnntArgs make_args(const void* x, int is_logits, int B, int T, int Umax, int V, 
   a.grad = grad;
   a.vec = 0;
   a.nvec = 0;
-  a.kh = ab_halo_k(Umax);
+  // diagonals per re-centring / 2 (the gradients' offset index)
+  a.kh = ab1_ppl(Umax) ? kAb1R / 2 : ab_halo_k(Umax);
   return a;
 }
 

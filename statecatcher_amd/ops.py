@@ -17,10 +17,13 @@ LAUNCH_EVENTS = None
 
 
 class _timed:
-    def __init__(self, name, t, nbytes):
+    """HIP events around a launch on t's stream (bench.py's per-kernel timing): algorithmic
+    bytes (HBM-bound kernels) or flops (MFMA-bound ones) per launch ride along."""
+
+    def __init__(self, name, t, nbytes, flops=0):
         self.rec = LAUNCH_EVENTS is not None
         if self.rec:
-            self.name, self.nbytes = name, nbytes
+            self.name, self.nbytes, self.flops = name, nbytes, flops
             self.stream = torch.cuda.current_stream(t.device)
             self.e0 = torch.cuda.Event(enable_timing=True)
             self.e1 = torch.cuda.Event(enable_timing=True)
@@ -33,7 +36,7 @@ class _timed:
     def __exit__(self, *exc):
         if self.rec:
             self.e1.record(self.stream)
-            LAUNCH_EVENTS.append((self.name, self.e0, self.e1, self.nbytes))
+            LAUNCH_EVENTS.append((self.name, self.e0, self.e1, self.nbytes, self.flops))
         return False
 
 
@@ -902,6 +905,39 @@ def lucy_step_cell(mode, g, h, s, out, lnz=None, lnh=None, u=None, hp=None, mask
     check(rc, "sc_lucy_step_cell")
 
 
+FRAME_PLAIN, FRAME_STATS, FRAME_CELL_UNFUSED, FRAME_CELL_FUSED = 0, 1, 2, 3
+
+
+def lucy_frame_gemm(epi, x, w, bias, y, st_out=None, ln=None, st_in=None, z=None, st_z=None,
+                    s=None, mask=None, eps=1e-5):
+    """One fused GEMM of the streaming frame (csrc/lucy_frame.hip, include/statecatcher.h
+    sc_lucy_frame_gemm): x fp32 [B, K] (row stride x.stride(0)), w fp32/bf16 [N, K], bias fp32
+    [N], y fp32; ln = (weight, bias) of a LayerNorm prologue over K with st_in its statistics
+    records ([n, B, 4] fp32).  No allocation: safe inside a hipGraph capture."""
+    B, K = x.shape
+    N = w.shape[0]
+    lw, lb = ln if ln is not None else (None, None)
+    rc = _lib.load().sc_lucy_frame_gemm(
+        int(epi), ptr(x), x.stride(0), K, ptr(lw), ptr(lb), ptr(st_in),
+        st_in.shape[0] if st_in is not None else 0, float(eps), ptr(w), dtype_code(w), w.stride(0),
+        ptr(bias), B, N, ptr(y), y.stride(0), ptr(st_out), ptr(z), ptr(st_z), ptr(s), ptr(mask),
+        stream_of(x))
+    check(rc, "sc_lucy_frame_gemm")
+
+
+def lucy_frame_cellb(z, hp, h, out, st_z=None, st_h=None, lnz=None, lnh=None, mask=None, eps=1e-5):
+    """h = (1 - sigmoid(LN_z z)) tanh(LN_h hp) + sigmoid(LN_z z) h, masked, in place; out = h
+    (sc_lucy_frame_cellb).  lnz / lnh (weight, bias) with their statistics records, or None."""
+    B, D = h.shape
+    zw, zb = lnz if lnz is not None else (None, None)
+    hw, hb = lnh if lnh is not None else (None, None)
+    rc = _lib.load().sc_lucy_frame_cellb(
+        ptr(z), ptr(st_z), st_z.shape[0] if st_z is not None else 0, ptr(hp), ptr(st_h),
+        st_h.shape[0] if st_h is not None else 0, ptr(zw), ptr(zb), ptr(hw), ptr(hb), float(eps),
+        ptr(h), ptr(out), out.stride(0), ptr(mask), B, D, stream_of(h))
+    check(rc, "sc_lucy_frame_cellb")
+
+
 # ------------------------------------------------------------------- feature frontend --------
 def fbank(audio, kind="mfcc", sample_rate=16000):
     """make_frontend(kind)(audio).transpose(-1, -2) on the GPU (fbank.hip): audio fp32
@@ -1581,7 +1617,8 @@ class AutocastLinearFn(torch.autograd.Function):
     def forward(ctx, x, w, b, cdt, bias_from=0):
         xc = x.to(cdt)
         wc = w.to(cdt)
-        y = torch.nn.functional.linear(xc, wc, None if b is None else b.to(cdt))
+        with _timed("xlstm_gemm", xc, 0, 2 * xc.numel() * wc.shape[0]):
+            y = torch.nn.functional.linear(xc, wc, None if b is None else b.to(cdt))
         ctx.save_for_backward(xc, wc)
         ctx.meta = (x.dtype, w.dtype, None if b is None else b.dtype)
         ctx.bias_from = bias_from
@@ -1602,9 +1639,14 @@ def _linear_grads(ctx, dy, need_x, need_w, need_b):
     dy2 = dy.reshape(-1, N).to(wc.dtype)
     x2 = xc.reshape(-1, K)
     dx = dw = db = None
+    gemm_flops = 2 * dy2.shape[0] * N * K
     if need_x:
-        dx = (dy2 @ wc).view(*dy.shape[:-1], K).to(xdt)
+        with _timed("xlstm_gemm", dy2, 0, gemm_flops):
+            dx = dy2 @ wc
+        dx = dx.view(*dy.shape[:-1], K).to(xdt)
     if need_w:
+        tw = _timed("xlstm_gemm", dy2, 0, gemm_flops)
+        tw.__enter__()
         dw = None
         if dy2.is_cuda and dy2.dtype == torch.bfloat16:
             dyc, xcc = dy2.contiguous(), x2.contiguous()
@@ -1624,7 +1666,9 @@ def _linear_grads(ctx, dy, need_x, need_w, need_b):
                     tail = win[256 - (N - n0):] if win is not None else \
                         _mm_f32(dyc[:, n0:].t(), xcc)
                     dw = torch.cat([head, tail])
-        dw = (dw if dw is not None else (dy2.t() @ x2).float()).to(wdt)
+        dw = (dw if dw is not None else (dy2.t() @ x2).float())
+        tw.__exit__()
+        dw = dw.to(wdt)
     if bdt is not None and need_b:
         f = ctx.bias_from
         if f and f < N and (f * dy2.element_size()) % 16 == 0:
@@ -1654,7 +1698,8 @@ class FusedLinearFn(torch.autograd.Function):
             off += r
         _image_jobs(jobs, list(ws))
         xc = x.to(cdt)
-        y = torch.nn.functional.linear(xc, wc, None if b is None else b.to(cdt))
+        with _timed("xlstm_gemm", xc, 0, 2 * xc.numel() * wc.shape[0]):
+            y = torch.nn.functional.linear(xc, wc, None if b is None else b.to(cdt))
         ctx.save_for_backward(xc, wc)
         ctx.meta = (x.dtype, ws[0].dtype, None if b is None else b.dtype)
         ctx.bias_from = bias_from

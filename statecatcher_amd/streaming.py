@@ -18,6 +18,16 @@ with h, s resident on the GPU in fp32 between calls and every buffer static, so 
 ``frames_per_call`` frames is captured once as a hipGraph (torch.cuda.CUDAGraph) and replayed:
 one host launch per block instead of ~(4-6 L + 2) kernel launches per frame.
 
+engine="frame" (the default where it applies: hidden_dim a multiple of 16) replaces the library
+GEMMs and the LayerNorm / cell kernels by the fused chain of csrc/lucy_frame.hip: per layer
+    a = x W_in^T + b_in (+ row statistics)            lucy_frame_gemm
+    gates on LN_in(a), cell stage in the epilogue     lucy_frame_gemm  (s, z, y / hp, statistics)
+    hp = y W_h^T + b_h (+ statistics)  [unfused]      lucy_frame_gemm
+    h = (1 - z~) tanh(LN_h hp) + z~ h                 lucy_frame_cellb
+then logits (lucy_frame_gemm) and the greedy step: 3-4 launches per layer instead of 5-6, no
+LayerNorm launch (statistics ride with the producing GEMM), MFMA on fp32 (exact f32) or bf16
+weights, fp32 activations.
+
 The decode is incremental: ``prev`` holds each stream's last argmax (-1 at stream start, as
 decoder.py's ``prev_token = None``), and emit[b, t] is the token decoder.py would append at
 frame t, or -1.  Frames with mask 0 (past a stream's end) keep state (lucyrnn.py:66-68) and
@@ -43,7 +53,7 @@ class StreamingLucyRNN:
     """
 
     def __init__(self, model: LucyRNN, batch: int, frames_per_call: int = 1,
-                 dtype=torch.float32, blank: int = 0, graph: bool = True):
+                 dtype=torch.float32, blank: int = 0, graph: bool = True, engine: str = "auto"):
         cfg = model.config
         dev = next(model.parameters()).device
         ops._lib.require_device(next(model.parameters()))
@@ -70,7 +80,41 @@ class StreamingLucyRNN:
                 e["w_h"], e["b_h"] = w(cell.W_h.weight), w(cell.W_h.bias)
             self.layers.append(e)
         self.w_out, self.b_out = w(model.output_proj.weight), w(model.output_proj.bias)
+        frame_ok = (D % 16 == 0 and self.Din % 8 == 0 and dtype in (torch.float32, torch.bfloat16))
+        if engine == "auto":
+            engine = "frame" if frame_ok else "library"
+        if engine == "frame" and not frame_ok:
+            raise ValueError("engine='frame' needs hidden_dim % 16 == 0, input width % 8 == 0 and "
+                             "fp32 / bf16 weights")
+        self.engine = engine
         z = lambda *s, dt=dtype: torch.zeros(*s, dtype=dt, device=dev)   # noqa: E731
+        if engine == "frame":
+            f32 = torch.float32
+            fb = lambda t: t.detach().float().contiguous()   # noqa: E731
+            for e, cell in zip(self.layers, model.layers):
+                e["b_in"] = fb(cell.input_proj.bias)
+                e["b_g"] = fb(cell.W_fused.bias[D:]) if cfg.fused_ops else fb(torch.cat(
+                    [m.bias for m in (cell.W_z, cell.W_k, cell.W_v, cell.W_decay)]))
+                if not cfg.fused_ops:
+                    e["b_h"] = fb(cell.W_h.bias)
+            self.b_out = fb(model.output_proj.bias)
+            self.x = z(K, B, self.Din, dt=f32)
+            self.mask = torch.ones(K, B, dtype=f32, device=dev)
+            self.fa, self.fz, self.fy, self.fhp = (z(B, D, dt=f32) for _ in range(4))
+            self.st_a = z(D // 64 if D % 64 == 0 else (D + 63) // 64, B, 4, dt=f32)
+            self.st_z = z(D // 16, B, 4, dt=f32)
+            self.st_h = z(D // 16, B, 4, dt=f32)
+            self.xo = [z(B, D, dt=f32) for _ in range(self.L)]
+            self.h = [z(B, D, dt=f32) for _ in range(self.L)]
+            self.s = [z(B, D, dt=f32) for _ in range(self.L)]
+            self.logits = z(K, B, self.V, dt=f32)
+            self.emit = torch.full((K, B), -1, dtype=torch.int32, device=dev)
+            self.prev = torch.full((B,), -1, dtype=torch.int32, device=dev)
+            self.graph = None
+            if graph:
+                self._capture()
+            self.reset()
+            return
         ng = 5 if cfg.fused_ops else 4
         self.x = z(K, B, self.Din)
         self.mask = torch.ones(K, B, dtype=torch.float32, device=dev)
@@ -88,7 +132,37 @@ class StreamingLucyRNN:
         self.reset()
 
     # ------------------------------------------------------------------------------ frame --
+    def _frame_fused_chain(self, j):
+        """One frame on csrc/lucy_frame.hip's fused kernels (engine="frame")."""
+        cfg, m, D = self.cfg, self.mask[j], self.D
+        inp = self.x[j]
+        for l, e in enumerate(self.layers):
+            ln = e["ln_in"] is not None
+            nst_a = (D + 63) // 64
+            ops.lucy_frame_gemm(ops.FRAME_STATS if ln else ops.FRAME_PLAIN, inp, e["w_in"], e["b_in"],
+                                self.fa, st_out=self.st_a[:nst_a] if ln else None)
+            lnin = dict(ln=e["ln_in"], st_in=self.st_a[:nst_a]) if ln else {}
+            if cfg.fused_ops:
+                ops.lucy_frame_gemm(ops.FRAME_CELL_FUSED, self.fa, e["w_g"], e["b_g"], self.fhp,
+                                    st_out=self.st_h, z=self.fz, st_z=self.st_z, s=self.s[l],
+                                    mask=m, **lnin)
+                st_h = self.st_h
+            else:
+                ops.lucy_frame_gemm(ops.FRAME_CELL_UNFUSED, self.fa, e["w_g"], e["b_g"], self.fy,
+                                    z=self.fz, st_z=self.st_z, s=self.s[l], mask=m, **lnin)
+                lnh = e["lnh"] is not None
+                st_h = self.st_h[:nst_a]
+                ops.lucy_frame_gemm(ops.FRAME_STATS if lnh else ops.FRAME_PLAIN, self.fy, e["w_h"],
+                                    e["b_h"], self.fhp, st_out=st_h if lnh else None)
+            ops.lucy_frame_cellb(self.fz, self.fhp, self.h[l], self.xo[l], st_z=self.st_z,
+                                 st_h=st_h, lnz=e["lnz"], lnh=e["lnh"], mask=m)
+            inp = self.xo[l]
+        ops.lucy_frame_gemm(ops.FRAME_PLAIN, inp, self.w_out, self.b_out, self.logits[j])
+        ops.ctc_greedy_step(self.logits[j], self.prev, self.emit[j], mask=m, blank=self.blank)
+
     def _frame(self, j):
+        if self.engine == "frame":
+            return self._frame_fused_chain(j)
         cfg, m = self.cfg, self.mask[j]
         inp = self.x[j]
         for l, e in enumerate(self.layers):

@@ -60,3 +60,24 @@ def test_invalid_arguments_rejected_without_gpu(lib):
     # empty problems are no-ops
     assert lib.sc_lucy_scan_fwd(null, 0, null, null, null, null, null, null, 0, 5, 5, 1, 1, 1, 64, 1, 1, null, null) == 0
     assert lib.sc_ctc_greedy_decode(null, 0, 0, 5, 5, 1, 1, null, 0, null, null, null) == 0
+
+
+def test_round4_entry_points_reject_bad_arguments_without_gpu(lib):
+    """The split-precision scan and the streaming frame kernels validate before launching."""
+    null = ctypes.c_void_p()
+    # split planes need a 16-bit out
+    rc = lib.sc_lucy_scan_fwd_split(null, 0, null, null, null, null, null, null, null, null, 1, 1, 64,
+                                    1, 1, 1, 64, 1, 1, null, null)
+    assert rc == -1 and b"16-bit" in lib.sc_last_error()
+    # frame GEMM: bad epilogue, bad weight dtype, cell shape
+    rc = lib.sc_lucy_frame_gemm(9, null, 4, 4, null, null, null, 0, ctypes.c_float(1e-5), null, 0, 8,
+                                null, 1, 64, null, 4, null, null, null, null, null, null)
+    assert rc == -1 and b"epilogue" in lib.sc_last_error()
+    rc = lib.sc_lucy_frame_gemm(0, null, 4, 4, null, null, null, 0, ctypes.c_float(1e-5), null, 2, 8,
+                                null, 1, 64, null, 4, null, null, null, null, null, null)
+    assert rc == -1 and b"fp32 or bf16" in lib.sc_last_error()
+    assert lib.sc_lucy_frame_gemm(0, null, 4, 4, null, null, null, 0, ctypes.c_float(1e-5), null, 0,
+                                  8, null, 0, 64, null, 4, null, null, null, null, null, null) == 0
+    rc = lib.sc_lucy_frame_cellb(null, null, 0, null, null, 0, null, null, null, null,
+                                 ctypes.c_float(1e-5), null, null, 4, null, 1, 16, null)
+    assert rc == -1 and b"null" in lib.sc_last_error()

@@ -85,11 +85,12 @@ def test_ctc_full_size_vs_aten_cpu():
     assert ours <= max(aten32, 1e-4)
 
 
-@pytest.mark.parametrize("U", [57, 300, 1007])
+@pytest.mark.parametrize("U", [57, 100, 150, 200, 300, 1007])
 def test_ctc_long_targets_many_waves_vs_aten_cpu(U):
-    """Targets spanning 1-16 waves of state pairs (K = 8 / 4 steps between halo exchanges), with
-    runs of repeated labels (no skip transition) and blank-free stretches, vs ATen fp64 on CPU;
-    U = 1007 is the longest target the ABI accepts."""
+    """Targets from the one-wave lattice (U + 1 <= 256 pairs: 1, 2, 3 and 4 pairs per lane at
+    U = 57, 100, 150, 200) to the multi-wave one (U = 300, 1007: 6 and 16 waves, K = 24 / 4 steps
+    between halo exchanges), with runs of repeated labels (no skip transition) and blank-free
+    stretches, vs ATen fp64 on CPU; U = 1007 is the longest target the ABI accepts."""
     g = torch.Generator().manual_seed(U)
     B, V = 2, 40
     T = 2 * U + 40

@@ -37,8 +37,11 @@ def ref(x, labels, fl, ll, logits, reduction="mean", average_frames=False):
     return loss, costs, g
 
 
+# one-wave lattice with 1, 2, 3, 4 label positions per lane (U + 1 <= 64, 128, 192, 256), then the
+# multi-wave one (last: 15 waves, K = 8)
 @pytest.mark.parametrize("B,T,U,V", [(3, 7, 4, 11), (2, 1, 3, 5), (2, 9, 0, 6), (4, 40, 12, 33),
-                                     (2, 130, 70, 17), (2, 24, 800, 5)])   # last: 15 waves, K = 8
+                                     (2, 130, 70, 17), (2, 60, 150, 9), (2, 30, 220, 7),
+                                     (2, 24, 800, 5)])
 @pytest.mark.parametrize("logits", [True, False])
 def test_rnnt_dense_vs_oracle(B, T, U, V, logits):
     x, labels, fl, ll = make(B, T, U, V, seed=B * 100 + T + U)

@@ -81,8 +81,8 @@ def oracle_stream(p, x, masks, L, fused, ln):
 
 @pytest.mark.parametrize("fused", [True, False])
 @pytest.mark.parametrize("ln", [True, False])
-@pytest.mark.parametrize("D", [128, 200])
-def test_streaming_vs_oracle_ragged(fused, ln, D):
+@pytest.mark.parametrize("D,engine", [(128, "frame"), (128, "library"), (200, "auto")])
+def test_streaming_vs_oracle_ragged(fused, ln, D, engine):
     import statecatcher_amd as sc
     from statecatcher_amd.streaming import StreamingLucyRNN
     torch.manual_seed(D + 2 * fused + ln)
@@ -99,7 +99,8 @@ def test_streaming_vs_oracle_ragged(fused, ln, D):
     p = oracle_params(m)
     rl, rh, rs = oracle_stream(p, x.double().numpy(), masks.numpy(), L, fused, ln)
     for K, graph in ((1, True), (4, True), (2, False)):
-        st = StreamingLucyRNN(m, batch=B, frames_per_call=K, graph=graph)
+        st = StreamingLucyRNN(m, batch=B, frames_per_call=K, graph=graph, engine=engine)
+        assert st.engine == ("library" if D == 200 else engine)
         toks, logits = st.decode(x.to(DEV), masks.to(DEV), return_logits=True)
         close(logits, rl, rtol=1e-4, afrac=1e-4)
         h, s = st.state()
@@ -132,6 +133,37 @@ def test_streaming_bf16_tracks_fp32():
             outs.append(lg.float())
     rel_ac = float((torch.stack(outs, 1) - l32).norm() / l32.norm())
     assert rel < 1.5 * rel_ac + 1e-3, (rel, rel_ac)
+
+
+@pytest.mark.parametrize("fused", [True, False])
+def test_frame_engine_equals_library_engine_at_bench_size(fused):
+    """The fused frame chain (csrc/lucy_frame.hip) against the library-GEMM engine on the stream
+    bench's model (6 x 512, V 1024, layer_norm on), 64 streams with ragged masks, fp32: logits,
+    state and tokens."""
+    import statecatcher_amd as sc
+    from statecatcher_amd.streaming import StreamingLucyRNN
+    torch.manual_seed(7 + fused)
+    m = sc.LucyRNN(sc.LucyRNNConfig(input_dim=80, hidden_dim=512, num_layers=6, vocab_size=1024,
+                                    is_training=False, fused_ops=fused)).to(DEV)
+    with torch.no_grad():
+        m.output_proj.weight.normal_(0.0, 0.05)
+    B, T = 64, 24
+    x = torch.randn(B, T, 80, device=DEV)
+    lens = torch.randint(0, T + 1, (B,))
+    masks = (torch.arange(T)[None, :] < lens[:, None]).to(DEV)
+    out = {}
+    for engine in ("frame", "library"):
+        st = StreamingLucyRNN(m, B, 8, engine=engine)
+        toks, lg = st.decode(x, masks, return_logits=True)
+        out[engine] = (toks, lg.float(), st.state())
+    (tf, lf, (hf, sf)), (tl, ll, (hl, sl)) = out["frame"], out["library"]
+    rel = float((lf - ll).norm() / ll.norm())
+    print(f"frame vs library engine (fused={fused}): logits rel {rel:.2e}")
+    assert rel < 1e-4
+    for a, b in zip(hf + sf, hl + sl):
+        assert float((a - b).norm() / max(float(b.norm()), 1e-30)) < 1e-4
+    lg = ll.cpu().numpy()
+    assert tf == odec.ctc_greedy(lf.cpu().numpy(), lens.numpy())
 
 
 def test_streaming_reset_subset_and_blocks_equal_one_pass():

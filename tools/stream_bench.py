@@ -50,9 +50,10 @@ def main():
     N = args.frames
     for B in [int(b) for b in args.batches.split(",")]:
         x = torch.randn(B, N, 80, device=dev)
-        for dt in (torch.float32, torch.bfloat16):
-            for K, graph in ((1, True), (8, True), (1, False)):
-                st = StreamingLucyRNN(m, B, K, dtype=dt, graph=graph)
+        for engine, dt, K, graph in [(e, d, k, g) for e in ("frame", "library")
+                                     for d in (torch.float32, torch.bfloat16)
+                                     for k, g in ((1, True), (8, True), (1, False))]:
+                st = StreamingLucyRNN(m, B, K, dtype=dt, graph=graph, engine=engine)
                 blocks = [x[:, i:i + K].contiguous() for i in range(0, N, K)]
                 it = iter(range(10 ** 9))
 
@@ -60,7 +61,7 @@ def main():
                     st.step(blocks[next(it) % len(blocks)])
                 nb = N // K
                 dt_s = timed(run, nb)
-                print(json.dumps({"impl": "hip_step" + ("_graph" if graph else "_eager"),
+                print(json.dumps({"impl": f"hip_{engine}" + ("_graph" if graph else "_eager"),
                                   "dtype": str(dt).split(".")[-1], "B": B, "K": K,
                                   "fused": args.fused, "frames": nb * K,
                                   "stream_frames_per_s": round(B * nb * K / dt_s, 1),
