@@ -170,8 +170,13 @@ def build_workload(args, device):
                         f"{args.segments}-segment carry")
     split = args.output_head == "split"
     if args.dtype == "bf16":
-        conf["output_projection"] = ("bf16 GEMM on split-precision operands, fp32 logits" if split
-                                     else "bf16 operands and logits")
+        from statecatcher_amd import ops as _ops
+        conf["output_projection"] = (
+            {"emis": "bf16 GEMM and logits; the lattice's emission columns to fp32 accuracy from "
+                     "split-precision operands (side array)",
+             "labels": "bf16 GEMM on split-precision operands, fp32 logits",
+             "full": "split-precision GEMM, fp32 logits"}.get(_ops.HEAD_SPLIT, _ops.HEAD_SPLIT)
+            if split else "bf16 operands and logits")
     return model, CTCLoss(blank=0, zero_infinity=True, fused_head=split), list(model.parameters()), \
         dict(mode="ctc"), conf
 

@@ -204,6 +204,29 @@ int sc_ctc_bwd(const void* x, int x_dtype, int is_logits, int B, int T, int V,
                const void* workspace, size_t workspace_bytes, void* stream);
 
 /*
+ * sc_ctc_fwd / sc_ctc_bwd with the emission columns given exactly (is_logits = 1): ex fp32
+ * [B][T][max_target_len + 1] (strides ex_stride_b, ex_stride_t; column stride 1), ex[b][t][0] =
+ * the blank's logit, ex[b][t][1 + u] = label u's, replace x's values at those columns in the
+ * lattice's emissions and in the gradient row (softmax term and occupancy); the row's
+ * log-sum-exp still reads x.  For a bf16 output projection whose emission columns were computed
+ * to fp32 accuracy (statecatcher_amd.ops.CTCHeadFn): the same head, model.py:68-71 +
+ * lucyrnn_triton.py:150, with the logits' bf16 rounding kept out of the lattice.
+ */
+int sc_ctc_fwd_ex(const void* x, int x_dtype, int is_logits, int B, int T, int V,
+                  int64_t stride_b, int64_t stride_t,
+                  const int64_t* targets, int64_t target_stride, int max_target_len,
+                  const int64_t* in_lens, const int64_t* tgt_lens, int blank,
+                  const float* ex, int64_t ex_stride_b, int64_t ex_stride_t,
+                  float* nll, void* workspace, size_t workspace_bytes, void* stream);
+int sc_ctc_bwd_ex(const void* x, int x_dtype, int is_logits, int B, int T, int V,
+                  int64_t stride_b, int64_t stride_t,
+                  const int64_t* targets, int64_t target_stride, int max_target_len,
+                  const int64_t* in_lens, const int64_t* tgt_lens, int blank,
+                  const float* ex, int64_t ex_stride_b, int64_t ex_stride_t,
+                  const float* nll, const float* scale, void* grad, int grad_dtype,
+                  const void* workspace, size_t workspace_bytes, void* stream);
+
+/*
  * The reduction nn.CTCLoss(reduction='mean', zero_infinity=True) applies to sc_ctc_fwd's nll
  * (train.py:142): loss[0] = mean_b(nll_b / max(U_b, 1)) with infinite nll_b counted as 0, and
  * factor[b] = d loss / d nll_b (0 for infinite nll_b), the `scale` sc_ctc_bwd takes times the

@@ -19,7 +19,13 @@
 //                     tools/ctc_precision.py)
 //   ctc_chain_kernel  per b: for every target position the next position with the same label,
 //                     so label occupancies are summed in a fixed order (deterministic, no atomics)
-//   ctc_ab_kernel     one workgroup per (sequence, direction): 2B workgroups run alpha forward
+//   ctc_lin_kernel    (Umax <= 255, the default) ONE WAVE per (sequence, direction), 2B waves:
+//                     the lattice in linear probability space, fp64, renormalised every 16 steps
+//                     by exact powers of two — five full-rate fp64 adds / multiplies per state
+//                     pair and step instead of five quarter-rate exp2 / log2 (see lin_run); falls
+//                     back per sequence to ab1_run (the same one-wave layout in fp32 log space)
+//                     when an emission or the whole wave would underflow
+//   ctc_ab_kernel     (Umax > 255) one workgroup per (sequence, direction): 2B workgroups run alpha forward
 //                     and beta backward concurrently.  Two states (a blank and its label) per
 //                     lane; each wave also carries a K-pair halo of its neighbour's pairs so it
 //                     advances K steps with DPP wave_shr:1 / wave_shl:1 only (no LDS, no
@@ -55,6 +61,10 @@ struct CtcWs {
   double* ll2s;   // [B]        base-2 log-likelihood of the SHIFTED lattice (log2 p - sum_t c_t)
   int* chain;     // [B,Um]
   int* first;     // [B,Um]
+  // one-wave family (Umax <= 255) only:
+  float* ylin;    // [B,T,Sp]   linear shifted emissions 2^(lpe) (0: dead)
+  int* flag;      // [3][B]     tiny[b]: a live emission below 2^-kTiny (the linear lattice is not
+                  //            used); lin[dir][b]: that direction's rows are linear fp64 values
 };
 
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -62,9 +72,13 @@ static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 // states per lane for a given max state count
 static int states_per_lane(int S) { return (S + 63) / 64; }
 
+static int lin_ppl(int Umax);
+
 static size_t ws_layout(int B, int T, int Umax, CtcWs* w, void* base) {
   const int S = 2 * Umax + 1;
   const int Sp = 64 * states_per_lane(S);
+  const bool lin = lin_ppl(Umax) > 0;
+  const size_t ab = lin ? 8 : 4;   // alpha / beta element: fp64 (linear) rows or fp32 (log)
   const int Um = Umax > 0 ? Umax : 1;
   char* p = (char*)base;
   size_t off = 0;
@@ -76,14 +90,16 @@ static size_t ws_layout(int B, int T, int Umax, CtcWs* w, void* base) {
   CtcWs t;
   t.lse = (float*)take((size_t)B * T * 4);
   t.lpe = (float*)take((size_t)B * T * Sp * 4);
-  t.alpha = (float*)take((size_t)B * T * Sp * 4);
-  t.beta = (float*)take((size_t)B * T * Sp * 4);
+  t.alpha = (float*)take((size_t)B * T * Sp * ab);
+  t.beta = (float*)take((size_t)B * T * Sp * ab);
   t.offA = (double*)take((size_t)B * T * 8);
   t.offB = (double*)take((size_t)B * T * 8);
   t.cst = (float*)take((size_t)B * T * 4);
   t.ll2s = (double*)take((size_t)B * 8);
   t.chain = (int*)take((size_t)B * Um * 4);
   t.first = (int*)take((size_t)B * Um * 4);
+  t.ylin = lin ? (float*)take((size_t)B * T * Sp * 4) : nullptr;
+  t.flag = lin ? (int*)take((size_t)3 * B * 4) : nullptr;
   if (w) *w = t;
   return off;
 }
@@ -100,6 +116,8 @@ struct CtcArgs {
   const void* x;
   int is_logits, B, T, V, S, Sp, Umax, blank;
   int kh;   // steps between halo exchanges of ctc_ab_kernel (re-centring every 2 kh steps)
+  int lin;      // the one-wave family (ctc_lin_kernel) runs the lattice
+  int apitch;   // floats per alpha / beta row (2 Sp in the one-wave family: room for fp64)
   int64_t sb, stt;
   const int64_t* tg;
   int64_t tgs;
@@ -109,6 +127,10 @@ struct CtcArgs {
   CtcWs ws;
   const float* scale;
   void* grad;
+  // optional emission logits (sc_ctc_*_ex): ex[b][t][0] the blank's logit, ex[b][t][1 + u] label
+  // u's, fp32 — what the lattice and the gradient's emission columns read instead of x
+  const float* ex;
+  int64_t exb, ext;
 };
 
 __device__ __forceinline__ int clampi(int64_t v, int lo, int hi) {
@@ -123,6 +145,8 @@ __device__ __forceinline__ int state_label(const int64_t* tg, int s, int blank, 
 }
 
 // ---------------------------------------------------------------------------- emissions -----
+constexpr float kTiny = 120.0f;   // (2^-120: a normal fp32 with 6 bits of headroom)
+
 template <int DT>
 __global__ void __launch_bounds__(256) ctc_emit_kernel(CtcArgs a) {
   using E = Elem<DT>;
@@ -169,15 +193,28 @@ __global__ void __launch_bounds__(256) ctc_emit_kernel(CtcArgs a) {
   const int Sb = 2 * clampi(a.tgt_lens[b], 0, a.Umax) + 1;
   const int64_t* tg = a.tg + (int64_t)b * a.tgs;
   float* out = a.ws.lpe + row * a.Sp;
+  const float* exr = a.ex ? a.ex + (int64_t)b * a.exb + (int64_t)t * a.ext : nullptr;
   auto lp2 = [&](int s) {
-    return fmaxf((E::ld(p[state_label(tg, s, a.blank, a.V)]) - lse) * kLog2e, -1e30f);
+    const float xl = exr ? exr[(s + 1) >> 1] : E::ld(p[state_label(tg, s, a.blank, a.V)]);
+    return fmaxf((xl - lse) * kLog2e, -1e30f);
   };
   float c = -1e30f;
   for (int s = lane; s < Sb; s += 64) c = fmaxf(c, lp2(s));
   c = wave_max_dpp(c);
   if (!(c > -1e29f)) c = 0.0f;   // every state dead (or NaN): no shift, the sentinel stays
-  for (int s = lane; s < a.Sp; s += 64) out[s] = s < Sb ? fmaxf(lp2(s) - c, -1e30f) : -1e30f;
+  bool tiny = false;
+  for (int s = lane; s < a.Sp; s += 64) {
+    const float e = s < Sb ? fmaxf(lp2(s) - c, -1e30f) : -1e30f;
+    out[s] = e;
+    if (a.lin) {
+      // linear emission for ctc_lin_kernel; a live one below 2^-kTiny sends the sequence to the
+      // log-space lattice (fp32 would lose it, and it may carry every path)
+      tiny |= e > -1e29f && e < -kTiny;
+      a.ws.ylin[row * a.Sp + s] = e > -1e29f ? exp2_(e) : 0.0f;
+    }
+  }
   if (lane == 0) a.ws.cst[row] = c;
+  if (a.lin && __ballot(tiny) && lane == 0) a.ws.flag[b] = 1;   // (every writer stores 1)
 }
 
 // ---------------------------------------------------------------------------- chains --------
@@ -517,7 +554,7 @@ __global__ void __launch_bounds__(1024) ctc_ab_kernel(CtcArgs a) {
 // 2 PPL chains of a step fill each other's issue gaps.  (The multi-wave kernel above spends a
 // workgroup barrier every K steps on its halo exchange and a third of its lanes on halo pairs.)
 // Re-centred on the wave max every kAb1R steps (fp64 offsets, stored per re-centring).
-constexpr int kAb1R = 32;
+constexpr int kAb1R = 16;   // (also the linear lattice's renormalisation period: same offsets)
 constexpr int kAb1P = 16;   // emission prefetch depth (steps)
 
 template <int PPL, bool BETA>
@@ -543,12 +580,12 @@ __device__ __forceinline__ void ab1_run(const CtcArgs& a, int b, int Tb, int Ub)
     }
     vo[j] = p < npairs ? (uint32_t)(8 * p) : kDrop;
   }
-  const uint32_t rowb = (uint32_t)(a.Sp * 4);
+  const uint32_t rowb = (uint32_t)(a.Sp * 4), orowb = (uint32_t)(a.apitch * 4);
   const __amdgpu_buffer_rsrc_t ers = __builtin_amdgcn_make_buffer_rsrc(
       a.ws.lpe + (int64_t)b * a.T * a.Sp, 0, (int)(rowb * (uint32_t)a.T), 0x00020000);
   const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
-      (BETA ? a.ws.beta : a.ws.alpha) + (int64_t)b * a.T * a.Sp, 0, (int)(rowb * (uint32_t)a.T),
-      0x00020000);
+      (BETA ? a.ws.beta : a.ws.alpha) + (int64_t)b * a.T * a.apitch, 0,
+      (int)(orowb * (uint32_t)a.T), 0x00020000);
   double* offn = (BETA ? a.ws.offB : a.ws.offA) + (int64_t)b * a.T;
   if (lane == 0) offn[0] = 0.0;
   auto tstep = [&](int i) { return BETA ? Tb - 1 - i : i; };
@@ -622,7 +659,7 @@ __device__ __forceinline__ void ab1_run(const CtcArgs& a, int b, int Tb, int Ub)
         }
         if (lane == 0) offn[(i + 1) / kAb1R] = off;
       }
-      const uint32_t so = (uint32_t)tstep(i) * rowb;
+      const uint32_t so = (uint32_t)tstep(i) * orowb;
 #pragma unroll
       for (int j = 0; j < PPL; ++j)
         __builtin_amdgcn_raw_buffer_store_b64(
@@ -667,8 +704,189 @@ __device__ __forceinline__ void ab1_run(const CtcArgs& a, int b, int Tb, int Ub)
   }
 }
 
+// Linear-domain one-wave lattice (the default for Umax <= 255).  The same pair-per-lane layout
+// as ab1_run, but the values are probabilities in fp64: one step of a pair is
+//   alpha:  B' = (B + L[p-1]) e(2p);          L' = (L + B + skip L[p-1]) e(2p+1)
+//   beta:   B' = (B + L) e(2p);               L' = (L + B[p+1] + skip L[p+1]) e(2p+1)
+// five fp64 adds / multiplies (full rate on gfx950's vector ALU) instead of five exp2 / log2 on
+// the quarter-rate transcendental unit, and exact 0 is "dead" (the DPP shifts' bound_ctrl zero is
+// the right boundary value).  Every kAb1R steps the wave max is renormalised to [0.5, 1) by an
+// exact power of two (v_ldexp_f64: no rounding), its exponent added to the fp64 offset, which the
+// gradient reads exactly as the log-space kernels' re-centring offsets (log2 alpha = log2(row) +
+// offset).  fp64 keeps 2^-1022 of range below the wave max between renormalisations (fp32 log
+// space keeps all of it; a state 2^1000 below the max that later carries the likelihood is the
+// one case the two differ).  Falls back to the log-space lattice (ab1_run) for a sequence whose
+// live emissions reach below 2^-kTiny (the emit kernel's flag) and for a direction whose wave
+// max underflows to 0 at a renormalisation or whose final likelihood does: then the rows are
+// rewritten in fp32 log space and flag[1 + dir][b] says so to the gradient.
+__device__ __forceinline__ double dpp_shr1d(double v) {   // lane-1's value (lane 0: 0)
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), 0x138, 0xf, 0xf, true);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), 0x138, 0xf, 0xf, true);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double dpp_shl1d(double v) {   // lane+1's value (lane 63: 0)
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), 0x130, 0xf, 0xf, true);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), 0x130, 0xf, 0xf, true);
+  return __hiloint2double(hi, lo);
+}
+typedef double d2v __attribute__((ext_vector_type(2)));
+
+template <int PPL, bool BETA>
+__device__ __forceinline__ bool lin_run(const CtcArgs& a, int b, int Tb, int Ub) {
+  const int lane = threadIdx.x;
+  const int64_t* tg = a.tg + (int64_t)b * a.tgs;
+  const int npairs = a.Sp / 2;
+  double skip[PPL];
+  uint32_t vo[PPL], oo[PPL];   // emission pair / output pair byte offsets (kDrop past the row)
+  constexpr uint32_t kDrop = 0x80000000u;
+#pragma unroll
+  for (int j = 0; j < PPL; ++j) {
+    const int p = lane * PPL + j;
+    bool sk = false;
+    if (p < Ub) {
+      const int lab = (int)tg[p];
+      if (!BETA) {
+        sk = p >= 1 && lab != a.blank && lab != (int)tg[p - 1];
+      } else if (p + 1 < Ub) {
+        const int l2 = (int)tg[p + 1];
+        sk = l2 != a.blank && l2 != lab;
+      }
+    }
+    skip[j] = sk ? 1.0 : 0.0;
+    vo[j] = p < npairs ? (uint32_t)(8 * p) : kDrop;
+    oo[j] = p < npairs ? (uint32_t)(16 * p) : kDrop;
+  }
+  const uint32_t rowb = (uint32_t)(a.Sp * 4), orowb = (uint32_t)(a.apitch * 4);
+  const __amdgpu_buffer_rsrc_t ers = __builtin_amdgcn_make_buffer_rsrc(
+      a.ws.ylin + (int64_t)b * a.T * a.Sp, 0, (int)(rowb * (uint32_t)a.T), 0x00020000);
+  const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
+      (BETA ? a.ws.beta : a.ws.alpha) + (int64_t)b * a.T * a.apitch, 0,
+      (int)(orowb * (uint32_t)a.T), 0x00020000);
+  double* offn = (BETA ? a.ws.offB : a.ws.offA) + (int64_t)b * a.T;
+  if (lane == 0) offn[0] = 0.0;
+  auto tstep = [&](int i) { return BETA ? Tb - 1 - i : i; };
+  f2v bufA[kAb1P][PPL], bufB[kAb1P][PPL];
+  auto load = [&](f2v (&buf)[kAb1P][PPL], int i0) {
+#pragma unroll
+    for (int s = 0; s < kAb1P; ++s) {
+      const uint32_t so = (uint32_t)tstep(min(i0 + s, Tb - 1)) * rowb;
+#pragma unroll
+      for (int j = 0; j < PPL; ++j)
+        buf[s][j] = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(ers, vo[j], so, 0));
+    }
+  };
+  double vB[PPL], vL[PPL];
+#pragma unroll
+  for (int j = 0; j < PPL; ++j) vB[j] = vL[j] = 0.0;
+  double off = 0.0;
+  bool fail = false;
+  auto body = [&](const f2v (&buf)[kAb1P][PPL], int i0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int s = 0; s < kAb1P; ++s) {
+      const int i = i0 + s;
+      if (i >= Tb) break;
+      if (i == 0) {
+#pragma unroll
+        for (int j = 0; j < PPL; ++j) {
+          const int p = lane * PPL + j;
+          vB[j] = (p <= Ub && p == (BETA ? Ub : 0)) ? (double)buf[s][j].x : 0.0;
+          vL[j] = (p < Ub && p == (BETA ? Ub - 1 : 0)) ? (double)buf[s][j].y : 0.0;
+        }
+      } else if (!BETA) {
+        double prevL[PPL];
+        prevL[0] = dpp_shr1d(vL[PPL - 1]);
+#pragma unroll
+        for (int j = 1; j < PPL; ++j) prevL[j] = vL[j - 1];
+#pragma unroll
+        for (int j = 0; j < PPL; ++j) {
+          const double nb = (vB[j] + prevL[j]) * (double)buf[s][j].x;
+          const double nl = __builtin_fma(skip[j], prevL[j], vL[j] + vB[j]) * (double)buf[s][j].y;
+          vB[j] = nb;
+          vL[j] = nl;
+        }
+      } else {
+        double nB[PPL], nL[PPL];
+        nB[PPL - 1] = dpp_shl1d(vB[0]);
+        nL[PPL - 1] = dpp_shl1d(vL[0]);
+#pragma unroll
+        for (int j = 0; j + 1 < PPL; ++j) {
+          nB[j] = vB[j + 1];
+          nL[j] = vL[j + 1];
+        }
+#pragma unroll
+        for (int j = 0; j < PPL; ++j) {
+          const double nb = (vB[j] + vL[j]) * (double)buf[s][j].x;
+          const double nl = __builtin_fma(skip[j], nL[j], vL[j] + nB[j]) * (double)buf[s][j].y;
+          vB[j] = nb;
+          vL[j] = nl;
+        }
+      }
+      if ((i + 1) % kAb1R == 0) {   // renormalise the wave max to [0.5, 1) (exact)
+        double m = 0.0;
+#pragma unroll
+        for (int j = 0; j < PPL; ++j) m = fmax(m, fmax(vB[j], vL[j]));
+        int e = 0;
+        (void)frexp(m, &e);
+        const float E = wave_max_dpp(m > 0.0 ? (float)e : -1e9f);
+        if (E < -1e8f) {   // every state underflowed (or the lattice died): log space instead
+          fail = true;
+          return;
+        }
+        const int ie = (int)E;
+#pragma unroll
+        for (int j = 0; j < PPL; ++j) {
+          vB[j] = ldexp(vB[j], -ie);
+          vL[j] = ldexp(vL[j], -ie);
+        }
+        off += (double)ie;
+        if (lane == 0) offn[(i + 1) / kAb1R] = off;
+      }
+      const uint32_t so = (uint32_t)tstep(i) * orowb;
+#pragma unroll
+      for (int j = 0; j < PPL; ++j)
+        __builtin_amdgcn_raw_buffer_store_b128(
+            __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, d2v{vB[j], vL[j]}),
+            ors, oo[j], so, 0);
+    }
+  };
+  load(bufA, 0);
+  for (int i0 = 0; i0 < Tb; i0 += 2 * kAb1P) {
+    load(bufB, i0 + kAb1P);
+    body(bufA, i0);
+    if (fail || i0 + kAb1P >= Tb) break;
+    load(bufA, i0 + 2 * kAb1P);
+    body(bufB, i0 + kAb1P);
+    if (fail) break;
+  }
+  if (fail) return false;
+  if (!BETA) {
+    // P = alpha_{Tb-1}(2Ub) + alpha_{Tb-1}(2Ub-1), fixed-order fp64 sums
+    double c = 0.0;
+#pragma unroll
+    for (int j = 0; j < PPL; ++j) {
+      const int p = lane * PPL + j;
+      if (p == Ub) c += vB[j];
+      if (p == Ub - 1) c += vL[j];
+    }
+    double cs = 0.0;
+    for (int t = lane; t < Tb; t += 64) cs += (double)a.ws.cst[(int64_t)b * a.T + t];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      c += __shfl_xor(c, o);
+      cs += __shfl_xor(cs, o);
+    }
+    if (!(c > 0.0)) return false;   // underflowed at the end (or infeasible): log space decides
+    if (lane == 0) {
+      const double ll2s = log2(c) + off;
+      a.ws.ll2s[b] = ll2s;
+      a.nll[b] = (float)(-(ll2s + cs) * 0.6931471805599453);
+    }
+  }
+  return true;
+}
+
 template <int PPL>
-__global__ void __launch_bounds__(64) ctc_ab1_kernel(CtcArgs a) {
+__global__ void __launch_bounds__(64) ctc_lin_kernel(CtcArgs a) {
   const bool is_beta = blockIdx.x >= a.B;
   const int b = is_beta ? blockIdx.x - a.B : blockIdx.x;
   const int Tb = clampi(a.in_lens[b], 0, a.T);
@@ -680,15 +898,20 @@ __global__ void __launch_bounds__(64) ctc_ab1_kernel(CtcArgs a) {
     }
     return;
   }
-  if (is_beta) ab1_run<PPL, true>(a, b, Tb, Ub);
-  else ab1_run<PPL, false>(a, b, Tb, Ub);
+  bool lin = uniform(a.ws.flag[b]) == 0;
+  if (lin) lin = is_beta ? lin_run<PPL, true>(a, b, Tb, Ub) : lin_run<PPL, false>(a, b, Tb, Ub);
+  if (!lin) {
+    if (is_beta) ab1_run<PPL, true>(a, b, Tb, Ub);
+    else ab1_run<PPL, false>(a, b, Tb, Ub);
+  }
+  if (threadIdx.x == 0) a.ws.flag[(is_beta ? 2 : 1) * a.B + b] = lin ? 1 : 0;
 }
 
-// pairs per lane of the one-wave lattice (0: the multi-wave kernel).  SC_CTC_AB1=0 in the
-// environment forces the multi-wave kernel (A/B timing in tools only).
-static int ab1_ppl(int Umax) {
+// pairs per lane of the one-wave lattice family (0: the multi-wave kernel, Umax > 255).
+// SC_CTC_LIN=0 in the environment forces the multi-wave kernel (A/B timing in tools only).
+static int lin_ppl(int Umax) {
   static const bool on = [] {
-    const char* e = getenv("SC_CTC_AB1");
+    const char* e = getenv("SC_CTC_LIN");
     return !(e && e[0] == '0');
   }();
   const int ppl = (Umax + 1 + 63) / 64;
@@ -721,11 +944,12 @@ template <int DT, int GT>
 __global__ void __launch_bounds__(256) ctc_grad_kernel(CtcArgs a) {
   using E = Elem<DT>;
   using G = Elem<GT>;
-  extern __shared__ __attribute__((aligned(16))) float lcab_all[];   // [4][V + 4]
+  extern __shared__ __attribute__((aligned(16))) float lcab_all[];   // [4][V + 4] (x2 with ex)
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t row = (int64_t)blockIdx.x * (blockDim.x >> 6) + w;
   if (row >= (int64_t)a.B * a.T) return;
-  float* lcab = lcab_all + w * (a.V + 4);
+  float* lcab = lcab_all + w * (a.ex ? 2 : 1) * (a.V + 4);
+  float* xex = lcab + (a.V + 4);   // (ex) the row's emission logits by column, NaN elsewhere
   const int b = (int)(row / a.T), t = (int)(row % a.T);
   const int Tb = clampi(a.in_lens[b], 0, a.T);
   typename G::T* g = (typename G::T*)a.grad + row * a.V;
@@ -752,9 +976,22 @@ __global__ void __launch_bounds__(256) ctc_grad_kernel(CtcArgs a) {
   const int Um = a.Umax > 0 ? a.Umax : 1;
   const int64_t* tg = a.tg + (int64_t)b * a.tgs;
   for (int v = lane; v < a.V; v += 64) lcab[v] = kNegInf;
+  if (a.ex)
+    for (int v = lane; v < a.V; v += 64) xex[v] = __builtin_nanf("");
   wave_lds_sync();
-  const float* al = a.ws.alpha + ((int64_t)b * a.T + t) * a.Sp;
-  const float* be = a.ws.beta + ((int64_t)b * a.T + t) * a.Sp;
+  const float* exr = a.ex ? a.ex + (int64_t)b * a.exb + (int64_t)t * a.ext : nullptr;
+  const float* al = a.ws.alpha + ((int64_t)b * a.T + t) * a.apitch;
+  const float* be = a.ws.beta + ((int64_t)b * a.T + t) * a.apitch;
+  // base-2 log of a row's state s: fp32 log-space rows as they are, linear fp64 rows
+  // (ctc_lin_kernel) through frexp (0 -> -inf)
+  const bool linA = a.lin && a.ws.flag[a.B + b], linB = a.lin && a.ws.flag[2 * a.B + b];
+  auto lv = [&](const float* r, bool lin, int s) -> float {
+    if (!lin) return r[s];
+    const double v = ((const double*)r)[s];
+    int e;
+    const double m = frexp(v, &e);
+    return v > 0.0 ? (float)e + log2_((float)m) : kNegInf;
+  };
   // exp(lcab + nll - lp) = 2^(lcab2 + offA + offB + c_t - ll2s - lp*log2e): the lattice holds
   // alpha_t - sum_{t'<=t} c and beta_t - sum_{t'>=t} c, so alpha + beta carries c_t once more than
   // the shifted log-likelihood ll2s; offsets folded in fp64
@@ -767,7 +1004,7 @@ __global__ void __launch_bounds__(256) ctc_grad_kernel(CtcArgs a) {
   float m = kNegInf, l = 0.0f;   // blank-label occupancy (base 2), per lane
   for (int s = lane; s < Sb; s += 64) {
     const int lab = (s & 1) ? (int)tg[(s - 1) >> 1] : a.blank;
-    const float val = al[s] + be[s];
+    const float val = lv(al, linA, s) + lv(be, linB, s);
     if (lab == a.blank) {
       const float mn = fmaxf(m, val);
       if (mn != kNegInf) {
@@ -778,8 +1015,12 @@ __global__ void __launch_bounds__(256) ctc_grad_kernel(CtcArgs a) {
       const int u = (s - 1) >> 1;
       if (first[u]) {
         float acc = val;
-        for (int q = chain[u]; q >= 0; q = chain[q]) acc = lse2_b2(acc, al[2 * q + 1] + be[2 * q + 1]);
-        if (lab >= 0 && lab < a.V) lcab[lab] = acc;
+        for (int q = chain[u]; q >= 0; q = chain[q])
+          acc = lse2_b2(acc, lv(al, linA, 2 * q + 1) + lv(be, linB, 2 * q + 1));
+        if (lab >= 0 && lab < a.V) {
+          lcab[lab] = acc;
+          if (exr) xex[lab] = exr[1 + u];
+        }
       }
     }
   }
@@ -788,7 +1029,10 @@ __global__ void __launch_bounds__(256) ctc_grad_kernel(CtcArgs a) {
     l = wave_sum_dpp(m == kNegInf ? 0.0f : l * exp2_(m - M));
     m = M;
   }
-  if (lane == 0 && a.blank >= 0 && a.blank < a.V) lcab[a.blank] = (m == kNegInf) ? kNegInf : m + log2_(l);
+  if (lane == 0 && a.blank >= 0 && a.blank < a.V) {
+    lcab[a.blank] = (m == kNegInf) ? kNegInf : m + log2_(l);
+    if (exr) xex[a.blank] = exr[0];
+  }
   wave_lds_sync();
   const typename E::T* xr = (const typename E::T*)a.x + (int64_t)b * a.sb + (int64_t)t * a.stt;
   const float lse = a.is_logits ? a.ws.lse[(int64_t)b * a.T + t] : 0.0f;
@@ -804,6 +1048,12 @@ __global__ void __launch_bounds__(256) ctc_grad_kernel(CtcArgs a) {
       }
       const float4 l0 = *(const float4*)&lcab[8 * c], l1 = *(const float4*)&lcab[8 * c + 4];
       const float lc[8] = {l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, l1.z, l1.w};
+      if (a.ex) {   // the emission columns' exact logits (softmax term and occupancy alike)
+        const float4 e0 = *(const float4*)&xex[8 * c], e1 = *(const float4*)&xex[8 * c + 4];
+        const float ev[8] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) xv[k] = ev[k] == ev[k] ? ev[k] : xv[k];
+      }
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         const float lp2 = (xv[k] - lse) * kLog2e;
@@ -819,7 +1069,9 @@ __global__ void __launch_bounds__(256) ctc_grad_kernel(CtcArgs a) {
     return;
   }
   for (int v = lane; v < a.V; v += 64) {
-    const float lp2 = (E::ld(xr[v]) - lse) * kLog2e;
+    float xv = E::ld(xr[v]);
+    if (a.ex && xex[v] == xex[v]) xv = xex[v];
+    const float lp2 = (xv - lse) * kLog2e;
     const float gv = exp2_(lp2) - exp2_(lcab[v] + koff - lp2);
     g[v] = G::st(gv * sc);
   }
@@ -828,14 +1080,15 @@ __global__ void __launch_bounds__(256) ctc_grad_kernel(CtcArgs a) {
 template <int DT>
 static void launch_fwd(const CtcArgs& a, hipStream_t st) {
   const int64_t rows = (int64_t)a.B * a.T;
+  if (a.lin) (void)hipMemsetAsync(a.ws.flag, 0, (size_t)a.B * sizeof(int), st);   // tiny[b]
   hipLaunchKernelGGL((ctc_emit_kernel<DT>), dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, a);
   hipLaunchKernelGGL(ctc_chain_kernel, dim3(a.B, ((a.Umax > 0 ? a.Umax : 1) + 3) / 4), dim3(256), 0,
                      st, a);
-  switch (ab1_ppl(a.Umax)) {
-    case 1: hipLaunchKernelGGL((ctc_ab1_kernel<1>), dim3(2 * a.B), dim3(64), 0, st, a); return;
-    case 2: hipLaunchKernelGGL((ctc_ab1_kernel<2>), dim3(2 * a.B), dim3(64), 0, st, a); return;
-    case 3: hipLaunchKernelGGL((ctc_ab1_kernel<3>), dim3(2 * a.B), dim3(64), 0, st, a); return;
-    case 4: hipLaunchKernelGGL((ctc_ab1_kernel<4>), dim3(2 * a.B), dim3(64), 0, st, a); return;
+  switch (a.lin ? lin_ppl(a.Umax) : 0) {
+    case 1: hipLaunchKernelGGL((ctc_lin_kernel<1>), dim3(2 * a.B), dim3(64), 0, st, a); return;
+    case 2: hipLaunchKernelGGL((ctc_lin_kernel<2>), dim3(2 * a.B), dim3(64), 0, st, a); return;
+    case 3: hipLaunchKernelGGL((ctc_lin_kernel<3>), dim3(2 * a.B), dim3(64), 0, st, a); return;
+    case 4: hipLaunchKernelGGL((ctc_lin_kernel<4>), dim3(2 * a.B), dim3(64), 0, st, a); return;
     default: break;
   }
   const int K = a.kh;
@@ -856,9 +1109,10 @@ static void launch_fwd(const CtcArgs& a, hipStream_t st) {
 template <int DT, int GT>
 static void launch_bwd(const CtcArgs& a, hipStream_t st) {
   // 4 rows (waves) per workgroup while their LDS rows fit the default 64 KB, else 1
-  const int R = 4 * (a.V + 4) * (int)sizeof(float) <= 65536 ? 4 : 1;
+  const int nr = a.ex ? 2 : 1;   // LDS rows per wave
+  const int R = 4 * nr * (a.V + 4) * (int)sizeof(float) <= 65536 ? 4 : 1;
   hipLaunchKernelGGL((ctc_grad_kernel<DT, GT>), dim3((unsigned)(((int64_t)a.B * a.T + R - 1) / R)),
-                     dim3(64 * R), R * (a.V + 4) * sizeof(float), st, a);
+                     dim3(64 * R), R * nr * (a.V + 4) * sizeof(float), st, a);
 }
 
 // nn.CTCLoss(reduction='mean', zero_infinity=True) on device in one launch: loss =
@@ -925,9 +1179,11 @@ static CtcArgs make_args(const void* x, int is_logits, int B, int T, int V, int6
   a.S = 2 * umax + 1;
   a.Sp = 64 * states_per_lane(a.S);
   a.Umax = umax;
-  // steps per re-centring / 2 (the gradient's offset index): the one-wave lattice re-centres
+  // steps per re-centring / 2 (the gradient's offset index): the one-wave lattices re-centre
   // every kAb1R steps, the multi-wave one at every second halo exchange
-  a.kh = ab1_ppl(umax) ? kAb1R / 2 : ab_halo_k(umax);
+  a.lin = lin_ppl(umax) > 0;
+  a.apitch = a.lin ? 2 * a.Sp : a.Sp;
+  a.kh = a.lin ? kAb1R / 2 : ab_halo_k(umax);
   a.blank = blank;
   a.sb = sb;
   a.stt = st;
@@ -939,14 +1195,26 @@ static CtcArgs make_args(const void* x, int is_logits, int B, int T, int V, int6
   ws_layout(B, T, umax, &a.ws, (void*)ws);
   a.scale = scale;
   a.grad = grad;
+  a.ex = nullptr;
+  a.exb = a.ext = 0;
   return a;
 }
 
-extern "C" int sc_ctc_fwd(const void* x, int x_dtype, int is_logits, int B, int T, int V,
-                          int64_t stride_b, int64_t stride_t, const int64_t* targets,
-                          int64_t target_stride, int max_target_len, const int64_t* in_lens,
-                          const int64_t* tgt_lens, int blank, float* nll, void* workspace,
-                          size_t workspace_bytes, void* stream) {
+static int ex_check(const float* ex, int64_t ex_stride_b, int64_t ex_stride_t, int is_logits,
+                    int T, int max_target_len, const char* who) {
+  if (!ex) return 0;
+  SC_REQUIRE(is_logits, "%s: emission logits need is_logits = 1", who);
+  SC_REQUIRE(ex_stride_t >= max_target_len + 1 && ex_stride_b >= (int64_t)T * ex_stride_t,
+             "%s: emission logits rows of max_target_len + 1 = %d", who, max_target_len + 1);
+  return 0;
+}
+
+extern "C" int sc_ctc_fwd_ex(const void* x, int x_dtype, int is_logits, int B, int T, int V,
+                             int64_t stride_b, int64_t stride_t, const int64_t* targets,
+                             int64_t target_stride, int max_target_len, const int64_t* in_lens,
+                             const int64_t* tgt_lens, int blank, const float* ex,
+                             int64_t ex_stride_b, int64_t ex_stride_t, float* nll, void* workspace,
+                             size_t workspace_bytes, void* stream) {
   clear_error();
   int rc = ctc_check(x, x_dtype, B, T, V, max_target_len, targets, in_lens, tgt_lens, blank,
                      workspace, workspace_bytes, "sc_ctc_fwd");
@@ -954,8 +1222,13 @@ extern "C" int sc_ctc_fwd(const void* x, int x_dtype, int is_logits, int B, int 
   if (B == 0) return 0;
   SC_REQUIRE(nll, "sc_ctc_fwd: null nll");
   SC_REQUIRE(T > 0, "sc_ctc_fwd: T == 0 is handled by the caller");
+  if ((rc = ex_check(ex, ex_stride_b, ex_stride_t, is_logits, T, max_target_len, "sc_ctc_fwd_ex")))
+    return rc;
   CtcArgs a = make_args(x, is_logits, B, T, V, stride_b, stride_t, targets, target_stride,
                         max_target_len, in_lens, tgt_lens, blank, nll, workspace, nullptr, nullptr);
+  a.ex = ex;
+  a.exb = ex_stride_b;
+  a.ext = ex_stride_t;
   hipStream_t st = (hipStream_t)stream;
   switch (x_dtype) {
     case SC_F32: launch_fwd<SC_F32>(a, st); break;
@@ -965,12 +1238,23 @@ extern "C" int sc_ctc_fwd(const void* x, int x_dtype, int is_logits, int B, int 
   return launch_status("sc_ctc_fwd");
 }
 
-extern "C" int sc_ctc_bwd(const void* x, int x_dtype, int is_logits, int B, int T, int V,
+extern "C" int sc_ctc_fwd(const void* x, int x_dtype, int is_logits, int B, int T, int V,
                           int64_t stride_b, int64_t stride_t, const int64_t* targets,
                           int64_t target_stride, int max_target_len, const int64_t* in_lens,
-                          const int64_t* tgt_lens, int blank, const float* nll,
-                          const float* scale, void* grad, int grad_dtype, const void* workspace,
+                          const int64_t* tgt_lens, int blank, float* nll, void* workspace,
                           size_t workspace_bytes, void* stream) {
+  return sc_ctc_fwd_ex(x, x_dtype, is_logits, B, T, V, stride_b, stride_t, targets, target_stride,
+                       max_target_len, in_lens, tgt_lens, blank, nullptr, 0, 0, nll, workspace,
+                       workspace_bytes, stream);
+}
+
+extern "C" int sc_ctc_bwd_ex(const void* x, int x_dtype, int is_logits, int B, int T, int V,
+                             int64_t stride_b, int64_t stride_t, const int64_t* targets,
+                             int64_t target_stride, int max_target_len, const int64_t* in_lens,
+                             const int64_t* tgt_lens, int blank, const float* ex,
+                             int64_t ex_stride_b, int64_t ex_stride_t, const float* nll,
+                             const float* scale, void* grad, int grad_dtype, const void* workspace,
+                             size_t workspace_bytes, void* stream) {
   clear_error();
   int rc = ctc_check(x, x_dtype, B, T, V, max_target_len, targets, in_lens, tgt_lens, blank,
                      workspace, workspace_bytes, "sc_ctc_bwd");
@@ -979,9 +1263,14 @@ extern "C" int sc_ctc_bwd(const void* x, int x_dtype, int is_logits, int B, int 
   SC_REQUIRE(grad_dtype == SC_F32 || grad_dtype == SC_BF16 || grad_dtype == SC_F16,
              "sc_ctc_bwd: unsupported grad dtype %d", grad_dtype);
   SC_REQUIRE(nll && scale && grad, "sc_ctc_bwd: null pointer");
+  if ((rc = ex_check(ex, ex_stride_b, ex_stride_t, is_logits, T, max_target_len, "sc_ctc_bwd_ex")))
+    return rc;
   CtcArgs a = make_args(x, is_logits, B, T, V, stride_b, stride_t, targets, target_stride,
                         max_target_len, in_lens, tgt_lens, blank, (float*)nll, workspace, scale,
                         grad);
+  a.ex = ex;
+  a.exb = ex_stride_b;
+  a.ext = ex_stride_t;
   hipStream_t st = (hipStream_t)stream;
 #define SC_CTC_BWD(DT)                                               \
   switch (grad_dtype) {                                              \
@@ -996,6 +1285,17 @@ extern "C" int sc_ctc_bwd(const void* x, int x_dtype, int is_logits, int B, int 
   }
 #undef SC_CTC_BWD
   return launch_status("sc_ctc_bwd");
+}
+
+extern "C" int sc_ctc_bwd(const void* x, int x_dtype, int is_logits, int B, int T, int V,
+                          int64_t stride_b, int64_t stride_t, const int64_t* targets,
+                          int64_t target_stride, int max_target_len, const int64_t* in_lens,
+                          const int64_t* tgt_lens, int blank, const float* nll,
+                          const float* scale, void* grad, int grad_dtype, const void* workspace,
+                          size_t workspace_bytes, void* stream) {
+  return sc_ctc_bwd_ex(x, x_dtype, is_logits, B, T, V, stride_b, stride_t, targets, target_stride,
+                       max_target_len, in_lens, tgt_lens, blank, nullptr, 0, 0, nll, scale, grad,
+                       grad_dtype, workspace, workspace_bytes, stream);
 }
 
 extern "C" int sc_ctc_mean(const float* nll, const int64_t* tgt_lens, int B, float* loss,

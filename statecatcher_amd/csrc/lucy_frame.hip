@@ -98,11 +98,16 @@ template <bool BF16W, bool LN, int EPI, int NT, int KS>
 __global__ void __launch_bounds__(64 * NT * KS) lucy_frame_gemm(FrameGemmArgs a) {
   __shared__ float part[NT * KS][16][17];   // per-wave 16 x 16 partial sums (padded rows)
   __shared__ float stat[16][2];             // PRO_LN: (mean, rstd) of the workgroup's rows
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  extern __shared__ __attribute__((aligned(16))) float xs[];   // the A rows [16][kpitch]
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // (wave-uniform: scalar)
   const int t = w % NT, ks = w / NT;
   const int r0 = blockIdx.y * 16;
   constexpr bool CELL = EPI == FR_CELL_UNFUSED || EPI == FR_CELL_FUSED;
+  constexpr int KSTEP = BF16W ? 32 : 16;
   const int cbase = CELL ? blockIdx.x * 16 + t * a.gstride : (blockIdx.x * NT + t) * 16;
+  const int nsteps = (a.K + KSTEP - 1) / KSTEP;
+  const int kpad = nsteps * KSTEP, kpitch = kpad + 4;   // +4 floats: conflict-free row reads
   // the row statistics of the prologue, once per workgroup
   if (LN) {
     if (threadIdx.x < 16) {
@@ -114,96 +119,90 @@ __global__ void __launch_bounds__(64 * NT * KS) lucy_frame_gemm(FrameGemmArgs a)
     }
     __syncthreads();
   }
-  const int arow = r0 + (lane & 15);
-  const bool rok = arow < a.B;
-  const float* xr = a.x + (int64_t)min(arow, a.B - 1) * a.ldx;
+  // The workgroup's 16 A rows (LayerNorm applied, rows past B and columns past K zero) into LDS
+  // with coalesced 16-byte loads: every wave then reads its fragments from LDS, and no global
+  // load of the MFMA loop depends on a row or K condition
+  {
+    const int per_row = kpad / 4;   // float4 pieces per row
+    for (int i = threadIdx.x; i < 16 * per_row; i += 64 * NT * KS) {
+      const int rr = i / per_row, k = 4 * (i % per_row);
+      const int r = r0 + rr;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (r < a.B && k < a.K) {   // (K % 4 == 0: a piece is wholly inside or outside)
+        v = *(const float4*)(a.x + (int64_t)r * a.ldx + k);
+        if (LN) {
+          const float mu = stat[rr][0], rs = stat[rr][1];
+          const float4 lw = *(const float4*)(a.ln_w + k), lb = *(const float4*)(a.ln_b + k);
+          v.x = (v.x - mu) * rs * lw.x + lb.x;
+          v.y = (v.y - mu) * rs * lw.y + lb.y;
+          v.z = (v.z - mu) * rs * lw.z + lb.z;
+          v.w = (v.w - mu) * rs * lw.w + lb.w;
+        }
+      }
+      *(float4*)(xs + rr * kpitch + k) = v;
+    }
+    __syncthreads();
+  }
   const int col = cbase + (lane & 15);
   const bool cok = CELL || col < a.N;
-  const float mean = LN ? stat[lane & 15][0] : 0.0f, rstd = LN ? stat[lane & 15][1] : 1.0f;
-  // K slice of this wave, in steps of KSTEP
-  constexpr int KSTEP = BF16W ? 32 : 16;
-  const int nsteps = (a.K + KSTEP - 1) / KSTEP;
   const int sb = (int)((int64_t)nsteps * ks / KS), se = (int)((int64_t)nsteps * (ks + 1) / KS);
   f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
   const int q = lane >> 4;
-  // Every load of a chunk of up to SMAX steps is issued before its first MFMA (one exposed
-  // memory latency per chunk, not per step: the operands come from L2 / the Infinity Cache)
+  const float* xrow = xs + (lane & 15) * kpitch;
+  // Every weight load of a chunk of SMAX steps is issued before its first MFMA (one exposed memory
+  // latency per chunk).  The chunk always runs SMAX steps: a load past the slice or past K reads a
+  // clamped address (always inside the matrix) and is zeroed by a select, so the loop carries no
+  // branch around a load and no per-step wait.
   if constexpr (!BF16W) {
     constexpr int SMAX = NT * KS > 8 ? 8 : 16;   // (10 waves: 3 per SIMD, <= 168 VGPRs)
     const float* wr = (const float*)a.w + (int64_t)(cok ? col : 0) * a.ldw;
     for (int c0 = sb; c0 < se; c0 += SMAX) {
-      float4 xa[SMAX], wb[SMAX];
+      float4 wb[SMAX], xb[SMAX];
 #pragma unroll
       for (int i = 0; i < SMAX; ++i) {
-        const int k0 = (c0 + i) * 16 + 4 * q;   // this lane's 4 consecutive k of step c0 + i
-        const bool full = c0 + i < se && k0 + 3 < a.K && rok && cok;
-        xa[i] = full ? *(const float4*)(xr + k0) : make_float4(0.f, 0.f, 0.f, 0.f);
-        wb[i] = full ? *(const float4*)(wr + k0) : make_float4(0.f, 0.f, 0.f, 0.f);
+        const int k0 = (c0 + i) * 16 + 4 * q;
+        wb[i] = *(const float4*)(wr + min(k0, a.K - 4));
       }
 #pragma unroll
+      for (int i = 0; i < SMAX; ++i) xb[i] = *(const float4*)(xrow + min((c0 + i) * 16, kpad - 16) + 4 * q);
+      __builtin_amdgcn_sched_barrier(0);   // keep the loads ahead of the MFMAs (no sinking)
+#pragma unroll
       for (int i = 0; i < SMAX; ++i) {
-        if (c0 + i >= se) break;
         const int k0 = (c0 + i) * 16 + 4 * q;
-        float av[4] = {xa[i].x, xa[i].y, xa[i].z, xa[i].w};
-        float bv[4] = {wb[i].x, wb[i].y, wb[i].z, wb[i].w};
-        if (!(k0 + 3 < a.K && rok && cok)) {   // a ragged K tail (layer 0: K = 80 x stack)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            av[j] = k0 + j < a.K && rok ? xr[k0 + j] : 0.0f;
-            bv[j] = k0 + j < a.K && cok ? wr[k0 + j] : 0.0f;
-          }
-        }
-        if (LN) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            av[j] = k0 + j < a.K ? (av[j] - mean) * rstd * a.ln_w[k0 + j] + a.ln_b[k0 + j] : 0.0f;
-        }
+        const bool in = c0 + i < se && k0 < a.K && cok;
+        float4 xa = xb[i];
+        xa.x = in ? xa.x : 0.f;   // (zero the LDS operand: the weight may be any clamped value)
+        xa.y = in ? xa.y : 0.f;
+        xa.z = in ? xa.z : 0.f;
+        xa.w = in ? xa.w : 0.f;
         // k slot q of MFMA j is k0 + j for both operands: the sum runs over the same k set
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[0], bv[0], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[1], bv[1], acc1, 0, 0, 0);
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[2], bv[2], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[3], bv[3], acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(xa.x, wb[i].x, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(xa.y, wb[i].y, acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(xa.z, wb[i].z, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(xa.w, wb[i].w, acc1, 0, 0, 0);
       }
     }
   } else {
     constexpr int SMAX = 8;
     const __bf16* wr = (const __bf16*)a.w + (int64_t)(cok ? col : 0) * a.ldw;
+    const bf16x8 zero8 = {};
     for (int c0 = sb; c0 < se; c0 += SMAX) {
-      float4 x0[SMAX], x1[SMAX];
       bf16x8 wb[SMAX];
 #pragma unroll
       for (int i = 0; i < SMAX; ++i) {
-        const int k0 = (c0 + i) * 32 + 8 * q;   // this lane's 8 consecutive k of step c0 + i
-        const bool full = c0 + i < se && k0 + 7 < a.K && rok && cok;
-        x0[i] = full ? *(const float4*)(xr + k0) : make_float4(0.f, 0.f, 0.f, 0.f);
-        x1[i] = full ? *(const float4*)(xr + k0 + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
-        if (full) wb[i] = *(const bf16x8*)(wr + k0);
-        else {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) wb[i][j] = (__bf16)0.0f;
-        }
+        const int k0 = (c0 + i) * 32 + 8 * q;
+        wb[i] = *(const bf16x8*)(wr + min(k0, a.K - 8));
       }
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < SMAX; ++i) {
-        if (c0 + i >= se) break;
         const int k0 = (c0 + i) * 32 + 8 * q;
-        float f[8] = {x0[i].x, x0[i].y, x0[i].z, x0[i].w, x1[i].x, x1[i].y, x1[i].z, x1[i].w};
-        bf16x8 bv = wb[i];
-        if (!(k0 + 7 < a.K && rok && cok)) {   // ragged K tail
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            f[j] = k0 + j < a.K && rok ? xr[k0 + j] : 0.0f;
-            bv[j] = k0 + j < a.K && cok ? wr[k0 + j] : (__bf16)0.0f;
-          }
-        }
-        bf16x8 av;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float v = LN && k0 + j < a.K ? (f[j] - mean) * rstd * a.ln_w[k0 + j] + a.ln_b[k0 + j]
-                                             : f[j];
-          av[j] = (__bf16)v;
-        }
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc0, 0, 0, 0);
+        const bool in = c0 + i < se && k0 < a.K && cok;
+        const int kx = min((c0 + i) * 32, kpad - 32) + 8 * q;
+        const float4 x0 = *(const float4*)(xrow + kx), x1 = *(const float4*)(xrow + kx + 4);
+        const bf16x8 av = {(__bf16)x0.x, (__bf16)x0.y, (__bf16)x0.z, (__bf16)x0.w,
+                           (__bf16)x1.x, (__bf16)x1.y, (__bf16)x1.z, (__bf16)x1.w};
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(in ? av : zero8, wb[i], acc0, 0, 0, 0);
       }
     }
   }
@@ -266,9 +265,7 @@ __global__ void __launch_bounds__(64 * NT * KS) lucy_frame_gemm(FrameGemmArgs a)
       if (EPI == FR_CELL_FUSED) {
         o = gate(3) + sn;                                   // hp = h_pre + s'
       } else {
-        const float av = a.x[(int64_t)rc * a.ldx + d];      // u = LN_in(a), unit d
-        o = LN ? (av - stat[rr][0]) * stat[rr][1] * a.ln_w[d] + a.ln_b[d] : av;
-        o += sn;                                            // y = u + s'
+        o = xs[rr * kpitch + d] + sn;                       // y = u + s', u = LN_in(a)
       }
       const float4 sz = stats16(z), so = stats16(o);
       if (ok) {
@@ -329,8 +326,16 @@ __global__ void __launch_bounds__(256) lucy_frame_cellb(FrameCellArgs a) {
 
 template <bool BF16W, bool LN, int EPI, int NT, int KS>
 static void launch_gemm(const FrameGemmArgs& a, int nblk, hipStream_t st) {
+  const int kstep = BF16W ? 32 : 16;
+  const size_t lds = (size_t)16 * (((a.K + kstep - 1) / kstep) * kstep + 4) * sizeof(float);
+  static bool big_lds = false;   // (the A rows of K > ~800 exceed the default 64 KB window)
+  if (lds > 48 * 1024 && !big_lds) {
+    (void)hipFuncSetAttribute((const void*)lucy_frame_gemm<BF16W, LN, EPI, NT, KS>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 140 * 1024);
+    big_lds = true;
+  }
   hipLaunchKernelGGL((lucy_frame_gemm<BF16W, LN, EPI, NT, KS>), dim3(nblk, (a.B + 15) / 16),
-                     dim3(64 * NT * KS), 0, st, a);
+                     dim3(64 * NT * KS), lds, st, a);
 }
 
 template <bool BF16W, bool LN>
@@ -363,6 +368,10 @@ extern "C" int sc_lucy_frame_gemm(int epi, const float* x, int64_t ldx, int K, c
   SC_REQUIRE(ldx % 4 == 0 && ldw % 8 == 0 && K % 4 == 0 && (uintptr_t)x % 16 == 0 &&
                  (uintptr_t)w % 16 == 0,
              "sc_lucy_frame_gemm: rows must be 16-byte aligned (ldx %% 4, ldw %% 8, K %% 4)");
+  SC_REQUIRE(w_dtype == SC_F32 || K % 8 == 0, "sc_lucy_frame_gemm: bf16 weights need K %% 8 == 0");
+  SC_REQUIRE(K <= 2048, "sc_lucy_frame_gemm: K = %d above 2048 (the A rows live in LDS)", K);
+  SC_REQUIRE(!ln_w || ((uintptr_t)ln_w % 16 == 0 && (uintptr_t)ln_b % 16 == 0),
+             "sc_lucy_frame_gemm: LayerNorm parameters must be 16-byte aligned");
   SC_REQUIRE((ln_w == nullptr) == (ln_b == nullptr) && (!ln_w || (st_in && nst_in > 0)),
              "sc_lucy_frame_gemm: LayerNorm prologue needs weight, bias and statistics");
   const bool cell = epi >= FR_CELL_UNFUSED;

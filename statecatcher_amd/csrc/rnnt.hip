@@ -512,12 +512,15 @@ __global__ void __launch_bounds__(64) rnnt_ab1_kernel(RnntArgs a) {
   else ab1_run<PPL, false>(a, b, Tb, Ub);
 }
 
-// label positions per lane of the one-wave lattice (0: the multi-wave kernel).  SC_RNNT_AB1=0 in
-// the environment forces the multi-wave kernel (A/B timing in tools only).
+// label positions per lane of the one-wave lattice (0: the multi-wave kernel).  Off unless
+// SC_RNNT_AB1=1 in the environment: measured at C5 (B=32, T=1500, U=150; profiles/
+// r4_lattice_ab.md) the one-wave kernel took 411 us against the multi-wave kernel's 205 us —
+// with PPL = 3 label positions per lane, one wave issues three log-sum-exps (6 quarter-rate
+// exp2 / log2) per diagonal, where three waves of the multi-wave kernel issue one each.
 int ab1_ppl(int Umax) {
   static const bool on = [] {
     const char* e = getenv("SC_RNNT_AB1");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   const int ppl = (Umax + 1 + 63) / 64;
   return (on && ppl <= 4) ? ppl : 0;

@@ -643,7 +643,9 @@ class CTCFn(torch.autograd.Function):
     """nll [B] fp32 of CTC over x [B,T,V] (logits with fused log_softmax, or log-probs)."""
 
     @staticmethod
-    def forward(ctx, x, targets, in_lens, tgt_lens, blank, is_logits):
+    def forward(ctx, x, targets, in_lens, tgt_lens, blank, is_logits, ex=None):
+        """ex: optional fp32 [B, T, U_max + 1] exact emission logits (blank, then each label;
+        sc_ctc_fwd_ex), read instead of x's values at those columns."""
         require_device(x, targets, in_lens, tgt_lens)
         if x.dim() != 3:
             raise ValueError(f"x must be [B,T,V], got {tuple(x.shape)}")
@@ -659,17 +661,38 @@ class CTCFn(torch.autograd.Function):
         lib = _lib.load()
         wsb = lib.sc_ctc_workspace_bytes(B, max(T, 1), umax)
         ws = torch.empty(wsb, dtype=torch.uint8, device=x.device)
+        if ex is not None:
+            require_device(x, ex)
+            if (ex.dtype != torch.float32 or ex.shape != (B, T, umax + 1) or ex.stride(2) != 1):
+                raise ValueError(f"ex must be fp32 [B, T, U_max + 1] = {(B, T, umax + 1)} with unit "
+                                 f"column stride; got {ex.dtype} {tuple(ex.shape)}")
         if T == 0:
             nll = torch.where(tgt_lens == 0, 0.0, float("inf")).to(torch.float32)
         else:
-            rc = lib.sc_ctc_fwd(ptr(x), dtype_code(x), int(is_logits), B, T, V, x.stride(0),
-                                x.stride(1), ptr(targets), targets.stride(0) if umax else 0, umax,
-                                ptr(in_lens), ptr(tgt_lens), blank, ptr(nll), ptr(ws), wsb,
-                                stream_of(x))
-            check(rc, "sc_ctc_fwd")
+            rc = lib.sc_ctc_fwd_ex(ptr(x), dtype_code(x), int(is_logits), B, T, V, x.stride(0),
+                                   x.stride(1), ptr(targets), targets.stride(0) if umax else 0, umax,
+                                   ptr(in_lens), ptr(tgt_lens), blank, ptr(ex),
+                                   ex.stride(0) if ex is not None else 0,
+                                   ex.stride(1) if ex is not None else 0, ptr(nll), ptr(ws), wsb,
+                                   stream_of(x))
+            check(rc, "sc_ctc_fwd_ex")
         ctx.save_for_backward(x, targets, in_lens, tgt_lens, nll, ws)
         ctx.meta = (blank, int(is_logits), umax, wsb)
+        ctx.ex = ex
         return nll
+
+    @staticmethod
+    def _bwd(ctx, x, targets, in_lens, tgt_lens, nll, ws, scale, grad):
+        blank, is_logits, umax, wsb = ctx.meta
+        B, T, V = x.shape
+        ex = ctx.ex
+        rc = _lib.load().sc_ctc_bwd_ex(ptr(x), dtype_code(x), is_logits, B, T, V, x.stride(0),
+                                       x.stride(1), ptr(targets), targets.stride(0) if umax else 0,
+                                       umax, ptr(in_lens), ptr(tgt_lens), blank, ptr(ex),
+                                       ex.stride(0) if ex is not None else 0,
+                                       ex.stride(1) if ex is not None else 0, ptr(nll), ptr(scale),
+                                       ptr(grad), dtype_code(grad), ptr(ws), wsb, stream_of(x))
+        check(rc, "sc_ctc_bwd_ex")
 
     @staticmethod
     def backward(ctx, grad_nll):
@@ -679,13 +702,8 @@ class CTCFn(torch.autograd.Function):
         grad = torch.empty(B, T, V, dtype=x.dtype, device=x.device)
         if T > 0:
             scale = grad_nll.to(torch.float32).contiguous()
-            rc = _lib.load().sc_ctc_bwd(ptr(x), dtype_code(x), is_logits, B, T, V, x.stride(0),
-                                        x.stride(1), ptr(targets), targets.stride(0) if umax else 0,
-                                        umax, ptr(in_lens), ptr(tgt_lens), blank, ptr(nll),
-                                        ptr(scale), ptr(grad), dtype_code(grad), ptr(ws), wsb,
-                                        stream_of(x))
-            check(rc, "sc_ctc_bwd")
-        return grad, None, None, None, None, None
+            CTCFn._bwd(ctx, x, targets, in_lens, tgt_lens, nll, ws, scale, grad)
+        return grad, None, None, None, None, None, None
 
 
 class CTCMeanFn(torch.autograd.Function):
@@ -694,8 +712,8 @@ class CTCMeanFn(torch.autograd.Function):
     forward; the backward is one scale (factor x upstream gradient) and sc_ctc_bwd."""
 
     @staticmethod
-    def forward(ctx, x, targets, in_lens, tgt_lens, blank, is_logits):
-        nll = CTCFn.forward(ctx, x, targets, in_lens, tgt_lens, blank, is_logits)
+    def forward(ctx, x, targets, in_lens, tgt_lens, blank, is_logits, ex=None):
+        nll = CTCFn.forward(ctx, x, targets, in_lens, tgt_lens, blank, is_logits, ex)
         B = nll.shape[0]
         loss = torch.empty((), dtype=torch.float32, device=x.device)
         factor = torch.empty(B, dtype=torch.float32, device=x.device)
@@ -720,6 +738,39 @@ def _logits_fp32(x2, wc, b):
 
 
 _SPLIT_W = WeakIdKeyDictionary()
+
+# CTCHeadFn with the scan's split planes:
+#   "emis" (default) = the bf16 GEMM's bf16 logits, plus the columns the lattice reads as
+#          emissions (blank and each sequence's labels) computed to fp32 accuracy into a
+#          [B, T, U + 1] side array that sc_ctc_fwd_ex / _bwd_ex read instead of those columns;
+#   "labels" = fp32 logits from the bf16 GEMM with the emission columns scattered in;
+#   "full" = every logit from the split-precision GEMM (3x the flops).
+# All three give the fp32 oracle's gradients (cosine 1.0000, tools/bf16_logits_diag.py
+# "round+exact"): the CTC gradient's sensitivity to the logits is in the lattice's emissions; the
+# other columns enter only through the row's log-sum-exp (a per-frame shift every path shares)
+# and the softmax term, where bf16 rounding is noise-sized.
+HEAD_SPLIT = os.environ.get("SC_HEAD_SPLIT", "emis")
+
+
+def _emission_logits(wide, w, b, targets, blank, V):
+    """fp32 [B, T, U + 1]: x.W + b at the blank and at each sequence's label columns, to fp32
+    accuracy from the scan's [x_hi | x_hi | x_lo] planes (one batched bf16 GEMM against the
+    gathered [W_hi | W_lo | W_hi] rows, K = 3D, fp32 out), and the gathered columns' index."""
+    B, T, K3 = wide.shape
+    lab = torch.cat([torch.full((B, 1), blank, dtype=torch.int64, device=wide.device),
+                     targets.clamp(0, V - 1)], 1)                           # [B, U + 1]
+    wg = split_weight_image(w)[lab]                                        # [B, U + 1, 3D]
+    ex = torch.bmm(wide, wg.transpose(1, 2), out_dtype=torch.float32)
+    ex += b[lab].unsqueeze(1)
+    return ex, lab
+
+
+def _exact_emission_columns(logits, wide, w, b, targets, blank):
+    """logits [B,T,V] fp32 in place: the emission columns set to _emission_logits' values
+    (duplicates write equal values)."""
+    B, T, V = logits.shape
+    ex, lab = _emission_logits(wide, w, b, targets, blank, V)
+    logits.scatter_(2, lab.unsqueeze(1).expand(B, T, lab.shape[1]), ex)
 
 
 def split_weight_image(w):
@@ -758,11 +809,17 @@ class CTCHeadFn(torch.autograd.Function):
         B, T, K = x.shape
         V = w.shape[0]
         x2 = x.reshape(-1, K)
-        if wide is not None:   # [x_hi | x_hi | x_lo] from the scan: fp32-accurate logits
+        ex = None
+        if wide is not None and HEAD_SPLIT == "full":   # every logit from [x_hi | x_hi | x_lo]
             logits = _logits_fp32(wide.view(-1, 3 * K), split_weight_image(w), b).view(B, T, V)
+        elif wide is not None and HEAD_SPLIT == "emis":
+            logits = torch.addmm(b.to(torch.bfloat16), x2, wc.t()).view(B, T, V)
+            ex, _ = _emission_logits(wide.view(B, T, 3 * K), w, b, targets, blank, V)
         else:
             logits = _logits_fp32(x2, wc, b).view(B, T, V)
-        loss = CTCMeanFn.forward(ctx, logits, targets, in_lens, tgt_lens, blank, True)
+            if wide is not None:
+                _exact_emission_columns(logits, wide, w, b, targets, blank)
+        loss = CTCMeanFn.forward(ctx, logits, targets, in_lens, tgt_lens, blank, True, ex)
         ctx.head = (x2, wt, x.shape, x.dtype)
         return loss, logits
 
@@ -777,12 +834,7 @@ class CTCHeadFn(torch.autograd.Function):
             dy.zero_()
         elif T > 0:
             scale = (ctx.factor * g_loss).to(torch.float32).contiguous()
-            rc = _lib.load().sc_ctc_bwd(ptr(logits), dtype_code(logits), 1, B, T, V,
-                                        logits.stride(0), logits.stride(1), ptr(targets),
-                                        targets.stride(0) if umax else 0, umax, ptr(in_lens),
-                                        ptr(tgt_lens), blank, ptr(nll), ptr(scale), ptr(dy),
-                                        dtype_code(dy), ptr(ws), wsb, stream_of(logits))
-            check(rc, "sc_ctc_bwd")
+            CTCFn._bwd(ctx, logits, targets, in_lens, tgt_lens, nll, ws, scale, dy)
         if g_logits is not None:
             dy = (dy.float() + g_logits).to(torch.bfloat16)
         dy2 = dy.view(-1, V)

@@ -116,6 +116,44 @@ def test_ctc_long_targets_many_waves_vs_aten_cpu(U):
     assert rel <= 1e-3
 
 
+@pytest.mark.parametrize("scales", [(2.0, 2.0, 2.0), (8.0, 30.0, 2.0), (100.0, 2.0, 400.0)])
+def test_ctc_linear_lattice_and_log_fallback_vs_aten_cpu(scales):
+    """ctc_lin_kernel (fp64 probabilities, renormalised by powers of two) and its per-sequence
+    fallback to the log-space lattice: a sequence whose live emissions reach below 2^-120 of the
+    frame's best (logits x 100 and x 400 over V = 40: log-prob gaps of hundreds of bits) runs in
+    log space, its neighbours in the same launch stay linear; x 8 and x 30 put 2^-40 .. 2^-100
+    per-frame gaps on the linear path.  nll and gradient vs ATen fp64, with an infeasible
+    sequence (T < U) among them (inf, zero gradient under zero_infinity)."""
+    g = torch.Generator().manual_seed(int(sum(scales)))
+    B, V, U, T = 4, 40, 120, 400
+    logits = torch.randn(B, T, V, generator=g)
+    for b, sc_ in enumerate(scales):
+        logits[b] *= sc_
+    tg = torch.randint(1, V, (B, U), generator=g)
+    tl = torch.tensor([U, U - 7, U - 20, U])
+    il = torch.tensor([T, T - 9, T, U - 10])   # sequence 3: infeasible
+    for b in range(B):
+        tg[b, tl[b]:] = 0
+    x = logits.to(DEV).requires_grad_(True)
+    nll = sc().ctc_nll(x, tg.to(DEV), il, tl)
+    xr = logits.double().requires_grad_(True)
+    ref = torch.nn.functional.ctc_loss(xr.log_softmax(-1).transpose(0, 1), tg, il, tl,
+                                       reduction="none", zero_infinity=False)
+    got = nll.detach().cpu().numpy()
+    r = ref.detach().numpy()
+    assert np.array_equal(np.isfinite(got), np.isfinite(r)) and not np.isfinite(got[3])
+    fin = np.isfinite(r)
+    np.testing.assert_allclose(got[fin], r[fin], rtol=1e-4)
+    nll[:3].sum().backward()
+    ref[:3].sum().backward()
+    g32, g64 = x.grad.cpu().numpy(), xr.grad.numpy()
+    assert not g32[3].any()
+    for b in range(3):
+        rel = np.linalg.norm(g32[b] - g64[b]) / np.linalg.norm(g64[b])
+        print(f"scale {scales[b]}: CTC grad rel err vs fp64 {rel:.2e}")
+        assert rel <= 1e-3
+
+
 def test_ctc_bf16_logits_vs_oracle():
     g = torch.Generator().manual_seed(5)
     B, T, V = 3, 120, 64

@@ -1,7 +1,8 @@
 """The fused output projection + CTC node (ops.CTCHeadFn) that compute_loss uses under bf16
-autocast: output_proj (lucyrnn_triton.py:107-109, :150) writes fp32 logits, the lattice
-(model.py:68-71, train.py:142: log_softmax + nn.CTCLoss(mean, zero_infinity)) reads them, and its
-gradient goes to the projection backward in bf16.
+autocast: output_proj (lucyrnn_triton.py:107-109, :150) and the lattice (model.py:68-71,
+train.py:142: log_softmax + nn.CTCLoss(mean, zero_infinity)) with the lattice's emission logits at
+fp32 accuracy (fp32 logits without the scan's split planes; with them, by default, bf16 logits plus
+the emission columns as a side array), and the gradient to the projection backward in bf16.
 
 * Against the same computation unfused on the same bf16 operands (fp32 logits from the bf16
   GEMM, the fp32 HIP lattice, the projection's backward in fp32 torch): loss 1e-5 relative,
@@ -95,7 +96,9 @@ def test_compute_loss_uses_head_under_bf16_autocast(monkeypatch):
     with torch.autocast("cuda", dtype=torch.bfloat16):
         loss, _, enc_out, _ = sc().compute_loss("ctc", crit, model, feats, masks, tok, [64, 64],
                                                 [10, 10], 0)
-    assert calls and enc_out.dtype == torch.float32 and enc_out.shape == (2, 64, 256)
+    # (the split planes are present here: "emis" keeps the bf16 GEMM's logits)
+    want = torch.bfloat16 if sc().ops.HEAD_SPLIT == "emis" else torch.float32
+    assert calls and enc_out.dtype == want and enc_out.shape == (2, 64, 256)
     loss.backward()
     assert model.encoder.output_proj.weight.grad is not None
     # fp32 training and a non-fusing criterion keep the module's own logits
@@ -128,10 +131,15 @@ def test_split_scan_planes():
     assert err < 2 ** -15
 
 
-def test_ctc_head_split_logits_match_fp32():
-    """With the scan's [x_hi | x_hi | x_lo] buffer and [W_hi | W_lo | W_hi], the head's logits
-    are the fp32 x.W + b to ~1e-5 (one bf16 GEMM)."""
+@pytest.mark.parametrize("mode", ["labels", "full"])
+def test_ctc_head_split_logits_match_fp32(mode, monkeypatch):
+    """With the scan's [x_hi | x_hi | x_lo] buffer: "full" -- every logit from one bf16 GEMM
+    against [W_hi | W_lo | W_hi] -- is the fp32 x.W + b to ~1e-5; "labels" -- the
+    bf16 GEMM's fp32 logits with the emission columns (blank and each sequence's labels)
+    recomputed from the split planes -- has those columns to ~1e-5 and the rest at the bf16
+    operands' ~2e-3."""
     ops = sc().ops
+    monkeypatch.setattr(ops, "HEAD_SPLIT", mode)
     g = torch.Generator().manual_seed(4)
     B, T, D, V = 2, 128, 256, 512
     x32 = torch.randn(B, T, D, generator=g).to(DEV)
@@ -140,11 +148,61 @@ def test_ctc_head_split_logits_match_fp32():
     x = wide[..., :D]
     w = (torch.randn(V, D, generator=g) * 0.05).to(DEV)
     b = (torch.randn(V, generator=g) * 0.1).to(DEV)
-    tg = torch.randint(1, V, (B, 12), generator=g).to(DEV)
+    tg = torch.randint(1, V, (B, 12), generator=g)
+    tg[1, 9:] = 0
     imgs = (w.to(torch.bfloat16), w.t().contiguous().to(torch.bfloat16))
-    _, logits = ops.ctc_head_loss(x, w, b, imgs, tg, [T, T], [12, 12], wide=wide)
+    _, logits = ops.ctc_head_loss(x, w, b, imgs, tg.to(DEV), [T, T], [12, 9], wide=wide)
     ref = x32.double() @ w.double().t() + b.double()
-    _, l1 = ops.ctc_head_loss(x, w, b, imgs, tg, [T, T], [12, 12])
-    e_split, e_plain = rel(logits, ref), rel(l1, ref)
-    print(f"head logits rel err vs fp64: split {e_split:.2e}, bf16 operands {e_plain:.2e}")
-    assert e_split < 2e-5 < e_plain
+    _, l1 = ops.ctc_head_loss(x, w, b, imgs, tg.to(DEV), [T, T], [12, 9])
+    e_plain = rel(l1, ref)
+    for bi in range(B):
+        cols = torch.unique(torch.cat([torch.zeros(1, dtype=torch.int64), tg[bi]])).to(DEV)
+        e_em = rel(logits[bi][:, cols], ref[bi][:, cols])
+        print(f"head ({mode}) emission-column logits rel err vs fp64: {e_em:.2e} "
+              f"(bf16 operands {e_plain:.2e})")
+        assert e_em < 2e-5
+    e_all = rel(logits, ref)
+    assert (e_all < 2e-5) if mode == "full" else (e_all <= 1.01 * e_plain)
+    assert e_plain > 2e-4
+
+
+def test_ctc_head_emission_side_input_matches_scattered_columns(monkeypatch):
+    """"emis" (the default with the scan's split planes): bf16 logits from the bf16 GEMM and the
+    emission columns to fp32 accuracy in a [B, T, U + 1] side array (sc_ctc_fwd_ex / _bwd_ex)
+    against the same head with those columns scattered into fp32 logits and the plain fp32 HIP
+    lattice: loss 1e-4, dW / db / dx 1e-2 in norm (bf16 logits in the row log-sum-exp and the
+    softmax term of the other columns, bf16 dlogits)."""
+    ops = sc().ops
+    monkeypatch.setattr(ops, "HEAD_SPLIT", "emis")
+    g = torch.Generator().manual_seed(7)
+    B, T, D, V = 2, 160, 256, 512
+    x32 = torch.randn(B, T, D, generator=g).to(DEV)
+    hi = x32.to(torch.bfloat16)
+    wide = torch.cat([hi, hi, (x32 - hi.float()).to(torch.bfloat16)], -1).contiguous()
+    x = wide[..., :D]
+    w = (torch.randn(V, D, generator=g) * 0.05).to(DEV)
+    b = (torch.randn(V, generator=g) * 0.1).to(DEV)
+    tg = torch.randint(1, V, (B, 14), generator=g)
+    tg[1, 11:] = 0
+    tg[0, 3:6] = 9   # repeats: duplicate emission columns
+    tgd = tg.to(DEV)
+    imgs = (w.to(torch.bfloat16), w.t().contiguous().to(torch.bfloat16))
+    w1, b1 = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    loss, logits = ops.ctc_head_loss(x, w1, b1, imgs, tgd, [T, T - 20], [14, 11], wide=wide)
+    assert logits.dtype == torch.bfloat16
+    loss.backward()
+    # reference: the bf16 logits as fp32 with the emission columns replaced by the side array's
+    # values, through the plain fp32 lattice; gradients pushed through the same bf16 operands
+    ex, lab = ops._emission_logits(wide, w, b, tgd, 0, V)
+    ref_logits = logits.detach().float().clone()
+    ref_logits.scatter_(2, lab.unsqueeze(1).expand(B, T, lab.shape[1]), ex)
+    ref_logits.requires_grad_(True)
+    ref = sc().ctc_loss(ref_logits, tgd, [T, T - 20], [14, 11])
+    ref.backward()
+    dl = ref_logits.grad.reshape(-1, V)
+    dw_ref = dl.t() @ x.float().reshape(-1, D)
+    db_ref = dl.sum(0)
+    print(f"emis head: loss {loss.item():.6f} vs {ref.item():.6f}; dW {rel(w1.grad, dw_ref):.2e} "
+          f"db {rel(b1.grad, db_ref):.2e}")
+    np.testing.assert_allclose(loss.item(), ref.item(), rtol=1e-4)
+    assert rel(w1.grad, dw_ref) < 1e-2 and rel(b1.grad, db_ref) < 1e-2

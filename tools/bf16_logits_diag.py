@@ -10,6 +10,7 @@ other part of the step exact.  Perturbations:
   operand fp32 logits from bf16-rounded operands (hidden and Wo rounded, fp32 accumulation: what
           an fp32-output GEMM under bf16 autocast computes)
   noise   fp32 logits + N(0, (2^-9 |logit|)^2) noise (rounding-sized, unbiased)
+  +exact  round / operand with the emission columns (blank and the sequence's labels) exact
 All three give the same 2-5% loss: at this init the CTC gradient over T=1500 frames is that
 sensitive to any perturbation of bf16 size in the logits (MEASURED on MI355X too: an fp32-output
 projection, ops.CTCHeadFn, moved the cosines by < 0.01 either way, profiles/r4_parity_measured.md).
@@ -46,17 +47,26 @@ def main():
     lo = (bf(x.reshape(-1, D512)) @ bf(p["Wo"]).T + p["bo"]).reshape(logits.shape).astype(np.float32)
     rng = np.random.default_rng(0)
     ln = (logits * (1 + 2.0 ** -9 * rng.standard_normal(logits.shape))).astype(np.float32)
+    # the same with the emission columns (blank + the sequence's labels) exact: what a bf16
+    # output projection plus exact emission logits would feed the loss
+    emis = np.zeros((B, 1, logits.shape[-1]), bool)
+    for b in range(B):
+        emis[b, 0, 0] = True
+        emis[b, 0, np.asarray(tok[b][:U[b]])] = True
+    lbx = np.where(emis, logits, lb).astype(np.float32)
+    lox = np.where(emis, logits, lo).astype(np.float32)
+    names = ("round", "operand", "noise", "round+exact", "operand+exact")
     res = {}
-    for name, lg in (("round", lb), ("operand", lo), ("noise", ln)):
+    for name, lg in zip(names, (lb, lo, ln, lbx, lox)):
         print(f"{name}: |logits - fp32| rms {np.sqrt(((lg - logits) ** 2).mean()):.2e}")
         got = grads_for(p, lg, tok, in_lens, U, x, caches, h, s)
         for k in ref:
             g, r = got[k].ravel().astype(np.float64), ref[k].ravel().astype(np.float64)
             res.setdefault(k, []).append((g @ r / (np.linalg.norm(g) * np.linalg.norm(r)),
                                           np.linalg.norm(g) / np.linalg.norm(r)))
-    print("tensor   " + "   ".join(f"{n:>7s} cos / ratio" for n in ("round", "operand", "noise")))
+    print("tensor   " + "   ".join(f"{n:>13s} cos / ratio" for n in names))
     for k, v in res.items():
-        print(f"{k:4s}     " + "   ".join(f"{c:.4f} / {q:.4f}" for c, q in v))
+        print(f"{k:4s}     " + "   ".join(f"      {c:.4f} / {q:.4f}" for c, q in v))
 
 
 if __name__ == "__main__":
