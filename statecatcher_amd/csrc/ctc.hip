@@ -19,13 +19,14 @@
 //                     tools/ctc_precision.py)
 //   ctc_chain_kernel  per b: for every target position the next position with the same label,
 //                     so label occupancies are summed in a fixed order (deterministic, no atomics)
-//   ctc_lin_kernel    (Umax <= 255, the default) ONE WAVE per (sequence, direction), 2B waves:
+//   ctc_lin_kernel    (Umax <= 255, SC_CTC_LIN=1; measured slower, see lin_run) ONE WAVE per
+//                     (sequence, direction), 2B waves:
 //                     the lattice in linear probability space, fp64, renormalised every 16 steps
 //                     by exact powers of two — five full-rate fp64 adds / multiplies per state
 //                     pair and step instead of five quarter-rate exp2 / log2 (see lin_run); falls
 //                     back per sequence to ab1_run (the same one-wave layout in fp32 log space)
 //                     when an emission or the whole wave would underflow
-//   ctc_ab_kernel     (Umax > 255) one workgroup per (sequence, direction): 2B workgroups run alpha forward
+//   ctc_ab_kernel     (the default) one workgroup per (sequence, direction): 2B workgroups run alpha forward
 //                     and beta backward concurrently.  Two states (a blank and its label) per
 //                     lane; each wave also carries a K-pair halo of its neighbour's pairs so it
 //                     advances K steps with DPP wave_shr:1 / wave_shl:1 only (no LDS, no
@@ -40,8 +41,8 @@
 #include "sc_common.h"
 
 #ifndef SC_CTC_ABL   // ablation bitmask (timing studies only; results are wrong when set):
-#define SC_CTC_ABL 0  // 1 no halo exchange, 2 no per-step stores, 4 max instead of log-sum-exp
-#endif
+#define SC_CTC_ABL 0  // 1 no halo exchange, 2 no per-step stores, 4 max instead of log-sum-exp,
+#endif                // (ctc_lin_kernel) 8 no renormalisation, 16 no emission loads
 #ifndef SC_CTC_KMAX   // most steps between halo exchanges (8 or 16)
 #define SC_CTC_KMAX 16
 #endif
@@ -195,7 +196,8 @@ __global__ void __launch_bounds__(256) ctc_emit_kernel(CtcArgs a) {
   float* out = a.ws.lpe + row * a.Sp;
   const float* exr = a.ex ? a.ex + (int64_t)b * a.exb + (int64_t)t * a.ext : nullptr;
   auto lp2 = [&](int s) {
-    const float xl = exr ? exr[(s + 1) >> 1] : E::ld(p[state_label(tg, s, a.blank, a.V)]);
+    // (ex column: 0 for the blank states, 1 + u for label state 2u + 1)
+    const float xl = exr ? exr[(s & 1) ? (s + 1) >> 1 : 0] : E::ld(p[state_label(tg, s, a.blank, a.V)]);
     return fmaxf((xl - lse) * kLog2e, -1e30f);
   };
   float c = -1e30f;
@@ -772,7 +774,8 @@ __device__ __forceinline__ bool lin_run(const CtcArgs& a, int b, int Tb, int Ub)
       const uint32_t so = (uint32_t)tstep(min(i0 + s, Tb - 1)) * rowb;
 #pragma unroll
       for (int j = 0; j < PPL; ++j)
-        buf[s][j] = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(ers, vo[j], so, 0));
+        buf[s][j] = (SC_CTC_ABL & 16) ? f2v{0.5f, 0.25f}
+                                      : __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(ers, vo[j], so, 0));
     }
   };
   double vB[PPL], vL[PPL];
@@ -821,7 +824,7 @@ __device__ __forceinline__ bool lin_run(const CtcArgs& a, int b, int Tb, int Ub)
           vL[j] = nl;
         }
       }
-      if ((i + 1) % kAb1R == 0) {   // renormalise the wave max to [0.5, 1) (exact)
+      if (!(SC_CTC_ABL & 8) && (i + 1) % kAb1R == 0) {   // renormalise the wave max to [0.5, 1)
         double m = 0.0;
 #pragma unroll
         for (int j = 0; j < PPL; ++j) m = fmax(m, fmax(vB[j], vL[j]));
@@ -844,9 +847,10 @@ __device__ __forceinline__ bool lin_run(const CtcArgs& a, int b, int Tb, int Ub)
       const uint32_t so = (uint32_t)tstep(i) * orowb;
 #pragma unroll
       for (int j = 0; j < PPL; ++j)
-        __builtin_amdgcn_raw_buffer_store_b128(
-            __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, d2v{vB[j], vL[j]}),
-            ors, oo[j], so, 0);
+        if (!(SC_CTC_ABL & 2))
+          __builtin_amdgcn_raw_buffer_store_b128(
+              __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, d2v{vB[j], vL[j]}),
+              ors, oo[j], so, 0);
     }
   };
   load(bufA, 0);
@@ -907,12 +911,16 @@ __global__ void __launch_bounds__(64) ctc_lin_kernel(CtcArgs a) {
   if (threadIdx.x == 0) a.ws.flag[(is_beta ? 2 : 1) * a.B + b] = lin ? 1 : 0;
 }
 
-// pairs per lane of the one-wave lattice family (0: the multi-wave kernel, Umax > 255).
-// SC_CTC_LIN=0 in the environment forces the multi-wave kernel (A/B timing in tools only).
+// pairs per lane of the one-wave lattice family (0: the multi-wave kernel).  Off unless
+// SC_CTC_LIN=1 in the environment.  Measured at C2 (tools/scan_bench.py --only ctc, ablation
+// builds of tools/ctc_abl.sh; profiles/r4_lattice_ab.md): emit + chain + lattice 256 us against
+// 211 us for the multi-wave log-space kernel, and the gradient 60 us slower on the fp64 rows.
+// Dropping the per-step stores (ABL 2) takes 62 us off: vmcnt retires loads and stores in issue
+// order, so waiting for a prefetched emission row also waits for the older row stores.
 static int lin_ppl(int Umax) {
   static const bool on = [] {
     const char* e = getenv("SC_CTC_LIN");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   const int ppl = (Umax + 1 + 63) / 64;
   return (on && ppl <= 4) ? ppl : 0;
@@ -944,12 +952,14 @@ template <int DT, int GT>
 __global__ void __launch_bounds__(256) ctc_grad_kernel(CtcArgs a) {
   using E = Elem<DT>;
   using G = Elem<GT>;
-  extern __shared__ __attribute__((aligned(16))) float lcab_all[];   // [4][V + 4] (x2 with ex)
+  extern __shared__ __attribute__((aligned(16))) float lcab_all[];   // [4][V + 4]
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t row = (int64_t)blockIdx.x * (blockDim.x >> 6) + w;
   if (row >= (int64_t)a.B * a.T) return;
-  float* lcab = lcab_all + w * (a.ex ? 2 : 1) * (a.V + 4);
-  float* xex = lcab + (a.V + 4);   // (ex) the row's emission logits by column, NaN elsewhere
+  // the row's label occupancies by column (base-2 log-sums; -inf off the emission columns).  With
+  // emission logits (a.ex) an emission column holds its finished gradient value instead: softmax
+  // term and occupancy both from the exact logit, so the output pass only needs "is it -inf"
+  float* lcab = lcab_all + w * (a.V + 4);
   const int b = (int)(row / a.T), t = (int)(row % a.T);
   const int Tb = clampi(a.in_lens[b], 0, a.T);
   typename G::T* g = (typename G::T*)a.grad + row * a.V;
@@ -976,8 +986,6 @@ __global__ void __launch_bounds__(256) ctc_grad_kernel(CtcArgs a) {
   const int Um = a.Umax > 0 ? a.Umax : 1;
   const int64_t* tg = a.tg + (int64_t)b * a.tgs;
   for (int v = lane; v < a.V; v += 64) lcab[v] = kNegInf;
-  if (a.ex)
-    for (int v = lane; v < a.V; v += 64) xex[v] = __builtin_nanf("");
   wave_lds_sync();
   const float* exr = a.ex ? a.ex + (int64_t)b * a.exb + (int64_t)t * a.ext : nullptr;
   const float* al = a.ws.alpha + ((int64_t)b * a.T + t) * a.apitch;
@@ -1001,6 +1009,12 @@ __global__ void __launch_bounds__(256) ctc_grad_kernel(CtcArgs a) {
                              (double)a.ws.cst[(int64_t)b * a.T + t] - a.ws.ll2s[b]);
   const int* chain = a.ws.chain + (int64_t)b * Um;
   const int* first = a.ws.first + (int64_t)b * Um;
+  const float lse = a.is_logits ? a.ws.lse[(int64_t)b * a.T + t] : 0.0f;
+  // (ex) the finished gradient of an emission column from its exact logit and occupancy
+  auto exact_grad = [&](float logit, float occ2) {
+    const float lp2 = (logit - lse) * kLog2e;
+    return (exp2_(lp2) - exp2_(occ2 + koff - lp2)) * sc;
+  };
   float m = kNegInf, l = 0.0f;   // blank-label occupancy (base 2), per lane
   for (int s = lane; s < Sb; s += 64) {
     const int lab = (s & 1) ? (int)tg[(s - 1) >> 1] : a.blank;
@@ -1017,10 +1031,7 @@ __global__ void __launch_bounds__(256) ctc_grad_kernel(CtcArgs a) {
         float acc = val;
         for (int q = chain[u]; q >= 0; q = chain[q])
           acc = lse2_b2(acc, lv(al, linA, 2 * q + 1) + lv(be, linB, 2 * q + 1));
-        if (lab >= 0 && lab < a.V) {
-          lcab[lab] = acc;
-          if (exr) xex[lab] = exr[1 + u];
-        }
+        if (lab >= 0 && lab < a.V) lcab[lab] = exr ? exact_grad(exr[1 + u], acc) : acc;
       }
     }
   }
@@ -1030,12 +1041,11 @@ __global__ void __launch_bounds__(256) ctc_grad_kernel(CtcArgs a) {
     m = M;
   }
   if (lane == 0 && a.blank >= 0 && a.blank < a.V) {
-    lcab[a.blank] = (m == kNegInf) ? kNegInf : m + log2_(l);
-    if (exr) xex[a.blank] = exr[0];
+    const float ob = (m == kNegInf) ? kNegInf : m + log2_(l);
+    lcab[a.blank] = exr ? exact_grad(exr[0], ob) : ob;
   }
   wave_lds_sync();
   const typename E::T* xr = (const typename E::T*)a.x + (int64_t)b * a.sb + (int64_t)t * a.stt;
-  const float lse = a.is_logits ? a.ws.lse[(int64_t)b * a.T + t] : 0.0f;
   // grad = (softmax - occupancy) * scale
   if (gvec && ((uintptr_t)xr & 15) == 0) {
     for (int c = lane; c < (a.V >> 3); c += 64) {
@@ -1048,16 +1058,11 @@ __global__ void __launch_bounds__(256) ctc_grad_kernel(CtcArgs a) {
       }
       const float4 l0 = *(const float4*)&lcab[8 * c], l1 = *(const float4*)&lcab[8 * c + 4];
       const float lc[8] = {l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, l1.z, l1.w};
-      if (a.ex) {   // the emission columns' exact logits (softmax term and occupancy alike)
-        const float4 e0 = *(const float4*)&xex[8 * c], e1 = *(const float4*)&xex[8 * c + 4];
-        const float ev[8] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w};
-#pragma unroll
-        for (int k = 0; k < 8; ++k) xv[k] = ev[k] == ev[k] ? ev[k] : xv[k];
-      }
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         const float lp2 = (xv[k] - lse) * kLog2e;
         gv[k] = (exp2_(lp2) - exp2_(lc[k] + koff - lp2)) * sc;
+        if (a.ex && lc[k] != kNegInf) gv[k] = lc[k];   // (an emission column's finished value)
       }
       if constexpr (Vec16<GT>::N == 8) {
         Vec16<GT>::st(g + 8 * c, gv);
@@ -1069,11 +1074,10 @@ __global__ void __launch_bounds__(256) ctc_grad_kernel(CtcArgs a) {
     return;
   }
   for (int v = lane; v < a.V; v += 64) {
-    float xv = E::ld(xr[v]);
-    if (a.ex && xex[v] == xex[v]) xv = xex[v];
-    const float lp2 = (xv - lse) * kLog2e;
-    const float gv = exp2_(lp2) - exp2_(lcab[v] + koff - lp2);
-    g[v] = G::st(gv * sc);
+    const float lp2 = (E::ld(xr[v]) - lse) * kLog2e;
+    const float lc = lcab[v];
+    const float gv = (a.ex && lc != kNegInf) ? lc : (exp2_(lp2) - exp2_(lc + koff - lp2)) * sc;
+    g[v] = G::st(gv);
   }
 }
 
@@ -1109,10 +1113,9 @@ static void launch_fwd(const CtcArgs& a, hipStream_t st) {
 template <int DT, int GT>
 static void launch_bwd(const CtcArgs& a, hipStream_t st) {
   // 4 rows (waves) per workgroup while their LDS rows fit the default 64 KB, else 1
-  const int nr = a.ex ? 2 : 1;   // LDS rows per wave
-  const int R = 4 * nr * (a.V + 4) * (int)sizeof(float) <= 65536 ? 4 : 1;
+  const int R = 4 * (a.V + 4) * (int)sizeof(float) <= 65536 ? 4 : 1;
   hipLaunchKernelGGL((ctc_grad_kernel<DT, GT>), dim3((unsigned)(((int64_t)a.B * a.T + R - 1) / R)),
-                     dim3(64 * R), R * nr * (a.V + 4) * sizeof(float), st, a);
+                     dim3(64 * R), R * (a.V + 4) * sizeof(float), st, a);
 }
 
 // nn.CTCLoss(reduction='mean', zero_infinity=True) on device in one launch: loss =

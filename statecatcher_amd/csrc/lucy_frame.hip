@@ -169,9 +169,11 @@ __global__ void __launch_bounds__(64 * NT * KS) lucy_frame_gemm(FrameGemmArgs a)
 #pragma unroll
       for (int i = 0; i < SMAX; ++i) {
         const int k0 = (c0 + i) * 16 + 4 * q;
-        const bool in = c0 + i < se && k0 < a.K && cok;
+        // (zero the LDS operand's k slots past the slice or K: the weight there may be any
+        // clamped value.  Columns past N read W row 0 and are never stored.)
+        const bool in = c0 + i < se && k0 < a.K;
         float4 xa = xb[i];
-        xa.x = in ? xa.x : 0.f;   // (zero the LDS operand: the weight may be any clamped value)
+        xa.x = in ? xa.x : 0.f;
         xa.y = in ? xa.y : 0.f;
         xa.z = in ? xa.z : 0.f;
         xa.w = in ? xa.w : 0.f;
@@ -197,7 +199,7 @@ __global__ void __launch_bounds__(64 * NT * KS) lucy_frame_gemm(FrameGemmArgs a)
 #pragma unroll
       for (int i = 0; i < SMAX; ++i) {
         const int k0 = (c0 + i) * 32 + 8 * q;
-        const bool in = c0 + i < se && k0 < a.K && cok;
+        const bool in = c0 + i < se && k0 < a.K;   // (as the fp32 path)
         const int kx = min((c0 + i) * 32, kpad - 32) + 8 * q;
         const float4 x0 = *(const float4*)(xrow + kx), x1 = *(const float4*)(xrow + kx + 4);
         const bf16x8 av = {(__bf16)x0.x, (__bf16)x0.y, (__bf16)x0.z, (__bf16)x0.w,

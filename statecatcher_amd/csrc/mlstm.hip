@@ -126,6 +126,7 @@ struct MArgs {
   // xLSTM layer reads them in place from its fused projection [B][T][N] (h = D, t = N).
   int NH;
   int64_t qb, qh, qt, vb, vh, vt;
+  int xcd;   // mlstm_fw_walk on a 1-D grid with the column blocks of one bh on one XCD
 };
 
 __device__ __forceinline__ int64_t qrow(const MArgs& a, int bh, int64_t t) {
@@ -307,8 +308,17 @@ __global__ void __launch_bounds__(256, 2) mlstm_fw_walk(MArgs a) {
   // image; the outputs come from mlstm_fw_out).
   static_assert(MODE == 0 || MODE == 1, "walk modes");
   constexpr bool kOut = MODE == 0;
-  const int cb = blockIdx.x, w = threadIdx.x >> 6;
-  const int bh = (int)blockIdx.y;
+  // XCD-aware order (a.xcd): workgroup i runs on XCD i % 8, so the DV / kCB column blocks of
+  // sequence bh take i = x + 8 (NCB s + cb) for bh = 8 s + x: they read the same K / Q rows
+  // chunk by chunk, and on one XCD the second and third reads hit its L2 instead of HBM
+  constexpr int NCB = DV / kCB;
+  int cb = blockIdx.x, bh = (int)blockIdx.y;
+  if (a.xcd) {
+    const int x = (int)blockIdx.x & 7, sl = (int)blockIdx.x >> 3;
+    cb = sl % NCB;
+    bh = (sl / NCB) * 8 + x;
+  }
+  const int w = threadIdx.x >> 6;
   int tid = threadIdx.x, lane = tid & 63;
   const int cj0 = cb * kCB;
   __shared__ __attribute__((aligned(16))) T Qs[kL * LQ];
@@ -1297,13 +1307,21 @@ bool fwd_split() {
   const char* e = getenv("SC_MLSTM_SPLIT");
   return !(e && e[0] == '0');
 }
+// SC_MLSTM_XCD=0 (environment, read per launch) keeps the plain (column block, bh) grid (A/B)
+bool fwd_xcd() {
+  const char* e = getenv("SC_MLSTM_XCD");
+  return !(e && e[0] == '0');
+}
 template <int DT, int IO, int DQ, int DV>
-void launch_fwd(const MArgs& a, hipStream_t st) {
+void launch_fwd(const MArgs& a0, hipStream_t st) {
+  MArgs a = a0;
+  a.xcd = (a.BH % 8 == 0 && fwd_xcd()) ? 1 : 0;
+  const dim3 grid = a.xcd ? dim3((DV / kCB) * a.BH) : dim3(DV / kCB, a.BH);
   if (!fwd_split()) {
-    hipLaunchKernelGGL((mlstm_fw_walk<DT, IO, DQ, DV, 0>), dim3(DV / kCB, a.BH), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((mlstm_fw_walk<DT, IO, DQ, DV, 0>), grid, dim3(256), 0, st, a);
     return;
   }
-  hipLaunchKernelGGL((mlstm_fw_walk<DT, IO, DQ, DV, 1>), dim3(DV / kCB, a.BH), dim3(256), 0, st, a);
+  hipLaunchKernelGGL((mlstm_fw_walk<DT, IO, DQ, DV, 1>), grid, dim3(256), 0, st, a);
   if (a.nc > 0)
     hipLaunchKernelGGL((mlstm_fw_out<DT, IO, DQ, DV>), dim3(a.BH * a.nc), dim3(256), 0, st, a);
 }

@@ -7,6 +7,7 @@
 //   rd_seg192     16 B per lane, 192-B row segments at a 4624-B row stride (q / k rows of the
 //                 xLSTM's fused projection, DQ = 96 bf16, N = 2312 columns)
 //   rd_seg384     the same with 384-B segments (v rows, DV = 192)
+//   rd_seg128     the same with 128-B segments (one 64-column block of a v row: mlstm_fw_walk)
 //   rd_seg<192,1> 16 B per lane, contiguous 192-B rows (a [BH][T][96] bf16 operand)
 //   wr_stream     16 B per lane contiguous stores
 //   wr_seg192     16 B per lane, 192-B segments at 4624 B (dq / dk written into the gradient
@@ -89,6 +90,7 @@ int main() {
     hipLaunchKernelGGL(rd_stream, g, b, 0, 0, (const u32x4*)buf, span / 16, sink);
     hipLaunchKernelGGL((rd_seg<192, 0>), g, b, 0, 0, buf, kRows, kStride, sink);
     hipLaunchKernelGGL((rd_seg<384, 0>), g, b, 0, 0, buf, kRows, kStride, sink);
+    hipLaunchKernelGGL((rd_seg<128, 0>), g, b, 0, 0, buf + 1536, kRows, kStride, sink);
     hipLaunchKernelGGL((rd_seg<192, 1>), g, b, 0, 0, buf, kRows, (int64_t)192, sink);
     hipLaunchKernelGGL(wr_stream, g, b, 0, 0, (u32x4*)buf, span / 16);
     hipLaunchKernelGGL((wr_seg<192>), g, b, 0, 0, buf, kRows, kStride);
@@ -98,6 +100,7 @@ int main() {
   printf("rd_stream %lld\n", (long long)span);
   printf("rd_seg<192, 0> %lld\n", (long long)(kRows * 192));
   printf("rd_seg<384, 0> %lld\n", (long long)(kRows * 384));
+  printf("rd_seg<128, 0> %lld\n", (long long)(kRows * 128));
   printf("rd_seg<192, 1> %lld\n", (long long)(kRows * 192));
   printf("wr_stream %lld\n", (long long)span);
   printf("wr_seg<192> %lld\n", (long long)(kRows * 192));
