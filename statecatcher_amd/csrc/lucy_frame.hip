@@ -98,6 +98,7 @@ template <bool BF16W, bool LN, int EPI, int NT, int KS>
 __global__ void __launch_bounds__(64 * NT * KS) lucy_frame_gemm(FrameGemmArgs a) {
   __shared__ float part[NT * KS][16][17];   // per-wave 16 x 16 partial sums (padded rows)
   __shared__ float stat[16][2];             // PRO_LN: (mean, rstd) of the workgroup's rows
+  __shared__ float4 recs[LN ? 16 : 1][16];  // PRO_LN: the rows' statistics records
   extern __shared__ __attribute__((aligned(16))) float xs[];   // the A rows [16][kpitch]
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // (wave-uniform: scalar)
@@ -108,103 +109,159 @@ __global__ void __launch_bounds__(64 * NT * KS) lucy_frame_gemm(FrameGemmArgs a)
   const int cbase = CELL ? blockIdx.x * 16 + t * a.gstride : (blockIdx.x * NT + t) * 16;
   const int nsteps = (a.K + KSTEP - 1) / KSTEP;
   const int kpad = nsteps * KSTEP, kpitch = kpad + 4;   // +4 floats: conflict-free row reads
-  // the row statistics of the prologue, once per workgroup
-  if (LN) {
-    if (threadIdx.x < 16) {
-      const int r = min(r0 + (int)threadIdx.x, a.B - 1);
-      float mean, rstd;
-      combine_stats(a.st_in + r, a.nst_in, a.B, a.eps, mean, rstd);
-      stat[threadIdx.x][0] = mean;
-      stat[threadIdx.x][1] = rstd;
-    }
-    __syncthreads();
-  }
-  // The workgroup's 16 A rows (LayerNorm applied, rows past B and columns past K zero) into LDS
-  // with coalesced 16-byte loads: every wave then reads its fragments from LDS, and no global
-  // load of the MFMA loop depends on a row or K condition
-  {
-    const int per_row = kpad / 4;   // float4 pieces per row
-    for (int i = threadIdx.x; i < 16 * per_row; i += 64 * NT * KS) {
-      const int rr = i / per_row, k = 4 * (i % per_row);
-      const int r = r0 + rr;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (r < a.B && k < a.K) {   // (K % 4 == 0: a piece is wholly inside or outside)
-        v = *(const float4*)(a.x + (int64_t)r * a.ldx + k);
-        if (LN) {
-          const float mu = stat[rr][0], rs = stat[rr][1];
-          const float4 lw = *(const float4*)(a.ln_w + k), lb = *(const float4*)(a.ln_b + k);
-          v.x = (v.x - mu) * rs * lw.x + lb.x;
-          v.y = (v.y - mu) * rs * lw.y + lb.y;
-          v.z = (v.z - mu) * rs * lw.z + lb.z;
-          v.w = (v.w - mu) * rs * lw.w + lb.w;
-        }
-      }
-      *(float4*)(xs + rr * kpitch + k) = v;
-    }
-    __syncthreads();
-  }
   const int col = cbase + (lane & 15);
   const bool cok = CELL || col < a.N;
   const int sb = (int)((int64_t)nsteps * ks / KS), se = (int)((int64_t)nsteps * (ks + 1) / KS);
-  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
   const int q = lane >> 4;
-  const float* xrow = xs + (lane & 15) * kpitch;
-  // Every weight load of a chunk of SMAX steps is issued before its first MFMA (one exposed memory
-  // latency per chunk).  The chunk always runs SMAX steps: a load past the slice or past K reads a
-  // clamped address (always inside the matrix) and is zeroed by a select, so the loop carries no
-  // branch around a load and no per-step wait.
-  if constexpr (!BF16W) {
-    constexpr int SMAX = NT * KS > 8 ? 8 : 16;   // (10 waves: 3 per SIMD, <= 168 VGPRs)
-    const float* wr = (const float*)a.w + (int64_t)(cok ? col : 0) * a.ldw;
-    for (int c0 = sb; c0 < se; c0 += SMAX) {
-      float4 wb[SMAX], xb[SMAX];
+  constexpr int NTH = 64 * NT * KS;
+  // Latency chain of a frame kernel: one memory round trip for everything the MFMAs need (the
+  // first weight chunk, the A rows, the LayerNorm records and parameters, the epilogue's bias /
+  // state / mask), then the MFMAs, then the epilogue.  So every one of those loads is issued
+  // before the first wait.
+  constexpr int SMAXF = NT * KS > 8 ? 8 : 16;   // fp32: steps per weight chunk (10 waves: 3 per SIMD)
+  constexpr int SMAXB = 8;                      // bf16
+  float4 wf[BF16W ? 1 : SMAXF];
+  bf16x8 wh[BF16W ? SMAXB : 1];
+  const float* wrf = (const float*)a.w + (int64_t)(cok ? col : 0) * a.ldw;
+  const __bf16* wrh = (const __bf16*)a.w + (int64_t)(cok ? col : 0) * a.ldw;
+  auto load_chunk = [&](int c0) __attribute__((always_inline)) {
+    if constexpr (!BF16W) {
 #pragma unroll
-      for (int i = 0; i < SMAX; ++i) {
-        const int k0 = (c0 + i) * 16 + 4 * q;
-        wb[i] = *(const float4*)(wr + min(k0, a.K - 4));
+      for (int i = 0; i < SMAXF; ++i) wf[i] = *(const float4*)(wrf + min((c0 + i) * 16 + 4 * q, a.K - 4));
+    } else {
+#pragma unroll
+      for (int i = 0; i < SMAXB; ++i) wh[i] = *(const bf16x8*)(wrh + min((c0 + i) * 32 + 8 * q, a.K - 8));
+    }
+  };
+  load_chunk(sb);
+  // epilogue operands
+  float e_bias[5] = {0.f, 0.f, 0.f, 0.f, 0.f}, e_s = 0.f, e_m = 1.f;
+  {
+    if constexpr (CELL) {
+      if (w < 4) {
+        const int rr = 4 * w + q, rc = min(r0 + rr, a.B - 1), d = blockIdx.x * 16 + (lane & 15);
+#pragma unroll
+        for (int g = 0; g < (EPI == FR_CELL_FUSED ? 5 : 4); ++g) e_bias[g] = a.bias[g * a.gstride + d];
+        e_s = a.s[(int64_t)rc * a.gstride + d];
+        if (a.mask) e_m = a.mask[rc];
+      }
+    } else {
+      if (w < NT && cok) e_bias[0] = a.bias[col];
+    }
+  }
+  // The workgroup's 16 A rows (LayerNorm applied, rows past B and columns past K zero) into LDS
+  // with coalesced 16-byte loads: every wave then reads its fragments from LDS, and no global
+  // load of the MFMA loop depends on a row or K condition.  Up to 4 pieces per thread are loaded
+  // before the LayerNorm statistics are combined.
+  {
+    const int per_row = kpad / 4;   // float4 pieces per row
+    const int npc = 16 * per_row;
+    for (int i0 = 0; i0 < npc; i0 += 4 * NTH) {
+      float4 v[4], lw[4], lb[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int i = i0 + j * NTH + threadIdx.x;
+        const int rr = i / per_row, k = 4 * (i % per_row), r = r0 + rr;
+        v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (i < npc && r < a.B && k < a.K) {   // (K % 4 == 0: a piece is wholly in or out)
+          v[j] = *(const float4*)(a.x + (int64_t)r * a.ldx + k);
+          if (LN) {
+            lw[j] = *(const float4*)(a.ln_w + k);
+            lb[j] = *(const float4*)(a.ln_b + k);
+          }
+        }
+      }
+      if (LN && i0 == 0) {   // the row statistics, once per workgroup, while the pieces load
+        if (a.nst_in <= 16) {   // one record per thread into LDS, then 16 threads combine them
+          if (threadIdx.x < 256) {
+            const int rr = threadIdx.x >> 4, j = threadIdx.x & 15;
+            const int r = min(r0 + rr, a.B - 1);
+            recs[rr][j] = j < a.nst_in ? a.st_in[(int64_t)j * a.B + r] : make_float4(0.f, 0.f, 0.f, 0.f);
+          }
+          __syncthreads();
+          if (threadIdx.x < 16) {   // Chan: (n, mean, M2) of the row from its records
+            const int rr = threadIdx.x;
+            float n = 0.0f, sm = 0.0f;
+            for (int j = 0; j < a.nst_in; ++j) {
+              n += recs[rr][j].x;
+              sm += recs[rr][j].x * recs[rr][j].y;
+            }
+            const float mean = sm / n;
+            float m2 = 0.0f;
+            for (int j = 0; j < a.nst_in; ++j) {
+              const float d = recs[rr][j].y - mean;
+              m2 += recs[rr][j].z + recs[rr][j].x * d * d;
+            }
+            stat[rr][0] = mean;
+            stat[rr][1] = 1.0f / sqrtf(m2 / n + a.eps);
+          }
+        } else if (threadIdx.x < 16) {
+          const int r = min(r0 + (int)threadIdx.x, a.B - 1);
+          float mean, rstd;
+          combine_stats(a.st_in + r, a.nst_in, a.B, a.eps, mean, rstd);
+          stat[threadIdx.x][0] = mean;
+          stat[threadIdx.x][1] = rstd;
+        }
+        __syncthreads();
       }
 #pragma unroll
-      for (int i = 0; i < SMAX; ++i) xb[i] = *(const float4*)(xrow + min((c0 + i) * 16, kpad - 16) + 4 * q);
+      for (int j = 0; j < 4; ++j) {
+        const int i = i0 + j * NTH + threadIdx.x;
+        const int rr = i / per_row, k = 4 * (i % per_row), r = r0 + rr;
+        if (i < npc) {
+          if (LN && r < a.B && k < a.K) {
+            const float mu = stat[rr][0], rs = stat[rr][1];
+            v[j].x = (v[j].x - mu) * rs * lw[j].x + lb[j].x;
+            v[j].y = (v[j].y - mu) * rs * lw[j].y + lb[j].y;
+            v[j].z = (v[j].z - mu) * rs * lw[j].z + lb[j].z;
+            v[j].w = (v[j].w - mu) * rs * lw[j].w + lb[j].w;
+          }
+          *(float4*)(xs + rr * kpitch + k) = v[j];
+        }
+      }
+    }
+    __syncthreads();
+  }
+  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  const float* xrow = xs + (lane & 15) * kpitch;
+  // A chunk runs SMAX steps: a load past the slice or past K reads a clamped address (always
+  // inside the matrix) and the LDS operand's k slots there are zeroed by a select (no branch
+  // around a load, no per-step wait).  Columns past N read W row 0 and are never stored.
+  if constexpr (!BF16W) {
+    for (int c0 = sb; c0 < se; c0 += SMAXF) {
+      if (c0 != sb) load_chunk(c0);
+      float4 xb[SMAXF];
+#pragma unroll
+      for (int i = 0; i < SMAXF; ++i) xb[i] = *(const float4*)(xrow + min((c0 + i) * 16, kpad - 16) + 4 * q);
       __builtin_amdgcn_sched_barrier(0);   // keep the loads ahead of the MFMAs (no sinking)
 #pragma unroll
-      for (int i = 0; i < SMAX; ++i) {
-        const int k0 = (c0 + i) * 16 + 4 * q;
-        // (zero the LDS operand's k slots past the slice or K: the weight there may be any
-        // clamped value.  Columns past N read W row 0 and are never stored.)
-        const bool in = c0 + i < se && k0 < a.K;
+      for (int i = 0; i < SMAXF; ++i) {
+        const bool in = c0 + i < se && (c0 + i) * 16 + 4 * q < a.K;
         float4 xa = xb[i];
         xa.x = in ? xa.x : 0.f;
         xa.y = in ? xa.y : 0.f;
         xa.z = in ? xa.z : 0.f;
         xa.w = in ? xa.w : 0.f;
         // k slot q of MFMA j is k0 + j for both operands: the sum runs over the same k set
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(xa.x, wb[i].x, acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(xa.y, wb[i].y, acc1, 0, 0, 0);
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(xa.z, wb[i].z, acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(xa.w, wb[i].w, acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(xa.x, wf[i].x, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(xa.y, wf[i].y, acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(xa.z, wf[i].z, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(xa.w, wf[i].w, acc1, 0, 0, 0);
       }
     }
   } else {
-    constexpr int SMAX = 8;
-    const __bf16* wr = (const __bf16*)a.w + (int64_t)(cok ? col : 0) * a.ldw;
     const bf16x8 zero8 = {};
-    for (int c0 = sb; c0 < se; c0 += SMAX) {
-      bf16x8 wb[SMAX];
-#pragma unroll
-      for (int i = 0; i < SMAX; ++i) {
-        const int k0 = (c0 + i) * 32 + 8 * q;
-        wb[i] = *(const bf16x8*)(wr + min(k0, a.K - 8));
-      }
+    for (int c0 = sb; c0 < se; c0 += SMAXB) {
+      if (c0 != sb) load_chunk(c0);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int i = 0; i < SMAX; ++i) {
-        const int k0 = (c0 + i) * 32 + 8 * q;
-        const bool in = c0 + i < se && k0 < a.K;   // (as the fp32 path)
+      for (int i = 0; i < SMAXB; ++i) {
+        const bool in = c0 + i < se && (c0 + i) * 32 + 8 * q < a.K;
         const int kx = min((c0 + i) * 32, kpad - 32) + 8 * q;
         const float4 x0 = *(const float4*)(xrow + kx), x1 = *(const float4*)(xrow + kx + 4);
         const bf16x8 av = {(__bf16)x0.x, (__bf16)x0.y, (__bf16)x0.z, (__bf16)x0.w,
                            (__bf16)x1.x, (__bf16)x1.y, (__bf16)x1.z, (__bf16)x1.w};
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(in ? av : zero8, wb[i], acc0, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(in ? av : zero8, wh[i], acc0, 0, 0, 0);
       }
     }
   }
@@ -229,7 +286,7 @@ __global__ void __launch_bounds__(64 * NT * KS) lucy_frame_gemm(FrameGemmArgs a)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int r = r0 + 4 * q + i, c = cbase + (lane & 15);
-        const float v = part[w][4 * q + i][lane & 15] + (c < a.N ? a.bias[c] : 0.0f);
+        const float v = part[w][4 * q + i][lane & 15] + e_bias[0];
         part[w][4 * q + i][lane & 15] = v;
         if (r < a.B && c < a.N) a.y[(int64_t)r * a.ldy + c] = v;
       }
@@ -256,12 +313,11 @@ __global__ void __launch_bounds__(64 * NT * KS) lucy_frame_gemm(FrameGemmArgs a)
       const int rr = 4 * w + q, r = r0 + rr, d = blockIdx.x * 16 + (lane & 15);
       const int D = a.gstride;
       const bool ok = r < a.B;
-      const int rc = ok ? r : a.B - 1;
-      auto gate = [&](int g) { return part[g][rr][lane & 15] + a.bias[g * a.gstride + d]; };
+      auto gate = [&](int g) { return part[g][rr][lane & 15] + e_bias[g]; };
       const float z = gate(0), k = gate(1), v = gate(2);
       const float dl = gate(EPI == FR_CELL_FUSED ? 4 : 3);
-      const float m = a.mask ? a.mask[rc] : 1.0f;
-      const float sp = a.s[(int64_t)rc * D + d];
+      const float m = e_m;
+      const float sp = e_s;
       const float sn = (1.0f / (1.0f + expf(-dl))) * sp + k * v;
       float o;
       if (EPI == FR_CELL_FUSED) {
