@@ -19,12 +19,11 @@
 //                     tools/ctc_precision.py)
 //   ctc_chain_kernel  per b: for every target position the next position with the same label,
 //                     so label occupancies are summed in a fixed order (deterministic, no atomics)
-//   ctc_lin_kernel    (Umax <= 255, SC_CTC_LIN=1; measured slower, see lin_run) ONE WAVE per
-//                     (sequence, direction), 2B waves:
-//                     the lattice in linear probability space, fp64, renormalised every 16 steps
-//                     by exact powers of two — five full-rate fp64 adds / multiplies per state
-//                     pair and step instead of five quarter-rate exp2 / log2 (see lin_run); falls
-//                     back per sequence to ab1_run (the same one-wave layout in fp32 log space)
+//   ctc_lin_kernel    (Umax <= 255, SC_CTC_LIN=1) the lattice in linear probability space, fp64,
+//                     renormalised every 16 steps by exact powers of two: five full-rate fp64
+//                     adds / multiplies per state pair and step instead of five exp2 / log2; one
+//                     wave computes, two more store its rows as fp32 logs (lin_produce /
+//                     lin_consume); falls back per sequence to ab1_run (one wave, fp32 log space)
 //                     when an emission or the whole wave would underflow
 //   ctc_ab_kernel     (the default) one workgroup per (sequence, direction): 2B workgroups run alpha forward
 //                     and beta backward concurrently.  Two states (a blank and its label) per
@@ -64,8 +63,7 @@ struct CtcWs {
   int* first;     // [B,Um]
   // one-wave family (Umax <= 255) only:
   float* ylin;    // [B,T,Sp]   linear shifted emissions 2^(lpe) (0: dead)
-  int* flag;      // [3][B]     tiny[b]: a live emission below 2^-kTiny (the linear lattice is not
-                  //            used); lin[dir][b]: that direction's rows are linear fp64 values
+  int* flag;      // [B]        a live emission below 2^-kTiny: the linear lattice is not used
 };
 
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -79,7 +77,7 @@ static size_t ws_layout(int B, int T, int Umax, CtcWs* w, void* base) {
   const int S = 2 * Umax + 1;
   const int Sp = 64 * states_per_lane(S);
   const bool lin = lin_ppl(Umax) > 0;
-  const size_t ab = lin ? 8 : 4;   // alpha / beta element: fp64 (linear) rows or fp32 (log)
+  const size_t ab = 4;   // alpha / beta: fp32 base-2 log rows (every lattice)
   const int Um = Umax > 0 ? Umax : 1;
   char* p = (char*)base;
   size_t off = 0;
@@ -100,7 +98,7 @@ static size_t ws_layout(int B, int T, int Umax, CtcWs* w, void* base) {
   t.chain = (int*)take((size_t)B * Um * 4);
   t.first = (int*)take((size_t)B * Um * 4);
   t.ylin = lin ? (float*)take((size_t)B * T * Sp * 4) : nullptr;
-  t.flag = lin ? (int*)take((size_t)3 * B * 4) : nullptr;
+  t.flag = lin ? (int*)take((size_t)B * 4) : nullptr;
   if (w) *w = t;
   return off;
 }
@@ -117,8 +115,7 @@ struct CtcArgs {
   const void* x;
   int is_logits, B, T, V, S, Sp, Umax, blank;
   int kh;   // steps between halo exchanges of ctc_ab_kernel (re-centring every 2 kh steps)
-  int lin;      // the one-wave family (ctc_lin_kernel) runs the lattice
-  int apitch;   // floats per alpha / beta row (2 Sp in the one-wave family: room for fp64)
+  int lin;      // the linear-domain lattice (ctc_lin_kernel) runs
   int64_t sb, stt;
   const int64_t* tg;
   int64_t tgs;
@@ -582,12 +579,12 @@ __device__ __forceinline__ void ab1_run(const CtcArgs& a, int b, int Tb, int Ub)
     }
     vo[j] = p < npairs ? (uint32_t)(8 * p) : kDrop;
   }
-  const uint32_t rowb = (uint32_t)(a.Sp * 4), orowb = (uint32_t)(a.apitch * 4);
+  const uint32_t rowb = (uint32_t)(a.Sp * 4), orowb = rowb;
   const __amdgpu_buffer_rsrc_t ers = __builtin_amdgcn_make_buffer_rsrc(
       a.ws.lpe + (int64_t)b * a.T * a.Sp, 0, (int)(rowb * (uint32_t)a.T), 0x00020000);
   const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
-      (BETA ? a.ws.beta : a.ws.alpha) + (int64_t)b * a.T * a.apitch, 0,
-      (int)(orowb * (uint32_t)a.T), 0x00020000);
+      (BETA ? a.ws.beta : a.ws.alpha) + (int64_t)b * a.T * a.Sp, 0, (int)(orowb * (uint32_t)a.T),
+      0x00020000);
   double* offn = (BETA ? a.ws.offB : a.ws.offA) + (int64_t)b * a.T;
   if (lane == 0) offn[0] = 0.0;
   auto tstep = [&](int i) { return BETA ? Tb - 1 - i : i; };
@@ -706,21 +703,28 @@ __device__ __forceinline__ void ab1_run(const CtcArgs& a, int b, int Tb, int Ub)
   }
 }
 
-// Linear-domain one-wave lattice (the default for Umax <= 255).  The same pair-per-lane layout
-// as ab1_run, but the values are probabilities in fp64: one step of a pair is
+// Linear-domain lattice (SC_CTC_LIN=1, Umax <= 255).  The pair-per-lane layout of ab1_run, but
+// the values are probabilities in fp64: one step of a pair is
 //   alpha:  B' = (B + L[p-1]) e(2p);          L' = (L + B + skip L[p-1]) e(2p+1)
 //   beta:   B' = (B + L) e(2p);               L' = (L + B[p+1] + skip L[p+1]) e(2p+1)
-// five fp64 adds / multiplies (full rate on gfx950's vector ALU) instead of five exp2 / log2 on
-// the quarter-rate transcendental unit, and exact 0 is "dead" (the DPP shifts' bound_ctrl zero is
-// the right boundary value).  Every kAb1R steps the wave max is renormalised to [0.5, 1) by an
-// exact power of two (v_ldexp_f64: no rounding), its exponent added to the fp64 offset, which the
-// gradient reads exactly as the log-space kernels' re-centring offsets (log2 alpha = log2(row) +
-// offset).  fp64 keeps 2^-1022 of range below the wave max between renormalisations (fp32 log
-// space keeps all of it; a state 2^1000 below the max that later carries the likelihood is the
-// one case the two differ).  Falls back to the log-space lattice (ab1_run) for a sequence whose
-// live emissions reach below 2^-kTiny (the emit kernel's flag) and for a direction whose wave
-// max underflows to 0 at a renormalisation or whose final likelihood does: then the rows are
-// rewritten in fp32 log space and flag[1 + dir][b] says so to the gradient.
+// five fp64 adds / multiplies (gfx950's vector ALU issues them at the fp32 rate) instead of five
+// exp2 / log2 at the transcendental rate, and exact 0 is "dead" (the DPP shifts' bound_ctrl zero
+// is the right boundary value).  Every kAb1R steps the wave max is renormalised into [0.5, 1) by
+// an exact power of two (v_ldexp_f64: no rounding), its exponent added to the fp64 offset that
+// the gradient reads exactly as the log-space kernels' re-centring offsets.
+//
+// One workgroup of three waves per (sequence, direction).  Wave 0 runs the recurrence and
+// leaves each 16-step chunk of rows in an LDS slot; waves 1 and 2 turn the previous chunk into
+// fp32 base-2 logs (frexp exponent + v_log_f32 of the mantissa) and store it.  So wave 0 issues no
+// global store: its vmcnt holds only the emission prefetch (a wait for a prefetched row would
+// otherwise also wait for every older row store — one workgroup of one wave that stored its own
+// rows measured 217 us at C2, no faster than the multi-wave log-space kernel), and the rows
+// are the same fp32 log-space rows the gradient reads from every other lattice.
+// fp64 keeps 2^1022 of range below the wave max between renormalisations (fp32 log space keeps
+// all of it; a state 2^1022 below the max that later carries the likelihood is the one case the
+// two differ).  A sequence whose live emissions reach below 2^-kTiny (the emit kernel's flag), and
+// a direction whose wave max or final likelihood underflows to 0, run ab1_run (fp32 log space) on
+// wave 0 instead.
 __device__ __forceinline__ double dpp_shr1d(double v) {   // lane-1's value (lane 0: 0)
   const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), 0x138, 0xf, 0xf, true);
   const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), 0x138, 0xf, 0xf, true);
@@ -733,13 +737,25 @@ __device__ __forceinline__ double dpp_shl1d(double v) {   // lane+1's value (lan
 }
 typedef double d2v __attribute__((ext_vector_type(2)));
 
+constexpr int kLinC = kAb1P;   // steps per chunk (LDS slot)
+
+// base-2 log of a non-negative double as fp32 (0 -> the dead sentinel): exact exponent plus the
+// mantissa's v_log_f32
+__device__ __forceinline__ float log2d(double v) {
+  int e;
+  const double m = frexp(v, &e);
+  return v > 0.0 ? (float)e + log2_((float)m) : kDead;
+}
+
+// wave 0: the recurrence over chunks; returns false on underflow (log space then decides)
 template <int PPL, bool BETA>
-__device__ __forceinline__ bool lin_run(const CtcArgs& a, int b, int Tb, int Ub) {
+__device__ __forceinline__ bool lin_produce(const CtcArgs& a, int b, int Tb, int Ub, d2v* slots,
+                                            int* fail_lds) {
   const int lane = threadIdx.x;
   const int64_t* tg = a.tg + (int64_t)b * a.tgs;
   const int npairs = a.Sp / 2;
   double skip[PPL];
-  uint32_t vo[PPL], oo[PPL];   // emission pair / output pair byte offsets (kDrop past the row)
+  uint32_t vo[PPL];   // emission pair byte offsets (kDrop past the row)
   constexpr uint32_t kDrop = 0x80000000u;
 #pragma unroll
   for (int j = 0; j < PPL; ++j) {
@@ -756,21 +772,17 @@ __device__ __forceinline__ bool lin_run(const CtcArgs& a, int b, int Tb, int Ub)
     }
     skip[j] = sk ? 1.0 : 0.0;
     vo[j] = p < npairs ? (uint32_t)(8 * p) : kDrop;
-    oo[j] = p < npairs ? (uint32_t)(16 * p) : kDrop;
   }
-  const uint32_t rowb = (uint32_t)(a.Sp * 4), orowb = (uint32_t)(a.apitch * 4);
+  const uint32_t rowb = (uint32_t)(a.Sp * 4);
   const __amdgpu_buffer_rsrc_t ers = __builtin_amdgcn_make_buffer_rsrc(
       a.ws.ylin + (int64_t)b * a.T * a.Sp, 0, (int)(rowb * (uint32_t)a.T), 0x00020000);
-  const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
-      (BETA ? a.ws.beta : a.ws.alpha) + (int64_t)b * a.T * a.apitch, 0,
-      (int)(orowb * (uint32_t)a.T), 0x00020000);
   double* offn = (BETA ? a.ws.offB : a.ws.offA) + (int64_t)b * a.T;
   if (lane == 0) offn[0] = 0.0;
   auto tstep = [&](int i) { return BETA ? Tb - 1 - i : i; };
-  f2v bufA[kAb1P][PPL], bufB[kAb1P][PPL];
-  auto load = [&](f2v (&buf)[kAb1P][PPL], int i0) {
+  f2v bufA[kLinC][PPL], bufB[kLinC][PPL];
+  auto load = [&](f2v (&buf)[kLinC][PPL], int i0) {
 #pragma unroll
-    for (int s = 0; s < kAb1P; ++s) {
+    for (int s = 0; s < kLinC; ++s) {
       const uint32_t so = (uint32_t)tstep(min(i0 + s, Tb - 1)) * rowb;
 #pragma unroll
       for (int j = 0; j < PPL; ++j)
@@ -783,10 +795,12 @@ __device__ __forceinline__ bool lin_run(const CtcArgs& a, int b, int Tb, int Ub)
   for (int j = 0; j < PPL; ++j) vB[j] = vL[j] = 0.0;
   double off = 0.0;
   bool fail = false;
-  auto body = [&](const f2v (&buf)[kAb1P][PPL], int i0) __attribute__((always_inline)) {
+  // one chunk of steps into slot (chunk & 1); false when the wave underflowed
+  auto body = [&](const f2v (&buf)[kLinC][PPL], int ci) __attribute__((always_inline)) {
+    d2v* slot = slots + (size_t)(ci & 1) * kLinC * PPL * 64;
 #pragma unroll
-    for (int s = 0; s < kAb1P; ++s) {
-      const int i = i0 + s;
+    for (int s = 0; s < kLinC; ++s) {
+      const int i = ci * kLinC + s;
       if (i >= Tb) break;
       if (i == 0) {
 #pragma unroll
@@ -844,23 +858,24 @@ __device__ __forceinline__ bool lin_run(const CtcArgs& a, int b, int Tb, int Ub)
         off += (double)ie;
         if (lane == 0) offn[(i + 1) / kAb1R] = off;
       }
-      const uint32_t so = (uint32_t)tstep(i) * orowb;
 #pragma unroll
-      for (int j = 0; j < PPL; ++j)
-        if (!(SC_CTC_ABL & 2))
-          __builtin_amdgcn_raw_buffer_store_b128(
-              __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, d2v{vB[j], vL[j]}),
-              ors, oo[j], so, 0);
+      for (int j = 0; j < PPL; ++j) slot[(s * PPL + j) * 64 + lane] = d2v{vB[j], vL[j]};
     }
   };
+  const int nch = (Tb + kLinC - 1) / kLinC;
   load(bufA, 0);
-  for (int i0 = 0; i0 < Tb; i0 += 2 * kAb1P) {
-    load(bufB, i0 + kAb1P);
-    body(bufA, i0);
-    if (fail || i0 + kAb1P >= Tb) break;
-    load(bufA, i0 + 2 * kAb1P);
-    body(bufB, i0 + kAb1P);
-    if (fail) break;
+  for (int ci = 0; ci < nch; ++ci) {
+    if (!fail) {
+      if ((ci & 1) == 0) {
+        if (ci + 1 < nch) load(bufB, (ci + 1) * kLinC);
+        body(bufA, ci);
+      } else {
+        if (ci + 1 < nch) load(bufA, (ci + 1) * kLinC);
+        body(bufB, ci);
+      }
+    }
+    if (lane == 0) *fail_lds = fail ? 1 : 0;
+    __syncthreads();   // chunk ci is in its slot (or the lattice failed); consumers take it
   }
   if (fail) return false;
   if (!BETA) {
@@ -889,12 +904,60 @@ __device__ __forceinline__ bool lin_run(const CtcArgs& a, int b, int Tb, int Ub)
   return true;
 }
 
+// waves 1 and 2: chunk ci - 1's rows (slot (ci - 1) & 1) as fp32 base-2 logs into alpha / beta,
+// half of the chunk's steps each, while wave 0 computes chunk ci
+template <int PPL, bool BETA>
+__device__ __forceinline__ void lin_consume(const CtcArgs& a, int b, int Tb, const d2v* slots,
+                                            const int* fail_lds) {
+  const int lane = threadIdx.x & 63, half = (threadIdx.x >> 6) - 1;
+  const int npairs = a.Sp / 2;
+  constexpr uint32_t kDrop = 0x80000000u;
+  uint32_t vo[PPL];
+#pragma unroll
+  for (int j = 0; j < PPL; ++j) {
+    const int p = lane * PPL + j;
+    vo[j] = p < npairs ? (uint32_t)(8 * p) : kDrop;
+  }
+  const uint32_t rowb = (uint32_t)(a.Sp * 4);
+  const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
+      (BETA ? a.ws.beta : a.ws.alpha) + (int64_t)b * a.T * a.Sp, 0, (int)(rowb * (uint32_t)a.T),
+      0x00020000);
+  const int nch = (Tb + kLinC - 1) / kLinC;
+  bool stop = false;
+  auto consume = [&](int ci) {
+    const d2v* slot = slots + (size_t)(ci & 1) * kLinC * PPL * 64;
+#pragma unroll
+    for (int s2 = 0; s2 < kLinC / 2; ++s2) {
+      const int s = half * (kLinC / 2) + s2, i = ci * kLinC + s;
+      if (i >= Tb) break;
+      const uint32_t so = (uint32_t)(BETA ? Tb - 1 - i : i) * rowb;
+#pragma unroll
+      for (int j = 0; j < PPL; ++j) {
+        const d2v v = slot[(s * PPL + j) * 64 + lane];
+        if (!(SC_CTC_ABL & 2))
+          __builtin_amdgcn_raw_buffer_store_b64(
+              __builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, f2v{log2d(v.x), log2d(v.y)}),
+              ors, vo[j], so, 0);
+      }
+    }
+  };
+  for (int ci = 0; ci < nch; ++ci) {
+    __syncthreads();   // chunk ci produced (wave 0); chunk ci - 1 consumed by both waves
+    if (!stop) stop = *fail_lds != 0;
+    if (!stop) consume(ci);
+  }
+}
+
 template <int PPL>
-__global__ void __launch_bounds__(64) ctc_lin_kernel(CtcArgs a) {
+__global__ void __launch_bounds__(192) ctc_lin_kernel(CtcArgs a) {
+  // two 16-step slots of PPL pairs x 64 lanes of (B, L) fp64
+  __shared__ d2v slots[2 * kLinC * PPL * 64];
+  __shared__ int fail_lds;
   const bool is_beta = blockIdx.x >= a.B;
   const int b = is_beta ? blockIdx.x - a.B : blockIdx.x;
   const int Tb = clampi(a.in_lens[b], 0, a.T);
   const int Ub = clampi(a.tgt_lens[b], 0, a.Umax);
+  const int w = uniform(threadIdx.x >> 6);
   if (Tb == 0) {
     if (!is_beta && threadIdx.x == 0) {
       a.nll[b] = (Ub == 0) ? 0.0f : __builtin_huge_valf();
@@ -902,13 +965,24 @@ __global__ void __launch_bounds__(64) ctc_lin_kernel(CtcArgs a) {
     }
     return;
   }
-  bool lin = uniform(a.ws.flag[b]) == 0;
-  if (lin) lin = is_beta ? lin_run<PPL, true>(a, b, Tb, Ub) : lin_run<PPL, false>(a, b, Tb, Ub);
-  if (!lin) {
+  // (uniform over the workgroup: every wave takes the same branch, so the barriers match)
+  const bool tiny = a.ws.flag[b] != 0;
+  bool lin = !tiny;
+  if (lin) {
+    if (w == 0) {
+      lin = is_beta ? lin_produce<PPL, true>(a, b, Tb, Ub, slots, &fail_lds)
+                    : lin_produce<PPL, false>(a, b, Tb, Ub, slots, &fail_lds);
+    } else {
+      if (is_beta) lin_consume<PPL, true>(a, b, Tb, slots, &fail_lds);
+      else lin_consume<PPL, false>(a, b, Tb, slots, &fail_lds);
+      __builtin_amdgcn_s_waitcnt(0);   // (the stores retire before a fallback rewrites rows)
+    }
+    __syncthreads();
+  }
+  if (!lin && w == 0) {   // log space: the same rows, one wave
     if (is_beta) ab1_run<PPL, true>(a, b, Tb, Ub);
     else ab1_run<PPL, false>(a, b, Tb, Ub);
   }
-  if (threadIdx.x == 0) a.ws.flag[(is_beta ? 2 : 1) * a.B + b] = lin ? 1 : 0;
 }
 
 // pairs per lane of the one-wave lattice family (0: the multi-wave kernel).  Off unless
@@ -988,18 +1062,8 @@ __global__ void __launch_bounds__(256) ctc_grad_kernel(CtcArgs a) {
   for (int v = lane; v < a.V; v += 64) lcab[v] = kNegInf;
   wave_lds_sync();
   const float* exr = a.ex ? a.ex + (int64_t)b * a.exb + (int64_t)t * a.ext : nullptr;
-  const float* al = a.ws.alpha + ((int64_t)b * a.T + t) * a.apitch;
-  const float* be = a.ws.beta + ((int64_t)b * a.T + t) * a.apitch;
-  // base-2 log of a row's state s: fp32 log-space rows as they are, linear fp64 rows
-  // (ctc_lin_kernel) through frexp (0 -> -inf)
-  const bool linA = a.lin && a.ws.flag[a.B + b], linB = a.lin && a.ws.flag[2 * a.B + b];
-  auto lv = [&](const float* r, bool lin, int s) -> float {
-    if (!lin) return r[s];
-    const double v = ((const double*)r)[s];
-    int e;
-    const double m = frexp(v, &e);
-    return v > 0.0 ? (float)e + log2_((float)m) : kNegInf;
-  };
+  const float* al = a.ws.alpha + ((int64_t)b * a.T + t) * a.Sp;
+  const float* be = a.ws.beta + ((int64_t)b * a.T + t) * a.Sp;
   // exp(lcab + nll - lp) = 2^(lcab2 + offA + offB + c_t - ll2s - lp*log2e): the lattice holds
   // alpha_t - sum_{t'<=t} c and beta_t - sum_{t'>=t} c, so alpha + beta carries c_t once more than
   // the shifted log-likelihood ll2s; offsets folded in fp64
@@ -1018,7 +1082,7 @@ __global__ void __launch_bounds__(256) ctc_grad_kernel(CtcArgs a) {
   float m = kNegInf, l = 0.0f;   // blank-label occupancy (base 2), per lane
   for (int s = lane; s < Sb; s += 64) {
     const int lab = (s & 1) ? (int)tg[(s - 1) >> 1] : a.blank;
-    const float val = lv(al, linA, s) + lv(be, linB, s);
+    const float val = al[s] + be[s];
     if (lab == a.blank) {
       const float mn = fmaxf(m, val);
       if (mn != kNegInf) {
@@ -1030,7 +1094,7 @@ __global__ void __launch_bounds__(256) ctc_grad_kernel(CtcArgs a) {
       if (first[u]) {
         float acc = val;
         for (int q = chain[u]; q >= 0; q = chain[q])
-          acc = lse2_b2(acc, lv(al, linA, 2 * q + 1) + lv(be, linB, 2 * q + 1));
+          acc = lse2_b2(acc, al[2 * q + 1] + be[2 * q + 1]);
         if (lab >= 0 && lab < a.V) lcab[lab] = exr ? exact_grad(exr[1 + u], acc) : acc;
       }
     }
@@ -1089,10 +1153,10 @@ static void launch_fwd(const CtcArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(ctc_chain_kernel, dim3(a.B, ((a.Umax > 0 ? a.Umax : 1) + 3) / 4), dim3(256), 0,
                      st, a);
   switch (a.lin ? lin_ppl(a.Umax) : 0) {
-    case 1: hipLaunchKernelGGL((ctc_lin_kernel<1>), dim3(2 * a.B), dim3(64), 0, st, a); return;
-    case 2: hipLaunchKernelGGL((ctc_lin_kernel<2>), dim3(2 * a.B), dim3(64), 0, st, a); return;
-    case 3: hipLaunchKernelGGL((ctc_lin_kernel<3>), dim3(2 * a.B), dim3(64), 0, st, a); return;
-    case 4: hipLaunchKernelGGL((ctc_lin_kernel<4>), dim3(2 * a.B), dim3(64), 0, st, a); return;
+    case 1: hipLaunchKernelGGL((ctc_lin_kernel<1>), dim3(2 * a.B), dim3(192), 0, st, a); return;
+    case 2: hipLaunchKernelGGL((ctc_lin_kernel<2>), dim3(2 * a.B), dim3(192), 0, st, a); return;
+    case 3: hipLaunchKernelGGL((ctc_lin_kernel<3>), dim3(2 * a.B), dim3(192), 0, st, a); return;
+    case 4: hipLaunchKernelGGL((ctc_lin_kernel<4>), dim3(2 * a.B), dim3(192), 0, st, a); return;
     default: break;
   }
   const int K = a.kh;
@@ -1185,7 +1249,6 @@ static CtcArgs make_args(const void* x, int is_logits, int B, int T, int V, int6
   // steps per re-centring / 2 (the gradient's offset index): the one-wave lattices re-centre
   // every kAb1R steps, the multi-wave one at every second halo exchange
   a.lin = lin_ppl(umax) > 0;
-  a.apitch = a.lin ? 2 * a.Sp : a.Sp;
   a.kh = a.lin ? kAb1R / 2 : ab_halo_k(umax);
   a.blank = blank;
   a.sb = sb;

@@ -1018,8 +1018,13 @@ __global__ void __launch_bounds__(512, 1) mlstm_bw_walk(MArgs a) {
   if (!walk) {
     // ================= dq role: every chunk of sequence bh, independently =================
     TI* dQg = (TI*)a.dq + qrow(a, bh, 0);
+    // (in the walk's order, last chunk first: both roles of bh run on one XCD — workgroups bh
+    // and BH + bh, BH % 8 == 0 at the bench shape — and read the same q / k / v / dh / h rows,
+    // so the second reader of a chunk finds them in that XCD's L2.  In forward order the two
+    // met only in the middle and every row came from HBM twice.)
 #pragma unroll 1
-    for (int k = 0; k < a.nc; ++k) {
+    for (int kr = 0; kr < a.nc; ++kr) {
+      const int k = a.nc - 1 - kr;
       const int64_t t0 = (int64_t)k * kL;
       asm volatile("" : "+v"(tid), "+v"(lane));   // see mlstm_fw_walk
       u32x4 rc[UC] = {};

@@ -37,6 +37,9 @@ def main():
     ap.add_argument("--frames", type=int, default=256)
     ap.add_argument("--batches", default="1,16,64,256")
     ap.add_argument("--fused", type=int, default=0)
+    ap.add_argument("--engines", default="frame,library")
+    ap.add_argument("--dtypes", default="float32,bfloat16")
+    ap.add_argument("--no-reference", action="store_true")
     args = ap.parse_args()
     import statecatcher_amd as sc
     from statecatcher_amd.streaming import StreamingLucyRNN
@@ -50,9 +53,9 @@ def main():
     N = args.frames
     for B in [int(b) for b in args.batches.split(",")]:
         x = torch.randn(B, N, 80, device=dev)
-        for engine, dt, K, graph in [(e, d, k, g) for e in ("frame", "library")
-                                     for d in (torch.float32, torch.bfloat16)
-                                     for k, g in ((1, True), (8, True), (1, False))]:
+        for engine, dt, K, graph in [(e, getattr(torch, d)) + kg for e in args.engines.split(",")
+                                     for d in args.dtypes.split(",")
+                                     for kg in ((1, True), (8, True), (1, False))]:
                 st = StreamingLucyRNN(m, B, K, dtype=dt, graph=graph, engine=engine)
                 blocks = [x[:, i:i + K].contiguous() for i in range(0, N, K)]
                 it = iter(range(10 ** 9))
@@ -66,6 +69,8 @@ def main():
                                   "fused": args.fused, "frames": nb * K,
                                   "stream_frames_per_s": round(B * nb * K / dt_s, 1),
                                   "ms_per_frame": round(1e3 * dt_s / (nb * K), 4)}), flush=True)
+        if args.no_reference:
+            continue
         # reference-structured eager per-frame loop (fp32), argmax per frame
         states = ([torch.zeros(B, 512, device=dev) for _ in range(6)],
                   [torch.zeros(B, 512, device=dev) for _ in range(6)])
