@@ -294,7 +294,7 @@ int sc_lucy_step_cell(int mode, const void* g, int dtype, int64_t g_stride, cons
  *
  * sc_lucy_frame_gemm: y[b][j] = sum_k x~[b][k] w[j][k] + bias[j], x~ = x or, when ln_w is given,
  *   LayerNorm(x) from the nst_in records of st_in (lucyrnn.py:45 layernorm_in).  epi:
- *   0 plain; 1 plain + one statistics record of y per 64 columns into st_out ([N/64][B]);
+ *   0 plain; 1 plain + one statistics record of y per 32 columns into st_out ([ceil(N/32)][B]);
  *   2 unfused gates (N = 4D: z k v decay, lucyrnn.py:55-59): s' = sigmoid(decay) s + k v into s
  *     (masked), y = x~ + s' ([B][D], K == D), z ([B][D]), records of z per 16 units into st_z;
  *   3 fused gates (N = 5D: z k v h_pre decay; W_fused without its unused r rows, :47-53): s as

@@ -4,7 +4,7 @@
 //
 // A frame of B streams is, per layer (u = LN_in(a) etc. as in lucyrnn.py:45-68):
 //   lucy_frame_gemm  PRO_NONE / EPI_STATS  a = x W_in^T + b_in, plus per-row LayerNorm partial
-//                                          statistics of a (one record per 64 output columns)
+//                                          statistics of a (one record per 32 output columns)
 //   lucy_frame_gemm  PRO_LN / EPI_CELL     g = LN_in(a) W_g^T + b_g, the workgroup owning 16 units
 //                                          of EVERY gate, so the cell's elementwise part runs in
 //                                          its epilogue: s' = sigmoid(dl) s + k v (state, masked),
@@ -50,7 +50,7 @@ struct FrameGemmArgs {
   // outputs
   float* y;              // PLAIN / STATS: [B][ldy]; CELL: y (unfused) or hp (fused) [B][D]
   int64_t ldy;
-  float4* st_out;        // STATS: [N / (NT * 16)][B]; CELL: [D / 16][B] records of y/hp (fused)
+  float4* st_out;        // STATS: [ceil(N / 32)][B]; CELL: [D / 16][B] records of y/hp (fused)
   float* z;              // CELL: raw z [B][D]
   float4* st_z;          // CELL: [D / 16][B] records of z
   float* s;              // CELL: fp32 state [B][D], in place
@@ -79,6 +79,32 @@ __device__ __forceinline__ void combine_stats(const float4* rec, int nrec, int64
   rstd = 1.0f / sqrtf(m2 / n + eps);
 }
 
+// Chan's combination of two (n, mean, M2) records
+__device__ __forceinline__ float4 chan2(float4 a, float4 b) {
+  const float n = a.x + b.x;
+  if (n == 0.0f) return a;
+  const float d = b.y - a.y, f = b.x / n;
+  return make_float4(n, a.y + d * f, a.z + b.z + d * d * a.x * f, 0.0f);
+}
+// the records of lanes l, l ^ 1, ..., l ^ (W - 1) combined (xor butterflies over W lanes): every
+// lane of the group ends with the group's total
+template <int W>
+__device__ __forceinline__ float4 chan_xor(float4 r) {
+#pragma unroll
+  for (int o = 1; o < W; o <<= 1) {
+    const float4 q = make_float4(__shfl_xor(r.x, o), __shfl_xor(r.y, o), __shfl_xor(r.z, o), 0.0f);
+    r = chan2(r, q);
+  }
+  return r;
+}
+// (mean, rstd) of one row from its nrec <= 64 records (stride apart), one record per lane
+__device__ __forceinline__ float2 row_stats_wave(const float4* rec, int nrec, int64_t stride,
+                                                 float eps, int lane) {
+  float4 r = lane < nrec ? rec[(int64_t)lane * stride] : make_float4(0.f, 0.f, 0.f, 0.f);
+  r = chan_xor<64>(r);
+  return make_float2(r.y, 1.0f / sqrtf(r.z / r.x + eps));
+}
+
 // (n, mean, M2) of 16 values held by the 16 lanes of a lane group (xor butterflies within it)
 __device__ __forceinline__ float4 stats16(float v) {
   float sm = v;
@@ -95,10 +121,10 @@ __device__ __forceinline__ float4 stats16(float v) {
 //   PLAIN / STATS: tile t = columns n0 + 16 t .. (n0 = blockIdx.x * 16 NT)
 //   CELL: tile t = gate t, units d0 .. d0 + 15 (d0 = 16 blockIdx.x), W rows t * gstride + d
 template <bool BF16W, bool LN, int EPI, int NT, int KS>
-__global__ void __launch_bounds__(64 * NT * KS) lucy_frame_gemm(FrameGemmArgs a) {
+// (at most 128 VGPRs: four waves per SIMD, two 8-wave or one 16-wave workgroup per CU)
+__global__ void __launch_bounds__(64 * NT * KS, 4) lucy_frame_gemm(FrameGemmArgs a) {
   __shared__ float part[NT * KS][16][17];   // per-wave 16 x 16 partial sums (padded rows)
   __shared__ float stat[16][2];             // PRO_LN: (mean, rstd) of the workgroup's rows
-  __shared__ float4 recs[LN ? 16 : 1][16];  // PRO_LN: the rows' statistics records
   extern __shared__ __attribute__((aligned(16))) float xs[];   // the A rows [16][kpitch]
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // (wave-uniform: scalar)
@@ -118,7 +144,7 @@ __global__ void __launch_bounds__(64 * NT * KS) lucy_frame_gemm(FrameGemmArgs a)
   // first weight chunk, the A rows, the LayerNorm records and parameters, the epilogue's bias /
   // state / mask), then the MFMAs, then the epilogue.  So every one of those loads is issued
   // before the first wait.
-  constexpr int SMAXF = NT * KS > 8 ? 8 : 16;   // fp32: steps per weight chunk (10 waves: 3 per SIMD)
+  constexpr int SMAXF = 8;   // fp32: steps per weight chunk (few registers: two workgroups per CU)
   constexpr int SMAXB = 8;                      // bf16
   float4 wf[BF16W ? 1 : SMAXF];
   bf16x8 wh[BF16W ? SMAXB : 1];
@@ -172,28 +198,14 @@ __global__ void __launch_bounds__(64 * NT * KS) lucy_frame_gemm(FrameGemmArgs a)
         }
       }
       if (LN && i0 == 0) {   // the row statistics, once per workgroup, while the pieces load
-        if (a.nst_in <= 16) {   // one record per thread into LDS, then 16 threads combine them
-          if (threadIdx.x < 256) {
-            const int rr = threadIdx.x >> 4, j = threadIdx.x & 15;
-            const int r = min(r0 + rr, a.B - 1);
-            recs[rr][j] = j < a.nst_in ? a.st_in[(int64_t)j * a.B + r] : make_float4(0.f, 0.f, 0.f, 0.f);
-          }
-          __syncthreads();
-          if (threadIdx.x < 16) {   // Chan: (n, mean, M2) of the row from its records
-            const int rr = threadIdx.x;
-            float n = 0.0f, sm = 0.0f;
-            for (int j = 0; j < a.nst_in; ++j) {
-              n += recs[rr][j].x;
-              sm += recs[rr][j].x * recs[rr][j].y;
+        if (a.nst_in <= 64) {   // wave w: rows w, w + nwaves, ...; one record per lane
+          for (int rr = w; rr < 16; rr += NT * KS) {
+            const float2 st = row_stats_wave(a.st_in + min(r0 + rr, a.B - 1), a.nst_in, a.B,
+                                             a.eps, lane);
+            if (lane == 0) {
+              stat[rr][0] = st.x;
+              stat[rr][1] = st.y;
             }
-            const float mean = sm / n;
-            float m2 = 0.0f;
-            for (int j = 0; j < a.nst_in; ++j) {
-              const float d = recs[rr][j].y - mean;
-              m2 += recs[rr][j].z + recs[rr][j].x * d * d;
-            }
-            stat[rr][0] = mean;
-            stat[rr][1] = 1.0f / sqrtf(m2 / n + a.eps);
           }
         } else if (threadIdx.x < 16) {
           const int r = min(r0 + (int)threadIdx.x, a.B - 1);
@@ -292,19 +304,27 @@ __global__ void __launch_bounds__(64 * NT * KS) lucy_frame_gemm(FrameGemmArgs a)
       }
     }
     if (EPI == FR_STATS) {
-      __syncthreads();
-      if (threadIdx.x < 16) {   // one lane per row: two passes over the 16 NT values
-        const int rr = threadIdx.x;
+      // per tile (wave w < NT) and row 4 q + i: (16, mean, M2) of its 16 columns by xor
+      // butterflies within each 16-lane group, then the NT tiles' records per row combined
+      __shared__ float4 trec[NT][16];
+      if (w < NT) {
         const int ncol = min(16 * NT, a.N - (int)blockIdx.x * 16 * NT);
-        float sm = 0.0f;
-        for (int c = 0; c < ncol; ++c) sm += part[c >> 4][rr][c & 15];
-        const float mn = sm / (float)ncol;
-        float m2 = 0.0f;
-        for (int c = 0; c < ncol; ++c) {
-          const float d = part[c >> 4][rr][c & 15] - mn;
-          m2 += d * d;
+        const bool live = (lane & 15) + 16 * w < ncol;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float v = part[w][4 * q + i][lane & 15];
+          const float4 r = chan_xor<16>(live ? make_float4(1.0f, v, 0.0f, 0.0f)
+                                             : make_float4(0.f, 0.f, 0.f, 0.f));
+          if ((lane & 15) == 0) trec[w][4 * q + i] = r;
         }
-        if (r0 + rr < a.B) a.st_out[(int64_t)blockIdx.x * a.B + r0 + rr] = make_float4((float)ncol, mn, m2, 0.0f);
+      }
+      __syncthreads();
+      if (threadIdx.x < 16) {
+        const int rr = threadIdx.x;
+        float4 r = trec[0][rr];
+#pragma unroll
+        for (int t2 = 1; t2 < NT; ++t2) r = chan2(r, trec[t2][rr]);
+        if (r0 + rr < a.B) a.st_out[(int64_t)blockIdx.x * a.B + r0 + rr] = make_float4(r.x, r.y, r.z, 0.0f);
       }
     }
   } else {
@@ -360,14 +380,56 @@ struct FrameCellArgs {
 __global__ void __launch_bounds__(256) lucy_frame_cellb(FrameCellArgs a) {
   __shared__ float st[4];
   const int r = blockIdx.x;
-  if (threadIdx.x == 0) {
-    float mz = 0.0f, rz = 1.0f, mh = 0.0f, rh = 1.0f;
-    if (a.lnz_w) combine_stats(a.st_z + r, a.nst_z, a.B, a.eps, mz, rz);
-    if (a.lnh_w) combine_stats(a.st_h + r, a.nst_h, a.B, a.eps, mh, rh);
-    st[0] = mz; st[1] = rz; st[2] = mh; st[3] = rh;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  // every operand of the row is loaded before the statistics are combined (one memory latency)
+  constexpr int kPer = 4;   // D <= 1024: up to 4 units per thread in registers
+  float zv[kPer], hv[kPer], hpv[kPer];
+  const bool regs = a.D <= 256 * kPer;
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const int d = threadIdx.x + 256 * j;
+    if (regs && d < a.D) {
+      const int64_t i = (int64_t)r * a.D + d;
+      zv[j] = a.z[i];
+      hpv[j] = a.hp[i];
+      hv[j] = a.h[i];
+    }
+  }
+  // (wave 0: LN_z's records, wave 1: LN_h's; one record per lane, xor butterflies)
+  if (w == 0) {
+    float2 s2 = make_float2(0.0f, 1.0f);
+    if (a.lnz_w) {
+      if (a.nst_z <= 64) s2 = row_stats_wave(a.st_z + r, a.nst_z, a.B, a.eps, lane);
+      else combine_stats(a.st_z + r, a.nst_z, a.B, a.eps, s2.x, s2.y);
+    }
+    if (lane == 0) { st[0] = s2.x; st[1] = s2.y; }
+  } else if (w == 1) {
+    float2 s2 = make_float2(0.0f, 1.0f);
+    if (a.lnh_w) {
+      if (a.nst_h <= 64) s2 = row_stats_wave(a.st_h + r, a.nst_h, a.B, a.eps, lane);
+      else combine_stats(a.st_h + r, a.nst_h, a.B, a.eps, s2.x, s2.y);
+    }
+    if (lane == 0) { st[2] = s2.x; st[3] = s2.y; }
   }
   __syncthreads();
   const float m = a.mask ? a.mask[r] : 1.0f;
+  if (regs) {
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const int d = threadIdx.x + 256 * j;
+      if (d < a.D) {
+        float z = zv[j], hp = hpv[j];
+        if (a.lnz_w) z = (z - st[0]) * st[1] * a.lnz_w[d] + a.lnz_b[d];
+        if (a.lnh_w) hp = (hp - st[2]) * st[3] * a.lnh_w[d] + a.lnh_b[d];
+        const float zg = 1.0f / (1.0f + expf(-z));
+        const float hv2 = (1.0f - zg) * tanhf(hp) + zg * hv[j];
+        const float hn = m * hv2 + (1.0f - m) * hv[j];
+        a.h[(int64_t)r * a.D + d] = hn;
+        a.out[(int64_t)r * a.ldo + d] = hn;
+      }
+    }
+    return;
+  }
   for (int d = threadIdx.x; d < a.D; d += 256) {
     const int64_t i = (int64_t)r * a.D + d;
     float z = a.z[i], hp = a.hp[i];
@@ -399,11 +461,14 @@ static void launch_gemm(const FrameGemmArgs& a, int nblk, hipStream_t st) {
 template <bool BF16W, bool LN>
 static void dispatch_gemm(int epi, int ngate, const FrameGemmArgs& a, hipStream_t st) {
   switch (epi) {
-    case FR_PLAIN: launch_gemm<BF16W, LN, FR_PLAIN, 4, 2>(a, (a.N + 63) / 64, st); break;
-    case FR_STATS: launch_gemm<BF16W, LN, FR_STATS, 4, 2>(a, (a.N + 63) / 64, st); break;
+    // (K split over 3-4 waves: a wave's share of K = 512 is one weight chunk, one memory
+    // latency; PLAIN / STATS 32 columns per workgroup, so a 512-wide output is 16 x B/16
+    // workgroups)
+    case FR_PLAIN: launch_gemm<BF16W, LN, FR_PLAIN, 2, 4>(a, (a.N + 31) / 32, st); break;
+    case FR_STATS: launch_gemm<BF16W, LN, FR_STATS, 2, 4>(a, (a.N + 31) / 32, st); break;
     case FR_CELL_UNFUSED:
-      launch_gemm<BF16W, LN, FR_CELL_UNFUSED, 4, 2>(a, a.gstride / 16, st); break;
-    default: launch_gemm<BF16W, LN, FR_CELL_FUSED, 5, 2>(a, a.gstride / 16, st); break;
+      launch_gemm<BF16W, LN, FR_CELL_UNFUSED, 4, 4>(a, a.gstride / 16, st); break;
+    default: launch_gemm<BF16W, LN, FR_CELL_FUSED, 5, 3>(a, a.gstride / 16, st); break;
   }
   (void)ngate;
 }

@@ -101,7 +101,7 @@ class StreamingLucyRNN:
             self.x = z(K, B, self.Din, dt=f32)
             self.mask = torch.ones(K, B, dtype=f32, device=dev)
             self.fa, self.fz, self.fy, self.fhp = (z(B, D, dt=f32) for _ in range(4))
-            self.st_a = z(D // 64 if D % 64 == 0 else (D + 63) // 64, B, 4, dt=f32)
+            self.st_a = z((D + 31) // 32, B, 4, dt=f32)   # (one record per 32 columns)
             self.st_z = z(D // 16, B, 4, dt=f32)
             self.st_h = z(D // 16, B, 4, dt=f32)
             self.xo = [z(B, D, dt=f32) for _ in range(self.L)]
@@ -138,7 +138,7 @@ class StreamingLucyRNN:
         inp = self.x[j]
         for l, e in enumerate(self.layers):
             ln = e["ln_in"] is not None
-            nst_a = (D + 63) // 64
+            nst_a = (D + 31) // 32
             ops.lucy_frame_gemm(ops.FRAME_STATS if ln else ops.FRAME_PLAIN, inp, e["w_in"], e["b_in"],
                                 self.fa, st_out=self.st_a[:nst_a] if ln else None)
             lnin = dict(ln=e["ln_in"], st_in=self.st_a[:nst_a]) if ln else {}
