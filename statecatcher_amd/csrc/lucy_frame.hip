@@ -466,9 +466,11 @@ static void dispatch_gemm(int epi, int ngate, const FrameGemmArgs& a, hipStream_
     // workgroups)
     case FR_PLAIN: launch_gemm<BF16W, LN, FR_PLAIN, 2, 4>(a, (a.N + 31) / 32, st); break;
     case FR_STATS: launch_gemm<BF16W, LN, FR_STATS, 2, 4>(a, (a.N + 31) / 32, st); break;
+    // (the gate GEMMs keep 2 K-slices: at 4 the 16-wave workgroups ran one per CU and took
+    // 23.5 us against 19.3 us at B = 256, profiles/r4_stream_frame.md)
     case FR_CELL_UNFUSED:
-      launch_gemm<BF16W, LN, FR_CELL_UNFUSED, 4, 4>(a, a.gstride / 16, st); break;
-    default: launch_gemm<BF16W, LN, FR_CELL_FUSED, 5, 3>(a, a.gstride / 16, st); break;
+      launch_gemm<BF16W, LN, FR_CELL_UNFUSED, 4, 2>(a, a.gstride / 16, st); break;
+    default: launch_gemm<BF16W, LN, FR_CELL_FUSED, 5, 2>(a, a.gstride / 16, st); break;
   }
   (void)ngate;
 }
