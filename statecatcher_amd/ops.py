@@ -1332,7 +1332,12 @@ class MLSTMCoreFn(torch.autograd.Function):
     q, k, v and o are read in place from a (sc_mlstm_* layout strides, the gated norm's row
     stride): no split copies or head transposes.  The backward writes dq / dk / dv / do / di / df
     straight into ONE gradient tensor of a's shape: no concatenation of six slice gradients.
-    Same kernels and roundings as MLSTMFn + GatedHeadNormFn + the torch soft caps.
+    The forward runs the same kernels and roundings as MLSTMFn + GatedHeadNormFn + the torch
+    soft caps (bit-identical output and state).  The backward does not round the same way: the
+    gate gradients go through the soft cap in fp32 with ONE bf16 rounding (sc_mlstm_gate_bwd),
+    where the composed path and the reference's autocast chain round after each of five bf16
+    ops; the gradients agree to 1e-2 relative Frobenius (measured ~1e-3,
+    tests/test_gpu_xlstm_glue.py::test_mlstm_core_equals_composed_ops).
     cell_dtype: the cell's compute dtype -- bf16, or float16 as the reference configures it
     (autocast_kernel_dtype, model.py:227): q / k / v are then rounded to f16 on load inside the
     kernels (sc_mlstm_*_io), as the split path's .to(float16) rounds them, and h / dq / dk / dv
