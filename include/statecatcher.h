@@ -227,6 +227,17 @@ int sc_ctc_bwd_ex(const void* x, int x_dtype, int is_logits, int B, int T, int V
                   const void* workspace, size_t workspace_bytes, void* stream);
 
 /*
+ * The operand of the emission-logit GEMM of that head: out bf16 [B][max_target_len + 1][3 K],
+ * row (b, c) = [bf16(w_r) | bf16(w_r - bf16(w_r)) | bf16(w_r)] with r = blank (c = 0) or
+ * targets[b][c - 1] clamped into [0, V); bias_out fp32 [B][max_target_len + 1] = bias[r] (0 if
+ * bias is NULL).  w fp32 [V][ldw], K % 4 == 0.  Against the last scan's [x_hi | x_hi | x_lo]
+ * rows one bf16 GEMM gives the emission logits to ~2^-16 relative (lucyrnn_triton.py:150).
+ */
+int sc_ctc_split_rows(const float* w, int64_t ldw, const float* bias, int V, int K,
+                      const int64_t* targets, int64_t target_stride, int max_target_len,
+                      int blank, void* out, float* bias_out, int B, void* stream);
+
+/*
  * The reduction nn.CTCLoss(reduction='mean', zero_infinity=True) applies to sc_ctc_fwd's nll
  * (train.py:142): loss[0] = mean_b(nll_b / max(U_b, 1)) with infinite nll_b counted as 0, and
  * factor[b] = d loss / d nll_b (0 for infinite nll_b), the `scale` sc_ctc_bwd takes times the

@@ -18,7 +18,7 @@ _DTYPE = {torch.float32: SC_F32, torch.bfloat16: SC_BF16, torch.float16: SC_F16}
 
 _c = ctypes
 _i32, _i64, _vp, _fp = _c.c_int, _c.c_int64, _c.c_void_p, _c.c_void_p
-ABI_VERSION = 10  # include/statecatcher.h; bumped on any signature change
+ABI_VERSION = 11  # include/statecatcher.h; bumped on any signature change
 
 _SIGS = {
     "sc_abi_version": (_i32, []),
@@ -52,6 +52,8 @@ _SIGS = {
     "sc_ctc_bwd_ex": (_i32, [_vp, _i32, _i32, _i32, _i32, _i32, _i64, _i64, _vp, _i64, _i32, _vp,
                             _vp, _i32, _fp, _i64, _i64, _fp, _fp, _vp, _i32, _vp, _c.c_size_t,
                             _vp]),
+    "sc_ctc_split_rows": (_i32, [_fp, _i64, _fp, _i32, _i32, _vp, _i64, _i32, _i32, _vp, _fp,
+                                 _i32, _vp]),
     "sc_ctc_greedy_decode": (_i32, [_vp, _i32, _i32, _i32, _i32, _i64, _i64, _vp, _i32, _vp, _vp, _vp]),
     "sc_colsum_workspace_bytes": (_c.c_size_t, [_i64, _i64]),
     "sc_colsum": (_i32, [_vp, _i32, _i64, _i64, _i64, _i64, _i64, _fp, _vp, _c.c_size_t, _vp]),

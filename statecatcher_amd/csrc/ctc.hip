@@ -1206,9 +1206,58 @@ __global__ void __launch_bounds__(256) ctc_mean_kernel(const float* nll, const i
   if (threadIdx.x == 0) *loss = part[0] / (float)B;
 }
 
+// The CTC head's emission-column operand (ops._emission_logits): row (b, c) of out is
+// [bf16(w_r) | bf16(w_r - bf16(w_r)) | bf16(w_r)] for r = blank (c = 0) or targets[b][c - 1]
+// (clamped into [0, V)), and bout[b][c] = bias[r] — one launch instead of the split image's
+// casts, a concatenation and two gathers.  One wave per row, 16-byte loads, 8-byte stores.
+__global__ void __launch_bounds__(256) ctc_split_rows_kernel(const float* w, int64_t ldw,
+                                                             const float* bias, int V, int K,
+                                                             const int64_t* tg, int64_t tgs, int U1,
+                                                             int blank, __bf16* out, float* bout,
+                                                             int B) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= (int64_t)B * U1) return;
+  const int b = (int)(row / U1), c = (int)(row % U1);
+  int r = c == 0 ? blank : (int)tg[(int64_t)b * tgs + c - 1];
+  r = r < 0 ? 0 : (r >= V ? V - 1 : r);
+  const float* wr = w + (int64_t)r * ldw;
+  __bf16* o = out + row * 3 * (int64_t)K;
+  typedef __bf16 bf4 __attribute__((ext_vector_type(4)));
+  for (int k = 4 * lane; k < K; k += 256) {
+    const float4 v = *(const float4*)(wr + k);
+    const bf4 hi = {(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
+    const bf4 lo = {(__bf16)(v.x - (float)hi[0]), (__bf16)(v.y - (float)hi[1]),
+                    (__bf16)(v.z - (float)hi[2]), (__bf16)(v.w - (float)hi[3])};
+    *(bf4*)(o + k) = hi;
+    *(bf4*)(o + K + k) = lo;
+    *(bf4*)(o + 2 * K + k) = hi;
+  }
+  if (lane == 0) bout[row] = bias ? bias[r] : 0.0f;
+}
+
 }  // namespace sc
 
 using namespace sc;
+
+extern "C" int sc_ctc_split_rows(const float* w, int64_t ldw, const float* bias, int V, int K,
+                                 const int64_t* targets, int64_t target_stride, int max_target_len,
+                                 int blank, void* out, float* bias_out, int B, void* stream) {
+  clear_error();
+  SC_REQUIRE(B >= 0 && V > 0 && K > 0 && max_target_len >= 0, "sc_ctc_split_rows: bad shape");
+  if (B == 0) return 0;
+  SC_REQUIRE(w && out && bias_out && (max_target_len == 0 || targets),
+             "sc_ctc_split_rows: null pointer");
+  SC_REQUIRE(K % 4 == 0 && ldw % 4 == 0 && (uintptr_t)w % 16 == 0 && (uintptr_t)out % 8 == 0,
+             "sc_ctc_split_rows: rows must be 16-byte aligned (K %% 4, ldw %% 4)");
+  SC_REQUIRE(blank >= 0 && blank < V, "sc_ctc_split_rows: blank outside [0, V)");
+  const int U1 = max_target_len + 1;
+  const int64_t rows = (int64_t)B * U1;
+  hipLaunchKernelGGL(ctc_split_rows_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0,
+                     (hipStream_t)stream, w, ldw, bias, V, K, targets, target_stride, U1, blank,
+                     (__bf16*)out, bias_out, B);
+  return launch_status("sc_ctc_split_rows");
+}
 
 extern "C" size_t sc_ctc_workspace_bytes(int B, int T, int max_target_len) {
   if (B <= 0 || T <= 0 || max_target_len < 0) return 256;

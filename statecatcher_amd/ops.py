@@ -754,22 +754,38 @@ HEAD_SPLIT = os.environ.get("SC_HEAD_SPLIT", "emis")
 
 def _emission_logits(wide, w, b, targets, blank, V):
     """fp32 [B, T, U + 1]: x.W + b at the blank and at each sequence's label columns, to fp32
-    accuracy from the scan's [x_hi | x_hi | x_lo] planes (one batched bf16 GEMM against the
-    gathered [W_hi | W_lo | W_hi] rows, K = 3D, fp32 out), and the gathered columns' index."""
+    accuracy from the scan's [x_hi | x_hi | x_lo] planes: one batched bf16 GEMM against the
+    [W_hi | W_lo | W_hi] rows of those columns (K = 3D, fp32 out), gathered and split in one
+    launch (sc_ctc_split_rows)."""
     B, T, K3 = wide.shape
-    lab = torch.cat([torch.full((B, 1), blank, dtype=torch.int64, device=wide.device),
-                     targets.clamp(0, V - 1)], 1)                           # [B, U + 1]
-    wg = split_weight_image(w)[lab]                                        # [B, U + 1, 3D]
+    K = K3 // 3
+    U1 = targets.shape[1] + 1
+    wg = torch.empty(B, U1, K3, dtype=torch.bfloat16, device=wide.device)   # [B, U + 1, 3D]
+    bg = torch.empty(B, U1, dtype=torch.float32, device=wide.device)
+    tgc = targets.to(torch.int64).contiguous()
+    wc_ = w.detach().contiguous()
+    rc = _lib.load().sc_ctc_split_rows(ptr(wc_), wc_.stride(0), ptr(b.detach().contiguous()), V, K,
+                                       ptr(tgc), tgc.stride(0) if U1 > 1 else 0, U1 - 1, blank,
+                                       ptr(wg), ptr(bg), B, stream_of(wide))
+    check(rc, "sc_ctc_split_rows")
     ex = torch.bmm(wide, wg.transpose(1, 2), out_dtype=torch.float32)
-    ex += b[lab].unsqueeze(1)
-    return ex, lab
+    ex += bg.unsqueeze(1)
+    return ex
+
+
+def _emission_columns(targets, blank, V):
+    """[B, U + 1] column index of _emission_logits' entries (blank, then each label)."""
+    B = targets.shape[0]
+    return torch.cat([torch.full((B, 1), blank, dtype=torch.int64, device=targets.device),
+                      targets.clamp(0, V - 1)], 1)
 
 
 def _exact_emission_columns(logits, wide, w, b, targets, blank):
     """logits [B,T,V] fp32 in place: the emission columns set to _emission_logits' values
     (duplicates write equal values)."""
     B, T, V = logits.shape
-    ex, lab = _emission_logits(wide, w, b, targets, blank, V)
+    ex = _emission_logits(wide, w, b, targets, blank, V)
+    lab = _emission_columns(targets, blank, V)
     logits.scatter_(2, lab.unsqueeze(1).expand(B, T, lab.shape[1]), ex)
 
 
@@ -814,7 +830,7 @@ class CTCHeadFn(torch.autograd.Function):
             logits = _logits_fp32(wide.view(-1, 3 * K), split_weight_image(w), b).view(B, T, V)
         elif wide is not None and HEAD_SPLIT == "emis":
             logits = torch.addmm(b.to(torch.bfloat16), x2, wc.t()).view(B, T, V)
-            ex, _ = _emission_logits(wide.view(B, T, 3 * K), w, b, targets, blank, V)
+            ex = _emission_logits(wide.view(B, T, 3 * K), w, b, targets, blank, V)
         else:
             logits = _logits_fp32(x2, wc, b).view(B, T, V)
             if wide is not None:

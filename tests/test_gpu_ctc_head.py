@@ -193,7 +193,12 @@ def test_ctc_head_emission_side_input_matches_scattered_columns(monkeypatch):
     loss.backward()
     # reference: the bf16 logits as fp32 with the emission columns replaced by the side array's
     # values, through the plain fp32 lattice; gradients pushed through the same bf16 operands
-    ex, lab = ops._emission_logits(wide, w, b, tgd, 0, V)
+    ex = ops._emission_logits(wide, w, b, tgd, 0, V)
+    lab = ops._emission_columns(tgd, 0, V)
+    # (the one-launch split rows against the cached split image: the same operand)
+    lab_w = ops.split_weight_image(w)[lab]
+    ex_ref = torch.bmm(wide, lab_w.transpose(1, 2), out_dtype=torch.float32) + b[lab].unsqueeze(1)
+    assert torch.equal(ex, ex_ref)
     ref_logits = logits.detach().float().clone()
     ref_logits.scatter_(2, lab.unsqueeze(1).expand(B, T, lab.shape[1]), ex)
     ref_logits.requires_grad_(True)
