@@ -155,6 +155,33 @@ __global__ void __launch_bounds__(256) ctc_emit_kernel(CtcArgs a) {
   const int b = (int)(row / a.T), t = (int)(row % a.T);
   if (t >= clampi(a.in_lens[b], 0, a.T)) return;     // rows past in_len are never read
   const T* p = (const T*)a.x + (int64_t)b * a.sb + (int64_t)t * a.stt;
+  const int Sb = 2 * clampi(a.tgt_lens[b], 0, a.Umax) + 1;
+  const int64_t* tg = a.tg + (int64_t)b * a.tgs;
+  const float* exr = a.ex ? a.ex + (int64_t)b * a.exb + (int64_t)t * a.ext : nullptr;
+  // the row's state logits, gathered ONCE and before the row reduction (their loads overlap
+  // it): up to kGx per lane in registers (Sp <= 512, U <= 255), else gathered again below
+  constexpr int kGx = 8;
+  auto state_logit = [&](int s) {
+    // (ex column: 0 for the blank states, 1 + u for label state 2u + 1)
+    return exr ? exr[(s & 1) ? (s + 1) >> 1 : 0] : E::ld(p[state_label(tg, s, a.blank, a.V)]);
+  };
+  const bool inreg = a.Sp <= 64 * kGx;
+  float xs[kGx];
+  if (inreg) {   // (clamped states: every load unconditional, all in flight together)
+    if (exr) {
+#pragma unroll
+      for (int j = 0; j < kGx; ++j) {
+        const int s = min(lane + 64 * j, Sb - 1);
+        xs[j] = exr[(s & 1) ? (s + 1) >> 1 : 0];
+      }
+    } else {
+      int lab[kGx];
+#pragma unroll
+      for (int j = 0; j < kGx; ++j) lab[j] = state_label(tg, min(lane + 64 * j, Sb - 1), a.blank, a.V);
+#pragma unroll
+      for (int j = 0; j < kGx; ++j) xs[j] = E::ld(p[lab[j]]);
+    }
+  }
   float lse = 0.0f;
   if (a.is_logits) {
     float m = kNegInf, l = 0.0f;
@@ -188,22 +215,21 @@ __global__ void __launch_bounds__(256) ctc_emit_kernel(CtcArgs a) {
     lse = M + flog(l);
     if (lane == 0) a.ws.lse[row] = lse;
   }
-  const int Sb = 2 * clampi(a.tgt_lens[b], 0, a.Umax) + 1;
-  const int64_t* tg = a.tg + (int64_t)b * a.tgs;
   float* out = a.ws.lpe + row * a.Sp;
-  const float* exr = a.ex ? a.ex + (int64_t)b * a.exb + (int64_t)t * a.ext : nullptr;
-  auto lp2 = [&](int s) {
-    // (ex column: 0 for the blank states, 1 + u for label state 2u + 1)
-    const float xl = exr ? exr[(s & 1) ? (s + 1) >> 1 : 0] : E::ld(p[state_label(tg, s, a.blank, a.V)]);
-    return fmaxf((xl - lse) * kLog2e, -1e30f);
-  };
+  auto lp2x = [&](float xl) { return fmaxf((xl - lse) * kLog2e, -1e30f); };
+  auto lp2 = [&](int s) { return lp2x(state_logit(s)); };
   float c = -1e30f;
-  for (int s = lane; s < Sb; s += 64) c = fmaxf(c, lp2(s));
+  if (inreg) {
+#pragma unroll
+    for (int j = 0; j < kGx; ++j)
+      if (lane + 64 * j < Sb) c = fmaxf(c, lp2x(xs[j]));
+  } else {
+    for (int s = lane; s < Sb; s += 64) c = fmaxf(c, lp2(s));
+  }
   c = wave_max_dpp(c);
   if (!(c > -1e29f)) c = 0.0f;   // every state dead (or NaN): no shift, the sentinel stays
   bool tiny = false;
-  for (int s = lane; s < a.Sp; s += 64) {
-    const float e = s < Sb ? fmaxf(lp2(s) - c, -1e30f) : -1e30f;
+  auto put = [&](int s, float e) {
     out[s] = e;
     if (a.lin) {
       // linear emission for ctc_lin_kernel; a live one below 2^-kTiny sends the sequence to the
@@ -211,6 +237,15 @@ __global__ void __launch_bounds__(256) ctc_emit_kernel(CtcArgs a) {
       tiny |= e > -1e29f && e < -kTiny;
       a.ws.ylin[row * a.Sp + s] = e > -1e29f ? exp2_(e) : 0.0f;
     }
+  };
+  if (inreg) {
+#pragma unroll
+    for (int j = 0; j < kGx; ++j) {
+      const int s = lane + 64 * j;
+      if (s < a.Sp) put(s, s < Sb ? fmaxf(lp2x(xs[j]) - c, -1e30f) : -1e30f);
+    }
+  } else {
+    for (int s = lane; s < a.Sp; s += 64) put(s, s < Sb ? fmaxf(lp2(s) - c, -1e30f) : -1e30f);
   }
   if (lane == 0) a.ws.cst[row] = c;
   if (a.lin && __ballot(tiny) && lane == 0) a.ws.flag[b] = 1;   // (every writer stores 1)
