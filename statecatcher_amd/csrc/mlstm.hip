@@ -127,10 +127,7 @@ struct MArgs {
   int NH;
   int64_t qb, qh, qt, vb, vh, vt;
   int xcd;   // mlstm_fw_walk on a 1-D grid with the column blocks of one bh on one XCD
-  int* prog;   // mlstm_bw_walk: [BH] chunks the walk role has started (NULL: no pacing)
 };
-
-constexpr int kLead = 2;   // chunks the backward's dq role may run ahead of its walk role
 
 __device__ __forceinline__ int64_t qrow(const MArgs& a, int bh, int64_t t) {
   return (int64_t)(bh / a.NH) * a.qb + (int64_t)(bh % a.NH) * a.qh + t * a.qt;
@@ -1029,14 +1026,6 @@ __global__ void __launch_bounds__(512, 1) mlstm_bw_walk(MArgs a) {
     for (int kr = 0; kr < a.nc; ++kr) {
       const int k = a.nc - 1 - kr;
       const int64_t t0 = (int64_t)k * kL;
-      // pacing: at most kLead chunks ahead of the walk role, so the rows both roles read are
-      // still in the XCD's L2 when the walk reads them (the walk never waits for this role,
-      // and its workgroups are dispatched first: no deadlock)
-      if (a.prog && tid == 0) {
-        while (__hip_atomic_load(a.prog + bh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
-               kr + 1 - kLead)
-          __builtin_amdgcn_s_sleep(2);
-      }
       asm volatile("" : "+v"(tid), "+v"(lane));   // see mlstm_fw_walk
       u32x4 rc[UC] = {};
       const T* Ck = (const T*)a.Cs + ((int64_t)bh * a.nc + k) * DQ * DV;
@@ -1145,8 +1134,6 @@ __global__ void __launch_bounds__(512, 1) mlstm_bw_walk(MArgs a) {
   for (int k = a.nc - 1; k >= 0; --k) {
     const int64_t t0 = (int64_t)k * kL;
     asm volatile("" : "+v"(tid), "+v"(lane));   // see mlstm_fw_walk
-    if (a.prog && tid == 0)   // chunks started, for the dq role's pacing
-      __hip_atomic_store(a.prog + bh, a.nc - k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // dn~_{k+1}: the previous chunk's four partial sums (after its closing barrier)
     if (k < a.nc - 1 && tid < DQ)
       dn = decay * dn + dnp[tid] + dnp[DQ + tid] + dnp[2 * DQ + tid] + dnp[3 * DQ + tid];
@@ -1343,29 +1330,8 @@ void launch_fwd(const MArgs& a0, hipStream_t st) {
   if (a.nc > 0)
     hipLaunchKernelGGL((mlstm_fw_out<DT, IO, DQ, DV>), dim3(a.BH * a.nc), dim3(256), 0, st, a);
 }
-// The pacing counters of mlstm_bw_walk: one small device buffer per device, grown on demand,
-// zeroed on the stream before each launch.  SC_MLSTM_PACE=0 (environment, read per launch)
-// launches without pacing (A/B).
-int* pace_buffer(int BH, hipStream_t st) {
-  const char* e = getenv("SC_MLSTM_PACE");
-  if (e && e[0] == '0') return nullptr;
-  static int* buf[16] = {};
-  static int cap[16] = {};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return nullptr;
-  if (cap[dev] < BH) {
-    int* p = nullptr;
-    if (hipMalloc(&p, (size_t)BH * sizeof(int)) != hipSuccess) return nullptr;
-    buf[dev] = p;   // (a smaller earlier buffer is kept: a launch in flight may still use it)
-    cap[dev] = BH;
-  }
-  if (hipMemsetAsync(buf[dev], 0, (size_t)BH * sizeof(int), st) != hipSuccess) return nullptr;
-  return buf[dev];
-}
 template <int DT, int IO, int DQ, int DV>
-void launch_bwd(const MArgs& a0, hipStream_t st) {
-  MArgs a = a0;
-  a.prog = pace_buffer(a.BH, st);
+void launch_bwd(const MArgs& a, hipStream_t st) {
   // workgroups 0 .. BH-1 walk, BH .. 2BH-1 take the dq terms
   hipLaunchKernelGGL((mlstm_bw_walk<DT, IO, DQ, DV>), dim3(2 * a.BH), dim3(512), 0, st, a);
 }
