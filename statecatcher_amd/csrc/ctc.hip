@@ -1115,29 +1115,9 @@ __global__ void __launch_bounds__(256) ctc_grad_kernel(CtcArgs a) {
     return (exp2_(lp2) - exp2_(occ2 + koff - lp2)) * sc;
   };
   float m = kNegInf, l = 0.0f;   // blank-label occupancy (base 2), per lane
-  // the lane's states' alpha + beta, labels, first-occurrence flags and emission logits: up
-  // to kGx per lane loaded together (clamped states, no load under a branch), else per state
-  constexpr int kGx = 8;
-  const bool inreg = a.Sp <= 64 * kGx;
-  float gv_[kGx], ge_[kGx];
-  int gl_[kGx], gf_[kGx], gc_[kGx];
-  if (inreg) {
-#pragma unroll
-    for (int j = 0; j < kGx; ++j) {
-      const int s = min(lane + 64 * j, Sb - 1);
-      const int u = (s - 1) >> 1;
-      gv_[j] = al[s] + be[s];
-      gl_[j] = (s & 1) ? (int)tg[u] : a.blank;
-      gf_[j] = (s & 1) ? first[u] : 0;
-      gc_[j] = (s & 1) ? chain[u] : -1;
-      ge_[j] = (exr && (s & 1)) ? exr[1 + u] : 0.0f;
-    }
-  }
-  for (int j = 0; j < (inreg ? kGx : (Sb + 63) / 64); ++j) {
-    const int s = lane + 64 * j;
-    if (s >= Sb) break;
-    const int lab = inreg ? gl_[j] : ((s & 1) ? (int)tg[(s - 1) >> 1] : a.blank);
-    const float val = inreg ? gv_[j] : al[s] + be[s];
+  for (int s = lane; s < Sb; s += 64) {
+    const int lab = (s & 1) ? (int)tg[(s - 1) >> 1] : a.blank;
+    const float val = al[s] + be[s];
     if (lab == a.blank) {
       const float mn = fmaxf(m, val);
       if (mn != kNegInf) {
@@ -1146,12 +1126,11 @@ __global__ void __launch_bounds__(256) ctc_grad_kernel(CtcArgs a) {
       }
     } else {
       const int u = (s - 1) >> 1;
-      if (inreg ? gf_[j] : first[u]) {
+      if (first[u]) {
         float acc = val;
-        for (int q = inreg ? gc_[j] : chain[u]; q >= 0; q = chain[q])
+        for (int q = chain[u]; q >= 0; q = chain[q])
           acc = lse2_b2(acc, al[2 * q + 1] + be[2 * q + 1]);
-        if (lab >= 0 && lab < a.V)
-          lcab[lab] = exr ? exact_grad(inreg ? ge_[j] : exr[1 + u], acc) : acc;
+        if (lab >= 0 && lab < a.V) lcab[lab] = exr ? exact_grad(exr[1 + u], acc) : acc;
       }
     }
   }
