@@ -81,3 +81,31 @@ def test_round4_entry_points_reject_bad_arguments_without_gpu(lib):
     rc = lib.sc_lucy_frame_cellb(null, null, 0, null, null, 0, null, null, null, null,
                                  ctypes.c_float(1e-5), null, null, 4, null, 1, 16, null)
     assert rc == -1 and b"null" in lib.sc_last_error()
+
+
+def test_ctc_side_array_entry_points_reject_bad_arguments_without_gpu(lib):
+    """sc_ctc_fwd_ex / sc_ctc_bwd_ex / sc_ctc_split_rows (ABI v10-11) validate before launching:
+    emission logits need is_logits and rows of max_target_len + 1; split rows need aligned rows
+    and a blank inside V; empty batches are no-ops."""
+    null = ctypes.c_void_p()
+    fake = ctypes.c_void_p(0x1000)   # never dereferenced: validation fails first
+    ws = lib.sc_ctc_workspace_bytes(2, 10, 3)
+    # is_logits = 0 with emission logits
+    rc = lib.sc_ctc_fwd_ex(fake, 0, 0, 2, 10, 8, 80, 8, fake, 3, 3, fake, fake, 0, fake, 40, 4,
+                           fake, fake, ws, null)
+    assert rc == -1 and b"is_logits" in lib.sc_last_error()
+    # rows shorter than max_target_len + 1
+    rc = lib.sc_ctc_fwd_ex(fake, 0, 1, 2, 10, 8, 80, 8, fake, 3, 3, fake, fake, 0, fake, 40, 3,
+                           fake, fake, ws, null)
+    assert rc == -1 and b"max_target_len + 1" in lib.sc_last_error()
+    rc = lib.sc_ctc_bwd_ex(fake, 0, 1, 2, 10, 8, 80, 8, fake, 3, 3, fake, fake, 0, fake, 40, 3,
+                           fake, fake, fake, 0, fake, ws, null)
+    assert rc == -1 and b"max_target_len + 1" in lib.sc_last_error()
+    # split rows: K % 4, blank range, null pointers; B = 0 is a no-op
+    rc = lib.sc_ctc_split_rows(fake, 6, null, 8, 6, fake, 3, 3, 0, fake, fake, 2, null)
+    assert rc == -1 and b"16-byte" in lib.sc_last_error()
+    rc = lib.sc_ctc_split_rows(fake, 8, null, 8, 8, fake, 3, 3, 8, fake, fake, 2, null)
+    assert rc == -1 and b"blank" in lib.sc_last_error()
+    rc = lib.sc_ctc_split_rows(null, 8, null, 8, 8, fake, 3, 3, 0, fake, fake, 2, null)
+    assert rc == -1 and b"null" in lib.sc_last_error()
+    assert lib.sc_ctc_split_rows(null, 8, null, 8, 8, null, 3, 3, 0, null, null, 0, null) == 0
