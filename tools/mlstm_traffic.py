@@ -60,12 +60,10 @@ def main():
     print("| kernel | FETCH_SIZE raw | factor | reads (calibrated) | reads (algorithmic) | "
           "WRITE_SIZE raw | factor | writes | writes (algorithmic) | total / algorithmic |")
     print("|---|---:|---:|---:|---:|---:|---:|---:|---:|---:|")
-    tots = collections.Counter()
     for k in ("mlstm_fw_walk", "mlstm_fw_out", "mlstm_bw_walk"):
         fr, fa = blend(READS[k], CAL)
         wr, wa = blend(WRITES[k], WCAL)
         rd, wt = fetch.get(k, 0.0) * fr, write.get(k, 0.0) * wr
-        tots["fwd" if "fw" in k else "bwd"] += 0
         print(f"| {k} | {fetch.get(k, 0) / 1e6:.1f} MB | x{fr:.3f} | {rd / 1e6:.1f} MB | {fa / 1e6:.1f} MB "
               f"| {write.get(k, 0) / 1e6:.1f} MB | x{wr:.3f} | {wt / 1e6:.1f} MB | {wa / 1e6:.1f} MB "
               f"| {(rd + wt) / (fa + wa):.2f} |")
