@@ -33,17 +33,42 @@ __device__ __forceinline__ bool beats(float va, int ia, float vb, int ib) {
   return ia < ib;
 }
 
-// argmax of one row by one wave (first maximal index, NaN maximal); the result in every lane
+// argmax of one row by one wave (first maximal index, NaN maximal); the result in every lane.
+// Aligned rows go by 16-byte pieces, kGu pieces per lane in flight at once (a row of V = 1024 is
+// one memory round trip, not one per 64 elements); `beats` orders ties by index, so the order in
+// which a lane visits its elements does not change the result.
 template <int DT>
 __device__ __forceinline__ int wave_argmax(const typename Elem<DT>::T* p, int V, int lane) {
   using E = Elem<DT>;
   float bv = -__builtin_huge_valf();
   int bi = 0x7fffffff;
-  for (int v = lane; v < V; v += 64) {
-    const float xv = E::ld(p[v]);
-    if (bi == 0x7fffffff || beats(xv, v, bv, bi)) {
-      bv = xv;
-      bi = v;
+  constexpr int N = Vec16<DT>::N, kGu = 4;
+  if (V % N == 0 && ((uintptr_t)p & 15) == 0) {
+    const int nc = V / N;
+    for (int c0 = lane; c0 < nc; c0 += 64 * kGu) {
+      float xv[kGu][N];
+#pragma unroll
+      for (int u = 0; u < kGu; ++u) Vec16<DT>::ld(p + N * min(c0 + 64 * u, nc - 1), xv[u]);
+#pragma unroll
+      for (int u = 0; u < kGu; ++u) {
+        if (c0 + 64 * u >= nc) break;
+#pragma unroll
+        for (int k = 0; k < N; ++k) {
+          const int v = N * (c0 + 64 * u) + k;
+          if (bi == 0x7fffffff || beats(xv[u][k], v, bv, bi)) {
+            bv = xv[u][k];
+            bi = v;
+          }
+        }
+      }
+    }
+  } else {
+    for (int v = lane; v < V; v += 64) {
+      const float xv = E::ld(p[v]);
+      if (bi == 0x7fffffff || beats(xv, v, bv, bi)) {
+        bv = xv;
+        bi = v;
+      }
     }
   }
 #pragma unroll

@@ -193,6 +193,46 @@ def test_streaming_reset_subset_and_blocks_equal_one_pass():
     assert torch.equal(e_tail[1], e_fresh[1])
 
 
+@pytest.mark.parametrize("fused", [True, False])
+def test_frame_engine_odd_blocks_reset_and_state_equal_frame_by_frame(fused):
+    """The frame engine's h pairs flip every frame: 3 frames per call (two captured graphs, one
+    per starting buffer) equal 1-frame eager calls bitwise, through a reset with given state at
+    an odd frame count and a ragged mask; state() reads the live buffer."""
+    import statecatcher_amd as sc
+    from statecatcher_amd.streaming import StreamingLucyRNN
+    torch.manual_seed(11 + fused)
+    m = sc.LucyRNN(sc.LucyRNNConfig(input_dim=24, hidden_dim=64, num_layers=3, vocab_size=40,
+                                    is_training=False, fused_ops=fused))
+    with torch.no_grad():
+        m.output_proj.weight.normal_(0.0, 0.4)
+    m = m.to(DEV)
+    B, T = 4, 15
+    x = torch.randn(B, T, 24, device=DEV)
+    mask = (torch.rand(B, T, device=DEV) > 0.2).float()
+    h0 = [torch.randn(B, 64, device=DEV) * 0.3 for _ in range(3)]
+    s0 = [torch.randn(B, 64, device=DEV) * 0.3 for _ in range(3)]
+    ref = StreamingLucyRNN(m, B, 1, graph=False)
+    blk = StreamingLucyRNN(m, B, 3, graph=True)
+    assert ref.engine == blk.engine == "frame" and len(blk.graph) == 2
+    e_ref, l_ref = [], []
+    for t in range(T):
+        if t == 3:
+            ref.reset(hidden_states=(h0, s0))
+        e_ref.append(ref.step(x[:, t:t + 1], mask[:, t:t + 1]).clone())
+        l_ref.append(ref.logits[0].clone())
+    e_blk, l_blk = [], []
+    for c in range(T // 3):
+        if c == 1:
+            blk.reset(hidden_states=(h0, s0))
+        e_blk.append(blk.step(x[:, 3 * c:3 * c + 3], mask[:, 3 * c:3 * c + 3]).clone())
+        l_blk.append(blk.logits.clone())
+    assert torch.equal(torch.cat(e_ref, 1), torch.cat(e_blk, 1))
+    assert torch.equal(torch.stack(l_ref), torch.cat(l_blk))
+    (hr, sr), (hb, sb) = ref.state(), blk.state()
+    for a, b in zip(hr + sr, hb + sb):
+        assert torch.equal(a, b)
+
+
 def test_greedy_step_kernel_ties_nan_masks_vs_oracle():
     """sc_ctc_greedy_step frame by frame == decoder.py over the sequence (ties -> lowest index,
     NaN wins, masked frames past the length emit nothing), bf16 and fp32 logits."""
