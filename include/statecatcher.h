@@ -313,12 +313,6 @@ int sc_lucy_step_cell(int mode, const void* g, int dtype, int64_t g_stride, cons
  *   x 16-byte aligned with ldx % 4 == 0, K % 4 == 0; w 16-byte aligned with ldw % 8 == 0.
  * sc_lucy_frame_cellb: h = (1 - sigmoid(LN_z z)) tanh(LN_h hp) + sigmoid(LN_z z) h (masked,
  *   :61-68) in place, and out[b][:D] = h (the next layer's input).
- * sc_lucy_frame_gemm_cellb (ABI 12): sc_lucy_frame_cellb folded into the next GEMM — the next
- *   layer's input projection or the output projection, epi 0 or 1 as sc_lucy_frame_gemm — whose
- *   A rows are h' = (1 - sigmoid(LN_z z)) tanh(LN_h hp) + sigmoid(LN_z z) h (masked), formed
- *   while the rows are staged, with the same arithmetic as sc_lucy_frame_cellb.  z, hp, h, h_out
- *   [B][K] contiguous, 16-byte aligned; h' is written to h_out, which must not alias h (the
- *   workgroups of every column block read h); K % 4 == 0 (bf16 weights: % 8), K <= 1536.
  */
 int sc_lucy_frame_gemm(int epi, const float* x, int64_t ldx, int K, const float* ln_w,
                        const float* ln_b, const void* st_in, int nst_in, float eps, const void* w,
@@ -329,12 +323,6 @@ int sc_lucy_frame_cellb(const float* z, const void* st_z, int nst_z, const float
                         const void* st_h, int nst_h, const float* lnz_w, const float* lnz_b,
                         const float* lnh_w, const float* lnh_b, float eps, float* h, float* out,
                         int64_t ldo, const float* mask, int B, int D, void* stream);
-int sc_lucy_frame_gemm_cellb(int epi, const float* z, const void* st_z, int nst_z, const float* hp,
-                             const void* st_h, int nst_h, const float* lnz_w, const float* lnz_b,
-                             const float* lnh_w, const float* lnh_b, float eps, const float* h,
-                             float* h_out, const float* mask, int K, const void* w, int w_dtype,
-                             int64_t ldw, const float* bias, int B, int N, float* y, int64_t ldy,
-                             void* st_out, void* stream);
 
 /* ---------------------------------------------------------------- column sums ----------- */
 

@@ -18,7 +18,7 @@ _DTYPE = {torch.float32: SC_F32, torch.bfloat16: SC_BF16, torch.float16: SC_F16}
 
 _c = ctypes
 _i32, _i64, _vp, _fp = _c.c_int, _c.c_int64, _c.c_void_p, _c.c_void_p
-ABI_VERSION = 12  # include/statecatcher.h; bumped on any signature change
+ABI_VERSION = 11  # include/statecatcher.h; bumped on any signature change
 
 _SIGS = {
     "sc_abi_version": (_i32, []),
@@ -70,9 +70,6 @@ _SIGS = {
                                   _i64, _fp, _i32, _i32, _fp, _i64, _vp, _fp, _vp, _fp, _fp, _vp]),
     "sc_lucy_frame_cellb": (_i32, [_fp, _vp, _i32, _fp, _vp, _i32, _fp, _fp, _fp, _fp, _c.c_float,
                                    _fp, _fp, _i64, _fp, _i32, _i32, _vp]),
-    "sc_lucy_frame_gemm_cellb": (_i32, [_i32, _fp, _vp, _i32, _fp, _vp, _i32, _fp, _fp, _fp, _fp,
-                                        _c.c_float, _fp, _fp, _fp, _i32, _vp, _i32, _i64, _fp, _i32,
-                                        _i32, _fp, _i64, _vp, _vp]),
     "sc_mlstm_supported": (_i32, [_i32, _i32, _i32]),
     "sc_mlstm_chunk_state_numel": (_i64, [_i32, _i32, _i32, _i32]),
     "sc_mlstm_fwd": (_i32, [_vp, _vp, _vp, _i32, _fp, _fp, _fp, _fp, _fp, _i32, _i32, _i32, _i32,

@@ -14,10 +14,7 @@
 //   lucy_frame_cellb                       h = (1 - sigmoid(LN_z z)) tanh(LN_h hp)
 //                                              + sigmoid(LN_z z) h_prev, masked; the next input
 // and after the last layer the output projection (lucy_frame_gemm PRO_NONE / EPI_PLAIN) and the
-// greedy step (sc_ctc_greedy_step, decode.hip).  PRO_CELLB folds lucy_frame_cellb into the NEXT
-// GEMM (the next layer's input projection, or the output projection): its workgroups form h from
-// z, hp and h_prev while staging their A rows, and the workgroups of column block 0 store it
-// (into the other buffer of a per-frame pair: the other column blocks still read h_prev).  The W_r rows are never computed: the reference
+// greedy step (sc_ctc_greedy_step, decode.hip).  The W_r rows are never computed: the reference
 // evaluates sigmoid(LN_r(W_r u)) and never uses it.
 //
 // LayerNorm (nn.LayerNorm: biased variance, eps inside the rsqrt) is split over the producing GEMM
@@ -58,19 +55,7 @@ struct FrameGemmArgs {
   float4* st_z;          // CELL: [D / 16][B] records of z
   float* s;              // CELL: fp32 state [B][D], in place
   const float* mask;     // CELL: [B] or NULL
-  // PRO_CELLB: the A rows are h = cellb(z, hp, h_prev) ([B][K] each, contiguous)
-  const float* cz;
-  const float4* cst_z;   // [cnst_z][B] records of z, or NULL (no LN_z)
-  int cnst_z;
-  const float* chp;
-  const float4* cst_h;   // [cnst_h][B] records of hp, or NULL (no LN_h)
-  int cnst_h;
-  const float *lnz_w, *lnz_b, *lnh_w, *lnh_b;
-  const float* ch;       // h_prev
-  float* ch_out;         // h (written by column block 0)
-  const float* cmask;    // [B] or NULL
 };
-enum { PRO_NONE = 0, PRO_LN = 1, PRO_CELLB = 2 };
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -135,12 +120,9 @@ __device__ __forceinline__ float4 stats16(float v) {
 // One workgroup: rows r0 .. r0 + 15, NT output tiles x KS K-slices (one wave each).
 //   PLAIN / STATS: tile t = columns n0 + 16 t .. (n0 = blockIdx.x * 16 NT)
 //   CELL: tile t = gate t, units d0 .. d0 + 15 (d0 = 16 blockIdx.x), W rows t * gstride + d
-template <bool BF16W, int PRO, int EPI, int NT, int KS>
-// (at most 128 VGPRs: four waves per SIMD, two 8-wave or one 16-wave workgroup per CU; PRO_CELLB
-// holds three operands per piece in flight and takes up to 256, one 8-wave workgroup per CU, which
-// is what its grids of <= 16 x 16 workgroups use at <= 256 streams anyway)
-__global__ void __launch_bounds__(64 * NT * KS, PRO == PRO_CELLB ? 2 : 4) lucy_frame_gemm(FrameGemmArgs a) {
-  constexpr bool LN = PRO == PRO_LN;
+template <bool BF16W, bool LN, int EPI, int NT, int KS>
+// (at most 128 VGPRs: four waves per SIMD, two 8-wave or one 16-wave workgroup per CU)
+__global__ void __launch_bounds__(64 * NT * KS, 4) lucy_frame_gemm(FrameGemmArgs a) {
   __shared__ float part[NT * KS][16][17];   // per-wave 16 x 16 partial sums (padded rows)
   __shared__ float stat[16][2];             // PRO_LN: (mean, rstd) of the workgroup's rows
   extern __shared__ __attribute__((aligned(16))) float xs[];   // the A rows [16][kpitch]
@@ -193,89 +175,6 @@ __global__ void __launch_bounds__(64 * NT * KS, PRO == PRO_CELLB ? 2 : 4) lucy_f
       if (w < NT && cok) e_bias[0] = a.bias[col];
     }
   }
-  // PRO_CELLB: the rows are h = (1 - sigmoid(LN_z z)) tanh(LN_h hp) + sigmoid(LN_z z) h_prev
-  // (masked), formed here exactly as lucy_frame_cellb does: z / hp / h_prev pieces, the four
-  // LayerNorm vectors (into LDS behind the rows) and the row records are all loaded before the
-  // first wait; column block 0 stores h.
-  if constexpr (PRO == PRO_CELLB) {
-    const int per_row = kpad / 4;
-    const int npc = 16 * per_row;
-    const int kq = a.K / 4;                               // float4 pieces per LayerNorm vector
-    float* lnp = xs + 16 * kpitch;                        // [4][K]: z w, z b, h w, h b
-    __shared__ float2 stat2[32];                          // [16][2]: (mean, rstd) of z, of hp
-    for (int i0 = 0; i0 < npc; i0 += 4 * NTH) {
-      float4 zv[4], hv[4], pv[4];
-      float mk[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int i = min(i0 + j * NTH + (int)threadIdx.x, npc - 1);
-        const int rr = i / per_row, k = min(4 * (i % per_row), a.K - 4), r = min(r0 + rr, a.B - 1);
-        const int64_t o = (int64_t)r * a.K + k;           // (clamped: every load unconditional)
-        zv[j] = *(const float4*)(a.cz + o);
-        hv[j] = *(const float4*)(a.chp + o);
-        pv[j] = *(const float4*)(a.ch + o);
-        mk[j] = a.cmask ? a.cmask[r] : 1.0f;
-      }
-      if (i0 == 0) {
-        float4 lv[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {   // piece q of the four vectors (K <= 2048, NTH >= 512)
-          const int q = min(j * NTH + (int)threadIdx.x, 4 * kq - 1), v = q / kq;
-          const float* src = v == 0 ? a.lnz_w : v == 1 ? a.lnz_b : v == 2 ? a.lnh_w : a.lnh_b;
-          src = src ? src : a.cz;                         // (absent: read and never used)
-          lv[j] = *(const float4*)(src + 4 * (q % kq));
-        }
-        for (int rr = w; rr < 32; rr += NT * KS) {        // (row, z | hp) pairs over the waves
-          const int row = rr >> 1;
-          const bool zs = (rr & 1) == 0;
-          const float4* rec = zs ? a.cst_z : a.cst_h;
-          const int nrec = zs ? a.cnst_z : a.cnst_h;
-          float2 st = make_float2(0.0f, 1.0f);
-          if (rec) {
-            const float4* rp = rec + min(r0 + row, a.B - 1);
-            if (nrec <= 64) st = row_stats_wave(rp, nrec, a.B, a.eps, lane);
-            else combine_stats(rp, nrec, a.B, a.eps, st.x, st.y);
-          }
-          if (lane == 0) stat2[2 * row + (zs ? 0 : 1)] = st;
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int q = j * NTH + (int)threadIdx.x;
-          if (q < 4 * kq) *(float4*)(lnp + (q / kq) * a.K + 4 * (q % kq)) = lv[j];
-        }
-        __syncthreads();
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int i = i0 + j * NTH + threadIdx.x;
-        const int rr = i / per_row, k = 4 * (i % per_row), r = r0 + rr;
-        if (i < npc) {
-          float4 hn = make_float4(0.f, 0.f, 0.f, 0.f);
-          if (r < a.B && k < a.K) {
-            const float2 sz = stat2[2 * rr], sh = stat2[2 * rr + 1];
-            const float m = mk[j];
-            const float zin[4] = {zv[j].x, zv[j].y, zv[j].z, zv[j].w};
-            const float hin[4] = {hv[j].x, hv[j].y, hv[j].z, hv[j].w};
-            const float pin[4] = {pv[j].x, pv[j].y, pv[j].z, pv[j].w};
-            float o[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              float z = zin[e], hp = hin[e];
-              if (a.lnz_w) z = (z - sz.x) * sz.y * lnp[k + e] + lnp[a.K + k + e];
-              if (a.lnh_w) hp = (hp - sh.x) * sh.y * lnp[2 * a.K + k + e] + lnp[3 * a.K + k + e];
-              const float zg = 1.0f / (1.0f + expf(-z));
-              const float hv2 = (1.0f - zg) * tanhf(hp) + zg * pin[e];
-              o[e] = m * hv2 + (1.0f - m) * pin[e];
-            }
-            hn = make_float4(o[0], o[1], o[2], o[3]);
-            if (blockIdx.x == 0) *(float4*)(a.ch_out + (int64_t)r * a.K + k) = hn;
-          }
-          *(float4*)(xs + rr * kpitch + k) = hn;
-        }
-      }
-    }
-    __syncthreads();
-  } else
   // The workgroup's 16 A rows (LayerNorm applied, rows past B and columns past K zero) into LDS
   // with coalesced 16-byte loads: every wave then reads its fragments from LDS, and no global
   // load of the MFMA loop depends on a row or K condition.  Up to 4 pieces per thread are loaded
@@ -545,37 +444,33 @@ __global__ void __launch_bounds__(256) lucy_frame_cellb(FrameCellArgs a) {
   }
 }
 
-template <bool BF16W, int PRO, int EPI, int NT, int KS>
+template <bool BF16W, bool LN, int EPI, int NT, int KS>
 static void launch_gemm(const FrameGemmArgs& a, int nblk, hipStream_t st) {
   const int kstep = BF16W ? 32 : 16;
-  size_t lds = (size_t)16 * (((a.K + kstep - 1) / kstep) * kstep + 4) * sizeof(float);
-  if (PRO == PRO_CELLB) lds += (size_t)4 * a.K * sizeof(float);   // the four LayerNorm vectors
-  static size_t lds_set = 48 * 1024;   // (the A rows of K > ~800 exceed the default 64 KB window)
-  if (lds > lds_set) {
-    (void)hipFuncSetAttribute((const void*)lucy_frame_gemm<BF16W, PRO, EPI, NT, KS>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    lds_set = lds;
+  const size_t lds = (size_t)16 * (((a.K + kstep - 1) / kstep) * kstep + 4) * sizeof(float);
+  static bool big_lds = false;   // (the A rows of K > ~800 exceed the default 64 KB window)
+  if (lds > 48 * 1024 && !big_lds) {
+    (void)hipFuncSetAttribute((const void*)lucy_frame_gemm<BF16W, LN, EPI, NT, KS>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 140 * 1024);
+    big_lds = true;
   }
-  hipLaunchKernelGGL((lucy_frame_gemm<BF16W, PRO, EPI, NT, KS>), dim3(nblk, (a.B + 15) / 16),
+  hipLaunchKernelGGL((lucy_frame_gemm<BF16W, LN, EPI, NT, KS>), dim3(nblk, (a.B + 15) / 16),
                      dim3(64 * NT * KS), lds, st, a);
 }
 
-template <bool BF16W, int PRO>
+template <bool BF16W, bool LN>
 static void dispatch_gemm(int epi, int ngate, const FrameGemmArgs& a, hipStream_t st) {
   switch (epi) {
     // (K split over 3-4 waves: a wave's share of K = 512 is one weight chunk, one memory
     // latency; PLAIN / STATS 32 columns per workgroup, so a 512-wide output is 16 x B/16
     // workgroups)
-    case FR_PLAIN: launch_gemm<BF16W, PRO, FR_PLAIN, 2, 4>(a, (a.N + 31) / 32, st); break;
-    case FR_STATS: launch_gemm<BF16W, PRO, FR_STATS, 2, 4>(a, (a.N + 31) / 32, st); break;
-    default:
-      if constexpr (PRO != PRO_CELLB) {
-        // (the gate GEMMs keep 2 K-slices: at 4 the 16-wave workgroups ran one per CU and took
-        // 23.5 us against 19.3 us at B = 256, profiles/r4_stream_frame.md)
-        if (epi == FR_CELL_UNFUSED) launch_gemm<BF16W, PRO, FR_CELL_UNFUSED, 4, 2>(a, a.gstride / 16, st);
-        else launch_gemm<BF16W, PRO, FR_CELL_FUSED, 5, 2>(a, a.gstride / 16, st);
-      }
-      break;
+    case FR_PLAIN: launch_gemm<BF16W, LN, FR_PLAIN, 2, 4>(a, (a.N + 31) / 32, st); break;
+    case FR_STATS: launch_gemm<BF16W, LN, FR_STATS, 2, 4>(a, (a.N + 31) / 32, st); break;
+    // (the gate GEMMs keep 2 K-slices: at 4 the 16-wave workgroups ran one per CU and took
+    // 23.5 us against 19.3 us at B = 256, profiles/r4_stream_frame.md)
+    case FR_CELL_UNFUSED:
+      launch_gemm<BF16W, LN, FR_CELL_UNFUSED, 4, 2>(a, a.gstride / 16, st); break;
+    default: launch_gemm<BF16W, LN, FR_CELL_FUSED, 5, 2>(a, a.gstride / 16, st); break;
   }
   (void)ngate;
 }
@@ -621,53 +516,13 @@ extern "C" int sc_lucy_frame_gemm(int epi, const float* x, int64_t ldx, int K, c
   a.mask = mask;
   hipStream_t st = (hipStream_t)stream;
   if (w_dtype == SC_BF16) {
-    if (ln_w) dispatch_gemm<true, PRO_LN>(epi, ng, a, st);
-    else dispatch_gemm<true, PRO_NONE>(epi, ng, a, st);
+    if (ln_w) dispatch_gemm<true, true>(epi, ng, a, st);
+    else dispatch_gemm<true, false>(epi, ng, a, st);
   } else {
-    if (ln_w) dispatch_gemm<false, PRO_LN>(epi, ng, a, st);
-    else dispatch_gemm<false, PRO_NONE>(epi, ng, a, st);
+    if (ln_w) dispatch_gemm<false, true>(epi, ng, a, st);
+    else dispatch_gemm<false, false>(epi, ng, a, st);
   }
   return launch_status("sc_lucy_frame_gemm");
-}
-
-extern "C" int sc_lucy_frame_gemm_cellb(int epi, const float* z, const void* st_z, int nst_z,
-                                        const float* hp, const void* st_h, int nst_h,
-                                        const float* lnz_w, const float* lnz_b, const float* lnh_w,
-                                        const float* lnh_b, float eps, const float* h, float* h_out,
-                                        const float* mask, int K, const void* w, int w_dtype,
-                                        int64_t ldw, const float* bias, int B, int N, float* y,
-                                        int64_t ldy, void* st_out, void* stream) {
-  clear_error();
-  SC_REQUIRE(epi == FR_PLAIN || epi == FR_STATS, "sc_lucy_frame_gemm_cellb: epilogue %d (plain or statistics)", epi);
-  SC_REQUIRE(w_dtype == SC_F32 || w_dtype == SC_BF16, "sc_lucy_frame_gemm_cellb: weights must be fp32 or bf16");
-  SC_REQUIRE(B >= 0 && N > 0 && K > 0, "sc_lucy_frame_gemm_cellb: bad shape");
-  if (B == 0) return 0;
-  SC_REQUIRE(z && hp && h && h_out && w && bias && y, "sc_lucy_frame_gemm_cellb: null pointer");
-  SC_REQUIRE(h_out != h, "sc_lucy_frame_gemm_cellb: h_out must not alias h (other workgroups read h)");
-  SC_REQUIRE(K % 4 == 0 && (w_dtype == SC_F32 || K % 8 == 0) && K <= 1536,
-             "sc_lucy_frame_gemm_cellb: K = %d (a multiple of 4, of 8 for bf16 weights; <= 1536: "
-             "the rows and the LayerNorm vectors live in LDS)", K);
-  SC_REQUIRE((uintptr_t)z % 16 == 0 && (uintptr_t)hp % 16 == 0 && (uintptr_t)h % 16 == 0 &&
-                 (uintptr_t)h_out % 16 == 0 && (uintptr_t)w % 16 == 0 && ldw % 8 == 0,
-             "sc_lucy_frame_gemm_cellb: operands must be 16-byte aligned");
-  SC_REQUIRE((lnz_w == nullptr) == (lnz_b == nullptr) && (lnh_w == nullptr) == (lnh_b == nullptr) &&
-                 (!lnz_w || (st_z && nst_z > 0)) && (!lnh_w || (st_h && nst_h > 0)),
-             "sc_lucy_frame_gemm_cellb: LayerNorm needs weight, bias and statistics");
-  SC_REQUIRE((!lnz_w || ((uintptr_t)lnz_w % 16 == 0 && (uintptr_t)lnz_b % 16 == 0)) &&
-                 (!lnh_w || ((uintptr_t)lnh_w % 16 == 0 && (uintptr_t)lnh_b % 16 == 0)),
-             "sc_lucy_frame_gemm_cellb: LayerNorm parameters must be 16-byte aligned");
-  SC_REQUIRE(epi == FR_PLAIN || st_out, "sc_lucy_frame_gemm_cellb: statistics output missing");
-  FrameGemmArgs a = {};
-  a.x = z; a.ldx = K; a.K = K; a.eps = eps; a.w = w; a.ldw = ldw; a.bias = bias; a.B = B; a.N = N;
-  a.gstride = 16; a.y = y; a.ldy = ldy; a.st_out = (float4*)st_out;
-  a.cz = z; a.cst_z = lnz_w ? (const float4*)st_z : nullptr; a.cnst_z = nst_z;
-  a.chp = hp; a.cst_h = lnh_w ? (const float4*)st_h : nullptr; a.cnst_h = nst_h;
-  a.lnz_w = lnz_w; a.lnz_b = lnz_b; a.lnh_w = lnh_w; a.lnh_b = lnh_b;
-  a.ch = h; a.ch_out = h_out; a.cmask = mask;
-  hipStream_t st = (hipStream_t)stream;
-  if (w_dtype == SC_BF16) dispatch_gemm<true, PRO_CELLB>(epi, 4, a, st);
-  else dispatch_gemm<false, PRO_CELLB>(epi, 4, a, st);
-  return launch_status("sc_lucy_frame_gemm_cellb");
 }
 
 extern "C" int sc_lucy_frame_cellb(const float* z, const void* st_z, int nst_z, const float* hp,

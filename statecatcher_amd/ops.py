@@ -1006,23 +1006,6 @@ def lucy_frame_cellb(z, hp, h, out, st_z=None, st_h=None, lnz=None, lnh=None, ma
     check(rc, "sc_lucy_frame_cellb")
 
 
-def lucy_frame_gemm_cellb(epi, z, hp, h, h_out, w, bias, y, st_out=None, st_z=None, st_h=None,
-                          lnz=None, lnh=None, mask=None, eps=1e-5):
-    """lucy_frame_cellb folded into the next frame GEMM (sc_lucy_frame_gemm_cellb): y = h' W^T +
-    bias with h' = (1 - sigmoid(LN_z z)) tanh(LN_h hp) + sigmoid(LN_z z) h (masked) formed on
-    load and written to h_out (a different buffer from h).  epi FRAME_PLAIN / FRAME_STATS."""
-    B, K = h.shape
-    N = w.shape[0]
-    zw, zb = lnz if lnz is not None else (None, None)
-    hw, hb = lnh if lnh is not None else (None, None)
-    rc = _lib.load().sc_lucy_frame_gemm_cellb(
-        int(epi), ptr(z), ptr(st_z), st_z.shape[0] if st_z is not None else 0, ptr(hp), ptr(st_h),
-        st_h.shape[0] if st_h is not None else 0, ptr(zw), ptr(zb), ptr(hw), ptr(hb), float(eps),
-        ptr(h), ptr(h_out), ptr(mask), K, ptr(w), dtype_code(w), w.stride(0), ptr(bias), B, N,
-        ptr(y), y.stride(0), ptr(st_out), stream_of(h))
-    check(rc, "sc_lucy_frame_gemm_cellb")
-
-
 # ------------------------------------------------------------------- feature frontend --------
 def fbank(audio, kind="mfcc", sample_rate=16000):
     """make_frontend(kind)(audio).transpose(-1, -2) on the GPU (fbank.hip): audio fp32

@@ -23,15 +23,10 @@ GEMMs and the LayerNorm / cell kernels by the fused chain of csrc/lucy_frame.hip
     a = x W_in^T + b_in (+ row statistics)            lucy_frame_gemm
     gates on LN_in(a), cell stage in the epilogue     lucy_frame_gemm  (s, z, y / hp, statistics)
     hp = y W_h^T + b_h (+ statistics)  [unfused]      lucy_frame_gemm
-    h = (1 - z~) tanh(LN_h hp) + z~ h                 folded into the NEXT GEMM (the next layer's
-                                                      input projection, or the output projection):
-                                                      lucy_frame_gemm_cellb forms h while staging
-                                                      its rows and stores it
-then logits and the greedy step: 2-3 launches per layer instead of 5-6, no LayerNorm launch
-(statistics ride with the producing GEMM), MFMA on fp32 (exact f32) or bf16 weights, fp32
-activations.  h is double-buffered by frame parity (the GEMM's other column blocks still read
-h_prev while block 0 stores h); with an odd number of frames per call two graphs are captured,
-one per starting parity.
+    h = (1 - z~) tanh(LN_h hp) + z~ h                 lucy_frame_cellb
+then logits (lucy_frame_gemm) and the greedy step: 3-4 launches per layer instead of 5-6, no
+LayerNorm launch (statistics ride with the producing GEMM), MFMA on fp32 (exact f32) or bf16
+weights, fp32 activations.
 
 The decode is incremental: ``prev`` holds each stream's last argmax (-1 at stream start, as
 decoder.py's ``prev_token = None``), and emit[b, t] is the token decoder.py would append at
@@ -85,13 +80,12 @@ class StreamingLucyRNN:
                 e["w_h"], e["b_h"] = w(cell.W_h.weight), w(cell.W_h.bias)
             self.layers.append(e)
         self.w_out, self.b_out = w(model.output_proj.weight), w(model.output_proj.bias)
-        frame_ok = (D % 16 == 0 and D <= 1536 and self.Din % 8 == 0
-                    and dtype in (torch.float32, torch.bfloat16))
+        frame_ok = (D % 16 == 0 and self.Din % 8 == 0 and dtype in (torch.float32, torch.bfloat16))
         if engine == "auto":
             engine = "frame" if frame_ok else "library"
         if engine == "frame" and not frame_ok:
-            raise ValueError("engine='frame' needs hidden_dim % 16 == 0 (<= 1536), input width % 8 "
-                             "== 0 and fp32 / bf16 weights")
+            raise ValueError("engine='frame' needs hidden_dim % 16 == 0, input width % 8 == 0 and "
+                             "fp32 / bf16 weights")
         self.engine = engine
         z = lambda *s, dt=dtype: torch.zeros(*s, dtype=dt, device=dev)   # noqa: E731
         if engine == "frame":
@@ -110,9 +104,8 @@ class StreamingLucyRNN:
             self.st_a = z((D + 31) // 32, B, 4, dt=f32)   # (one record per 32 columns)
             self.st_z = z(D // 16, B, 4, dt=f32)
             self.st_h = z(D // 16, B, 4, dt=f32)
-            # h of every layer in two buffers: frame t reads hbuf[l][t % 2] and writes the other
-            self.hbuf = [[z(B, D, dt=f32), z(B, D, dt=f32)] for _ in range(self.L)]
-            self.par = 0
+            self.xo = [z(B, D, dt=f32) for _ in range(self.L)]
+            self.h = [z(B, D, dt=f32) for _ in range(self.L)]
             self.s = [z(B, D, dt=f32) for _ in range(self.L)]
             self.logits = z(K, B, self.V, dt=f32)
             self.emit = torch.full((K, B), -1, dtype=torch.int32, device=dev)
@@ -122,7 +115,6 @@ class StreamingLucyRNN:
                 self._capture()
             self.reset()
             return
-        self.par = 0
         ng = 5 if cfg.fused_ops else 4
         self.x = z(K, B, self.Din)
         self.mask = torch.ones(K, B, dtype=torch.float32, device=dev)
@@ -140,20 +132,15 @@ class StreamingLucyRNN:
         self.reset()
 
     # ------------------------------------------------------------------------------ frame --
-    def _frame_fused_chain(self, j, par):
-        """One frame on csrc/lucy_frame.hip's fused kernels (engine="frame"); h_prev of every
-        layer in hbuf[l][par], the new h into hbuf[l][1 - par]."""
+    def _frame_fused_chain(self, j):
+        """One frame on csrc/lucy_frame.hip's fused kernels (engine="frame")."""
         cfg, m, D = self.cfg, self.mask[j], self.D
-        cb = None   # the previous layer's cell second half, folded into the next GEMM
+        inp = self.x[j]
         for l, e in enumerate(self.layers):
             ln = e["ln_in"] is not None
             nst_a = (D + 31) // 32
-            epi = ops.FRAME_STATS if ln else ops.FRAME_PLAIN
-            sto = self.st_a[:nst_a] if ln else None
-            if cb is None:
-                ops.lucy_frame_gemm(epi, self.x[j], e["w_in"], e["b_in"], self.fa, st_out=sto)
-            else:
-                ops.lucy_frame_gemm_cellb(epi, w=e["w_in"], bias=e["b_in"], y=self.fa, st_out=sto, **cb)
+            ops.lucy_frame_gemm(ops.FRAME_STATS if ln else ops.FRAME_PLAIN, inp, e["w_in"], e["b_in"],
+                                self.fa, st_out=self.st_a[:nst_a] if ln else None)
             lnin = dict(ln=e["ln_in"], st_in=self.st_a[:nst_a]) if ln else {}
             if cfg.fused_ops:
                 ops.lucy_frame_gemm(ops.FRAME_CELL_FUSED, self.fa, e["w_g"], e["b_g"], self.fhp,
@@ -167,14 +154,15 @@ class StreamingLucyRNN:
                 st_h = self.st_h[:nst_a]
                 ops.lucy_frame_gemm(ops.FRAME_STATS if lnh else ops.FRAME_PLAIN, self.fy, e["w_h"],
                                     e["b_h"], self.fhp, st_out=st_h if lnh else None)
-            cb = dict(z=self.fz, hp=self.fhp, h=self.hbuf[l][par], h_out=self.hbuf[l][1 - par],
-                      st_z=self.st_z, st_h=st_h, lnz=e["lnz"], lnh=e["lnh"], mask=m)
-        ops.lucy_frame_gemm_cellb(ops.FRAME_PLAIN, w=self.w_out, bias=self.b_out, y=self.logits[j], **cb)
+            ops.lucy_frame_cellb(self.fz, self.fhp, self.h[l], self.xo[l], st_z=self.st_z,
+                                 st_h=st_h, lnz=e["lnz"], lnh=e["lnh"], mask=m)
+            inp = self.xo[l]
+        ops.lucy_frame_gemm(ops.FRAME_PLAIN, inp, self.w_out, self.b_out, self.logits[j])
         ops.ctc_greedy_step(self.logits[j], self.prev, self.emit[j], mask=m, blank=self.blank)
 
-    def _frame(self, j, par):
+    def _frame(self, j):
         if self.engine == "frame":
-            return self._frame_fused_chain(j, par)
+            return self._frame_fused_chain(j)
         cfg, m = self.cfg, self.mask[j]
         inp = self.x[j]
         for l, e in enumerate(self.layers):
@@ -197,31 +185,19 @@ class StreamingLucyRNN:
         torch.addmm(self.b_out, inp, self.w_out.t(), out=self.logits[j])
         ops.ctc_greedy_step(self.logits[j], self.prev, self.emit[j], mask=m, blank=self.blank)
 
-    def _block(self, par0):
+    def _block(self):
         for j in range(self.K):
-            self._frame(j, (par0 + j) & 1)
+            self._frame(j)
 
     def _capture(self):
         side = torch.cuda.Stream(self.x.device)
         side.wait_stream(torch.cuda.current_stream(self.x.device))
         with torch.cuda.stream(side):   # warm-up: library workspaces, kernel loading
-            self._block(0)
+            self._block()
         torch.cuda.current_stream(self.x.device).wait_stream(side)
-        # one graph per starting h buffer (the frame engine's h pair flips every frame: with an
-        # odd K a call starts on either buffer)
-        pars = (0, 1) if self.engine == "frame" and self.K % 2 else (0,)
-        self.graph = []
-        for p in pars:
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                self._block(p)
-            self.graph.append(g)
-
-    def _hcur(self):
-        """The current h of every layer (the frame engine's live buffer of each pair)."""
-        if self.engine == "frame":
-            return [pair[self.par] for pair in self.hbuf]
-        return self.h
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self._block()
 
     # ------------------------------------------------------------------------------- API ---
     def reset(self, hidden_states=None, streams=None):
@@ -229,9 +205,8 @@ class StreamingLucyRNN:
         reference's forward takes) or zero, prev token = none.  ``streams``: index tensor/list
         of the streams to reset (default all)."""
         idx = slice(None) if streams is None else torch.as_tensor(streams, device=self.x.device)
-        hc = self._hcur()
         for l in range(self.L):
-            for buf, src in ((hc[l], None if hidden_states is None else hidden_states[0][l]),
+            for buf, src in ((self.h[l], None if hidden_states is None else hidden_states[0][l]),
                              (self.s[l], None if hidden_states is None else hidden_states[1][l])):
                 if src is None:
                     buf[idx] = 0.0
@@ -241,7 +216,7 @@ class StreamingLucyRNN:
 
     def state(self):
         """(h list, s list) fp32 copies — the reference's (h, s) return (lucyrnn.py:188-189)."""
-        return [t.clone() for t in self._hcur()], [t.clone() for t in self.s]
+        return [t.clone() for t in self.h], [t.clone() for t in self.s]
 
     def step(self, x, mask=None):
         """Advance every stream by K = frames_per_call model frames.  x [B, K, input_dim *
@@ -254,11 +229,9 @@ class StreamingLucyRNN:
         else:
             self.mask.copy_(mask.transpose(0, 1))
         if self.graph is not None:
-            self.graph[self.par % len(self.graph)].replay()
+            self.graph.replay()
         else:
-            self._block(self.par)
-        if self.engine == "frame":
-            self.par ^= self.K & 1
+            self._block()
         return self.emit.t()
 
     def decode(self, feats, masks=None, return_logits=False):

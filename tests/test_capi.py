@@ -36,7 +36,7 @@ def test_binding_covers_header(lib):
 
 
 def test_abi_version_and_sizes(lib):
-    assert lib.sc_abi_version() == 12
+    assert lib.sc_abi_version() == 11
     assert lib.sc_lucy_scan_chunk() == 64
     assert lib.sc_lucy_scan_ckpt_numel(32, 1500, 512) == 32 * 24 * 2 * 512
     assert lib.sc_lucy_scan_ckpt_numel(2, 64, 3) == 2 * 1 * 2 * 3
@@ -81,25 +81,6 @@ def test_round4_entry_points_reject_bad_arguments_without_gpu(lib):
     rc = lib.sc_lucy_frame_cellb(null, null, 0, null, null, 0, null, null, null, null,
                                  ctypes.c_float(1e-5), null, null, 4, null, 1, 16, null)
     assert rc == -1 and b"null" in lib.sc_last_error()
-
-
-def test_frame_gemm_cellb_rejects_bad_arguments_without_gpu(lib):
-    """sc_lucy_frame_gemm_cellb (ABI 12): plain / statistics epilogues only, h_out distinct from
-    h, K within the LDS rows, LayerNorm with its records; B = 0 is a no-op."""
-    null = ctypes.c_void_p()
-    f = [ctypes.c_void_p(0x1000 * (i + 1)) for i in range(8)]   # never dereferenced
-    eps = ctypes.c_float(1e-5)
-
-    def call(epi=0, h=f[2], h_out=f[3], K=512, lnz=(null, null), B=4, st_z=null, nst_z=0):
-        return lib.sc_lucy_frame_gemm_cellb(epi, f[0], st_z, nst_z, f[1], null, 0, lnz[0], lnz[1],
-                                            null, null, eps, h, h_out, null, K, f[4], 0, 512, f[5],
-                                            B, 1024, f[6], 1024, f[7], null)
-    assert call(epi=2) == -1 and b"epilogue" in lib.sc_last_error()
-    assert call(h_out=f[2]) == -1 and b"alias" in lib.sc_last_error()
-    assert call(K=2048) == -1 and b"1536" in lib.sc_last_error()
-    assert call(K=510) == -1 and b"multiple of 4" in lib.sc_last_error()
-    assert call(lnz=(f[0], f[1])) == -1 and b"statistics" in lib.sc_last_error()
-    assert call(B=0) == 0
 
 
 def test_ctc_side_array_entry_points_reject_bad_arguments_without_gpu(lib):

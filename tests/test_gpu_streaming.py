@@ -195,9 +195,8 @@ def test_streaming_reset_subset_and_blocks_equal_one_pass():
 
 @pytest.mark.parametrize("fused", [True, False])
 def test_frame_engine_odd_blocks_reset_and_state_equal_frame_by_frame(fused):
-    """The frame engine's h pairs flip every frame: 3 frames per call (two captured graphs, one
-    per starting buffer) equal 1-frame eager calls bitwise, through a reset with given state at
-    an odd frame count and a ragged mask; state() reads the live buffer."""
+    """3 frames per captured call equal 1-frame eager calls bitwise, through a reset with given
+    state after an odd frame count and a ragged mask; state() after the last call too."""
     import statecatcher_amd as sc
     from statecatcher_amd.streaming import StreamingLucyRNN
     torch.manual_seed(11 + fused)
@@ -213,7 +212,7 @@ def test_frame_engine_odd_blocks_reset_and_state_equal_frame_by_frame(fused):
     s0 = [torch.randn(B, 64, device=DEV) * 0.3 for _ in range(3)]
     ref = StreamingLucyRNN(m, B, 1, graph=False)
     blk = StreamingLucyRNN(m, B, 3, graph=True)
-    assert ref.engine == blk.engine == "frame" and len(blk.graph) == 2
+    assert ref.engine == blk.engine == "frame" and blk.graph is not None
     e_ref, l_ref = [], []
     for t in range(T):
         if t == 3:
