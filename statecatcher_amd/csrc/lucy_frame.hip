@@ -29,6 +29,12 @@
 // Activations between kernels are fp32.
 #include "sc_common.h"
 
+// SC_FRAME_ABL: ablation bitmask for tools timing only (never set in a shipped build; wrong
+// results): 1 no MFMAs (fp32 weights), 2 no epilogue stores, 4 no weight loads, 8 no A-row loads
+#ifndef SC_FRAME_ABL
+#define SC_FRAME_ABL 0
+#endif
+
 namespace sc {
 
 enum { FR_PLAIN = 0, FR_STATS = 1, FR_CELL_UNFUSED = 2, FR_CELL_FUSED = 3 };
@@ -153,7 +159,9 @@ __global__ void __launch_bounds__(64 * NT * KS, 4) lucy_frame_gemm(FrameGemmArgs
   auto load_chunk = [&](int c0) __attribute__((always_inline)) {
     if constexpr (!BF16W) {
 #pragma unroll
-      for (int i = 0; i < SMAXF; ++i) wf[i] = *(const float4*)(wrf + min((c0 + i) * 16 + 4 * q, a.K - 4));
+      for (int i = 0; i < SMAXF; ++i)
+        wf[i] = (SC_FRAME_ABL & 4) ? make_float4((float)c0, 1.f, 1.f, 1.f)
+                                   : *(const float4*)(wrf + min((c0 + i) * 16 + 4 * q, a.K - 4));
     } else {
 #pragma unroll
       for (int i = 0; i < SMAXB; ++i) wh[i] = *(const bf16x8*)(wrh + min((c0 + i) * 32 + 8 * q, a.K - 8));
@@ -190,7 +198,7 @@ __global__ void __launch_bounds__(64 * NT * KS, 4) lucy_frame_gemm(FrameGemmArgs
         const int rr = i / per_row, k = 4 * (i % per_row), r = r0 + rr;
         v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
         if (i < npc && r < a.B && k < a.K) {   // (K % 4 == 0: a piece is wholly in or out)
-          v[j] = *(const float4*)(a.x + (int64_t)r * a.ldx + k);
+          if (!(SC_FRAME_ABL & 8)) v[j] = *(const float4*)(a.x + (int64_t)r * a.ldx + k);
           if (LN) {
             lw[j] = *(const float4*)(a.ln_w + k);
             lb[j] = *(const float4*)(a.ln_b + k);
@@ -255,6 +263,11 @@ __global__ void __launch_bounds__(64 * NT * KS, 4) lucy_frame_gemm(FrameGemmArgs
         xa.z = in ? xa.z : 0.f;
         xa.w = in ? xa.w : 0.f;
         // k slot q of MFMA j is k0 + j for both operands: the sum runs over the same k set
+        if (SC_FRAME_ABL & 1) {
+          acc0[0] += xa.x * wf[i].x + xa.z * wf[i].z;
+          acc1[0] += xa.y * wf[i].y + xa.w * wf[i].w;
+          continue;
+        }
         acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(xa.x, wf[i].x, acc0, 0, 0, 0);
         acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(xa.y, wf[i].y, acc1, 0, 0, 0);
         acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(xa.z, wf[i].z, acc0, 0, 0, 0);
@@ -346,7 +359,9 @@ __global__ void __launch_bounds__(64 * NT * KS, 4) lucy_frame_gemm(FrameGemmArgs
         o = xs[rr * kpitch + d] + sn;                       // y = u + s', u = LN_in(a)
       }
       const float4 sz = stats16(z), so = stats16(o);
-      if (ok) {
+      if (SC_FRAME_ABL & 2) {
+        asm volatile("" ::"v"(sz.x), "v"(so.x), "v"(sn), "v"(z), "v"(o));
+      } else if (ok) {
         a.s[(int64_t)r * D + d] = m * sn + (1.0f - m) * sp;
         a.z[(int64_t)r * D + d] = z;
         a.y[(int64_t)r * D + d] = o;
