@@ -23,8 +23,8 @@
 //                     renormalised every 16 steps by exact powers of two: five full-rate fp64
 //                     adds / multiplies per state pair and step instead of five exp2 / log2; one
 //                     wave computes, two more store its rows as fp32 logs (lin_produce /
-//                     lin_consume); falls back per sequence to ab1_run (one wave, fp32 log space)
-//                     when an emission or the whole wave would underflow
+//                     lin_consume); a sequence with an emission or a wave that would underflow
+//                     goes to ctc_x64_kernel
 //   ctc_ab_kernel     (the default) one workgroup per (sequence, direction): 2B workgroups run alpha forward
 //                     and beta backward concurrently.  Two states (a blank and its label) per
 //                     lane; each wave also carries a K-pair halo of its neighbour's pairs so it
@@ -35,6 +35,12 @@
 //                     log-sum-exp) and are re-centred on the workgroup max every 16 steps; the
 //                     running offset is kept in fp64 (at T=1500 |alpha| ~ 1e4, where an fp32
 //                     ulp would put ~0.5% error into the posteriors).
+//                     A re-centring that finds the maximum more than kDrift bits below the last
+//                     one flags the sequence (sharp[b]): its fp32 values have drifted far enough
+//                     from 0 that their rounding reaches the posteriors
+//   ctc_x64_kernel    (flagged sequences, U <= 255) the lattice again, exactly: one wave, values
+//                     as fp64 mantissa + int exponent (no under- or overflow), emissions from the
+//                     logits in fp64, rows stored relative to each step's largest value
 //   ctc_grad_kernel   one wave per (b,t) row: label occupancies into an LDS row of V
 //                     log-sums, then one coalesced 16-byte pass writing the gradient row
 #include "sc_common.h"
@@ -52,11 +58,14 @@ constexpr float kNegInf = -__builtin_huge_valf();
 
 struct CtcWs {
   float* lse;     // [B,T]      natural-log row normaliser (logits input)
+  double* lse64;  // [B,T]      the same, row max + log(sum) kept in fp64 (the exact lattice and
+                  //            the gradient's log-probs: an fp32 lse of a row ~1e3 is 6e-5 off)
   float* lpe;     // [B,T,Sp]   base-2 emission log-probs of the blank-extended states
   float* alpha;   // [B,T,Sp]   base-2, relative to offA
   float* beta;    // [B,T,Sp]   base-2, relative to offB
-  double* offA;   // [B,T]      base-2 offsets: entry n = offset after the n-th re-centring (at
-  double* offB;   // [B,T]      step i = 2Kn - 1 of the direction), so step i has entry (i+1)/2K
+  double* offA;   // [B,T+1]    base-2 offsets: entry n = offset after the n-th re-centring (at
+  double* offB;   // [B,T+1]    step i = 2Kn - 1 of the direction), so step i has entry (i+1)/2K
+                  //            (the exact lattice re-centres every step: entry i + 1)
   float* cst;     // [B,T]      base-2 per-row emission shift c_t (lpe = log2 p - c_t)
   double* ll2s;   // [B]        base-2 log-likelihood of the SHIFTED lattice (log2 p - sum_t c_t)
   int* chain;     // [B,Um]
@@ -64,6 +73,8 @@ struct CtcWs {
   // one-wave family (Umax <= 255) only:
   float* ylin;    // [B,T,Sp]   linear shifted emissions 2^(lpe) (0: dead)
   int* flag;      // [B]        a live emission below 2^-kTiny: the linear lattice is not used
+  int* sharp;     // [B]        the log-space lattice drifted more than kDrift bits between two
+                  //            re-centrings: ctc_x64_kernel recomputes the sequence exactly
 };
 
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -88,17 +99,19 @@ static size_t ws_layout(int B, int T, int Umax, CtcWs* w, void* base) {
   };
   CtcWs t;
   t.lse = (float*)take((size_t)B * T * 4);
+  t.lse64 = (double*)take((size_t)B * T * 8);
   t.lpe = (float*)take((size_t)B * T * Sp * 4);
   t.alpha = (float*)take((size_t)B * T * Sp * ab);
   t.beta = (float*)take((size_t)B * T * Sp * ab);
-  t.offA = (double*)take((size_t)B * T * 8);
-  t.offB = (double*)take((size_t)B * T * 8);
+  t.offA = (double*)take((size_t)B * (T + 1) * 8);
+  t.offB = (double*)take((size_t)B * (T + 1) * 8);
   t.cst = (float*)take((size_t)B * T * 4);
   t.ll2s = (double*)take((size_t)B * 8);
   t.chain = (int*)take((size_t)B * Um * 4);
   t.first = (int*)take((size_t)B * Um * 4);
   t.ylin = lin ? (float*)take((size_t)B * T * Sp * 4) : nullptr;
   t.flag = lin ? (int*)take((size_t)B * 4) : nullptr;
+  t.sharp = (int*)take((size_t)B * 4);
   if (w) *w = t;
   return off;
 }
@@ -213,7 +226,10 @@ __global__ void __launch_bounds__(256) ctc_emit_kernel(CtcArgs a) {
     const float M = wave_max_dpp(m);
     l = wave_sum_dpp(m == kNegInf ? 0.0f : l * fexp(m - M));
     lse = M + flog(l);
-    if (lane == 0) a.ws.lse[row] = lse;
+    if (lane == 0) {
+      a.ws.lse[row] = lse;
+      a.ws.lse64[row] = (double)M + (double)flog(l);
+    }
   }
   float* out = a.ws.lpe + row * a.Sp;
   auto lp2x = [&](float xl) { return fmaxf((xl - lse) * kLog2e, -1e30f); };
@@ -263,6 +279,7 @@ __global__ void __launch_bounds__(256) ctc_chain_kernel(CtcArgs a) {
   const int Um = a.Umax > 0 ? a.Umax : 1;
   for (int u = threadIdx.x; u < Ub; u += blockDim.x) lt[u] = (int)tg[u];
   __syncthreads();
+  if (blockIdx.y == 0 && threadIdx.x == 0) a.ws.sharp[b] = 0;   // (ctc_ab's drift flag)
   const int u = blockIdx.y * 4 + (threadIdx.x >> 6);
   if (u >= Um) return;
   int nxt = -1, first = 0;
@@ -304,6 +321,9 @@ __device__ __forceinline__ float shl1(float v) {   // value of lane+1 (lane 63: 
 // Branch-free log2-sum-exp for the lattice: "dead" states carry kDead (finite), so no -inf
 // test is needed; exp2 of anything ~kDead below the max is exactly 0.
 constexpr float kDead = -1e30f;
+// a re-centring that finds the lattice's maximum this many bits below the last one sends the
+// sequence to the exact lattice (ctc_x64_kernel): |values| ~ 512 round by ~3e-5 per step
+constexpr float kDrift = 512.0f;
 __device__ __forceinline__ float lse3_live(float a, float b, float c) {
   const float m = fmaxf(fmaxf(a, b), c);
   if (SC_CTC_ABL & 4) return m;
@@ -412,7 +432,7 @@ __device__ __forceinline__ void ab_run(const CtcArgs& a, int b, int Tb, int Ub) 
       (BETA ? a.ws.beta : a.ws.alpha) + (int64_t)b * a.T * a.Sp, 0, (int)(rowb * (uint32_t)a.T),
       0x00020000);
   const uint32_t ovo = (own && 2 * p < a.Sp) ? (uint32_t)(8 * pc) : kDrop;
-  double* offn = (BETA ? a.ws.offB : a.ws.offA) + (int64_t)b * a.T;
+  double* offn = (BETA ? a.ws.offB : a.ws.offA) + (int64_t)b * (a.T + 1);
   if (tid == 0) offn[0] = 0.0;
   auto tstep = [&](int i) { return BETA ? Tb - 1 - i : i; };
   float2 bufA[kAbP], bufB[kAbP];
@@ -511,6 +531,9 @@ __device__ __forceinline__ void ab_run(const CtcArgs& a, int b, int Tb, int Ub) 
             vB -= m;
             vL -= m;
             off += (double)m;
+            // values that drifted this far below their re-centring carry fp32 rounding of
+            // ~|m| 2^-24 per step into the posteriors: the exact lattice redoes the sequence
+            if (tid == 0 && m < -kDrift) a.ws.sharp[b] = 1;
           }
           if (tid == 0) offn[(exch + 1) >> 1] = off;
         }
@@ -579,166 +602,13 @@ __global__ void __launch_bounds__(1024) ctc_ab_kernel(CtcArgs a) {
   else ab_run<K, false>(a, b, Tb, Ub);
 }
 
-// ONE WAVE per (sequence, direction) when the lattice's U + 1 state pairs fit PPL pairs per lane
-// (PPL <= 4: U <= 255; C2's U <= 150 takes PPL = 3).  Lane l holds pairs p = l PPL .. l PPL +
-// PPL - 1, so a step needs one DPP lane shift (alpha: the previous lane's last label state;
-// beta: the next lane's first pair) and 2 PPL independent log-sum-exps: no halo lanes, no LDS, no
-// barrier.  The recurrence's loop runs through PPL consecutive steps of one lane before it
-// crosses a lane, so the step's latency is one log-sum-exp plus a DPP every PPL steps, and the
-// 2 PPL chains of a step fill each other's issue gaps.  (The multi-wave kernel above spends a
-// workgroup barrier every K steps on its halo exchange and a third of its lanes on halo pairs.)
-// Re-centred on the wave max every kAb1R steps (fp64 offsets, stored per re-centring).
-constexpr int kAb1R = 16;   // (also the linear lattice's renormalisation period: same offsets)
-constexpr int kAb1P = 16;   // emission prefetch depth (steps)
+// The one-wave lattices (ctc_lin_kernel, ctc_x64_kernel) hold PPL pairs of states per lane
+// (PPL <= 4: U <= 255; C2's U <= 150 takes PPL = 3): lane l holds pairs p = l PPL .. l PPL +
+// PPL - 1, so a step needs one DPP lane shift and no halo, LDS or barrier.
+constexpr int kAb1R = 16;   // the linear lattice's renormalisation period (steps)
+constexpr int kAb1P = 16;   // its emission prefetch depth (steps)
 
-template <int PPL, bool BETA>
-__device__ __forceinline__ void ab1_run(const CtcArgs& a, int b, int Tb, int Ub) {
-  const int lane = threadIdx.x;
-  const int64_t* tg = a.tg + (int64_t)b * a.tgs;
-  const int npairs = a.Sp / 2;            // pairs in a workspace row
-  bool skip[PPL];
-  uint32_t vo[PPL];                       // byte offset of pair p in a row (kDrop past it)
-  constexpr uint32_t kDrop = 0x80000000u;
-#pragma unroll
-  for (int j = 0; j < PPL; ++j) {
-    const int p = lane * PPL + j;
-    skip[j] = false;
-    if (p < Ub) {   // the label state 2p+1 is live
-      const int lab = (int)tg[p];
-      if (!BETA) {
-        skip[j] = p >= 1 && lab != a.blank && lab != (int)tg[p - 1];
-      } else if (p + 1 < Ub) {
-        const int l2 = (int)tg[p + 1];
-        skip[j] = l2 != a.blank && l2 != lab;
-      }
-    }
-    vo[j] = p < npairs ? (uint32_t)(8 * p) : kDrop;
-  }
-  const uint32_t rowb = (uint32_t)(a.Sp * 4), orowb = rowb;
-  const __amdgpu_buffer_rsrc_t ers = __builtin_amdgcn_make_buffer_rsrc(
-      a.ws.lpe + (int64_t)b * a.T * a.Sp, 0, (int)(rowb * (uint32_t)a.T), 0x00020000);
-  const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
-      (BETA ? a.ws.beta : a.ws.alpha) + (int64_t)b * a.T * a.Sp, 0, (int)(orowb * (uint32_t)a.T),
-      0x00020000);
-  double* offn = (BETA ? a.ws.offB : a.ws.offA) + (int64_t)b * a.T;
-  if (lane == 0) offn[0] = 0.0;
-  auto tstep = [&](int i) { return BETA ? Tb - 1 - i : i; };
-  f2v bufA[kAb1P][PPL], bufB[kAb1P][PPL];
-  auto load = [&](f2v (&buf)[kAb1P][PPL], int i0) {
-#pragma unroll
-    for (int s = 0; s < kAb1P; ++s) {
-      const uint32_t so = (uint32_t)tstep(min(i0 + s, Tb - 1)) * rowb;
-#pragma unroll
-      for (int j = 0; j < PPL; ++j)
-        buf[s][j] = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(ers, vo[j], so, 0));
-    }
-  };
-  float vB[PPL], vL[PPL];
-#pragma unroll
-  for (int j = 0; j < PPL; ++j) vB[j] = vL[j] = kDead;
-  double off = 0.0;
-  auto body = [&](const f2v (&buf)[kAb1P][PPL], int i0) __attribute__((always_inline)) {
-#pragma unroll
-    for (int s = 0; s < kAb1P; ++s) {
-      const int i = i0 + s;
-      if (i >= Tb) break;
-      if (i == 0) {
-#pragma unroll
-        for (int j = 0; j < PPL; ++j) {
-          const int p = lane * PPL + j;
-          vB[j] = (p <= Ub && p == (BETA ? Ub : 0)) ? buf[s][j].x : kDead;
-          vL[j] = (p < Ub && p == (BETA ? Ub - 1 : 0)) ? buf[s][j].y : kDead;
-        }
-      } else if (!BETA) {
-        // pair p's predecessor label state 2p-1: pair p-1's, the previous lane's last for j = 0
-        float prevL[PPL];
-        prevL[0] = shr1(vL[PPL - 1]);   // lane 0: pair 0 has no predecessor (dead, not 0)
-#pragma unroll
-        for (int j = 1; j < PPL; ++j) prevL[j] = vL[j - 1];
-#pragma unroll
-        for (int j = 0; j < PPL; ++j) {
-          const f2v r = lse23(vB[j], prevL[j], vL[j], vB[j], skip[j] ? prevL[j] : kDead, buf[s][j]);
-          vB[j] = r.x;
-          vL[j] = r.y;
-        }
-      } else {
-        // pair p's successors 2p+2 (blank) and 2p+3 (label): pair p+1's, the next lane's first
-        float nB[PPL], nL[PPL];
-        nB[PPL - 1] = shl1(vB[0]);   // lane 63: no successor (dead, not 0)
-        nL[PPL - 1] = shl1(vL[0]);
-#pragma unroll
-        for (int j = 0; j + 1 < PPL; ++j) {
-          nB[j] = vB[j + 1];
-          nL[j] = vL[j + 1];
-        }
-#pragma unroll
-        for (int j = 0; j < PPL; ++j) {
-          const f2v r = lse23(vB[j], vL[j], vL[j], nB[j], skip[j] ? nL[j] : kDead, buf[s][j]);
-          vB[j] = r.x;
-          vL[j] = r.y;
-        }
-      }
-      if ((i + 1) % kAb1R == 0) {   // re-centre on the wave max
-        float m = kDead;
-#pragma unroll
-        for (int j = 0; j < PPL; ++j) m = vmax3(m, vB[j], vL[j]);
-        m = wave_max_dpp(m);
-        if (m > 0.5f * kDead) {   // all dead (infeasible): keep the sentinel
-#pragma unroll
-          for (int j = 0; j < PPL; ++j) {
-            vB[j] -= m;
-            vL[j] -= m;
-          }
-          off += (double)m;
-        }
-        if (lane == 0) offn[(i + 1) / kAb1R] = off;
-      }
-      const uint32_t so = (uint32_t)tstep(i) * orowb;
-#pragma unroll
-      for (int j = 0; j < PPL; ++j)
-        __builtin_amdgcn_raw_buffer_store_b64(
-            __builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, f2v{vB[j], vL[j]}),
-            ors, vo[j], so, 0);
-    }
-  };
-  load(bufA, 0);
-  for (int i0 = 0; i0 < Tb; i0 += 2 * kAb1P) {
-    load(bufB, i0 + kAb1P);
-    body(bufA, i0);
-    if (i0 + kAb1P >= Tb) break;
-    load(bufA, i0 + 2 * kAb1P);
-    body(bufB, i0 + kAb1P);
-  }
-  if (!BETA) {
-    // sum_t c_t in fp64, fixed order
-    double cs = 0.0;
-    for (int t = lane; t < Tb; t += 64) cs += (double)a.ws.cst[(int64_t)b * a.T + t];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) cs += __shfl_xor(cs, o);
-    // log p = log2sum(alpha_{Tb-1}(2Ub), alpha_{Tb-1}(2Ub-1)) + off
-    float c = kDead;
-#pragma unroll
-    for (int j = 0; j < PPL; ++j) {
-      const int p = lane * PPL + j;
-      if (p == Ub) c = lse2_live(c, vB[j]);
-      if (p == Ub - 1) c = lse2_live(c, vL[j]);
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const float co = __shfl_xor(c, o);
-      const float m = fmaxf(c, co);
-      c = m + log2_(exp2_(c - m) + exp2_(co - m));
-    }
-    if (lane == 0) {
-      const bool dead = c < 0.5f * kDead;
-      const double ll2s = (double)c + off;
-      a.ws.ll2s[b] = dead ? -__builtin_huge_val() : ll2s;
-      a.nll[b] = dead ? __builtin_huge_valf() : (float)(-(ll2s + cs) * 0.6931471805599453);
-    }
-  }
-}
-
-// Linear-domain lattice (SC_CTC_LIN=1, Umax <= 255).  The pair-per-lane layout of ab1_run, but
+// Linear-domain lattice (SC_CTC_LIN=1, Umax <= 255).  The pair-per-lane layout above, but
 // the values are probabilities in fp64: one step of a pair is
 //   alpha:  B' = (B + L[p-1]) e(2p);          L' = (L + B + skip L[p-1]) e(2p+1)
 //   beta:   B' = (B + L) e(2p);               L' = (L + B[p+1] + skip L[p+1]) e(2p+1)
@@ -758,8 +628,8 @@ __device__ __forceinline__ void ab1_run(const CtcArgs& a, int b, int Tb, int Ub)
 // fp64 keeps 2^1022 of range below the wave max between renormalisations (fp32 log space keeps
 // all of it; a state 2^1022 below the max that later carries the likelihood is the one case the
 // two differ).  A sequence whose live emissions reach below 2^-kTiny (the emit kernel's flag), and
-// a direction whose wave max or final likelihood underflows to 0, run ab1_run (fp32 log space) on
-// wave 0 instead.
+// a direction whose wave max or final likelihood underflows to 0, are flagged (sharp[b]) and
+// recomputed by ctc_x64_kernel.
 __device__ __forceinline__ double dpp_shr1d(double v) {   // lane-1's value (lane 0: 0)
   const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), 0x138, 0xf, 0xf, true);
   const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), 0x138, 0xf, 0xf, true);
@@ -811,7 +681,7 @@ __device__ __forceinline__ bool lin_produce(const CtcArgs& a, int b, int Tb, int
   const uint32_t rowb = (uint32_t)(a.Sp * 4);
   const __amdgpu_buffer_rsrc_t ers = __builtin_amdgcn_make_buffer_rsrc(
       a.ws.ylin + (int64_t)b * a.T * a.Sp, 0, (int)(rowb * (uint32_t)a.T), 0x00020000);
-  double* offn = (BETA ? a.ws.offB : a.ws.offA) + (int64_t)b * a.T;
+  double* offn = (BETA ? a.ws.offB : a.ws.offA) + (int64_t)b * (a.T + 1);
   if (lane == 0) offn[0] = 0.0;
   auto tstep = [&](int i) { return BETA ? Tb - 1 - i : i; };
   f2v bufA[kLinC][PPL], bufB[kLinC][PPL];
@@ -1014,10 +884,254 @@ __global__ void __launch_bounds__(192) ctc_lin_kernel(CtcArgs a) {
     }
     __syncthreads();
   }
-  if (!lin && w == 0) {   // log space: the same rows, one wave
-    if (is_beta) ab1_run<PPL, true>(a, b, Tb, Ub);
-    else ab1_run<PPL, false>(a, b, Tb, Ub);
+  // an underflow (or a flagged emission): ctc_x64_kernel recomputes the sequence exactly
+  if (!lin && threadIdx.x == 0) a.ws.sharp[b] = 1;
+}
+
+
+// ------------------------------------------------- exact lattice for sharp sequences --------
+// ctc_x64_kernel recomputes, ONE wave per (sequence, direction), every sequence whose log-space
+// lattice drifted more than kDrift bits between two re-centrings (sharp[b], set by ctc_ab_kernel).
+// That happens when the best alignment must pay emissions hundreds of bits below the frame's best
+// (logits x 100 over a small vocabulary: log-probs of -2000 nats): an fp32 log-space value of
+// magnitude ~1e4 carries 1e-3 of rounding per step, and an fp32 EMISSION of magnitude 3e3 is
+// already 1e-4 off before the lattice adds it.  Here every value is an extended-range number: an
+// fp64 mantissa in [0.5, 1) (0: dead) and an int exponent, so a state never under- or overflows
+// and the recurrence rounds at 2^-53.  Emissions come straight from the logits in fp64 (the
+// row's lse kept as max + log(sum), ws.lse64): e = x log2(e) - lse log2(e) - c_t, split into
+// the integer floor k and 2^frac.  One step of a pair:
+//   alpha:  B' = (B + L[p-1]) e(2p);          L' = (L + B + skip L[p-1]) e(2p+1)
+//   beta:   B' = (B + L) e(2p);               L' = (L + B[p+1] + skip L[p+1]) e(2p+1)
+// with the sums aligned to their largest exponent (v_ldexp_f64, exact but for what falls below
+// 2^-53 of it).  Each step's row is stored as the fp32 base-2 log relative to that step's largest
+// exponent O_t (entry i + 1 of the offsets: the gradient reads a sharp sequence's offsets per
+// step), so the live states' stored values sit near 0 whatever the drift.
+constexpr int kXDeadE = -(1 << 29);
+constexpr int kX64P = 16;   // steps per emission prefetch chunk
+constexpr double kLog2eD = 1.4426950408889634;
+
+struct Xv {
+  double m;
+  int e;
+};
+__device__ __forceinline__ Xv xnorm(double m, int e) {   // m >= 0 -> [0.5, 1) 2^e, 0 -> dead
+  int x;
+  const double mm = frexp(m, &x);
+  return m > 0.0 ? Xv{mm, e + x} : Xv{0.0, kXDeadE};
+}
+__device__ __forceinline__ Xv xadd2(Xv a, Xv b) {
+  const int E = max(a.e, b.e);
+  return Xv{ldexp(a.m, a.e - E) + ldexp(b.m, b.e - E), E};
+}
+__device__ __forceinline__ Xv xadd3(Xv a, Xv b, Xv c) {
+  const int E = max(max(a.e, b.e), c.e);
+  return Xv{ldexp(a.m, a.e - E) + ldexp(b.m, b.e - E) + ldexp(c.m, c.e - E), E};
+}
+template <bool RIGHT>
+__device__ __forceinline__ Xv xdpp(Xv v) {   // lane -1's (RIGHT) / lane +1's value, else dead
+  constexpr int ctl = RIGHT ? 0x138 : 0x130;
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v.m), ctl, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v.m), ctl, 0xf, 0xf, false);
+  const int e = __builtin_amdgcn_update_dpp(kXDeadE, v.e, ctl, 0xf, 0xf, false);
+  return Xv{__hiloint2double(hi, lo), e};
+}
+// emission factor of logit x at a step with q = lse log2(e) + c_t: (2^frac, floor) as an Xv
+__device__ __forceinline__ Xv xemit(float x, double q, bool live) {
+  const double e2 = (double)x * kLog2eD - q;
+  if (!live || !(e2 > -1e300)) return Xv{0.0, kXDeadE};
+  const double k = floor(e2);
+  return xnorm((double)exp2_((float)(e2 - k)), (int)k);
+}
+
+template <int PPL, int DT, bool BETA>
+__device__ __forceinline__ void x64_run(const CtcArgs& a, int b, int Tb, int Ub) {
+  using E = Elem<DT>;
+  const int lane = threadIdx.x;
+  const int64_t* tg = a.tg + (int64_t)b * a.tgs;
+  const int npairs = a.Sp / 2;
+  bool skip[PPL], liveB[PPL], liveL[PPL];
+  uint32_t cB[PPL], cL[PPL];   // byte offsets of the pair's blank / label logit in a row
+  uint32_t vo[PPL];            // byte offset of pair p in a lattice row (kDrop past it)
+  constexpr uint32_t kDrop = 0x80000000u;
+  const bool ex = a.ex != nullptr;
+  const uint32_t esz = ex ? 4u : (uint32_t)sizeof(typename E::T);
+#pragma unroll
+  for (int j = 0; j < PPL; ++j) {
+    const int p = lane * PPL + j;
+    skip[j] = false;
+    liveB[j] = p <= Ub;
+    liveL[j] = p < Ub;
+    int lab = a.blank;
+    if (p < Ub) {
+      lab = (int)tg[p];
+      if (!BETA) {
+        skip[j] = p >= 1 && lab != a.blank && lab != (int)tg[p - 1];
+      } else if (p + 1 < Ub) {
+        const int l2 = (int)tg[p + 1];
+        skip[j] = l2 != a.blank && l2 != lab;
+      }
+    }
+    lab = lab < 0 ? 0 : (lab >= a.V ? a.V - 1 : lab);
+    cB[j] = ex ? 0u : (uint32_t)a.blank * esz;
+    cL[j] = ex ? (uint32_t)(p < Ub ? 1 + p : 0) * 4u : (uint32_t)lab * esz;
+    vo[j] = p < npairs ? (uint32_t)(8 * p) : kDrop;
   }
+  // logits (or the emission-logit side array) of this sequence, rows at t * row stride
+  const void* xb = ex ? (const void*)(a.ex + (int64_t)b * a.exb)
+                      : (const void*)((const typename E::T*)a.x + (int64_t)b * a.sb);
+  const uint32_t xrow = ex ? (uint32_t)a.ext * 4u : (uint32_t)a.stt * esz;
+  const Buf<float> xf(xb);
+  const Buf<typename E::T> xe(xb);
+  auto ldx = [&](uint32_t col, uint32_t so) -> uint32_t {
+    return ex ? __float_as_uint(xf.ld(col, so)) : xe.ldw(col, so);
+  };
+  auto cvt = [&](uint32_t w) { return ex ? __uint_as_float(w) : E::ldw(w); };
+  const uint32_t rowb = (uint32_t)(a.Sp * 4);
+  const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
+      (BETA ? a.ws.beta : a.ws.alpha) + (int64_t)b * a.T * a.Sp, 0, (int)(rowb * (uint32_t)a.T),
+      0x00020000);
+  double* offn = (BETA ? a.ws.offB : a.ws.offA) + (int64_t)b * (a.T + 1);
+  const double* lse64 = a.ws.lse64 + (int64_t)b * a.T;
+  const float* cst = a.ws.cst + (int64_t)b * a.T;
+  if (lane == 0) offn[0] = 0.0;
+  auto tstep = [&](int i) { return BETA ? Tb - 1 - i : i; };
+  // a chunk's raw logits (blank, label per pair and step) and, on lane s, step s's q
+  uint32_t wA[kX64P][PPL][2], wB[kX64P][PPL][2];
+  double qA, qB;
+  auto load = [&](uint32_t (&w)[kX64P][PPL][2], double& q, int i0) {
+#pragma unroll
+    for (int s = 0; s < kX64P; ++s) {
+      const uint32_t so = (uint32_t)tstep(min(i0 + s, Tb - 1)) * xrow;
+#pragma unroll
+      for (int j = 0; j < PPL; ++j) {
+        w[s][j][0] = ldx(cB[j], so);
+        w[s][j][1] = ldx(cL[j], so);
+      }
+    }
+    const int t = tstep(min(i0 + (lane & (kX64P - 1)), Tb - 1));
+    q = (a.is_logits ? lse64[t] * kLog2eD : 0.0) + (double)cst[t];
+  };
+  Xv vB[PPL], vL[PPL];
+#pragma unroll
+  for (int j = 0; j < PPL; ++j) vB[j] = vL[j] = Xv{0.0, kXDeadE};
+  const Xv dead{0.0, kXDeadE};
+  auto body = [&](const uint32_t (&w)[kX64P][PPL][2], double qv, int i0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int s = 0; s < kX64P; ++s) {
+      const int i = i0 + s;
+      if (i >= Tb) break;
+      const double q = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(qv), s),
+                                        __builtin_amdgcn_readlane(__double2loint(qv), s));
+      Xv eB[PPL], eL[PPL];
+#pragma unroll
+      for (int j = 0; j < PPL; ++j) {
+        eB[j] = xemit(cvt(w[s][j][0]), q, liveB[j]);
+        eL[j] = xemit(cvt(w[s][j][1]), q, liveL[j]);
+      }
+      if (i == 0) {
+#pragma unroll
+        for (int j = 0; j < PPL; ++j) {
+          const int p = lane * PPL + j;
+          vB[j] = p == (BETA ? Ub : 0) ? eB[j] : dead;
+          vL[j] = p == (BETA ? Ub - 1 : 0) ? eL[j] : dead;
+        }
+      } else if (!BETA) {
+        Xv prevL[PPL];
+        prevL[0] = xdpp<true>(vL[PPL - 1]);
+#pragma unroll
+        for (int j = 1; j < PPL; ++j) prevL[j] = vL[j - 1];
+#pragma unroll
+        for (int j = 0; j < PPL; ++j) {
+          const Xv nb = xadd2(vB[j], prevL[j]);
+          const Xv nl = xadd3(vL[j], vB[j], skip[j] ? prevL[j] : dead);
+          vB[j] = xnorm(nb.m * eB[j].m, nb.e + eB[j].e);
+          vL[j] = xnorm(nl.m * eL[j].m, nl.e + eL[j].e);
+        }
+      } else {
+        Xv nB[PPL], nL[PPL];
+        nB[PPL - 1] = xdpp<false>(vB[0]);
+        nL[PPL - 1] = xdpp<false>(vL[0]);
+#pragma unroll
+        for (int j = 0; j + 1 < PPL; ++j) {
+          nB[j] = vB[j + 1];
+          nL[j] = vL[j + 1];
+        }
+#pragma unroll
+        for (int j = 0; j < PPL; ++j) {
+          const Xv nb = xadd2(vB[j], vL[j]);
+          const Xv nl = xadd3(vL[j], nB[j], skip[j] ? nL[j] : dead);
+          vB[j] = xnorm(nb.m * eB[j].m, nb.e + eB[j].e);
+          vL[j] = xnorm(nl.m * eL[j].m, nl.e + eL[j].e);
+        }
+      }
+      // the row, relative to its largest exponent
+      int mx = kXDeadE;
+#pragma unroll
+      for (int j = 0; j < PPL; ++j) mx = max(mx, max(vB[j].e, vL[j].e));
+      const int O = (int)wave_max_dpp((float)mx);
+      const bool alive = O > kXDeadE / 2;
+      if (lane == 0) offn[i + 1] = alive ? (double)O : 0.0;
+      const uint32_t so = (uint32_t)tstep(i) * rowb;
+#pragma unroll
+      for (int j = 0; j < PPL; ++j) {
+        const float rb = vB[j].m > 0.0 ? (float)(vB[j].e - O) + log2_((float)vB[j].m) : kDead;
+        const float rl = vL[j].m > 0.0 ? (float)(vL[j].e - O) + log2_((float)vL[j].m) : kDead;
+        __builtin_amdgcn_raw_buffer_store_b64(
+            __builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, f2v{rb, rl}), ors,
+            vo[j], so, 0);
+      }
+    }
+  };
+  load(wA, qA, 0);
+  for (int i0 = 0; i0 < Tb; i0 += 2 * kX64P) {
+    load(wB, qB, i0 + kX64P);
+    body(wA, qA, i0);
+    if (i0 + kX64P >= Tb) break;
+    load(wA, qA, i0 + 2 * kX64P);
+    body(wB, qB, i0 + kX64P);
+  }
+  if (!BETA) {
+    // P = alpha_{Tb-1}(2Ub) + alpha_{Tb-1}(2Ub-1); sum_t c_t; both in a fixed order
+    Xv c = dead;
+#pragma unroll
+    for (int j = 0; j < PPL; ++j) {
+      const int p = lane * PPL + j;
+      if (p == Ub) c = xadd2(c, vB[j]);
+      if (p == Ub - 1) c = xadd2(c, vL[j]);
+    }
+    double cs = 0.0;
+    for (int t = lane; t < Tb; t += 64) cs += (double)cst[t];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const Xv co{__shfl_xor(c.m, o), __shfl_xor(c.e, o)};
+      c = xadd2(c, co);
+      cs += __shfl_xor(cs, o);
+    }
+    if (lane == 0) {
+      const bool deadP = !(c.m > 0.0);
+      const double ll2s = (double)c.e + log2(c.m);
+      a.ws.ll2s[b] = deadP ? -__builtin_huge_val() : ll2s;
+      a.nll[b] = deadP ? __builtin_huge_valf() : (float)(-(ll2s + cs) * 0.6931471805599453);
+    }
+  }
+}
+
+template <int PPL, int DT>
+__global__ void __launch_bounds__(64) ctc_x64_kernel(CtcArgs a) {
+  const bool is_beta = blockIdx.x >= a.B;
+  const int b = is_beta ? blockIdx.x - a.B : blockIdx.x;
+  if (a.ws.sharp[b] == 0) return;   // (uniform: the common case costs one load)
+  const int Tb = clampi(a.in_lens[b], 0, a.T);
+  const int Ub = clampi(a.tgt_lens[b], 0, a.Umax);
+  if (Tb == 0) return;
+  if (is_beta) x64_run<PPL, DT, true>(a, b, Tb, Ub);
+  else x64_run<PPL, DT, false>(a, b, Tb, Ub);
+}
+
+// pairs per lane of the exact lattice (0: U > 255, not built)
+static int x64_ppl(int Umax) {
+  const int ppl = (Umax + 1 + 63) / 64;
+  return ppl <= 4 ? ppl : 0;
 }
 
 // pairs per lane of the one-wave lattice family (0: the multi-wave kernel).  Off unless
@@ -1102,16 +1216,19 @@ __global__ void __launch_bounds__(256) ctc_grad_kernel(CtcArgs a) {
   // exp(lcab + nll - lp) = 2^(lcab2 + offA + offB + c_t - ll2s - lp*log2e): the lattice holds
   // alpha_t - sum_{t'<=t} c and beta_t - sum_{t'>=t} c, so alpha + beta carries c_t once more than
   // the shifted log-likelihood ll2s; offsets folded in fp64
-  const int per = 2 * a.kh;   // steps per re-centring
-  const float koff = (float)(a.ws.offA[(int64_t)b * a.T + (t + 1) / per] +
-                             a.ws.offB[(int64_t)b * a.T + (Tb - t) / per] +
+  // steps per re-centring (a sequence the exact lattice recomputed has one offset per step)
+  const int per = a.ws.sharp[b] ? 1 : 2 * a.kh;
+  const float koff = (float)(a.ws.offA[(int64_t)b * (a.T + 1) + (t + 1) / per] +
+                             a.ws.offB[(int64_t)b * (a.T + 1) + (Tb - t) / per] +
                              (double)a.ws.cst[(int64_t)b * a.T + t] - a.ws.ll2s[b]);
   const int* chain = a.ws.chain + (int64_t)b * Um;
   const int* first = a.ws.first + (int64_t)b * Um;
+  // the log-probs as (x - lse) - lse_lo: lse's fp32 rounding (6e-5 at |lse| ~ 1e3) taken out
   const float lse = a.is_logits ? a.ws.lse[(int64_t)b * a.T + t] : 0.0f;
+  const float lse_lo = a.is_logits ? (float)(a.ws.lse64[(int64_t)b * a.T + t] - (double)lse) : 0.0f;
   // (ex) the finished gradient of an emission column from its exact logit and occupancy
   auto exact_grad = [&](float logit, float occ2) {
-    const float lp2 = (logit - lse) * kLog2e;
+    const float lp2 = ((logit - lse) - lse_lo) * kLog2e;
     return (exp2_(lp2) - exp2_(occ2 + koff - lp2)) * sc;
   };
   float m = kNegInf, l = 0.0f;   // blank-label occupancy (base 2), per lane
@@ -1159,7 +1276,7 @@ __global__ void __launch_bounds__(256) ctc_grad_kernel(CtcArgs a) {
       const float lc[8] = {l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, l1.z, l1.w};
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        const float lp2 = (xv[k] - lse) * kLog2e;
+        const float lp2 = ((xv[k] - lse) - lse_lo) * kLog2e;
         gv[k] = (exp2_(lp2) - exp2_(lc[k] + koff - lp2)) * sc;
         if (a.ex && lc[k] != kNegInf) gv[k] = lc[k];   // (an emission column's finished value)
       }
@@ -1173,12 +1290,14 @@ __global__ void __launch_bounds__(256) ctc_grad_kernel(CtcArgs a) {
     return;
   }
   for (int v = lane; v < a.V; v += 64) {
-    const float lp2 = (E::ld(xr[v]) - lse) * kLog2e;
+    const float lp2 = ((E::ld(xr[v]) - lse) - lse_lo) * kLog2e;
     const float lc = lcab[v];
     const float gv = (a.ex && lc != kNegInf) ? lc : (exp2_(lp2) - exp2_(lc + koff - lp2)) * sc;
     g[v] = G::st(gv);
   }
 }
+
+static void launch_ab(const CtcArgs& a, hipStream_t st);
 
 template <int DT>
 static void launch_fwd(const CtcArgs& a, hipStream_t st) {
@@ -1188,12 +1307,24 @@ static void launch_fwd(const CtcArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(ctc_chain_kernel, dim3(a.B, ((a.Umax > 0 ? a.Umax : 1) + 3) / 4), dim3(256), 0,
                      st, a);
   switch (a.lin ? lin_ppl(a.Umax) : 0) {
-    case 1: hipLaunchKernelGGL((ctc_lin_kernel<1>), dim3(2 * a.B), dim3(192), 0, st, a); return;
-    case 2: hipLaunchKernelGGL((ctc_lin_kernel<2>), dim3(2 * a.B), dim3(192), 0, st, a); return;
-    case 3: hipLaunchKernelGGL((ctc_lin_kernel<3>), dim3(2 * a.B), dim3(192), 0, st, a); return;
-    case 4: hipLaunchKernelGGL((ctc_lin_kernel<4>), dim3(2 * a.B), dim3(192), 0, st, a); return;
+    case 1: hipLaunchKernelGGL((ctc_lin_kernel<1>), dim3(2 * a.B), dim3(192), 0, st, a); break;
+    case 2: hipLaunchKernelGGL((ctc_lin_kernel<2>), dim3(2 * a.B), dim3(192), 0, st, a); break;
+    case 3: hipLaunchKernelGGL((ctc_lin_kernel<3>), dim3(2 * a.B), dim3(192), 0, st, a); break;
+    case 4: hipLaunchKernelGGL((ctc_lin_kernel<4>), dim3(2 * a.B), dim3(192), 0, st, a); break;
+    default: launch_ab(a, st); break;
+  }
+  // the sequences a lattice flagged (sharp[b]) again, exactly; the others' workgroups exit at
+  // once.  U <= 255 (the pairs fit one wave, 4 per lane); longer targets keep the log-space result
+  switch (x64_ppl(a.Umax)) {
+    case 1: hipLaunchKernelGGL((ctc_x64_kernel<1, DT>), dim3(2 * a.B), dim3(64), 0, st, a); break;
+    case 2: hipLaunchKernelGGL((ctc_x64_kernel<2, DT>), dim3(2 * a.B), dim3(64), 0, st, a); break;
+    case 3: hipLaunchKernelGGL((ctc_x64_kernel<3, DT>), dim3(2 * a.B), dim3(64), 0, st, a); break;
+    case 4: hipLaunchKernelGGL((ctc_x64_kernel<4, DT>), dim3(2 * a.B), dim3(64), 0, st, a); break;
     default: break;
   }
+}
+
+static void launch_ab(const CtcArgs& a, hipStream_t st) {
   const int K = a.kh;
   const int nw = (a.Umax + 1 + (64 - K) - 1) / (64 - K);
   const size_t sh = 2 * (size_t)nw * (64 - K) * sizeof(float2);

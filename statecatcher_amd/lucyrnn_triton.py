@@ -220,8 +220,14 @@ class LucyRNNtriton(nn.Module):
 
         cell_imgs, out_imgs = self._weight_images(x)
         req = getattr(_HEAD, "req", None)
+        op = self.output_proj
         if req is not None and not (out_imgs is not None and out_imgs[1] is not None
-                                    and self.num_tracks == 1):
+                                    and self.num_tracks == 1 and op.bias is not None
+                                    and op.weight.dtype == torch.float32
+                                    and op.bias.dtype == torch.float32
+                                    and self.config.hidden_dim % 4 == 0):
+            # CTCHeadFn's preconditions (ops.ctc_head_supported; sc_ctc_split_rows reads the
+            # weight rows in 4-element pieces): otherwise the projection runs here, unfused
             req = None
         sink = [] if req is not None else None
         track_outputs, final_h, final_s = [], [], []

@@ -94,6 +94,10 @@ def compute_loss(mode: str, criterion: nn.Module, model: nn.Module, feats: torch
             enc_out, output_state = model(feats, masks, input_state)
         if enc_out is DEFERRED_LOGITS:
             x, proj, imgs, wide = head.taken
+            if not ctc_head_supported(x, proj.weight, proj.bias, imgs):
+                enc_out = proj(x.contiguous(), imgs)   # the encoder's own (unfused) projection
+                return criterion.forward_logits(enc_out, tokens, in_lens, tgt_lens), \
+                    output_state, enc_out, output_state
             with torch.autocast("cuda", enabled=False):
                 loss, enc_out = ctc_head_loss(x, proj.weight, proj.bias, imgs, tokens, in_lens,
                                               tgt_lens, blank=criterion.blank, wide=wide)

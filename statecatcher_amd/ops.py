@@ -749,7 +749,13 @@ _SPLIT_W = WeakIdKeyDictionary()
 # "round+exact"): the CTC gradient's sensitivity to the logits is in the lattice's emissions; the
 # other columns enter only through the row's log-sum-exp (a per-frame shift every path shares)
 # and the softmax term, where bf16 rounding is noise-sized.
+# In "emis" the reported loss takes each row's log-sum-exp over the bf16 logits while the
+# emission numerators are the side array's exact values: the loss VALUE differs from an fp32 head
+# by a per-frame offset of bf16-rounding size (the gradient is unaffected: the lse enters it only
+# through the softmax term).
 HEAD_SPLIT = os.environ.get("SC_HEAD_SPLIT", "emis")
+if HEAD_SPLIT not in ("emis", "labels", "full"):
+    raise ValueError(f"SC_HEAD_SPLIT={HEAD_SPLIT!r}: expected 'emis', 'labels' or 'full'")
 
 
 def _emission_logits(wide, w, b, targets, blank, V):
@@ -816,7 +822,9 @@ class CTCHeadFn(torch.autograd.Function):
     cosines from that rounding alone).  Here the projection writes fp32 logits, which the lattice
     reads, and the lattice's gradient is written in bf16 straight into the projection backward's
     operand (a separate fp32 logits tensor would need an fp32 gradient and a cast pass, since
-    autograd casts a gradient to its input's dtype).  The logits output stays differentiable: a
+    autograd casts a gradient to its input's dtype).  Under HEAD_SPLIT "emis" (the default) the
+    returned logits are the bf16 GEMM's, and only the emission columns reach the lattice at fp32
+    accuracy (side array).  The logits output stays differentiable: a
     gradient reaching it from elsewhere is added before the projection backward."""
 
     @staticmethod
@@ -869,7 +877,9 @@ def ctc_head_supported(x, w, b, imgs):
 
 
 def ctc_head_loss(x, w, b, imgs, targets, in_lens, tgt_lens, blank=0, wide=None):
-    """(loss, fp32 logits) of CTCHeadFn: x [B,T,D] bf16 hidden, w [V,D] / b [V] the fp32
+    """(loss, logits) of CTCHeadFn -- logits bf16 under SC_HEAD_SPLIT=emis (the default; the
+    lattice read its emission columns from the fp32 side array), fp32 under 'labels' / 'full'
+    or without `wide`: x [B,T,D] bf16 hidden, w [V,D] / b [V] the fp32
     output_proj parameters, imgs their (W, W^T) bf16 images; wide: the scan's split-precision
     [B,T,3D] buffer whose first D columns are x (LucyCellFn split_sink), or None."""
     dev = x.device
@@ -1245,8 +1255,10 @@ class MLSTMFn(torch.autograd.Function):
     """mLSTM cell (mlstm.hip) over q, k [B,NH,T,DQ], v [B,NH,T,DV], gate pre-activations
     [B,NH,T]; returns h [B,NH,T,DV] and the final state (C [B,NH,DQ,DV], n [B,NH,DQ],
     m [B,NH,1]) like transformers' mlstm_chunkwise_native_autograd(return_last_states=True).
-    Compute dtype bf16/f16 (fp32 inputs are rounded to bf16, as the reference's kernels run
-    under autocast_kernel_dtype); fp32 state."""
+    Compute dtype bf16/f16; fp32 inputs are rounded to f16, the finer of the two compiled cells
+    (11-bit mantissa; the f16 backward scales its gradients per chunk, so dh below f16's normal
+    range is not lost) -- the reference's kernels run under autocast_kernel_dtype = float16
+    (model.py:227).  fp32 state."""
 
     @staticmethod
     def forward(ctx, q, k, v, igate, fgate, c0, n0, m0, eps):
@@ -1254,7 +1266,7 @@ class MLSTMFn(torch.autograd.Function):
         ctx.set_materialize_grads(False)   # detached carried states: no zero-filled gradients
         B, NH, T, DQ = q.shape
         DV = v.shape[-1]
-        cdt = q.dtype if q.dtype in (torch.bfloat16, torch.float16) else torch.bfloat16
+        cdt = q.dtype if q.dtype in (torch.bfloat16, torch.float16) else torch.float16
         lib = _lib.load()
         if not lib.sc_mlstm_supported(dtype_code(torch.empty(0, dtype=cdt)), DQ, DV):
             raise ValueError(f"mLSTM head dims (DQ={DQ}, DV={DV}) not compiled in")

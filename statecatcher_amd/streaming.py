@@ -80,12 +80,14 @@ class StreamingLucyRNN:
                 e["w_h"], e["b_h"] = w(cell.W_h.weight), w(cell.W_h.bias)
             self.layers.append(e)
         self.w_out, self.b_out = w(model.output_proj.weight), w(model.output_proj.bias)
-        frame_ok = (D % 16 == 0 and self.Din % 8 == 0 and dtype in (torch.float32, torch.bfloat16))
+        # sc_lucy_frame_gemm keeps a workgroup's A rows in LDS: K <= 2048 (D and Din)
+        frame_ok = (D % 16 == 0 and self.Din % 8 == 0 and D <= 2048 and self.Din <= 2048
+                    and dtype in (torch.float32, torch.bfloat16))
         if engine == "auto":
             engine = "frame" if frame_ok else "library"
         if engine == "frame" and not frame_ok:
-            raise ValueError("engine='frame' needs hidden_dim % 16 == 0, input width % 8 == 0 and "
-                             "fp32 / bf16 weights")
+            raise ValueError("engine='frame' needs hidden_dim % 16 == 0, input width % 8 == 0, "
+                             "both <= 2048, and fp32 / bf16 weights")
         self.engine = engine
         z = lambda *s, dt=dtype: torch.zeros(*s, dtype=dt, device=dev)   # noqa: E731
         if engine == "frame":

@@ -217,8 +217,10 @@ class mLSTMLayer(nn.Module):
             q, k, v, o, ig, fg = self.projections(x)
         # under autocast the cell runs in autocast_kernel_dtype (the reference passes float16,
         # model.py:227): q, k, v are cast to it as the xlstm fork's kernels cast their inputs.
-        # Without autocast the dtype is the activations' own, as transformers' native chunkwise
-        # cell (modeling_xlstm.py:323) ignores autocast_kernel_dtype
+        # Without autocast the activations' own dtype goes to the cell, as transformers' native
+        # chunkwise cell (modeling_xlstm.py:323) ignores autocast_kernel_dtype; there is no fp32
+        # HIP cell, so MLSTMFn computes fp32 activations in f16 (11-bit mantissa, the finer of
+        # the compiled cells) whatever autocast_kernel_dtype says
         cell_dt = (kdt if x.is_cuda and torch.is_autocast_enabled("cuda")
                    and kdt in (torch.bfloat16, torch.float16) else q.dtype)
         q = q.reshape(B, T, NH, -1).transpose(1, 2).to(cell_dt)

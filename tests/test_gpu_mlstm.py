@@ -69,6 +69,40 @@ def test_mlstm_fp32_reference_fixture_at_bf16_tolerance():
     close(h, z["c4/h"], 3e-2)
 
 
+def test_mlstm_fp32_inputs_run_the_f16_cell():
+    """fp32 q / k / v (an fp32 xLSTM without autocast) go through the f16 cell, the finer of the
+    two compiled cells: bitwise the explicit f16 call, and against fp64 on the
+    UNROUNDED inputs closer than the bf16 cell gets (f16 rounding is 8x finer)."""
+    from tests.torch_ref import mlstm64
+    z = load_golden("mlstm")
+    ins = [torch.as_tensor(z[f"c4/{k}"]) for k in ("q", "k", "v", "igate", "fgate")]
+    R = torch.as_tensor(z["c4/R"]) if "c4/R" in z.files else torch.randn_like(ins[2])
+    errs = {}
+    for dt in (torch.float32, torch.float16, torch.bfloat16):
+        leaves = [t.to(DEV).to(dt if i < 3 else torch.float32).requires_grad_(True)
+                  for i, t in enumerate(ins)]
+        h = ops().mlstm_chunkwise(*leaves)
+        (h.float() * R.to(DEV)).sum().backward()
+        errs[dt] = (h.detach().float(), [t.grad.float() for t in leaves])
+    assert torch.equal(errs[torch.float32][0], errs[torch.float16][0])
+    for a, b in zip(errs[torch.float32][1], errs[torch.float16][1]):
+        torch.testing.assert_close(a, b, rtol=1e-3, atol=1e-6)   # fp32 vs f16 gradient casts only
+    ref = [t.double().requires_grad_(True) for t in ins]
+    rh, _ = mlstm64(*ref)
+    (rh * R.double()).sum().backward()
+
+    def rel(a, b):
+        return float((a.double().cpu() - b).norm() / b.norm())
+    e32 = [rel(errs[torch.float32][0], rh.detach())] + \
+        [rel(g, r.grad) for g, r in zip(errs[torch.float32][1], ref)]
+    ebf = [rel(errs[torch.bfloat16][0], rh.detach())] + \
+        [rel(g, r.grad) for g, r in zip(errs[torch.bfloat16][1], ref)]
+    print("fp32-input (f16 cell) vs fp64:", [f"{e:.2e}" for e in e32],
+          "bf16 cell:", [f"{e:.2e}" for e in ebf])
+    assert e32[0] <= 5e-3 and max(e32) <= 2e-2, e32
+    assert e32[0] < ebf[0] and e32[1] < ebf[1], (e32, ebf)
+
+
 def test_mlstm_long_sequence_vs_oracle_and_state_carry():
     """T = 1536 (the C4 segment after padding to 64): h and final state vs the numpy step
     recurrence; two carried halves equal one pass."""

@@ -37,13 +37,36 @@ def ref(x, labels, fl, ll, logits, reduction="mean", average_frames=False):
     return loss, costs, g
 
 
-# one-wave lattice with 1, 2, 3, 4 label positions per lane (U + 1 <= 64, 128, 192, 256), then the
-# multi-wave one (last: 15 waves, K = 8)
-@pytest.mark.parametrize("B,T,U,V", [(3, 7, 4, 11), (2, 1, 3, 5), (2, 9, 0, 6), (4, 40, 12, 33),
-                                     (2, 130, 70, 17), (2, 60, 150, 9), (2, 30, 220, 7),
-                                     (2, 24, 800, 5)])
+# U + 1 <= 64, 128, 192, 256 (the opt-in one-wave lattice's 1, 2, 3, 4 label positions per lane
+# when SC_RNNT_AB1=1), then the multi-wave one's largest case (15 waves, K = 8)
+DENSE_CASES = [(3, 7, 4, 11), (2, 1, 3, 5), (2, 9, 0, 6), (4, 40, 12, 33), (2, 130, 70, 17),
+               (2, 60, 150, 9), (2, 30, 220, 7), (2, 24, 800, 5)]
+
+
+@pytest.mark.parametrize("B,T,U,V", DENSE_CASES)
 @pytest.mark.parametrize("logits", [True, False])
 def test_rnnt_dense_vs_oracle(B, T, U, V, logits):
+    _dense_check(B, T, U, V, logits)
+
+
+def test_rnnt_one_wave_lattice_vs_oracle():
+    """The opt-in one-wave lattice (rnnt_ab1_kernel, SC_RNNT_AB1=1, read once per process, so it
+    runs in a child process): every DENSE_CASES lattice with U + 1 <= 256 takes it (1 .. 4
+    label positions per lane, its kh = kAb1R / 2 offset indexing and terminal blank), the last
+    one falls back to the multi-wave kernel; nll, costs and gradients vs the oracle as above."""
+    import os
+    import subprocess
+    import sys
+    code = ("import sys; sys.path.insert(0, '.'); from tests.test_gpu_rnnt import DENSE_CASES, "
+            "_dense_check\nfor c in DENSE_CASES:\n  for lg in (True, False): _dense_check(*c, lg)\n"
+            "print('ONE-WAVE OK')")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, "-c", code], cwd=root, env=dict(os.environ, SC_RNNT_AB1="1"),
+                       capture_output=True, text=True, timeout=110)
+    assert p.returncode == 0 and "ONE-WAVE OK" in p.stdout, p.stderr[-3000:]
+
+
+def _dense_check(B, T, U, V, logits):
     x, labels, fl, ll = make(B, T, U, V, seed=B * 100 + T + U)
     if not logits:
         x = x - np.log(np.exp(x).sum(-1, keepdims=True))

@@ -4,12 +4,14 @@ The reference computes RNNTPredictorJoiner (model.py:129-145) -> (B, T, U+1, V) 
 log_softmax in fp32 (model.py:93) -> warp_rnnt (gather=True).  The fused kernels never build the
 logits; W and z = tanh(enc + pred) enter the MFMA in bf16 with fp32 accumulation.
 
-* Small lattices against an fp64 CPU restatement with the SAME bf16 rounding of W and z
-  (oracle/rnnt.py lattice, pinned by brute-force alignment sums): nll to 1e-4 relative; the
-  gradients of enc_proj / pred_proj outputs, W and bias to 1e-2 in norm (the backward's dlogits
-  also enter its MFMAs in bf16).
+* Small lattices against an fp64 CPU restatement with the SAME bf16 roundings as the kernels --
+  W and z, and the dlogits that enter the backward's dW / dZ MFMAs (oracle/rnnt.py lattice,
+  pinned by brute-force alignment sums): nll to 1e-4 relative, the gradients of enc_proj /
+  pred_proj outputs, W and bias to 1e-3 in norm (north_star); against fp64 without the dlogits
+  rounding to 5e-3 (that rounding's own size).
 * A C5-sized lattice (T=1500, U=150, V=1024, B=2) against the unfused HIP path on materialised
-  logits (the validated sc_rnnt_* kernels): nll 1e-3, gradients 2e-2 in norm; deterministic.
+  fp32 logits (the validated sc_rnnt_* kernels) with the same roundings: nll 1e-4, gradients
+  1e-3 in norm; deterministic.
 * compute_loss(mode="rnnt") with RNNTLoss runs the fused path for both joiners, DDP-safe
   (through the joiner's forward), and equals the materialised path.
 """
@@ -28,8 +30,23 @@ def sc():
     return s
 
 
-def ref_fp64(enc_p, pred_p, W, bias, labels, fl, ll, blank):
-    """nll and gradients (enc_p, pred_p, W, bias) in fp64 with the kernels' bf16 roundings."""
+class _Bf16Grad(torch.autograd.Function):
+    """Identity forward; the backward rounds the incoming gradient to bf16 (RNE) and hands it on
+    in the input's dtype: the joiner backward's dlogits p enter its dW and dZ MFMAs as bf16
+    (rnnt.hip joint_bwd_kernel: pack8(p) is the A operand of both), while d bias sums the fp32 p."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.to(torch.bfloat16).to(g.dtype)
+
+
+def ref_fp64(enc_p, pred_p, W, bias, labels, fl, ll, blank, round_p=False):
+    """nll and gradients (enc_p, pred_p, W, bias) in fp64 with the kernels' bf16 roundings of W
+    and z; round_p: also the bf16 rounding of the dlogits that feed dW / dZ (d bias unrounded)."""
     e = enc_p.double().cpu().requires_grad_(True)
     p = pred_p.double().cpu().requires_grad_(True)
     w = W.double().cpu().requires_grad_(True)
@@ -37,7 +54,8 @@ def ref_fp64(enc_p, pred_p, W, bias, labels, fl, ll, blank):
     z = torch.tanh(e.unsqueeze(2) + p.unsqueeze(1))
     zq = z + (z.to(torch.bfloat16).double() - z).detach()          # bf16 value, identity grad
     wq = w + (w.to(torch.bfloat16).double() - w).detach()
-    logits = zq @ wq.t() + b
+    mm = zq @ wq.t()
+    logits = (_Bf16Grad.apply(mm) if round_p else mm) + b
     lp = logits.log_softmax(-1)
     nll = []
     glp = torch.zeros_like(lp)
@@ -87,14 +105,20 @@ def test_fused_joint_vs_fp64(B, T, Umax, V, Tb, Ub):
     bias = bias.detach().requires_grad_(True)
     nll = sc().ops.RNNTJointFn.apply(enc_p, pred_p, W, bias, labels.to(DEV), fl.to(DEV), ll.to(DEV), 0)
     nll.mean().backward()
-    rn, ge, gp, gw, gb = ref_fp64(enc_p.detach(), pred_p.detach(), W.detach(), bias.detach(), labels,
-                                  fl, ll, 0)
+    args = (enc_p.detach(), pred_p.detach(), W.detach(), bias.detach(), labels, fl, ll, 0)
+    rn, *plain = ref_fp64(*args)
+    _, *rounded = ref_fp64(*args, round_p=True)
     np.testing.assert_allclose(nll.detach().cpu().numpy(), rn, rtol=1e-4)
-    for got, ref, name in [(enc_p.grad, ge, "enc"), (pred_p.grad, gp, "pred"), (W.grad, gw, "W"),
-                           (bias.grad, gb, "bias")]:
+    for got, ref, refq, name in zip([enc_p.grad, pred_p.grad, W.grad, bias.grad], plain, rounded,
+                                    ["enc", "pred", "W", "bias"]):
         assert torch.isfinite(got).all(), name
-        print(f"fused joint B={B} T={T} U={Umax} V={V} {name}: rel {rel(got, ref):.2e}")
-        assert rel(got, ref) < 1e-2, (name, rel(got, ref))
+        print(f"fused joint B={B} T={T} U={Umax} V={V} {name}: rel {rel(got, refq):.2e} vs fp64 "
+              f"with the kernel's roundings (plain fp64 with W / z rounded: {rel(got, ref):.2e})")
+        # north_star's 1e-3 against the reference that models every bf16 rounding the kernels
+        # make; against fp64 without the dlogits rounding the gap is that rounding itself (p sums
+        # to ~0 over the vocabulary, so dZ = p W cancels and magnifies it): measured <= 1.8e-3
+        assert rel(got, refq) <= 1e-3, (name, rel(got, refq))
+        assert rel(got, ref) <= 5e-3, (name, rel(got, ref))
 
 
 def test_fused_joint_zero_frames_is_inf():
@@ -125,19 +149,20 @@ def test_fused_joint_c5_size_vs_materialised_path():
     for x, y in zip(*outs):
         assert torch.equal(x, y)   # deterministic: fixed-order partial sums, no atomics
     assert all(torch.isfinite(t).all() for t in outs[0])
-    # materialised path, same roundings
+    # materialised path (fp32 logits, the validated sc_rnnt_* lattice) with the same roundings:
+    # bf16 z and W, and the dlogits rounded to bf16 before the dW / dZ products (_Bf16Grad)
     e, p, w, b = (t.clone().requires_grad_(True) for t in (enc_p, pred_p, W, bias))
     z = torch.tanh(e.unsqueeze(2) + p.unsqueeze(1))
     zq = z + (z.to(torch.bfloat16).float() - z).detach()
     wq = w + (w.to(torch.bfloat16).float() - w).detach()
-    logits = zq @ wq.t() + b
+    logits = _Bf16Grad.apply(zq @ wq.t()) + b
     nll_u = sc().rnnt_loss(logits, labels, fl, ll, reduction="none", is_logits=True)
     nll_u.mean().backward()
-    np.testing.assert_allclose(outs[0][0].cpu().numpy(), nll_u.detach().cpu().numpy(), rtol=1e-3)
+    np.testing.assert_allclose(outs[0][0].cpu().numpy(), nll_u.detach().cpu().numpy(), rtol=1e-4)
     for got, ref, name in zip(outs[0][1:], [e.grad, p.grad, w.grad, b.grad], ["enc", "pred", "W", "bias"]):
         r = rel(got, ref)
         print(f"C5 lattice {name}: rel {r:.2e}")
-        assert r < 2e-2, (name, r)
+        assert r <= 1e-3, (name, r)
 
 
 def _count_fused(monkeypatch):
