@@ -70,6 +70,12 @@ def parse():
     ap.add_argument("--op-probe", action="store_true",
                     help="diagnostics on stderr: every ATen op one step dispatches (count, shapes, "
                          "caller), to find the step's non-HIP kernels")
+    ap.add_argument("--rccl-footprint", default=None, metavar="WGS[:SLEEP]",
+                    help="diagnostic (1 GPU): mimic a DP all-reduce's footprint -- during the "
+                         "backward, as each large gradient is produced, WGS persistent workgroups "
+                         "on a side stream copy 2 (8 - 1) / 8 of its bytes (an 8-GPU ring's share), "
+                         "paced by SLEEP; the optimizer step waits for them, as DDP's does "
+                         "(tools/footprint.hip, built by tools/footprint.sh)")
     ap.add_argument("--tune-out", default=None,
                     help="rank 0 tunes GEMM shapes missing from the table and writes it here")
     ap.add_argument("--retune", action="store_true",
@@ -179,6 +185,40 @@ def build_workload(args, device):
             if split else "bf16 operands and logits")
     return model, CTCLoss(blank=0, zero_infinity=True, fused_head=split), list(model.parameters()), \
         dict(mode="ctc"), conf
+
+
+def footprint_hooks(model, spec, device):
+    """bench --rccl-footprint: per large gradient, a side-stream copy of 2 (N - 1) / N of its
+    bytes at N = 8 by `wgs` workgroups (RCCL's ring kernels hold a few dozen CUs for the whole
+    all-reduce); the main stream waits for the side stream once the last gradient is in (DDP's
+    wait before the optimizer step).  Returns the side stream."""
+    import ctypes
+    lib = ctypes.CDLL(os.path.join(ROOT, "tools", "ab", "footprint", "libfootprint.so"))
+    lib.sc_probe_footprint.restype = ctypes.c_int
+    lib.sc_probe_footprint.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                       ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    wgs, _, sleep = spec.partition(":")
+    wgs, sleep = int(wgs), int(sleep or 0)
+    big = [p for p in model.parameters() if p.numel() >= 1 << 20]
+    nbytes = max(p.numel() for p in big) * 4 * 2
+    src = torch.empty(nbytes // 4, device=device)
+    dst = torch.empty_like(src)
+    side = torch.cuda.Stream(device)
+
+    def launch(p):
+        b = int(2 * 7 / 8 * p.numel() * 4) // 16 * 16
+        side.wait_stream(torch.cuda.current_stream(device))
+        rc = lib.sc_probe_footprint(src.data_ptr(), dst.data_ptr(), b, wgs, sleep,
+                                    ctypes.c_void_p(side.cuda_stream))
+        assert rc == 0, rc
+
+    for p in big:
+        p.register_post_accumulate_grad_hook(launch)
+    # the input projection's weight gradient is the backward's last large one
+    last = model.encoder.tracks[0][0].linear.weight if hasattr(model.encoder, "tracks") else big[0]
+    last.register_post_accumulate_grad_hook(
+        lambda p: torch.cuda.current_stream(device).wait_stream(side))
+    return side
 
 
 def cpu_quota():
@@ -409,6 +449,8 @@ def main():
     trainer = SegmentTrainer(model, criterion, opt, accumulation_steps=1, max_grad_norm=50.0,
                              amp_dtype=amp, bucket_cap_mb=args.bucket_mb, **tkw)
     segs = synth_segments(args, rank, device)
+    if args.rccl_footprint:
+        footprint_hooks(model, args.rccl_footprint, device)
 
     def step():
         i = trainer.global_step
@@ -476,10 +518,14 @@ def main():
                                   "frac_of_peak": round(nbytes / avg / 1e9 / PEAK_HBM_GBS, 4)})
     scans = [k for k in kernels if k.startswith("lucy_scan") or k.startswith("mlstm")]
     dom = max(scans, key=lambda k: kstats[k][0]) if scans else None
+    # PMC-measured HBM bytes per launch of that kernel, from the rocprofv3 passes of a bench run
+    # of THIS workload and dtype (tools/pmc_traffic.py keys them "<workload>/<dtype>"); null when
+    # no such pass was taken
     traffic = None
     pmc_file = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    pmc_key = f"{args.workload}/{'bf16' if args.dtype == 'bf16' else 'fp32'}"
     if dom and os.path.exists(pmc_file):
-        traffic = json.load(open(pmc_file)).get(dom, {}).get("hbm_bytes_per_launch")
+        traffic = json.load(open(pmc_file)).get(pmc_key, {}).get(dom, {}).get("hbm_bytes_per_launch")
     roofline = None
     if dom:
         kd = kernels[dom]

@@ -18,6 +18,8 @@
  *                        lucyrnn.py:147-151; generalised with an optional initial state
  *   sc_decay_scan_bwd <- (absent) adjoint of the above
  *   sc_layernorm_*    <- nn.LayerNorm between layers, lucyrnn_triton.py:96-97, :136-137
+ *   sc_ln_fold_*, sc_lucy_scan_*_ln <- the same LayerNorm folded into the next layer's gate
+ *                        projection (LN(h) W^T + b = rstd (h W''^T - mean r) + b')
  *   sc_ctc_*          <- ATen ctc_loss behind nn.CTCLoss(blank=0, zero_infinity=True),
  *                        train.py:142 / model.py:68-71
  *   sc_ctc_greedy_decode <- decoder.py:3-30 `ctc_greedy_decoder`
@@ -112,6 +114,30 @@ int sc_lucy_scan_fwd_split(const void* gates, int gates_dtype, const float* gate
                            float* ckpt, void* stream);
 
 /*
+ * sc_lucy_scan_fwd(_split) with the inter-layer LayerNorm (lucyrnn_triton.py:96-97, :136-137)
+ * folded in.  16-bit gates, 16-byte pieces, D = 512 or 1024.  out_dup / out_lo: NULL, or the
+ * split planes of sc_lucy_scan_fwd_split.
+ *   ln_r       NULL, or fp32 [7,D]: this layer's gates are u = h W''^T of the RAW previous output h
+ *              (W'' the bf16 image of sc_weight_images with col_scale = gamma, row_shift = the
+ *              sc_ln_fold_prep shift) and r its row sums (sc_ln_fold_prep rowsum); each gate is
+ *              rebuilt on load as rstd (u - mean r) + gate_bias, gate_bias = b' (sc_ln_fold_prep
+ *              bias_out), which equals LN(h) W^T + b
+ *   ln_rec_in  with ln_r: fp32 [B][T][D/64][2], (mean, M2) of h's 64-unit blocks (the previous
+ *              layer's ln_rec_out); combined per row with Chan's formula, eps ln_eps
+ *   ln_stat    NULL, or fp32 [B][T][2] out: the rows' (rstd, mean) (what sc_lucy_scan_bwd_ln and
+ *              sc_ln_fold_bwd read)
+ *   ln_rec_out NULL, or fp32 [B][T][D/64][2] out: (mean, M2) of this layer's 16-bit output
+ *              values per 64-unit block, for the next layer's fold
+ */
+int sc_lucy_scan_fwd_ln(const void* gates, int gates_dtype, const float* gate_bias,
+                        const float* h0, const float* s0, void* out, void* out_dup, void* out_lo,
+                        float* s_out, float* h_out, int B, int T, int D,
+                        int64_t stride_g_bt, int64_t stride_g_td, int64_t stride_g_cd,
+                        int64_t stride_g_cb, int64_t stride_o_bt, int64_t stride_o_bd,
+                        float* ckpt, const float* ln_r, const float* ln_rec_in, float* ln_stat,
+                        float* ln_rec_out, float ln_eps, void* stream);
+
+/*
  * Backward scan.  Inputs: the forward's gates and ckpt, dout = dL/d out (same dtype as gates,
  * strides stride_d_bt/stride_d_bd), ds_last = dL/d s_out (fp32 [B,D], may be NULL = zero).
  * Outputs: dgates (gates_dtype, laid out like gates with strides stride_dg_*), dh0, ds0 (fp32
@@ -126,6 +152,21 @@ int sc_lucy_scan_bwd(const void* gates, int gates_dtype, const float* gate_bias,
                      int64_t stride_g_cb, int64_t stride_d_bt, int64_t stride_d_bd,
                      int64_t stride_dg_bt, int64_t stride_dg_td, int64_t stride_dg_cd,
                      int64_t stride_dg_cb, void* stream);
+
+/*
+ * Backward of sc_lucy_scan_fwd_ln's fold (16-bit, D = 512 or 1024, 16-byte aligned gates / dout /
+ * dgates): the gates are rebuilt from ln_r, gate_bias and the forward's ln_stat; dgates =
+ * dL/du = rstd dL/dgate (the input and weight gradients of u = h W''^T consume it); dbias keeps
+ * dL/dgate (the gradient of b').
+ */
+int sc_lucy_scan_bwd_ln(const void* gates, int gates_dtype, const float* gate_bias,
+                        const float* ckpt, const void* dout, const float* ds_last, void* dgates,
+                        float* dh0, float* ds0, float* dbias, int B, int T, int D,
+                        int64_t stride_g_bt, int64_t stride_g_td, int64_t stride_g_cd,
+                        int64_t stride_g_cb, int64_t stride_d_bt, int64_t stride_d_bd,
+                        int64_t stride_dg_bt, int64_t stride_dg_td, int64_t stride_dg_cd,
+                        int64_t stride_dg_cb, const float* ln_r, const float* ln_stat,
+                        void* stream);
 
 /* ---------------------------------------------------------------- decay scan ------------ */
 
@@ -170,6 +211,47 @@ int64_t sc_layernorm_bwd_workspace_numel(int64_t rows, int D);
 int sc_layernorm_bwd(const void* x, const void* dy, int dtype, const float* gamma,
                      const float* mean, const float* rstd, void* dx, float* dgamma_dbeta,
                      float* workspace, int64_t rows, int D, void* stream);
+
+/*
+ * The LayerNorm fold around the scans (see sc_lucy_scan_fwd_ln).  Per job (one gate projection
+ * W fp32 [rows = 7D][ld], the preceding LayerNorm's gamma / beta [D], the projection bias [rows]
+ * or NULL), in one launch for up to 16 jobs:
+ *   shift[n] = mean_k gamma_k W_nk   (row_shift of the W'' image; W''_nk = bf16(gamma_k W_nk -
+ *                                     shift_n), computed unfused, as sc_weight_images computes it)
+ *   bias_out[n] = b_n + sum_k W_nk beta_k
+ *   rowsum[n] = sum_k W''_nk
+ */
+typedef struct {
+  const float* w;
+  const float* gamma;
+  const float* beta;
+  const float* bias;
+  float* shift;
+  float* bias_out;
+  float* rowsum;
+  int64_t ld, rows, D;
+} sc_ln_fold_job;
+int sc_ln_fold_prep(const sc_ln_fold_job* jobs, int njobs, void* stream);
+
+/*
+ * dL/dh [rows][D] bf16 of the LayerNorm input h from g = dL/du W'' (the gate projection's input
+ * gradient with the scan's rstd-scaled dgates) and the forward's stat [rows][2] (rstd, mean):
+ * dh = g - mean(g) - xhat mean(xhat g), xhat = (h - mean) rstd.  D = 512 or 1024.
+ */
+int sc_ln_fold_bwd(const void* g, const void* h, int dtype, const float* stat, void* dh,
+                   int64_t rows, int D, void* stream);
+
+/* fp32 workspace floats of sc_ln_fold_wgrad. */
+int64_t sc_ln_fold_wgrad_workspace_numel(int rows, int D);
+
+/*
+ * From M = dL/dW'' fp32 [rows][D] (reference row order) and dL/db' fp32 [rows]:
+ * dw [rows][D] = gamma (M - rowmean M) + dL/db' beta^T  (dL/dW), and dgamma_dbeta fp32 [2][D] =
+ * (sum_n W (M - rowmean M), sum_n W dL/db') in a fixed order.  (dL/db = dL/db'.)
+ */
+int sc_ln_fold_wgrad(const float* M, const float* w, int64_t ld, const float* gamma,
+                     const float* beta, const float* dbias, int rows, int D, float* dw,
+                     float* dgamma_dbeta, float* workspace, void* stream);
 
 /* ---------------------------------------------------------------- CTC ------------------- */
 
@@ -403,12 +485,17 @@ int sc_adam_step(const sc_adam_tensor* t, int nt, const float* part, int64_t npa
  * zero columns cols..cols_pad-1, rows in step-blocked order (block, gate, unit) when block_d = D
  * > 0 (rows = 7 D, D % 64 == 0; dst row (b, g, u) = src row g D + 64 b + u); dst_t (optional)
  * bf16 [cols][rows] = dst's first cols columns transposed.  Round to nearest even.
+ * col_scale [cols] / row_shift [rows] (either may be NULL): the imaged value is
+ * col_scale[c] * src - row_shift[source row], computed unfused (the folded LayerNorm's W'',
+ * sc_ln_fold_prep).
  */
 typedef struct {
   const float* src;
   void* dst;
   void* dst_t;
   int64_t rows, cols, cols_pad, ld_src, block_d;
+  const float* col_scale;
+  const float* row_shift;
 } sc_image_job;
 int sc_weight_images(const sc_image_job* jobs, int njobs, void* stream);
 

@@ -18,7 +18,7 @@ _DTYPE = {torch.float32: SC_F32, torch.bfloat16: SC_BF16, torch.float16: SC_F16}
 
 _c = ctypes
 _i32, _i64, _vp, _fp = _c.c_int, _c.c_int64, _c.c_void_p, _c.c_void_p
-ABI_VERSION = 11  # include/statecatcher.h; bumped on any signature change
+ABI_VERSION = 12  # include/statecatcher.h; bumped on any signature change
 
 _SIGS = {
     "sc_abi_version": (_i32, []),
@@ -35,6 +35,16 @@ _SIGS = {
     "sc_lucy_scan_bwd": (_i32, [_vp, _i32, _fp, _fp, _vp, _fp, _vp, _fp, _fp, _fp, _i32, _i32, _i32,
                                _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64,
                                _vp]),
+    "sc_lucy_scan_fwd_ln": (_i32, [_vp, _i32, _fp, _fp, _fp, _vp, _vp, _vp, _fp, _fp, _i32, _i32,
+                                  _i32, _i64, _i64, _i64, _i64, _i64, _i64, _fp, _fp, _fp, _fp, _fp,
+                                  _c.c_float, _vp]),
+    "sc_lucy_scan_bwd_ln": (_i32, [_vp, _i32, _fp, _fp, _vp, _fp, _vp, _fp, _fp, _fp, _i32, _i32,
+                                  _i32, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64,
+                                  _fp, _fp, _vp]),
+    "sc_ln_fold_prep": (_i32, [_vp, _i32, _vp]),
+    "sc_ln_fold_bwd": (_i32, [_vp, _vp, _i32, _fp, _vp, _i64, _i32, _vp]),
+    "sc_ln_fold_wgrad_workspace_numel": (_i64, [_i32, _i32]),
+    "sc_ln_fold_wgrad": (_i32, [_fp, _fp, _i64, _fp, _fp, _fp, _i32, _i32, _fp, _fp, _fp, _vp]),
     "sc_decay_scan_fwd": (_i32, [_vp, _vp, _vp, _i32, _fp, _i32, _i32, _i32, _i64, _i64, _i64, _vp]),
     "sc_decay_scan_bwd": (_i32, [_vp, _vp, _vp, _vp, _vp, _i32, _fp, _fp, _i32, _i32, _i32,
                                 _i64, _i64, _i64, _vp]),
@@ -127,7 +137,14 @@ class AdamTensor(ctypes.Structure):
 class ImageJob(ctypes.Structure):
     """sc_image_job (include/statecatcher.h)."""
     _fields_ = [("src", _vp), ("dst", _vp), ("dst_t", _vp), ("rows", _i64), ("cols", _i64),
-                ("cols_pad", _i64), ("ld_src", _i64), ("block_d", _i64)]
+                ("cols_pad", _i64), ("ld_src", _i64), ("block_d", _i64), ("col_scale", _vp),
+                ("row_shift", _vp)]
+
+
+class LnFoldJob(ctypes.Structure):
+    """sc_ln_fold_job (include/statecatcher.h)."""
+    _fields_ = [("w", _vp), ("gamma", _vp), ("beta", _vp), ("bias", _vp), ("shift", _vp),
+                ("bias_out", _vp), ("rowsum", _vp), ("ld", _i64), ("rows", _i64), ("D", _i64)]
 
 _LIB = None
 

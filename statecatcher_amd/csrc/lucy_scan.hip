@@ -90,6 +90,18 @@ struct ScanFwdArgs {
   // is one bf16 GEMM with the error of an fp32 one (sc_lucy_scan_fwd_split)
   void* out_dup;
   void* out_lo;
+  // the inter-layer LayerNorm folded into the projection (sc_lucy_scan_fwd_ln; D % 64 == 0):
+  //   ln_r    [7,D] fp32 row sums of the bf16 folded weight W'' (NULL: no fold).  The gates the
+  //           GEMM wrote are u = h W''^T of the RAW previous output h; on load they become
+  //           rstd (u - mean r) + b' (b' = gate_bias), i.e. exactly LN(h) W^T + b
+  //   rec_in  [B][T][D/64] (mean, M2) records of h's 64-unit blocks (the previous scan's rec_out)
+  //   ln_stat [B][T] (rstd, mean) out: the combined statistics (block 0 writes them; NULL: none)
+  //   rec_out [B][T][D/64] (mean, M2) records of THIS output's 16-bit values (NULL: none)
+  const float* ln_r;
+  const float2* rec_in;
+  float2* ln_stat;
+  float2* rec_out;
+  float ln_eps;
 };
 
 struct ScanBwdArgs {
@@ -104,6 +116,11 @@ struct ScanBwdArgs {
   float* dbias;   // optional [B,7,D]: sum over t of dgates (gate-projection bias gradient part)
   int B, T, D, nsc;
   int64_t g_bt, g_td, g_cd, g_cb, d_bt, d_bd, dg_bt, dg_td, dg_cd, dg_cb;
+  // the folded LayerNorm (sc_lucy_scan_bwd_ln): gates rebuilt as in the forward from ln_r and
+  // the forward's ln_stat [B][T] (rstd, mean); the stored dgates are d gates / d u = rstd dL/dg
+  // (what the projection's input and weight gradients consume); dbias stays dL/dg
+  const float* ln_r;
+  const float2* ln_stat;
 };
 
 // LDS-DMA piece geometry: a 64-unit row of T elements is PPR pieces of PW bytes.  A partial
@@ -331,8 +348,23 @@ __device__ __forceinline__ float compose_prefix_sw(const float2 (*agg)[64], int 
 }
 
 // ------------------------------------------------------------------------ forward ----------
-// FD: LDS slots per wave (fetch depth), ring by super-chunk index.
-template <int DT, int NW, int LC, int PW, int FD, bool SPLIT = false>
+// Reductions over aligned groups of N lanes (N = 2, 4, 8, 16) through DPP: every lane of a group
+// ends with the group's sum.
+template <int N>
+__device__ __forceinline__ float group_sum_dpp(float x) {
+  static_assert(N == 2 || N == 4 || N == 8 || N == 16, "group of 2..16 lanes");
+  x = dpp_step<0xB1, 0xf, false>(x);                       // quad_perm [1,0,3,2]
+  if constexpr (N >= 4) x = dpp_step<0x4E, 0xf, false>(x);   // quad_perm [2,3,0,1]
+  if constexpr (N >= 8) x = dpp_step<0x141, 0xf, false>(x);  // row_half_mirror
+  if constexpr (N >= 16) x = dpp_step<0x140, 0xf, false>(x);  // row_mirror
+  return x;
+}
+
+// FD: LDS slots per wave (fetch depth), ring by super-chunk index.  LN (the folded inter-layer
+// LayerNorm, ScanFwdArgs::ln_r): bit 1 = this layer's gates are u = h W''^T of the previous raw
+// output (combine its block records, rebuild the gates on load); bit 2 = write this output's
+// block records.  NB = D / 64 column blocks per row (LN only).
+template <int DT, int NW, int LC, int PW, int FD, bool SPLIT = false, int LN = 0, int NB = 8>
 __global__ void __launch_bounds__(NW * 64)
 lucy_scan_fwd_kernel(ScanFwdArgs a) {
   static_assert(NW * LC == kChunk, "super-chunk must be 64 steps");
@@ -356,6 +388,11 @@ lucy_scan_fwd_kernel(ScanFwdArgs a) {
   __shared__ float2 aggH[NW][64];
   __shared__ float carS[2][64];
   __shared__ float carH[2][64];
+  // (LN & 1) the input's block records of the wave's LC steps, [step][block], by LDS-DMA with
+  // the gates (16-byte pieces of two blocks of one step)
+  constexpr int RECN = (LN & 1) ? LC * NB : 2;
+  static_assert(!(LN & 1) || (RECN <= 64 && NB % 2 == 0), "LN fold: LC * NB <= 64, NB even");
+  __shared__ __attribute__((aligned(16))) float2 recS[(LN & 1) ? FD : 1][(LN & 1) ? NW : 1][RECN];
   using L = LdsElem<T, PW>;
   constexpr int SLOTB = ROWS * 64 * L::BYTES;                       // wave-private [LC][7][64]
   const unsigned char* slots = dyn_lds + w * FD * SLOTB;            // FD of them
@@ -371,13 +408,31 @@ lucy_scan_fwd_kernel(ScanFwdArgs a) {
     carS[0][lane] = dok ? a.s0[(int64_t)b * a.D + d] : 0.0f;
     carH[0][lane] = dok ? a.h0[(int64_t)b * a.D + d] : 0.0f;
   }
-  float gb[7];
+  float gb[7], fr[7];
 #pragma unroll
-  for (int g = 0; g < 7; ++g) gb[g] = a.bias ? a.bias[g * a.D + dc] : 0.0f;
+  for (int g = 0; g < 7; ++g) {
+    gb[g] = a.bias ? a.bias[g * a.D + dc] : 0.0f;
+    fr[g] = (LN & 1) ? a.ln_r[g * a.D + dc] : 0.0f;
+  }
   settle(gb);
+  settle(fr);
   const int Tm1 = a.T - 1;
+  // (LN & 1) the records of super-chunk k's LC steps for this wave: lane p < LC NB / 2 copies
+  // blocks 2 (p % (NB/2)) .. +1 of step p / (NB/2) (time clamped like the gates)
+  auto issue_rec = [&](int k) __attribute__((always_inline)) {
+    if constexpr ((LN & 1) != 0) {
+      constexpr int NP = LC * NB / 2;
+      if (lane < NP) {
+        const int j = lane / (NB / 2), q2 = lane % (NB / 2);
+        const int t = min(k * kChunk + w * LC + j, Tm1);
+        dma_to_lds<16>(a.rec_in + ((int64_t)b * a.T + t) * NB + 2 * q2,
+                       lds_addr(&recS[(LN & 1) ? k % FD : 0][(LN & 1) ? w : 0][0]));
+      }
+    }
+  };
   // Past the end of the sequence the clamped step re-reads row T-1 (never out of bounds).
   auto issue = [&](int k) __attribute__((always_inline)) {
+    issue_rec(k);
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
       const int p = i * 64 + lane;
@@ -403,6 +458,7 @@ lucy_scan_fwd_kernel(ScanFwdArgs a) {
   }
   auto issue_next = [&](int k) __attribute__((always_inline)) {
     if (kFast && (k + 1) * kChunk <= a.T) {
+      issue_rec(k);
       const T* gt = gsrc + ((int64_t)k * kChunk + w * LC) * a.g_td;
 #pragma unroll
       for (int i = 0; i < (kFast ? NI : 0); ++i)
@@ -413,8 +469,9 @@ lucy_scan_fwd_kernel(ScanFwdArgs a) {
     }
   };
   // retire super-chunk k+1's DMA; with two slots, k+2's (the only younger loads) may fly on
+  constexpr int NIR = NI + ((LN & 1) ? 1 : 0);   // (+ the records piece)
   auto wait_next = [&](int k) __attribute__((always_inline)) {
-    if (FD == 2 && k + 2 < a.nsc) dma_wait_younger<NI>();
+    if (FD == 2 && k + 2 < a.nsc) dma_wait_younger<NIR>();
     else dma_wait();
   };
   if (a.nsc > 0) issue(0);
@@ -430,10 +487,31 @@ lucy_scan_fwd_kernel(ScanFwdArgs a) {
     f2 zg[LP], dec[LP], u[LP], x[LP], wz[LP];
     float gv[LC][7];
     const unsigned char* slot = slots + (k % FD) * SLOTB;
+    if constexpr ((LN & 1) != 0) {
+      // the LayerNorm statistics of the input rows: Chan's combination of the NB block records
+      // of each step over a group of NB lanes (lane = step * NB + block)
+      const float2 rq = recS[(LN & 1) ? k % FD : 0][(LN & 1) ? w : 0][lane % RECN];
+      const float mean = group_sum_dpp<NB>(rq.x) * (1.0f / NB);
+      const float dm = rq.x - mean;
+      const float m2 = group_sum_dpp<NB>(fmaf(64.0f * dm, dm, rq.y));
+      const float rstd = rsq(m2 * (1.0f / (64 * NB)) + a.ln_eps);
+      if (a.ln_stat && blk == 0 && lane % NB == 0 && lane < RECN && k * kChunk + w * LC + lane / NB < a.T)
+        a.ln_stat[(int64_t)b * a.T + k * kChunk + w * LC + lane / NB] = make_float2(rstd, mean);
 #pragma unroll
-    for (int j = 0; j < LC; ++j)
+      for (int j = 0; j < LC; ++j) {
+        const float rs = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(rstd), j * NB));
+        const float mu = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mean), j * NB));
+        const float rm = -rs * mu;
 #pragma unroll
-      for (int g = 0; g < 7; ++g) gv[j][g] = E::ld(L::get(slot, (j * 7 + g) * 64 + lane)) + gb[g];
+        for (int g = 0; g < 7; ++g)   // rstd (u - mean r) + b'
+          gv[j][g] = fmaf(E::ld(L::get(slot, (j * 7 + g) * 64 + lane)), rs, fmaf(rm, fr[g], gb[g]));
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < LC; ++j)
+#pragma unroll
+        for (int g = 0; g < 7; ++g) gv[j][g] = E::ld(L::get(slot, (j * 7 + g) * 64 + lane)) + gb[g];
+    }
     lds_read_wait();              // slot consumed: it may be refilled with super-chunk k+FD
     if (k + FD < a.nsc) issue_next(k + FD);
 #pragma unroll
@@ -510,6 +588,37 @@ lucy_scan_fwd_kernel(ScanFwdArgs a) {
           lbuf.st(E::st(hs[j] - E::ld(hi)), vo, (uint32_t)(t0 + j) * otd);
         }
       }
+    if constexpr ((LN & 2) != 0) {
+      // (mean, M2) of each step's 64 stored (rounded) values, shifted by unit 0's value: the
+      // 2 LC sums transposed over the wave (three halving exchanges, then a group-of-8 sum), so
+      // lane l ends with sum (l >> 3) & 7 -- 22 exchanges per super-chunk, not 2 LC reductions
+      static_assert(LC == 4, "record butterfly written for 4 steps per wave");
+      float v[8], ref[LC];
+#pragma unroll
+      for (int j = 0; j < LC; ++j) {
+        const float hb = E::ld(E::st(hs[j]));
+        ref[j] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(hb)));
+        const float dl = hb - ref[j];
+        v[2 * j] = dl;
+        v[2 * j + 1] = dl * dl;
+      }
+      const bool b5 = lane & 32, b4 = lane & 16, b3 = lane & 8;
+      float u4[4], u2[2];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        u4[i] = (b5 ? v[i + 4] : v[i]) + __shfl_xor(b5 ? v[i] : v[i + 4], 32);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        u2[i] = (b4 ? u4[i + 2] : u4[i]) + __shfl_xor(b4 ? u4[i] : u4[i + 2], 16);
+      float y = (b3 ? u2[1] : u2[0]) + __shfl_xor(b3 ? u2[0] : u2[1], 8);
+      y = group_sum_dpp<8>(y);
+      const float ysq = __shfl_xor(y, 8);   // lane 16 j: sum 2 j (dl) here, 2 j + 1 (dl^2) there
+      const int j = lane >> 4;
+      const float r = j == 0 ? ref[0] : j == 1 ? ref[1] : j == 2 ? ref[2] : ref[3];
+      if ((lane & 15) == 0 && t0 + j < a.T)
+        a.rec_out[((int64_t)b * a.T + t0 + j) * NB + blk] =
+            make_float2(fmaf(y, 1.0f / 64, r), fmaxf(ysq - y * y * (1.0f / 64), 0.0f));
+    }
   };
   const bool blk_full = (blk + 1) * 64 <= a.D;
   for (int k = 0; k < a.nsc; ++k) {
@@ -532,7 +641,7 @@ lucy_scan_fwd_kernel(ScanFwdArgs a) {
 // WST: the 7 gate gradients of each step are written back into the wave's LDS slot over the raw
 // gates they were computed from, then stored as whole 16-byte pieces (3.5 wave-instructions per
 // super-chunk instead of 28 two-byte stores).  Needs NBUF = 2 and 16-byte aligned dgates.
-template <int DT, int NW, int LC, int PW, int NBUF, bool WST>
+template <int DT, int NW, int LC, int PW, int NBUF, bool WST, bool LN = false>
 __global__ void __launch_bounds__(NW * 64)
 lucy_scan_bwd_kernel(ScanBwdArgs a) {
   static_assert(NW * LC == kChunk, "super-chunk must be 64 steps");
@@ -561,6 +670,9 @@ lucy_scan_bwd_kernel(ScanBwdArgs a) {
   __shared__ float carGh[2][64];
   __shared__ float carGs[2][64];
   __shared__ float ckS[2][2][64];   // (s, h) checkpoint of the super-chunk, shared by all waves
+  // (LN) the input rows' (rstd, mean) of the wave's LC steps, by LDS-DMA with the gates
+  static_assert(!LN || (NBUF == 2 && WST), "LN fold: 16-bit gates with staged stores");
+  __shared__ __attribute__((aligned(16))) float2 stS[LN ? NBUF : 1][LN ? NW : 1][LN ? LC : 1];
   using L = LdsElem<T, PW>;
   unsigned char* slots = dyn_lds + w * NBUF * ROWS * 64 * L::BYTES;   // [NBUF][LC*8][64]
   const uint32_t slots_lds = lds_addr(slots);
@@ -574,13 +686,33 @@ lucy_scan_bwd_kernel(ScanBwdArgs a) {
     carGh[0][lane] = 0.0f;
     carGs[0][lane] = (a.ds_last && dok) ? a.ds_last[(int64_t)b * a.D + d] : 0.0f;
   }
-  float gb[7];
+  float gb[LN ? 1 : 7];
+  // (LN) the folded bias b' and the row sums r of the folded weight, per gate and lane, in LDS
+  // (the fold's gate rebuild has no registers to spare)
+  __shared__ float2 fbS[LN ? 7 : 1][64];
+  if constexpr (LN) {
+    if (w < 7) fbS[LN ? w : 0][lane] = make_float2(a.bias[w * a.D + dc], a.ln_r[w * a.D + dc]);
+  } else {
 #pragma unroll
-  for (int g = 0; g < 7; ++g) gb[g] = a.bias ? a.bias[g * a.D + dc] : 0.0f;
-  settle(gb);
+    for (int g = 0; g < 7; ++g) gb[g] = a.bias ? a.bias[g * a.D + dc] : 0.0f;
+    settle(gb);
+  }
   const int Tm1 = a.T - 1;
+  // (LN) the statistics of super-chunk k's LC steps: lane p < 2 LC copies word p % 2 of step
+  // p / 2 (time clamped)
+  auto issue_stat = [&](int it) __attribute__((always_inline)) {
+    if constexpr (LN) {
+      if (lane < 2 * LC) {
+        const int k = a.nsc - 1 - it;
+        const int t = min(k * kChunk + w * LC + (lane >> 1), Tm1);
+        dma_to_lds<4>((const float*)(a.ln_stat + (int64_t)b * a.T + t) + (lane & 1),
+                      lds_addr(&stS[LN ? it % NBUF : 0][LN ? w : 0][0]));
+      }
+    }
+  };
   auto issue = [&](int it) __attribute__((always_inline)) {
     const int k = a.nsc - 1 - it;
+    issue_stat(it);
     const uint32_t base = slots_lds + (uint32_t)((it % NBUF) * ROWS * 64 * L::BYTES);
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
@@ -632,6 +764,7 @@ lucy_scan_bwd_kernel(ScanBwdArgs a) {
   }
   auto issue_full = [&](int it) __attribute__((always_inline)) {
     const int k = a.nsc - 1 - it;
+    issue_stat(it);
     const uint32_t base = slots_lds + (uint32_t)((it % NBUF) * ROWS * 64 * L::BYTES);
     const int64_t t = (int64_t)k * kChunk + w * LC;
     const T* gt = gsrc + t * a.g_td;
@@ -685,10 +818,23 @@ lucy_scan_bwd_kernel(ScanBwdArgs a) {
     for (int p = 0; p < LP; ++p) {
       const int j = 2 * p;
       f2 g7[7];
+      f2 lrs = {1.0f, 1.0f}, lrm = {0.0f, 0.0f};   // (LN) rstd and -rstd mean of the two steps
+      if constexpr (LN) {
+        const float2 s0 = stS[LN ? it % NBUF : 0][LN ? w : 0][j];
+        const float2 s1 = stS[LN ? it % NBUF : 0][LN ? w : 0][j + 1];
+        lrs = f2{s0.x, s1.x};
+        lrm = -lrs * f2{s0.y, s1.y};
+      }
 #pragma unroll
       for (int g = 0; g < 7; ++g) {
-        g7[g] = f2{E::ld(L::get(slot, (j * 7 + g) * 64 + lane)),
-                   E::ld(L::get(slot, ((j + 1) * 7 + g) * 64 + lane))} + gb[g];
+        const f2 raw = f2{E::ld(L::get(slot, (j * 7 + g) * 64 + lane)),
+                          E::ld(L::get(slot, ((j + 1) * 7 + g) * 64 + lane))};
+        if constexpr (LN) {   // rstd (u - mean r) + b', as the forward rebuilt it
+          const float2 fb = fbS[LN ? g : 0][lane];
+          g7[g] = raw * lrs + (lrm * f2{fb.y, fb.y} + f2{fb.x, fb.x});
+        } else {
+          g7[g] = raw + gb[LN ? 0 : g];
+        }
         if constexpr (NBUF == 1) {
           rg[j][g] = g7[g].x;
           rg[j + 1][g] = g7[g].y;
@@ -833,6 +979,14 @@ lucy_scan_bwd_kernel(ScanBwdArgs a) {
 #pragma unroll
         for (int g = 0; g < 7; ++g) bacc[g] += o[g];
       }
+      f2 lrs = {1.0f, 1.0f};   // (LN) the stored gradient is d/du = rstd d/dg
+      if constexpr (LN) {
+        lrs = f2{stS[LN ? it % NBUF : 0][LN ? w : 0][jp].x, stS[LN ? it % NBUF : 0][LN ? w : 0][jp + 1].x};
+        if constexpr (FULL) {
+#pragma unroll
+          for (int g = 0; g < 7; ++g) o[g] *= lrs;
+        }
+      }
       if constexpr (FULL && WST) {   // both steps' gradients rounded by one v_cvt_pk_bf16_f32
 #pragma unroll
         for (int g = 0; g < 7; ++g) {
@@ -849,7 +1003,7 @@ lucy_scan_bwd_kernel(ScanBwdArgs a) {
 #pragma unroll
             for (int g = 0; g < 7; ++g) {
               const float og = o[g][h2];
-              const T ogt = E::st(og);
+              const T ogt = E::st(LN ? og * lrs[h2] : og);
               if constexpr (WST) ((T*)slot)[(j * 7 + g) * 64 + lane] = ogt;   // over its raw gate
               else if (!(SC_ABL & 2)) dgbuf.st(ogt, vo, so + (uint32_t)(g * a.dg_cd * sizeof(T)));
               if constexpr (NBUF == 1) bacc1[g] += E::ld(ogt);
@@ -935,11 +1089,11 @@ static bool set_lds_limit(K kernel, size_t bytes) {
                              (int)bytes) == hipSuccess;
 }
 
-template <int DT, int PW, bool SPLIT = false>
+template <int DT, int PW, bool SPLIT = false, int LN = 0, int NB = 8>
 static void launch_fwd(const ScanFwdArgs& a, hipStream_t st) {
   using T = typename Elem<DT>::T;
   constexpr int FD = (SC_FWD_FD >= 2 && LdsElem<T, PW>::BYTES == 2) ? 2 : 1;   // 2 x 56 KiB fit
-  auto kern = lucy_scan_fwd_kernel<DT, kNW, kLC, PW, FD, SPLIT>;
+  auto kern = lucy_scan_fwd_kernel<DT, kNW, kLC, PW, FD, SPLIT, LN, NB>;
   const size_t lds = (size_t)FD * kNW * kLC * 7 * 64 * LdsElem<T, PW>::BYTES;
   static const bool lds_ok = set_lds_limit(kern, lds);
   (void)lds_ok;
@@ -947,12 +1101,12 @@ static void launch_fwd(const ScanFwdArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(kern, grid, dim3(kNW * 64), lds, st, a);
 }
 
-template <int DT, int PW, bool WST>
+template <int DT, int PW, bool WST, bool LN = false>
 static void launch_bwd(const ScanBwdArgs& a, hipStream_t st) {
   using T = typename Elem<DT>::T;
   // two slots per wave fit only for 2-byte LDS elements (160 KiB per CU)
   constexpr int NBUF = LdsElem<T, PW>::BYTES == 2 ? 2 : 1;
-  auto kern = lucy_scan_bwd_kernel<DT, kBNW, kBLC, PW, NBUF, WST>;
+  auto kern = lucy_scan_bwd_kernel<DT, kBNW, kBLC, PW, NBUF, WST, LN>;
   const size_t lds = (size_t)NBUF * kBNW * kBLC * 8 * 64 * LdsElem<T, PW>::BYTES;
   static const bool lds_ok = set_lds_limit(kern, lds);
   (void)lds_ok;
@@ -970,11 +1124,32 @@ static bool wide_pieces(const void* p, int esize, int D, std::initializer_list<i
   return true;
 }
 
+// the LN-fold instances (16-bit gates, 16-byte pieces, D = 64 NB): fold bit 1, records bit 2
+template <int DT, bool SPLIT, int NB>
+static void dispatch_fwd_ln(const ScanFwdArgs& a, int mode, hipStream_t st) {
+  switch (mode) {
+    case 1: launch_fwd<DT, 16, SPLIT, 1, NB>(a, st); break;
+    case 2: launch_fwd<DT, 16, SPLIT, 2, NB>(a, st); break;
+    default: launch_fwd<DT, 16, SPLIT, 3, NB>(a, st); break;
+  }
+}
+template <int DT, bool SPLIT>
+static void dispatch_fwd_ln_nb(const ScanFwdArgs& a, int mode, hipStream_t st) {
+  if (a.D == 512) dispatch_fwd_ln<DT, SPLIT, 8>(a, mode, st);
+  else dispatch_fwd_ln<DT, SPLIT, 16>(a, mode, st);
+}
+
 template <int DT>
 static void dispatch_fwd(const ScanFwdArgs& a, hipStream_t st) {
   constexpr int es = (int)sizeof(typename Elem<DT>::T);
   const bool wide = wide_pieces(a.gates, es, a.D, {a.g_bt, a.g_td, a.g_cd, a.g_cb});
   if constexpr (es == 2) {
+    const int mode = (a.ln_r ? 1 : 0) | (a.rec_out ? 2 : 0);
+    if (mode) {   // (scan_fwd checked wide pieces and D)
+      if (a.out_lo) dispatch_fwd_ln_nb<DT, true>(a, mode, st);
+      else dispatch_fwd_ln_nb<DT, false>(a, mode, st);
+      return;
+    }
     if (a.out_lo) {
       if (wide) launch_fwd<DT, 16, true>(a, st);
       else launch_fwd<DT, es, true>(a, st);
@@ -988,6 +1163,12 @@ static void dispatch_fwd(const ScanFwdArgs& a, hipStream_t st) {
 template <int DT>
 static void dispatch_bwd(const ScanBwdArgs& a, hipStream_t st) {
   constexpr int es = sizeof(typename Elem<DT>::T);
+  if constexpr (es == 2) {
+    if (a.ln_r) {   // (scan_bwd checked the layout)
+      launch_bwd<DT, 16, true, true>(a, st);
+      return;
+    }
+  }
   if (wide_pieces(a.gates, es, a.D, {a.g_bt, a.g_td, a.g_cd, a.g_cb}) &&
       wide_pieces(a.dout, es, a.D, {a.d_bt, a.d_bd})) {
     if (es == 2 && wide_pieces(a.dgates, es, a.D, {a.dg_bt, a.dg_td, a.dg_cd, a.dg_cb}))
@@ -1012,11 +1193,19 @@ extern "C" int64_t sc_lucy_scan_ckpt_numel(int B, int T, int D) {
 
 static int check_dtype(int dt) { return dt == SC_F32 || dt == SC_BF16 || dt == SC_F16; }
 
+struct LnFold {   // sc_lucy_scan_fwd_ln's extra arguments (all NULL: no fold, no records)
+  const float* r = nullptr;
+  const float* rec_in = nullptr;
+  float* stat = nullptr;
+  float* rec_out = nullptr;
+  float eps = 1e-5f;
+};
+
 static int scan_fwd(const void* gates, int gates_dtype, const float* gate_bias, const float* h0,
                     const float* s0, void* out, float* s_out, float* h_out, int B, int T, int D,
                     int64_t stride_g_bt, int64_t stride_g_td, int64_t stride_g_cd,
                     int64_t stride_g_cb, int64_t stride_o_bt, int64_t stride_o_bd, float* ckpt,
-                    void* out_dup, void* out_lo, void* stream) {
+                    void* out_dup, void* out_lo, void* stream, const LnFold& ln = LnFold{}) {
   SC_REQUIRE(check_dtype(gates_dtype), "sc_lucy_scan_fwd: unsupported gates dtype %d", gates_dtype);
   SC_REQUIRE(B >= 0 && T >= 0 && D >= 0, "sc_lucy_scan_fwd: negative shape B=%d T=%d D=%d", B, T, D);
   SC_REQUIRE(B <= 65535, "sc_lucy_scan_fwd: B=%d exceeds grid limit 65535", B);
@@ -1028,9 +1217,19 @@ static int scan_fwd(const void* gates, int gates_dtype, const float* gate_bias, 
              "sc_lucy_scan_fwd: negative stride");
   SC_REQUIRE((int64_t)T * stride_o_bd * 4 < (1ll << 31),
              "sc_lucy_scan_fwd: one batch row of out spans >= 2 GiB");
+  if (ln.r || ln.rec_out) {
+    const int es = gates_dtype == SC_F32 ? 4 : 2;
+    SC_REQUIRE(es == 2, "sc_lucy_scan_fwd_ln: the LayerNorm fold needs 16-bit gates");
+    SC_REQUIRE(D == 512 || D == 1024, "sc_lucy_scan_fwd_ln: D=%d must be 512 or 1024", D);
+    SC_REQUIRE(wide_pieces(gates, es, D, {stride_g_bt, stride_g_td, stride_g_cd, stride_g_cb}),
+               "sc_lucy_scan_fwd_ln: gates must be 16-byte aligned with 16-byte strides");
+    SC_REQUIRE(!ln.r || (ln.rec_in && gate_bias), "sc_lucy_scan_fwd_ln: the fold needs rec_in and "
+               "the folded bias b' as gate_bias");
+  }
   ScanFwdArgs a{gates, gate_bias, h0, s0, out, s_out, h_out, ckpt, B, T, D, (T + kChunk - 1) / kChunk,
                 stride_g_bt, stride_g_td, stride_g_cd, stride_g_cb, stride_o_bt, stride_o_bd,
-                out_dup, out_lo};
+                out_dup, out_lo, ln.r, (const float2*)ln.rec_in, (float2*)ln.stat,
+                (float2*)ln.rec_out, ln.eps};
   hipStream_t st = (hipStream_t)stream;
   switch (gates_dtype) {
     case SC_F32: dispatch_fwd<SC_F32>(a, st); break;
@@ -1069,6 +1268,35 @@ extern "C" int sc_lucy_scan_fwd_split(const void* gates, int gates_dtype, const 
                   out_lo, stream);
 }
 
+extern "C" int sc_lucy_scan_fwd_ln(const void* gates, int gates_dtype, const float* gate_bias,
+                                   const float* h0, const float* s0, void* out, void* out_dup,
+                                   void* out_lo, float* s_out, float* h_out, int B, int T, int D,
+                                   int64_t stride_g_bt, int64_t stride_g_td, int64_t stride_g_cd,
+                                   int64_t stride_g_cb, int64_t stride_o_bt, int64_t stride_o_bd,
+                                   float* ckpt, const float* ln_r, const float* ln_rec_in,
+                                   float* ln_stat, float* ln_rec_out, float ln_eps, void* stream) {
+  clear_error();
+  SC_REQUIRE((out_dup == nullptr) == (out_lo == nullptr),
+             "sc_lucy_scan_fwd_ln: out_dup and out_lo come together");
+  LnFold ln;
+  ln.r = ln_r;
+  ln.rec_in = ln_rec_in;
+  ln.stat = ln_stat;
+  ln.rec_out = ln_rec_out;
+  ln.eps = ln_eps;
+  return scan_fwd(gates, gates_dtype, gate_bias, h0, s0, out, s_out, h_out, B, T, D, stride_g_bt,
+                  stride_g_td, stride_g_cd, stride_g_cb, stride_o_bt, stride_o_bd, ckpt, out_dup,
+                  out_lo, stream, ln);
+}
+
+static int scan_bwd(const void* gates, int gates_dtype, const float* gate_bias, const float* ckpt,
+                    const void* dout, const float* ds_last, void* dgates, float* dh0, float* ds0,
+                    float* dbias, int B, int T, int D, int64_t stride_g_bt, int64_t stride_g_td,
+                    int64_t stride_g_cd, int64_t stride_g_cb, int64_t stride_d_bt,
+                    int64_t stride_d_bd, int64_t stride_dg_bt, int64_t stride_dg_td,
+                    int64_t stride_dg_cd, int64_t stride_dg_cb, const float* ln_r,
+                    const float* ln_stat, void* stream);
+
 extern "C" int sc_lucy_scan_bwd(const void* gates, int gates_dtype, const float* gate_bias,
                                 const float* ckpt,
                                 const void* dout, const float* ds_last, void* dgates, float* dh0,
@@ -1078,6 +1306,41 @@ extern "C" int sc_lucy_scan_bwd(const void* gates, int gates_dtype, const float*
                                 int64_t stride_dg_td, int64_t stride_dg_cd, int64_t stride_dg_cb,
                                 void* stream) {
   clear_error();
+  return scan_bwd(gates, gates_dtype, gate_bias, ckpt, dout, ds_last, dgates, dh0, ds0, dbias, B,
+                  T, D, stride_g_bt, stride_g_td, stride_g_cd, stride_g_cb, stride_d_bt,
+                  stride_d_bd, stride_dg_bt, stride_dg_td, stride_dg_cd, stride_dg_cb, nullptr,
+                  nullptr, stream);
+}
+
+extern "C" int sc_lucy_scan_bwd_ln(const void* gates, int gates_dtype, const float* gate_bias,
+                                   const float* ckpt, const void* dout, const float* ds_last,
+                                   void* dgates, float* dh0, float* ds0, float* dbias, int B, int T,
+                                   int D, int64_t stride_g_bt, int64_t stride_g_td,
+                                   int64_t stride_g_cd, int64_t stride_g_cb, int64_t stride_d_bt,
+                                   int64_t stride_d_bd, int64_t stride_dg_bt, int64_t stride_dg_td,
+                                   int64_t stride_dg_cd, int64_t stride_dg_cb, const float* ln_r,
+                                   const float* ln_stat, void* stream) {
+  clear_error();
+  SC_REQUIRE(ln_r && ln_stat && gate_bias, "sc_lucy_scan_bwd_ln: null ln_r / ln_stat / gate_bias");
+  SC_REQUIRE(gates_dtype != SC_F32, "sc_lucy_scan_bwd_ln: the LayerNorm fold needs 16-bit gates");
+  SC_REQUIRE((D == 512 || D == 1024) && wide_pieces(gates, 2, D, {stride_g_bt, stride_g_td, stride_g_cd, stride_g_cb}) &&
+                 wide_pieces(dout, 2, D, {stride_d_bt, stride_d_bd}) &&
+                 wide_pieces(dgates, 2, D, {stride_dg_bt, stride_dg_td, stride_dg_cd, stride_dg_cb}),
+             "sc_lucy_scan_bwd_ln: 16-byte aligned gates / dout / dgates with 16-byte strides, "
+             "D = 512 or 1024");
+  return scan_bwd(gates, gates_dtype, gate_bias, ckpt, dout, ds_last, dgates, dh0, ds0, dbias, B,
+                  T, D, stride_g_bt, stride_g_td, stride_g_cd, stride_g_cb, stride_d_bt,
+                  stride_d_bd, stride_dg_bt, stride_dg_td, stride_dg_cd, stride_dg_cb, ln_r,
+                  ln_stat, stream);
+}
+
+static int scan_bwd(const void* gates, int gates_dtype, const float* gate_bias, const float* ckpt,
+                    const void* dout, const float* ds_last, void* dgates, float* dh0, float* ds0,
+                    float* dbias, int B, int T, int D, int64_t stride_g_bt, int64_t stride_g_td,
+                    int64_t stride_g_cd, int64_t stride_g_cb, int64_t stride_d_bt,
+                    int64_t stride_d_bd, int64_t stride_dg_bt, int64_t stride_dg_td,
+                    int64_t stride_dg_cd, int64_t stride_dg_cb, const float* ln_r,
+                    const float* ln_stat, void* stream) {
   SC_REQUIRE(check_dtype(gates_dtype), "sc_lucy_scan_bwd: unsupported gates dtype %d", gates_dtype);
   SC_REQUIRE(B >= 0 && T >= 0 && D >= 0, "sc_lucy_scan_bwd: negative shape B=%d T=%d D=%d", B, T, D);
   SC_REQUIRE(B <= 65535, "sc_lucy_scan_bwd: B=%d exceeds grid limit 65535", B);
@@ -1095,7 +1358,8 @@ extern "C" int sc_lucy_scan_bwd(const void* gates, int gates_dtype, const float*
   ScanBwdArgs a{gates, gate_bias, ckpt, dout, ds_last, dgates, dh0, ds0, dbias, B, T, D,
                 (T + kChunk - 1) / kChunk,
                 stride_g_bt, stride_g_td, stride_g_cd, stride_g_cb, stride_d_bt, stride_d_bd,
-                stride_dg_bt, stride_dg_td, stride_dg_cd, stride_dg_cb};
+                stride_dg_bt, stride_dg_td, stride_dg_cd, stride_dg_cb, ln_r,
+                (const float2*)ln_stat};
   hipStream_t st = (hipStream_t)stream;
   switch (gates_dtype) {
     case SC_F32: dispatch_bwd<SC_F32>(a, st); break;

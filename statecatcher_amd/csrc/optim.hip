@@ -196,18 +196,25 @@ __global__ void __launch_bounds__(kThreads) images_kernel(ImageTable t) {
     }
     const float* src = j.src + sr * j.ld_src;
     const int64_t c = c0 + cs;
+    // (folded LayerNorm: col_scale[c] src - row_shift[sr], unfused as sc_ln_fold_prep's rowsum)
+    const float sh = j.row_shift ? j.row_shift[sr] : 0.0f;
+    auto val = [&](float x, int64_t cc) {
+      if (j.col_scale) x = __fmul_rn(j.col_scale[cc], x);
+      return j.row_shift ? __fsub_rn(x, sh) : x;
+    };
     if (c + 16 <= j.cols && (((uintptr_t)(src + c)) & 15) == 0) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const float4 x = *(const float4*)(src + c + 4 * q);
-        h[4 * q] = bf16_bits(x.x);
-        h[4 * q + 1] = bf16_bits(x.y);
-        h[4 * q + 2] = bf16_bits(x.z);
-        h[4 * q + 3] = bf16_bits(x.w);
+        h[4 * q] = bf16_bits(val(x.x, c + 4 * q));
+        h[4 * q + 1] = bf16_bits(val(x.y, c + 4 * q + 1));
+        h[4 * q + 2] = bf16_bits(val(x.z, c + 4 * q + 2));
+        h[4 * q + 3] = bf16_bits(val(x.w, c + 4 * q + 3));
       }
     } else {
 #pragma unroll
-      for (int e = 0; e < 16; ++e) h[e] = (c + e < j.cols) ? bf16_bits(src[c + e]) : (uint16_t)0;
+      for (int e = 0; e < 16; ++e)
+        h[e] = (c + e < j.cols) ? bf16_bits(val(src[c + e], c + e)) : (uint16_t)0;
     }
     uint16_t* dst = (uint16_t*)j.dst + r * j.cols_pad;
     if (c + 16 <= j.cols_pad && (((uintptr_t)(dst + c)) & 15) == 0) {

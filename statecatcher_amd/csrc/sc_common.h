@@ -178,6 +178,13 @@ __device__ __forceinline__ void dma_to_lds(const void* src, uint32_t lds_addr) {
 template <int PW>
 __device__ __forceinline__ void dma_to_lds_s(const void* sbase, uint32_t voff, uint32_t lds_addr) {
   lds_addr = __builtin_amdgcn_readfirstlane(lds_addr);
+  {   // the base is wave-uniform by contract: say so where the compiler cannot prove it (a
+      // preceding exec-masked DMA leaves it unsure), so the saddr operand stays in SGPRs
+    const uint64_t u = (uint64_t)(uintptr_t)sbase;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
+    sbase = (const void*)(uintptr_t)(((uint64_t)hi << 32) | lo);
+  }
   uint32_t keep;
   if constexpr (PW == 16) {
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"

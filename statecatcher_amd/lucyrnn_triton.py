@@ -19,8 +19,8 @@ import torch
 import torch.nn as nn
 
 from .lucyrnn_conf import LucyRNNConfig
-from .ops import (cell_image_spec, colsum, layer_norm, layer_norm_supported, lucy_cell, proj_dgrad,
-                  weight_images, wgrad_splitk)
+from .ops import (cell_image_spec, colsum, fold_images, layer_norm, layer_norm_supported, ln_fold_ok,
+                  lucy_cell, lucy_cell_ln, proj_dgrad, weight_images, wgrad_splitk)
 
 
 class _LinearFn(torch.autograd.Function):
@@ -154,12 +154,13 @@ class LucyRNNCellTriton(nn.Module):
         out, s_out, _ = self.forward_with_h(x, h0, s0)
         return out, s_out
 
-    def forward_with_h(self, x, h0, s0, imgs=None, split_sink=None):
+    def forward_with_h(self, x, h0, s0, imgs=None, split_sink=None, rec_sink=None):
         """(out, s_out, h_last): h_last = out[:, -1] in fp32, unrounded by a 16-bit out (the
         state LucyRNNtriton carries).  Projection GEMM + scan are one autograd node: the scan
         backward hands the bias gradient back from registers, the weight gradient runs on the
         MFMA split-L kernel.  imgs: this layer's entry of ops.weight_images (bf16 only);
-        split_sink: ops.LucyCellFn's (the scan's split-precision output planes)."""
+        split_sink: ops.LucyCellFn's (the scan's split-precision output planes); rec_sink: its
+        LayerNorm block records for a folded next layer."""
         w, b = self.linear.weight, self.linear.bias
         if x.is_cuda and torch.is_autocast_enabled("cuda"):
             cdt = torch.get_autocast_dtype("cuda")
@@ -170,7 +171,7 @@ class LucyRNNCellTriton(nn.Module):
         if imgs is not None and cdt != torch.bfloat16:
             imgs = None
         with torch.autocast("cuda", enabled=False):
-            return lucy_cell(x, w, b, h0, s0, cdt, imgs, split_sink)
+            return lucy_cell(x, w, b, h0, s0, cdt, imgs, split_sink, rec_sink)
 
 
 class LucyRNNtriton(nn.Module):
@@ -218,7 +219,7 @@ class LucyRNNtriton(nn.Module):
         else:
             h, s = hidden_states
 
-        cell_imgs, out_imgs = self._weight_images(x)
+        cell_imgs, out_imgs, fold = self._weight_images(x)
         req = getattr(_HEAD, "req", None)
         op = self.output_proj
         if req is not None and not (out_imgs is not None and out_imgs[1] is not None
@@ -236,13 +237,25 @@ class LucyRNNtriton(nn.Module):
             h_t, s_t = h[t], s[t]
             layers = self.tracks[t]
             norms = self.norms[t]
+            rec = None
             for l, layer in enumerate(layers):
+                last = l == len(layers) - 1
                 # h carry = out[:, -1] (lucyrnn_triton.py:135), taken in fp32 from the scan and
                 # contiguous
-                x_t, s_t[l], h_t[l] = layer.forward_with_h(
-                    x_t, h_t[l], s_t[l], cell_imgs.get((t, l)) if cell_imgs else None,
-                    sink if l == len(layers) - 1 else None)
-                if l < len(norms):
+                rsink = [] if fold and not last else None
+                if fold and l > 0:
+                    # norms[l-1] folded into this layer's projection (ops.LucyCellLNFn): x_t is
+                    # the previous layer's raw output, rec its block records
+                    ln = norms[l - 1]
+                    x_t, s_t[l], h_t[l] = lucy_cell_ln(
+                        x_t, layer.linear.weight, layer.linear.bias, ln.weight, ln.bias, h_t[l],
+                        s_t[l], fold[(t, l)], rec, ln.eps, sink if last else None, rsink)
+                else:
+                    x_t, s_t[l], h_t[l] = layer.forward_with_h(
+                        x_t, h_t[l], s_t[l], cell_imgs.get((t, l)) if cell_imgs else None,
+                        sink if last else None, rsink)
+                rec = rsink[0] if rsink else None
+                if l < len(norms) and not fold:
                     x_t = norms[l](x_t)
             track_outputs.append(x_t)
             final_h.append(h_t)
@@ -263,15 +276,60 @@ class LucyRNNtriton(nn.Module):
             return logits, (final_h, final_s)
         return logits
 
+    def _fold_ok(self):
+        """Every layer after the first takes its LayerNorm folded into its projection
+        (ops.LucyCellLNFn): D of 512 / 1024, affine LayerNorms, biased fp32 projections."""
+        if not ln_fold_ok(self.config.hidden_dim) or self.config.num_layers < 2:
+            return False
+        for layers, norms in zip(self.tracks, self.norms):
+            for l, layer in enumerate(layers):
+                w, b = layer.linear.weight, layer.linear.bias
+                if b is None or w.dtype != torch.float32 or not w.is_cuda or w.stride(1) != 1:
+                    return False
+            for ln in norms:
+                if not (ln.elementwise_affine and ln.weight is not None and ln.bias is not None
+                        and ln.weight.dtype == torch.float32 and ln.weight.is_contiguous()
+                        and ln.bias.is_contiguous()):
+                    return False
+        return True
+
     def _weight_images(self, x):
         """bf16 images of every projection weight for this forward (ops.weight_images: one
         launch after each optimizer step, cached otherwise) when the step runs under bf16
         autocast on the GPU; ({(track, layer): (W image, W^T image)}, output-projection
-        (W, W^T, b) images) or (None, None)."""
+        (W, W^T, b) images, {(track, layer): folded-LayerNorm images (ops.fold_images)} for layers
+        1.. or None) or (None, None, None)."""
         if not (x.is_cuda and torch.is_autocast_enabled("cuda")
                 and torch.get_autocast_dtype("cuda") == torch.bfloat16):
-            return None, None
+            return None, None, None
         grad = torch.is_grad_enabled()
+        fold = self._fold_ok()
+        specs, where, fspecs, fwhere = [], [], [], []
+        for t, layers in enumerate(self.tracks):
+            for l, layer in enumerate(layers):
+                sp = cell_image_spec(layer.linear.weight, torch.bfloat16,
+                                     grad and (l > 0 or x.requires_grad))
+                if fold and l > 0 and sp is not None:
+                    ln = self.norms[t][l - 1]
+                    w, bd, kp, want_t = sp
+                    fspecs.append((w, layer.linear.bias, ln.weight, ln.bias, bd, kp, want_t))
+                    fwhere.append((t, l))
+                elif sp is not None and layer.linear.bias is not None:
+                    specs.append(sp)
+                    where.append((t, l))
+        if fold and len(fwhere) != sum(len(layers) - 1 for layers in self.tracks):
+            return self._weight_images_plain(x, grad)   # (a layer without an image spec: no fold)
+        osp = self.output_proj.image_specs(grad) if self.num_tracks == 1 else None
+        imgs = weight_images(specs + (osp or []))
+        cell = {w: im for w, im in zip(where, imgs)}
+        out = None
+        if osp:
+            (wc, wt), rest = imgs[len(specs)], imgs[len(specs) + 1:]
+            out = (wc, wt, rest[0][0] if rest else None)
+        folded = {w: im for w, im in zip(fwhere, fold_images(fspecs))} if fold else None
+        return cell, out, folded
+
+    def _weight_images_plain(self, x, grad):
         specs, where = [], []
         for t, layers in enumerate(self.tracks):
             for l, layer in enumerate(layers):
@@ -287,4 +345,4 @@ class LucyRNNtriton(nn.Module):
         if osp:
             (wc, wt), rest = imgs[len(specs)], imgs[len(specs) + 1:]
             out = (wc, wt, rest[0][0] if rest else None)
-        return cell, out
+        return cell, out, None

@@ -54,9 +54,11 @@ def gate_layout(gates):
                      f"shape {tuple(gates.shape)} strides {gates.stride()}")
 
 
-def _scan_fwd(gates, h0, s0, need_ckpt, bias=None, want_h=False, split=False):
+def _scan_fwd(gates, h0, s0, need_ckpt, bias=None, want_h=False, split=False, ln=None):
     """split (16-bit gates): out is the first D columns of a [B,T,3D] buffer whose other two
-    blocks are out again and h - out (sc_lucy_scan_fwd_split), returned as the last element."""
+    blocks are out again and h - out (sc_lucy_scan_fwd_split), returned as the last element.
+    ln = (ln_r, rec_in, stat, rec_out, eps): the folded LayerNorm (sc_lucy_scan_fwd_ln; ln_r /
+    rec_in None: records out only)."""
     require_device(gates, h0, s0)
     if gates.dim() == 4 and gates.shape[2] == 7 and gates.stride(3) != 1:
         gates = gates.contiguous()
@@ -79,7 +81,15 @@ def _scan_fwd(gates, h0, s0, need_ckpt, bias=None, want_h=False, split=False):
     e = gates.element_size()
     nbytes = B * T * D * 8 * e + (ckpt.numel() * 4 if ckpt is not None else 0) + 4 * B * D * 4
     with _timed("lucy_scan_fwd", gates, nbytes):
-        if split:
+        if ln is not None:
+            ln_r, rec_in, stat, rec_out, eps = ln
+            rc = lib.sc_lucy_scan_fwd_ln(ptr(gates), dtype_code(gates), ptr(bias), ptr(h0c), ptr(s0c),
+                                         ptr(out), ptr(wide[..., D:2 * D]) if split else None,
+                                         ptr(wide[..., 2 * D:]) if split else None, ptr(s_out),
+                                         ptr(h_out), B, T, D, *gs, out.stride(0), out.stride(1),
+                                         ptr(ckpt), ptr(ln_r), ptr(rec_in), ptr(stat), ptr(rec_out),
+                                         float(eps), stream_of(gates))
+        elif split:
             rc = lib.sc_lucy_scan_fwd_split(ptr(gates), dtype_code(gates), ptr(bias), ptr(h0c),
                                             ptr(s0c), ptr(out), ptr(wide[..., D:2 * D]),
                                             ptr(wide[..., 2 * D:]), ptr(s_out), ptr(h_out), B, T, D,
@@ -94,8 +104,9 @@ def _scan_fwd(gates, h0, s0, need_ckpt, bias=None, want_h=False, split=False):
     return res + (wide,) if split else res
 
 
-def _scan_bwd(gates, ckpt, dout, ds_last, want_dbias, bias=None):
-    """dgates come back in the layout of `gates` (contiguous)."""
+def _scan_bwd(gates, ckpt, dout, ds_last, want_dbias, bias=None, ln=None):
+    """dgates come back in the layout of `gates` (contiguous).  ln = (ln_r, stat): the folded
+    LayerNorm's backward scan (sc_lucy_scan_bwd_ln: dgates = rstd dL/dgate)."""
     B, T, D, gs = gate_layout(gates)
     if dout is None:
         dout = torch.zeros(B, T, D, dtype=gates.dtype, device=gates.device)
@@ -112,10 +123,16 @@ def _scan_bwd(gates, ckpt, dout, ds_last, want_dbias, bias=None):
     e = gates.element_size()
     nbytes = B * T * D * 15 * e + ckpt.numel() * 4 + 3 * B * D * 4
     with _timed("lucy_scan_bwd", gates, nbytes):
-        rc = _lib.load().sc_lucy_scan_bwd(
-            ptr(gates), dtype_code(gates), ptr(bias), ptr(ckpt), ptr(dout), ptr(ds_last), ptr(dgates),
-            ptr(dh0), ptr(ds0), ptr(dbias), B, T, D, *gs, dout.stride(0), dout.stride(1), *dgs,
-            stream_of(gates))
+        if ln is not None:
+            rc = _lib.load().sc_lucy_scan_bwd_ln(
+                ptr(gates), dtype_code(gates), ptr(bias), ptr(ckpt), ptr(dout), ptr(ds_last),
+                ptr(dgates), ptr(dh0), ptr(ds0), ptr(dbias), B, T, D, *gs, dout.stride(0),
+                dout.stride(1), *dgs, ptr(ln[0]), ptr(ln[1]), stream_of(gates))
+        else:
+            rc = _lib.load().sc_lucy_scan_bwd(
+                ptr(gates), dtype_code(gates), ptr(bias), ptr(ckpt), ptr(dout), ptr(ds_last),
+                ptr(dgates), ptr(dh0), ptr(ds0), ptr(dbias), B, T, D, *gs, dout.stride(0),
+                dout.stride(1), *dgs, stream_of(gates))
     check(rc, "sc_lucy_scan_bwd")
     return dgates, dh0, ds0, dbias
 
@@ -331,9 +348,11 @@ def invalidate_weight_images(params=None):
     itself (optimizers, ``load_state_dict``, ``with torch.no_grad(): p.copy_(...)``) are seen."""
     if params is None:
         _IMAGES.clear()
+        _FOLD.clear()
         return
     for p in params:
         _IMAGES.pop(p, None)
+        _FOLD.pop(p, None)
 
 
 def _image_stale(w, img):
@@ -434,10 +453,12 @@ class LucyCellFn(torch.autograd.Function):
     """
 
     @staticmethod
-    def forward(ctx, x2d, w, b, h0, s0, B, T, cdt, imgs=None, split_sink=None):
+    def forward(ctx, x2d, w, b, h0, s0, B, T, cdt, imgs=None, split_sink=None, rec_sink=None):
         """split_sink: a list; when given (bf16), the scan also writes the split-precision planes
         of its output (sc_lucy_scan_fwd_split) and the [B,T,3D] buffer is appended to it (out is
-        its first D columns): the input of CTCHeadFn's one-GEMM fp32-accurate projection."""
+        its first D columns): the input of CTCHeadFn's one-GEMM fp32-accurate projection.
+        rec_sink: a list; when given, the scan also writes its output's LayerNorm block records
+        (sc_lucy_scan_fwd_ln) for the next layer's LucyCellLNFn, appended to it."""
         ctx.set_materialize_grads(False)   # unused state outputs: no zero-filled gradients
         D = w.shape[0] // 7
         blocked = D % 64 == 0
@@ -471,7 +492,12 @@ class LucyCellFn(torch.autograd.Function):
             gates = proj_fwd(xg, wg)
         gates = gates.view(B, T, D // 64, 7, 64) if blocked else gates.view(B, T, 7, D)
         need = any(ctx.needs_input_grad)
-        res = _scan_fwd(gates, h0, s0, need, bias, want_h=True, split=split_sink is not None)
+        rec = None
+        if rec_sink is not None:
+            rec = torch.empty(B, T, D // 64, 2, dtype=torch.float32, device=gates.device)
+            rec_sink.append(rec)
+        res = _scan_fwd(gates, h0, s0, need, bias, want_h=True, split=split_sink is not None,
+                        ln=None if rec is None else (None, None, None, rec, 0.0))
         gates, out, s_out, ckpt, h_out = res[:5]
         if len(res) > 5:
             split_sink.append(res[5])
@@ -525,17 +551,174 @@ class LucyCellFn(torch.autograd.Function):
                 dw = wgrad_splitk(dg2, xc, blocked_d=bd)
             dw = dw.to(wdt)
         db = colsum(dbias.view(dbias.shape[0], -1)).to(wdt) if dbias is not None else None
-        return dx, dw, db, dh0.to(hdt), ds0.to(sdt), None, None, None, None, None
+        return dx, dw, db, dh0.to(hdt), ds0.to(sdt), None, None, None, None, None, None
 
 
-def lucy_cell(x, w, b, h0, s0, cdt=None, imgs=None, split_sink=None):
+def lucy_cell(x, w, b, h0, s0, cdt=None, imgs=None, split_sink=None, rec_sink=None):
     """x [B,T,Din] -> (out [B,T,D], s_last [B,D] fp32, h_last [B,D] fp32) through projection
     + scan.  imgs: the (forward weight, transposed weight) images of cell_image_spec, or None
     (the cell casts w itself).  split_sink: see LucyCellFn.forward."""
     B, T, Din = x.shape
     if cdt is None:
         cdt = torch.promote_types(x.dtype, w.dtype)
-    return LucyCellFn.apply(x.reshape(B * T, Din), w, b, h0, s0, B, T, cdt, imgs, split_sink)
+    return LucyCellFn.apply(x.reshape(B * T, Din), w, b, h0, s0, B, T, cdt, imgs, split_sink,
+                            rec_sink)
+
+
+# ----------------------------------------------------------------------------- LayerNorm fold ---
+# SC_LN_FOLD=0 keeps the inter-layer LayerNorm as its own kernels (A/B only)
+USE_LN_FOLD = os.environ.get("SC_LN_FOLD", "1") != "0"
+_FOLD = WeakIdKeyDictionary()
+
+
+def ln_fold_ok(D):
+    return USE_LN_FOLD and D in (512, 1024)
+
+
+def fold_images(specs):
+    """specs: [(w, b, gamma, beta, block_d, cols_pad, want_t)] of gate projections that follow a
+    LayerNorm (gamma, beta).  Returns [(W'' image bf16 [rows, cols_pad] (step-blocked rows),
+    W''^T image or None, b' fp32 [rows], r fp32 [rows])] (csrc/ln_fold.hip header), cached per
+    weight and rebuilt when any of w, b, gamma, beta changed: one sc_ln_fold_prep launch and one
+    sc_weight_images launch for all stale ones."""
+    out, preps, jobs, keep = [None] * len(specs), [], [], []
+    for i, (w, b, g, be, bd, kp, want_t) in enumerate(specs):
+        key = (w._version, w.data_ptr(), b._version, b.data_ptr(), g._version, g.data_ptr(),
+               be._version, be.data_ptr(), bd, kp, bool(want_t))
+        hit = _FOLD.get(w)
+        if hit is not None and hit[0] == key:
+            out[i] = hit[1]
+            continue
+        rows, cols = w.shape
+        f32 = dict(dtype=torch.float32, device=w.device)
+        shift, bprime, rowsum = (torch.empty(rows, **f32) for _ in range(3))
+        preps.append(_lib.LnFoldJob(w.data_ptr(), g.data_ptr(), be.data_ptr(), b.data_ptr(),
+                                    shift.data_ptr(), bprime.data_ptr(), rowsum.data_ptr(),
+                                    w.stride(0), rows, cols))
+        img = torch.empty(rows, kp, dtype=torch.bfloat16, device=w.device)
+        img_t = torch.empty(cols, rows, dtype=torch.bfloat16, device=w.device) if want_t else None
+        jobs.append(_lib.ImageJob(w.data_ptr(), img.data_ptr(),
+                                  img_t.data_ptr() if img_t is not None else None, rows, cols, kp,
+                                  w.stride(0), bd, g.data_ptr(), shift.data_ptr()))
+        keep += [w, b, g, be, shift]
+        out[i] = (img, img_t, bprime, rowsum)
+        _FOLD[w] = (key, out[i])
+    if preps:
+        require_device(*keep)
+        lib = _lib.load()
+        for k in range(0, len(preps), 16):
+            part = preps[k:k + 16]
+            check(lib.sc_ln_fold_prep((_lib.LnFoldJob * len(part))(*part), len(part),
+                                      stream_of(keep[0])), "sc_ln_fold_prep")
+        _image_jobs(jobs, keep)
+    return out
+
+
+def ln_fold_bwd(g, h, stat):
+    """dL/dh [M, D] bf16 of the folded LayerNorm's input h from g = dL/du W'' (sc_ln_fold_bwd)."""
+    M, D = h.shape
+    g = g.contiguous()
+    dh = torch.empty_like(h)
+    check(_lib.load().sc_ln_fold_bwd(ptr(g), ptr(h), dtype_code(h), ptr(stat), ptr(dh), M, D,
+                                     stream_of(h)), "sc_ln_fold_bwd")
+    return dh
+
+
+def ln_fold_wgrad(Mw, w, gamma, beta, dbp):
+    """(dW [rows, D], dgamma [D], dbeta [D]) from M = dL/dW'' and dL/db' (sc_ln_fold_wgrad)."""
+    rows, D = Mw.shape
+    lib = _lib.load()
+    dw = torch.empty(rows, D, dtype=torch.float32, device=Mw.device)
+    dgb = torch.empty(2, D, dtype=torch.float32, device=Mw.device)
+    ws = torch.empty(lib.sc_ln_fold_wgrad_workspace_numel(rows, D), dtype=torch.float32,
+                     device=Mw.device)
+    g = gamma.detach().contiguous()
+    be = beta.detach().contiguous()
+    wd = w.detach()
+    check(lib.sc_ln_fold_wgrad(ptr(Mw.contiguous()), ptr(wd), wd.stride(0), ptr(g), ptr(be),
+                               ptr(dbp.contiguous()), rows, D, ptr(dw), ptr(dgb), ptr(ws),
+                               stream_of(Mw)), "sc_ln_fold_wgrad")
+    return dw, dgb[0], dgb[1]
+
+
+class LucyCellLNFn(torch.autograd.Function):
+    """LayerNorm(h_prev) (lucyrnn_triton.py:96-97, :136-137) + one LucyRNN layer (LucyCellFn) as
+    ONE node, with the LayerNorm folded into the gate projection (csrc/ln_fold.hip): the GEMM
+    reads the previous layer's RAW bf16 output against W'' = centred (W diag gamma), and the
+    scan rebuilds LN(h) W^T + b as rstd (u - mean r) + b' on load, from the block records the
+    previous scan wrote.  No LayerNorm pass in either direction.  bf16 autocast only (the
+    weights come from fold_images).
+
+    Backward: the scan's dgates are rstd dL/dgate = dL/du; dL/dh = ln_fold_bwd(dL/du W'');
+    dL/dW'' = dgates^T h (split-L MFMA kernel) -> dW, dgamma, dbeta (ln_fold_wgrad); db = the
+    scan's dL/db' partial sums."""
+
+    @staticmethod
+    def forward(ctx, h2d, w, b, gamma, beta, h0, s0, B, T, fimgs, rec_in, eps, split_sink=None,
+                rec_sink=None):
+        ctx.set_materialize_grads(False)
+        D = w.shape[0] // 7
+        wg, wt, bprime, rowsum = fimgs
+        with _timed("gate_gemm_fwd", h2d, 0):
+            gates = proj_fwd(h2d, wg)
+        gates = gates.view(B, T, D // 64, 7, 64)
+        need = any(ctx.needs_input_grad)
+        stat = torch.empty(B, T, 2, dtype=torch.float32, device=h2d.device)
+        rec = None
+        if rec_sink is not None:
+            rec = torch.empty(B, T, D // 64, 2, dtype=torch.float32, device=h2d.device)
+            rec_sink.append(rec)
+        res = _scan_fwd(gates, h0, s0, need, bprime, want_h=True, split=split_sink is not None,
+                        ln=(rowsum, rec_in, stat, rec, eps))
+        gates, out, s_out, ckpt, h_out = res[:5]
+        if len(res) > 5:
+            split_sink.append(res[5])
+        if need:
+            ctx.save_for_backward(h2d, wt, gates, ckpt, bprime, rowsum, stat, w, gamma, beta)
+            ctx.dtypes = (h2d.dtype, w.dtype, h0.dtype, s0.dtype, gamma.dtype, beta.dtype)
+        return out, s_out, h_out
+
+    @staticmethod
+    def backward(ctx, dout, ds_last, dh_last):
+        h2d, wt, gates, ckpt, bprime, rowsum, stat, w, gamma, beta = ctx.saved_tensors
+        xdt, wdt, hdt, sdt, gdt, bdt = ctx.dtypes
+        if dh_last is not None:   # h_last is out[:, -1]: its gradient joins dout's last step
+            B, T = gates.shape[:2]
+            if dout is None:
+                dout = torch.zeros(B, T, dh_last.shape[-1], dtype=gates.dtype, device=gates.device)
+            else:
+                dout = dout.clone()
+            dout[:, -1] += dh_last.to(dout.dtype)
+        need_w = any(ctx.needs_input_grad[1:5])
+        dgates, dh0, ds0, dbias = _scan_bwd(gates, ckpt, dout, ds_last, need_w, bprime,
+                                            ln=(rowsum, stat))
+        dg2 = dgates.view(h2d.shape[0], -1)
+        D = h2d.shape[1]
+        dh = None
+        if ctx.needs_input_grad[0]:
+            with _timed("gate_gemm_dgrad", dg2, 0):
+                g = torch.matmul(dg2, wt.t())
+            dh = ln_fold_bwd(g, h2d, stat.view(-1, 2)).to(xdt)
+        dw = db = dgam = dbet = None
+        if need_w:
+            with _timed("gate_gemm_wgrad", dg2, 0):
+                Mw = wgrad_splitk(dg2, h2d, blocked_d=D)
+            dbp = colsum(dbias.view(dbias.shape[0], -1))
+            dw, dgam, dbet = ln_fold_wgrad(Mw, w, gamma, beta, dbp)
+            dw, db, dgam, dbet = dw.to(wdt), dbp.to(wdt), dgam.to(gdt), dbet.to(bdt)
+        return (dh, dw, db, dgam, dbet, dh0.to(hdt), ds0.to(sdt), None, None, None, None, None,
+                None, None)
+
+
+def lucy_cell_ln(h, w, b, gamma, beta, h0, s0, fimgs, rec_in, eps, split_sink=None, rec_sink=None):
+    """h [B,T,D] bf16 (the previous layer's raw output) -> (out, s_last, h_last) of
+    LayerNorm(gamma, beta, eps) + the cell (w, b), folded (LucyCellLNFn)."""
+    B, T, D = h.shape
+    h2 = h.reshape(B * T, D)
+    if not h2.is_contiguous() or h2.data_ptr() % 16:
+        h2 = h2.contiguous()
+    return LucyCellLNFn.apply(h2, w, b, gamma, beta, h0, s0, B, T, fimgs, rec_in, eps,
+                              split_sink, rec_sink)
 
 
 # ----------------------------------------------------------------------------- LayerNorm -----

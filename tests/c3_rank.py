@@ -13,8 +13,9 @@ Rank r initialises its model with seed 11 + 1000 r and runs one no-grad forward 
 wrap, so its cached bf16 weight images (ops.weight_images, keyed on the parameters' version
 counters) hold its OWN weights: DDP's start-up broadcast of rank 0's parameters must reach them.
 After every segment rank 0 gathers rank 1's flattened parameters and records whether they are
-bitwise its own.  OUT.pt holds the losses, those flags and the final parameters (rank 0 / the
-single process only)."""
+bitwise its own.  The gradients the first optimizer step sees (after DDP's all-reduce, before the
+HIP clip + Adam) are captured.  OUT.pt holds the losses, those flags, the captured gradients and
+the final parameters (rank 0 / the single process only)."""
 import os
 import sys
 
@@ -45,8 +46,17 @@ def main():
     if world > 1:
         dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
                                 world_size=world)
+    import statecatcher_amd.train as train_mod
     from statecatcher_amd.model import ASRModel, CTCLoss, build_lucyrnn_config
     from statecatcher_amd.train import SegmentTrainer
+    first_grads = []
+    orig_step = train_mod.clip_and_adam_step
+
+    def capture(opt, params, max_norm):   # the all-reduced gradients of the first update
+        if not first_grads:
+            first_grads.extend(p.grad.detach().float().cpu().clone() for p in params)
+        return orig_step(opt, params, max_norm)
+    train_mod.clip_and_adam_step = capture
     torch.manual_seed(11 + 1000 * rank)
     model = ASRModel(None, build_lucyrnn_config(80, 512, 6, V), vocab_size=V, feat_dim=80,
                      proj_dim=-1).to(dev)
@@ -80,6 +90,7 @@ def main():
     res = {"losses": losses, "ranks_bitwise_equal": equal}
     if rank == 0:
         res["params"] = [p.detach().cpu() for p in params]
+        res["grads"] = first_grads
     torch.save(res, out)
     if world > 1:
         dist.barrier()

@@ -175,24 +175,32 @@ def test_c3_two_ranks_on_one_gpu_equal_one_process_on_the_full_batch(accumulatio
     weight images from them before the DDP wrap, so DDP's start-up broadcast must reach the
     version-keyed image cache.  Done when:
       * both ranks' parameters are bitwise equal after every segment;
-      * the mean of the per-rank losses (each the mean of its sequences' nll / U) is the
-        full-batch loss (CTC 'mean' over equal shards), every segment;
-      * the final parameters match the single process's (relative Frobenius, per tensor; the
-        two runs differ only in reduction order: GEMM row counts, split-L slabs, the all-reduce).
+      * until the first optimizer step (identical weights), the mean of the per-rank losses (each
+        the mean of its sequences' nll / U) is the full-batch loss (CTC 'mean' over equal shards);
+      * the gradients that step applies -- all-reduced over the ranks, with rank 1's shard
+        computed from the broadcast weights -- are the full-batch gradients (relative Frobenius
+        per tensor; the two runs differ only in reduction order: GEMM row counts, split-L slabs,
+        the all-reduce).
+    After it the runs drift apart by Adam's sign normalisation of near-zero gradient elements
+    (each such element moves by +-lr whichever way reduction-order noise tips it), so later losses
+    and the final parameters are reported, not pinned.
     Accumulation 1 and 2 (no_sync on the accumulating segments)."""
     single = _run_ranks(1, accumulation, tmp_path)[0]
     r0, r1 = _run_ranks(2, accumulation, tmp_path)
     assert r0["ranks_bitwise_equal"] == [True] * 4 and r1["ranks_bitwise_equal"] == [True] * 4
     loss_err = [abs((a + b) / 2 - s) / abs(s) for a, b, s in
                 zip(r0["losses"], r1["losses"], single["losses"])]
-    p_err = [float((a.double() - b.double()).norm() / b.double().norm())
+    g_err = [float((a.double() - b.double()).norm() / max(float(b.double().norm()), 1e-30))
+             for a, b in zip(r0["grads"], single["grads"])]
+    p_err = [float((a.double() - b.double()).norm() / max(float(b.double().norm()), 1e-30))
              for a, b in zip(r0["params"], single["params"])]
     print(f"C3 2 ranks acc={accumulation}: losses {r0['losses']} / {r1['losses']} vs "
-          f"{single['losses']}; loss rel {['%.1e' % e for e in loss_err]}; param rel max "
-          f"{max(p_err):.2e}")
-    assert loss_err[0] <= 1e-5, loss_err   # identical weights: reduction order only
-    assert max(loss_err) <= 1e-4, loss_err
-    assert max(p_err) <= 1e-5, p_err
+          f"{single['losses']}; loss rel {['%.1e' % e for e in loss_err]}; first-update gradient "
+          f"rel max {max(g_err):.2e} ({len(g_err)} tensors); final param rel max {max(p_err):.2e}")
+    assert len(g_err) == len(r0["params"])
+    for e in loss_err[:accumulation]:   # identical weights: reduction order only
+        assert e <= 1e-5, loss_err
+    assert max(g_err) <= 1e-5, g_err
 
 
 def test_rccl_allreduce_of_a_gradient_sized_buffer(rccl_group):

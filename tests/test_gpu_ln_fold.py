@@ -1,0 +1,173 @@
+"""GPU parity of the inter-layer LayerNorm folded into the next gate projection (csrc/ln_fold.hip,
+sc_lucy_scan_fwd_ln / _bwd_ln, ops.LucyCellLNFn), which replaces nn.LayerNorm +
+LinearSafe (lucyrnn_triton.py:96-97, :136-137, :20-25) under bf16 autocast.
+
+* The folded images (W'' = bf16(gamma W - shift)), b' and r against torch on the same fp32
+  values.
+* One LayerNorm + LucyRNN layer, fold against the unfused bf16 path (LayerNorm kernel -> bf16 ->
+  gate GEMM -> scan) and both against the fp32 path of the same module: the fold is at least as
+  close to fp32 as the unfused bf16 path (2x + floor), outputs, states and every gradient
+  (d input, dW, db, dgamma, dbeta, dh0, ds0).
+* A 6 x 512 stack under autocast, fold vs unfused: loss, logits and every parameter gradient
+  (cosine >= 0.999, norm within 1%)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0") if torch.cuda.is_available() else None
+
+
+def ops():
+    from statecatcher_amd import ops as o
+    return o
+
+
+def rel(a, b):
+    a, b = a.double(), b.double()
+    return float((a - b).norm() / max(float(b.norm()), 1e-30))
+
+
+def cos(a, b):
+    a, b = a.double().flatten(), b.double().flatten()
+    return float((a @ b) / max(float(a.norm() * b.norm()), 1e-30))
+
+
+def test_fold_images_match_torch():
+    g = torch.Generator().manual_seed(1)
+    D = 512
+    w = (torch.randn(7 * D, D, generator=g) * 0.03).to(DEV)
+    b = (torch.randn(7 * D, generator=g) * 0.1).to(DEV)
+    gam = (1.0 + 0.2 * torch.randn(D, generator=g)).to(DEV)
+    bet = (0.1 * torch.randn(D, generator=g)).to(DEV)
+    (img, img_t, bprime, rowsum), = ops().fold_images([(w, b, gam, bet, D, D, True)])
+    torch.cuda.synchronize()
+    gw = gam * w                                   # exact fp32 products, as the kernels form them
+    shift = gw.double().mean(1)
+    ref = (gw - shift.float().unsqueeze(1)).to(torch.bfloat16)
+    got = ops().step_blocked_rows(img, D, inverse=True)
+    # one shift's last-bit difference (summation order) may move a rounding boundary
+    assert (got.float() - ref.float()).abs().max() <= 2.0 ** -7 * ref.float().abs().max()
+    assert (got != ref).float().mean() < 1e-4
+    assert torch.equal(img_t, img.t())
+    torch.testing.assert_close(bprime.double(), (b.double() + w.double() @ bet.double()),
+                               rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(rowsum.double(), got.double().sum(1), rtol=0, atol=1e-6)
+    assert float(rowsum.abs().max()) < 1e-2 * float(gw.abs().sum(1).max())
+
+
+def _layer_pair(D=512, B=2, T=200, seed=3):
+    """(module with 2 layers, input x [B,T,80]) at a trained-like spread of LN parameters."""
+    from statecatcher_amd import LucyRNNConfig, LucyRNNtriton
+    torch.manual_seed(seed)
+    cfg = LucyRNNConfig(input_dim=80, hidden_dim=D, num_layers=2, vocab_size=128, fused_ops=True,
+                        layer_norm=False)
+    m = LucyRNNtriton(cfg).to(DEV)
+    with torch.no_grad():
+        m.norms[0][0].weight.normal_(1.0, 0.2)
+        m.norms[0][0].bias.normal_(0.0, 0.1)
+        m.output_proj.weight.normal_(0, 0.05)
+    x = torch.randn(B, T, 80, device=DEV)
+    return m, x
+
+
+def _run(m, x, autocast):
+    m.zero_grad(set_to_none=True)
+    xd = x.clone().requires_grad_(True)
+    B, D = x.shape[0], m.config.hidden_dim
+    h0 = [[torch.randn(B, D, device=DEV, generator=torch.Generator(DEV).manual_seed(5 + l))
+           .requires_grad_(True) for l in range(2)]]
+    s0 = [[torch.randn(B, D, device=DEV, generator=torch.Generator(DEV).manual_seed(9 + l))
+           .requires_grad_(True) for l in range(2)]]
+    R = torch.randn(x.shape[0], x.shape[1], m.config.vocab_size, device=DEV,
+                    generator=torch.Generator(DEV).manual_seed(7))
+    with torch.autocast("cuda", dtype=torch.bfloat16, enabled=autocast):
+        logits, (fh, fs) = m(xd, ([h0[0][:]], [s0[0][:]]))
+        loss = (logits.float() * R).sum() + fh[0][1].sum() + fs[0][1].square().sum()
+    loss.backward()
+    out = {"logits": logits.detach().float(), "h_last": fh[0][1].detach().float(),
+           "s_last": fs[0][1].detach().float(), "dx": xd.grad.float(),
+           "dh0_1": h0[0][1].grad.float(), "ds0_1": s0[0][1].grad.float()}
+    for n, p in m.named_parameters():
+        out["d " + n] = p.grad.detach().float().clone()
+    return out
+
+
+def test_fold_layer_vs_unfused_and_fp32(monkeypatch):
+    m, x = _layer_pair()
+    ref32 = _run(m, x, autocast=False)
+    folded = _run(m, x, autocast=True)
+    monkeypatch.setattr(ops(), "USE_LN_FOLD", False)
+    plain = _run(m, x, autocast=True)
+    lines = []
+    for k in ref32:
+        ef, ep = rel(folded[k], ref32[k]), rel(plain[k], ref32[k])
+        lines.append(f"{k}: fold {ef:.2e} unfused {ep:.2e} (cos {cos(folded[k], plain[k]):.5f})")
+        assert ef <= max(2.0 * ep, 5e-3), (k, ef, ep)
+        assert cos(folded[k], plain[k]) >= 0.999, k
+    print("LN fold vs fp32 (rel. Frobenius): " + "; ".join(lines))
+
+
+def test_fold_engaged_and_no_layernorm_launch(monkeypatch):
+    """The bf16 forward of a 3-layer stack takes LucyCellLNFn for layers 1 and 2 and never
+    launches the LayerNorm kernel."""
+    from statecatcher_amd import LucyRNNConfig, LucyRNNtriton
+    calls = {"ln": 0, "fold": 0}
+    o = ops()
+    orig_ln, orig_fold = o.LayerNormFn.apply, o.LucyCellLNFn.apply
+
+    def ln(*a):
+        calls["ln"] += 1
+        return orig_ln(*a)
+
+    def fold(*a):
+        calls["fold"] += 1
+        return orig_fold(*a)
+    monkeypatch.setattr(o.LayerNormFn, "apply", ln)
+    monkeypatch.setattr(o.LucyCellLNFn, "apply", fold)
+    torch.manual_seed(0)
+    m = LucyRNNtriton(LucyRNNConfig(input_dim=80, hidden_dim=512, num_layers=3, vocab_size=64,
+                                    fused_ops=True, layer_norm=False)).to(DEV)
+    x = torch.randn(1, 64, 80, device=DEV)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        m(x)
+    assert calls == {"ln": 0, "fold": 2}
+
+
+def test_c2_stack_fold_vs_unfused(monkeypatch):
+    """6 x 512, V = 1024, T = 1500, B = 2 under bf16 autocast with the CTC criterion: every
+    parameter gradient of the folded stack against the unfused one."""
+    from statecatcher_amd.model import ASRModel, CTCLoss, build_lucyrnn_config, compute_loss
+    torch.manual_seed(11)
+    V, B, T = 1024, 2, 1500
+    model = ASRModel(None, build_lucyrnn_config(80, 512, 6, V), vocab_size=V, feat_dim=80,
+                     proj_dim=-1).to(DEV)
+    with torch.no_grad():
+        model.encoder.output_proj.weight.normal_(0, 0.02)
+        for ln in model.encoder.norms[0]:
+            ln.weight.normal_(1.0, 0.1)
+            ln.bias.normal_(0.0, 0.05)
+    g = torch.Generator().manual_seed(7)
+    feats = torch.randn(B, T, 80, generator=g).to(DEV)
+    tok = torch.randint(1, V, (B, 150), generator=g).to(DEV)
+    crit = CTCLoss(blank=0, zero_infinity=True)
+
+    def run():
+        model.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            loss, _, _, _ = compute_loss("ctc", crit, model, feats,
+                                         torch.ones(B, T, dtype=torch.bool, device=DEV), tok,
+                                         [T, T], [150, 97], 0)
+        loss.backward()
+        return float(loss), {n: p.grad.detach().clone() for n, p in model.named_parameters()}
+    lf, gf = run()
+    monkeypatch.setattr(ops(), "USE_LN_FOLD", False)
+    lp, gp = run()
+    print(f"C2 stack loss fold {lf:.6f} unfused {lp:.6f}")
+    assert abs(lf - lp) <= 1e-3 * abs(lp)
+    worst = []
+    for n in gp:
+        c, r = cos(gf[n], gp[n]), float(gf[n].norm() / gp[n].norm())
+        worst.append((c, r, n))
+        assert c >= 0.999 and abs(r - 1) <= 0.01, (n, c, r)
+    worst.sort()
+    print("lowest cosines: " + "; ".join(f"{n} {c:.5f} ({r:.4f})" for c, r, n in worst[:4]))

@@ -1,14 +1,16 @@
 #!/usr/bin/env python3
 """Per-launch HBM traffic of the scan and mLSTM kernels from two rocprofv3 PMC passes.
 
-usage: tools/pmc_traffic.py FETCH_counter_collection.csv WRITE_counter_collection.csv [out.json]
+usage: tools/pmc_traffic.py FETCH_counter_collection.csv WRITE_counter_collection.csv [out.json KEY]
 
 FETCH_SIZE / WRITE_SIZE are in KiB per dispatch.  On gfx950 FETCH_SIZE reports half the bytes of
 a 16-byte-per-lane streaming read (MI355X_MICROARCH.md, HBM section); the scans read every gate
 byte with 16-byte LDS-DMA pieces, so fetch bytes = 2 x FETCH_SIZE x 1024.  WRITE_SIZE is taken
 as is (calibrated on the scan forward: its 52 MB of bf16 output + checkpoint read back exactly).
-Writes JSON {bench_kernel_name: {"hbm_bytes_per_launch", "fetch_bytes", "write_bytes",
-"dispatches"}} keyed like bench.py's "kernels" entries.
+Prints JSON {bench_kernel_name: {"hbm_bytes_per_launch", "fetch_bytes", "write_bytes",
+"dispatches"}} keyed like bench.py's "kernels" entries; with out.json, merges it into that table
+under KEY = "<workload>/<dtype>" of the profiled bench run (e.g. "ctc/bf16"), which is what
+bench.py's roofline.traffic looks up (no entry for the run's workload and dtype: null).
 """
 import csv
 import json
@@ -48,12 +50,14 @@ def main():
         out[name] = {"hbm_bytes_per_launch": round(f + w), "fetch_bytes": round(f),
                      "write_bytes": round(w), "dispatches": fetch[name][1]}
     if len(sys.argv) > 3:
-        # merge into an existing table (passes over different workloads fill different kernels)
+        key = sys.argv[4]
+        if "/" not in key:
+            sys.exit("KEY must be <workload>/<dtype>, e.g. ctc/bf16")
         try:
             prev = json.load(open(sys.argv[3]))
         except (OSError, ValueError):
             prev = {}
-        prev.update(out)
+        prev.setdefault(key, {}).update(out)
         out = prev
     txt = json.dumps(out, indent=1)
     if len(sys.argv) > 3:

@@ -1,9 +1,21 @@
 #!/bin/bash
-# Round-5 focused GPU tests (the changed areas), then the same-box drift A/B.
+# Round-5 focused GPU run: the given test files (default: the changed areas), then optionally
+# (AB=1) the LN-fold A/B bench pair, (DRIFT=1) the same-box drift A/B.  Every GPU step has its
+# own time limit; the first failure ends the call.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; mkdir -p gpurun_out
-timeout -k 10 600 python3 -u -m pytest -x -v --timeout 150 --timeout-method thread \
-  tests/test_gpu_ctc.py tests/test_gpu_rnnt_joint.py tests/test_gpu_rnnt.py tests/test_gpu_mlstm.py \
-  tests/test_gpu_ddp.py tests/test_gpu_ctc_head.py -s > gpurun_out/r5a_tests.log 2>&1
-rc=$?; tail -5 gpurun_out/r5a_tests.log; [ $rc -eq 0 ] || exit $rc
-if [ -n "$DRIFT" ]; then bash tools/drift_ab.sh r5a; fi
+TAG=${TAG:-r5}
+TESTS=${TESTS:-"tests/test_gpu_ln_fold.py tests/test_gpu_ddp.py"}
+timeout -k 10 900 python3 -u -m pytest -x -v -s --timeout 200 --timeout-method thread $TESTS \
+  > gpurun_out/${TAG}_tests.log 2>&1
+rc=$?; tail -4 gpurun_out/${TAG}_tests.log; [ $rc -eq 0 ] || exit $rc
+if [ -n "$AB" ]; then
+  for rnd in 1 2; do
+    for v in 1 0; do
+      SC_LN_FOLD=$v timeout -k 10 300 python3 bench.py --cpu-baseline off > gpurun_out/${TAG}_ab_fold${v}_$rnd.json \
+        2> gpurun_out/${TAG}_ab_fold${v}_$rnd.err || { echo "bench failed"; tail -20 gpurun_out/${TAG}_ab_fold${v}_$rnd.err; exit 1; }
+      python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[1], d['value'], d['ms_per_step'], {k: v['avg_us'] for k, v in d['kernels'].items()})" gpurun_out/${TAG}_ab_fold${v}_$rnd.json
+    done
+  done
+fi
+if [ -n "$DRIFT" ]; then bash tools/drift_ab.sh $TAG; fi
