@@ -40,10 +40,8 @@ struct FoldPrepTable {
 };
 
 // gamma_k W_nk - shift_n rounded as the weight image rounds it (optim.hip images_kernel): both
-// sides use this one expression, unfused
-__device__ __forceinline__ float fold_elem(float g, float w, float m) {
-  return __fsub_rn(__fmul_rn(g, w), m);
-}
+// sides use this one expression, unfused (sc_common.h mul_sub_rn)
+__device__ __forceinline__ float fold_elem(float g, float w, float m) { return mul_sub_rn(g, w, m); }
 
 __global__ void __launch_bounds__(256) ln_fold_prep_kernel(FoldPrepTable t) {
   const int wg = blockIdx.x;
@@ -56,7 +54,7 @@ __global__ void __launch_bounds__(256) ln_fold_prep_kernel(FoldPrepTable t) {
   const float* wr = j.w + (int64_t)n * j.ld;
   float gw = 0.0f, wb = 0.0f;
   for (int k = lane; k < j.D; k += 64) {
-    gw += __fmul_rn(j.gamma[k], wr[k]);
+    gw += mul_sub_rn(j.gamma[k], wr[k], 0.0f);
     wb = fmaf(wr[k], j.beta[k], wb);
   }
   const float m = wave_sum_dpp(gw) / (float)j.D;

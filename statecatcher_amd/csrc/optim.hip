@@ -199,8 +199,7 @@ __global__ void __launch_bounds__(kThreads) images_kernel(ImageTable t) {
     // (folded LayerNorm: col_scale[c] src - row_shift[sr], unfused as sc_ln_fold_prep's rowsum)
     const float sh = j.row_shift ? j.row_shift[sr] : 0.0f;
     auto val = [&](float x, int64_t cc) {
-      if (j.col_scale) x = __fmul_rn(j.col_scale[cc], x);
-      return j.row_shift ? __fsub_rn(x, sh) : x;
+      return j.col_scale ? mul_sub_rn(j.col_scale[cc], x, sh) : x - sh;
     };
     if (c + 16 <= j.cols && (((uintptr_t)(src + c)) & 15) == 0) {
 #pragma unroll

@@ -214,6 +214,14 @@ __device__ __forceinline__ void settle(float (&v)[N]) {
 #pragma unroll
   for (int i = 0; i < N; ++i) asm volatile("" : "+v"(v[i]));
 }
+// g * w - m with the product rounded on its own (an opaque v_mul_f32: hipcc's default fp-contract
+// would fuse it into an fma in one kernel and not in another).  Kernels that must round a value
+// identically (the folded LayerNorm's weight image and its row sums) share this one expression.
+__device__ __forceinline__ float mul_sub_rn(float g, float w, float m) {
+  float p;
+  asm volatile("v_mul_f32 %0, %1, %2" : "=v"(p) : "v"(g), "v"(w));
+  return p - m;
+}
 __device__ __forceinline__ void dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 // Retire every DMA but the N youngest vector-memory LOADS.  Loads complete in issue order among
 // themselves; stores may complete out of order with them, but they only make the counter larger:

@@ -46,7 +46,7 @@ typedef float f4v __attribute__((ext_vector_type(4)));
 typedef int i4v __attribute__((ext_vector_type(4)));
 
 // SC_TN_ABL (tools timing only, never in a shipped build): 1 no MFMAs, 2 no DMA after the
-// prologue (wrong results)
+// prologue, 4 no output stores (tn256) (wrong results)
 #ifndef SC_TN_ABL
 #define SC_TN_ABL 0
 #endif
@@ -271,15 +271,25 @@ __global__ void __launch_bounds__(512) tn_kernel(TnArgs a) {
 // complete in order among themselves): the wait stays exact.
 constexpr int kHalfB = 128 * kRowB;   // one operand half: 128 rows x 128 B
 
+// Wave layout over a 128 x 128 quadrant.  SC_TN_WL = 0: 2 (rows) x 4 (columns) waves of 64 x 32,
+// a lane's row fragment covers 8 consecutive columns (one 16-byte store; a 128-byte output line
+// takes stores from two waves).  SC_TN_WL = 1: 4 x 2 waves of 32 x 64, 16 consecutive columns per
+// lane (two 16-byte stores back to back, every output line written whole by one wave).
+#ifndef SC_TN_WL
+#define SC_TN_WL 0
+#endif
+constexpr int kTnWN = SC_TN_WL ? 2 : 4;        // waves along the columns
+constexpr int kTnMF = 128 / (8 / kTnWN) / 16;  // row fragments per wave (4 or 2)
+constexpr int kTnNF = 128 / kTnWN / 16;        // column fragments per wave (2 or 4)
 // MFMA fragment sets of one operand half, named (static indexing only: rule 20)
-struct FragA { i4v v[4][2]; };   // 4 row fragments (x rows) x 2 k-steps
-struct FragB { i4v v[2][2]; };   // 2 column fragments (W rows) x 2 k-steps
+struct FragA { i4v v[kTnMF][2]; };   // row fragments (x rows) x 2 k-steps
+struct FragB { i4v v[kTnNF][2]; };   // column fragments (W rows) x 2 k-steps
 
 __global__ void __launch_bounds__(512, 1) tn256_kernel(TnArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int lane = threadIdx.x & 63;
   const int w = uniform(threadIdx.x >> 6);
-  const int wm = w >> 2, wn = w & 3;
+  const int wm = w / kTnWN, wn = w % kTnWN;
   const int l15 = lane & 15, l4 = lane >> 4;
 
   const int G = gridDim.x, bid = blockIdx.x;
@@ -327,17 +337,17 @@ __global__ void __launch_bounds__(512, 1) tn256_kernel(TnArgs a) {
   };
 
   // ---- fragment reads (byte offsets within a half; k-step kk flips address bit 6) ----
-  uint32_t offA[4], offB[2];
+  uint32_t offA[kTnMF], offB[kTnNF];
 #pragma unroll
-  for (int mf = 0; mf < 4; ++mf) {
-    const int r = wm * 64 + mf * 16 + l15;
+  for (int mf = 0; mf < kTnMF; ++mf) {
+    const int r = wm * 16 * kTnMF + mf * 16 + l15;
     offA[mf] = (uint32_t)(r * kRowB + 16 * (l4 ^ swz(r)));
   }
 #pragma unroll
-  for (int nf = 0; nf < 2; ++nf) {
-    // W row for MFMA row i = l15 of column fragment nf: the lane's 2 x 4 accumulator values
-    // then hold output columns wn*32 + l4*8 + 0..7 (one 16-byte store per row fragment)
-    const int r = wn * 32 + (l15 >> 2) * 8 + nf * 4 + (l15 & 3);
+  for (int nf = 0; nf < kTnNF; ++nf) {
+    // W row for MFMA row i = l15 of column fragment nf: the lane's NF x 4 accumulator values
+    // then hold output columns wn*16NF + l4*4NF + 0..4NF-1 (NF/2 16-byte stores per row fragment)
+    const int r = wn * 16 * kTnNF + (l15 >> 2) * 4 * kTnNF + nf * 4 + (l15 & 3);
     offB[nf] = (uint32_t)(r * kRowB + 16 * (l4 ^ swz(r)));
   }
   auto half_base = [&](int buf, int h) __attribute__((always_inline)) {
@@ -348,31 +358,31 @@ __global__ void __launch_bounds__(512, 1) tn256_kernel(TnArgs a) {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-      for (int mf = 0; mf < 4; ++mf) f.v[mf][kk] = lds_read16(hb + (offA[mf] ^ (64u * kk)));
+      for (int mf = 0; mf < kTnMF; ++mf) f.v[mf][kk] = lds_read16(hb + (offA[mf] ^ (64u * kk)));
   };
   auto read_B = [&](int buf, int qn, FragB& f) __attribute__((always_inline)) {
     const uint32_t hb = half_base(buf, 2 + qn);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-      for (int nf = 0; nf < 2; ++nf) f.v[nf][kk] = lds_read16(hb + (offB[nf] ^ (64u * kk)));
+      for (int nf = 0; nf < kTnNF; ++nf) f.v[nf][kk] = lds_read16(hb + (offB[nf] ^ (64u * kk)));
   };
 
-  f4v acc[4][4][2];   // [quadrant (0,0) (0,1) (1,1) (1,0)][row frag][col frag]
+  f4v acc[4][kTnMF][kTnNF];   // [quadrant (0,0) (0,1) (1,1) (1,0)][row frag][col frag]
 #pragma unroll
   for (int q = 0; q < 4; ++q)
 #pragma unroll
-    for (int mf = 0; mf < 4; ++mf)
+    for (int mf = 0; mf < kTnMF; ++mf)
 #pragma unroll
-      for (int nf = 0; nf < 2; ++nf) acc[q][mf][nf] = f4v{0.f, 0.f, 0.f, 0.f};
-  auto quad = [&](f4v (&c)[4][2], const FragA& fa, const FragB& fb) __attribute__((always_inline)) {
+      for (int nf = 0; nf < kTnNF; ++nf) acc[q][mf][nf] = f4v{0.f, 0.f, 0.f, 0.f};
+  auto quad = [&](f4v (&c)[kTnMF][kTnNF], const FragA& fa, const FragB& fb) __attribute__((always_inline)) {
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-      for (int mf = 0; mf < 4; ++mf)
+      for (int mf = 0; mf < kTnMF; ++mf)
 #pragma unroll
-        for (int nf = 0; nf < 2; ++nf) {
+        for (int nf = 0; nf < kTnNF; ++nf) {
           if (SC_TN_ABL & 1)
             c[mf][nf][0] += (float)(fb.v[nf][kk][0] ^ fa.v[mf][kk][1]);
           else
@@ -385,21 +395,26 @@ __global__ void __launch_bounds__(512, 1) tn256_kernel(TnArgs a) {
 
   // ---- epilogue: one quadrant (4 row fragments x one 16-byte store), then zeroed ----
   const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(a.C, 0, a.cbytes, 0x00020000);
-  auto store_quad = [&](f4v (&c)[4][2], int m0, int n0, int qm, int qn) __attribute__((always_inline)) {
-    const uint32_t row = (uint32_t)(m0 + qm * 128 + wm * 64 + l15);
-    const uint32_t col = (uint32_t)(n0 + qn * 128 + wn * 32 + l4 * 8);
+  auto store_quad = [&](f4v (&c)[kTnMF][kTnNF], int m0, int n0, int qm, int qn) __attribute__((always_inline)) {
+    if (SC_TN_ABL & 4) return;   // (ablation: no output stores)
+    const uint32_t row = (uint32_t)(m0 + qm * 128 + wm * 16 * kTnMF + l15);
+    const uint32_t col = (uint32_t)(n0 + qn * 128 + wn * 16 * kTnNF + l4 * 4 * kTnNF);
 #pragma unroll
-    for (int mf = 0; mf < 4; ++mf) {
-      i4v v;
+    for (int mf = 0; mf < kTnMF; ++mf) {
 #pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        const int nf = d >> 1, j = 2 * (d & 1);
-        const b2v p = {(__bf16)c[mf][nf][j], (__bf16)c[mf][nf][j + 1]};
-        v[d] = __builtin_bit_cast(int, p);
+      for (int s2 = 0; s2 < kTnNF / 2; ++s2) {   // 8 consecutive columns per 16-byte store
+        i4v v;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          const int nf = 2 * s2 + (d >> 1), j = 2 * (d & 1);
+          const b2v p = {(__bf16)c[mf][nf][j], (__bf16)c[mf][nf][j + 1]};
+          v[d] = __builtin_bit_cast(int, p);
+        }
+        __builtin_amdgcn_raw_buffer_store_b128(v, crs, ((row + 16u * mf) * a.ldc + col + 8u * s2) * 2u,
+                                               0, 0);
       }
-      __builtin_amdgcn_raw_buffer_store_b128(v, crs, ((row + 16u * mf) * a.ldc + col) * 2u, 0, 0);
 #pragma unroll
-      for (int nf = 0; nf < 2; ++nf) c[mf][nf] = f4v{0.f, 0.f, 0.f, 0.f};
+      for (int nf = 0; nf < kTnNF; ++nf) c[mf][nf] = f4v{0.f, 0.f, 0.f, 0.f};
     }
   };
 

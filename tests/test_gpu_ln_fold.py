@@ -98,13 +98,14 @@ def test_fold_layer_vs_unfused_and_fp32(monkeypatch):
     folded = _run(m, x, autocast=True)
     monkeypatch.setattr(ops(), "USE_LN_FOLD", False)
     plain = _run(m, x, autocast=True)
-    lines = []
+    lines, bad = [], []
     for k in ref32:
         ef, ep = rel(folded[k], ref32[k]), rel(plain[k], ref32[k])
-        lines.append(f"{k}: fold {ef:.2e} unfused {ep:.2e} (cos {cos(folded[k], plain[k]):.5f})")
-        assert ef <= max(2.0 * ep, 5e-3), (k, ef, ep)
-        assert cos(folded[k], plain[k]) >= 0.999, k
+        lines.append(f"{k}: fold {ef:.2e} unfused {ep:.2e}")
+        if ef > max(1.5 * ep, 5e-3):   # (both carry bf16 noise of their own rounding points)
+            bad.append((k, ef, ep))
     print("LN fold vs fp32 (rel. Frobenius): " + "; ".join(lines))
+    assert not bad, bad
 
 
 def test_fold_engaged_and_no_layernorm_launch(monkeypatch):

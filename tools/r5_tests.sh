@@ -19,3 +19,12 @@ if [ -n "$AB" ]; then
   done
 fi
 if [ -n "$DRIFT" ]; then bash tools/drift_ab.sh $TAG; fi
+if [ -n "$TNABL" ]; then
+  for v in cur tn4 tn3 tn1; do
+    echo "== $v"
+    if [ "$v" = cur ]; then L=""; else L=$R/tools/ab/$v/libstatecatcher_hip.so; fi
+    SC_LIB_PATH=$L timeout -k 10 200 python3 -u tools/tn_bench.py --tm 256 > gpurun_out/${TAG}_tn_$v.log 2>&1 \
+      || { echo "tn bench failed"; tail -5 gpurun_out/${TAG}_tn_$v.log; exit 1; }
+    grep -i "layer-0" gpurun_out/${TAG}_tn_$v.log
+  done
+fi
