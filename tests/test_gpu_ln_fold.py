@@ -6,10 +6,12 @@ LinearSafe (lucyrnn_triton.py:96-97, :136-137, :20-25) under bf16 autocast.
   values.
 * One LayerNorm + LucyRNN layer, fold against the unfused bf16 path (LayerNorm kernel -> bf16 ->
   gate GEMM -> scan) and both against the fp32 path of the same module: the fold is at least as
-  close to fp32 as the unfused bf16 path (2x + floor), outputs, states and every gradient
+  close to fp32 as the unfused bf16 path (1.5x + floor), outputs, states and every gradient
   (d input, dW, db, dgamma, dbeta, dh0, ds0).
-* A 6 x 512 stack under autocast, fold vs unfused: loss, logits and every parameter gradient
-  (cosine >= 0.999, norm within 1%)."""
+* A 6 x 512 stack (config C2's model) under autocast: loss and every parameter gradient of the
+  fold against fp32, no further than the unfused bf16 stack (2x + floor).
+Both use conditioned gates (condition_): at xavier init the reference's gate normalisation makes
+any two precisions of the model differ at O(1) (tests/test_gpu_model.py's docstring)."""
 import pytest
 import torch
 
@@ -55,6 +57,19 @@ def test_fold_images_match_torch():
     assert float(rowsum.abs().max()) < 1e-2 * float(gw.abs().sum(1).max())
 
 
+def condition_(m, D, gen):
+    """Well-conditioned gates (tests/test_gpu_model.py's module docstring): the reference's
+    x / sqrt(x^2 + 1e-6) gate normalisation flips any gate within ~1e-5 of zero between two
+    precisions, so at xavier init bf16 and fp32 runs of one model differ by O(1) after a few
+    layers.  |bias| = 3 on z, k, v, h_pre, decay, alpha keeps them away from zero."""
+    with torch.no_grad():
+        for cell in m.tracks[0]:
+            W, b = cell.linear.weight.view(7, D, -1), cell.linear.bias.view(7, D)
+            for gi in (1, 2, 3, 4, 5, 6):
+                W[gi] *= 0.1
+                b[gi] = 3.0 * (torch.randint(0, 2, (D,), generator=gen).float() * 2 - 1).to(b.device)
+
+
 def _layer_pair(D=512, B=2, T=200, seed=3):
     """(module with 2 layers, input x [B,T,80]) at a trained-like spread of LN parameters."""
     from statecatcher_amd import LucyRNNConfig, LucyRNNtriton
@@ -62,6 +77,7 @@ def _layer_pair(D=512, B=2, T=200, seed=3):
     cfg = LucyRNNConfig(input_dim=80, hidden_dim=D, num_layers=2, vocab_size=128, fused_ops=True,
                         layer_norm=False)
     m = LucyRNNtriton(cfg).to(DEV)
+    condition_(m, D, torch.Generator().manual_seed(seed + 100))
     with torch.no_grad():
         m.norms[0][0].weight.normal_(1.0, 0.2)
         m.norms[0][0].bias.normal_(0.0, 0.1)
@@ -74,9 +90,9 @@ def _run(m, x, autocast):
     m.zero_grad(set_to_none=True)
     xd = x.clone().requires_grad_(True)
     B, D = x.shape[0], m.config.hidden_dim
-    h0 = [[torch.randn(B, D, device=DEV, generator=torch.Generator(DEV).manual_seed(5 + l))
+    h0 = [[(0.5 * torch.randn(B, D, device=DEV, generator=torch.Generator(DEV).manual_seed(5 + l)))
            .requires_grad_(True) for l in range(2)]]
-    s0 = [[torch.randn(B, D, device=DEV, generator=torch.Generator(DEV).manual_seed(9 + l))
+    s0 = [[(0.5 * torch.randn(B, D, device=DEV, generator=torch.Generator(DEV).manual_seed(9 + l)))
            .requires_grad_(True) for l in range(2)]]
     R = torch.randn(x.shape[0], x.shape[1], m.config.vocab_size, device=DEV,
                     generator=torch.Generator(DEV).manual_seed(7))
@@ -135,13 +151,15 @@ def test_fold_engaged_and_no_layernorm_launch(monkeypatch):
 
 
 def test_c2_stack_fold_vs_unfused(monkeypatch):
-    """6 x 512, V = 1024, T = 1500, B = 2 under bf16 autocast with the CTC criterion: every
-    parameter gradient of the folded stack against the unfused one."""
+    """6 x 512, V = 1024, T = 1500, B = 2 with the CTC criterion, conditioned gates: the loss and
+    every parameter gradient of the folded bf16 stack against the fp32 run of the same model, no
+    further from it than the unfused bf16 stack is (2x + floor)."""
     from statecatcher_amd.model import ASRModel, CTCLoss, build_lucyrnn_config, compute_loss
     torch.manual_seed(11)
     V, B, T = 1024, 2, 1500
     model = ASRModel(None, build_lucyrnn_config(80, 512, 6, V), vocab_size=V, feat_dim=80,
                      proj_dim=-1).to(DEV)
+    condition_(model.encoder, 512, torch.Generator().manual_seed(12))
     with torch.no_grad():
         model.encoder.output_proj.weight.normal_(0, 0.02)
         for ln in model.encoder.norms[0]:
@@ -152,23 +170,27 @@ def test_c2_stack_fold_vs_unfused(monkeypatch):
     tok = torch.randint(1, V, (B, 150), generator=g).to(DEV)
     crit = CTCLoss(blank=0, zero_infinity=True)
 
-    def run():
+    def run(amp):
         model.zero_grad(set_to_none=True)
-        with torch.autocast("cuda", dtype=torch.bfloat16):
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
             loss, _, _, _ = compute_loss("ctc", crit, model, feats,
                                          torch.ones(B, T, dtype=torch.bool, device=DEV), tok,
                                          [T, T], [150, 97], 0)
         loss.backward()
         return float(loss), {n: p.grad.detach().clone() for n, p in model.named_parameters()}
-    lf, gf = run()
+    l32, g32 = run(False)
+    lf, gf = run(True)
     monkeypatch.setattr(ops(), "USE_LN_FOLD", False)
-    lp, gp = run()
-    print(f"C2 stack loss fold {lf:.6f} unfused {lp:.6f}")
-    assert abs(lf - lp) <= 1e-3 * abs(lp)
-    worst = []
-    for n in gp:
-        c, r = cos(gf[n], gp[n]), float(gf[n].norm() / gp[n].norm())
-        worst.append((c, r, n))
-        assert c >= 0.999 and abs(r - 1) <= 0.01, (n, c, r)
-    worst.sort()
-    print("lowest cosines: " + "; ".join(f"{n} {c:.5f} ({r:.4f})" for c, r, n in worst[:4]))
+    lp, gp = run(True)
+    print(f"C2 stack loss fp32 {l32:.6f} fold {lf:.6f} unfused {lp:.6f}")
+    assert abs(lf - l32) <= max(2 * abs(lp - l32), 1e-3 * abs(l32))
+    errs, bad = [], []
+    for n in g32:
+        ef, ep = rel(gf[n], g32[n]), rel(gp[n], g32[n])
+        errs.append((ef, ep, n))
+        if ef > max(2.0 * ep, 2e-2):
+            bad.append((n, ef, ep))
+    errs.sort(reverse=True)
+    print("largest gradient errors vs fp32 (fold / unfused): "
+          + "; ".join(f"{n} {ef:.2e} / {ep:.2e}" for ef, ep, n in errs[:6]))
+    assert not bad, bad
