@@ -53,14 +53,43 @@ __global__ void __launch_bounds__(256) ln_fold_prep_kernel(FoldPrepTable t) {
   if (n >= j.rows) return;
   const float* wr = j.w + (int64_t)n * j.ld;
   float gw = 0.0f, wb = 0.0f;
-  for (int k = lane; k < j.D; k += 64) {
-    gw += mul_sub_rn(j.gamma[k], wr[k], 0.0f);
-    wb = fmaf(wr[k], j.beta[k], wb);
+  // the row in registers (D <= 1024: up to 4 pieces of 4 per lane), 16-byte loads when aligned
+  constexpr int kMaxP = 4;
+  float4 wv[kMaxP], gv[kMaxP];
+  const bool vec = (j.D % 256) == 0 && j.D <= 1024 && (j.ld % 4) == 0 &&
+                   (((uintptr_t)wr | (uintptr_t)j.gamma | (uintptr_t)j.beta) & 15) == 0;
+  if (vec) {
+    const int np = j.D / 256;
+#pragma unroll
+    for (int c = 0; c < kMaxP; ++c) {
+      if (c < np) {
+        wv[c] = *(const float4*)(wr + 4 * (lane + 64 * c));
+        gv[c] = *(const float4*)(j.gamma + 4 * (lane + 64 * c));
+        const float4 be = *(const float4*)(j.beta + 4 * (lane + 64 * c));
+        gw += mul_sub_rn(gv[c].x, wv[c].x, 0.0f) + mul_sub_rn(gv[c].y, wv[c].y, 0.0f) +
+              mul_sub_rn(gv[c].z, wv[c].z, 0.0f) + mul_sub_rn(gv[c].w, wv[c].w, 0.0f);
+        wb = fmaf(wv[c].x, be.x, fmaf(wv[c].y, be.y, fmaf(wv[c].z, be.z, fmaf(wv[c].w, be.w, wb))));
+      }
+    }
+  } else {
+    for (int k = lane; k < j.D; k += 64) {
+      gw += mul_sub_rn(j.gamma[k], wr[k], 0.0f);
+      wb = fmaf(wr[k], j.beta[k], wb);
+    }
   }
   const float m = wave_sum_dpp(gw) / (float)j.D;
   wb = wave_sum_dpp(wb);
   float r = 0.0f;
-  for (int k = lane; k < j.D; k += 64) r += (float)(__bf16)fold_elem(j.gamma[k], wr[k], m);
+  if (vec) {
+    const int np = j.D / 256;
+#pragma unroll
+    for (int c = 0; c < kMaxP; ++c)
+      if (c < np)
+        r += ((float)(__bf16)fold_elem(gv[c].x, wv[c].x, m) + (float)(__bf16)fold_elem(gv[c].y, wv[c].y, m)) +
+             ((float)(__bf16)fold_elem(gv[c].z, wv[c].z, m) + (float)(__bf16)fold_elem(gv[c].w, wv[c].w, m));
+  } else {
+    for (int k = lane; k < j.D; k += 64) r += (float)(__bf16)fold_elem(j.gamma[k], wr[k], m);
+  }
   r = wave_sum_dpp(r);
   if (lane == 0) {
     j.shift[n] = m;
@@ -118,7 +147,7 @@ __global__ void __launch_bounds__(256) ln_fold_bwd_kernel(const __bf16* __restri
 // ------------------------------------------------------------------------ weight gradient ---
 // Workgroup = 4 waves over a contiguous run of kRowsPerWg rows; lane holds columns
 // lane + 64 c (c < VPL).  Partial rows of dgamma / dbeta per workgroup in a fixed order.
-constexpr int kRowsPerWg = 32;
+constexpr int kRowsPerWg = 16;
 template <int VPL>
 __global__ void __launch_bounds__(256) ln_fold_wgrad_kernel(
     const float* __restrict__ M, const float* __restrict__ w, int64_t ld,
@@ -168,14 +197,25 @@ __global__ void __launch_bounds__(256) ln_fold_wgrad_kernel(
   }
 }
 
-// dgamma_dbeta [2][D] = sum over the P partial rows, in order
+// dgamma_dbeta [2][D] = sum over the P partial rows in a fixed order: a workgroup per 64 columns,
+// wave q sums rows q, q + 4, ... (loads unrolled by 4), then the 4 wave sums in order
 __global__ void __launch_bounds__(256) ln_fold_sum_kernel(const float* __restrict__ part, int P,
                                                          int D2, float* __restrict__ out) {
-  const int k = blockIdx.x * 256 + threadIdx.x;
-  if (k >= D2) return;
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int k = blockIdx.x * 64 + lane;
+  const int kc = k < D2 ? k : D2 - 1;
   float s = 0.0f;
-  for (int p = 0; p < P; ++p) s += part[(int64_t)p * D2 + k];
-  out[k] = s;
+  int p = q;
+  for (; p + 12 < P; p += 16) {
+    const float a0 = part[(int64_t)p * D2 + kc], a1 = part[(int64_t)(p + 4) * D2 + kc];
+    const float a2 = part[(int64_t)(p + 8) * D2 + kc], a3 = part[(int64_t)(p + 12) * D2 + kc];
+    s = (((s + a0) + a1) + a2) + a3;
+  }
+  for (; p < P; p += 4) s += part[(int64_t)p * D2 + kc];
+  red[q][lane] = s;
+  __syncthreads();
+  if (q == 0 && k < D2) out[k] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
 }
 
 }  // namespace sc
@@ -248,7 +288,7 @@ extern "C" int sc_ln_fold_wgrad(const float* M, const float* w, int64_t ld, cons
   else
     hipLaunchKernelGGL(ln_fold_wgrad_kernel<16>, dim3(P), dim3(256), 0, st, M, w, ld, gamma, beta,
                        dbias, rows, dw, workspace);
-  hipLaunchKernelGGL(ln_fold_sum_kernel, dim3((2 * D + 255) / 256), dim3(256), 0, st, workspace, P,
+  hipLaunchKernelGGL(ln_fold_sum_kernel, dim3((2 * D + 63) / 64), dim3(256), 0, st, workspace, P,
                      2 * D, dgamma_dbeta);
   return launch_status("sc_ln_fold_wgrad");
 }

@@ -1056,6 +1056,14 @@ __global__ void __launch_bounds__(512) joint_fwd_kernel(JointArgs a) {
 #ifndef SC_JOINT_ST8   // 1: column staging on all 8 waves (0: waves 0-3, A/B in tools only)
 #define SC_JOINT_ST8 1
 #endif
+// SC_JOINT_DEPTH: LDS-DMA landing buffers of the column operands from HBM (pred row, node fields):
+// 2 = the DMA of column u + 2 is issued while column u computes and retired at its end (one
+// column of latency cover), 3 = column u + 3, retired at the end of column u + 1 (two columns).
+// Measured equal (tools/j_ab.sh, C5 B=32: 6.24-6.44 ms either way): the column loop does not wait
+// on these loads, so the shorter ring stays.
+#ifndef SC_JOINT_DEPTH
+#define SC_JOINT_DEPTH 2
+#endif
 constexpr int kVbWg = 16;   // vocab blocks (of 32) per workgroup
 constexpr int kJW = 8;      // waves per workgroup: two per SIMD, so one wave's exp / pack /
                             // transpose work runs beside the other's MFMAs (<= 256 registers each)
@@ -1133,9 +1141,10 @@ struct BwdLds {   // byte offsets of the LDS regions
                                                         // task's end: over the p images
   static constexpr int kPr = kP + (kJW * 32 * 128 > 4 * 64 * kDeP * 4 ? kJW * 32 * 128
                                                                        : 4 * 64 * kDeP * 4);
-  // LDS-DMA landing zones, one column ahead: pred rows [2][64] fp32, node fields [2][kNF][32]
-  static constexpr int kNd = kPr + 2 * 64 * 4;
-  static constexpr int kEnd = kNd + 2 * kNF * 32 * 4;
+  // LDS-DMA landing zones, SC_JOINT_DEPTH - 1 columns ahead: pred rows [depth][64] fp32, node
+  // fields [depth][kNF][32]
+  static constexpr int kNd = kPr + SC_JOINT_DEPTH * 64 * 4;
+  static constexpr int kEnd = kNd + SC_JOINT_DEPTH * kNF * 32 * 4;
 };
 
 __global__ void __launch_bounds__(64 * kJW) joint_bwd_kernel(JointArgs a) {
@@ -1216,8 +1225,8 @@ __global__ void __launch_bounds__(64 * kJW) joint_bwd_kernel(JointArgs a) {
     // the column operands that come from HBM (pred row, node scalars, label) land in LDS one
     // column ahead by LDS-DMA from wave 0 (node_dma), retired by wave 0's dma_wait() before the
     // column's barrier; no VGPR holds them and no compiler-visible load sits in the column loop
-    uint32_t* const ndl0 = (uint32_t*)(lds + BwdLds::kNd);   // [2][kNF][32]
-    float* const prl0 = (float*)(lds + BwdLds::kPr);          // [2][64]
+    uint32_t* const ndl0 = (uint32_t*)(lds + BwdLds::kNd);   // [depth][kNF][32]
+    float* const prl0 = (float*)(lds + BwdLds::kPr);          // [depth][64]
     const double lp2 = r.ws.logp2[b];
     const float lsc = r.scale[b];
     auto col_dma = [&](int uu, int bf) __attribute__((always_inline)) {
@@ -1229,11 +1238,25 @@ __global__ void __launch_bounds__(64 * kJW) joint_bwd_kernel(JointArgs a) {
     auto col_dma_wait = [&]() __attribute__((always_inline)) {
       if (w == kWp || w == kWn) dma_wait();
     };
+    // retire every column DMA but the youngest column's (this wave's pieces per column: the pred
+    // row 1, the node fields 10 + the label)
+    auto col_dma_wait_older = [&]() __attribute__((always_inline)) {
+      if (w == kWp) dma_wait_younger<1>();
+      if (w == kWn) {
+        if (Ub > 0) dma_wait_younger<kNF>();
+        else dma_wait_younger<kNF - 1>();
+      }
+    };
+    // DMA buffer of column uu (its landing zone)
+    auto dbuf = [&](int uu) __attribute__((always_inline)) {
+      return SC_JOINT_DEPTH == 2 ? (uu - ua) & 1 : (uu - ua) % SC_JOINT_DEPTH;
+    };
     // stage column uu into buffer bf: z (bf16 image + fp32 1 - z^2), node scalars, label; the
     // DMA of the column after it is issued here and lands while this one computes
     auto stage = [&](int uu, int bf) __attribute__((always_inline)) {
       if (!stager) return;
-      const float* pr = prl0 + bf * 64 + kSE * jg;
+      const int db = dbuf(uu);
+      const float* pr = prl0 + db * 64 + kSE * jg;
       const float* el = encl + zn * 64 + kSE * jg;
       float xs[kSE];
 #pragma unroll
@@ -1268,7 +1291,7 @@ __global__ void __launch_bounds__(64 * kJW) joint_bwd_kernel(JointArgs a) {
       for (int e = 0; e < kSE; ++e) zz[e * BwdLds::kZP] = 1.0f - zf[e] * zf[e];
       if (w == kWf && lane < 32) {
         const int th = lane;
-        const uint32_t* nf = ndl0 + bf * kNF * 32;
+        const uint32_t* nf = ndl0 + db * kNF * 32;
         float wb, wy, l2;
         node_finish(nf, th, lp2, lsc, tb * 32 + th, uu, Tb, Ub, wb, wy, l2);
         const float an = wb + wy;
@@ -1282,16 +1305,19 @@ __global__ void __launch_bounds__(64 * kJW) joint_bwd_kernel(JointArgs a) {
           ((int*)ns)[96] = uu < Ub ? (lab < 0 ? 0 : (lab >= r.V ? r.V - 1 : lab)) : r.blank;
         }
       }
-      // (every read of DMA buffer bf ^ 1 happened before the barrier that ended column uu - 2)
-      if (uu + 1 < ue) col_dma(uu + 1, bf ^ 1);
+      // (DMA buffer dbuf(uu + depth - 1) = dbuf(uu - 1) was read by stage(uu - 1), before the
+      // barrier that ended column uu - 2)
+      if (uu + SC_JOINT_DEPTH - 1 < ue) col_dma(uu + SC_JOINT_DEPTH - 1, dbuf(uu + SC_JOINT_DEPTH - 1));
     };
     if (ua < ue) {
-      col_dma(ua, 0);
+#pragma unroll
+      for (int d = 0; d < SC_JOINT_DEPTH - 1; ++d)
+        if (ua + d < ue) col_dma(ua + d, d);
       col_dma_wait();
-      lds_barrier();   // the first column's DMA has landed
+      lds_barrier();   // the first columns' DMA has landed
       stage(ua, 0);
     }
-    col_dma_wait();
+    if (SC_JOINT_DEPTH == 2) col_dma_wait();
     lds_barrier();
     for (int u = ua; u < ue; ++u) {
       // lane-dependent addresses re-derived per column, not held across it (register budget of
@@ -1447,9 +1473,11 @@ __global__ void __launch_bounds__(64 * kJW) joint_bwd_kernel(JointArgs a) {
       }
       if (SC_JOINT_ABL & 2) asm volatile("" :: "v"(Y[0]), "v"(Y[1]));
       // the column's one barrier: its d pred partials and the next column's operands are
-      // complete (wave 0's DMA of column u + 2 included), and this column's buffer is free for
+      // complete (the DMA of column u + 2 included: at depth 3 issued one column earlier, the
+      // younger one of column u + 3 stays in flight), and this column's buffer is free for
       // column u + 2
-      col_dma_wait();
+      if (SC_JOINT_DEPTH == 2 || u + SC_JOINT_DEPTH >= ue) col_dma_wait();   // (none younger)
+      else col_dma_wait_older();
       lds_barrier();
       if (w == kWd) {   // d pred of this column: the wave partials (red buffers alternate)
         float s = 0.0f;

@@ -566,8 +566,12 @@ def lucy_cell(x, w, b, h0, s0, cdt=None, imgs=None, split_sink=None, rec_sink=No
 
 
 # ----------------------------------------------------------------------------- LayerNorm fold ---
-# SC_LN_FOLD=0 keeps the inter-layer LayerNorm as its own kernels (A/B only)
-USE_LN_FOLD = os.environ.get("SC_LN_FOLD", "1") != "0"
+# SC_LN_FOLD=1 selects the fold (opt-in).  Measured on the C2 step (same box, alternated twice,
+# profiles/r5_ln_fold_ab.md): 5.263-5.278 ms folded vs 5.149-5.178 ms unfused.  The fold removes
+# ln_fwd / ln_part_sum (~125 us per step) but adds ~14 us of VALU per layer to the scan forward
+# (the records and the rstd rebuild) and ~7 us to the scan backward, which are VALU-bound, plus
+# the fold's own weight-gradient pieces -- so the LayerNorm kernels stay the default.
+USE_LN_FOLD = os.environ.get("SC_LN_FOLD", "0") == "1"
 _FOLD = WeakIdKeyDictionary()
 
 

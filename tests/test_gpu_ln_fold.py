@@ -1,6 +1,7 @@
 """GPU parity of the inter-layer LayerNorm folded into the next gate projection (csrc/ln_fold.hip,
 sc_lucy_scan_fwd_ln / _bwd_ln, ops.LucyCellLNFn), which replaces nn.LayerNorm +
-LinearSafe (lucyrnn_triton.py:96-97, :136-137, :20-25) under bf16 autocast.
+LinearSafe (lucyrnn_triton.py:96-97, :136-137, :20-25) under bf16 autocast when SC_LN_FOLD=1
+(opt-in: ops.USE_LN_FOLD; the tests switch it on).
 
 * The folded images (W'' = bf16(gamma W - shift)), b' and r against torch on the same fp32
   values.
@@ -109,6 +110,7 @@ def _run(m, x, autocast):
 
 
 def test_fold_layer_vs_unfused_and_fp32(monkeypatch):
+    monkeypatch.setattr(ops(), "USE_LN_FOLD", True)   # (opt-in: SC_LN_FOLD=1)
     m, x = _layer_pair()
     ref32 = _run(m, x, autocast=False)
     folded = _run(m, x, autocast=True)
@@ -130,6 +132,7 @@ def test_fold_engaged_and_no_layernorm_launch(monkeypatch):
     from statecatcher_amd import LucyRNNConfig, LucyRNNtriton
     calls = {"ln": 0, "fold": 0}
     o = ops()
+    monkeypatch.setattr(o, "USE_LN_FOLD", True)
     orig_ln, orig_fold = o.LayerNormFn.apply, o.LucyCellLNFn.apply
 
     def ln(*a):
@@ -178,6 +181,7 @@ def test_c2_stack_fold_vs_unfused(monkeypatch):
                                          [T, T], [150, 97], 0)
         loss.backward()
         return float(loss), {n: p.grad.detach().clone() for n, p in model.named_parameters()}
+    monkeypatch.setattr(ops(), "USE_LN_FOLD", True)
     l32, g32 = run(False)
     lf, gf = run(True)
     monkeypatch.setattr(ops(), "USE_LN_FOLD", False)
