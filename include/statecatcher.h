@@ -24,6 +24,7 @@
  *                        train.py:142 / model.py:68-71
  *   sc_ctc_greedy_decode <- decoder.py:3-30 `ctc_greedy_decoder`
  *   sc_ctc_greedy_step   <- decoder.py:3-30 applied one frame at a time (streaming)
+ *   sc_ctc_greedy_frames <- the same over a block of frames in one launch
  *   sc_fbank          <- make_frontend (model.py:250-279, applied at train.py:473-475):
  *                        torchaudio MFCC / MelSpectrogram + AmplitudeToDB (unpinned, absent)
  *   sc_lucy_step_*    <- the native LucyRNN's infer-mode frame loop, lucyrnn.py:172-184, i.e.
@@ -348,6 +349,15 @@ int sc_ctc_greedy_decode(const void* log_probs, int dtype, int B, int T, int V,
 int sc_ctc_greedy_step(const void* logits, int dtype, int B, int V, int64_t stride_b,
                        const float* mask, int blank, int32_t* prev, int32_t* emit,
                        int64_t emit_stride, void* stream);
+/*
+ * sc_ctc_greedy_step over F consecutive frames in one launch, frame f = 0 .. F-1 in order:
+ * logits [F][B][V] (strides stride_f, stride_b), mask [F][B] (stride mask_f) or null, emit
+ * [F][B] (strides emit_f, emit_b); prev carried from frame to frame as F calls would.
+ */
+int sc_ctc_greedy_frames(const void* logits, int dtype, int F, int B, int V, int64_t stride_f,
+                         int64_t stride_b, const float* mask, int64_t mask_f, int blank,
+                         int32_t* prev, int32_t* emit, int64_t emit_f, int64_t emit_b,
+                         void* stream);
 
 /* ---------------------------------------------------------------- streaming LucyRNN step -- */
 
@@ -405,6 +415,52 @@ int sc_lucy_frame_cellb(const float* z, const void* st_z, int nst_z, const float
                         const void* st_h, int nst_h, const float* lnz_w, const float* lnz_b,
                         const float* lnh_w, const float* lnh_b, float eps, float* h, float* out,
                         int64_t ldo, const float* mask, int B, int D, void* stream);
+
+/*
+ * The same two kernels over up to 8 independent jobs in ONE launch each: a block of F frames of
+ * an L-layer model runs as a wavefront over (frame, layer) -- stage tau computes layer l of frame
+ * tau - l for every l at once, since layer l of frame j needs only layer l - 1 of frame j and
+ * layer l of frame j - 1 -- so a block takes 4 (F + L - 1) launches instead of 4 F L (statecatcher
+ * _amd/streaming.py).  Each job has the arguments of one sc_lucy_frame_gemm / _cellb call; the
+ * jobs of one call share epi, w_dtype, eps and the presence of the LayerNorm prologue.
+ */
+typedef struct sc_frame_gemm_job {
+  const float* x;
+  int64_t ldx;
+  int K;
+  const float* ln_w;
+  const float* ln_b;
+  const void* st_in;
+  int nst_in;
+  const void* w;
+  int64_t ldw;
+  const float* bias;
+  int B, N;
+  float* y;
+  int64_t ldy;
+  void* st_out;
+  float* z;
+  void* st_z;
+  float* s;
+  const float* mask;
+} sc_frame_gemm_job;
+int sc_lucy_frame_gemm_multi(int epi, int w_dtype, float eps, const sc_frame_gemm_job* jobs,
+                             int njobs, void* stream);
+typedef struct sc_frame_cell_job {
+  const float* z;
+  const void* st_z;
+  int nst_z;
+  const float* hp;
+  const void* st_h;
+  int nst_h;
+  const float *lnz_w, *lnz_b, *lnh_w, *lnh_b;
+  float* h;
+  float* out;
+  int64_t ldo;
+  const float* mask;
+  int B, D;
+} sc_frame_cell_job;
+int sc_lucy_frame_cellb_multi(float eps, const sc_frame_cell_job* jobs, int njobs, void* stream);
 
 /* ---------------------------------------------------------------- column sums ----------- */
 

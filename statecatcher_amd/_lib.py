@@ -18,7 +18,7 @@ _DTYPE = {torch.float32: SC_F32, torch.bfloat16: SC_BF16, torch.float16: SC_F16}
 
 _c = ctypes
 _i32, _i64, _vp, _fp = _c.c_int, _c.c_int64, _c.c_void_p, _c.c_void_p
-ABI_VERSION = 12  # include/statecatcher.h; bumped on any signature change
+ABI_VERSION = 13  # include/statecatcher.h; bumped on any signature change
 
 _SIGS = {
     "sc_abi_version": (_i32, []),
@@ -80,6 +80,10 @@ _SIGS = {
                                   _i64, _fp, _i32, _i32, _fp, _i64, _vp, _fp, _vp, _fp, _fp, _vp]),
     "sc_lucy_frame_cellb": (_i32, [_fp, _vp, _i32, _fp, _vp, _i32, _fp, _fp, _fp, _fp, _c.c_float,
                                    _fp, _fp, _i64, _fp, _i32, _i32, _vp]),
+    "sc_lucy_frame_gemm_multi": (_i32, [_i32, _i32, _c.c_float, _vp, _i32, _vp]),
+    "sc_lucy_frame_cellb_multi": (_i32, [_c.c_float, _vp, _i32, _vp]),
+    "sc_ctc_greedy_frames": (_i32, [_vp, _i32, _i32, _i32, _i32, _i64, _i64, _fp, _i64, _i32, _vp,
+                                    _vp, _i64, _i64, _vp]),
     "sc_mlstm_supported": (_i32, [_i32, _i32, _i32]),
     "sc_mlstm_chunk_state_numel": (_i64, [_i32, _i32, _i32, _i32]),
     "sc_mlstm_fwd": (_i32, [_vp, _vp, _vp, _i32, _fp, _fp, _fp, _fp, _fp, _i32, _i32, _i32, _i32,
@@ -145,6 +149,22 @@ class LnFoldJob(ctypes.Structure):
     """sc_ln_fold_job (include/statecatcher.h)."""
     _fields_ = [("w", _vp), ("gamma", _vp), ("beta", _vp), ("bias", _vp), ("shift", _vp),
                 ("bias_out", _vp), ("rowsum", _vp), ("ld", _i64), ("rows", _i64), ("D", _i64)]
+
+
+class FrameGemmJob(ctypes.Structure):
+    """sc_frame_gemm_job (include/statecatcher.h)."""
+    _fields_ = [("x", _vp), ("ldx", _i64), ("K", _i32), ("ln_w", _vp), ("ln_b", _vp),
+                ("st_in", _vp), ("nst_in", _i32), ("w", _vp), ("ldw", _i64), ("bias", _vp),
+                ("B", _i32), ("N", _i32), ("y", _vp), ("ldy", _i64), ("st_out", _vp), ("z", _vp),
+                ("st_z", _vp), ("s", _vp), ("mask", _vp)]
+
+
+class FrameCellJob(ctypes.Structure):
+    """sc_frame_cell_job (include/statecatcher.h)."""
+    _fields_ = [("z", _vp), ("st_z", _vp), ("nst_z", _i32), ("hp", _vp), ("st_h", _vp),
+                ("nst_h", _i32), ("lnz_w", _vp), ("lnz_b", _vp), ("lnh_w", _vp), ("lnh_b", _vp),
+                ("h", _vp), ("out", _vp), ("ldo", _i64), ("mask", _vp), ("B", _i32), ("D", _i32)]
+
 
 _LIB = None
 

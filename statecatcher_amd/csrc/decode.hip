@@ -118,6 +118,36 @@ __global__ void __launch_bounds__(256) greedy_step_kernel(GreedyStepArgs a) {
   }
 }
 
+// F frames of one stream per wave, in frame order (prev carried in a register of lane 0)
+struct GreedyFramesArgs {
+  const void* x;
+  int F, B, V, blank;
+  int64_t sf, sb;
+  const float* mask;
+  int64_t mf;
+  int32_t* prev;
+  int32_t* emit;
+  int64_t ef, eb;
+};
+
+template <int DT>
+__global__ void __launch_bounds__(256) greedy_frames_kernel(GreedyFramesArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= a.B) return;
+  int pv = a.prev[b];
+  for (int f = 0; f < a.F; ++f) {
+    const int tok = wave_argmax<DT>(
+        (const typename Elem<DT>::T*)a.x + (int64_t)f * a.sf + (int64_t)b * a.sb, a.V, lane);
+    if (lane == 0) {
+      const bool live = !a.mask || a.mask[(int64_t)f * a.mf + b] != 0.0f;
+      a.emit[(int64_t)f * a.ef + (int64_t)b * a.eb] = (live && tok != a.blank && tok != pv) ? tok : -1;
+      if (live) pv = tok;
+    }
+  }
+  if (lane == 0) a.prev[b] = pv;
+}
+
 __global__ void __launch_bounds__(1024) greedy_collapse_kernel(GreedyArgs a) {
   extern __shared__ __attribute__((aligned(16))) int sh[];   // T predictions + 16 wave sums
   const int b = blockIdx.x;
@@ -211,4 +241,26 @@ extern "C" int sc_ctc_greedy_step(const void* logits, int dtype, int B, int V, i
     default: hipLaunchKernelGGL(greedy_step_kernel<SC_F16>, grid, dim3(256), 0, st, a); break;
   }
   return launch_status("sc_ctc_greedy_step");
+}
+
+extern "C" int sc_ctc_greedy_frames(const void* logits, int dtype, int F, int B, int V,
+                                    int64_t stride_f, int64_t stride_b, const float* mask,
+                                    int64_t mask_f, int blank, int32_t* prev, int32_t* emit,
+                                    int64_t emit_f, int64_t emit_b, void* stream) {
+  clear_error();
+  SC_REQUIRE(dtype == SC_F32 || dtype == SC_BF16 || dtype == SC_F16,
+             "sc_ctc_greedy_frames: unsupported dtype %d", dtype);
+  SC_REQUIRE(F >= 0 && B >= 0 && V > 0, "sc_ctc_greedy_frames: bad shape");
+  if (B == 0 || F == 0) return 0;
+  SC_REQUIRE(logits && prev && emit, "sc_ctc_greedy_frames: null pointer");
+  GreedyFramesArgs a{logits, F, B, V, blank, stride_f, stride_b, mask, mask_f, prev, emit, emit_f,
+                     emit_b};
+  const dim3 grid((unsigned)((B + 3) / 4));
+  hipStream_t st = (hipStream_t)stream;
+  switch (dtype) {
+    case SC_F32: hipLaunchKernelGGL(greedy_frames_kernel<SC_F32>, grid, dim3(256), 0, st, a); break;
+    case SC_BF16: hipLaunchKernelGGL(greedy_frames_kernel<SC_BF16>, grid, dim3(256), 0, st, a); break;
+    default: hipLaunchKernelGGL(greedy_frames_kernel<SC_F16>, grid, dim3(256), 0, st, a); break;
+  }
+  return launch_status("sc_ctc_greedy_frames");
 }

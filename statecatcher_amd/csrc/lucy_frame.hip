@@ -29,6 +29,8 @@
 // Activations between kernels are fp32.
 #include "sc_common.h"
 
+#include <algorithm>
+
 // SC_FRAME_ABL: ablation bitmask for tools timing only (never set in a shipped build; wrong
 // results): 1 no MFMAs (fp32 weights), 2 no epilogue stores, 4 no weight loads, 8 no A-row loads
 #ifndef SC_FRAME_ABL
@@ -126,19 +128,19 @@ __device__ __forceinline__ float4 stats16(float v) {
 // One workgroup: rows r0 .. r0 + 15, NT output tiles x KS K-slices (one wave each).
 //   PLAIN / STATS: tile t = columns n0 + 16 t .. (n0 = blockIdx.x * 16 NT)
 //   CELL: tile t = gate t, units d0 .. d0 + 15 (d0 = 16 blockIdx.x), W rows t * gstride + d
+// (bx, by) = the workgroup's column block and 16-row block; the kernels below pass blockIdx
 template <bool BF16W, bool LN, int EPI, int NT, int KS>
-// (at most 128 VGPRs: four waves per SIMD, two 8-wave or one 16-wave workgroup per CU)
-__global__ void __launch_bounds__(64 * NT * KS, 4) lucy_frame_gemm(FrameGemmArgs a) {
+__device__ __forceinline__ void frame_gemm_body(const FrameGemmArgs& a, const int bx, const int by) {
   __shared__ float part[NT * KS][16][17];   // per-wave 16 x 16 partial sums (padded rows)
   __shared__ float stat[16][2];             // PRO_LN: (mean, rstd) of the workgroup's rows
   extern __shared__ __attribute__((aligned(16))) float xs[];   // the A rows [16][kpitch]
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // (wave-uniform: scalar)
   const int t = w % NT, ks = w / NT;
-  const int r0 = blockIdx.y * 16;
+  const int r0 = by * 16;
   constexpr bool CELL = EPI == FR_CELL_UNFUSED || EPI == FR_CELL_FUSED;
   constexpr int KSTEP = BF16W ? 32 : 16;
-  const int cbase = CELL ? blockIdx.x * 16 + t * a.gstride : (blockIdx.x * NT + t) * 16;
+  const int cbase = CELL ? bx * 16 + t * a.gstride : (bx * NT + t) * 16;
   const int nsteps = (a.K + KSTEP - 1) / KSTEP;
   const int kpad = nsteps * KSTEP, kpitch = kpad + 4;   // +4 floats: conflict-free row reads
   const int col = cbase + (lane & 15);
@@ -173,7 +175,7 @@ __global__ void __launch_bounds__(64 * NT * KS, 4) lucy_frame_gemm(FrameGemmArgs
   {
     if constexpr (CELL) {
       if (w < 4) {
-        const int rr = 4 * w + q, rc = min(r0 + rr, a.B - 1), d = blockIdx.x * 16 + (lane & 15);
+        const int rr = 4 * w + q, rc = min(r0 + rr, a.B - 1), d = bx * 16 + (lane & 15);
 #pragma unroll
         for (int g = 0; g < (EPI == FR_CELL_FUSED ? 5 : 4); ++g) e_bias[g] = a.bias[g * a.gstride + d];
         e_s = a.s[(int64_t)rc * a.gstride + d];
@@ -321,7 +323,7 @@ __global__ void __launch_bounds__(64 * NT * KS, 4) lucy_frame_gemm(FrameGemmArgs
       // butterflies within each 16-lane group, then the NT tiles' records per row combined
       __shared__ float4 trec[NT][16];
       if (w < NT) {
-        const int ncol = min(16 * NT, a.N - (int)blockIdx.x * 16 * NT);
+        const int ncol = min(16 * NT, a.N - bx * 16 * NT);
         const bool live = (lane & 15) + 16 * w < ncol;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -337,13 +339,13 @@ __global__ void __launch_bounds__(64 * NT * KS, 4) lucy_frame_gemm(FrameGemmArgs
         float4 r = trec[0][rr];
 #pragma unroll
         for (int t2 = 1; t2 < NT; ++t2) r = chan2(r, trec[t2][rr]);
-        if (r0 + rr < a.B) a.st_out[(int64_t)blockIdx.x * a.B + r0 + rr] = make_float4(r.x, r.y, r.z, 0.0f);
+        if (r0 + rr < a.B) a.st_out[(int64_t)bx * a.B + r0 + rr] = make_float4(r.x, r.y, r.z, 0.0f);
       }
     }
   } else {
     // the cell's elementwise part for the 16 x 16 (row, unit) elements: one per lane of wave 0..3
     if (w < 4) {
-      const int rr = 4 * w + q, r = r0 + rr, d = blockIdx.x * 16 + (lane & 15);
+      const int rr = 4 * w + q, r = r0 + rr, d = bx * 16 + (lane & 15);
       const int D = a.gstride;
       const bool ok = r < a.B;
       auto gate = [&](int g) { return part[g][rr][lane & 15] + e_bias[g]; };
@@ -366,12 +368,35 @@ __global__ void __launch_bounds__(64 * NT * KS, 4) lucy_frame_gemm(FrameGemmArgs
         a.z[(int64_t)r * D + d] = z;
         a.y[(int64_t)r * D + d] = o;
         if ((lane & 15) == 0) {
-          a.st_z[(int64_t)blockIdx.x * a.B + r] = sz;
-          if (a.st_out) a.st_out[(int64_t)blockIdx.x * a.B + r] = so;
+          a.st_z[(int64_t)bx * a.B + r] = sz;
+          if (a.st_out) a.st_out[(int64_t)bx * a.B + r] = so;
         }
       }
     }
   }
+}
+
+// (at most 128 VGPRs: four waves per SIMD, two 8-wave or one 16-wave workgroup per CU)
+template <bool BF16W, bool LN, int EPI, int NT, int KS>
+__global__ void __launch_bounds__(64 * NT * KS, 4) lucy_frame_gemm(FrameGemmArgs a) {
+  frame_gemm_body<BF16W, LN, EPI, NT, KS>(a, blockIdx.x, blockIdx.y);
+}
+
+// Up to kMaxFrameJobs independent GEMMs of one epilogue kind in ONE launch (blockIdx.z = job):
+// the layers of a frame block run as a wavefront over (frame, layer), so the jobs of a launch are
+// different layers at different frames (streaming.py).  Workgroups past a job's column or row
+// blocks leave at once (uniformly, before any barrier).
+constexpr int kMaxFrameJobs = 8;
+struct FrameGemmJobs {
+  FrameGemmArgs j[kMaxFrameJobs];
+};
+template <bool BF16W, bool LN, int EPI, int NT, int KS>
+__global__ void __launch_bounds__(64 * NT * KS, 4) lucy_frame_gemm_multi(FrameGemmJobs jobs) {
+  const FrameGemmArgs& a = jobs.j[blockIdx.z];
+  constexpr bool CELL = EPI == FR_CELL_UNFUSED || EPI == FR_CELL_FUSED;
+  const int nblk = CELL ? a.gstride / 16 : (a.N + 16 * NT - 1) / (16 * NT);
+  if ((int)blockIdx.x >= nblk || (int)blockIdx.y * 16 >= a.B) return;
+  frame_gemm_body<BF16W, LN, EPI, NT, KS>(a, blockIdx.x, blockIdx.y);
 }
 
 // h = (1 - zg) c + zg h_prev (masked), zg = sigmoid(LN_z z), c = tanh(LN_h hp): one workgroup of
@@ -392,9 +417,8 @@ struct FrameCellArgs {
   int B, D;
 };
 
-__global__ void __launch_bounds__(256) lucy_frame_cellb(FrameCellArgs a) {
+__device__ __forceinline__ void frame_cellb_body(const FrameCellArgs& a, const int r) {
   __shared__ float st[4];
-  const int r = blockIdx.x;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   // every operand of the row is loaded before the statistics are combined (one memory latency)
   constexpr int kPer = 4;   // D <= 1024: up to 4 units per thread in registers
@@ -459,6 +483,18 @@ __global__ void __launch_bounds__(256) lucy_frame_cellb(FrameCellArgs a) {
   }
 }
 
+__global__ void __launch_bounds__(256) lucy_frame_cellb(FrameCellArgs a) {
+  frame_cellb_body(a, blockIdx.x);
+}
+struct FrameCellJobs {
+  FrameCellArgs j[kMaxFrameJobs];
+};
+__global__ void __launch_bounds__(256) lucy_frame_cellb_multi(FrameCellJobs jobs) {
+  const FrameCellArgs& a = jobs.j[blockIdx.y];
+  if ((int)blockIdx.x >= a.B) return;
+  frame_cellb_body(a, blockIdx.x);
+}
+
 template <bool BF16W, bool LN, int EPI, int NT, int KS>
 static void launch_gemm(const FrameGemmArgs& a, int nblk, hipStream_t st) {
   const int kstep = BF16W ? 32 : 16;
@@ -471,6 +507,38 @@ static void launch_gemm(const FrameGemmArgs& a, int nblk, hipStream_t st) {
   }
   hipLaunchKernelGGL((lucy_frame_gemm<BF16W, LN, EPI, NT, KS>), dim3(nblk, (a.B + 15) / 16),
                      dim3(64 * NT * KS), lds, st, a);
+}
+
+template <bool BF16W, bool LN, int EPI, int NT, int KS>
+static void launch_gemm_multi(const FrameGemmJobs& jobs, int nj, hipStream_t st) {
+  const int kstep = BF16W ? 32 : 16;
+  constexpr bool CELL = EPI == FR_CELL_UNFUSED || EPI == FR_CELL_FUSED;
+  size_t lds = 0;
+  int gx = 1, gy = 1;
+  for (int i = 0; i < nj; ++i) {
+    const FrameGemmArgs& a = jobs.j[i];
+    lds = std::max(lds, (size_t)16 * (((a.K + kstep - 1) / kstep) * kstep + 4) * sizeof(float));
+    gx = std::max(gx, CELL ? a.gstride / 16 : (a.N + 16 * NT - 1) / (16 * NT));
+    gy = std::max(gy, (a.B + 15) / 16);
+  }
+  static bool big_lds = false;
+  if (lds > 48 * 1024 && !big_lds) {
+    (void)hipFuncSetAttribute((const void*)lucy_frame_gemm_multi<BF16W, LN, EPI, NT, KS>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 140 * 1024);
+    big_lds = true;
+  }
+  hipLaunchKernelGGL((lucy_frame_gemm_multi<BF16W, LN, EPI, NT, KS>), dim3(gx, gy, nj),
+                     dim3(64 * NT * KS), lds, st, jobs);
+}
+
+template <bool BF16W, bool LN>
+static void dispatch_gemm_multi(int epi, const FrameGemmJobs& jobs, int nj, hipStream_t st) {
+  switch (epi) {   // (the tilings of dispatch_gemm below)
+    case FR_PLAIN: launch_gemm_multi<BF16W, LN, FR_PLAIN, 2, 4>(jobs, nj, st); break;
+    case FR_STATS: launch_gemm_multi<BF16W, LN, FR_STATS, 2, 4>(jobs, nj, st); break;
+    case FR_CELL_UNFUSED: launch_gemm_multi<BF16W, LN, FR_CELL_UNFUSED, 4, 2>(jobs, nj, st); break;
+    default: launch_gemm_multi<BF16W, LN, FR_CELL_FUSED, 5, 2>(jobs, nj, st); break;
+  }
 }
 
 template <bool BF16W, bool LN>
@@ -494,41 +562,65 @@ static void dispatch_gemm(int epi, int ngate, const FrameGemmArgs& a, hipStream_
 
 using namespace sc;
 
-extern "C" int sc_lucy_frame_gemm(int epi, const float* x, int64_t ldx, int K, const float* ln_w,
-                                  const float* ln_b, const void* st_in, int nst_in, float eps,
-                                  const void* w, int w_dtype, int64_t ldw, const float* bias,
-                                  int B, int N, float* y, int64_t ldy, void* st_out, float* z,
-                                  void* st_z, float* s, const float* mask, void* stream) {
-  clear_error();
-  SC_REQUIRE(epi >= FR_PLAIN && epi <= FR_CELL_FUSED, "sc_lucy_frame_gemm: bad epilogue %d", epi);
-  SC_REQUIRE(w_dtype == SC_F32 || w_dtype == SC_BF16, "sc_lucy_frame_gemm: weights fp32 or bf16");
-  SC_REQUIRE(B >= 0 && K > 0 && N > 0, "sc_lucy_frame_gemm: bad shape B=%d K=%d N=%d", B, K, N);
+// the argument checks of one frame GEMM (0, or the error code with the message set)
+static int frame_gemm_check(const char* fn, int epi, int w_dtype, const float* x, int64_t ldx,
+                            int K, const float* ln_w, const float* ln_b, const void* st_in,
+                            int nst_in, const void* w, int64_t ldw, const float* bias, int B, int N,
+                            float* y, void* st_out, float* z, void* st_z, float* s) {
+  SC_REQUIRE(epi >= FR_PLAIN && epi <= FR_CELL_FUSED, "%s: bad epilogue %d", fn, epi);
+  SC_REQUIRE(w_dtype == SC_F32 || w_dtype == SC_BF16, "%s: weights fp32 or bf16", fn);
+  SC_REQUIRE(B >= 0 && K > 0 && N > 0, "%s: bad shape B=%d K=%d N=%d", fn, B, K, N);
   if (B == 0) return 0;
-  SC_REQUIRE(x && w && bias && y, "sc_lucy_frame_gemm: null pointer");
+  SC_REQUIRE(x && w && bias && y, "%s: null pointer", fn);
   SC_REQUIRE(ldx % 4 == 0 && ldw % 8 == 0 && K % 4 == 0 && (uintptr_t)x % 16 == 0 &&
                  (uintptr_t)w % 16 == 0,
-             "sc_lucy_frame_gemm: rows must be 16-byte aligned (ldx %% 4, ldw %% 8, K %% 4)");
-  SC_REQUIRE(w_dtype == SC_F32 || K % 8 == 0, "sc_lucy_frame_gemm: bf16 weights need K %% 8 == 0");
-  SC_REQUIRE(K <= 2048, "sc_lucy_frame_gemm: K = %d above 2048 (the A rows live in LDS)", K);
+             "%s: rows must be 16-byte aligned (ldx %% 4, ldw %% 8, K %% 4)", fn);
+  SC_REQUIRE(w_dtype == SC_F32 || K % 8 == 0, "%s: bf16 weights need K %% 8 == 0", fn);
+  SC_REQUIRE(K <= 2048, "%s: K = %d above 2048 (the A rows live in LDS)", fn, K);
   SC_REQUIRE(!ln_w || ((uintptr_t)ln_w % 16 == 0 && (uintptr_t)ln_b % 16 == 0),
-             "sc_lucy_frame_gemm: LayerNorm parameters must be 16-byte aligned");
+             "%s: LayerNorm parameters must be 16-byte aligned", fn);
   SC_REQUIRE((ln_w == nullptr) == (ln_b == nullptr) && (!ln_w || (st_in && nst_in > 0)),
-             "sc_lucy_frame_gemm: LayerNorm prologue needs weight, bias and statistics");
+             "%s: LayerNorm prologue needs weight, bias and statistics", fn);
   const bool cell = epi >= FR_CELL_UNFUSED;
   const int ng = epi == FR_CELL_FUSED ? 5 : 4;
   if (cell) {
-    SC_REQUIRE(N % (16 * ng) == 0, "sc_lucy_frame_gemm: N = %d gates x D, D a multiple of 16", N);
-    SC_REQUIRE(z && st_z && s, "sc_lucy_frame_gemm: cell outputs / state missing");
-    SC_REQUIRE(epi == FR_CELL_FUSED || K == N / ng, "sc_lucy_frame_gemm: unfused cell needs K == D");
+    SC_REQUIRE(N % (16 * ng) == 0, "%s: N = %d gates x D, D a multiple of 16", fn, N);
+    SC_REQUIRE(z && st_z && s, "%s: cell outputs / state missing", fn);
+    SC_REQUIRE(epi == FR_CELL_FUSED || K == N / ng, "%s: unfused cell needs K == D", fn);
   } else {
-    SC_REQUIRE(epi == FR_PLAIN || st_out, "sc_lucy_frame_gemm: statistics output missing");
+    SC_REQUIRE(epi == FR_PLAIN || st_out, "%s: statistics output missing", fn);
   }
+  return 0;
+}
+
+static FrameGemmArgs frame_gemm_args(int epi, const float* x, int64_t ldx, int K, const float* ln_w,
+                                     const float* ln_b, const void* st_in, int nst_in, float eps,
+                                     const void* w, int64_t ldw, const float* bias, int B, int N,
+                                     float* y, int64_t ldy, void* st_out, float* z, void* st_z,
+                                     float* s, const float* mask) {
+  const bool cell = epi >= FR_CELL_UNFUSED;
+  const int ng = epi == FR_CELL_FUSED ? 5 : 4;
   FrameGemmArgs a;
   a.x = x; a.ldx = ldx; a.K = K; a.ln_w = ln_w; a.ln_b = ln_b; a.st_in = (const float4*)st_in;
   a.nst_in = nst_in; a.eps = eps; a.w = w; a.ldw = ldw; a.bias = bias; a.B = B; a.N = N;
   a.gstride = cell ? N / ng : 16;
   a.y = y; a.ldy = ldy; a.st_out = (float4*)st_out; a.z = z; a.st_z = (float4*)st_z; a.s = s;
   a.mask = mask;
+  return a;
+}
+
+extern "C" int sc_lucy_frame_gemm(int epi, const float* x, int64_t ldx, int K, const float* ln_w,
+                                  const float* ln_b, const void* st_in, int nst_in, float eps,
+                                  const void* w, int w_dtype, int64_t ldw, const float* bias,
+                                  int B, int N, float* y, int64_t ldy, void* st_out, float* z,
+                                  void* st_z, float* s, const float* mask, void* stream) {
+  clear_error();
+  const int rc = frame_gemm_check("sc_lucy_frame_gemm", epi, w_dtype, x, ldx, K, ln_w, ln_b, st_in,
+                                  nst_in, w, ldw, bias, B, N, y, st_out, z, st_z, s);
+  if (rc || B == 0) return rc;
+  const FrameGemmArgs a = frame_gemm_args(epi, x, ldx, K, ln_w, ln_b, st_in, nst_in, eps, w, ldw,
+                                          bias, B, N, y, ldy, st_out, z, st_z, s, mask);
+  const int ng = epi == FR_CELL_FUSED ? 5 : 4;
   hipStream_t st = (hipStream_t)stream;
   if (w_dtype == SC_BF16) {
     if (ln_w) dispatch_gemm<true, true>(epi, ng, a, st);
@@ -540,20 +632,88 @@ extern "C" int sc_lucy_frame_gemm(int epi, const float* x, int64_t ldx, int K, c
   return launch_status("sc_lucy_frame_gemm");
 }
 
+extern "C" int sc_lucy_frame_gemm_multi(int epi, int w_dtype, float eps,
+                                        const sc_frame_gemm_job* jobs, int njobs, void* stream) {
+  clear_error();
+  SC_REQUIRE(njobs >= 0 && njobs <= kMaxFrameJobs && (njobs == 0 || jobs),
+             "sc_lucy_frame_gemm_multi: 0..%d jobs per call", kMaxFrameJobs);
+  FrameGemmJobs fj{};
+  int nj = 0, with_ln = -1;
+  for (int i = 0; i < njobs; ++i) {
+    const sc_frame_gemm_job& j = jobs[i];
+    const int rc = frame_gemm_check("sc_lucy_frame_gemm_multi", epi, w_dtype, j.x, j.ldx, j.K,
+                                    j.ln_w, j.ln_b, j.st_in, j.nst_in, j.w, j.ldw, j.bias, j.B,
+                                    j.N, j.y, j.st_out, j.z, j.st_z, j.s);
+    if (rc) return rc;
+    if (j.B == 0) continue;
+    SC_REQUIRE(with_ln < 0 || with_ln == (j.ln_w != nullptr),
+               "sc_lucy_frame_gemm_multi: every job of a call with or every job without the "
+               "LayerNorm prologue");
+    with_ln = j.ln_w != nullptr;
+    fj.j[nj++] = frame_gemm_args(epi, j.x, j.ldx, j.K, j.ln_w, j.ln_b, j.st_in, j.nst_in, eps,
+                                 j.w, j.ldw, j.bias, j.B, j.N, j.y, j.ldy, j.st_out, j.z, j.st_z,
+                                 j.s, j.mask);
+  }
+  if (nj == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  if (w_dtype == SC_BF16) {
+    if (with_ln) dispatch_gemm_multi<true, true>(epi, fj, nj, st);
+    else dispatch_gemm_multi<true, false>(epi, fj, nj, st);
+  } else {
+    if (with_ln) dispatch_gemm_multi<false, true>(epi, fj, nj, st);
+    else dispatch_gemm_multi<false, false>(epi, fj, nj, st);
+  }
+  return launch_status("sc_lucy_frame_gemm_multi");
+}
+
+static int frame_cellb_check(const char* fn, const float* z, const void* st_z, int nst_z,
+                             const float* hp, const void* st_h, int nst_h, const float* lnz_w,
+                             const float* lnz_b, const float* lnh_w, const float* lnh_b, float* h,
+                             float* out, int B, int D) {
+  SC_REQUIRE(B >= 0 && D > 0, "%s: bad shape", fn);
+  if (B == 0) return 0;
+  SC_REQUIRE(z && hp && h && out, "%s: null pointer", fn);
+  SC_REQUIRE((lnz_w == nullptr) == (lnz_b == nullptr) && (lnh_w == nullptr) == (lnh_b == nullptr) &&
+                 (!lnz_w || (st_z && nst_z > 0)) && (!lnh_w || (st_h && nst_h > 0)),
+             "%s: LayerNorm needs weight, bias and statistics", fn);
+  return 0;
+}
+
 extern "C" int sc_lucy_frame_cellb(const float* z, const void* st_z, int nst_z, const float* hp,
                                    const void* st_h, int nst_h, const float* lnz_w,
                                    const float* lnz_b, const float* lnh_w, const float* lnh_b,
                                    float eps, float* h, float* out, int64_t ldo, const float* mask,
                                    int B, int D, void* stream) {
   clear_error();
-  SC_REQUIRE(B >= 0 && D > 0, "sc_lucy_frame_cellb: bad shape");
-  if (B == 0) return 0;
-  SC_REQUIRE(z && hp && h && out, "sc_lucy_frame_cellb: null pointer");
-  SC_REQUIRE((lnz_w == nullptr) == (lnz_b == nullptr) && (lnh_w == nullptr) == (lnh_b == nullptr) &&
-                 (!lnz_w || (st_z && nst_z > 0)) && (!lnh_w || (st_h && nst_h > 0)),
-             "sc_lucy_frame_cellb: LayerNorm needs weight, bias and statistics");
+  const int rc = frame_cellb_check("sc_lucy_frame_cellb", z, st_z, nst_z, hp, st_h, nst_h, lnz_w,
+                                   lnz_b, lnh_w, lnh_b, h, out, B, D);
+  if (rc || B == 0) return rc;
   FrameCellArgs a{z, (const float4*)st_z, nst_z, hp, (const float4*)st_h, nst_h, lnz_w, lnz_b,
                   lnh_w, lnh_b, eps, h, out, ldo, mask, B, D};
   hipLaunchKernelGGL(lucy_frame_cellb, dim3(B), dim3(256), 0, (hipStream_t)stream, a);
   return launch_status("sc_lucy_frame_cellb");
+}
+
+extern "C" int sc_lucy_frame_cellb_multi(float eps, const sc_frame_cell_job* jobs, int njobs,
+                                         void* stream) {
+  clear_error();
+  SC_REQUIRE(njobs >= 0 && njobs <= kMaxFrameJobs && (njobs == 0 || jobs),
+             "sc_lucy_frame_cellb_multi: 0..%d jobs per call", kMaxFrameJobs);
+  FrameCellJobs fj{};
+  int nj = 0, gx = 1;
+  for (int i = 0; i < njobs; ++i) {
+    const sc_frame_cell_job& j = jobs[i];
+    const int rc = frame_cellb_check("sc_lucy_frame_cellb_multi", j.z, j.st_z, j.nst_z, j.hp,
+                                     j.st_h, j.nst_h, j.lnz_w, j.lnz_b, j.lnh_w, j.lnh_b, j.h,
+                                     j.out, j.B, j.D);
+    if (rc) return rc;
+    if (j.B == 0) continue;
+    fj.j[nj++] = FrameCellArgs{j.z, (const float4*)j.st_z, j.nst_z, j.hp, (const float4*)j.st_h,
+                               j.nst_h, j.lnz_w, j.lnz_b, j.lnh_w, j.lnh_b, eps, j.h, j.out,
+                               j.ldo, j.mask, j.B, j.D};
+    gx = std::max(gx, j.B);
+  }
+  if (nj == 0) return 0;
+  hipLaunchKernelGGL(lucy_frame_cellb_multi, dim3(gx, nj), dim3(256), 0, (hipStream_t)stream, fj);
+  return launch_status("sc_lucy_frame_cellb_multi");
 }

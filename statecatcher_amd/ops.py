@@ -1203,6 +1203,69 @@ def lucy_frame_cellb(z, hp, h, out, st_z=None, st_h=None, lnz=None, lnh=None, ma
     check(rc, "sc_lucy_frame_cellb")
 
 
+def frame_gemm_job(x, w, bias, y, st_out=None, ln=None, st_in=None, z=None, st_z=None, s=None,
+                   mask=None):
+    """One job of lucy_frame_gemm_multi (the arguments of one lucy_frame_gemm call)."""
+    B, K = x.shape
+    lw, lb = ln if ln is not None else (None, None)
+    return _lib.FrameGemmJob(ptr(x), x.stride(0), K, ptr(lw), ptr(lb), ptr(st_in),
+                             st_in.shape[0] if st_in is not None else 0, ptr(w), w.stride(0),
+                             ptr(bias), B, w.shape[0], ptr(y), y.stride(0), ptr(st_out), ptr(z),
+                             ptr(st_z), ptr(s), ptr(mask))
+
+
+def lucy_frame_gemm_multi(epi, w_dtype, jobs, stream, eps=1e-5):
+    """Independent frame GEMMs of one epilogue kind (FrameGemmJob list, <= 8 per launch: longer
+    lists take ceil(n / 8) launches) -- sc_lucy_frame_gemm_multi.  w_dtype: torch dtype of
+    every job's weights.  No allocation: safe inside a hipGraph capture."""
+    lib = _lib.load()
+    code = dtype_code(torch.empty(0, dtype=w_dtype))
+    for k in range(0, len(jobs), 8):
+        part = jobs[k:k + 8]
+        check(lib.sc_lucy_frame_gemm_multi(int(epi), code, float(eps),
+                                           (_lib.FrameGemmJob * len(part))(*part), len(part),
+                                           stream), "sc_lucy_frame_gemm_multi")
+
+
+def frame_cell_job(z, hp, h, out, st_z=None, st_h=None, lnz=None, lnh=None, mask=None):
+    """One job of lucy_frame_cellb_multi (the arguments of one lucy_frame_cellb call)."""
+    B, D = h.shape
+    zw, zb = lnz if lnz is not None else (None, None)
+    hw, hb = lnh if lnh is not None else (None, None)
+    return _lib.FrameCellJob(ptr(z), ptr(st_z), st_z.shape[0] if st_z is not None else 0, ptr(hp),
+                             ptr(st_h), st_h.shape[0] if st_h is not None else 0, ptr(zw), ptr(zb),
+                             ptr(hw), ptr(hb), ptr(h), ptr(out), out.stride(0), ptr(mask), B, D)
+
+
+def lucy_frame_cellb_multi(jobs, stream, eps=1e-5):
+    """Independent lucy_frame_cellb calls in <= 8-job launches (sc_lucy_frame_cellb_multi)."""
+    lib = _lib.load()
+    for k in range(0, len(jobs), 8):
+        part = jobs[k:k + 8]
+        check(lib.sc_lucy_frame_cellb_multi(float(eps), (_lib.FrameCellJob * len(part))(*part),
+                                            len(part), stream), "sc_lucy_frame_cellb_multi")
+
+
+def ctc_greedy_frames(logits, prev, emit, mask=None, blank=0):
+    """ctc_greedy_step over F frames in order, one launch (sc_ctc_greedy_frames): logits
+    [F, B, V] (unit inner stride), prev int32 [B] contiguous, emit int32 [F, B], mask fp32
+    [F, B] (unit inner stride) or None."""
+    require_device(logits, prev, emit)
+    F, B, V = logits.shape
+    if logits.stride(2) != 1 or prev.dtype != torch.int32 or emit.dtype != torch.int32:
+        raise ValueError("ctc_greedy_frames: logits need unit inner stride, prev/emit int32")
+    if prev.numel() != B or not prev.is_contiguous() or tuple(emit.shape) != (F, B):
+        raise ValueError("ctc_greedy_frames: prev [B] contiguous, emit [F, B]")
+    if mask is not None and (mask.dtype != torch.float32 or tuple(mask.shape) != (F, B)
+                             or mask.stride(1) != 1):
+        raise ValueError("ctc_greedy_frames: mask must be fp32 [F, B] with unit inner stride")
+    rc = _lib.load().sc_ctc_greedy_frames(
+        ptr(logits), dtype_code(logits), F, B, V, logits.stride(0), logits.stride(1), ptr(mask),
+        mask.stride(0) if mask is not None else 0, int(blank), ptr(prev), ptr(emit),
+        emit.stride(0), emit.stride(1), stream_of(logits))
+    check(rc, "sc_ctc_greedy_frames")
+
+
 # ------------------------------------------------------------------- feature frontend --------
 def fbank(audio, kind="mfcc", sample_rate=16000):
     """make_frontend(kind)(audio).transpose(-1, -2) on the GPU (fbank.hip): audio fp32

@@ -18,6 +18,11 @@ with h, s resident on the GPU in fp32 between calls and every buffer static, so 
 ``frames_per_call`` frames is captured once as a hipGraph (torch.cuda.CUDAGraph) and replayed:
 one host launch per block instead of ~(4-6 L + 2) kernel launches per frame.
 
+schedule="wavefront" (the default with the frame engine) runs a block of K frames as K + L - 1
+stages over (frame, layer), each stage one launch per kernel kind for all its layers
+(_block_wavefront): 4 (K + L - 1) + 2 launches per block instead of K (4 L + 2), identical
+arithmetic.
+
 engine="frame" (the default where it applies: hidden_dim a multiple of 16) replaces the library
 GEMMs and the LayerNorm / cell kernels by the fused chain of csrc/lucy_frame.hip: per layer
     a = x W_in^T + b_in (+ row statistics)            lucy_frame_gemm
@@ -53,7 +58,8 @@ class StreamingLucyRNN:
     """
 
     def __init__(self, model: LucyRNN, batch: int, frames_per_call: int = 1,
-                 dtype=torch.float32, blank: int = 0, graph: bool = True, engine: str = "auto"):
+                 dtype=torch.float32, blank: int = 0, graph: bool = True, engine: str = "auto",
+                 schedule: str = "wavefront"):
         cfg = model.config
         dev = next(model.parameters()).device
         ops._lib.require_device(next(model.parameters()))
@@ -89,6 +95,10 @@ class StreamingLucyRNN:
             raise ValueError("engine='frame' needs hidden_dim % 16 == 0, input width % 8 == 0, "
                              "both <= 2048, and fp32 / bf16 weights")
         self.engine = engine
+        if schedule not in ("wavefront", "frame"):
+            raise ValueError("schedule must be 'wavefront' or 'frame'")
+        # wavefront: the frame engine's block as stages over (frame, layer) (_block_wavefront)
+        self.schedule = schedule if engine == "frame" else "frame"
         z = lambda *s, dt=dtype: torch.zeros(*s, dtype=dt, device=dev)   # noqa: E731
         if engine == "frame":
             f32 = torch.float32
@@ -109,6 +119,14 @@ class StreamingLucyRNN:
             self.xo = [z(B, D, dt=f32) for _ in range(self.L)]
             self.h = [z(B, D, dt=f32) for _ in range(self.L)]
             self.s = [z(B, D, dt=f32) for _ in range(self.L)]
+            if self.schedule == "wavefront":
+                # the layers of a stage run at once: each its own scratch; the last layer's
+                # output per frame, for one output projection over the block
+                self.wf = [dict(fa=z(B, D, dt=f32), fz=z(B, D, dt=f32), fy=z(B, D, dt=f32),
+                                fhp=z(B, D, dt=f32), st_a=z((D + 31) // 32, B, 4, dt=f32),
+                                st_z=z(D // 16, B, 4, dt=f32), st_h=z(D // 16, B, 4, dt=f32))
+                           for _ in range(self.L)]
+                self.xlast = z(K, B, D, dt=f32)
             self.logits = z(K, B, self.V, dt=f32)
             self.emit = torch.full((K, B), -1, dtype=torch.int32, device=dev)
             self.prev = torch.full((B,), -1, dtype=torch.int32, device=dev)
@@ -187,7 +205,61 @@ class StreamingLucyRNN:
         torch.addmm(self.b_out, inp, self.w_out.t(), out=self.logits[j])
         ops.ctc_greedy_step(self.logits[j], self.prev, self.emit[j], mask=m, blank=self.blank)
 
+    def _block_wavefront(self):
+        """The frame engine's block as K + L - 1 stages: stage tau runs layer l of frame tau - l
+        for every l at once (layer l of frame j needs layer l - 1 of frame j, from stage tau - 1,
+        and layer l of frame j - 1, from stage tau - 1: its state).  A stage is the four kernels
+        of a layer, each ONE launch over the stage's layers (sc_lucy_frame_gemm_multi /
+        _cellb_multi); then one output projection over the K frames and one greedy launch.
+        4 (K + L - 1) + 2 launches per block instead of K (4 L + 2), the same arithmetic per
+        (frame, layer) as _frame_fused_chain.  Layer l's input xo[l - 1] is read by the stage's
+        first launch and rewritten (next frame) by its last, so one buffer per layer suffices."""
+        cfg, D, K, L = self.cfg, self.D, self.K, self.L
+        stream = ops._lib.stream_of(self.x)
+        wdt = self.w_out.dtype
+        nst_a = (D + 31) // 32
+        for tau in range(K + L - 1):
+            act = [(l, tau - l) for l in range(L) if 0 <= tau - l < K]
+            ln = self.layers[0]["ln_in"] is not None
+            inproj, gates, whs, cells = [], [], [], []
+            for l, j in act:
+                e, sc, m = self.layers[l], self.wf[l], self.mask[j]
+                inp = self.x[j] if l == 0 else self.xo[l - 1]
+                inproj.append(ops.frame_gemm_job(inp, e["w_in"], e["b_in"], sc["fa"],
+                                                 st_out=sc["st_a"][:nst_a] if ln else None))
+                lnin = dict(ln=e["ln_in"], st_in=sc["st_a"][:nst_a]) if ln else {}
+                if cfg.fused_ops:
+                    gates.append(ops.frame_gemm_job(sc["fa"], e["w_g"], e["b_g"], sc["fhp"],
+                                                    st_out=sc["st_h"], z=sc["fz"], st_z=sc["st_z"],
+                                                    s=self.s[l], mask=m, **lnin))
+                    st_h = sc["st_h"]
+                else:
+                    gates.append(ops.frame_gemm_job(sc["fa"], e["w_g"], e["b_g"], sc["fy"],
+                                                    z=sc["fz"], st_z=sc["st_z"], s=self.s[l],
+                                                    mask=m, **lnin))
+                    lnh = e["lnh"] is not None
+                    st_h = sc["st_h"][:nst_a]
+                    whs.append(ops.frame_gemm_job(sc["fy"], e["w_h"], e["b_h"], sc["fhp"],
+                                                  st_out=st_h if lnh else None))
+                out = self.xlast[j] if l == L - 1 else self.xo[l]
+                cells.append(ops.frame_cell_job(sc["fz"], sc["fhp"], self.h[l], out,
+                                                st_z=sc["st_z"], st_h=st_h, lnz=e["lnz"],
+                                                lnh=e["lnh"], mask=m))
+            ops.lucy_frame_gemm_multi(ops.FRAME_STATS if ln else ops.FRAME_PLAIN, wdt, inproj, stream)
+            ops.lucy_frame_gemm_multi(ops.FRAME_CELL_FUSED if cfg.fused_ops else ops.FRAME_CELL_UNFUSED,
+                                      wdt, gates, stream)
+            if whs:
+                lnh = self.layers[0]["lnh"] is not None
+                ops.lucy_frame_gemm_multi(ops.FRAME_STATS if lnh else ops.FRAME_PLAIN, wdt, whs,
+                                          stream)
+            ops.lucy_frame_cellb_multi(cells, stream)
+        ops.lucy_frame_gemm(ops.FRAME_PLAIN, self.xlast.view(K * self.B, D), self.w_out, self.b_out,
+                            self.logits.view(K * self.B, self.V))
+        ops.ctc_greedy_frames(self.logits, self.prev, self.emit, mask=self.mask, blank=self.blank)
+
     def _block(self):
+        if self.schedule == "wavefront":
+            return self._block_wavefront()
         for j in range(self.K):
             self._frame(j)
 

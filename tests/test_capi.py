@@ -36,7 +36,7 @@ def test_binding_covers_header(lib):
 
 
 def test_abi_version_and_sizes(lib):
-    assert lib.sc_abi_version() == 12
+    assert lib.sc_abi_version() == 13
     assert lib.sc_lucy_scan_chunk() == 64
     assert lib.sc_lucy_scan_ckpt_numel(32, 1500, 512) == 32 * 24 * 2 * 512
     assert lib.sc_lucy_scan_ckpt_numel(2, 64, 3) == 2 * 1 * 2 * 3
@@ -81,6 +81,29 @@ def test_round4_entry_points_reject_bad_arguments_without_gpu(lib):
     rc = lib.sc_lucy_frame_cellb(null, null, 0, null, null, 0, null, null, null, null,
                                  ctypes.c_float(1e-5), null, null, 4, null, 1, 16, null)
     assert rc == -1 and b"null" in lib.sc_last_error()
+
+
+def test_frame_multi_entry_points_reject_bad_arguments_without_gpu(lib):
+    """sc_lucy_frame_gemm_multi / _cellb_multi / sc_ctc_greedy_frames (ABI v13) validate every job
+    before launching; empty calls are no-ops."""
+    from statecatcher_amd._lib import FrameCellJob, FrameGemmJob
+    null = ctypes.c_void_p()
+    assert lib.sc_lucy_frame_gemm_multi(0, 0, ctypes.c_float(1e-5), null, 0, null) == 0
+    rc = lib.sc_lucy_frame_gemm_multi(0, 0, ctypes.c_float(1e-5), null, 9, null)
+    assert rc == -1 and b"jobs per call" in lib.sc_last_error()
+    jobs = (FrameGemmJob * 2)()
+    jobs[0].B, jobs[0].K, jobs[0].N = 1, 4, 64     # job 0: null pointers
+    rc = lib.sc_lucy_frame_gemm_multi(0, 0, ctypes.c_float(1e-5), jobs, 2, null)
+    assert rc == -1 and b"null" in lib.sc_last_error()
+    rc = lib.sc_lucy_frame_gemm_multi(7, 0, ctypes.c_float(1e-5), jobs, 2, null)
+    assert rc == -1 and b"epilogue" in lib.sc_last_error()
+    cj = (FrameCellJob * 1)()
+    cj[0].B, cj[0].D = 1, 16
+    rc = lib.sc_lucy_frame_cellb_multi(ctypes.c_float(1e-5), cj, 1, null)
+    assert rc == -1 and b"null" in lib.sc_last_error()
+    assert lib.sc_ctc_greedy_frames(null, 0, 0, 4, 8, 32, 8, null, 4, 0, null, null, 4, 1, null) == 0
+    rc = lib.sc_ctc_greedy_frames(null, 5, 2, 4, 8, 32, 8, null, 4, 0, null, null, 4, 1, null)
+    assert rc == -1 and b"dtype" in lib.sc_last_error()
 
 
 def test_ctc_side_array_entry_points_reject_bad_arguments_without_gpu(lib):

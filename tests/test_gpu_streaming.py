@@ -168,6 +168,39 @@ def test_frame_engine_equals_library_engine_at_bench_size(fused, B):
     assert tf == odec.ctc_greedy(lf.cpu().numpy(), lens.numpy())
 
 
+@pytest.mark.parametrize("K", [8, 2])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("fused", [True, False])
+def test_wavefront_schedule_equals_frame_by_frame_schedule(fused, dtype, K):
+    """The block as stages over (frame, layer) (schedule="wavefront": multi-job launches of
+    sc_lucy_frame_gemm_multi / _cellb_multi, one output projection over the block, one greedy
+    launch) against the frame-by-frame chain (schedule="frame") on the stream bench's model
+    (6 x 512, V 1024, layer_norm on), 77 ragged streams, blocks of 8 and of 2 (< L) frames:
+    tokens, logits and state BITWISE equal (same kernels, same arithmetic per (frame, layer))."""
+    import statecatcher_amd as sc
+    from statecatcher_amd.streaming import StreamingLucyRNN
+    torch.manual_seed(21 + fused)
+    m = sc.LucyRNN(sc.LucyRNNConfig(input_dim=80, hidden_dim=512, num_layers=6, vocab_size=1024,
+                                    is_training=False, fused_ops=fused)).to(DEV)
+    with torch.no_grad():
+        m.output_proj.weight.normal_(0.0, 0.05)
+    B, T = 77, 20
+    x = torch.randn(B, T, 80, device=DEV)
+    lens = torch.randint(0, T + 1, (B,))
+    masks = (torch.arange(T)[None, :] < lens[:, None]).to(DEV)
+    out = {}
+    for sched in ("wavefront", "frame"):
+        st = StreamingLucyRNN(m, B, K, dtype=dtype, schedule=sched)
+        assert st.engine == "frame" and st.schedule == sched
+        toks, lg = st.decode(x, masks, return_logits=True)
+        out[sched] = (toks, lg, st.state())
+    (tw, lw, (hw, sw)), (tf, lf, (hf, sf)) = out["wavefront"], out["frame"]
+    assert tw == tf
+    assert torch.equal(lw, lf)
+    for a, b in zip(hw + sw, hf + sf):
+        assert torch.equal(a, b)
+
+
 def test_streaming_reset_subset_and_blocks_equal_one_pass():
     """Feeding an utterance in two calls equals one call; resetting one stream restarts only
     that stream (its tokens equal a fresh decoder's)."""
@@ -230,6 +263,26 @@ def test_frame_engine_odd_blocks_reset_and_state_equal_frame_by_frame(fused):
     (hr, sr), (hb, sb) = ref.state(), blk.state()
     for a, b in zip(hr + sr, hb + sb):
         assert torch.equal(a, b)
+
+
+def test_greedy_frames_kernel_equals_greedy_steps():
+    """sc_ctc_greedy_frames over F frames == F sc_ctc_greedy_step calls (ties, NaN, masks)."""
+    from statecatcher_amd import ops
+    g = torch.Generator().manual_seed(3)
+    F, B, V = 9, 37, 50
+    lg = torch.randint(0, 6, (F, B, V), generator=g).float().to(DEV)   # many ties
+    lg[2, 5, 7] = float("nan")
+    mask = (torch.rand(F, B, generator=g) > 0.3).float().to(DEV)
+    for dt in (torch.float32, torch.bfloat16):
+        x = lg.to(dt)
+        p1 = torch.full((B,), -1, dtype=torch.int32, device=DEV)
+        p2 = p1.clone()
+        e1 = torch.empty(F, B, dtype=torch.int32, device=DEV)
+        e2 = torch.empty(F, B, dtype=torch.int32, device=DEV)
+        for f in range(F):
+            ops.ctc_greedy_step(x[f], p1, e1[f], mask=mask[f], blank=0)
+        ops.ctc_greedy_frames(x, p2, e2, mask=mask, blank=0)
+        assert torch.equal(e1, e2) and torch.equal(p1, p2)
 
 
 def test_greedy_step_kernel_ties_nan_masks_vs_oracle():

@@ -40,6 +40,9 @@ def main():
     ap.add_argument("--engines", default="frame,library")
     ap.add_argument("--dtypes", default="float32,bfloat16")
     ap.add_argument("--no-reference", action="store_true")
+    ap.add_argument("--schedules", default="wavefront,frame",
+                    help="frame engine block schedules (StreamingLucyRNN schedule=)")
+    ap.add_argument("--ks", default="1,8", help="frames per graph call")
     args = ap.parse_args()
     import statecatcher_amd as sc
     from statecatcher_amd.streaming import StreamingLucyRNN
@@ -53,10 +56,15 @@ def main():
     N = args.frames
     for B in [int(b) for b in args.batches.split(",")]:
         x = torch.randn(B, N, 80, device=dev)
-        for engine, dt, K, graph in [(e, getattr(torch, d)) + kg for e in args.engines.split(",")
-                                     for d in args.dtypes.split(",")
-                                     for kg in ((1, True), (8, True), (1, False))]:
-                st = StreamingLucyRNN(m, B, K, dtype=dt, graph=graph, engine=engine)
+        kgs = [(int(k), True) for k in args.ks.split(",")] + [(1, False)]
+        for engine, sched, dt, K, graph in [
+                (e, sc_, getattr(torch, d)) + kg for e in args.engines.split(",")
+                for sc_ in (args.schedules.split(",") if e == "frame" else ["frame"])
+                for d in args.dtypes.split(",") for kg in kgs]:
+                if sched == "wavefront" and K == 1:
+                    continue   # (one frame per block: the same launches as "frame")
+                st = StreamingLucyRNN(m, B, K, dtype=dt, graph=graph, engine=engine,
+                                      schedule=sched)
                 blocks = [x[:, i:i + K].contiguous() for i in range(0, N, K)]
                 it = iter(range(10 ** 9))
 
@@ -64,7 +72,8 @@ def main():
                     st.step(blocks[next(it) % len(blocks)])
                 nb = N // K
                 dt_s = timed(run, nb)
-                print(json.dumps({"impl": f"hip_{engine}" + ("_graph" if graph else "_eager"),
+                print(json.dumps({"impl": f"hip_{engine}" + (f"_{sched}" if engine == "frame" else "")
+                                  + ("_graph" if graph else "_eager"),
                                   "dtype": str(dt).split(".")[-1], "B": B, "K": K,
                                   "fused": args.fused, "frames": nb * K,
                                   "stream_frames_per_s": round(B * nb * K / dt_s, 1),
