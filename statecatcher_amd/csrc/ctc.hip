@@ -51,6 +51,19 @@
 #ifndef SC_CTC_KMAX   // most steps between halo exchanges (8 or 16)
 #define SC_CTC_KMAX 16
 #endif
+// SC_CTC_FLAGX: the halo exchanges that do not re-centre hand the halo to the one neighbour that
+// reads it through an LDS flag (the writer's exchange count) instead of a workgroup barrier; the
+// re-centring exchanges keep the barrier (they need the workgroup maximum).  0: every exchange
+// on the barrier (A/B only).
+// Measured (tools/r5_ctc.sh, scan_bench ctc_fwd at C2 size, alternated): flags 233.6 us vs
+// barriers 211.6 us -- the chained waits (wave w on w - 1 on w - 2 ...) cost more than the
+// barrier they replace, so the barrier stays.
+#ifndef SC_CTC_FLAGX
+#define SC_CTC_FLAGX 0
+#endif
+#ifndef SC_CTC_FLAG_SLEEP   // (SC_CTC_FLAGX) s_sleep in the flag spin
+#define SC_CTC_FLAG_SLEEP 1
+#endif
 
 namespace sc {
 
@@ -418,7 +431,12 @@ __device__ __forceinline__ void ab_run(const CtcArgs& a, int b, int Tb, int Ub) 
     }
   }
   extern __shared__ __attribute__((aligned(16))) float2 full2[];   // [2][nw*OW] published pairs
-  __shared__ float wmax[16];
+  __shared__ __attribute__((aligned(16))) float wmax[16];
+  __shared__ int xflag[16];   // (SC_CTC_FLAGX) exchanges published by each wave
+  if (SC_CTC_FLAGX) {
+    if (tid < 16) xflag[tid] = 0;
+    lds_barrier();
+  }
   const int nst = nw * OW;
   const int pc = p < 0 ? 0 : (2 * p >= a.Sp ? a.Sp / 2 - 1 : p);   // clamped for addressing only
   const float2* lrow = (const float2*)(a.ws.lpe + (int64_t)b * a.T * a.Sp) + pc;
@@ -507,6 +525,30 @@ __device__ __forceinline__ void ab_run(const CtcArgs& a, int b, int Tb, int Ub) 
         const int par = exch & 1;
         const bool norm = par == 1;
         if (own) full2[par * nst + p] = make_float2(vB, vL);
+        // (buffer 0 is written only at the exchanges that do not re-centre: the barrier of the
+        // re-centring exchange between two of them orders every read before the next write)
+        if (SC_CTC_FLAGX && !norm) {
+          // the halo comes from one neighbour (alpha: wave w - 1, beta: w + 1): publish this
+          // wave's count after its pairs (one wave's LDS operations complete in order), then wait
+          // for the neighbour's
+          lds_read_wait();   // (every lane's pairs written before lane 0's count)
+          if (lane == 0)
+            __hip_atomic_store(&xflag[w], exch + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+          const int nb = BETA ? w + 1 : w - 1;
+          if (nb >= 0 && nb < nw) {
+            while (__hip_atomic_load(&xflag[nb], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <= exch)
+              if (SC_CTC_FLAG_SLEEP) __builtin_amdgcn_s_sleep(1);
+          }
+          if (!own) {
+            const bool has = p >= 0 && p < nst;
+            const float2 q = has ? full2[par * nst + p] : make_float2(kDead, kDead);
+            vB = q.x;
+            vL = q.y;
+          }
+          ++exch;
+          if (!(SC_CTC_ABL & 2)) emit(tstep(i), vB, vL);
+          continue;
+        }
         if (norm) {
           float m = own ? fmaxf(vB, vL) : kDead;
 #if SC_CTC_V2
@@ -526,7 +568,16 @@ __device__ __forceinline__ void ab_run(const CtcArgs& a, int b, int Tb, int Ub) 
         }
         if (norm) {
           float m = kDead;
-          for (int q = 0; q < nw; ++q) m = fmaxf(m, wmax[q]);
+#pragma unroll
+          for (int q4 = 0; q4 < 16; q4 += 4) {   // (nw <= 16: four 16-byte reads, unused slots skipped)
+            if (q4 < nw) {
+              const float4 wm = *(const float4*)&wmax[q4];
+              m = fmaxf(m, q4 + 0 < nw ? wm.x : kDead);
+              m = fmaxf(m, q4 + 1 < nw ? wm.y : kDead);
+              m = fmaxf(m, q4 + 2 < nw ? wm.z : kDead);
+              m = fmaxf(m, q4 + 3 < nw ? wm.w : kDead);
+            }
+          }
           if (m > 0.5f * kDead) {   // all dead (infeasible): keep the sentinel
             vB -= m;
             vL -= m;

@@ -1056,6 +1056,14 @@ __global__ void __launch_bounds__(512) joint_fwd_kernel(JointArgs a) {
 #ifndef SC_JOINT_ST8   // 1: column staging on all 8 waves (0: waves 0-3, A/B in tools only)
 #define SC_JOINT_ST8 1
 #endif
+// SC_JOINT_SKEW: the two waves of a SIMD run the column's phases in different orders -- waves
+// 0-3 stage column u + 1 first and then compute column u, waves 4-7 (s_setprio 1) compute
+// column u first and stage afterwards -- so that one wave's staging VALU / LDS work sits beside
+// the other's MFMA blocks instead of both waves of a SIMD doing the same phase at once.  The
+// DMA-issuing and node roles move to waves 0-3 (they issue early in the column).
+#ifndef SC_JOINT_SKEW
+#define SC_JOINT_SKEW 0
+#endif
 // SC_JOINT_DEPTH: LDS-DMA landing buffers of the column operands from HBM (pred row, node fields):
 // 2 = the DMA of column u + 2 is issued while column u computes and retired at its end (one
 // column of latency cover), 3 = column u + 3, retired at the end of column u + 1 (two columns).
@@ -1191,7 +1199,8 @@ __global__ void __launch_bounds__(64 * kJW) joint_bwd_kernel(JointArgs a) {
   // wave 4
   const int zn = th >> 4, jg = th & 15;
   constexpr bool stager = true;
-  constexpr int kWn = 6, kWp = 5, kWf = 7, kWd = 4;
+  constexpr int kWn = SC_JOINT_SKEW ? 2 : 6, kWp = SC_JOINT_SKEW ? 1 : 5,
+                kWf = SC_JOINT_SKEW ? 3 : 7, kWd = SC_JOINT_SKEW ? 0 : 4;
 #else
   const int zn = (th >> 3) & 31, jg = th & 7;   // staging (threads < 256): node zn, j = 8 jg ..
   const bool stager = th < 256;
@@ -1330,7 +1339,8 @@ __global__ void __launch_bounds__(64 * kJW) joint_bwd_kernel(JointArgs a) {
       const float* ns_wb = ns_c + 32;
       const float* ns_wy = ns_c + 64;
       float* red = red0 + cb * kJW * 64;
-      if (u + 1 < ue) stage(u + 1, cb ^ 1);   // into the other buffer (read two columns ago)
+      const bool stage_late = SC_JOINT_SKEW && w >= 4;
+      if (u + 1 < ue && !stage_late) stage(u + 1, cb ^ 1);   // into the other buffer (read two columns ago)
       // column operands: z rows (logits A operand), z^T (dW B operand), node terms per register
       jbf8 zA[4];
 #pragma unroll
@@ -1472,6 +1482,7 @@ __global__ void __launch_bounds__(64 * kJW) joint_bwd_kernel(JointArgs a) {
         if (h == 0) red[w * 64 + j] = sp;
       }
       if (SC_JOINT_ABL & 2) asm volatile("" :: "v"(Y[0]), "v"(Y[1]));
+      if (u + 1 < ue && stage_late) stage(u + 1, cb ^ 1);   // (SC_JOINT_SKEW: waves 4-7 stage last)
       // the column's one barrier: its d pred partials and the next column's operands are
       // complete (the DMA of column u + 2 included: at depth 3 issued one column earlier, the
       // younger one of column u + 3 stays in flight), and this column's buffer is free for
