@@ -181,22 +181,6 @@ __global__ void __launch_bounds__(256) ctc_emit_kernel(CtcArgs a) {
   const int b = (int)(row / a.T), t = (int)(row % a.T);
   if (t >= clampi(a.in_lens[b], 0, a.T)) return;     // rows past in_len are never read
   const T* p = (const T*)a.x + (int64_t)b * a.sb + (int64_t)t * a.stt;
-  // 16-bit logits: the row's 16-byte pieces are issued first, ahead of the state gathers (up to
-  // kXQ per lane: V <= 2048), and reduced from registers below
-  constexpr int kXQ = 4;
-  constexpr bool x16 = sizeof(T) == 2;
-  const bool xpre = x16 && a.is_logits && (a.V % 8) == 0 && ((uintptr_t)p & 15) == 0 &&
-                    (a.V >> 3) <= 64 * kXQ;
-  uint4 xraw[kXQ];
-  if constexpr (x16) {
-    if (xpre) {
-#pragma unroll
-      for (int q = 0; q < kXQ; ++q) {
-        const int c = lane + 64 * q;
-        xraw[q] = c < (a.V >> 3) ? *(const uint4*)(p + 8 * c) : make_uint4(0u, 0u, 0u, 0u);
-      }
-    }
-  }
   const int Sb = 2 * clampi(a.tgt_lens[b], 0, a.Umax) + 1;
   const int64_t* tg = a.tg + (int64_t)b * a.tgs;
   const float* exr = a.ex ? a.ex + (int64_t)b * a.exb + (int64_t)t * a.ext : nullptr;
@@ -228,36 +212,7 @@ __global__ void __launch_bounds__(256) ctc_emit_kernel(CtcArgs a) {
   if (a.is_logits) {
     float m = kNegInf, l = 0.0f;
     constexpr int N = Vec16<DT>::N;
-    bool done = false;
-    if constexpr (x16) {
-      if (xpre) {   // the prefetched pieces: one max over all of them, then one sum
-        float xv[kXQ][8];
-        float cm = kNegInf;
-#pragma unroll
-        for (int q = 0; q < kXQ; ++q) {
-          const uint32_t wd[4] = {xraw[q].x, xraw[q].y, xraw[q].z, xraw[q].w};
-          const bool in = lane + 64 * q < (a.V >> 3);
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            xv[q][2 * k] = in ? E::ld(__builtin_bit_cast(T, (uint16_t)(wd[k] & 0xffffu))) : kNegInf;
-            xv[q][2 * k + 1] = in ? E::ld(__builtin_bit_cast(T, (uint16_t)(wd[k] >> 16))) : kNegInf;
-            cm = fmaxf(cm, fmaxf(xv[q][2 * k], xv[q][2 * k + 1]));
-          }
-        }
-        float cs = 0.0f;
-        if (cm != kNegInf) {
-#pragma unroll
-          for (int q = 0; q < kXQ; ++q)
-#pragma unroll
-            for (int k = 0; k < 8; ++k) cs += fexp(xv[q][k] - cm);
-        }
-        m = cm;
-        l = cs;
-        done = true;
-      }
-    }
-    if (done) {
-    } else if ((a.V % N) == 0 && ((uintptr_t)p & 15) == 0) {   // 16-byte loads (online max per chunk)
+    if ((a.V % N) == 0 && ((uintptr_t)p & 15) == 0) {   // 16-byte loads (online max per chunk)
       for (int c = lane; c < a.V / N; c += 64) {
         float xv[N];
         Vec16<DT>::ld(p + N * c, xv);
@@ -1304,20 +1259,6 @@ __global__ void __launch_bounds__(256) ctc_grad_kernel(CtcArgs a) {
   const int Sb = 2 * Ub + 1;
   const int Um = a.Umax > 0 ? a.Umax : 1;
   const int64_t* tg = a.tg + (int64_t)b * a.tgs;
-  const typename E::T* xr = (const typename E::T*)a.x + (int64_t)b * a.sb + (int64_t)t * a.stt;
-  // 16-bit logits: the row's 16-byte pieces go out NOW, before the occupancy phase's dependent
-  // loads, and are converted in the output pass (up to kXQ pieces per lane: V <= 2048)
-  constexpr int kXQ = 4;
-  constexpr bool x16 = sizeof(typename E::T) == 2;
-  const bool xpre = x16 && gvec && ((uintptr_t)xr & 15) == 0 && (a.V >> 3) <= 64 * kXQ;
-  uint4 xraw[kXQ];
-  if (xpre) {
-#pragma unroll
-    for (int q = 0; q < kXQ; ++q) {
-      const int c = lane + 64 * q;
-      xraw[q] = c < (a.V >> 3) ? *(const uint4*)(xr + 8 * c) : make_uint4(0u, 0u, 0u, 0u);
-    }
-  }
   for (int v = lane; v < a.V; v += 64) lcab[v] = kNegInf;
   wave_lds_sync();
   const float* exr = a.ex ? a.ex + (int64_t)b * a.exb + (int64_t)t * a.ext : nullptr;
@@ -1371,51 +1312,31 @@ __global__ void __launch_bounds__(256) ctc_grad_kernel(CtcArgs a) {
     lcab[a.blank] = exr ? exact_grad(exr[0], ob) : ob;
   }
   wave_lds_sync();
+  const typename E::T* xr = (const typename E::T*)a.x + (int64_t)b * a.sb + (int64_t)t * a.stt;
   // grad = (softmax - occupancy) * scale
-  auto out8 = [&](int c, const float (&xv)[8]) __attribute__((always_inline)) {
-    float gv[8];
-    const float4 l0 = *(const float4*)&lcab[8 * c], l1 = *(const float4*)&lcab[8 * c + 4];
-    const float lc[8] = {l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, l1.z, l1.w};
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const float lp2 = ((xv[k] - lse) - lse_lo) * kLog2e;
-      gv[k] = (exp2_(lp2) - exp2_(lc[k] + koff - lp2)) * sc;
-      if (a.ex && lc[k] != kNegInf) gv[k] = lc[k];   // (an emission column's finished value)
-    }
-    if constexpr (Vec16<GT>::N == 8) {
-      Vec16<GT>::st(g + 8 * c, gv);
-    } else {
-      Vec16<GT>::st(g + 8 * c, *(float(*)[4])&gv[0]);
-      Vec16<GT>::st(g + 8 * c + 4, *(float(*)[4])&gv[4]);
-    }
-  };
-  if constexpr (x16) if (xpre) {   // the prefetched pieces, unrolled so they stay in registers
-#pragma unroll
-    for (int q = 0; q < kXQ; ++q) {
-      const int c = lane + 64 * q;
-      if (c < (a.V >> 3)) {
-        const uint32_t wd[4] = {xraw[q].x, xraw[q].y, xraw[q].z, xraw[q].w};
-        float xv[8];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          xv[2 * k] = E::ld(__builtin_bit_cast(typename E::T, (uint16_t)(wd[k] & 0xffffu)));
-          xv[2 * k + 1] = E::ld(__builtin_bit_cast(typename E::T, (uint16_t)(wd[k] >> 16)));
-        }
-        out8(c, xv);
-      }
-    }
-    return;
-  }
   if (gvec && ((uintptr_t)xr & 15) == 0) {
     for (int c = lane; c < (a.V >> 3); c += 64) {
-      float xv[8];
+      float xv[8], gv[8];
       if constexpr (Vec16<DT>::N == 8) {
         Vec16<DT>::ld(xr + 8 * c, xv);
       } else {
         Vec16<DT>::ld(xr + 8 * c, *(float(*)[4])&xv[0]);
         Vec16<DT>::ld(xr + 8 * c + 4, *(float(*)[4])&xv[4]);
       }
-      out8(c, xv);
+      const float4 l0 = *(const float4*)&lcab[8 * c], l1 = *(const float4*)&lcab[8 * c + 4];
+      const float lc[8] = {l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, l1.z, l1.w};
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float lp2 = ((xv[k] - lse) - lse_lo) * kLog2e;
+        gv[k] = (exp2_(lp2) - exp2_(lc[k] + koff - lp2)) * sc;
+        if (a.ex && lc[k] != kNegInf) gv[k] = lc[k];   // (an emission column's finished value)
+      }
+      if constexpr (Vec16<GT>::N == 8) {
+        Vec16<GT>::st(g + 8 * c, gv);
+      } else {
+        Vec16<GT>::st(g + 8 * c, *(float(*)[4])&gv[0]);
+        Vec16<GT>::st(g + 8 * c + 4, *(float(*)[4])&gv[4]);
+      }
     }
     return;
   }

@@ -232,7 +232,7 @@ def test_module_with_weight_images_equals_self_cast(monkeypatch):
 
     with_images = run()
     assert m._weight_images(x.to(DEV))[0] is None   # outside autocast: no images
-    monkeypatch.setattr(type(m), "_weight_images", lambda self, x: (None, None))
+    monkeypatch.setattr(type(m), "_weight_images", lambda self, x: (None, None, None))
     self_cast = run()
     for a, b in zip(with_images, self_cast):
         assert torch.equal(a, b)
