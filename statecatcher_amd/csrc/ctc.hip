@@ -61,6 +61,9 @@
 #ifndef SC_CTC_FLAGX
 #define SC_CTC_FLAGX 0
 #endif
+#ifndef SC_CTC_WMV   // 1: the re-centring exchange reads the wave maxima as float4s (A/B)
+#define SC_CTC_WMV 1
+#endif
 #ifndef SC_CTC_FLAG_SLEEP   // (SC_CTC_FLAGX) s_sleep in the flag spin
 #define SC_CTC_FLAG_SLEEP 1
 #endif
@@ -568,6 +571,7 @@ __device__ __forceinline__ void ab_run(const CtcArgs& a, int b, int Tb, int Ub) 
         }
         if (norm) {
           float m = kDead;
+#if SC_CTC_WMV
 #pragma unroll
           for (int q4 = 0; q4 < 16; q4 += 4) {   // (nw <= 16: four 16-byte reads, unused slots skipped)
             if (q4 < nw) {
@@ -578,6 +582,9 @@ __device__ __forceinline__ void ab_run(const CtcArgs& a, int b, int Tb, int Ub) 
               m = fmaxf(m, q4 + 3 < nw ? wm.w : kDead);
             }
           }
+#else
+          for (int q = 0; q < nw; ++q) m = fmaxf(m, wmax[q]);
+#endif
           if (m > 0.5f * kDead) {   // all dead (infeasible): keep the sentinel
             vB -= m;
             vL -= m;
