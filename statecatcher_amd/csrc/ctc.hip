@@ -61,8 +61,10 @@
 #ifndef SC_CTC_FLAGX
 #define SC_CTC_FLAGX 0
 #endif
-#ifndef SC_CTC_WMV   // 1: the re-centring exchange reads the wave maxima as float4s (A/B)
-#define SC_CTC_WMV 1
+// SC_CTC_WMV: 1 = the re-centring exchange reads the wave maxima as float4s.  Measured slower
+// (tools/r5_pc.sh, scan_bench ctc_fwd: 211.4-212.0 us vs 199.9-200.0 us for the scalar loop)
+#ifndef SC_CTC_WMV
+#define SC_CTC_WMV 0
 #endif
 #ifndef SC_CTC_FLAG_SLEEP   // (SC_CTC_FLAGX) s_sleep in the flag spin
 #define SC_CTC_FLAG_SLEEP 1

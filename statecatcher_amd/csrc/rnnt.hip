@@ -1553,6 +1553,380 @@ __global__ void __launch_bounds__(64 * kJW) joint_bwd_kernel(JointArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// joint_bwd_pc_kernel: the same backward with the two waves of each SIMD in PRODUCER / CONSUMER
+// roles (SC_JOINT_PC=1).  joint_bwd_kernel's column loop is one dependency chain per wave and
+// vocab block (logits MFMA -> exp -> pack -> dW MFMA -> p image -> transposed reads -> dZ MFMA),
+// ~3 k cycles per block against 384 MFMA cycles (profiles/r3c_joint_stamps.txt).  Here the chain
+// is cut at the p image:
+//   producer (waves 4-7, s_setprio 1), pair i = w - 4, vocab blocks i, i + 4, i + 8, i + 12:
+//     per step one block of the current column: logits (4 MFMAs), p = exp(...) with the sparse
+//     arcs, d bias, dW += p z (4 MFMAs, dW of the 4 blocks in registers), p image -> the pair's
+//     LDS slot of this step;
+//   consumer (waves 0-3), pair i: per step the block its producer finished one step earlier:
+//     dZ += p^T W (the slot's transposed p, 4 MFMAs); after a column's last block the epilogue
+//     (d pre = dZ (1 - z^2) into the d enc partial and the d pred partial) and, one step later,
+//     the column staging (tanh of z, 1 - z^2, node scalars, the DMA of the column after next).
+// One barrier per step (4 per column); the p slots alternate by step parity.  Staging runs one
+// column ahead of the producer, so 1 - z^2 is triple-buffered (the consumer's epilogue of column
+// u, column u + 1 waiting, u + 2 being staged).
+// Measured (tools/r5_pc.sh, C5 B=32, alternated): 8.72-8.80 ms against 6.21-6.24 ms for
+// joint_bwd_kernel, every joiner test passing on it.  The producer's per-block chain (logits ->
+// exp -> dW -> p image, ~2 k cycles) is now the only chain in flight on its SIMD, where the
+// one-pass kernel keeps two (one per wave); two chains per producer need ~270 registers with the
+// consumer's dW / dZ / d enc state live across the same loop.  Kept off.
+#ifndef SC_JOINT_PC
+#define SC_JOINT_PC 0
+#endif
+constexpr int kPcBlk = 4;   // vocab blocks per producer
+
+struct PcLds {   // byte offsets
+  static constexpr int kDeP = 36;
+  static constexpr int kZP = 36;
+  static constexpr int kW = 0;                            // W half image [512][128 B]
+  static constexpr int kBias = kW + kVbWg * 32 * 128;     // [512] fp32, x log2(e)
+  static constexpr int kZ = kBias + kVbWg * 32 * 4;       // z bf16 image [2][32][128 B]
+  static constexpr int kZ32 = kZ + 2 * 32 * 128;          // 1 - z^2 [3][64 j][kZP], node fastest
+  static constexpr int kNs = kZ32 + 3 * 64 * kZP * 4;     // node scalars c, wb, wy, label [2][128]
+  static constexpr int kRed = kNs + 2 * 128 * 4;          // d pred partials [2][4][64]
+  static constexpr int kEnc = kRed + 2 * 4 * 64 * 4;      // the task's enc rows fp32 [32][64]
+  static constexpr int kP = kEnc + 32 * 64 * 4;           // p slots [2][4 pairs][32][128 B]
+  static constexpr int kDe = kP;                          // d enc partials [4][64 j][kDeP]: at
+                                                          // the task's end, over the p slots
+  static constexpr int kPr = kP + (2 * 4 * 32 * 128 > 4 * 64 * kDeP * 4 ? 2 * 4 * 32 * 128
+                                                                       : 4 * 64 * kDeP * 4);
+  static constexpr int kNd = kPr + 2 * 64 * 4;            // LDS-DMA landing: pred [2][64]
+  static constexpr int kEnd = kNd + 2 * kNF * 32 * 4;     // node fields [2][kNF][32]
+};
+static_assert(PcLds::kEnd <= 160 * 1024, "joint_bwd_pc LDS");
+
+__global__ void __launch_bounds__(512) joint_bwd_pc_kernel(JointArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const RnntArgs& r = a.r;
+  const int nvb = r.V / 32, VS = a.vs;
+  const int vh = blockIdx.x % VS, slot = blockIdx.x / VS, nslot = gridDim.x / VS;
+  const int vb0 = vh * kVbWg, nvw = min(kVbWg, nvb - vb0);
+  const int w = uniform(threadIdx.x >> 6);
+  const bool prod = w >= 4;
+  const int pi = w & 3;   // pair
+  int th = threadIdx.x, lane = th & 63, h = lane >> 5;
+  int g1 = (lane >> 4) & 1;
+  unsigned char* wl = lds + PcLds::kW;
+  float* bias_l = (float*)(lds + PcLds::kBias);
+  unsigned char* const zimg0 = lds + PcLds::kZ;
+  float* const z320 = (float*)(lds + PcLds::kZ32);
+  float* encl = (float*)(lds + PcLds::kEnc);
+  float* const ns0 = (float*)(lds + PcLds::kNs);
+  float* const red0 = (float*)(lds + PcLds::kRed);
+  float* dep = (float*)(lds + PcLds::kDe);
+  for (int i = th; i < nvw * 32 * 8; i += 512) {
+    const int v = i >> 3, c = i & 7;
+    *(uint4*)(wl + wimg(v, c)) = *(const uint4*)(a.W + (int64_t)(vb0 * 32 + v) * kJ + 8 * c);
+  }
+  for (int i = th; i < nvw * 32; i += 512) bias_l[i] = a.bias[vb0 * 32 + i] * kLog2e;
+
+  // producer state: dW of its 4 blocks and their bias-gradient partial sums.  The consumers keep
+  // their dZ (Y) in acc[0] and their d enc partial in acc[1]: one register set for both roles
+  // (the compiler would otherwise keep both live across the step loop)
+  jf16 acc[kPcBlk][2];
+  float dbs[kPcBlk];
+#pragma unroll
+  for (int k = 0; k < kPcBlk; ++k) {
+    dbs[k] = 0.0f;
+#pragma unroll
+    for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[k][jb][q] = 0.0f;
+  }
+  const int ntbp = VS * a.ntb;
+  const int64_t ntask = (int64_t)r.B * a.ntb * a.nus;
+  // staging on the consumers (threads < 256): node zn, j = 8 jg .. 8 jg + 7; roles: node DMA
+  // wave 1, pred DMA wave 2, node_finish wave 3, d pred sum wave 0
+  const bool stager = th < 256;
+  const int zn = (th >> 3) & 31, jg = th & 7;
+  constexpr int kWn = 1, kWp = 2, kWf = 3, kWd = 0;
+  if (prod) __builtin_amdgcn_s_setprio(1);
+  for (int64_t task = slot; task < ntask; task += nslot) {
+    const int b = (int)(task / ((int64_t)a.ntb * a.nus));
+    const int tb = (int)((task / a.nus) % a.ntb), us = (int)(task % a.nus);
+    const int Tb = clampr(r.flen[b], 0, r.T), Ub = clampr(r.llen[b], 0, r.Umax);
+    const int ua = (int)((int64_t)us * r.U1 / a.nus);
+    const int ue = tb * 32 < Tb ? min((int)((int64_t)(us + 1) * r.U1 / a.nus), Ub + 1) : ua;
+    const bool zok = tb * 32 + zn < Tb;
+    lds_barrier();   // the previous task's reads of encl / d enc partials are done
+    jf16 (&Y)[2] = acc[0];      // consumer: dZ of the column it is draining
+    jf16 (&dacc)[2] = acc[1];   // consumer: this task's d enc partial (Y's layout)
+    if (!prod) {
+#pragma unroll
+      for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          dacc[jb][q] = 0.0f;
+          Y[jb][q] = 0.0f;
+        }
+    }
+    if (ua < ue && stager) {
+      const float* ep = a.enc + ((int64_t)b * r.T + (zok ? tb * 32 + zn : Tb - 1)) * kJ + 8 * jg;
+      *(float4*)(encl + zn * 64 + 8 * jg) = *(const float4*)ep;
+      *(float4*)(encl + zn * 64 + 8 * jg + 4) = *(const float4*)(ep + 4);
+    }
+    uint32_t* const ndl0 = (uint32_t*)(lds + PcLds::kNd);
+    float* const prl0 = (float*)(lds + PcLds::kPr);
+    const double lp2 = r.ws.logp2[b];
+    const float lsc = r.scale[b];
+    auto col_dma = [&](int uu, int bf) __attribute__((always_inline)) {
+      if (w == kWp)
+        dma_to_lds<4>(a.pred + ((int64_t)b * r.U1 + uu) * kJ + lane, lds_addr(prl0 + bf * 64));
+      if (w == kWn && lane < 32)
+        node_dma(r, b, tb * 32 + lane, uu, Tb, Ub, lds_addr(ndl0 + bf * kNF * 32));
+    };
+    auto col_dma_wait = [&]() __attribute__((always_inline)) {
+      if (w == kWp || w == kWn) dma_wait();
+    };
+    // stage column uu (consumers): z image (buffer uu - ua & 1), 1 - z^2 ((uu - ua) % 3), node
+    // scalars (& 1); the DMA of column uu + 1 is issued at its end (landing buffer (uu+1-ua) & 1)
+    auto stage = [&](int uu) __attribute__((always_inline)) {
+      if (!stager) return;
+      const int cu = uu - ua, bf = cu & 1, b3 = cu % 3;
+      const float* pr = prl0 + bf * 64 + 8 * jg;
+      const float* el = encl + zn * 64 + 8 * jg;
+      float zf[8];
+      jbf8 z8;
+#pragma unroll
+      for (int e = 0; e < 8; e += 4) {
+        const float4 pv = *(const float4*)(pr + e), ev = *(const float4*)(el + e);
+        const float xs[4] = {ev.x + pv.x, ev.y + pv.y, ev.z + pv.z, ev.w + pv.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          zf[e + q] = zok ? tanh_(xs[q]) : 0.0f;
+          z8[e + q] = (__bf16)zf[e + q];
+        }
+      }
+      *(jbf8*)(zimg0 + bf * 32 * 128 + wimg(zn, jg)) = z8;
+      float* zz = z320 + b3 * 64 * PcLds::kZP + 8 * jg * PcLds::kZP + zn;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) zz[e * PcLds::kZP] = 1.0f - zf[e] * zf[e];
+      if (w == kWf && lane < 32) {
+        const uint32_t* nf = ndl0 + bf * kNF * 32;
+        float wb, wy, l2;
+        node_finish(nf, lane, lp2, lsc, tb * 32 + lane, uu, Tb, Ub, wb, wy, l2);
+        const float an = wb + wy;
+        float* ns = ns0 + bf * 128;
+        ns[lane] = an > 0.0f ? log2_(an) - l2 : -1e30f;
+        ns[32 + lane] = wb;
+        ns[64 + lane] = wy;
+        if (lane == 0) {
+          const int lab = (int)nf[10 * 32];
+          ((int*)ns)[96] = uu < Ub ? (lab < 0 ? 0 : (lab >= r.V ? r.V - 1 : lab)) : r.blank;
+        }
+      }
+      if (uu + 1 < ue) col_dma(uu + 1, (cu + 1) & 1);
+    };
+    const int ncol = ue - ua;
+    if (ncol > 0) {
+      col_dma(ua, 0);
+      col_dma_wait();
+      lds_barrier();
+      stage(ua);   // (issues the DMA of column ua + 1)
+    }
+    col_dma_wait();
+    lds_barrier();
+    jbf8 zA[4];   // producer: the current column's z rows (logits A operand)
+    const int nstep = ncol > 0 ? 4 * ncol + 1 : 0;
+    for (int g = 0; g < nstep; ++g) {
+      asm volatile("" : "+v"(th), "+v"(lane), "+v"(h), "+v"(g1));
+      const int up = g >> 2, kp = g & 3;   // producer: column ua + up, block kp
+      if (prod) {
+        if (up < ncol) {
+          const int cb = up & 1;
+          const unsigned char* zimg = zimg0 + cb * 32 * 128;
+          const float* ns_c = ns0 + cb * 128;
+          if (kp == 0) {
+#pragma unroll
+            for (int s2 = 0; s2 < 4; ++s2) zA[s2] = lds_b128(zimg, wimg(lane & 31, 2 * s2 + h));
+          }
+          const int yl = uniform(((const int*)ns_c)[96]);
+          unsigned char* pslot = lds + PcLds::kP + ((g & 1) * 4 + pi) * 32 * 128;
+#pragma unroll
+          for (int k = 0; k < kPcBlk; ++k) {   // (static register index: one block per step)
+            if (k != kp) continue;
+            const int lvb = pi + 4 * k;
+            const bool vok = lvb < nvw;
+            const int vl = (vok ? lvb : 0) * 32 + (lane & 31);
+            jf16 x;
+#pragma unroll
+            for (int q = 0; q < 16; ++q) x[q] = 0.0f;
+#pragma unroll
+            for (int s2 = 0; s2 < 4; ++s2) x = mfma32(zA[s2], lds_b128(wl, wimg(vl, 2 * s2 + h)), x);
+            const float bl = vok ? bias_l[vl] : -1e30f;
+            float p[16], ps = 0.0f;
+#pragma unroll
+            for (int gq = 0; gq < 4; ++gq) {
+              const float4 cv = *(const float4*)(ns_c + 8 * gq + 4 * h);
+              p[4 * gq] = exp2_(fmaf(x[4 * gq], kLog2e, bl + cv.x));
+              p[4 * gq + 1] = exp2_(fmaf(x[4 * gq + 1], kLog2e, bl + cv.y));
+              p[4 * gq + 2] = exp2_(fmaf(x[4 * gq + 2], kLog2e, bl + cv.z));
+              p[4 * gq + 3] = exp2_(fmaf(x[4 * gq + 3], kLog2e, bl + cv.w));
+            }
+            const int vg0 = (vb0 + lvb) * 32;
+            if (vok && ((unsigned)(r.blank - vg0) < 32u || (unsigned)(yl - vg0) < 32u)) {
+              const int v = vg0 + (lane & 31);
+              const float mb = v == r.blank ? 1.0f : 0.0f, my = v == yl ? 1.0f : 0.0f;
+#pragma unroll
+              for (int gq = 0; gq < 4; ++gq) {
+                const float4 bw = *(const float4*)(ns_c + 32 + 8 * gq + 4 * h);
+                const float4 yw = *(const float4*)(ns_c + 64 + 8 * gq + 4 * h);
+                p[4 * gq] -= mb * bw.x + my * yw.x;
+                p[4 * gq + 1] -= mb * bw.y + my * yw.y;
+                p[4 * gq + 2] -= mb * bw.z + my * yw.z;
+                p[4 * gq + 3] -= mb * bw.w + my * yw.w;
+              }
+            }
+#pragma unroll
+            for (int q = 0; q < 16; ++q) ps += p[q];
+            dbs[k] += ps;
+            jbf8 pf[2];
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) {
+              pf[s2] = pack8(p + 8 * s2);
+#pragma unroll
+              for (int jb = 0; jb < 2; ++jb)
+                acc[k][jb] = mfma32(pf[s2],
+                                    cat8(tr_rd(zimg, 16 * s2 + 4 * h, jb * 32 + 16 * g1, lane),
+                                         tr_rd(zimg, 16 * s2 + 8 + 4 * h, jb * 32 + 16 * g1, lane)),
+                                    acc[k][jb]);
+            }
+            typedef int ji2 __attribute__((ext_vector_type(2)));
+            typedef int ji4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+            for (int gq = 0; gq < 4; ++gq) {
+              const ji4 d = __builtin_bit_cast(ji4, pf[gq >> 1]);
+              *(ji2*)(pslot + pimg_off(lane & 31, 8 * gq + 4 * h)) =
+                  ji2{d[2 * (gq & 1)], d[2 * (gq & 1) + 1]};
+            }
+          }
+        }
+      } else {
+        // consumer: the block its producer wrote one step ago (step g - 1)
+        const int gc = g - 1;
+        if (gc >= 0) {
+          const int kc = gc & 3;
+          const int lvb = pi + 4 * kc;
+          const int lvc = lvb < nvw ? lvb : 0;   // (a block past the vocabulary has p = 0)
+          const unsigned char* pslot = lds + PcLds::kP + ((gc & 1) * 4 + pi) * 32 * 128;
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2) {
+            const jbf8 pt = cat8(tr_rd<true>(pslot, 16 * s2 + 4 * h, 16 * g1, lane),
+                                 tr_rd<true>(pslot, 16 * s2 + 8 + 4 * h, 16 * g1, lane));
+#pragma unroll
+            for (int jb = 0; jb < 2; ++jb) {
+              const jbf8 wt = cat8(tr_rd(wl, lvc * 32 + 16 * s2 + 4 * h, jb * 32 + 16 * g1, lane),
+                                   tr_rd(wl, lvc * 32 + 16 * s2 + 8 + 4 * h, jb * 32 + 16 * g1, lane));
+              Y[jb] = mfma32(pt, wt, Y[jb]);
+            }
+          }
+          if (kc == 3) {
+            // the column's epilogue: d pre = dZ (1 - z^2) into the d enc partial and the d pred
+            // partial (red, buffer by column parity), then Y starts the next column at 0
+            const int cc = gc >> 2;
+            const float* z32 = z320 + (cc % 3) * 64 * PcLds::kZP;
+            float* red = red0 + (cc & 1) * 4 * 64;
+            typedef float jf2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+            for (int jb = 0; jb < 2; ++jb) {
+              const int j = jb * 32 + (lane & 31);
+              jf2 sp2 = {0.0f, 0.0f};
+#pragma unroll
+              for (int gq = 0; gq < 4; ++gq) {
+                const float4 zz = *(const float4*)(z32 + j * PcLds::kZP + 8 * gq + 4 * h);
+                const jf2 o0 = jf2{Y[jb][4 * gq], Y[jb][4 * gq + 1]} * jf2{zz.x, zz.y};
+                const jf2 o1 = jf2{Y[jb][4 * gq + 2], Y[jb][4 * gq + 3]} * jf2{zz.z, zz.w};
+                const jf2 a0 = jf2{dacc[jb][4 * gq], dacc[jb][4 * gq + 1]} + o0;
+                const jf2 a1 = jf2{dacc[jb][4 * gq + 2], dacc[jb][4 * gq + 3]} + o1;
+                dacc[jb][4 * gq] = a0.x;
+                dacc[jb][4 * gq + 1] = a0.y;
+                dacc[jb][4 * gq + 2] = a1.x;
+                dacc[jb][4 * gq + 3] = a1.y;
+                sp2 += o0 + o1;
+              }
+              float sp = sp2.x + sp2.y;
+              sp += __shfl_xor(sp, 32);
+              if (h == 0) red[pi * 64 + j] = sp;
+#pragma unroll
+              for (int q = 0; q < 16; ++q) Y[jb][q] = 0.0f;
+            }
+          }
+        }
+        // one step into producer column up (>= 1): the d pred of column up - 1 (its epilogue
+        // wrote red one barrier ago); and the staging of column up + 1
+        if (kp == 1 && up >= 1 && up - 1 < ncol && w == kWd) {
+          const int cc = up - 1;
+          const float* red = red0 + (cc & 1) * 4 * 64;
+          const float s4 = ((red[lane] + red[64 + lane]) + red[128 + lane]) + red[192 + lane];
+          a.d_pred[(((int64_t)b * ntbp + vh * a.ntb + tb) * r.U1 + ua + cc) * kJ + lane] = s4;
+        }
+        if (kp == 1 && up + 1 < ncol) stage(ua + up + 1);
+      }
+      // the DMA of the column staged next (issued one column ago) lands before that staging
+      if (kp == 0) col_dma_wait();
+      lds_barrier();
+    }
+    // the last column's d pred (its epilogue ran in the final step)
+    if (ncol > 0 && w == kWd) {
+      const int cc = ncol - 1;
+      const float* red = red0 + (cc & 1) * 4 * 64;
+      const float s4 = ((red[lane] + red[64 + lane]) + red[128 + lane]) + red[192 + lane];
+      a.d_pred[(((int64_t)b * ntbp + vh * a.ntb + tb) * r.U1 + ua + cc) * kJ + lane] = s4;
+    }
+    lds_barrier();   // (the p slots are free: the d enc partials go over them)
+    // d enc of the task: the 4 consumers' register partials in 4 LDS slots, then 4 values per
+    // thread (j fastest)
+    if (!prod) {
+      float* slotp = dep + pi * 64 * PcLds::kDeP;
+#pragma unroll
+      for (int jb = 0; jb < 2; ++jb) {
+        const int j = jb * 32 + (lane & 31);
+#pragma unroll
+        for (int gq = 0; gq < 4; ++gq)
+          *(float4*)(slotp + j * PcLds::kDeP + 8 * gq + 4 * h) =
+              make_float4(dacc[jb][4 * gq], dacc[jb][4 * gq + 1], dacc[jb][4 * gq + 2], dacc[jb][4 * gq + 3]);
+      }
+    }
+    lds_barrier();
+    float* dst = a.d_enc + ((int64_t)(vh * a.nus + us) * r.B + b) * r.T * kJ;
+#pragma unroll
+    for (int i = 0; i < 32 * 64 / 512; ++i) {
+      const int e = th + 512 * i, n = e >> 6, j = e & 63;
+      const int tq = tb * 32 + n;
+      float sum = 0.0f;
+      if (ua < ue) {
+#pragma unroll
+        for (int ww = 0; ww < 4; ++ww) sum += dep[(ww * 64 + j) * PcLds::kDeP + n];
+      }
+      if (tq < r.T) dst[(int64_t)tq * kJ + j] = sum;
+    }
+  }
+  // acc[k][jb][q] = dW[v = (vb0 + pi + 4k) * 32 + (q&3) + 8(q>>2) + 4h][j = jb*32 + (lane&31)]
+  if (prod) {
+    float* dw = a.dW + (int64_t)slot * r.V * kJ;
+#pragma unroll
+    for (int k = 0; k < kPcBlk; ++k) {
+      const int lvb = pi + 4 * k;
+      if (lvb >= nvw) continue;
+      const int vbg = vb0 + lvb;
+#pragma unroll
+      for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int v = vbg * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
+          dw[(int64_t)v * kJ + jb * 32 + (lane & 31)] = acc[k][jb][q];
+        }
+      const float tot = dbs[k] + __shfl_xor(dbs[k], 32);
+      if (h == 0) a.db[(int64_t)slot * r.V + vbg * 32 + (lane & 31)] = tot;
+    }
+  }
+}
+
 size_t joint_lds_fwd() { return (size_t)kVmaxJ * 128 + kVmaxJ * 4; }
 
 template <typename K>
@@ -1742,9 +2116,15 @@ extern "C" int sc_rnnt_joint_bwd(const float* enc, const float* pred, const void
   j.d_pred = d_pred;
   j.dW = dW;
   j.db = db;
+  hipStream_t st = (hipStream_t)stream;
+  if (SC_JOINT_PC) {
+    static const bool okpc = joint_lds_attr(joint_bwd_pc_kernel, (size_t)PcLds::kEnd);
+    SC_REQUIRE(okpc, "sc_rnnt_joint_bwd: LDS attribute");
+    hipLaunchKernelGGL(joint_bwd_pc_kernel, dim3(j.S * j.vs), dim3(512), (size_t)PcLds::kEnd, st, j);
+    return launch_status("sc_rnnt_joint_bwd");
+  }
   static const bool ok = joint_lds_attr(joint_bwd_kernel, joint_lds_bwd());
   SC_REQUIRE(ok, "sc_rnnt_joint_bwd: LDS attribute");
-  hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(joint_bwd_kernel, dim3(j.S * j.vs), dim3(64 * kJW), joint_lds_bwd(), st, j);
   return launch_status("sc_rnnt_joint_bwd");
 }
