@@ -924,6 +924,12 @@ __device__ __forceinline__ float half_sum(float x) {
   return x;
 }
 
+// SC_JOINT_FWD_TREE: 1 = the vocab block's max and exponential sum as pairwise trees.  Measured
+// slower (tools/j_ab.sh, C5 B=32: 2.28-2.29 ms vs 2.12-2.17 ms for the chains): the two columns
+// and two waves per SIMD already cover the chains' latency, and the trees cost registers.
+#ifndef SC_JOINT_FWD_TREE
+#define SC_JOINT_FWD_TREE 0
+#endif
 __global__ void __launch_bounds__(512) joint_fwd_kernel(JointArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   load_w(a, lds);
@@ -960,6 +966,27 @@ __global__ void __launch_bounds__(512) joint_fwd_kernel(JointArgs a) {
       for (int c = 0; c < 2; ++c) {
         if (c >= nc) break;
         const jf16 x = logits_vblock(lds, v0, lane, zb[c]);
+#if SC_JOINT_FWD_TREE
+        // the block's max and exponential sum as pairwise trees (depth 4, not chains of 15 / 16
+        // dependent operations: the loop is one latency chain per column and wave)
+        float t8[8], e[16];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) t8[q] = fmaxf(x[2 * q], x[2 * q + 1]);
+#pragma unroll
+        for (int w2 = 4; w2 >= 1; w2 >>= 1)
+#pragma unroll
+          for (int q = 0; q < w2; ++q) t8[q] = fmaxf(t8[2 * q], t8[2 * q + 1]);
+        const float bm = t8[0];
+        const float mn = fmaxf(m[c], bm), ml = mn * kLog2e;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) e[q] = exp2_(fmaf(x[q], kLog2e, -ml));
+#pragma unroll
+        for (int w2 = 8; w2 >= 1; w2 >>= 1)
+#pragma unroll
+          for (int q = 0; q < w2; ++q) e[q] = e[2 * q] + e[2 * q + 1];
+        s[c] = fmaf(s[c], exp2_(m[c] * kLog2e - ml), e[0]);
+        m[c] = mn;
+#else
         float bm = x[0];
 #pragma unroll
         for (int q = 1; q < 16; ++q) bm = fmaxf(bm, x[q]);
@@ -969,6 +996,7 @@ __global__ void __launch_bounds__(512) joint_fwd_kernel(JointArgs a) {
         for (int q = 0; q < 16; ++q) acc += exp2_(fmaf(x[q], kLog2e, -ml));
         s[c] = acc;
         m[c] = mn;
+#endif
       }
     }
 #pragma unroll
