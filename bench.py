@@ -67,6 +67,11 @@ def parse():
     ap.add_argument("--optimizer", choices=["hip", "torch-fused"], default="hip",
                     help="hip: torch.optim.Adam stepped by the HIP clip+Adam kernels (default); "
                          "torch-fused: torch's fused Adam kernel (A/B)")
+    ap.add_argument("--graph", choices=["on", "off"], default="off",
+                    help="on: each segment position's forward + backward captured once as a HIP "
+                         "graph and replayed (graphs.GraphedSegments; clip + Adam eager); the "
+                         "per-kernel roofline timing then comes from --timing-steps eager steps "
+                         "right after the timed region (events are not recorded by a replay)")
     ap.add_argument("--op-probe", action="store_true",
                     help="diagnostics on stderr: every ATen op one step dispatches (count, shapes, "
                          "caller), to find the step's non-HIP kernels")
@@ -452,7 +457,7 @@ def main():
     if args.rccl_footprint:
         footprint_hooks(model, args.rccl_footprint, device)
 
-    def step():
+    def eager_step():
         i = trainer.global_step
         if i % args.segments == 0:
             trainer.begin_batch()   # new batch: state reset (train.py:460)
@@ -460,9 +465,26 @@ def main():
         return trainer.train_segment(seg["feats"], seg["masks"], seg["tokens"], seg["in_lens"],
                                      seg["tgt_lens"])
 
+    step = eager_step
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    graphed = None
+    if args.graph == "on":
+        if world > 1:
+            sys.exit("bench.py: --graph on is single-process (DDP's all-reduce hooks are not "
+                     "captured)")
+        from statecatcher_amd.graphs import GraphedSegments
+        graphed = GraphedSegments(trainer, segs).capture()
+
+        def step():
+            if trainer.global_step % args.segments == 0:
+                graphed.begin_batch()
+            return graphed.step()
+        if args.warmup:
+            for _ in range(args.segments):   # one replay of every graph before timing
+                step()
+        torch.cuda.synchronize()
     if args.host_probe:
         torch.cuda.set_sync_debug_mode(1)
         step()
@@ -483,7 +505,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        if k == max(0, args.steps - args.timing_steps):
+        if graphed is None and k == max(0, args.steps - args.timing_steps):
             ops.LAUNCH_EVENTS = []
         loss = step()
     torch.cuda.synchronize()
@@ -491,12 +513,21 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    events, ops.LAUNCH_EVENTS = ops.LAUNCH_EVENTS or [], None
     if world > 1:
         t = torch.tensor([dt], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     last_loss = float(loss.item())
+    if graphed is not None and args.timing_steps > 0:
+        # a replay records no per-launch events: the kernel timings come from eager steps of the
+        # same segments right after the timed region (same kernels, same shapes)
+        for p in graphed.params:
+            p.grad = None
+        ops.LAUNCH_EVENTS = []
+        for _ in range(args.timing_steps):
+            eager_step()
+        torch.cuda.synchronize()
+    events, ops.LAUNCH_EVENTS = ops.LAUNCH_EVENTS or [], None
 
     # per-kernel average launch duration from the HIP events recorded on the launch stream
     kstats = {}
@@ -588,8 +619,12 @@ def main():
             "per_gpu_frames_per_s": round(value / world, 1),
             "roofline": roofline,
             "kernels": kernels,
-            "kernel_timing": f"HIP events on the launch stream, last {min(args.timing_steps, args.steps)} "
-                             "timed steps",
+            "kernel_timing": (f"HIP events on the launch stream, last {min(args.timing_steps, args.steps)} "
+                              "timed steps") if graphed is None else
+                             (f"HIP events on the launch stream, {args.timing_steps} eager steps "
+                              "right after the timed graph replays"),
+            "launch": "hip-graph replay per segment (forward + backward), clip + Adam eager"
+                      if graphed is not None else "eager",
             "gemm_TFLOPs_effective": round(gemm_tflops / world, 1) if gemm_tflops else None,
             "cpu_baseline": cpu,
             "loss_last": round(last_loss, 4),

@@ -100,6 +100,27 @@ __global__ void __launch_bounds__(256) colsum_final_kernel(ColsumArgs a) {
   a.out[out_index(a, n)] = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
 }
 
+// zero_async: see sc_common.h.  Words when dst and bytes allow it, else bytes.
+__global__ void __launch_bounds__(256) zero_words_kernel(uint32_t* p, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    p[i] = 0u;
+}
+__global__ void __launch_bounds__(256) zero_bytes_kernel(unsigned char* p, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    p[i] = 0;
+}
+
+void zero_async(void* dst, size_t bytes, hipStream_t st) {
+  if (!dst || bytes == 0) return;
+  const bool words = ((uintptr_t)dst % 4) == 0 && bytes % 4 == 0;
+  const int64_t n = words ? (int64_t)(bytes / 4) : (int64_t)bytes;
+  const unsigned g = (unsigned)std::min<int64_t>((n + 255) / 256, 2048);
+  if (words)
+    hipLaunchKernelGGL(zero_words_kernel, dim3(g), dim3(256), 0, st, (uint32_t*)dst, n);
+  else
+    hipLaunchKernelGGL(zero_bytes_kernel, dim3(g), dim3(256), 0, st, (unsigned char*)dst, n);
+}
+
 static int colsum_chunks(int64_t M, int64_t N) {
   // enough workgroups to fill the chip (slabs x chunks >= ~512), each chunk >= 128 rows, and
   // at most 128 chunks so the second pass stays short
@@ -132,7 +153,7 @@ extern "C" int sc_colsum(const void* x, int dtype, int64_t M, int64_t N, int64_t
   SC_REQUIRE(out, "sc_colsum: null output");
   hipStream_t st = (hipStream_t)stream;
   if (M == 0) {
-    (void)hipMemsetAsync(out, 0, N * sizeof(float), st);
+    zero_async(out, N * sizeof(float), st);
     return launch_status("sc_colsum");
   }
   SC_REQUIRE(x, "sc_colsum: null pointer");

@@ -1362,7 +1362,7 @@ static void launch_ab(const CtcArgs& a, hipStream_t st);
 template <int DT>
 static void launch_fwd(const CtcArgs& a, hipStream_t st) {
   const int64_t rows = (int64_t)a.B * a.T;
-  if (a.lin) (void)hipMemsetAsync(a.ws.flag, 0, (size_t)a.B * sizeof(int), st);   // tiny[b]
+  if (a.lin) zero_async(a.ws.flag, (size_t)a.B * sizeof(int), st);   // tiny[b]
   hipLaunchKernelGGL((ctc_emit_kernel<DT>), dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, a);
   hipLaunchKernelGGL(ctc_chain_kernel, dim3(a.B, ((a.Umax > 0 ? a.Umax : 1) + 3) / 4), dim3(256), 0,
                      st, a);

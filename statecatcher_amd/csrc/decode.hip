@@ -212,7 +212,7 @@ extern "C" int sc_ctc_greedy_decode(const void* log_probs, int dtype, int B, int
   GreedyArgs a{log_probs, B, T, V, blank, stride_b, stride_t, lengths, tokens, counts};
   hipStream_t st = (hipStream_t)stream;
   if (T == 0) {
-    (void)hipMemsetAsync(counts, 0, sizeof(int32_t) * B, st);
+    zero_async(counts, sizeof(int32_t) * B, st);
     return launch_status("sc_ctc_greedy_decode");
   }
   switch (dtype) {

@@ -197,7 +197,7 @@ extern "C" int sc_fbank(const float* audio, int B, int64_t n_samples, int64_t au
   SC_REQUIRE(kind == 0 || (workspace && workspace_bytes >= 4), "sc_fbank: mel needs the workspace");
   hipStream_t st = (hipStream_t)stream;
   FbankArgs a{audio, B, n_samples, audio_stride, F, kind, sample_rate, out, (unsigned*)workspace};
-  if (kind == 1) (void)hipMemsetAsync(workspace, 0, 4, st);
+  if (kind == 1) zero_async(workspace, 4, st);
   const int64_t frames = (int64_t)B * F;
   const unsigned grid = (unsigned)std::min<int64_t>((frames + 3) / 4, 2048);
   hipLaunchKernelGGL(fbank_kernel, dim3(grid), dim3(256), 0, st, a);

@@ -265,7 +265,7 @@ extern "C" int sc_layernorm_bwd(const void* x, const void* dy, int dtype, const 
   SC_REQUIRE(ch, "sc_layernorm_bwd: unsupported (dtype %d, D %d)", dtype, D);
   hipStream_t st = (hipStream_t)stream;
   if (rows == 0) {
-    (void)hipMemsetAsync(dgamma, 0, 2 * sizeof(float) * D, st);
+    zero_async(dgamma, 2 * sizeof(float) * D, st);
     return launch_status("sc_layernorm_bwd");
   }
   SC_REQUIRE(x && dy && gamma && mean && rstd && dx && dgamma && workspace,

@@ -1346,7 +1346,7 @@ static int scan_bwd(const void* gates, int gates_dtype, const float* gate_bias, 
   SC_REQUIRE(B <= 65535, "sc_lucy_scan_bwd: B=%d exceeds grid limit 65535", B);
   if (B == 0 || D == 0) return 0;
   SC_REQUIRE(dh0 && ds0, "sc_lucy_scan_bwd: null dh0/ds0");
-  if (T == 0 && dbias) (void)hipMemsetAsync(dbias, 0, sizeof(float) * 7 * B * D, (hipStream_t)stream);
+  if (T == 0 && dbias) zero_async(dbias, sizeof(float) * 7 * B * D, (hipStream_t)stream);
   SC_REQUIRE(T == 0 || (gates && ckpt && dout && dgates),
              "sc_lucy_scan_bwd: null gates/ckpt/dout/dgates pointer");
   SC_REQUIRE(stride_g_bt >= 0 && stride_g_td >= 0 && stride_g_cd >= 0 && stride_g_cb >= 0 &&

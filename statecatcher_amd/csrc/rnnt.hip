@@ -664,7 +664,7 @@ void launch_ab(const RnntArgs& a, hipStream_t st) {
 
 // the shift maxima start at key 0 ("nothing seen"); the emission producers raise them
 void clear_shift(const RnntArgs& a, hipStream_t st) {
-  (void)hipMemsetAsync(a.ws.cmb, 0, (size_t)a.B * (a.T + a.U1) * 4, st);
+  zero_async(a.ws.cmb, (size_t)a.B * (a.T + a.U1) * 4, st);
 }
 // shift the emissions, then alpha / beta
 void launch_lattice(const RnntArgs& a, hipStream_t st) {

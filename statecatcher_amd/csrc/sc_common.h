@@ -13,6 +13,12 @@ void set_error(const char* fmt, ...);
 void clear_error();
 // Converts the launch status of the kernel(s) just enqueued into the ABI return code.
 int launch_status(const char* what);
+// Zeroes `bytes` bytes at dst on `st` with a kernel (colsum.hip).  Used instead of
+// hipMemsetAsync everywhere: inside a captured HIP graph (graphs.GraphedSegments) a captured
+// hipMemsetAsync was not ordered before the next kernel on replay -- the RNN-T lattice's
+// shift maxima, cleared by one, came out as garbage from the second replay on
+// (tools/graph_diag5.py).  Kernel nodes keep stream order.
+void zero_async(void* dst, size_t bytes, hipStream_t st);
 
 #define SC_REQUIRE(cond, ...)            \
   do {                                   \

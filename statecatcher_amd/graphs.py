@@ -1,0 +1,116 @@
+"""The segment loop's forward + backward replayed as HIP graphs (one per segment position).
+
+The reference's training loop (/root/reference/train.py:460-581) runs, per segment, compute_loss
+with the carried state, backward, clip + Adam.  On MI355X the forward + backward of one segment
+is ~90 kernel launches; the host issues them in ~2.8 ms against a ~5 ms GPU step
+(DESIGN.md §6 item 7), so the host is one halving of the GPU step away from being the bound.
+``GraphedSegments`` captures ``SegmentTrainer.forward_backward`` of a FIXED list of
+device-resident segments once, one graph per position in the server batch, and replays them:
+
+  * graph 0 starts the batch (no input state, train.py:460); graph i > 0 reads graph i - 1's
+    output state in place, so replaying 0, 1, ..., n - 1 is the eager loop's state chain;
+  * each graph rebuilds the bf16 weight images it reads (ops.weight_images, inside the graph),
+    so it always sees the weights of the optimizer step before it;
+  * the gradients each graph writes are its own static tensors: after a replay they become the
+    parameters' ``.grad`` and the clip + Adam step (optim.clip_and_adam_step, 3-4 launches) runs
+    eagerly, as in ``SegmentTrainer.train_segment``.
+
+Same kernels in the same order as the eager step, so the losses and weights are bitwise the
+eager loop's (tests/test_gpu_graphs.py).  Restrictions, all checked: one process (no DDP: its
+bucketed all-reduce hooks are not captured), ``accumulation_steps == 1`` (every segment steps),
+HIP Adam (optim.hip_adam_eligible), no per-launch timing events during capture
+(ops.LAUNCH_EVENTS is None).  The segments' tensors are the graphs' inputs: overwrite them in
+place (``copy_``) to feed new data of the same shapes.
+"""
+import gc
+from typing import List, Optional
+
+import torch
+
+from . import ops
+from .optim import hip_adam_eligible
+
+
+class GraphedSegments:
+    def __init__(self, trainer, segments: List[dict]):
+        if trainer.ddp:
+            raise ValueError("GraphedSegments: DDP is not captured (one process only)")
+        if trainer.accumulation_steps != 1:
+            raise ValueError("GraphedSegments: accumulation_steps must be 1")
+        if not hip_adam_eligible(trainer.optimizer):
+            raise ValueError("GraphedSegments: needs the HIP clip + Adam path "
+                             "(optim.hip_adam_eligible)")
+        if not segments or not all(s["feats"].is_cuda for s in segments):
+            raise ValueError("GraphedSegments: segments must be device tensors")
+        self.trainer = trainer
+        self.segments = segments
+        self.params = [p for g in trainer.optimizer.param_groups for p in g["params"]
+                       if p.requires_grad]
+        self.graphs: List[torch.cuda.CUDAGraph] = []
+        self.losses: List[torch.Tensor] = []
+        self.grads: List[List[Optional[torch.Tensor]]] = []
+        self.pos = 0
+
+    def _run(self, i, state):
+        s = self.segments[i]
+        return self.trainer.forward_backward(s["feats"], s["masks"], s["tokens"], s["in_lens"],
+                                             s["tgt_lens"], state)
+
+    def capture(self, warmup: int = 1):
+        """Warm every segment position up on a side stream (lazy library state: the capture
+        stream's BLAS handle and workspace), then capture one graph per position."""
+        if ops.LAUNCH_EVENTS is not None:
+            raise RuntimeError("GraphedSegments.capture: per-launch timing events are on")
+        dev = self.segments[0]["feats"].device
+        # the eager loop's carried state still references its last autograd graph, whose
+        # AccumulateGrad nodes belong to the eager stream: drop it (with them) before capturing
+        self.trainer.encoder_state = None
+        for p in self.params:
+            p.grad = None
+        gc.collect()
+        torch.cuda.synchronize(dev)
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for _ in range(warmup):
+                state = None
+                for i in range(len(self.segments)):
+                    _, state = self._run(i, state)
+                    for p in self.params:
+                        p.grad = None
+        torch.cuda.current_stream(dev).wait_stream(side)
+        torch.cuda.synchronize(dev)
+        state = None
+        for i in range(len(self.segments)):
+            ops.invalidate_weight_images()   # this graph builds (at replay) the images it reads
+            for p in self.params:
+                p.grad = None
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                loss, state = self._run(i, state)
+            self.graphs.append(g)
+            self.losses.append(loss)
+            self.grads.append([p.grad for p in self.params])
+        for p in self.params:
+            p.grad = None
+        ops.invalidate_weight_images()   # (the cache holds graph memory not yet written)
+        self.pos = 0
+        return self
+
+    def begin_batch(self):
+        """New server batch: the next replay is position 0 (no input state)."""
+        self.pos = 0
+
+    def step(self):
+        """Replay the next segment position, then clip + Adam on its gradients.  Returns the
+        (graph-owned) loss tensor of that segment."""
+        if not self.graphs:
+            raise RuntimeError("GraphedSegments.step before capture()")
+        i = self.pos
+        self.graphs[i].replay()
+        for p, g in zip(self.params, self.grads[i]):
+            p.grad = g
+        self.trainer._clip_and_step()
+        self.trainer.global_step += 1
+        self.pos = (i + 1) % len(self.graphs)
+        return self.losses[i]

@@ -349,10 +349,12 @@ def invalidate_weight_images(params=None):
     if params is None:
         _IMAGES.clear()
         _FOLD.clear()
+        _SPLIT_W.clear()
         return
     for p in params:
         _IMAGES.pop(p, None)
         _FOLD.pop(p, None)
+        _SPLIT_W.pop(p, None)
 
 
 def _image_stale(w, img):

@@ -155,6 +155,20 @@ class SegmentTrainer:
     def _steps_now(self) -> bool:
         return (self.global_step + 1) % self.accumulation_steps == 0
 
+    def forward_backward(self, feats, masks, tokens, in_lens, tgt_lens, input_state):
+        """compute_loss under the trainer's autocast + backward of loss / accumulation_steps
+        (train.py:508-537) from ``input_state``.  Returns (loss, output_state).  No host sync:
+        graphs.GraphedSegments captures this call as one HIP graph."""
+        with torch.autocast(feats.device.type, dtype=self.amp_dtype or torch.float32,
+                            enabled=self.amp_dtype is not None):
+            loss, output_state, _, _ = compute_loss(
+                self.mode, self.criterion, self.net, feats, masks, tokens, in_lens, tgt_lens,
+                self.blank_id, use_rnnt_joiner=self.joiner_net, input_state=input_state,
+                compact=self.compact_rnnt)
+        # loss / accumulation_steps (train.py:535); a division by 1 is the identity
+        (loss / self.accumulation_steps if self.accumulation_steps != 1 else loss).backward()
+        return loss, output_state
+
     def train_segment(self, feats, masks, tokens, in_lens, tgt_lens):
         """One segment (train.py:508-581).  Returns the (un-divided) loss tensor."""
         stepping = self._steps_now()
@@ -163,16 +177,9 @@ class SegmentTrainer:
             sync.enter_context(self.net.no_sync())
             if self.joiner_net is not None:
                 sync.enter_context(self.joiner_net.no_sync())
-        dev_type = feats.device.type
         with sync:
-            with torch.autocast(dev_type, dtype=self.amp_dtype or torch.float32,
-                                enabled=self.amp_dtype is not None):
-                loss, output_state, _, _ = compute_loss(
-                    self.mode, self.criterion, self.net, feats, masks, tokens, in_lens, tgt_lens,
-                    self.blank_id, use_rnnt_joiner=self.joiner_net, input_state=self.encoder_state,
-                    compact=self.compact_rnnt)
-            # loss / accumulation_steps (train.py:535); a division by 1 is the identity
-            (loss / self.accumulation_steps if self.accumulation_steps != 1 else loss).backward()
+            loss, output_state = self.forward_backward(feats, masks, tokens, in_lens, tgt_lens,
+                                                       self.encoder_state)
         if stepping:
             self._clip_and_step()
             self.optimizer.zero_grad(set_to_none=True)
