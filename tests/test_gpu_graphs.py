@@ -32,13 +32,17 @@ def _segments(n, B, T, V, U, seed):
 
 def _trainer(mode, layers, hidden, V, seed=3):
     from statecatcher_amd.model import (ASRModel, CTCLoss, RNNTLoss, RNNTPredictorJoiner,
-                                        build_lucyrnn_config)
+                                        build_lucyrnn_config, build_xlstm_config)
     from statecatcher_amd.train import SegmentTrainer
     torch.manual_seed(seed)
-    model = ASRModel(None, build_lucyrnn_config(80, hidden, layers, V), vocab_size=V, feat_dim=80,
-                     proj_dim=-1).to(DEV)
-    with torch.no_grad():
-        model.encoder.output_proj.weight.normal_(0, 0.02)
+    if mode == "xlstm":   # C4's encoder family: layers = blocks, hidden = embedding_dim
+        cfg = build_xlstm_config(80, V, num_heads=2, num_blocks=layers, embedding_dim=hidden)
+        model = ASRModel(None, cfg, vocab_size=V, feat_dim=80, proj_dim=-1).to(DEV)
+    else:
+        model = ASRModel(None, build_lucyrnn_config(80, hidden, layers, V), vocab_size=V,
+                         feat_dim=80, proj_dim=-1).to(DEV)
+        with torch.no_grad():
+            model.encoder.output_proj.weight.normal_(0, 0.02)
     params = list(model.parameters())
     kw = {}
     crit = CTCLoss(blank=0, zero_infinity=True)
@@ -56,6 +60,7 @@ def _trainer(mode, layers, hidden, V, seed=3):
     ("ctc", 3, 256, 256, 4, 300, 20),
     ("ctc", 6, 512, 1024, 2, 1500, 150),   # config C2's model and segment length
     ("rnnt", 2, 256, 256, 2, 200, 12),
+    ("xlstm", 2, 256, 256, 2, 256, 20),    # C4's encoder (mLSTM blocks) + CTC
 ])
 def test_graphed_segments_train_bitwise_as_the_eager_loop(mode, layers, hidden, V, B, T, U):
     from statecatcher_amd.graphs import GraphedSegments
