@@ -20,7 +20,8 @@ eager loop's (tests/test_gpu_graphs.py).  Restrictions, all checked: one process
 bucketed all-reduce hooks are not captured), ``accumulation_steps == 1`` (every segment steps),
 HIP Adam (optim.hip_adam_eligible), no per-launch timing events during capture
 (ops.LAUNCH_EVENTS is None).  The segments' tensors are the graphs' inputs: overwrite them in
-place (``copy_``) to feed new data of the same shapes.
+place (``copy_``) to feed new data of the same shapes.  Periodic checkpoints
+(``SegmentTrainer.save_every_n_updates``) are the caller's: ``step`` replays and steps only.
 """
 import gc
 from typing import List, Optional
