@@ -129,6 +129,25 @@ def test_capture_after_eager_steps_continues_the_eager_run():
     assert all(torch.equal(a, b) for a, b in zip(p_a, p_b))
 
 
+def test_bench_graph_mode_prints_its_line():
+    """`bench.py --graph on` end to end at a small size (a child process: the bench owns its
+    process): one JSON line with the replay named in `launch` and the kernel timings taken from
+    the eager steps after the timed region."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, "bench.py", "--graph", "on", "--steps", "4", "--warmup", "2",
+                        "--batch", "2", "--seq", "300", "--segments", "2", "--cpu-baseline", "off"],
+                       cwd=root, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["launch"].startswith("hip-graph") and "eager steps" in line["kernel_timing"]
+    assert line["value"] > 0 and line["roofline"]["achieved"] > 0
+    assert line["kernels"]["lucy_scan_bwd"]["launches"] > 0
+
+
 def test_graphed_segments_refuse_what_they_cannot_capture():
     from statecatcher_amd import ops
     from statecatcher_amd.graphs import GraphedSegments
