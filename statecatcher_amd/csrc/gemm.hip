@@ -250,6 +250,154 @@ __global__ void __launch_bounds__(512) wgrad_kernel(WgradArgs a) {
       }
 }
 
+// SC_GEMM_MF32 (A/B): the TI = 224 tile on v_mfma_f32_32x32x16_bf16.  Each wave owns one 32-column
+// block of the tile (columns 32 w .. 32 w + 31) and all 7 row blocks of 32: per half-stage (two
+// k-steps of 16 L-rows) 14 MFMAs of 32 cycles instead of 28 of 16 (half the matrix-instruction
+// issue), from 2 x (1 + 7) fragments of two transposed reads each.  The LDS ring, its DMA and
+// the images are wgrad_kernel's; the ring runs kSlots - 1 half-stages ahead (the slot a DMA
+// refills was read in the previous iteration, before this iteration's barrier).
+// Correct (tests/test_gpu_gemm.py on it) and measured SLOWER (tools/r5_mf32.sh, one box): 202-204
+// vs 187-189 us alone, 169-173 vs 166-167 us in the C2 step -- a 224 x 32 wave tile reads 32
+// fragments per half-stage where the 2 x 4 grid of 112 x 64 tiles reads 22, and halving the MFMA
+// instruction count does not buy that back.  Off by default.
+#ifndef SC_GEMM_MF32
+#define SC_GEMM_MF32 0
+#endif
+typedef float f16v __attribute__((ext_vector_type(16)));
+
+__global__ void __launch_bounds__(512) wgrad32_kernel(WgradArgs a) {
+  constexpr int TTI = 7, TI = 32 * TTI, NCA = TI / 8;
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const int lane = threadIdx.x & 63;
+  const int w = uniform(threadIdx.x >> 6);
+  const int nwg = a.tiles * a.S;
+  const int bid = blockIdx.x;
+  const int xcd = bid % 8, qq = nwg / 8, rr = nwg % 8;
+  const int lid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + bid / 8;
+  const int split = lid / a.tiles, tile = lid % a.tiles;
+  const int ti = tile / a.ntj, tj = tile % a.ntj;
+  const int i0 = ti * TI, j0 = tj * kTJ;
+  const int nkb = a.L / kTL;
+  const int kb0 = (int)((int64_t)split * nkb / a.S), kb1 = (int)((int64_t)(split + 1) * nkb / a.S);
+
+  uint32_t voA[2], voB[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int row = 4 * w + 2 * q + (lane >> 5);
+    const int c = (lane & 31) ^ (swz_f(row) << 1);
+    voA[q] = (uint32_t)(row * a.lda + i0 + 8 * min(c, NCA - 1)) * 2u;
+    voB[q] = (uint32_t)(row * a.ldb + j0 + 8 * c) * 2u;
+  }
+  constexpr int kHalf = 32 * kRowB;
+  const uint32_t lds0 = lds_addr(lds);
+  auto stage = [&](int h) __attribute__((always_inline)) {
+    const int64_t r = (int64_t)kb0 * kTL + 32 * h;
+    const uint32_t la = lds0 + (h % kSlots) * 2 * kHalf + 4 * w * kRowB;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) dma_to_lds_s<16>(a.A + r * a.lda, voA[q], la + q * 1024);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) dma_to_lds_s<16>(a.B + r * a.ldb, voB[q], la + kHalf + q * 1024);
+  };
+  // 32x32x16 operand geometry: lane l holds column 32-block-base + (l & 31), k-rows
+  // 8 (l >> 5) .. +7 of the k-step.  Group g = lane >> 4: columns 16 (g & 1) .., rows 8 (g >> 1) ..;
+  // within the group lane 4q+p addresses row q (+4 for the second read), columns 4p .. 4p+3
+  const int g = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
+  f16v acc[TTI];
+#pragma unroll
+  for (int t = 0; t < TTI; ++t)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[t][e] = 0.0f;
+  const int nh = 2 * (kb1 - kb0);
+  auto frag = [&](uint32_t img, int r0, int col) __attribute__((always_inline)) {
+    const uint32_t o = (uint32_t)((col & 7) ? 8 : 0);
+    const i2v lo = tr_read(img + img_off(r0, col >> 3) + o);
+    const i2v hi = tr_read(img + img_off(r0 + 4, col >> 3) + o);
+    return i4v{lo.x, lo.y, hi.x, hi.y};
+  };
+  auto load_ks = [&](int h, int ks, i4v& bf, i4v (&af)[TTI]) __attribute__((always_inline)) {
+    const uint32_t ia = lds0 + (h % kSlots) * 2 * kHalf, ib = ia + kHalf;
+    const int r0 = 16 * ks + 8 * (g >> 1) + q4;
+    bf = frag(ib, r0, 32 * w + 16 * (g & 1) + 4 * p4);
+#pragma unroll
+    for (int t = 0; t < TTI; ++t) af[t] = frag(ia, r0, 32 * t + 16 * (g & 1) + 4 * p4);
+  };
+  auto mfmas = [&](const i4v& bf, const i4v (&af)[TTI]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int t = 0; t < TTI; ++t)
+      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(b8v, af[t]),
+                                                       __builtin_bit_cast(b8v, bf), acc[t], 0, 0, 0);
+  };
+  auto wait_younger = [&](int n) __attribute__((always_inline)) {
+    if (n >= 3) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else if (n == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (n == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else dma_wait();
+  };
+  constexpr int kAhead = kSlots - 1;   // half-stages in flight beyond the one being read
+  for (int h = 0; h < kAhead && h < nh; ++h) stage(h);
+  // k-step software pipeline: iteration h multiplies k-step (h, 0) from registers while (h, 1)
+  // comes out of LDS, then (h, 1) while (h + 1, 0) does -- so h + 1 must have landed before the
+  // iteration's barrier, and the slot refilled there is (h - 1)'s (read during iteration h - 1)
+  // (the last iteration re-reads slot h for its (h + 1, 0): unused, in bounds)
+  i4v bfX, afX[TTI], bfY, afY[TTI], bfZ, afZ[TTI];
+  if (nh > 0) {
+    wait_younger(min(kAhead - 1, nh - 1));
+    lds_barrier();
+    load_ks(0, 0, bfX, afX);
+  }
+  auto iter = [&](int h, i4v& bc, i4v (&ac)[TTI], i4v& bn, i4v (&an)[TTI])
+      __attribute__((always_inline)) {
+    if (h + 1 < nh) wait_younger(min(kAhead - 2, nh - 2 - h));   // h + 1 landed
+    lds_barrier();
+    if (h + kAhead < nh) stage(h + kAhead);
+    load_ks(h, 1, bfY, afY);
+    mfmas(bc, ac);
+#if SC_GEMM_SGB
+#pragma unroll
+    for (int q = 0; q < TTI; ++q) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // DS reads
+    }
+    __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+#endif
+    load_ks(min(h + 1, nh - 1) == h + 1 ? h + 1 : h, 0, bn, an);
+    mfmas(bfY, afY);
+#if SC_GEMM_SGB
+#pragma unroll
+    for (int q = 0; q < TTI; ++q) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+#endif
+  };
+  int h = 0;
+  for (; h + 1 < nh; h += 2) {
+    iter(h, bfX, afX, bfZ, afZ);
+    iter(h + 1, bfZ, afZ, bfX, afX);
+  }
+  if (h < nh) iter(h, bfX, afX, bfZ, afZ);
+  // epilogue: acc[t][e] = dW[i = 32 t + (e & 3) + 8 (e >> 2) + 4 (lane >> 5)][j = 32 w + (lane & 31)]
+  float* cs = a.C + (int64_t)split * a.I * a.J;
+#pragma unroll
+  for (int t = 0; t < TTI; ++t)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int i = i0 + 32 * t + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+      const int j = j0 + 32 * w + (lane & 31);
+      cs[(int64_t)i * a.J + j] = acc[t][e];
+    }
+}
+
+static void launch_wgrad32(const WgradArgs& a, hipStream_t st) {
+  constexpr size_t lds = (size_t)kSlots * 2 * 32 * kRowB;
+  static const bool ok = hipFuncSetAttribute((const void*)wgrad32_kernel,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             (int)lds) == hipSuccess;
+  (void)ok;
+  hipLaunchKernelGGL(wgrad32_kernel, dim3(a.tiles * a.S), dim3(512), lds, st, a);
+}
+
 template <int TTI>
 static void launch_wgrad(const WgradArgs& a, hipStream_t st) {
   auto kern = wgrad_kernel<TTI>;
@@ -298,7 +446,8 @@ extern "C" int sc_gemm_wgrad_bf16(const void* A, int64_t lda, const void* B, int
               (I / ti) * (J / kTJ), lda, ldb};
   SC_REQUIRE(S >= 1 && S <= L / kTL, "sc_gemm_wgrad_bf16: S=%d outside [1, L/64]", S);
   hipStream_t st = (hipStream_t)stream;
-  if (ti == 224) launch_wgrad<7>(a, st);
+  if (ti == 224 && SC_GEMM_MF32) launch_wgrad32(a, st);
+  else if (ti == 224) launch_wgrad<7>(a, st);
   else launch_wgrad<8>(a, st);
   return launch_status("sc_gemm_wgrad_bf16");
 }
