@@ -204,3 +204,62 @@ def test_rnnt_segment_through_trainer_saves_joiner_and_skips_joiner_clip(tmp_pat
     assert any(not torch.equal(j0[k], v) for k, v in joiner.state_dict().items())   # joiner trained
     ck = torch.load(os.path.join(tmp_path, "model_epoch1_step1.pt"), weights_only=True)
     assert set(ck) == {"model", "joiner"} and set(ck["joiner"]) == set(joiner.state_dict())
+
+
+def train_rnnt(rank, world, shard):
+    """C5's loop shape: the encoder AND the joiner DDP-wrapped (train.py:368-375 puts both in one
+    optimizer), clip over the encoder's parameters only."""
+    from statecatcher_amd.model import RNNTPredictorJoiner
+    torch.manual_seed(0)
+    model = TinyStateful()
+    joiner = RNNTPredictorJoiner(V, 4, 6, V)
+    opt = torch.optim.Adam(list(model.parameters()) + list(joiner.parameters()), lr=1e-2)
+    tr = SegmentTrainer(model, TorchRNNTLoss(), opt, mode="rnnt", joiner=joiner, max_grad_norm=0.5,
+                        bucket_cap_mb=0.001)
+    if world > 1:
+        assert isinstance(tr.joiner_net, nn.parallel.DistributedDataParallel)
+    lo, hi = (rank * B // world, (rank + 1) * B // world) if shard else (0, B)
+    losses = []
+    for segs in data(2)[:1]:
+        tr.begin_batch()
+        for feats, mask, tok, il, tl in segs[:2]:
+            loss = tr.train_segment(feats[lo:hi], mask[lo:hi], tok[lo:hi], il[lo:hi], tl[lo:hi])
+            losses.append(float(loss.detach()))
+    sd = {f"m.{k}": v.detach().clone() for k, v in model.state_dict().items()}
+    sd.update({f"j.{k}": v.detach().clone() for k, v in joiner.state_dict().items()})
+    return sd, losses
+
+
+def _worker_rnnt(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        sd, losses = train_rnnt(rank, world, shard=True)
+        q.put((rank, {k: v.numpy() for k, v in sd.items()}, losses))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rnnt_ddp_world2_matches_single_process_full_batch():
+    """The C5 (RNN-T) loop at world size 2: encoder and joiner both all-reduced, ranks bitwise
+    equal, and equal to one process on the full batch (mean-reduced loss over equal shards)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_worker_rnnt, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in procs:
+        rank, sd, losses = q.get(timeout=180)
+        res[rank] = ({k: torch.from_numpy(v) for k, v in sd.items()}, losses)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ref_sd, ref_losses = train_rnnt(0, 1, shard=False)
+    assert any(k.startswith("j.") for k in ref_sd)
+    for k in ref_sd:
+        torch.testing.assert_close(res[0][0][k], res[1][0][k], rtol=0, atol=0)
+        torch.testing.assert_close(res[0][0][k], ref_sd[k], rtol=1e-5, atol=1e-6)
+    for a, b, r in zip(res[0][1], res[1][1], ref_losses):
+        assert abs((a + b) / 2 - r) < 1e-5 * max(1.0, abs(r))
