@@ -263,3 +263,62 @@ def test_rnnt_ddp_world2_matches_single_process_full_batch():
         torch.testing.assert_close(res[0][0][k], ref_sd[k], rtol=1e-5, atol=1e-6)
     for a, b, r in zip(res[0][1], res[1][1], ref_losses):
         assert abs((a + b) / 2 - r) < 1e-5 * max(1.0, abs(r))
+
+
+class TinyDictStateful(TinyStateful):
+    """The xLSTM encoder's state shape (C4): a dict of per-block tuples, carried the same way."""
+
+    def forward(self, feats, mask, states=None):
+        prev = None if states is None else ([states["block0"][0]], None)
+        logits, (hs, _) = super().forward(feats, mask, prev)
+        return logits, {"block0": (hs[0], hs[0] * 0.25, torch.zeros(feats.shape[0], 1))}
+
+
+def train_dict(rank, world, shard):
+    torch.manual_seed(0)
+    model = TinyDictStateful()
+    opt = torch.optim.Adam(model.parameters(), lr=1e-2)
+    tr = SegmentTrainer(model, nn.CTCLoss(blank=0, zero_infinity=True), opt, max_grad_norm=0.5,
+                        bucket_cap_mb=0.001)
+    lo, hi = (rank * B // world, (rank + 1) * B // world) if shard else (0, B)
+    losses = []
+    for segs in data(4):
+        tr.begin_batch()
+        for feats, mask, tok, il, tl in segs:
+            losses.append(float(tr.train_segment(feats[lo:hi], mask[lo:hi], tok[lo:hi], il[lo:hi],
+                                                 tl[lo:hi]).detach()))
+            assert isinstance(tr.encoder_state, dict)
+    return {k: v.detach().clone() for k, v in model.state_dict().items()}, losses
+
+
+def _worker_dict(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        sd, losses = train_dict(rank, world, shard=True)
+        q.put((rank, {k: v.numpy() for k, v in sd.items()}, losses))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dict_state_ddp_world2_matches_single_process_full_batch():
+    """C4's loop shape (dict-of-tuples encoder state, as xLSTMLarge returns) at world size 2."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_worker_dict, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in procs:
+        rank, sd, losses = q.get(timeout=120)
+        res[rank] = ({k: torch.from_numpy(v) for k, v in sd.items()}, losses)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ref_sd, ref_losses = train_dict(0, 1, shard=False)
+    for k in ref_sd:
+        torch.testing.assert_close(res[0][0][k], res[1][0][k], rtol=0, atol=0)
+        torch.testing.assert_close(res[0][0][k], ref_sd[k], rtol=1e-5, atol=1e-6)
+    for a, b, r in zip(res[0][1], res[1][1], ref_losses):
+        assert abs((a + b) / 2 - r) < 1e-5 * max(1.0, abs(r))
