@@ -82,6 +82,7 @@ class GraphedSegments:
         torch.cuda.current_stream(dev).wait_stream(side)
         torch.cuda.synchronize(dev)
         state = None
+        self.graphs, self.losses, self.grads = [], [], []   # (a second capture replaces the first)
         for i in range(len(self.segments)):
             ops.invalidate_weight_images()   # this graph builds (at replay) the images it reads
             for p in self.params:
