@@ -1184,6 +1184,10 @@ __global__ void __launch_bounds__(64) ctc_x64_kernel(CtcArgs a) {
   const int Tb = clampi(a.in_lens[b], 0, a.T);
   const int Ub = clampi(a.tgt_lens[b], 0, a.Umax);
   if (Tb == 0) return;
+  // sharp[b] = 2: this sequence's rows and offsets are the exact lattice's (one offset per step),
+  // which is what the gradient reads them as.  A flagged sequence this kernel does not redo
+  // (U > 255: no launch) keeps sharp[b] = 1 and the log-space rows and offsets.
+  if (threadIdx.x == 0) a.ws.sharp[b] = 2;
   if (is_beta) x64_run<PPL, DT, true>(a, b, Tb, Ub);
   else x64_run<PPL, DT, false>(a, b, Tb, Ub);
 }
@@ -1276,8 +1280,9 @@ __global__ void __launch_bounds__(256) ctc_grad_kernel(CtcArgs a) {
   // exp(lcab + nll - lp) = 2^(lcab2 + offA + offB + c_t - ll2s - lp*log2e): the lattice holds
   // alpha_t - sum_{t'<=t} c and beta_t - sum_{t'>=t} c, so alpha + beta carries c_t once more than
   // the shifted log-likelihood ll2s; offsets folded in fp64
-  // steps per re-centring (a sequence the exact lattice recomputed has one offset per step)
-  const int per = a.ws.sharp[b] ? 1 : 2 * a.kh;
+  // steps per re-centring (a sequence the exact lattice recomputed, sharp[b] == 2, has one
+  // offset per step; a flagged one it did not redo, sharp[b] == 1, keeps the log-space offsets)
+  const int per = a.ws.sharp[b] == 2 ? 1 : 2 * a.kh;
   const float koff = (float)(a.ws.offA[(int64_t)b * (a.T + 1) + (t + 1) / per] +
                              a.ws.offB[(int64_t)b * (a.T + 1) + (Tb - t) / per] +
                              (double)a.ws.cst[(int64_t)b * a.T + t] - a.ws.ll2s[b]);
@@ -1374,7 +1379,9 @@ static void launch_fwd(const CtcArgs& a, hipStream_t st) {
     default: launch_ab(a, st); break;
   }
   // the sequences a lattice flagged (sharp[b]) again, exactly; the others' workgroups exit at
-  // once.  U <= 255 (the pairs fit one wave, 4 per lane); longer targets keep the log-space result
+  // once.  U <= 255 only (the pairs fit one wave, 4 per lane): a flagged sequence with a longer
+  // target keeps the log-space result, whose fp32 drift at such sharpness is ~1e-3 .. 1e-2
+  // relative in the gradient (tests/test_gpu_ctc.py::test_ctc_sharp_long_targets_keep_log_space)
   switch (x64_ppl(a.Umax)) {
     case 1: hipLaunchKernelGGL((ctc_x64_kernel<1, DT>), dim3(2 * a.B), dim3(64), 0, st, a); break;
     case 2: hipLaunchKernelGGL((ctc_x64_kernel<2, DT>), dim3(2 * a.B), dim3(64), 0, st, a); break;

@@ -264,6 +264,7 @@ __global__ void __launch_bounds__(512) wgrad_kernel(WgradArgs a) {
 #define SC_GEMM_MF32 0
 #endif
 typedef float f16v __attribute__((ext_vector_type(16)));
+#if SC_GEMM_MF32   // (A/B builds only: tools/ab/mf32; not in the product library)
 
 __global__ void __launch_bounds__(512) wgrad32_kernel(WgradArgs a) {
   constexpr int TTI = 7, TI = 32 * TTI, NCA = TI / 8;
@@ -397,6 +398,7 @@ static void launch_wgrad32(const WgradArgs& a, hipStream_t st) {
   (void)ok;
   hipLaunchKernelGGL(wgrad32_kernel, dim3(a.tiles * a.S), dim3(512), lds, st, a);
 }
+#endif  // SC_GEMM_MF32
 
 template <int TTI>
 static void launch_wgrad(const WgradArgs& a, hipStream_t st) {
@@ -446,8 +448,11 @@ extern "C" int sc_gemm_wgrad_bf16(const void* A, int64_t lda, const void* B, int
               (I / ti) * (J / kTJ), lda, ldb};
   SC_REQUIRE(S >= 1 && S <= L / kTL, "sc_gemm_wgrad_bf16: S=%d outside [1, L/64]", S);
   hipStream_t st = (hipStream_t)stream;
-  if (ti == 224 && SC_GEMM_MF32) launch_wgrad32(a, st);
-  else if (ti == 224) launch_wgrad<7>(a, st);
+#if SC_GEMM_MF32
+  if (ti == 224) launch_wgrad32(a, st);
+  else
+#endif
+  if (ti == 224) launch_wgrad<7>(a, st);
   else launch_wgrad<8>(a, st);
   return launch_status("sc_gemm_wgrad_bf16");
 }

@@ -1606,6 +1606,7 @@ __global__ void __launch_bounds__(64 * kJW) joint_bwd_kernel(JointArgs a) {
 #ifndef SC_JOINT_PC
 #define SC_JOINT_PC 0
 #endif
+#if SC_JOINT_PC   // (A/B builds only: tools/ab/jpc; not in the product library)
 constexpr int kPcBlk = 4;   // vocab blocks per producer
 
 struct PcLds {   // byte offsets
@@ -1954,6 +1955,7 @@ __global__ void __launch_bounds__(512) joint_bwd_pc_kernel(JointArgs a) {
     }
   }
 }
+#endif  // SC_JOINT_PC
 
 size_t joint_lds_fwd() { return (size_t)kVmaxJ * 128 + kVmaxJ * 4; }
 
@@ -2145,12 +2147,14 @@ extern "C" int sc_rnnt_joint_bwd(const float* enc, const float* pred, const void
   j.dW = dW;
   j.db = db;
   hipStream_t st = (hipStream_t)stream;
-  if (SC_JOINT_PC) {
+#if SC_JOINT_PC
+  {
     static const bool okpc = joint_lds_attr(joint_bwd_pc_kernel, (size_t)PcLds::kEnd);
     SC_REQUIRE(okpc, "sc_rnnt_joint_bwd: LDS attribute");
     hipLaunchKernelGGL(joint_bwd_pc_kernel, dim3(j.S * j.vs), dim3(512), (size_t)PcLds::kEnd, st, j);
     return launch_status("sc_rnnt_joint_bwd");
   }
+#endif
   static const bool ok = joint_lds_attr(joint_bwd_kernel, joint_lds_bwd());
   SC_REQUIRE(ok, "sc_rnnt_joint_bwd: LDS attribute");
   hipLaunchKernelGGL(joint_bwd_kernel, dim3(j.S * j.vs), dim3(64 * kJW), joint_lds_bwd(), st, j);

@@ -63,6 +63,7 @@ struct TnArgs {
   int M, N, K, ntn, tiles;
   uint32_t lda, ldb, ldc;   // elements
   uint32_t cbytes;          // addressable bytes of C (M * ldc * 2)
+  int gm;                   // tnw: row panels per tile group (the per-XCD raster)
 };
 
 // physical-chunk XOR of image row r (8 chunks of 16 B per 128-byte row)
@@ -700,6 +701,168 @@ __global__ void __launch_bounds__(512, 1) tnpp_kernel(TnArgs a) {
   if (hf == 0) __builtin_amdgcn_s_barrier();   // same barrier count in both halves
 }
 
+// ------------------------------------------------------------------------------------------
+// One wave per SIMD, 256 x 256 tiles (tile_m = 1): tnw_kernel.
+//
+// tn256 / tnpp run 8 waves (two per SIMD) of 128 x 64 outputs each; with 16x16x32 MFMAs a wave
+// then reads ~0.4 fragments per MFMA, and the CU's four SIMDs together ask the LDS for ~220
+// B/clk of its 256: fragment reads, not the MFMA pipe, pace their loops (0.70-0.85 PF at the
+// gate shape against hipBLASLt's 1.0-1.2).  Here 4 waves each own a 128 x 128 block of the
+// tile: the 256 fp32 accumulators live in the AGPR half of the 512-entry register file that one
+// wave per SIMD may use (MI355X_MICROARCH.md §Register files), the two 16-fragment operand sets
+// (x rows / W rows of one 32-deep k-step, 64 VGPRs each) in the VGPR half.  Per k-step a wave
+// issues 16 ds_read_b128 for 64 MFMAs (1,024 cycles): ~64 B/clk/CU of LDS reads.
+//   * LDS: two 64 KiB slots of one 64-deep K-tile ([256 x rows][128 B] then [256 W rows][128 B]),
+//     the 16-byte chunk of image row r at physical position c ^ swz(r) (applied on the DMA source
+//     address; every fragment read conflict-free under ds_read_b128's lane groups, checked by
+//     script);
+//   * K-tile kt: k-step 0 MFMAs on set X while set Y (k-step 1) is read; then this wave's DMA of
+//     K-tile kt + 1 is retired (vmcnt(0)) and ONE barrier passed -- every wave's share of it has
+//     landed and every wave has finished reading slot kt % 2 -- after which K-tile kt + 2 is DMA'd
+//     into that slot and set X of K-tile kt + 1 is read while k-step 1's MFMAs run on Y.  A DMA
+//     has two k-steps (2,048 MFMA cycles) to land;
+//   * one tile per workgroup, no persistence: the output (32 16-byte stores per wave, each lane
+//     writing 32 consecutive columns of one row) is issued after the K loop and nothing waits for
+//     it, so it drains while the CU's next workgroup runs.  (A persistent workgroup would have to
+//     retire those stores at its next DMA wait: gfx9's vmcnt counts both.)
+//   * the MFMA A operand is the W image (lane rows drawn so that a lane's 8 x 4 accumulators of
+//     one x fragment are 32 consecutive output columns), the B operand the x image;
+//   * XCD-aware tile order: the tiles of an XCD are consecutive, column tiles fastest, so an x
+//     panel comes from HBM once per XCD and W stays in its L2.
+namespace tnw {
+constexpr int kSlotB = 64 * 1024;   // one K-tile: A image 32 KiB + B image 32 KiB
+struct Frag { i4v v[8]; };          // 8 fragments of one operand for one k-step
+}  // namespace tnw
+
+__global__ void __launch_bounds__(256, 1) tnw_kernel(TnArgs a) {
+  using namespace tnw;
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const int lane = threadIdx.x & 63;
+  const int w = uniform(threadIdx.x >> 6);
+  const int wm = w >> 1, wn = w & 1;
+  const int l15 = lane & 15, l4 = lane >> 4;
+  // ---- tile: XCD x (bids go round-robin over the 8 XCDs) owns row panels [p0, p0 + np); its
+  // k-th workgroup takes tile k of a grouped raster: groups of gm panels, columns outer, panels
+  // inner, so the ~32 tiles in flight on an XCD share gm x-panels and 32 / gm W-panels in its L2
+  const int bid = blockIdx.x;
+  const int npan = (a.M + 255) / 256;
+  const int xcd = bid % 8, k = bid / 8;
+  const int pq = npan / 8, pr = npan % 8;
+  const int np = pq + (xcd < pr), p0 = xcd * pq + min(xcd, pr);
+  if (k >= np * a.ntn) return;
+  const int grp = k / (a.gm * a.ntn), first = grp * a.gm;
+  const int gsz = min(a.gm, np - first), within = k - grp * a.gm * a.ntn;
+  const int m0 = (p0 + first + within % gsz) * 256, n0 = (within / gsz) * 256;
+  const int nkt = a.K / kBK;
+  const uint32_t lds0 = lds_addr(lds);
+
+  // ---- DMA: wave w stages image rows 64 w .. 64 w + 63 of both operands (8 + 8 pieces) ----
+  uint32_t voA[8], voB[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int r = 64 * w + 8 * q + (lane >> 3);
+    const uint32_t ch = 8u * (uint32_t)((lane & 7) ^ swz(r));
+    voA[q] = ((uint32_t)min(m0 + r, a.M - 1) * a.lda + ch) * 2u;
+    voB[q] = ((uint32_t)(n0 + r) * a.ldb + ch) * 2u;
+  }
+  auto dma = [&](int kt) __attribute__((always_inline)) {
+    const uint32_t sb = lds0 + (uint32_t)((kt & 1) * kSlotB) + (uint32_t)(w * 8 * 1024);
+    const __bf16* pa = a.A + kt * kBK;
+    const __bf16* pb = a.B + kt * kBK;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) dma_to_lds_s<16>(pa, voA[q], sb + q * 1024);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) dma_to_lds_s<16>(pb, voB[q], sb + 32 * 1024 + q * 1024);
+  };
+
+  // ---- fragment offsets within a slot (k-step kk flips address bit 6) ----
+  uint32_t offX[8], offW[8];
+#pragma unroll
+  for (int f = 0; f < 8; ++f) {
+    const int rx = wm * 128 + f * 16 + l15;                              // x rows
+    offX[f] = (uint32_t)(rx * kRowB + 16 * (l4 ^ swz(rx)));
+    const int rw = wn * 128 + (l15 >> 2) * 32 + f * 4 + (l15 & 3);       // W rows
+    offW[f] = (uint32_t)(32 * 1024 + rw * kRowB + 16 * (l4 ^ swz(rw)));
+  }
+  auto read = [&](int kt, int kk, Frag& fx, Frag& fw) __attribute__((always_inline)) {
+    const uint32_t sb = lds0 + (uint32_t)((kt & 1) * kSlotB);
+    const uint32_t x = 64u * kk;
+#pragma unroll
+    for (int f = 0; f < 8; ++f) fw.v[f] = lds_read16(sb + (offW[f] ^ x));
+#pragma unroll
+    for (int f = 0; f < 8; ++f) fx.v[f] = lds_read16(sb + (offX[f] ^ x));
+  };
+  f4v acc[8][8];   // [x fragment][W fragment]
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
+  auto mfmas = [&](const Frag& fx, const Frag& fw) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+            __builtin_bit_cast(b8v, fw.v[j]), __builtin_bit_cast(b8v, fx.v[i]), acc[i][j], 0, 0, 0);
+  };
+
+  // ---- prologue: K-tiles 0 and 1 in flight, 0 retired ----
+  dma(0);
+  if (nkt > 1) {
+    dma(1);
+    dma_wait_younger<16>();
+  } else {
+    dma_wait();
+  }
+  lds_barrier();
+  Frag X, Xw, Y, Yw;
+  read(0, 0, X, Xw);
+  for (int kt = 0; kt < nkt; ++kt) {
+    // k-step 0 on X while k-step 1's fragments come in
+    read(kt, 1, Y, Yw);
+    mfmas(X, Xw);
+    lds_read_wait();
+    if (kt + 1 < nkt) {
+      dma_wait();      // this wave's share of K-tile kt + 1 (nothing younger is in flight)
+      lds_barrier();   // ... everyone's, and every read of slot kt % 2 is done
+      if (kt + 2 < nkt) dma(kt + 2);
+      read(kt + 1, 0, X, Xw);
+    }
+    mfmas(Y, Yw);
+  }
+
+  // ---- epilogue: per x fragment, 32 consecutive bf16 columns per lane = four 16-byte stores ----
+  const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(a.C, 0, a.cbytes, 0x00020000);
+  const uint32_t col = (uint32_t)(n0 + wn * 128 + l4 * 32);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint32_t row = (uint32_t)(m0 + wm * 128 + i * 16 + l15);
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) {
+      i4v v;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const int j = 2 * s4 + (d >> 1), e = 2 * (d & 1);
+        const b2v p = {(__bf16)acc[i][j][e], (__bf16)acc[i][j][e + 1]};
+        v[d] = __builtin_bit_cast(int, p);
+      }
+      __builtin_amdgcn_raw_buffer_store_b128(v, crs, (row * a.ldc + col + 8u * s4) * 2u, 0, 0);
+    }
+  }
+}
+
+int launch_tnw(const TnArgs& a, hipStream_t st) {
+  constexpr size_t lds = 2 * (size_t)tnw::kSlotB;   // 128 KiB
+  static const bool ok = hipFuncSetAttribute((const void*)tnw_kernel,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             (int)lds) == hipSuccess;
+  (void)ok;
+  const int npan = (a.M + 255) / 256;
+  const int grid = 8 * ((npan + 7) / 8) * a.ntn;
+  hipLaunchKernelGGL(tnw_kernel, dim3(grid), dim3(256), lds, st, a);
+  return 0;
+}
+
 int launch_tn256(const TnArgs& a, hipStream_t st) {
   constexpr size_t lds = 2 * 4 * (size_t)kHalfB;   // 128 KiB
   static const bool ok = hipFuncSetAttribute((const void*)tn256_kernel,
@@ -747,9 +910,10 @@ extern "C" int sc_gemm_tn_bf16(const void* A, int64_t lda, const void* B, int64_
   SC_REQUIRE(M > 0 && N > 0 && K > 0, "sc_gemm_tn_bf16: empty shape M=%d N=%d K=%d", M, N, K);
   SC_REQUIRE(K % kBK == 0, "sc_gemm_tn_bf16: K=%d must be a multiple of 64 (zero-pad it)", K);
   SC_REQUIRE(N % kTN == 0, "sc_gemm_tn_bf16: N=%d must be a multiple of 256", N);
-  SC_REQUIRE(tile_m == 0 || tile_m == 128 || tile_m == 192 || tile_m == 256 || tile_m == 257,
-             "sc_gemm_tn_bf16: tile_m=%d must be 0 (default 192), 128, 192, 256 or 257 (256, "
-             "ping-pong schedule)", tile_m);
+  SC_REQUIRE(tile_m == 0 || tile_m == 1 || tile_m == 128 || tile_m == 192 || tile_m == 256 ||
+                 tile_m == 257,
+             "sc_gemm_tn_bf16: tile_m=%d must be 0 (default 192), 1 (256, one wave per SIMD), "
+             "128, 192, 256 or 257 (256, ping-pong schedule)", tile_m);
   SC_REQUIRE(lda >= K && ldb >= K && ldc >= N && lda % 8 == 0 && ldb % 8 == 0 && ldc % 8 == 0,
              "sc_gemm_tn_bf16: leading dimensions must cover the rows in 16-byte pieces");
   SC_REQUIRE((uintptr_t)A % 16 == 0 && (uintptr_t)B % 16 == 0 && (uintptr_t)C % 16 == 0,
@@ -757,13 +921,22 @@ extern "C" int sc_gemm_tn_bf16(const void* A, int64_t lda, const void* B, int64_
   SC_REQUIRE((int64_t)M * lda * 2 < (1ll << 32) && (int64_t)N * ldb * 2 < (1ll << 32) &&
                  ((int64_t)M + 256) * ldc * 2 < (1ll << 32),
              "sc_gemm_tn_bf16: operands must be smaller than 4 GiB");
-  const int tm = tile_m == 257 ? 256 : tile_m ? tile_m : 192;
+  const int tm = (tile_m == 257 || tile_m == 1) ? 256 : tile_m ? tile_m : 192;
   const int ntn = N / kTN;
   const int64_t tiles = (int64_t)((M + tm - 1) / tm) * ntn;
   SC_REQUIRE(tiles < (1 << 30), "sc_gemm_tn_bf16: too many tiles");
+  static const int gm = [] {
+    const char* e = getenv("SC_TN_GM");
+    const int v = e ? atoi(e) : 8;
+    return v >= 1 ? v : 8;
+  }();
   TnArgs a{(const __bf16*)A, (const __bf16*)B, (__bf16*)C, M, N, K, ntn, (int)tiles,
-           (uint32_t)lda, (uint32_t)ldb, (uint32_t)ldc, (uint32_t)((int64_t)M * ldc * 2)};
+           (uint32_t)lda, (uint32_t)ldb, (uint32_t)ldc, (uint32_t)((int64_t)M * ldc * 2), gm};
   hipStream_t st = (hipStream_t)stream;
+  if (tile_m == 1) {
+    launch_tnw(a, st);
+    return launch_status("sc_gemm_tn_bf16");
+  }
   if (tile_m == 257) {
     launch_tnpp(a, st);
     return launch_status("sc_gemm_tn_bf16");

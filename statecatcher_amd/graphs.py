@@ -5,7 +5,8 @@ with the carried state, backward, clip + Adam.  On MI355X the forward + backward
 is ~90 kernel launches; the host issues them in ~2.8 ms against a ~5 ms GPU step
 (DESIGN.md §6 item 7), so the host is one halving of the GPU step away from being the bound.
 ``GraphedSegments`` captures ``SegmentTrainer.forward_backward`` of a FIXED list of
-device-resident segments once, one graph per position in the server batch, and replays them:
+device-resident segments once, one graph per position in the server batch (one shared memory
+pool), and replays them:
 
   * graph 0 starts the batch (no input state, train.py:460); graph i > 0 reads graph i - 1's
     output state in place, so replaying 0, 1, ..., n - 1 is the eager loop's state chain;
@@ -19,9 +20,10 @@ Same kernels in the same order as the eager step, so the losses and weights are 
 eager loop's (tests/test_gpu_graphs.py).  Restrictions, all checked: one process (no DDP: its
 bucketed all-reduce hooks are not captured), ``accumulation_steps == 1`` (every segment steps),
 HIP Adam (optim.hip_adam_eligible), no per-launch timing events during capture
-(ops.LAUNCH_EVENTS is None).  The segments' tensors are the graphs' inputs: overwrite them in
-place (``copy_``) to feed new data of the same shapes.  Periodic checkpoints
-(``SegmentTrainer.save_every_n_updates``) are the caller's: ``step`` replays and steps only.
+(ops.LAUNCH_EVENTS is None), no ``save_every_n_updates`` (periodic checkpoints are the
+caller's: ``step`` replays and steps only).  The segments' tensors are the graphs' inputs:
+overwrite them in place (``copy_``) to feed new data of the same shapes.  After ``step`` the
+parameters' ``.grad`` are None again, as after the eager loop's ``zero_grad``.
 """
 import gc
 from typing import List, Optional
@@ -43,6 +45,9 @@ class GraphedSegments:
                              "(optim.hip_adam_eligible)")
         if not segments or not all(s["feats"].is_cuda for s in segments):
             raise ValueError("GraphedSegments: segments must be device tensors")
+        if trainer.save_every_n_updates:
+            raise ValueError("GraphedSegments: periodic checkpoints (save_every_n_updates) are "
+                             "the caller's in replay mode; build the trainer without them")
         self.trainer = trainer
         self.segments = segments
         self.params = [p for g in trainer.optimizer.param_groups for p in g["params"]
@@ -88,7 +93,11 @@ class GraphedSegments:
             for p in self.params:
                 p.grad = None
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            # one memory pool for every position: replays run in capture order and what must
+            # outlive a replay (state, gradients, loss) stays referenced, so position i + 1's
+            # activations reuse position i's instead of holding one copy per position
+            pool = self.graphs[0].pool() if self.graphs else None
+            with torch.cuda.graph(g, pool=pool):
                 loss, state = self._run(i, state)
             self.graphs.append(g)
             self.losses.append(loss)
@@ -113,6 +122,8 @@ class GraphedSegments:
         for p, g in zip(self.params, self.grads[i]):
             p.grad = g
         self.trainer._clip_and_step()
+        for p in self.params:   # as the eager loop's zero_grad(set_to_none=True): no caller
+            p.grad = None       # backward may accumulate into graph-owned gradient memory
         self.trainer.global_step += 1
         self.pos = (i + 1) % len(self.graphs)
         return self.losses[i]

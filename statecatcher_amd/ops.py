@@ -1503,6 +1503,20 @@ def rnnt_joint_loss(enc_p, pred_p, W, bias, labels, frames_lengths, labels_lengt
 
 
 # ----------------------------------------------------------------------------- mLSTM ---------
+_F16_MAX = 65504.0
+
+
+def _mlstm_fp32_cell(q, k, v):
+    """Cell dtype for fp32 q / k / v: f16 (11-bit mantissa, the finer cell) when all three fit
+    its range, else bf16 (fp32's range): a magnitude above 65504 would become inf in f16 and NaN
+    downstream.  The range check reads one scalar back; inside a HIP-graph capture,
+    where it cannot, the range-safe bf16 cell is used."""
+    if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+        return torch.bfloat16
+    m = torch.stack([q.abs().amax(), k.abs().amax(), v.abs().amax()]).amax()
+    return torch.float16 if bool(m <= _F16_MAX) else torch.bfloat16
+
+
 class MLSTMFn(torch.autograd.Function):
     """mLSTM cell (mlstm.hip) over q, k [B,NH,T,DQ], v [B,NH,T,DV], gate pre-activations
     [B,NH,T]; returns h [B,NH,T,DV] and the final state (C [B,NH,DQ,DV], n [B,NH,DQ],
@@ -1510,7 +1524,8 @@ class MLSTMFn(torch.autograd.Function):
     Compute dtype bf16/f16; fp32 inputs are rounded to f16, the finer of the two compiled cells
     (11-bit mantissa; the f16 backward scales its gradients per chunk, so dh below f16's normal
     range is not lost) -- the reference's kernels run under autocast_kernel_dtype = float16
-    (model.py:227).  fp32 state."""
+    (model.py:227) -- unless a value exceeds f16's range, then to bf16 (_mlstm_fp32_cell).
+    fp32 state."""
 
     @staticmethod
     def forward(ctx, q, k, v, igate, fgate, c0, n0, m0, eps):
@@ -1518,7 +1533,7 @@ class MLSTMFn(torch.autograd.Function):
         ctx.set_materialize_grads(False)   # detached carried states: no zero-filled gradients
         B, NH, T, DQ = q.shape
         DV = v.shape[-1]
-        cdt = q.dtype if q.dtype in (torch.bfloat16, torch.float16) else torch.float16
+        cdt = q.dtype if q.dtype in (torch.bfloat16, torch.float16) else _mlstm_fp32_cell(q, k, v)
         lib = _lib.load()
         if not lib.sc_mlstm_supported(dtype_code(torch.empty(0, dtype=cdt)), DQ, DV):
             raise ValueError(f"mLSTM head dims (DQ={DQ}, DV={DV}) not compiled in")

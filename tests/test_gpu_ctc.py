@@ -208,6 +208,45 @@ def test_ctc_exact_lattice_bf16_logits_and_log_probs(dtype, is_logits):
     assert max(out["grad_rel"]) <= lim, out["grad_rel"]
 
 
+def test_ctc_sharp_long_targets_keep_log_space():
+    """Targets longer than the exact lattice holds (U = 300 > 255) with logits x 100: the
+    log-space lattice drifts past kDrift and flags the sequence, but ctc_x64_kernel does not run
+    for U > 255, so the gradient must read the LOG-SPACE offsets (one per re-centring), not the
+    exact lattice's per-step ones (it read unwritten offset entries).  A x 2 neighbour
+    in the same launch, and the same pair at U = 200 (which the exact lattice does redo)."""
+    out = {}
+    for U in (300, 200):
+        g = torch.Generator().manual_seed(U + 1)
+        B, V = 2, 40
+        T = 2 * U + 40
+        logits = torch.randn(B, T, V, generator=g)
+        logits[0] *= 100.0
+        logits[1] *= 2.0
+        tg = torch.randint(1, V, (B, U), generator=g)
+        tl = torch.tensor([U, U - 5])
+        tg[1, U - 5:] = 0
+        il = torch.tensor([T, T - 11])
+        x = logits.to(DEV).requires_grad_(True)
+        nll = sc().ctc_nll(x, tg.to(DEV), il, tl)
+        nll.sum().backward()
+        xr = logits.double().requires_grad_(True)
+        ref = torch.nn.functional.ctc_loss(xr.log_softmax(-1).transpose(0, 1), tg, il, tl,
+                                           reduction="none", zero_infinity=False)
+        ref.sum().backward()
+        got, r = nll.detach().cpu().numpy(), ref.detach().numpy()
+        gg, g64 = x.grad.cpu().numpy(), xr.grad.numpy()
+        assert np.isfinite(gg).all()
+        rel = [float(np.linalg.norm(gg[b] - g64[b]) / np.linalg.norm(g64[b])) for b in range(B)]
+        out[U] = (np.abs(got - r) / np.abs(r), rel)
+        print(f"U={U}: nll rel {out[U][0]}, grad rel {rel}")
+        np.testing.assert_allclose(got, r, rtol=1e-4)
+        assert rel[1] <= 1e-3
+    # U = 200: exact lattice, north_star's 1e-3; U = 300: the log-space lattice at x 100 (fp32
+    # rounding of values ~1e4 per step), documented as outside the exact lattice's range
+    assert out[200][1][0] <= 1e-3
+    assert out[300][1][0] <= 2e-2
+
+
 def test_ctc_bf16_logits_vs_oracle():
     g = torch.Generator().manual_seed(5)
     B, T, V = 3, 120, 64

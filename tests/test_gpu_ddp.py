@@ -137,8 +137,8 @@ def test_c3_model_ddp_over_rccl_equals_single_process(rccl_group, accumulation):
     assert all(torch.isfinite(torch.tensor(l_ref)))
 
 
-def _run_ranks(world, acc, tmp_path):
-    """tests/c3_rank.py as `world` fresh processes (none forked from this HIP-initialised one),
+def _run_ranks(world, acc, tmp_path, workload="c3", optim="adam"):
+    """tests/ddp_rank.py as `world` fresh processes (none forked from this HIP-initialised one),
     with a common deadline; returns each rank's saved results."""
     import socket
     import subprocess
@@ -147,16 +147,17 @@ def _run_ranks(world, acc, tmp_path):
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    outs = [str(tmp_path / f"w{world}_a{acc}_r{r}.pt") for r in range(world)]
+    outs = [str(tmp_path / f"{workload}_{optim}_w{world}_a{acc}_r{r}.pt") for r in range(world)]
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
-    procs = [subprocess.Popen([sys.executable, os.path.join(root, "tests", "c3_rank.py"), str(r),
-                               str(world), str(port), str(acc), outs[r]], cwd=root, env=env,
-                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    procs = [subprocess.Popen([sys.executable, os.path.join(root, "tests", "ddp_rank.py"), str(r),
+                               str(world), str(port), str(acc), outs[r], workload, optim],
+                              cwd=root, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                              text=True)
              for r in range(world)]
     logs = []
     try:
         for p in procs:
-            logs.append(p.communicate(timeout=100)[0])
+            logs.append(p.communicate(timeout=150)[0])
     finally:
         for p in procs:
             if p.poll() is None:
@@ -167,43 +168,108 @@ def _run_ranks(world, acc, tmp_path):
     return [torch.load(o, weights_only=True) for o in outs]
 
 
+def _rel(a, b):
+    return float((a.double() - b.double()).norm() / max(float(b.double().norm()), 1e-30))
+
+
+def _two_rank_case(workload, optim, acc, tmp_path):
+    """Two ranks (B = 2 each) against one process on the full B = 4 batch; returns the measured
+    errors after checking what holds exactly: ranks bitwise equal after every segment."""
+    single = _run_ranks(1, acc, tmp_path, workload, optim)[0]
+    r0, r1 = _run_ranks(2, acc, tmp_path, workload, optim)
+    assert r0["ranks_bitwise_equal"] == [True] * 4 and r1["ranks_bitwise_equal"] == [True] * 4
+    assert all(torch.equal(a, b) for a, b in zip(r0["init"], single["init"]))
+    lr = {"adam": 3e-4, "sgd": 1e-3}[optim]
+    e = {"loss": [abs((a + b) / 2 - s) / abs(s) for a, b, s in
+                  zip(r0["losses"], r1["losses"], single["losses"])],
+         "grad": [_rel(a, b) for a, b in zip(r0["grads"], single["grads"])],
+         # the parameters after the last step, and the update they made from the common start
+         "param": [_rel(a, b) for a, b in zip(r0["params"], single["params"])],
+         "update": [_rel(a - i, b - i) for a, b, i in
+                    zip(r0["params"], single["params"], single["init"])],
+         # the largest element-wise parameter difference, in units of lr x steps taken
+         "flip": max(float((a.double() - b.double()).abs().max()) for a, b in
+                     zip(r0["params"], single["params"])) / (lr * (4 // acc)),
+         "numel": [a.numel() for a in r0["params"]]}
+    assert len(e["grad"]) == len(r0["params"]) and all(map(lambda x: x == x, e["update"]))
+    print(f"{workload} {optim} acc={acc}: losses {r0['losses']} / {r1['losses']} vs "
+          f"{single['losses']}; loss rel {['%.1e' % x for x in e['loss']]}; first-update gradient "
+          f"rel max {max(e['grad']):.2e} ({len(e['grad'])} tensors); final param rel max "
+          f"{max(e['param']):.2e}; update rel max {max(e['update']):.2e} median "
+          f"{sorted(e['update'])[len(e['update']) // 2]:.2e}; largest element difference "
+          f"{e['flip']:.2f} lr-steps")
+    print("  per tensor (numel, param rel, update rel):",
+          [(n, f"{p:.1e}", f"{u:.1e}") for n, p, u in zip(e["numel"], e["param"], e["update"])])
+    return e
+
+
 @pytest.mark.parametrize("accumulation", [1, 2])
 def test_c3_two_ranks_on_one_gpu_equal_one_process_on_the_full_batch(accumulation, tmp_path):
-    """Config C3's sharding with the real HIP model at world size 2 (verdict r4, item 1): two rank
-    processes on cuda:0 over a gloo group, B = 2 each (tests/c3_rank.py), against one process
-    training the same B = 4 batch.  Rank 1 starts from DIFFERENT weights and has built its bf16
-    weight images from them before the DDP wrap, so DDP's start-up broadcast must reach the
-    version-keyed image cache.  Done when:
+    """Config C3's sharding with the real HIP model at world size 2 (verdict r4 item 1, r5 item 2):
+    two rank processes on cuda:0 over a gloo group, B = 2 each (tests/ddp_rank.py), against one
+    process training the same B = 4 batch with the reference's Adam.  Rank 1 starts from DIFFERENT
+    weights and has built its bf16 weight images from them before the DDP wrap, so DDP's start-up
+    broadcast must reach the version-keyed image cache.  Done when:
       * both ranks' parameters are bitwise equal after every segment;
       * until the first optimizer step (identical weights), the mean of the per-rank losses (each
         the mean of its sequences' nll / U) is the full-batch loss (CTC 'mean' over equal shards);
       * the gradients that step applies -- all-reduced over the ranks, with rank 1's shard
         computed from the broadcast weights -- are the full-batch gradients (relative Frobenius
-        per tensor, <= 1e-4; the two runs differ only in reduction order: GEMM row counts,
-        split-L slabs, the all-reduce).
-    After it the runs drift apart by Adam's sign normalisation of near-zero gradient elements
-    (each such element moves by +-lr whichever way reduction-order noise tips it), so later losses
-    and the final parameters are reported, not pinned.
+        per tensor, <= 1e-4; the runs differ only in reduction order: GEMM row counts, split-L
+        slabs, the all-reduce);
+      * every later segment's loss stays within north_star's 1e-3 of the full-batch run's;
+      * the final parameters part only the way Adam's sign normalisation allows: an element whose
+        gradient is reduction-order noise moves by about +-lr per step whichever way the noise
+        tips it, so no element may differ by more than 2 lr per step taken, and every weight
+        matrix (>= 64 K elements, where such elements are a small share of the norm) stays within
+        1e-3 relative Frobenius.  (Small tensors -- biases, LayerNorm vectors -- whose gradients
+        are mostly such noise can part by O(1) of their small updates: measured 0.27 on one;
+        test_c3_two_ranks_sgd_stay_equal_through_every_step pins the multi-step equality without
+        the sign normalisation.)
     Accumulation 1 and 2 (no_sync on the accumulating segments)."""
-    single = _run_ranks(1, accumulation, tmp_path)[0]
-    r0, r1 = _run_ranks(2, accumulation, tmp_path)
-    assert r0["ranks_bitwise_equal"] == [True] * 4 and r1["ranks_bitwise_equal"] == [True] * 4
-    loss_err = [abs((a + b) / 2 - s) / abs(s) for a, b, s in
-                zip(r0["losses"], r1["losses"], single["losses"])]
-    g_err = [float((a.double() - b.double()).norm() / max(float(b.double().norm()), 1e-30))
-             for a, b in zip(r0["grads"], single["grads"])]
-    p_err = [float((a.double() - b.double()).norm() / max(float(b.double().norm()), 1e-30))
-             for a, b in zip(r0["params"], single["params"])]
-    print(f"C3 2 ranks acc={accumulation}: losses {r0['losses']} / {r1['losses']} vs "
-          f"{single['losses']}; loss rel {['%.1e' % e for e in loss_err]}; first-update gradient "
-          f"rel max {max(g_err):.2e} ({len(g_err)} tensors); final param rel max {max(p_err):.2e}")
-    assert len(g_err) == len(r0["params"])
-    for e in loss_err[:accumulation]:   # identical weights: reduction order only
-        assert e <= 1e-5, loss_err
+    e = _two_rank_case("c3", "adam", accumulation, tmp_path)
+    for x in e["loss"][:accumulation]:   # identical weights: reduction order only
+        assert x <= 1e-5, e["loss"]
     # measured 3e-7 (acc 1) and 1.1e-5 (acc 2: the second segment's state was carried from the
     # first segment's split-batch scans, so two steps of reduction-order noise); north_star's
     # 1e-3 is the bar, 1e-4 leaves 10x of it for the reduction order alone
-    assert max(g_err) <= 1e-4, g_err
+    assert max(e["grad"]) <= 1e-4, e["grad"]
+    _adam_bounds(e)
+
+
+def _adam_bounds(e):
+    assert max(e["loss"]) <= 1e-3, e["loss"]
+    assert e["flip"] <= 2.0, e["flip"]
+    big = [p for p, n in zip(e["param"], e["numel"]) if n >= 65536]
+    assert big and max(big) <= 1e-3, big
+
+
+def test_c3_two_ranks_sgd_stay_equal_through_every_step(tmp_path):
+    """The multi-step leg without Adam's sign normalisation (verdict r5 item 2): with
+    clip_grad_norm_ + torch.optim.SGD the reduction-order noise of each step stays proportional
+    to itself, so DDP training must STAY equal to single-process training through all 4 steps:
+    every loss within 1e-4 and every tensor's total update (final - initial parameters) within
+    1e-4 relative."""
+    e = _two_rank_case("c3", "sgd", 1, tmp_path)
+    assert max(e["grad"]) <= 1e-4, e["grad"]
+    assert max(e["loss"]) <= 1e-4, e["loss"]
+    assert max(e["update"]) <= 1e-4, e["update"]
+
+
+@pytest.mark.parametrize("workload", ["c4", "c5"])
+def test_c4_c5_two_ranks_on_one_gpu_equal_one_process_on_the_full_batch(workload, tmp_path):
+    """The other north-star workloads at world size 2 on the HIP kernels (verdict r5 item 2):
+      * c4: the xLSTM encoder (2 blocks x 768, T = 1536, mLSTM on the float16 cell), whose
+        carried state is a dict of per-block tuples (/root/reference/model.py:17-18);
+      * c5: LucyRNN 6 x 512 + RNN-T with the fused joiner (U = 150), encoder and joiner both
+        DDP modules with their own buckets and one optimizer (model.py:73-145).
+    Same bar as C3: ranks bitwise equal every segment, the first update's all-reduced gradients
+    the full batch's to 1e-4, every loss to 1e-3, the final parameters within Adam's sign-flip
+    bound (2 lr per step per element, weight matrices 1e-3)."""
+    e = _two_rank_case(workload, "adam", 1, tmp_path)
+    assert e["loss"][0] <= 1e-5, e["loss"]
+    assert max(e["grad"]) <= 1e-4, e["grad"]
+    _adam_bounds(e)
 
 
 def test_rccl_allreduce_of_a_gradient_sized_buffer(rccl_group):

@@ -103,6 +103,28 @@ def test_mlstm_fp32_inputs_run_the_f16_cell():
     assert e32[0] < ebf[0] and e32[1] < ebf[1], (e32, ebf)
 
 
+def test_mlstm_fp32_inputs_beyond_f16_range_run_the_bf16_cell():
+    """fp32 q / k / v with a value above f16's 65504: the f16 cell would turn it into
+    inf and the outputs into NaN; the fp32 path then takes the bf16 cell (fp32's range) and is
+    bitwise the explicit bf16 call, finite, in the forward and the backward."""
+    z = load_golden("mlstm")
+    ins = [torch.as_tensor(z[f"c4/{k}"]) for k in ("q", "k", "v", "igate", "fgate")]
+    ins[2] = ins[2].clone()
+    ins[2][0, 0, 5, 3] = 1.0e5   # one v element past f16's range
+    outs = {}
+    for dt in (torch.float32, torch.bfloat16):
+        leaves = [t.to(DEV).to(dt if i < 3 else torch.float32).requires_grad_(True)
+                  for i, t in enumerate(ins)]
+        h = ops().mlstm_chunkwise(*leaves)
+        h.float().sum().backward()
+        outs[dt] = (h.detach().float(), [t.grad.float() for t in leaves])
+    assert torch.isfinite(outs[torch.float32][0]).all()
+    assert torch.equal(outs[torch.float32][0], outs[torch.bfloat16][0])
+    for a, b in zip(outs[torch.float32][1], outs[torch.bfloat16][1]):
+        assert torch.isfinite(a).all()
+        torch.testing.assert_close(a, b, rtol=1e-2, atol=1e-6)   # fp32 vs bf16 gradient casts only
+
+
 def test_mlstm_long_sequence_vs_oracle_and_state_carry():
     """T = 1536 (the C4 segment after padding to 64): h and final state vs the numpy step
     recurrence; two carried halves equal one pass."""

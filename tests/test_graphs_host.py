@@ -60,3 +60,15 @@ def test_step_before_capture_raises(monkeypatch):
     gs = graphs.GraphedSegments(_trainer(), [seg])
     with pytest.raises(RuntimeError, match="before capture"):
         gs.step()
+
+
+def test_refuses_periodic_checkpoints(monkeypatch, tmp_path):
+    """save_every_n_updates is skipped by replay (step only replays and steps): refused up front
+    instead of silently never saving."""
+    from statecatcher_amd import graphs
+    monkeypatch.setattr(graphs, "hip_adam_eligible", lambda opt: True)
+    seg = _segs()[0]
+    seg["feats"] = types.SimpleNamespace(is_cuda=True, device=torch.device("cpu"))
+    tr = _trainer(save_every_n_updates=10, model_dir=str(tmp_path))
+    with pytest.raises(ValueError, match="save_every_n_updates"):
+        graphs.GraphedSegments(tr, [seg])

@@ -36,6 +36,9 @@ def timeit(fn, n=10):
 SHAPES = [("gate fwd", 48000, 3584, 512), ("layer-0 fwd", 48000, 3584, 128),
           ("gate dgrad", 48000, 512, 3584), ("out-proj dgrad", 48000, 512, 1024),
           ("out-proj fwd", 48000, 1024, 512)]
+if "--shapes" in sys.argv:   # e.g. --shapes 0,2: a subset of SHAPES by index
+    SHAPES = [SHAPES[int(i)] for i in sys.argv[sys.argv.index("--shapes") + 1].split(",")]
+NOLIB = "--nolib" in sys.argv
 for name, M, N, K in SHAPES:
     R = 3
     As = [torch.randn(M, K, device=dev).to(torch.bfloat16) for _ in range(R)]
@@ -44,7 +47,8 @@ for name, M, N, K in SHAPES:
     arms = {f"tn{tm}": (lambda tm: lambda i: ops.gemm_tn(As[i % R], Bs[i % R], tm))(tm) for tm in TMS}
     arms["lib"] = lambda i: torch.matmul(As[i % R], Bs[i % R].t())
     Bts = [b.t().contiguous() for b in Bs]
-    arms["libNN"] = lambda i: torch.matmul(As[i % R], Bts[i % R])
+    if not NOLIB:
+        arms["libNN"] = lambda i: torch.matmul(As[i % R], Bts[i % R])
     for f in arms.values():   # warm-up
         for i in range(3):
             f(i)
