@@ -471,9 +471,8 @@ def main():
     torch.cuda.synchronize()
     graphed = None
     if args.graph == "on":
-        if world > 1:
-            sys.exit("bench.py: --graph on is single-process (DDP's all-reduce hooks are not "
-                     "captured)")
+        # world > 1: the graphs hold each rank's forward + backward, the gradients are
+        # all-reduced after every replay (graphs.GraphedSegments)
         from statecatcher_amd.graphs import GraphedSegments
         graphed = GraphedSegments(trainer, segs).capture()
 

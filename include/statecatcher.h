@@ -158,7 +158,9 @@ int sc_lucy_scan_bwd(const void* gates, int gates_dtype, const float* gate_bias,
  * Backward of sc_lucy_scan_fwd_ln's fold (16-bit, D = 512 or 1024, 16-byte aligned gates / dout /
  * dgates): the gates are rebuilt from ln_r, gate_bias and the forward's ln_stat; dgates =
  * dL/du = rstd dL/dgate (the input and weight gradients of u = h W''^T consume it); dbias keeps
- * dL/dgate (the gradient of b').
+ * dL/dgate (the gradient of b').  ln_r = NULL: the gates are sc_gemm_tn_ln_bf16's output, which
+ * already holds rstd (u - mean r); the scan adds gate_bias (= b') alone, ln_stat is that GEMM's
+ * stat, and dgates / dbias are as above.
  */
 int sc_lucy_scan_bwd_ln(const void* gates, int gates_dtype, const float* gate_bias,
                         const float* ckpt, const void* dout, const float* ds_last, void* dgates,
@@ -503,6 +505,22 @@ int sc_gemm_wgrad_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, f
  */
 int sc_gemm_tn_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc,
                     int M, int N, int K, int tile_m, void* stream);
+
+/*
+ * The gate projection of layers 1.. with the inter-layer LayerNorm folded in
+ * (lucyrnn_triton.py:96-97 + :20-25: LinearSafe(LayerNorm(h))): C [M][ldc] bf16 =
+ *   rstd (h W''^T - mean r) = LN(h) W^T - W beta      (the scan adds b' = b + W beta)
+ * for H = the previous layer's RAW output [M][ldh] bf16 (K = D, the LayerNorm width), Wpp = the
+ * W'' image [N][ldw] (sc_weight_images with a LayerNorm fold job, step-blocked rows), r [N] =
+ * its row sums in the image's row order (sc_ln_fold_prep's rowsum, permuted like the rows).  Each
+ * row's mean and rstd = 1 / sqrt(biased variance + eps) come from the rows as they stream
+ * through the GEMM; stat [M] (float pairs (rstd, mean)) receives them for the backward
+ * (sc_lucy_scan_bwd_ln with ln_r = NULL, sc_ln_fold_bwd).  K % 64 == 0, N % 256 == 0, 16-byte
+ * aligned operands.  Replaces sc_layernorm_fwd + the projection GEMM.
+ */
+int sc_gemm_tn_ln_bf16(const void* H, int64_t ldh, const void* Wpp, int64_t ldw, void* C,
+                       int64_t ldc, int M, int N, int K, const float* r, void* stat, float eps,
+                       void* stream);
 
 /* ---------------------------------------------------------------- optimizer step -------- */
 

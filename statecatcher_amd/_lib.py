@@ -18,13 +18,15 @@ _DTYPE = {torch.float32: SC_F32, torch.bfloat16: SC_BF16, torch.float16: SC_F16}
 
 _c = ctypes
 _i32, _i64, _vp, _fp = _c.c_int, _c.c_int64, _c.c_void_p, _c.c_void_p
-ABI_VERSION = 13  # include/statecatcher.h; bumped on any signature change
+ABI_VERSION = 14  # include/statecatcher.h; bumped on any signature change
 
 _SIGS = {
     "sc_abi_version": (_i32, []),
     "sc_gemm_wgrad_splits": (_i32, [_i32, _i32, _i32]),
     "sc_gemm_wgrad_bf16": (_i32, [_vp, _i64, _vp, _i64, _fp, _i32, _i32, _i32, _i32, _vp]),
     "sc_gemm_tn_bf16": (_i32, [_vp, _i64, _vp, _i64, _vp, _i64, _i32, _i32, _i32, _i32, _vp]),
+    "sc_gemm_tn_ln_bf16": (_i32, [_vp, _i64, _vp, _i64, _vp, _i64, _i32, _i32, _i32, _fp, _vp,
+                                 _c.c_float, _vp]),
     "sc_last_error": (_c.c_char_p, []),
     "sc_lucy_scan_chunk": (_i32, []),
     "sc_lucy_scan_ckpt_numel": (_i64, [_i32, _i32, _i32]),

@@ -28,5 +28,5 @@ int launch_status(const char* what) {
 
 }  // namespace sc
 
-extern "C" int sc_abi_version(void) { return 13; }
+extern "C" int sc_abi_version(void) { return 14; }
 extern "C" const char* sc_last_error(void) { return sc::g_err; }

@@ -641,7 +641,11 @@ lucy_scan_fwd_kernel(ScanFwdArgs a) {
 // WST: the 7 gate gradients of each step are written back into the wave's LDS slot over the raw
 // gates they were computed from, then stored as whole 16-byte pieces (3.5 wave-instructions per
 // super-chunk instead of 28 two-byte stores).  Needs NBUF = 2 and 16-byte aligned dgates.
-template <int DT, int NW, int LC, int PW, int NBUF, bool WST, bool LN = false>
+// LN: the folded inter-layer LayerNorm.  1 (sc_lucy_scan_bwd_ln with ln_r): the gates are
+// u = h W''^T, rebuilt as rstd (u - mean r) + b' on load; 2 (ln_r NULL): the projection GEMM has
+// already applied the fold (sc_gemm_tn_ln_bf16 wrote rstd (u - mean r)), the gates take b' alone.
+// Both store d/du = rstd dL/dgate.
+template <int DT, int NW, int LC, int PW, int NBUF, bool WST, int LN = 0>
 __global__ void __launch_bounds__(NW * 64)
 lucy_scan_bwd_kernel(ScanBwdArgs a) {
   static_assert(NW * LC == kChunk, "super-chunk must be 64 steps");
@@ -691,7 +695,8 @@ lucy_scan_bwd_kernel(ScanBwdArgs a) {
   // (the fold's gate rebuild has no registers to spare)
   __shared__ float2 fbS[LN ? 7 : 1][64];
   if constexpr (LN) {
-    if (w < 7) fbS[LN ? w : 0][lane] = make_float2(a.bias[w * a.D + dc], a.ln_r[w * a.D + dc]);
+    if (w < 7)
+      fbS[LN ? w : 0][lane] = make_float2(a.bias[w * a.D + dc], LN == 1 ? a.ln_r[w * a.D + dc] : 0.0f);
   } else {
 #pragma unroll
     for (int g = 0; g < 7; ++g) gb[g] = a.bias ? a.bias[g * a.D + dc] : 0.0f;
@@ -829,9 +834,12 @@ lucy_scan_bwd_kernel(ScanBwdArgs a) {
       for (int g = 0; g < 7; ++g) {
         const f2 raw = f2{E::ld(L::get(slot, (j * 7 + g) * 64 + lane)),
                           E::ld(L::get(slot, ((j + 1) * 7 + g) * 64 + lane))};
-        if constexpr (LN) {   // rstd (u - mean r) + b', as the forward rebuilt it
+        if constexpr (LN == 1) {   // rstd (u - mean r) + b', as the forward rebuilt it
           const float2 fb = fbS[LN ? g : 0][lane];
           g7[g] = raw * lrs + (lrm * f2{fb.y, fb.y} + f2{fb.x, fb.x});
+        } else if constexpr (LN == 2) {   // (the GEMM applied rstd and mean) + b'
+          const float fbx = fbS[LN ? g : 0][lane].x;
+          g7[g] = raw + f2{fbx, fbx};
         } else {
           g7[g] = raw + gb[LN ? 0 : g];
         }
@@ -1101,7 +1109,7 @@ static void launch_fwd(const ScanFwdArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(kern, grid, dim3(kNW * 64), lds, st, a);
 }
 
-template <int DT, int PW, bool WST, bool LN = false>
+template <int DT, int PW, bool WST, int LN = 0>
 static void launch_bwd(const ScanBwdArgs& a, hipStream_t st) {
   using T = typename Elem<DT>::T;
   // two slots per wave fit only for 2-byte LDS elements (160 KiB per CU)
@@ -1164,8 +1172,9 @@ template <int DT>
 static void dispatch_bwd(const ScanBwdArgs& a, hipStream_t st) {
   constexpr int es = sizeof(typename Elem<DT>::T);
   if constexpr (es == 2) {
-    if (a.ln_r) {   // (scan_bwd checked the layout)
-      launch_bwd<DT, 16, true, true>(a, st);
+    if (a.ln_stat) {   // (scan_bwd checked the layout)
+      if (a.ln_r) launch_bwd<DT, 16, true, 1>(a, st);
+      else launch_bwd<DT, 16, true, 2>(a, st);
       return;
     }
   }
@@ -1321,7 +1330,7 @@ extern "C" int sc_lucy_scan_bwd_ln(const void* gates, int gates_dtype, const flo
                                    int64_t stride_dg_cd, int64_t stride_dg_cb, const float* ln_r,
                                    const float* ln_stat, void* stream) {
   clear_error();
-  SC_REQUIRE(ln_r && ln_stat && gate_bias, "sc_lucy_scan_bwd_ln: null ln_r / ln_stat / gate_bias");
+  SC_REQUIRE(ln_stat && gate_bias, "sc_lucy_scan_bwd_ln: null ln_stat / gate_bias");
   SC_REQUIRE(gates_dtype != SC_F32, "sc_lucy_scan_bwd_ln: the LayerNorm fold needs 16-bit gates");
   SC_REQUIRE((D == 512 || D == 1024) && wide_pieces(gates, 2, D, {stride_g_bt, stride_g_td, stride_g_cd, stride_g_cb}) &&
                  wide_pieces(dout, 2, D, {stride_d_bt, stride_d_bd}) &&

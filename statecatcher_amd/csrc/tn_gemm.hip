@@ -798,6 +798,11 @@ __global__ void __launch_bounds__(256, 1) tnw_kernel(TnArgs a) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
   auto mfmas = [&](const Frag& fx, const Frag& fw) __attribute__((always_inline)) {
+    if (SC_TN_ABL & 1) {   // (ablation: operands kept live, no MFMA)
+#pragma unroll
+      for (int f = 0; f < 8; ++f) asm volatile("" ::"v"(fx.v[f]), "v"(fw.v[f]));
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -825,12 +830,19 @@ __global__ void __launch_bounds__(256, 1) tnw_kernel(TnArgs a) {
     if (kt + 1 < nkt) {
       dma_wait();      // this wave's share of K-tile kt + 1 (nothing younger is in flight)
       lds_barrier();   // ... everyone's, and every read of slot kt % 2 is done
-      if (kt + 2 < nkt) dma(kt + 2);
+      if (kt + 2 < nkt && !(SC_TN_ABL & 2)) dma(kt + 2);
       read(kt + 1, 0, X, Xw);
     }
     mfmas(Y, Yw);
   }
 
+  if (SC_TN_ABL & 4) {   // (ablation: accumulators kept live, no stores)
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) asm volatile("" ::"a"(acc[i][j]));
+    return;
+  }
   // ---- epilogue: per x fragment, 32 consecutive bf16 columns per lane = four 16-byte stores ----
   const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(a.C, 0, a.cbytes, 0x00020000);
   const uint32_t col = (uint32_t)(n0 + wn * 128 + l4 * 32);
@@ -860,6 +872,254 @@ int launch_tnw(const TnArgs& a, hipStream_t st) {
   const int npan = (a.M + 255) / 256;
   const int grid = 8 * ((npan + 7) / 8) * a.ntn;
   hipLaunchKernelGGL(tnw_kernel, dim3(grid), dim3(256), lds, st, a);
+  return 0;
+}
+
+// ------------------------------------------------------------------------------------------
+// tnw with a deeper DMA ring (tile_m = 2): tnw32_kernel<NS>.
+// The same 4 waves x 128 x 128 outputs, but the K loop runs in 32-deep stages (one k-step, 64
+// MFMAs per wave) held in NS slots of 32 KiB (A and W images of [256 rows][64 B]), NS - 1 of them
+// in flight: with NS = 5 the whole 160 KiB of LDS, 128 KiB of operands on their way per CU and
+// 4 k-steps (4,096 MFMA cycles) for each DMA to land, against one K-tile (64 KiB, 2,048 cycles)
+// in tnw.  Iteration s: retire stage s (counted vmcnt: the 8 (NS - 2) younger pieces stay in
+// flight) + barrier; DMA stage s + NS - 1 into the slot stage s - 1 vacated; read stage s's
+// fragments while the MFMAs of stage s - 1 run.  64-byte image rows: the 16-byte chunk c of row
+// r sits at c ^ f(r), f(r) = (2 (r >> 3) ^ (r >> 4)) & 3 -- conflict-free for both fragment
+// patterns under ds_read_b128's lane groups (searched by script).
+// LN = true: the inter-layer LayerNorm folded in (tnw32_kernel<4, true>, sc_gemm_tn_ln_bf16):
+// A = the previous layer's RAW bf16 output h, B = W'' (ln_fold.hip), and
+//   C = rstd (h W''^T - mean r) = LN(h) W^T - W beta   (b' = b + W beta goes into the scan's bias)
+// Each thread owns one tile row: while its 32-column stages pass through LDS it reads the row's
+// 4 chunks beside the fragment reads and accumulates shifted sums (shift = the row's first
+// element) in VALU slots between the MFMAs; after the K loop the (rstd, mean) of the 256 rows go
+// to LDS (and, from the first column tile, to stat[] for the backward) and the epilogue applies
+// them with r (DMA'd into LDS in the prologue).  Every column tile of a row panel computes the
+// same statistics from the same data in the same order: bitwise equal across tiles.
+struct TnLn {
+  const float* r;   // [N] row sums of the W'' image, image row (= output column) order
+  float2* stat;     // [M] out: (rstd, mean) per row (written by the tiles of column 0)
+  float eps;
+};
+
+namespace tnw32 {
+constexpr int kRow = 64;                 // image row pitch (bytes): 32 bf16
+constexpr int kHalf = 256 * kRow;        // one operand image (16 KiB)
+constexpr int kSlot = 2 * kHalf;         // A + W (32 KiB)
+__device__ __forceinline__ int f64(int r) { return ((2 * (r >> 3)) ^ (r >> 4)) & 3; }
+}  // namespace tnw32
+
+template <int NS, bool LN>
+__global__ void __launch_bounds__(256, 1) tnw32_kernel(TnArgs a, TnLn ln) {
+  using namespace tnw32;
+  using tnw::Frag;
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const int lane = threadIdx.x & 63;
+  const int w = uniform(threadIdx.x >> 6);
+  const int wm = w >> 1, wn = w & 1;
+  const int l15 = lane & 15, l4 = lane >> 4;
+  const int bid = blockIdx.x;
+  const int npan = (a.M + 255) / 256;
+  const int xcd = bid % 8, k = bid / 8;
+  const int pq = npan / 8, pr = npan % 8;
+  const int np = pq + (xcd < pr), p0 = xcd * pq + min(xcd, pr);
+  if (k >= np * a.ntn) return;
+  const int grp = k / (a.gm * a.ntn), first = grp * a.gm;
+  const int gsz = min(a.gm, np - first), within = k - grp * a.gm * a.ntn;
+  const int m0 = (p0 + first + within % gsz) * 256, n0 = (within / gsz) * 256;
+  const int nst = a.K / 32;
+  const uint32_t lds0 = lds_addr(lds);
+
+  // ---- DMA: wave w stages image rows 64 w .. 64 w + 63 of both operands (4 + 4 pieces of 16 rows) ----
+  uint32_t voA[4], voB[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int r = 64 * w + 16 * q + (lane >> 2);
+    const uint32_t ch = 8u * (uint32_t)((lane & 3) ^ f64(r));
+    voA[q] = ((uint32_t)min(m0 + r, a.M - 1) * a.lda + ch) * 2u;
+    voB[q] = ((uint32_t)(n0 + r) * a.ldb + ch) * 2u;
+  }
+  auto dma = [&](int st) __attribute__((always_inline)) {
+    const uint32_t sb = lds0 + (uint32_t)((st % NS) * kSlot) + (uint32_t)(w * 4 * 1024);
+    const __bf16* pa = a.A + st * 32;
+    const __bf16* pb = a.B + st * 32;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) dma_to_lds_s<16>(pa, voA[q], sb + q * 1024);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) dma_to_lds_s<16>(pb, voB[q], sb + kHalf + q * 1024);
+  };
+  uint32_t offX[8], offW[8];
+#pragma unroll
+  for (int f = 0; f < 8; ++f) {
+    const int rx = wm * 128 + f * 16 + l15;
+    offX[f] = (uint32_t)(rx * kRow + 16 * (l4 ^ f64(rx)));
+    const int rw = wn * 128 + (l15 >> 2) * 32 + f * 4 + (l15 & 3);
+    offW[f] = (uint32_t)(kHalf + rw * kRow + 16 * (l4 ^ f64(rw)));
+  }
+  auto read = [&](int st, Frag& fx, Frag& fw) __attribute__((always_inline)) {
+    const uint32_t sb = lds0 + (uint32_t)((st % NS) * kSlot);
+#pragma unroll
+    for (int f = 0; f < 8; ++f) fw.v[f] = lds_read16(sb + offW[f]);
+#pragma unroll
+    for (int f = 0; f < 8; ++f) fx.v[f] = lds_read16(sb + offX[f]);
+  };
+  f4v acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
+  auto mfmas = [&](const Frag& fx, const Frag& fw) __attribute__((always_inline)) {
+    if (SC_TN_ABL & 1) {
+#pragma unroll
+      for (int f = 0; f < 8; ++f) asm volatile("" ::"v"(fx.v[f]), "v"(fw.v[f]));
+      return;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+            __builtin_bit_cast(b8v, fw.v[j]), __builtin_bit_cast(b8v, fx.v[i]), acc[i][j], 0, 0, 0);
+  };
+  // retire stage st: the pieces of the stages issued after it (up to NS - 2) may stay in flight
+  auto retire = [&](int st) __attribute__((always_inline)) {
+    const int younger = min(NS - 2, nst - 1 - st);
+    if (younger >= NS - 2) dma_wait_younger<8 * (NS - 2)>();
+    else if (younger == 2) dma_wait_younger<16>();
+    else if (younger == 1) dma_wait_younger<8>();
+    else dma_wait();
+  };
+  // ---- LN: r of the tile's 256 columns into LDS (older than every stage: the first wait
+  // retires it), the row statistics of thread t's tile row ----
+  constexpr uint32_t kR = (uint32_t)NS * kSlot, kStat = kR + 1024;
+  const int t = threadIdx.x;
+  float lsh = 0.f, ls1a = 0.f, ls1b = 0.f, ls2a = 0.f, ls2b = 0.f;
+  const uint32_t statoff = (uint32_t)(t * kRow + 16 * f64(t));   // chunk c at statoff ^ 16 c
+  if constexpr (LN) {
+    if (w == 0) dma_to_lds_s<16>(ln.r + n0, (uint32_t)lane * 16u, lds0 + kR);
+  }
+  auto stat_read = [&](int st, i4v (&rv)[4]) __attribute__((always_inline)) {
+    if constexpr (LN) {
+      const uint32_t sb = lds0 + (uint32_t)((st % NS) * kSlot);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) rv[c] = lds_read16(sb + (statoff ^ (16u * c)));
+    }
+  };
+  auto stat_acc = [&](int st, const i4v (&rv)[4]) __attribute__((always_inline)) {
+    if constexpr (LN) {
+      if (st == 0) lsh = __uint_as_float((uint32_t)rv[0][0] << 16);
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          const uint32_t u = (uint32_t)rv[c][d];
+          const float x0 = __uint_as_float(u << 16) - lsh, x1 = __uint_as_float(u & 0xffff0000u) - lsh;
+          ls1a += x0;
+          ls1b += x1;
+          ls2a = fmaf(x0, x0, ls2a);
+          ls2b = fmaf(x1, x1, ls2b);
+        }
+    }
+  };
+  i4v sv[4];
+  // ---- prologue: stages 0 .. NS - 1 in flight (every slot), stage 0 retired and read ----
+#pragma unroll
+  for (int st = 0; st < NS; ++st)
+    if (st < nst) dma(st);
+  if (nst >= NS) dma_wait_younger<8 * (NS - 1)>();
+  else retire(0);
+  lds_barrier();
+  Frag X, Xw, Y, Yw;
+  read(0, X, Xw);
+  stat_read(0, sv);
+  stat_acc(0, sv);
+  // stage s is read after the barrier that retires it and multiplied one barrier later; at that
+  // barrier every read of stage s - 1 is done, so its slot takes stage s - 1 + NS
+  for (int st = 0; st < nst; st += 2) {   // nst = K / 32 is even
+    lds_read_wait();
+    retire(st + 1);
+    lds_barrier();
+    if (st + NS < nst && !(SC_TN_ABL & 2)) dma(st + NS);
+    read(st + 1, Y, Yw);
+    stat_read(st + 1, sv);
+    mfmas(X, Xw);
+    stat_acc(st + 1, sv);
+    lds_read_wait();
+    if (st + 2 < nst) {
+      retire(st + 2);
+      lds_barrier();
+      if (st + 1 + NS < nst && !(SC_TN_ABL & 2)) dma(st + 1 + NS);
+      read(st + 2, X, Xw);
+      stat_read(st + 2, sv);
+    }
+    mfmas(Y, Yw);
+    if (st + 2 < nst) stat_acc(st + 2, sv);
+  }
+  if (SC_TN_ABL & 4) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) asm volatile("" ::"a"(acc[i][j]));
+    return;
+  }
+  const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(a.C, 0, a.cbytes, 0x00020000);
+  const uint32_t col = (uint32_t)(n0 + wn * 128 + l4 * 32);
+  float rr[32];   // (LN) r of the lane's 32 columns
+  if constexpr (LN) {
+    // row statistics (biased variance, nn.LayerNorm) -> LDS and, from column tile 0, stat[]
+    const float inv = 1.0f / (float)a.K;
+    const float m1 = (ls1a + ls1b) * inv;
+    const float var = fmaxf((ls2a + ls2b) * inv - m1 * m1, 0.0f);
+    const float2 sr = make_float2(rsq(var + ln.eps), lsh + m1);
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    *(__attribute__((address_space(3))) f2*)(size_t)(lds0 + kStat + (uint32_t)t * 8u) = f2{sr.x, sr.y};
+    if (n0 == 0 && m0 + t < a.M) ln.stat[m0 + t] = sr;
+    lds_barrier();
+    const uint32_t rb = lds0 + kR + (uint32_t)(wn * 128 + l4 * 32) * 4u;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const i4v v = lds_read16(rb + 16u * q);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) rr[4 * q + e] = __int_as_float(v[e]);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint32_t row = (uint32_t)(m0 + wm * 128 + i * 16 + l15);
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    f2 sr = {1.f, 0.f};
+    if constexpr (LN)
+      sr = *(const __attribute__((address_space(3))) f2*)(size_t)(
+          lds0 + kStat + (uint32_t)(wm * 128 + i * 16 + l15) * 8u);
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) {
+      i4v v;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const int j = 2 * s4 + (d >> 1), e = 2 * (d & 1);
+        float c0 = acc[i][j][e], c1 = acc[i][j][e + 1];
+        if constexpr (LN) {   // rstd (u - mean r), column j*4 + e of the lane's 32
+          c0 = (c0 - sr.y * rr[4 * j + e]) * sr.x;
+          c1 = (c1 - sr.y * rr[4 * j + e + 1]) * sr.x;
+        }
+        const b2v p = {(__bf16)c0, (__bf16)c1};
+        v[d] = __builtin_bit_cast(int, p);
+      }
+      __builtin_amdgcn_raw_buffer_store_b128(v, crs, (row * a.ldc + col + 8u * s4) * 2u, 0, 0);
+    }
+  }
+}
+
+template <int NS, bool LN>
+int launch_tnw32(const TnArgs& a, const TnLn& ln, hipStream_t st) {
+  constexpr size_t lds = (size_t)NS * tnw32::kSlot + (LN ? 3072 : 0);
+  static_assert(!LN || lds <= 160 * 1024, "LN needs a spare 3 KiB of LDS");
+  static const bool ok = hipFuncSetAttribute((const void*)tnw32_kernel<NS, LN>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             (int)lds) == hipSuccess;
+  (void)ok;
+  const int npan = (a.M + 255) / 256;
+  const int grid = 8 * ((npan + 7) / 8) * a.ntn;
+  hipLaunchKernelGGL((tnw32_kernel<NS, LN>), dim3(grid), dim3(256), lds, st, a, ln);
   return 0;
 }
 
@@ -910,10 +1170,11 @@ extern "C" int sc_gemm_tn_bf16(const void* A, int64_t lda, const void* B, int64_
   SC_REQUIRE(M > 0 && N > 0 && K > 0, "sc_gemm_tn_bf16: empty shape M=%d N=%d K=%d", M, N, K);
   SC_REQUIRE(K % kBK == 0, "sc_gemm_tn_bf16: K=%d must be a multiple of 64 (zero-pad it)", K);
   SC_REQUIRE(N % kTN == 0, "sc_gemm_tn_bf16: N=%d must be a multiple of 256", N);
-  SC_REQUIRE(tile_m == 0 || tile_m == 1 || tile_m == 128 || tile_m == 192 || tile_m == 256 ||
-                 tile_m == 257,
+  SC_REQUIRE(tile_m == 0 || tile_m == 1 || tile_m == 2 || tile_m == 3 || tile_m == 128 ||
+                 tile_m == 192 || tile_m == 256 || tile_m == 257,
              "sc_gemm_tn_bf16: tile_m=%d must be 0 (default 192), 1 (256, one wave per SIMD), "
-             "128, 192, 256 or 257 (256, ping-pong schedule)", tile_m);
+             "2 / 3 (the same, 32-deep stages in a 5 / 4-slot ring), 128, 192, 256 or 257 (256, "
+             "ping-pong schedule)", tile_m);
   SC_REQUIRE(lda >= K && ldb >= K && ldc >= N && lda % 8 == 0 && ldb % 8 == 0 && ldc % 8 == 0,
              "sc_gemm_tn_bf16: leading dimensions must cover the rows in 16-byte pieces");
   SC_REQUIRE((uintptr_t)A % 16 == 0 && (uintptr_t)B % 16 == 0 && (uintptr_t)C % 16 == 0,
@@ -921,7 +1182,7 @@ extern "C" int sc_gemm_tn_bf16(const void* A, int64_t lda, const void* B, int64_
   SC_REQUIRE((int64_t)M * lda * 2 < (1ll << 32) && (int64_t)N * ldb * 2 < (1ll << 32) &&
                  ((int64_t)M + 256) * ldc * 2 < (1ll << 32),
              "sc_gemm_tn_bf16: operands must be smaller than 4 GiB");
-  const int tm = (tile_m == 257 || tile_m == 1) ? 256 : tile_m ? tile_m : 192;
+  const int tm = (tile_m == 257 || (tile_m >= 1 && tile_m <= 3)) ? 256 : tile_m ? tile_m : 192;
   const int ntn = N / kTN;
   const int64_t tiles = (int64_t)((M + tm - 1) / tm) * ntn;
   SC_REQUIRE(tiles < (1 << 30), "sc_gemm_tn_bf16: too many tiles");
@@ -935,6 +1196,11 @@ extern "C" int sc_gemm_tn_bf16(const void* A, int64_t lda, const void* B, int64_
   hipStream_t st = (hipStream_t)stream;
   if (tile_m == 1) {
     launch_tnw(a, st);
+    return launch_status("sc_gemm_tn_bf16");
+  }
+  if (tile_m == 2 || tile_m == 3) {
+    if (tile_m == 2) launch_tnw32<5, false>(a, TnLn{}, st);
+    else launch_tnw32<4, false>(a, TnLn{}, st);
     return launch_status("sc_gemm_tn_bf16");
   }
   if (tile_m == 257) {
@@ -961,4 +1227,27 @@ extern "C" int sc_gemm_tn_bf16(const void* A, int64_t lda, const void* B, int64_
     else launch_tn<6, 12>(a, st);
   }
   return launch_status("sc_gemm_tn_bf16");
+}
+
+extern "C" int sc_gemm_tn_ln_bf16(const void* H, int64_t ldh, const void* Wpp, int64_t ldw, void* C,
+                                  int64_t ldc, int M, int N, int K, const float* r, void* stat,
+                                  float eps, void* stream) {
+  clear_error();
+  SC_REQUIRE(H && Wpp && C && r && stat, "sc_gemm_tn_ln_bf16: null pointer");
+  SC_REQUIRE(M > 0 && N > 0 && K > 0 && K % 64 == 0 && N % 256 == 0,
+             "sc_gemm_tn_ln_bf16: shape M=%d N=%d K=%d (K %% 64, N %% 256)", M, N, K);
+  SC_REQUIRE(ldh >= K && ldw >= K && ldc >= N && ldh % 8 == 0 && ldw % 8 == 0 && ldc % 8 == 0,
+             "sc_gemm_tn_ln_bf16: leading dimensions must cover the rows in 16-byte pieces");
+  SC_REQUIRE(((uintptr_t)H | (uintptr_t)Wpp | (uintptr_t)C | (uintptr_t)r) % 16 == 0 &&
+                 (uintptr_t)stat % 8 == 0,
+             "sc_gemm_tn_ln_bf16: misaligned operand");
+  SC_REQUIRE((int64_t)M * ldh * 2 < (1ll << 32) && (int64_t)N * ldw * 2 < (1ll << 32) &&
+                 ((int64_t)M + 256) * ldc * 2 < (1ll << 32),
+             "sc_gemm_tn_ln_bf16: operands must be smaller than 4 GiB");
+  const int ntn = N / 256;
+  const int64_t tiles = (int64_t)((M + 255) / 256) * ntn;
+  TnArgs a{(const __bf16*)H, (const __bf16*)Wpp, (__bf16*)C, M, N, K, ntn, (int)tiles,
+           (uint32_t)ldh, (uint32_t)ldw, (uint32_t)ldc, (uint32_t)((int64_t)M * ldc * 2), 8};
+  launch_tnw32<4, true>(a, TnLn{r, (float2*)stat, eps}, (hipStream_t)stream);
+  return launch_status("sc_gemm_tn_ln_bf16");
 }

@@ -17,8 +17,18 @@ pool), and replays them:
     eagerly, as in ``SegmentTrainer.train_segment``.
 
 Same kernels in the same order as the eager step, so the losses and weights are bitwise the
-eager loop's (tests/test_gpu_graphs.py).  Restrictions, all checked: one process (no DDP: its
-bucketed all-reduce hooks are not captured), ``accumulation_steps == 1`` (every segment steps),
+eager loop's (tests/test_gpu_graphs.py).
+
+Under DDP (world > 1) the graphs hold the bare modules' forward + backward (this rank's
+gradients; DDP's bucket hooks are host callbacks and are not captured), and ``step`` all-reduces
+the gradients after the replay -- one flat fp32 all-reduce of every gradient, divided by the world
+size as DDP's default hook does -- then clips and steps.  The all-reduce then no longer overlaps
+the backward (DDP's buckets do); in exchange the host issues ~0.2 ms per segment instead of
+~2.8 ms.  The backend is the process group's (RCCL on the GPUs; gloo in the one-GPU two-rank
+test, tests/test_gpu_ddp.py), and DDP's own start-up broadcast has already made the ranks'
+weights equal.
+
+Restrictions, all checked: ``accumulation_steps == 1`` (every segment steps),
 HIP Adam (optim.hip_adam_eligible), no per-launch timing events during capture
 (ops.LAUNCH_EVENTS is None), no ``save_every_n_updates`` (periodic checkpoints are the
 caller's: ``step`` replays and steps only).  The segments' tensors are the graphs' inputs:
@@ -36,8 +46,6 @@ from .optim import hip_adam_eligible
 
 class GraphedSegments:
     def __init__(self, trainer, segments: List[dict]):
-        if trainer.ddp:
-            raise ValueError("GraphedSegments: DDP is not captured (one process only)")
         if trainer.accumulation_steps != 1:
             raise ValueError("GraphedSegments: accumulation_steps must be 1")
         if not hip_adam_eligible(trainer.optimizer):
@@ -56,11 +64,34 @@ class GraphedSegments:
         self.losses: List[torch.Tensor] = []
         self.grads: List[List[Optional[torch.Tensor]]] = []
         self.pos = 0
+        self.ddp = bool(trainer.ddp)
+        self._flat = None    # (DDP) the flat all-reduce buffer and its per-parameter views
+        self._views = None
 
     def _run(self, i, state):
         s = self.segments[i]
         return self.trainer.forward_backward(s["feats"], s["masks"], s["tokens"], s["in_lens"],
-                                             s["tgt_lens"], state)
+                                             s["tgt_lens"], state, local=self.ddp)
+
+    def _allreduce(self, grads):
+        """(DDP) this rank's gradients -> their mean over the ranks, as per-parameter views of
+        one flat fp32 buffer: two copies and ONE all-reduce.  Returns the views."""
+        import torch.distributed as dist
+        if self._flat is None:
+            n = sum(p.numel() for p in self.params)
+            self._flat = torch.empty(n, dtype=torch.float32, device=self.params[0].device)
+            self._views, off = [], 0
+            for p in self.params:
+                self._views.append(self._flat[off:off + p.numel()].view_as(p))
+                off += p.numel()
+        present = [(v, g) for v, g in zip(self._views, grads) if g is not None]
+        if len(present) != len(self._views):
+            self._flat.zero_()   # (a parameter without a gradient this segment: zeros, as DDP)
+        if present:
+            torch._foreach_copy_([v for v, _ in present], [g for _, g in present])
+        dist.all_reduce(self._flat)
+        self._flat.div_(dist.get_world_size())
+        return self._views
 
     def capture(self, warmup: int = 1):
         """Warm every segment position up on a side stream (lazy library state: the capture
@@ -119,7 +150,8 @@ class GraphedSegments:
             raise RuntimeError("GraphedSegments.step before capture()")
         i = self.pos
         self.graphs[i].replay()
-        for p, g in zip(self.params, self.grads[i]):
+        grads = self._allreduce(self.grads[i]) if self.ddp else self.grads[i]
+        for p, g in zip(self.params, grads):
             p.grad = g
         self.trainer._clip_and_step()
         for p in self.params:   # as the eager loop's zero_grad(set_to_none=True): no caller

@@ -19,7 +19,8 @@ import torch
 import torch.nn as nn
 
 from .lucyrnn_conf import LucyRNNConfig
-from .ops import (cell_image_spec, colsum, fold_images, layer_norm, layer_norm_supported, ln_fold_ok,
+from .ops import (LN_FOLD_MODE, cell_image_spec, colsum, fold_images, layer_norm,
+                  layer_norm_supported, ln_fold_ok,
                   lucy_cell, lucy_cell_ln, proj_dgrad, weight_images, wgrad_splitk)
 
 
@@ -242,7 +243,8 @@ class LucyRNNtriton(nn.Module):
                 last = l == len(layers) - 1
                 # h carry = out[:, -1] (lucyrnn_triton.py:135), taken in fp32 from the scan and
                 # contiguous
-                rsink = [] if fold and not last else None
+                # (block records for the next layer: the scan-side fold only)
+                rsink = [] if fold and not last and LN_FOLD_MODE == 1 else None
                 if fold and l > 0:
                     # norms[l-1] folded into this layer's projection (ops.LucyCellLNFn): x_t is
                     # the previous layer's raw output, rec its block records

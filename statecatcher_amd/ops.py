@@ -290,6 +290,11 @@ def tn_ok(a, b):
             and b.shape[0] * b.stride(0) * 2 < 2 ** 32)
 
 
+# SC_TN_FWD=<tile_m>: the K = 512 forward projections on sc_gemm_tn_bf16 with that tile code
+# (A/B of the hand-written kernels against the library in the step; default: the library)
+TN_FWD_TILE = int(os.environ.get("SC_TN_FWD", "-1"))
+
+
 def proj_fwd(x, w):
     """x [M,K] @ w [N,K]^T for the frame-major projections.  Measured at the C2 shapes
     (tools/tn_bench.py): the hand-written kernel wins where the output stream dominates (layer 0,
@@ -297,6 +302,8 @@ def proj_fwd(x, w):
     246 us; csrc/tn_gemm.hip header)."""
     if x.shape[1] <= 128 and tn_ok(x, w):
         return gemm_tn(x, w, 256)   # 256 x 256 four-phase kernel: 114 us vs 120 (192-row tiles)
+    if TN_FWD_TILE >= 0 and tn_ok(x, w):
+        return gemm_tn(x, w, TN_FWD_TILE)
     return torch.matmul(x, w.t())
 
 
@@ -573,12 +580,31 @@ def lucy_cell(x, w, b, h0, s0, cdt=None, imgs=None, split_sink=None, rec_sink=No
 # ln_fwd / ln_part_sum (~125 us per step) but adds ~14 us of VALU per layer to the scan forward
 # (the records and the rstd rebuild) and ~7 us to the scan backward, which are VALU-bound, plus
 # the fold's own weight-gradient pieces -- so the LayerNorm kernels stay the default.
-USE_LN_FOLD = os.environ.get("SC_LN_FOLD", "0") == "1"
+# SC_LN_FOLD=2: the fold applied by the gate GEMM itself (sc_gemm_tn_ln_bf16, round 6): the row
+# statistics come from the rows as they stream through the GEMM and its epilogue writes the
+# normalised gates, so the forward scan is the plain one (no records, no rebuild); the backward
+# scan only scales its stored gradient by rstd (sc_lucy_scan_bwd_ln with ln_r = NULL).
+LN_FOLD_MODE = int(os.environ.get("SC_LN_FOLD", "0") or 0)
+USE_LN_FOLD = LN_FOLD_MODE in (1, 2)
 _FOLD = WeakIdKeyDictionary()
 
 
 def ln_fold_ok(D):
     return USE_LN_FOLD and D in (512, 1024)
+
+
+def gemm_tn_ln(h2d, wpp, r_img, eps):
+    """(gates [M, N] bf16 = rstd (h W''^T - mean r), stat [M, 2] fp32 (rstd, mean)) for the raw
+    previous-layer output h2d [M, D] (sc_gemm_tn_ln_bf16)."""
+    M, K = h2d.shape
+    N = wpp.shape[0]
+    c = torch.empty(M, N, dtype=torch.bfloat16, device=h2d.device)
+    stat = torch.empty(M, 2, dtype=torch.float32, device=h2d.device)
+    rc = _lib.load().sc_gemm_tn_ln_bf16(ptr(h2d), h2d.stride(0), ptr(wpp), wpp.stride(0), ptr(c),
+                                        c.stride(0), M, N, K, ptr(r_img), ptr(stat), float(eps),
+                                        stream_of(h2d))
+    check(rc, "sc_gemm_tn_ln_bf16")
+    return c, stat
 
 
 def fold_images(specs):
@@ -607,7 +633,9 @@ def fold_images(specs):
                                   img_t.data_ptr() if img_t is not None else None, rows, cols, kp,
                                   w.stride(0), bd, g.data_ptr(), shift.data_ptr()))
         keep += [w, b, g, be, shift]
-        out[i] = (img, img_t, bprime, rowsum)
+        # r in the image's (step-blocked) row order, for the GEMM-side fold's epilogue
+        r_img = torch.empty_like(rowsum) if bd and rows % (7 * 64) == 0 else None
+        out[i] = (img, img_t, bprime, rowsum, r_img if r_img is not None else rowsum)
         _FOLD[w] = (key, out[i])
     if preps:
         require_device(*keep)
@@ -617,6 +645,10 @@ def fold_images(specs):
             check(lib.sc_ln_fold_prep((_lib.LnFoldJob * len(part))(*part), len(part),
                                       stream_of(keep[0])), "sc_ln_fold_prep")
         _image_jobs(jobs, keep)
+        for o in out:   # (new entries) r permuted to the image's row order, after the prep
+            if o is not None and o[4] is not o[3]:
+                rows = o[3].numel()
+                o[4].copy_(o[3].view(7, rows // (7 * 64), 64).transpose(0, 1).reshape(-1))
     return out
 
 
@@ -664,18 +696,27 @@ class LucyCellLNFn(torch.autograd.Function):
                 rec_sink=None):
         ctx.set_materialize_grads(False)
         D = w.shape[0] // 7
-        wg, wt, bprime, rowsum = fimgs
-        with _timed("gate_gemm_fwd", h2d, 0):
-            gates = proj_fwd(h2d, wg)
-        gates = gates.view(B, T, D // 64, 7, 64)
+        wg, wt, bprime, rowsum, r_img = fimgs
         need = any(ctx.needs_input_grad)
-        stat = torch.empty(B, T, 2, dtype=torch.float32, device=h2d.device)
-        rec = None
-        if rec_sink is not None:
-            rec = torch.empty(B, T, D // 64, 2, dtype=torch.float32, device=h2d.device)
-            rec_sink.append(rec)
-        res = _scan_fwd(gates, h0, s0, need, bprime, want_h=True, split=split_sink is not None,
-                        ln=(rowsum, rec_in, stat, rec, eps))
+        if LN_FOLD_MODE == 2:
+            # the GEMM applies the fold (row statistics from the streaming rows), the scan is plain
+            with _timed("gate_gemm_fwd", h2d, 0):
+                gates, stat = gemm_tn_ln(h2d, wg, r_img, eps)
+            gates = gates.view(B, T, D // 64, 7, 64)
+            stat = stat.view(B, T, 2)
+            res = _scan_fwd(gates, h0, s0, need, bprime, want_h=True, split=split_sink is not None)
+            rowsum = None   # (the backward scan: ln_r = NULL, scale only)
+        else:
+            with _timed("gate_gemm_fwd", h2d, 0):
+                gates = proj_fwd(h2d, wg)
+            gates = gates.view(B, T, D // 64, 7, 64)
+            stat = torch.empty(B, T, 2, dtype=torch.float32, device=h2d.device)
+            rec = None
+            if rec_sink is not None:
+                rec = torch.empty(B, T, D // 64, 2, dtype=torch.float32, device=h2d.device)
+                rec_sink.append(rec)
+            res = _scan_fwd(gates, h0, s0, need, bprime, want_h=True, split=split_sink is not None,
+                            ln=(rowsum, rec_in, stat, rec, eps))
         gates, out, s_out, ckpt, h_out = res[:5]
         if len(res) > 5:
             split_sink.append(res[5])

@@ -1,6 +1,6 @@
 """One rank of the two-rank training runs on a single GPU (tests/test_gpu_ddp.py::test_*_two_ranks_*).
 
-    python tests/ddp_rank.py RANK WORLD PORT ACCUMULATION OUT.pt [WORKLOAD [OPTIM]]
+    python tests/ddp_rank.py RANK WORLD PORT ACCUMULATION OUT.pt [WORKLOAD [OPTIM [MODE]]]
 
 WORKLOAD (default c3), each on a 4-sequence batch, 4 segments with the encoder state carried,
 bf16 autocast, 8 MB buckets:
@@ -12,6 +12,9 @@ bf16 autocast, 8 MB buckets:
 OPTIM: adam (the reference's optim.Adam(lr 3e-4), stepped by the HIP clip + Adam) or sgd
 (torch.optim.SGD(lr 1e-3) after clip_grad_norm_: no sign normalisation, so reduction-order noise
 stays proportional to itself through the later steps).
+MODE: eager (SegmentTrainer.train_segment, DDP's bucket hooks) or graph (graphs.GraphedSegments:
+each segment's forward + backward captured once and replayed, the gradients all-reduced after
+the replay; adam, accumulation 1).
 
 WORLD = 2 ranks train rows [2 r, 2 r + 2) each under DistributedDataParallel over a "gloo" group
 (both ranks on cuda:0 -- RCCL refuses two ranks on one device; gloo all-reduces the CUDA
@@ -69,6 +72,7 @@ def main():
                                    int(sys.argv[4]), sys.argv[5])
     workload = sys.argv[6] if len(sys.argv) > 6 else "c3"
     optim = sys.argv[7] if len(sys.argv) > 7 else "adam"
+    mode_run = sys.argv[8] if len(sys.argv) > 8 else "eager"
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     torch.cuda.set_device(0)
     dev = torch.device("cuda:0")
@@ -115,10 +119,26 @@ def main():
     rows = slice(rank * B, (rank + 1) * B)
     tr.begin_batch()
     losses, equal = [], []
+    segs = []   # this rank's rows of the 4 segments, device-resident (as bench.py feeds them)
     for seg in range(SEGS):
         feats, tok, tl = batch(seg, T, U)
-        loss = tr.train_segment(feats[rows].to(dev), torch.ones(B, T, dtype=torch.bool, device=dev),
-                                tok[rows].to(dev), [T] * B, tl[rows])
+        segs.append(dict(feats=feats[rows].to(dev),
+                         masks=torch.ones(B, T, dtype=torch.bool, device=dev),
+                         tokens=tok[rows].to(dev),
+                         in_lens=torch.full((B,), T, dtype=torch.int64, device=dev),
+                         tgt_lens=torch.tensor(tl[rows], dtype=torch.int64, device=dev)))
+    graphed = None
+    if mode_run == "graph":
+        from statecatcher_amd.graphs import GraphedSegments
+        graphed = GraphedSegments(tr, segs).capture()
+        graphed.begin_batch()
+    for seg in range(SEGS):
+        if graphed is not None:
+            loss = graphed.step()
+        else:
+            sg = segs[seg]
+            loss = tr.train_segment(sg["feats"], sg["masks"], sg["tokens"], sg["in_lens"],
+                                    sg["tgt_lens"])
         losses.append(float(loss.detach()))
         if world > 1:
             flat = torch.cat([p.detach().reshape(-1) for p in all_params])
@@ -126,7 +146,7 @@ def main():
             dist.all_gather(got, flat)
             equal.append(all(torch.equal(got[0], x) for x in got[1:]))
     torch.cuda.synchronize()
-    if workload == "c4":   # the carried state is the xLSTM's dict of per-block tuples
+    if workload == "c4" and graphed is None:   # the xLSTM's dict of per-block tuples
         st = tr.encoder_state
         assert isinstance(st, dict) and st, type(st)
     res = {"losses": losses, "ranks_bitwise_equal": equal}

@@ -36,7 +36,7 @@ def test_binding_covers_header(lib):
 
 
 def test_abi_version_and_sizes(lib):
-    assert lib.sc_abi_version() == 13
+    assert lib.sc_abi_version() == 14
     assert lib.sc_lucy_scan_chunk() == 64
     assert lib.sc_lucy_scan_ckpt_numel(32, 1500, 512) == 32 * 24 * 2 * 512
     assert lib.sc_lucy_scan_ckpt_numel(2, 64, 3) == 2 * 1 * 2 * 3

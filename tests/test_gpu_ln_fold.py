@@ -1,7 +1,13 @@
 """GPU parity of the inter-layer LayerNorm folded into the next gate projection (csrc/ln_fold.hip,
-sc_lucy_scan_fwd_ln / _bwd_ln, ops.LucyCellLNFn), which replaces nn.LayerNorm +
-LinearSafe (lucyrnn_triton.py:96-97, :136-137, :20-25) under bf16 autocast when SC_LN_FOLD=1
-(opt-in: ops.USE_LN_FOLD; the tests switch it on).
+ops.LucyCellLNFn), which replaces nn.LayerNorm + LinearSafe (lucyrnn_triton.py:96-97, :136-137,
+:20-25) under bf16 autocast, in both of its forms (the tests switch them on):
+  mode 1 (SC_LN_FOLD=1, round 5): the scans apply it (sc_lucy_scan_fwd_ln / _bwd_ln rebuild the
+         gates from block records);
+  mode 2 (SC_LN_FOLD=2, round 6): the gate GEMM applies it (sc_gemm_tn_ln_bf16: row statistics
+         from the streaming rows, normalised gates out), the backward scan only scales.
+
+* sc_gemm_tn_ln_bf16 against fp64 torch (LN(h) W^T - W beta from the same bf16 h) and its
+  statistics against torch's.
 
 * The folded images (W'' = bf16(gamma W - shift)), b' and r against torch on the same fp32
   values.
@@ -42,7 +48,7 @@ def test_fold_images_match_torch():
     b = (torch.randn(7 * D, generator=g) * 0.1).to(DEV)
     gam = (1.0 + 0.2 * torch.randn(D, generator=g)).to(DEV)
     bet = (0.1 * torch.randn(D, generator=g)).to(DEV)
-    (img, img_t, bprime, rowsum), = ops().fold_images([(w, b, gam, bet, D, D, True)])
+    (img, img_t, bprime, rowsum, r_img), = ops().fold_images([(w, b, gam, bet, D, D, True)])
     torch.cuda.synchronize()
     gw = gam * w                                   # exact fp32 products, as the kernels form them
     shift = gw.double().mean(1)
@@ -56,6 +62,51 @@ def test_fold_images_match_torch():
                                rtol=1e-5, atol=1e-5)
     torch.testing.assert_close(rowsum.double(), got.double().sum(1), rtol=0, atol=1e-6)
     assert float(rowsum.abs().max()) < 1e-2 * float(gw.abs().sum(1).max())
+    # r in the image's (step-blocked) row order: the row sums of the image's own rows
+    torch.testing.assert_close(r_img.double(), img.double().sum(1), rtol=0, atol=1e-6)
+
+
+def _set_mode(monkeypatch, mode):
+    from statecatcher_amd import lucyrnn_triton as lt
+    o = ops()
+    monkeypatch.setattr(o, "USE_LN_FOLD", mode != 0)
+    monkeypatch.setattr(o, "LN_FOLD_MODE", mode)
+    monkeypatch.setattr(lt, "LN_FOLD_MODE", mode)
+
+
+@pytest.mark.parametrize("M", [48000, 1000, 7])
+def test_gemm_tn_ln_vs_torch(M):
+    """sc_gemm_tn_ln_bf16 = rstd (h W''^T - mean r) against fp64 torch's LN(h) W^T - W beta on the
+    same bf16 h (the scan adds b' = b + W beta), at C2's shape, a ragged panel and fewer rows than
+    a fragment; the (rstd, mean) it writes against torch's biased statistics.  Tolerance: the
+    bf16 output rounding (2^-8 of each value) plus the W'' image's bf16 rounding, which the
+    unfused path pays on LN(h) instead (1e-2 of the largest |C|)."""
+    g = torch.Generator().manual_seed(M)
+    D = 512
+    w = (torch.randn(7 * D, D, generator=g) * 0.03).to(DEV)
+    b = (torch.randn(7 * D, generator=g) * 0.1).to(DEV)
+    gam = (1.0 + 0.2 * torch.randn(D, generator=g)).to(DEV)
+    bet = (0.1 * torch.randn(D, generator=g)).to(DEV)
+    h = (torch.randn(M, D, generator=g) * 0.4 + 0.3 * torch.randn(M, 1, generator=g)).to(DEV) \
+        .to(torch.bfloat16)
+    (img, _, bprime, _, r_img), = ops().fold_images([(w, b, gam, bet, D, D, False)])
+    c, stat = ops().gemm_tn_ln(h, img, r_img, 1e-5)
+    torch.cuda.synchronize()
+    h64 = h.double()
+    mean = h64.mean(1, keepdim=True)
+    var = h64.var(1, unbiased=False, keepdim=True)
+    y = (h64 - mean) / torch.sqrt(var + 1e-5) * gam.double() + bet.double()
+    wsb = ops().step_blocked_rows(w, D).double()           # the image's row order
+    ref = y @ wsb.t() - (wsb @ bet.double())
+    err = (c.double() - ref).abs()
+    tol = ref.abs() * 2.0 ** -8 + 1e-2 * float(ref.abs().max())
+    print(f"M={M}: max err {float(err.max()):.3e} (|C| max {float(ref.abs().max()):.2f}), rel "
+          f"Frobenius {rel(c, ref):.2e}")
+    assert bool((err <= tol).all())
+    assert rel(c, ref) <= 5e-3
+    torch.testing.assert_close(stat[:, 1].double(), mean[:, 0], rtol=0, atol=2e-6)
+    torch.testing.assert_close(stat[:, 0].double(), 1.0 / torch.sqrt(var[:, 0] + 1e-5),
+                               rtol=2e-5, atol=0)
 
 
 def condition_(m, D, gen):
@@ -109,12 +160,13 @@ def _run(m, x, autocast):
     return out
 
 
-def test_fold_layer_vs_unfused_and_fp32(monkeypatch):
-    monkeypatch.setattr(ops(), "USE_LN_FOLD", True)   # (opt-in: SC_LN_FOLD=1)
+@pytest.mark.parametrize("mode", [1, 2])
+def test_fold_layer_vs_unfused_and_fp32(monkeypatch, mode):
+    _set_mode(monkeypatch, mode)   # (opt-in: SC_LN_FOLD=1 / 2)
     m, x = _layer_pair()
     ref32 = _run(m, x, autocast=False)
     folded = _run(m, x, autocast=True)
-    monkeypatch.setattr(ops(), "USE_LN_FOLD", False)
+    _set_mode(monkeypatch, 0)
     plain = _run(m, x, autocast=True)
     lines, bad = [], []
     for k in ref32:
@@ -126,13 +178,14 @@ def test_fold_layer_vs_unfused_and_fp32(monkeypatch):
     assert not bad, bad
 
 
-def test_fold_engaged_and_no_layernorm_launch(monkeypatch):
+@pytest.mark.parametrize("mode", [1, 2])
+def test_fold_engaged_and_no_layernorm_launch(monkeypatch, mode):
     """The bf16 forward of a 3-layer stack takes LucyCellLNFn for layers 1 and 2 and never
     launches the LayerNorm kernel."""
     from statecatcher_amd import LucyRNNConfig, LucyRNNtriton
     calls = {"ln": 0, "fold": 0}
     o = ops()
-    monkeypatch.setattr(o, "USE_LN_FOLD", True)
+    _set_mode(monkeypatch, mode)
     orig_ln, orig_fold = o.LayerNormFn.apply, o.LucyCellLNFn.apply
 
     def ln(*a):
@@ -153,7 +206,8 @@ def test_fold_engaged_and_no_layernorm_launch(monkeypatch):
     assert calls == {"ln": 0, "fold": 2}
 
 
-def test_c2_stack_fold_vs_unfused(monkeypatch):
+@pytest.mark.parametrize("mode", [1, 2])
+def test_c2_stack_fold_vs_unfused(monkeypatch, mode):
     """6 x 512, V = 1024, T = 1500, B = 2 with the CTC criterion, conditioned gates: the loss and
     every parameter gradient of the folded bf16 stack against the fp32 run of the same model, no
     further from it than the unfused bf16 stack is (2x + floor)."""
@@ -181,10 +235,10 @@ def test_c2_stack_fold_vs_unfused(monkeypatch):
                                          [T, T], [150, 97], 0)
         loss.backward()
         return float(loss), {n: p.grad.detach().clone() for n, p in model.named_parameters()}
-    monkeypatch.setattr(ops(), "USE_LN_FOLD", True)
+    _set_mode(monkeypatch, mode)
     l32, g32 = run(False)
     lf, gf = run(True)
-    monkeypatch.setattr(ops(), "USE_LN_FOLD", False)
+    _set_mode(monkeypatch, 0)
     lp, gp = run(True)
     print(f"C2 stack loss fp32 {l32:.6f} fold {lf:.6f} unfused {lp:.6f}")
     assert abs(lf - l32) <= max(2 * abs(lp - l32), 1e-3 * abs(l32))

@@ -35,12 +35,22 @@ def test_refuses_an_optimizer_the_hip_adam_does_not_step():
         GraphedSegments(tr, _segs())
 
 
-def test_refuses_ddp(monkeypatch):
-    from statecatcher_amd.graphs import GraphedSegments
+def test_ddp_trainer_captures_the_bare_modules(monkeypatch):
+    """Under DDP the graphs run the bare modules (local=True: no bucket hooks in the capture) and
+    step() all-reduces afterwards (graphs.GraphedSegments; the GPU test pins it bitwise against
+    eager DDP)."""
+    from statecatcher_amd import graphs
+    monkeypatch.setattr(graphs, "hip_adam_eligible", lambda opt: True)
     tr = _trainer()
     tr.ddp = True
-    with pytest.raises(ValueError, match="DDP"):
-        GraphedSegments(tr, _segs())
+    seg = _segs()[0]
+    seg["feats"] = types.SimpleNamespace(is_cuda=True, device=torch.device("cpu"))
+    gs = graphs.GraphedSegments(tr, [seg])
+    assert gs.ddp
+    seen = {}
+    monkeypatch.setattr(tr, "forward_backward", lambda *a, **k: seen.update(k) or (None, None))
+    gs._run(0, None)
+    assert seen.get("local") is True
 
 
 def test_refuses_host_segments(monkeypatch):
