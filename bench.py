@@ -451,8 +451,11 @@ def main():
         opt = torch.optim.Adam(params, lr=3e-4)
     amp = torch.bfloat16 if args.dtype == "bf16" else None
     # the reference segment loop (train.py:460-581) with DDP over RCCL when world > 1
+    # --graph on: no DDP wrapper; the graphs broadcast rank 0's weights and all-reduce the
+    # gradients after each replay themselves (graphs.GraphedSegments)
     trainer = SegmentTrainer(model, criterion, opt, accumulation_steps=1, max_grad_norm=50.0,
-                             amp_dtype=amp, bucket_cap_mb=args.bucket_mb, **tkw)
+                             amp_dtype=amp, bucket_cap_mb=args.bucket_mb,
+                             ddp=(world > 1 and args.graph != "on"), **tkw)
     segs = synth_segments(args, rank, device)
     if args.rccl_footprint:
         footprint_hooks(model, args.rccl_footprint, device)
@@ -466,7 +469,9 @@ def main():
                                      seg["tgt_lens"])
 
     step = eager_step
-    for _ in range(args.warmup):
+    # (data-parallel graph mode: no eager warm-up -- without the DDP wrapper its steps would not
+    # all-reduce; the capture warms up on its own and the replays below warm the graphs)
+    for _ in range(args.warmup if not (args.graph == "on" and world > 1) else 0):
         step()
     torch.cuda.synchronize()
     graphed = None
@@ -481,8 +486,8 @@ def main():
                 graphed.begin_batch()
             return graphed.step()
         if args.warmup:
-            for _ in range(args.segments):   # one replay of every graph before timing
-                step()
+            for _ in range(max(args.segments, args.warmup if world > 1 else 0)):
+                step()   # one replay of every graph (data parallel: the warm-up steps) before timing
         torch.cuda.synchronize()
     if args.host_probe:
         torch.cuda.set_sync_debug_mode(1)

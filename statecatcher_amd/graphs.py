@@ -19,14 +19,16 @@ pool), and replays them:
 Same kernels in the same order as the eager step, so the losses and weights are bitwise the
 eager loop's (tests/test_gpu_graphs.py).
 
-Under DDP (world > 1) the graphs hold the bare modules' forward + backward (this rank's
-gradients; DDP's bucket hooks are host callbacks and are not captured), and ``step`` all-reduces
-the gradients after the replay -- one flat fp32 all-reduce of every gradient, divided by the world
-size as DDP's default hook does -- then clips and steps.  The all-reduce then no longer overlaps
-the backward (DDP's buckets do); in exchange the host issues ~0.2 ms per segment instead of
-~2.8 ms.  The backend is the process group's (RCCL on the GPUs; gloo in the one-GPU two-rank
-test, tests/test_gpu_ddp.py), and DDP's own start-up broadcast has already made the ranks'
-weights equal.
+Data parallel (an initialised process group with world > 1): the trainer is built WITHOUT the
+DDP wrapper (``SegmentTrainer(..., ddp=False)``) -- DDP's reducer hangs its hooks on the
+parameters' gradient accumulators, which would then run inside the capture -- and
+GraphedSegments does DDP's two jobs itself: at construction it broadcasts rank 0's parameters
+(DDP's start-up broadcast), and ``step`` all-reduces the gradients after each replay (one flat
+fp32 all-reduce of every gradient, divided by the world size as DDP's default hook does) before
+the clip + Adam.  The all-reduce no longer overlaps the backward (DDP's buckets do); in exchange
+the host issues ~0.2 ms per segment instead of ~2.8 ms.  The backend is the process group's
+(RCCL on the GPUs; gloo in the one-GPU two-rank test, tests/test_gpu_ddp.py, bitwise equal to
+eager DDP).
 
 Restrictions, all checked: ``accumulation_steps == 1`` (every segment steps),
 HIP Adam (optim.hip_adam_eligible), no per-launch timing events during capture
@@ -46,6 +48,10 @@ from .optim import hip_adam_eligible
 
 class GraphedSegments:
     def __init__(self, trainer, segments: List[dict]):
+        if trainer.ddp:
+            raise ValueError("GraphedSegments: build the trainer with ddp=False; under a process "
+                             "group of world > 1 the graphs broadcast and all-reduce themselves "
+                             "(DDP's reducer hooks would run inside the capture)")
         if trainer.accumulation_steps != 1:
             raise ValueError("GraphedSegments: accumulation_steps must be 1")
         if not hip_adam_eligible(trainer.optimizer):
@@ -64,14 +70,20 @@ class GraphedSegments:
         self.losses: List[torch.Tensor] = []
         self.grads: List[List[Optional[torch.Tensor]]] = []
         self.pos = 0
-        self.ddp = bool(trainer.ddp)
-        self._flat = None    # (DDP) the flat all-reduce buffer and its per-parameter views
+        import torch.distributed as dist
+        self.ddp = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+        self._flat = None    # (data parallel) the flat all-reduce buffer, per-parameter views
         self._views = None
+        if self.ddp:   # DDP's start-up broadcast: every rank starts from rank 0's weights
+            with torch.no_grad():
+                for p in self.params:
+                    dist.broadcast(p.data, 0)
+            ops.invalidate_weight_images()
 
     def _run(self, i, state):
         s = self.segments[i]
         return self.trainer.forward_backward(s["feats"], s["masks"], s["tokens"], s["in_lens"],
-                                             s["tgt_lens"], state, local=self.ddp)
+                                             s["tgt_lens"], state)
 
     def _allreduce(self, grads):
         """(DDP) this rank's gradients -> their mean over the ranks, as per-parameter views of

@@ -155,20 +155,15 @@ class SegmentTrainer:
     def _steps_now(self) -> bool:
         return (self.global_step + 1) % self.accumulation_steps == 0
 
-    def forward_backward(self, feats, masks, tokens, in_lens, tgt_lens, input_state,
-                         local: bool = False):
+    def forward_backward(self, feats, masks, tokens, in_lens, tgt_lens, input_state):
         """compute_loss under the trainer's autocast + backward of loss / accumulation_steps
         (train.py:508-537) from ``input_state``.  Returns (loss, output_state).  No host sync:
-        graphs.GraphedSegments captures this call as one HIP graph.  local=True runs the bare
-        modules, not their DDP wrappers: this rank's gradients only, no bucket all-reduce (the
-        graph route all-reduces them after the replay, graphs.GraphedSegments)."""
-        net = self.model if local else self.net
-        joiner = self.joiner if local else self.joiner_net
+        graphs.GraphedSegments captures this call as one HIP graph."""
         with torch.autocast(feats.device.type, dtype=self.amp_dtype or torch.float32,
                             enabled=self.amp_dtype is not None):
             loss, output_state, _, _ = compute_loss(
-                self.mode, self.criterion, net, feats, masks, tokens, in_lens, tgt_lens,
-                self.blank_id, use_rnnt_joiner=joiner, input_state=input_state,
+                self.mode, self.criterion, self.net, feats, masks, tokens, in_lens, tgt_lens,
+                self.blank_id, use_rnnt_joiner=self.joiner_net, input_state=input_state,
                 compact=self.compact_rnnt)
         # loss / accumulation_steps (train.py:535); a division by 1 is the identity
         (loss / self.accumulation_steps if self.accumulation_steps != 1 else loss).backward()

@@ -12,9 +12,10 @@ bf16 autocast, 8 MB buckets:
 OPTIM: adam (the reference's optim.Adam(lr 3e-4), stepped by the HIP clip + Adam) or sgd
 (torch.optim.SGD(lr 1e-3) after clip_grad_norm_: no sign normalisation, so reduction-order noise
 stays proportional to itself through the later steps).
-MODE: eager (SegmentTrainer.train_segment, DDP's bucket hooks) or graph (graphs.GraphedSegments:
+MODE: eager (SegmentTrainer.train_segment, DDP's bucket hooks), graph (graphs.GraphedSegments:
 each segment's forward + backward captured once and replayed, the gradients all-reduced after
-the replay; adam, accumulation 1).
+the replay; no DDP wrapper; adam, accumulation 1) or split (WORLD 1: the two ranks' halves as two
+micro-batches of one process with their own carried states, gradients summed and halved).
 
 WORLD = 2 ranks train rows [2 r, 2 r + 2) each under DistributedDataParallel over a "gloo" group
 (both ranks on cuda:0 -- RCCL refuses two ranks on one device; gloo all-reduces the CUDA
@@ -107,47 +108,77 @@ def main():
     else:
         opt = torch.optim.Adam(all_params, lr=3e-4)
     kw = dict(mode="rnnt", joiner=joiner) if mode == "rnnt" else {}
+    # graph mode: no DDP wrapper (its reducer's hooks sit on the parameters' gradient
+    # accumulators and would run inside the capture); GraphedSegments broadcasts rank 0's
+    # weights and all-reduces the gradients itself
+    ddp = world > 1 and mode_run != "graph"
     tr = SegmentTrainer(model, crit, opt, amp_dtype=torch.bfloat16, max_grad_norm=50.0,
-                        bucket_cap_mb=8.0, accumulation_steps=acc, ddp=world > 1, **kw)
-    if world > 1:
+                        bucket_cap_mb=8.0, accumulation_steps=acc, ddp=ddp, **kw)
+    if ddp:
         assert isinstance(tr.net, torch.nn.parallel.DistributedDataParallel)
         assert tr.net.bucket_bytes_cap == 8 * 1024 * 1024
         if joiner is not None:
             assert isinstance(tr.joiner_net, torch.nn.parallel.DistributedDataParallel)
-    init = [p.detach().cpu().clone() for p in all_params]   # (DDP has broadcast rank 0's)
-    B = BFULL // world
-    rows = slice(rank * B, (rank + 1) * B)
-    tr.begin_batch()
-    losses, equal = [], []
+    # split (WORLD 1): the two ranks' halves as two micro-batches of ONE process, each with its
+    # own carried state, gradients summed and halved before the clip + step -- the arithmetic of a
+    # two-rank DDP step done without DDP (tests/test_gpu_ddp.py: bitwise equal to it)
+    halves = 2 if mode_run == "split" else 1
+    B = BFULL // (world * halves)
+
+    def rows_of(r):
+        return slice(r * B, (r + 1) * B)
     segs = []   # this rank's rows of the 4 segments, device-resident (as bench.py feeds them)
     for seg in range(SEGS):
         feats, tok, tl = batch(seg, T, U)
-        segs.append(dict(feats=feats[rows].to(dev),
-                         masks=torch.ones(B, T, dtype=torch.bool, device=dev),
-                         tokens=tok[rows].to(dev),
-                         in_lens=torch.full((B,), T, dtype=torch.int64, device=dev),
-                         tgt_lens=torch.tensor(tl[rows], dtype=torch.int64, device=dev)))
+        per = []
+        for hh in range(halves):
+            rows = rows_of(rank * halves + hh)
+            per.append(dict(feats=feats[rows].to(dev),
+                            masks=torch.ones(B, T, dtype=torch.bool, device=dev),
+                            tokens=tok[rows].to(dev),
+                            in_lens=torch.full((B,), T, dtype=torch.int64, device=dev),
+                            tgt_lens=torch.tensor(tl[rows], dtype=torch.int64, device=dev)))
+        segs.append(per)
     graphed = None
     if mode_run == "graph":
         from statecatcher_amd.graphs import GraphedSegments
-        graphed = GraphedSegments(tr, segs).capture()
+        graphed = GraphedSegments(tr, [sg[0] for sg in segs])   # (broadcasts rank 0's weights)
+    init = [p.detach().cpu().clone() for p in all_params]   # (rank 0's, broadcast)
+    if graphed is not None:
+        graphed.capture()
         graphed.begin_batch()
+    tr.begin_batch()
+    losses, equal = [], []
+    states = [None] * halves
     for seg in range(SEGS):
         if graphed is not None:
-            loss = graphed.step()
+            loss = float(graphed.step().detach())
+        elif mode_run == "split":
+            assert world == 1 and acc == 1
+            loss = []
+            for hh in range(halves):
+                sg = segs[seg][hh]
+                lh, states[hh] = tr.forward_backward(sg["feats"], sg["masks"], sg["tokens"],
+                                                     sg["in_lens"], sg["tgt_lens"], states[hh])
+                loss.append(float(lh.detach()))
+            for p in all_params:
+                if p.grad is not None:
+                    p.grad.div_(halves)
+            tr._clip_and_step()
+            tr.optimizer.zero_grad(set_to_none=True)
         else:
-            sg = segs[seg]
-            loss = tr.train_segment(sg["feats"], sg["masks"], sg["tokens"], sg["in_lens"],
-                                    sg["tgt_lens"])
-        losses.append(float(loss.detach()))
+            sg = segs[seg][0]
+            loss = float(tr.train_segment(sg["feats"], sg["masks"], sg["tokens"], sg["in_lens"],
+                                          sg["tgt_lens"]).detach())
+        losses.append(loss)
         if world > 1:
             flat = torch.cat([p.detach().reshape(-1) for p in all_params])
             got = [torch.empty_like(flat) for _ in range(world)]
             dist.all_gather(got, flat)
             equal.append(all(torch.equal(got[0], x) for x in got[1:]))
     torch.cuda.synchronize()
-    if workload == "c4" and graphed is None:   # the xLSTM's dict of per-block tuples
-        st = tr.encoder_state
+    if workload == "c4" and graphed is None and mode_run != "split":
+        st = tr.encoder_state   # the carried state is the xLSTM's dict of per-block tuples
         assert isinstance(st, dict) and st, type(st)
     res = {"losses": losses, "ranks_bitwise_equal": equal}
     if rank == 0:

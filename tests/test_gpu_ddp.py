@@ -191,7 +191,11 @@ def _two_rank_case(workload, optim, acc, tmp_path):
          # the largest element-wise parameter difference, in units of lr x steps taken
          "flip": max(float((a.double() - b.double()).abs().max()) for a, b in
                      zip(r0["params"], single["params"])) / (lr * (4 // acc)),
-         "numel": [a.numel() for a in r0["params"]]}
+         "numel": [a.numel() for a in r0["params"]],
+         # the whole first-update gradient as one vector (small tensors whose gradient nearly
+         # cancels weigh by their size)
+         "grad_all": _rel(torch.cat([a.reshape(-1) for a in r0["grads"]]),
+                          torch.cat([b.reshape(-1) for b in single["grads"]]))}
     assert len(e["grad"]) == len(r0["params"]) and all(map(lambda x: x == x, e["update"]))
     print(f"{workload} {optim} acc={acc}: losses {r0['losses']} / {r1['losses']} vs "
           f"{single['losses']}; loss rel {['%.1e' % x for x in e['loss']]}; first-update gradient "
@@ -199,8 +203,9 @@ def _two_rank_case(workload, optim, acc, tmp_path):
           f"{max(e['param']):.2e}; update rel max {max(e['update']):.2e} median "
           f"{sorted(e['update'])[len(e['update']) // 2]:.2e}; largest element difference "
           f"{e['flip']:.2f} lr-steps")
-    print("  per tensor (numel, param rel, update rel):",
-          [(n, f"{p:.1e}", f"{u:.1e}") for n, p, u in zip(e["numel"], e["param"], e["update"])])
+    print("  per tensor (numel, first-update gradient rel, param rel, update rel):",
+          [(n, f"{g:.1e}", f"{p:.1e}", f"{u:.1e}")
+           for n, g, p, u in zip(e["numel"], e["grad"], e["param"], e["update"])])
     return e
 
 
@@ -266,25 +271,54 @@ def test_c4_c5_two_ranks_on_one_gpu_equal_one_process_on_the_full_batch(workload
         carried state is a dict of per-block tuples (/root/reference/model.py:17-18);
       * c5: LucyRNN 6 x 512 + RNN-T with the fused joiner (U = 150), encoder and joiner both
         DDP modules with their own buckets and one optimizer (model.py:73-145).
-    Same bar as C3: ranks bitwise equal every segment, the first update's all-reduced gradients
-    the full batch's to 1e-4, every loss to 1e-3, the final parameters within Adam's sign-flip
-    bound (2 lr per step per element, weight matrices 1e-2)."""
+    Against one process on the full B = 4 batch the first loss is equal to 1e-5, but unlike C3
+    (whose GEMM shapes the shipped TunableOp table pins to one kernel for any row count) the
+    xLSTM projections and the joiner's enc / pred projections run library GEMMs whose kernel
+    the library picks by the row count (B = 2 vs 4): their bf16 outputs differ by an ulp here and
+    there, so the first update's gradients agree only at bf16 level (measured 4e-3 (c4) / 2.3e-3
+    (c5) on the largest tensors, 0.57 on a 4-element gate bias whose gradient nearly cancels).
+    Pinned here: the first loss to 1e-5, the whole first-update gradient to 1e-2, every loss to
+    5e-3, no parameter element more than 2 lr per step apart (Adam's sign-flip bound).  That
+    DDP itself adds nothing is pinned bitwise by
+    test_two_ranks_bitwise_equal_to_split_batch_single_process."""
     e = _two_rank_case(workload, "adam", 1, tmp_path)
     assert e["loss"][0] <= 1e-5, e["loss"]
-    assert max(e["grad"]) <= 1e-4, e["grad"]
-    _adam_bounds(e)
+    assert e["grad_all"] <= 1e-2, e["grad_all"]
+    assert max(e["loss"]) <= 5e-3, e["loss"]
+    assert e["flip"] <= 2.0, e["flip"]
+
+
+@pytest.mark.parametrize("workload", ["c3", "c4", "c5"])
+def test_two_ranks_bitwise_equal_to_split_batch_single_process(workload, tmp_path):
+    """DDP adds nothing to the arithmetic: two rank processes (B = 2 each, DDP over gloo, 4
+    segments with carried state, the HIP clip + Adam) against ONE process that runs the same two
+    halves as two micro-batches with their own carried states, sums their gradients, halves them
+    and steps (tests/ddp_rank.py mode split): the same kernels at the same row counts, and a
+    two-rank mean is one fp32 add and an exact halving however it is bucketed, so every loss of
+    every half and every parameter after the 4 updates must be BITWISE equal -- for the LucyRNN
+    + CTC step (c3), the xLSTM encoder with its dict state (c4) and the RNN-T encoder + joiner
+    as two DDP modules (c5)."""
+    split = _run_ranks(1, 1, tmp_path, workload, "adam", "split")[0]
+    r0, r1 = _run_ranks(2, 1, tmp_path, workload, "adam", "eager")
+    assert r0["ranks_bitwise_equal"] == [True] * 4
+    print(f"{workload}: split halves {split['losses']}; ranks {r0['losses']} / {r1['losses']}")
+    assert [l[0] for l in split["losses"]] == r0["losses"]
+    assert [l[1] for l in split["losses"]] == r1["losses"]
+    assert all(torch.equal(a, b) for a, b in zip(r0["params"], split["params"]))
+    assert any(not torch.equal(a, b) for a, b in zip(r0["params"], r0["init"]))
 
 
 @pytest.mark.parametrize("workload", ["c3", "c5"])
 def test_graph_replay_ddp_two_ranks_bitwise_equal_to_eager_ddp(workload, tmp_path):
-    """DDP under HIP-graph replay (verdict r5 item 8): two rank processes on cuda:0 over gloo,
-    each capturing its 4 segment positions (graphs.GraphedSegments: the bare modules' forward +
+    """Data-parallel training under HIP-graph replay (verdict r5 item 8): two rank processes on
+    cuda:0 over gloo, each capturing its 4 segment positions (graphs.GraphedSegments on a trainer
+    without the DDP wrapper: rank 0's weights broadcast at construction, the bare forward +
     backward in the graph, one flat all-reduce of the gradients after each replay, then the HIP
     clip + Adam), against the same two ranks training eagerly under DDP's bucket hooks.  The
     per-rank gradients are the same kernels' and a two-rank mean is one fp32 add and an exact
     halving whichever way it is bucketed, so losses and parameters must be BITWISE equal after
-    all 4 segments, and the ranks bitwise equal to each other throughout.  c5: the joiner is a
-    second module in the same all-reduce."""
+    all 4 segments, and the ranks bitwise equal to each other throughout.  c5: the joiner's
+    gradients ride in the same flat all-reduce."""
     eager = _run_ranks(2, 1, tmp_path, workload, "adam", "eager")
     graph = _run_ranks(2, 1, tmp_path, workload, "adam", "graph")
     for r in graph:

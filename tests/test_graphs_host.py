@@ -35,22 +35,15 @@ def test_refuses_an_optimizer_the_hip_adam_does_not_step():
         GraphedSegments(tr, _segs())
 
 
-def test_ddp_trainer_captures_the_bare_modules(monkeypatch):
-    """Under DDP the graphs run the bare modules (local=True: no bucket hooks in the capture) and
-    step() all-reduces afterwards (graphs.GraphedSegments; the GPU test pins it bitwise against
-    eager DDP)."""
-    from statecatcher_amd import graphs
-    monkeypatch.setattr(graphs, "hip_adam_eligible", lambda opt: True)
+def test_refuses_a_ddp_wrapped_trainer(monkeypatch):
+    """A DDP-wrapped trainer is refused: DDP's reducer hooks sit on the gradient accumulators and
+    would run inside the capture; under world > 1 the graphs broadcast and all-reduce themselves
+    (build the trainer with ddp=False; tests/test_gpu_ddp.py pins it against eager DDP)."""
+    from statecatcher_amd.graphs import GraphedSegments
     tr = _trainer()
     tr.ddp = True
-    seg = _segs()[0]
-    seg["feats"] = types.SimpleNamespace(is_cuda=True, device=torch.device("cpu"))
-    gs = graphs.GraphedSegments(tr, [seg])
-    assert gs.ddp
-    seen = {}
-    monkeypatch.setattr(tr, "forward_backward", lambda *a, **k: seen.update(k) or (None, None))
-    gs._run(0, None)
-    assert seen.get("local") is True
+    with pytest.raises(ValueError, match="ddp=False"):
+        GraphedSegments(tr, _segs())
 
 
 def test_refuses_host_segments(monkeypatch):
