@@ -50,6 +50,12 @@ typedef int i4v __attribute__((ext_vector_type(4)));
 #ifndef SC_TN_ABL
 #define SC_TN_ABL 0
 #endif
+// SC_TNW_AB: also build the plain one-wave-per-SIMD kernels (tile_m 1 / 2 / 3; A/B only, measured
+// slower than the library: profiles/r6_tnw.md).  The LayerNorm-fold instance tnw32_kernel<4, true>
+// (sc_gemm_tn_ln_bf16, SC_LN_FOLD=2) is always built.
+#ifndef SC_TNW_AB
+#define SC_TNW_AB 0
+#endif
 
 constexpr int kBK = 64;      // K columns per stage (two v_mfma_f32_16x16x32_bf16 k-steps)
 constexpr int kRowB = 128;   // LDS image row pitch (bytes): whole 128-byte lines per DMA row
@@ -731,8 +737,16 @@ __global__ void __launch_bounds__(512, 1) tnpp_kernel(TnArgs a) {
 //     panel comes from HBM once per XCD and W stays in its L2.
 namespace tnw {
 constexpr int kSlotB = 64 * 1024;   // one K-tile: A image 32 KiB + B image 32 KiB
+// lgkmcnt(0) as the builtin (vmcnt and expcnt left at their maxima), which the compiler's waitcnt
+// pass sees.  (Read in the generated code, profiles/r6_tnw.md: with either this or an inline-asm
+// wait the pass still puts an lgkmcnt(0) after the first MFMA of the k-step whose next fragments
+// were just issued, so each k-step exposes the LDS read latency; fragment reads issued from
+// inline asm instead spill 40-48 VGPRs into the loop.)
+__device__ __forceinline__ void frag_wait() { __builtin_amdgcn_s_waitcnt(0xC07F); }
 struct Frag { i4v v[8]; };          // 8 fragments of one operand for one k-step
 }  // namespace tnw
+
+#if SC_TNW_AB   // (A/B builds only: measured slower than hipBLASLt, profiles/r6_tnw.md)
 
 __global__ void __launch_bounds__(256, 1) tnw_kernel(TnArgs a) {
   using namespace tnw;
@@ -826,7 +840,7 @@ __global__ void __launch_bounds__(256, 1) tnw_kernel(TnArgs a) {
     // k-step 0 on X while k-step 1's fragments come in
     read(kt, 1, Y, Yw);
     mfmas(X, Xw);
-    lds_read_wait();
+    tnw::frag_wait();
     if (kt + 1 < nkt) {
       dma_wait();      // this wave's share of K-tile kt + 1 (nothing younger is in flight)
       lds_barrier();   // ... everyone's, and every read of slot kt % 2 is done
@@ -874,6 +888,7 @@ int launch_tnw(const TnArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(tnw_kernel, dim3(grid), dim3(256), lds, st, a);
   return 0;
 }
+#endif  // SC_TNW_AB
 
 // ------------------------------------------------------------------------------------------
 // tnw with a deeper DMA ring (tile_m = 2): tnw32_kernel<NS>.
@@ -1035,7 +1050,7 @@ __global__ void __launch_bounds__(256, 1) tnw32_kernel(TnArgs a, TnLn ln) {
   // stage s is read after the barrier that retires it and multiplied one barrier later; at that
   // barrier every read of stage s - 1 is done, so its slot takes stage s - 1 + NS
   for (int st = 0; st < nst; st += 2) {   // nst = K / 32 is even
-    lds_read_wait();
+    tnw::frag_wait();
     retire(st + 1);
     lds_barrier();
     if (st + NS < nst && !(SC_TN_ABL & 2)) dma(st + NS);
@@ -1043,7 +1058,7 @@ __global__ void __launch_bounds__(256, 1) tnw32_kernel(TnArgs a, TnLn ln) {
     stat_read(st + 1, sv);
     mfmas(X, Xw);
     stat_acc(st + 1, sv);
-    lds_read_wait();
+    tnw::frag_wait();
     if (st + 2 < nst) {
       retire(st + 2);
       lds_barrier();
@@ -1170,11 +1185,11 @@ extern "C" int sc_gemm_tn_bf16(const void* A, int64_t lda, const void* B, int64_
   SC_REQUIRE(M > 0 && N > 0 && K > 0, "sc_gemm_tn_bf16: empty shape M=%d N=%d K=%d", M, N, K);
   SC_REQUIRE(K % kBK == 0, "sc_gemm_tn_bf16: K=%d must be a multiple of 64 (zero-pad it)", K);
   SC_REQUIRE(N % kTN == 0, "sc_gemm_tn_bf16: N=%d must be a multiple of 256", N);
-  SC_REQUIRE(tile_m == 0 || tile_m == 1 || tile_m == 2 || tile_m == 3 || tile_m == 128 ||
+  SC_REQUIRE(tile_m == 0 || (SC_TNW_AB && tile_m >= 1 && tile_m <= 3) || tile_m == 128 ||
                  tile_m == 192 || tile_m == 256 || tile_m == 257,
-             "sc_gemm_tn_bf16: tile_m=%d must be 0 (default 192), 1 (256, one wave per SIMD), "
-             "2 / 3 (the same, 32-deep stages in a 5 / 4-slot ring), 128, 192, 256 or 257 (256, "
-             "ping-pong schedule)", tile_m);
+             "sc_gemm_tn_bf16: tile_m=%d must be 0 (default 192), 128, 192, 256 or 257 (256, "
+             "ping-pong schedule); 1 / 2 / 3 (one wave per SIMD) in SC_TNW_AB builds only",
+             tile_m);
   SC_REQUIRE(lda >= K && ldb >= K && ldc >= N && lda % 8 == 0 && ldb % 8 == 0 && ldc % 8 == 0,
              "sc_gemm_tn_bf16: leading dimensions must cover the rows in 16-byte pieces");
   SC_REQUIRE((uintptr_t)A % 16 == 0 && (uintptr_t)B % 16 == 0 && (uintptr_t)C % 16 == 0,
@@ -1194,6 +1209,7 @@ extern "C" int sc_gemm_tn_bf16(const void* A, int64_t lda, const void* B, int64_
   TnArgs a{(const __bf16*)A, (const __bf16*)B, (__bf16*)C, M, N, K, ntn, (int)tiles,
            (uint32_t)lda, (uint32_t)ldb, (uint32_t)ldc, (uint32_t)((int64_t)M * ldc * 2), gm};
   hipStream_t st = (hipStream_t)stream;
+#if SC_TNW_AB
   if (tile_m == 1) {
     launch_tnw(a, st);
     return launch_status("sc_gemm_tn_bf16");
@@ -1203,6 +1219,7 @@ extern "C" int sc_gemm_tn_bf16(const void* A, int64_t lda, const void* B, int64_
     else launch_tnw32<4, false>(a, TnLn{}, st);
     return launch_status("sc_gemm_tn_bf16");
   }
+#endif
   if (tile_m == 257) {
     launch_tnpp(a, st);
     return launch_status("sc_gemm_tn_bf16");

@@ -149,15 +149,7 @@ def _tn_check(c, ref):
                                       # the 256 x 256 ping-pong schedule (tile_m 257)
                                       (48000, 3584, 512, 257), (48000, 512, 3584, 257),
                                       (48000, 1024, 512, 257), (5000, 1024, 64, 257),
-                                      (300, 512, 192, 257), (7, 256, 128, 257),
-                                      # one wave per SIMD, 256 x 256 (tile_m 1)
-                                      (48000, 3584, 512, 1), (48000, 512, 3584, 1),
-                                      (48000, 1024, 512, 1), (5000, 1024, 64, 1),
-                                      (300, 512, 192, 1), (7, 256, 128, 1),
-                                      # the same with 32-deep stages in a 5- / 4-slot ring
-                                      (48000, 3584, 512, 2), (48000, 512, 3584, 2),
-                                      (48000, 1024, 512, 3), (5000, 1024, 64, 2),
-                                      (300, 512, 192, 3), (7, 256, 128, 2), (7, 256, 64, 3)])
+                                      (300, 512, 192, 257), (7, 256, 128, 257)])
 def test_tn_gemm_vs_fp32(M, N, K, tm):
     g = torch.Generator(device=DEV).manual_seed(M + N + K)
     a = torch.randn(M, K, device=DEV, generator=g).to(torch.bfloat16)
@@ -166,7 +158,7 @@ def test_tn_gemm_vs_fp32(M, N, K, tm):
     _tn_check(ops().gemm_tn(a, b, tm), _tn_ref(a, b))
 
 
-@pytest.mark.parametrize("tm", [1, 2, 3, 128, 192, 256, 257])
+@pytest.mark.parametrize("tm", [128, 192, 256, 257])
 def test_tn_gemm_structured_exact(tm):
     """Small-integer operands: every sum is exact in fp32 and |C| <= 256 is exact in bf16, so the
     result must equal the reference bitwise — pins the fragment maps, the swizzle and the
