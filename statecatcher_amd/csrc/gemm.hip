@@ -89,10 +89,15 @@ __device__ __forceinline__ i2v tr_read(uint32_t lds_byte) {
                                      (s4v __attribute__((address_space(3)))*)(size_t)lds_byte));
 }
 
-template <int TTI>
+// NU: 16-column fragments per wave along J (4: the 256-column tile; 2: a 128-column tile for
+// layer 0's J = 80 padded to 128, whose X rows are half an image row: the lanes past them fetch
+// a clamped duplicate chunk that no fragment reads)
+template <int TTI, int NU = 4>
 __global__ void __launch_bounds__(512) wgrad_kernel(WgradArgs a) {
   constexpr int TI = 32 * TTI;
+  constexpr int TJ = 64 * NU;
   constexpr int NCA = TI / 8;   // valid 16-byte chunks per A image row
+  constexpr int NCB = TJ / 8;   // ... per X image row
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];   // [2 stages][A, B]
   const int lane = threadIdx.x & 63;
   const int w = uniform(threadIdx.x >> 6);
@@ -105,7 +110,7 @@ __global__ void __launch_bounds__(512) wgrad_kernel(WgradArgs a) {
   const int lid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + bid / 8;
   const int split = lid / a.tiles, tile = lid % a.tiles;
   const int ti = tile / a.ntj, tj = tile % a.ntj;
-  const int i0 = ti * TI, j0 = tj * kTJ;
+  const int i0 = ti * TI, j0 = tj * TJ;
   const int nkb = a.L / kTL;
   const int kb0 = (int)((int64_t)split * nkb / a.S), kb1 = (int)((int64_t)(split + 1) * nkb / a.S);
 
@@ -119,7 +124,7 @@ __global__ void __launch_bounds__(512) wgrad_kernel(WgradArgs a) {
     const int row = 4 * w + 2 * q + (lane >> 5);
     const int c = (lane & 31) ^ (swz_f(row) << 1);   // logical chunk this lane fetches
     voA[q] = (uint32_t)(row * a.lda + i0 + 8 * min(c, NCA - 1)) * 2u;
-    voB[q] = (uint32_t)(row * a.ldb + j0 + 8 * c) * 2u;
+    voB[q] = (uint32_t)(row * a.ldb + j0 + 8 * min(c, NCB - 1)) * 2u;
   }
   constexpr int kHalf = 32 * kRowB;   // one half-image (16 KiB)
   const uint32_t lds0 = lds_addr(lds);
@@ -140,20 +145,20 @@ __global__ void __launch_bounds__(512) wgrad_kernel(WgradArgs a) {
   // transposed-read lane geometry: group g = lane >> 4 takes rows 8g .. 8g+7 of the 32-row
   // half-stage; within the group lane 4q+p addresses row q, columns 4p .. 4p+3
   const int g = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
-  f4v acc[TTI][4];
+  f4v acc[TTI][NU];
 #pragma unroll
   for (int t = 0; t < TTI; ++t)
 #pragma unroll
-    for (int u = 0; u < 4; ++u) acc[t][u] = f4v{0.f, 0.f, 0.f, 0.f};
+    for (int u = 0; u < NU; ++u) acc[t][u] = f4v{0.f, 0.f, 0.f, 0.f};
 
   const int nh = 2 * (kb1 - kb0);
-  // fragments of one half-stage: B (4 j-tiles) and A (TTI i-tiles), 8 bf16 each
-  auto load_frags = [&](int h, i4v (&bf)[4], i4v (&af)[TTI]) __attribute__((always_inline)) {
+  // fragments of one half-stage: B (NU j-tiles) and A (TTI i-tiles), 8 bf16 each
+  auto load_frags = [&](int h, i4v (&bf)[NU], i4v (&af)[TTI]) __attribute__((always_inline)) {
     const uint32_t ia = lds0 + (h % kSlots) * 2 * kHalf, ib = ia + kHalf;
     const int r0 = 8 * g + q4;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int col = wj * 64 + 16 * u + 4 * p4;
+    for (int u = 0; u < NU; ++u) {
+      const int col = wj * 16 * NU + 16 * u + 4 * p4;
       const uint32_t o = (uint32_t)((col & 7) ? 8 : 0);
       i2v lo = i2v{u, 1}, hi = lo;
       if (!(SC_GEMM_ABL & 4)) {
@@ -175,11 +180,11 @@ __global__ void __launch_bounds__(512) wgrad_kernel(WgradArgs a) {
     }
   };
   // (DMA pieces interleaved between the MFMAs measured slower: 203 vs 192 us)
-  auto mfmas = [&](const i4v (&bf)[4], const i4v (&af)[TTI]) __attribute__((always_inline)) {
+  auto mfmas = [&](const i4v (&bf)[NU], const i4v (&af)[TTI]) __attribute__((always_inline)) {
 #pragma unroll
     for (int t = 0; t < TTI; ++t)
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < NU; ++u) {
         if (SC_GEMM_ABL & 1)
           acc[t][u][0] += (float)af[t][u] * (float)bf[u][t & 3];
         else
@@ -200,7 +205,7 @@ __global__ void __launch_bounds__(512) wgrad_kernel(WgradArgs a) {
     else dma_wait();
   };
   for (int h = 0; h < kSlots && h < nh; ++h) stage(h);
-  i4v bfA[4], afA[TTI], bfB[4], afB[TTI];
+  i4v bfA[NU], afA[TTI], bfB[NU], afB[TTI];
   wait_younger(min(kSlots - 1, nh - 1));
   lds_barrier();
   if (nh > 0) load_frags(0, bfA, afA);
@@ -209,7 +214,7 @@ __global__ void __launch_bounds__(512) wgrad_kernel(WgradArgs a) {
   // the memory queues are full, and the other wave's MFMAs then keep the SIMD busy.  The
   // per-wave DMA counts are the same either way (vmcnt unchanged).
   const bool late = SC_GEMM_STAGGER && TTI <= 7 && w >= 4;   // (TTI = 8: no registers to spare)
-  auto iter = [&](int h, i4v (&bc)[4], i4v (&ac)[TTI], i4v (&bn)[4], i4v (&an)[TTI])
+  auto iter = [&](int h, i4v (&bc)[NU], i4v (&ac)[TTI], i4v (&bn)[NU], i4v (&an)[TTI])
       __attribute__((always_inline)) {
     if (h + 1 < nh) wait_younger(min(kSlots - 2, nh - 2 - h));
     if (!(SC_GEMM_ABL & 8)) lds_barrier();
@@ -220,13 +225,15 @@ __global__ void __launch_bounds__(512) wgrad_kernel(WgradArgs a) {
     mfmas(bc, ac);
     if (SC_GEMM_PRIO) __builtin_amdgcn_s_setprio(0);
 #if SC_GEMM_SGB
-    // interleave: one transposed read after each MFMA, then the remaining MFMAs
+    // interleave: one transposed read after each MFMA, then the remaining MFMAs (or reads)
+    constexpr int NMF = NU * TTI, NRD = 2 * (NU + TTI);
 #pragma unroll
-    for (int q = 0; q < 2 * (4 + TTI); ++q) {
+    for (int q = 0; q < (NMF < NRD ? NMF : NRD); ++q) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
       __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // DS read
     }
-    __builtin_amdgcn_sched_group_barrier(0x008, 4 * TTI - 2 * (4 + TTI), 0);
+    if constexpr (NMF > NRD) __builtin_amdgcn_sched_group_barrier(0x008, NMF - NRD, 0);
+    else if constexpr (NRD > NMF) __builtin_amdgcn_sched_group_barrier(0x100, NRD - NMF, 0);
 #endif
     if (late && st) stage(h + kSlots);
   };
@@ -241,11 +248,11 @@ __global__ void __launch_bounds__(512) wgrad_kernel(WgradArgs a) {
 #pragma unroll
   for (int t = 0; t < TTI; ++t)
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
+    for (int u = 0; u < NU; ++u)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int i = i0 + wi * (TI / 2) + 16 * t + 4 * g + r;
-        const int j = j0 + wj * 64 + 16 * u + (lane & 15);
+        const int j = j0 + wj * 16 * NU + 16 * u + (lane & 15);
         cs[(int64_t)i * a.J + j] = acc[t][u][r];
       }
 }
@@ -400,9 +407,9 @@ static void launch_wgrad32(const WgradArgs& a, hipStream_t st) {
 }
 #endif  // SC_GEMM_MF32
 
-template <int TTI>
+template <int TTI, int NU = 4>
 static void launch_wgrad(const WgradArgs& a, hipStream_t st) {
-  auto kern = wgrad_kernel<TTI>;
+  auto kern = wgrad_kernel<TTI, NU>;
   constexpr size_t lds = (size_t)kSlots * 2 * 32 * kRowB;   // kSlots x (dY, X) x 16 KiB
   static const bool ok = hipFuncSetAttribute((const void*)kern,
                                              hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -415,11 +422,22 @@ static void launch_wgrad(const WgradArgs& a, hipStream_t st) {
 
 using namespace sc;
 
+// J-tile of a shape: 256 columns, or 128 when J is an odd multiple of 128 (layer 0's 80 features
+// zero-padded to 128)
+static int wgrad_tj(int J) { return J % 256 == 0 ? 256 : 128; }
+// I-tile: 224 where (I / 224) tiles x the J tiles x the splits that fill 256 CUs come out whole
+static int wgrad_ti(int I, int J) {
+  const int tj = wgrad_tj(J);
+  const int per = tj == 256 ? 8 : 16;   // L-splits of the 224-row layout
+  return I % 224 == 0 && (I / 224) * (J / tj) * per == 256 ? 224 : 256;
+}
+
 extern "C" int sc_gemm_wgrad_splits(int L, int I, int J) {
-  if (L <= 0 || I <= 0 || J <= 0 || L % kTL || J % kTJ) return 0;
-  const int ti = I % 224 == 0 && (I / 224) * (J / kTJ) * 8 == 256 ? 224 : 256;
+  if (L <= 0 || I <= 0 || J <= 0 || L % kTL || J % 128) return 0;
+  const int tj = wgrad_tj(J);
+  const int ti = wgrad_ti(I, J);
   if (I % ti) return 0;
-  const int tiles = (I / ti) * (J / kTJ);
+  const int tiles = (I / ti) * (J / tj);
   // as many L-splits as fill the 256 CUs (any count: the split ranges are nkb * s / S, so they
   // may differ by one K-block), each of at least 8 K-blocks.  Powers of two left C4's shapes
   // at 56-84% of the CUs (out_proj 9 tiles x 16, FFN 48 x 4 / 24 x 8, q|k|v|o head 27 x 8).
@@ -433,26 +451,32 @@ extern "C" int sc_gemm_wgrad_bf16(const void* A, int64_t lda, const void* B, int
   clear_error();
   SC_REQUIRE(A && B && part, "sc_gemm_wgrad_bf16: null pointer");
   SC_REQUIRE(L > 0 && L % kTL == 0, "sc_gemm_wgrad_bf16: L=%d must be a positive multiple of 64", L);
-  SC_REQUIRE(J > 0 && J % kTJ == 0, "sc_gemm_wgrad_bf16: J=%d must be a multiple of 256", J);
-  SC_REQUIRE(I > 0 && (I % 256 == 0 || (I % 224 == 0 && (I / 224) * (J / kTJ) * 8 == 256)),
-             "sc_gemm_wgrad_bf16: I=%d must be a multiple of 256, or of 224 when (I/224)*(J/256)*8 "
-             "== 256 (use sc_gemm_wgrad_splits to gate)", I);
+  SC_REQUIRE(J > 0 && J % 128 == 0, "sc_gemm_wgrad_bf16: J=%d must be a multiple of 128", J);
+  SC_REQUIRE(I > 0 && I % wgrad_ti(I, J) == 0,
+             "sc_gemm_wgrad_bf16: I=%d must be a multiple of 256, or of 224 at the 256-workgroup "
+             "layouts (use sc_gemm_wgrad_splits to gate)", I);
   SC_REQUIRE(lda >= I && ldb >= J && lda % 8 == 0 && ldb % 8 == 0,
              "sc_gemm_wgrad_bf16: leading dimensions must cover the rows in 16-byte pieces");
   SC_REQUIRE((uintptr_t)A % 16 == 0 && (uintptr_t)B % 16 == 0, "sc_gemm_wgrad_bf16: unaligned operand");
   SC_REQUIRE((int64_t)kTL * lda * 2 < (1ll << 31) && (int64_t)kTL * ldb * 2 < (1ll << 31),
              "sc_gemm_wgrad_bf16: row pitch too large");
-  const int ti = I % 224 == 0 && (I / 224) * (J / kTJ) * 8 == 256 ? 224 : 256;
+  const int ti = wgrad_ti(I, J), tj = wgrad_tj(J);
   SC_REQUIRE(I % ti == 0, "sc_gemm_wgrad_bf16: I=%d not a multiple of the %d-row tile", I, ti);
-  WgradArgs a{(const __bf16*)A, (const __bf16*)B, part, L, I, J, S, J / kTJ,
-              (I / ti) * (J / kTJ), lda, ldb};
+  WgradArgs a{(const __bf16*)A, (const __bf16*)B, part, L, I, J, S, J / tj,
+              (I / ti) * (J / tj), lda, ldb};
   SC_REQUIRE(S >= 1 && S <= L / kTL, "sc_gemm_wgrad_bf16: S=%d outside [1, L/64]", S);
   hipStream_t st = (hipStream_t)stream;
 #if SC_GEMM_MF32
   if (ti == 224) launch_wgrad32(a, st);
   else
 #endif
-  if (ti == 224) launch_wgrad<7>(a, st);
-  else launch_wgrad<8>(a, st);
+  if (tj == 128) {
+    if (ti == 224) launch_wgrad<7, 2>(a, st);
+    else launch_wgrad<8, 2>(a, st);
+  } else if (ti == 224) {
+    launch_wgrad<7>(a, st);
+  } else {
+    launch_wgrad<8>(a, st);
+  }
   return launch_status("sc_gemm_wgrad_bf16");
 }

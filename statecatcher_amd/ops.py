@@ -511,9 +511,14 @@ class LucyCellFn(torch.autograd.Function):
         if len(res) > 5:
             split_sink.append(res[5])
         if need:
-            ctx.save_for_backward(xc, wc, wt, gates, ckpt, bias)
+            # layer 0 (Din = 80): the weight gradient runs on the MFMA kernel's 128-column tile over
+            # the zero-padded copy (sc_gemm_wgrad_bf16, J = 128), and dW keeps the first Din columns
+            xw = xg if (xg is not xc and xg.shape[1] % 128 == 0 and xg.shape[1] % 256
+                        and ctx.needs_input_grad[1]) else xc
+            ctx.save_for_backward(xw, wc, wt, gates, ckpt, bias)
             ctx.dtypes = (x2d.dtype, w.dtype, h0.dtype, s0.dtype)
             ctx.blocked = blocked
+            ctx.din = Din
         return out, s_out, h_out
 
     @staticmethod
@@ -554,10 +559,15 @@ class LucyCellFn(torch.autograd.Function):
         if part is not None:
             main.wait_stream(side)
             part.record_stream(main)
-            dw = wgrad_slab_sum(part, bd).to(wdt)
+            dw = wgrad_slab_sum(part, bd)
+            if dw.shape[1] != ctx.din:   # (the zero-padded columns of layer 0's copy)
+                dw = dw[:, :ctx.din].contiguous()
+            dw = dw.to(wdt)
         elif ctx.needs_input_grad[1]:
             with _timed("gate_gemm_wgrad", dg2, 0):
                 dw = wgrad_splitk(dg2, xc, blocked_d=bd)
+            if dw.shape[1] != ctx.din:   # (the zero-padded columns of layer 0's copy)
+                dw = dw[:, :ctx.din].contiguous()
             dw = dw.to(wdt)
         db = colsum(dbias.view(dbias.shape[0], -1)).to(wdt) if dbias is not None else None
         return dx, dw, db, dh0.to(hdt), ds0.to(sdt), None, None, None, None, None, None

@@ -26,7 +26,11 @@ def _ref(dy, x):
                                    (1024, 768, 768),
                                    (14336, 768, 768),    # C4 out_proj: 9 tiles x 28 splits
                                    (4096, 4096, 768),    # C4 FFN up: 48 x 5, uneven ranges
-                                   (6400, 768, 2048)])   # C4 FFN down: 24 x 10
+                                   (6400, 768, 2048),    # C4 FFN down: 24 x 10
+                                   # 128-column tiles (round 6): layer 0's 80 features padded
+                                   (48000, 3584, 128),   # to 128 (224-row tiles, 16 splits)
+                                   (4096, 512, 384),     # 256-row tiles, 3 column tiles
+                                   (1024, 1024, 128)])
 def test_wgrad_mfma_vs_fp32(L, I, J):
     from statecatcher_amd import _lib
     assert _lib.load().sc_gemm_wgrad_splits(L, I, J) > 0
@@ -53,12 +57,16 @@ def test_wgrad_splits_fill_the_chip():
     assert lib.sc_gemm_wgrad_splits(48000, 768, 2048) == 10    # 24 tiles
     assert lib.sc_gemm_wgrad_splits(1024, 768, 768) == 2       # 16 K-blocks: 8 per split
     assert lib.sc_gemm_wgrad_splits(512, 4096, 4096) == 1
+    assert lib.sc_gemm_wgrad_splits(48000, 3584, 128) == 16   # layer 0: 16 tiles of 224 x 128
+    assert lib.sc_gemm_wgrad_splits(48000, 3584, 80) == 0     # (the caller pads to 128)
 
 
-def test_wgrad_mfma_structured_exact():
+@pytest.mark.parametrize("J", [256, 128])
+def test_wgrad_mfma_structured_exact(J):
     """Integer-valued operands: every partial sum is exact in fp32, so the result must be bitwise
-    equal — pins the fragment maps (i, j, L order) independent of rounding."""
-    L, I, J = 2048, 512, 256
+    equal — pins the fragment maps (i, j, L order) independent of rounding, for the 256- and the
+    128-column tile."""
+    L, I = 2048, 512
     li = torch.arange(L, device=DEV)
     dy = ((li[:, None] * 3 + torch.arange(I, device=DEV)[None, :] * 7) % 5 - 2).to(torch.bfloat16)
     x = ((li[:, None] * 5 + torch.arange(J, device=DEV)[None, :] * 11) % 7 - 3).to(torch.bfloat16)
@@ -266,3 +274,39 @@ def test_cell_side_stream_wgrad_bitwise(din, monkeypatch):
 
     for a, c in zip(run(True), run(False)):
         assert torch.equal(a, c)
+
+
+def test_layer0_cell_weight_gradient_on_the_128_column_tile(monkeypatch):
+    """Layer 0 (Din = 80): LucyCellFn's weight gradient runs on the MFMA kernel's 128-column tile
+    over the zero-padded bf16 copy of x and keeps dW's first 80 columns (round 6; the library's
+    MT80x256 kernel ran at 12% MFMA).  Against the library path on the same dgates (wgrad_mfma
+    forced off): the same fp32 sums in another order, 1e-5 of the largest |dW|; the bias and
+    state gradients are bitwise the same (they do not touch the weight gradient)."""
+    o = ops()
+    g = torch.Generator(device="cuda").manual_seed(5)
+    B, T, D, din = 2, 1600, 512, 80   # B T = 3200 rows, a multiple of 64
+    x = torch.randn(B, T, din, device="cuda", generator=g)
+    w = torch.randn(7 * D, din, device="cuda", generator=g) * 0.05
+    b = torch.randn(7 * D, device="cuda", generator=g) * 0.1
+    h0 = torch.zeros(B, D, device="cuda")
+    s0 = torch.zeros(B, D, device="cuda")
+    dout = torch.randn(B, T, D, device="cuda", generator=g).to(torch.bfloat16)
+    seen = []
+    orig = o.wgrad_mfma
+
+    def run(mfma):
+        def wg(dy, xx, blocked_d=0):
+            seen.append(tuple(xx.shape))
+            return orig(dy, xx, blocked_d) if mfma else None
+        monkeypatch.setattr(o, "wgrad_mfma", wg)
+        leaves = [t.clone().requires_grad_(True) for t in (w, b)]
+        out, _, _ = o.lucy_cell(x, leaves[0], leaves[1], h0, s0, cdt=torch.bfloat16)
+        out.backward(dout)
+        torch.cuda.synchronize()
+        return [t.grad for t in leaves]
+    gm, gl = run(True), run(False)
+    assert seen[0] == (B * T, 128)   # the padded copy reached the kernel
+    assert gm[0].shape == (7 * D, din) and gm[0].is_contiguous()
+    err = (gm[0] - gl[0]).abs().max().item() / gl[0].abs().max().item()
+    assert err <= 1e-5, err
+    assert torch.equal(gm[1], gl[1])
