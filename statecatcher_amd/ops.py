@@ -274,6 +274,10 @@ def _side_stream(dev):
     return s
 
 
+# SC_WGRAD128=0 (A/B only): layer 0's weight gradient back on the library GEMM (its 80 features
+# are otherwise zero-padded to the MFMA kernel's 128-column tile, round 6)
+USE_WGRAD128 = os.environ.get("SC_WGRAD128", "1") != "0"
+
 # SC_TN=0 routes the projection GEMMs back to the library (A/B timing in tools/ only)
 USE_TN = os.environ.get("SC_TN", "1") != "0"
 
@@ -513,8 +517,8 @@ class LucyCellFn(torch.autograd.Function):
         if need:
             # layer 0 (Din = 80): the weight gradient runs on the MFMA kernel's 128-column tile over
             # the zero-padded copy (sc_gemm_wgrad_bf16, J = 128), and dW keeps the first Din columns
-            xw = xg if (xg is not xc and xg.shape[1] % 128 == 0 and xg.shape[1] % 256
-                        and ctx.needs_input_grad[1]) else xc
+            xw = xg if (USE_WGRAD128 and xg is not xc and xg.shape[1] % 128 == 0
+                        and xg.shape[1] % 256 and ctx.needs_input_grad[1]) else xc
             ctx.save_for_backward(xw, wc, wt, gates, ckpt, bias)
             ctx.dtypes = (x2d.dtype, w.dtype, h0.dtype, s0.dtype)
             ctx.blocked = blocked

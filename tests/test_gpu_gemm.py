@@ -279,9 +279,10 @@ def test_cell_side_stream_wgrad_bitwise(din, monkeypatch):
 def test_layer0_cell_weight_gradient_on_the_128_column_tile(monkeypatch):
     """Layer 0 (Din = 80): LucyCellFn's weight gradient runs on the MFMA kernel's 128-column tile
     over the zero-padded bf16 copy of x and keeps dW's first 80 columns (round 6; the library's
-    MT80x256 kernel ran at 12% MFMA).  Against the library path on the same dgates (wgrad_mfma
-    forced off): the same fp32 sums in another order, 1e-5 of the largest |dW|; the bias and
-    state gradients are bitwise the same (they do not touch the weight gradient)."""
+    MT80x256 kernel ran at 12% MFMA).  Against fp32 torch on the dgates and x the kernel received:
+    1e-5 of the largest |dW| (fp32 summation order).  The library path it replaces (wgrad_mfma
+    forced off) rounds its split-K partials to bf16 and lands ~2.6e-3 away (measured); the bias
+    gradient is bitwise the same either way (it does not touch the weight gradient)."""
     o = ops()
     g = torch.Generator(device="cuda").manual_seed(5)
     B, T, D, din = 2, 1600, 512, 80   # B T = 3200 rows, a multiple of 64
@@ -296,7 +297,7 @@ def test_layer0_cell_weight_gradient_on_the_128_column_tile(monkeypatch):
 
     def run(mfma):
         def wg(dy, xx, blocked_d=0):
-            seen.append(tuple(xx.shape))
+            seen.append((dy.detach().clone(), xx.detach().clone(), blocked_d))
             return orig(dy, xx, blocked_d) if mfma else None
         monkeypatch.setattr(o, "wgrad_mfma", wg)
         leaves = [t.clone().requires_grad_(True) for t in (w, b)]
@@ -305,8 +306,15 @@ def test_layer0_cell_weight_gradient_on_the_128_column_tile(monkeypatch):
         torch.cuda.synchronize()
         return [t.grad for t in leaves]
     gm, gl = run(True), run(False)
-    assert seen[0] == (B * T, 128)   # the padded copy reached the kernel
+    dy, xx, bd = seen[0]
+    assert tuple(xx.shape) == (B * T, 128) and bool((xx[:, din:] == 0).all())   # padded copy
+    ref = _ref(dy, xx)
+    if bd:   # dy's columns step-blocked: the reference order of dW's rows
+        ref = ops().step_blocked_rows(ref, bd, inverse=True)
+    ref = ref[:, :din]
     assert gm[0].shape == (7 * D, din) and gm[0].is_contiguous()
-    err = (gm[0] - gl[0]).abs().max().item() / gl[0].abs().max().item()
+    err = (gm[0] - ref).abs().max().item() / ref.abs().max().item()
+    err_lib = (gl[0] - ref).abs().max().item() / ref.abs().max().item()
+    print(f"layer-0 dW vs fp32: MFMA 128-column tile {err:.2e}, library path {err_lib:.2e}")
     assert err <= 1e-5, err
     assert torch.equal(gm[1], gl[1])
