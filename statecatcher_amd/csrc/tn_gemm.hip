@@ -53,6 +53,12 @@ typedef int i4v __attribute__((ext_vector_type(4)));
 // SC_TNW_AB: also build the plain one-wave-per-SIMD kernels (tile_m 1 / 2 / 3; A/B only, measured
 // slower than the library: profiles/r6_tnw.md).  The LayerNorm-fold instance tnw32_kernel<4, true>
 // (sc_gemm_tn_ln_bf16, SC_LN_FOLD=2) is always built.
+#ifndef SC_TNW_FENCE
+#define SC_TNW_FENCE 1
+#endif
+#ifndef SC_TNW_IL
+#define SC_TNW_IL 0
+#endif
 #ifndef SC_TNW_AB
 #define SC_TNW_AB 0
 #endif
@@ -742,7 +748,23 @@ constexpr int kSlotB = 64 * 1024;   // one K-tile: A image 32 KiB + B image 32 K
 // wait the pass still puts an lgkmcnt(0) after the first MFMA of the k-step whose next fragments
 // were just issued, so each k-step exposes the LDS read latency; fragment reads issued from
 // inline asm instead spill 40-48 VGPRs into the loop.)
-__device__ __forceinline__ void frag_wait() { __builtin_amdgcn_s_waitcnt(0xC07F); }
+__device__ __forceinline__ void frag_wait() {
+  if (SC_TNW_FENCE) __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  if (SC_TNW_FENCE) __builtin_amdgcn_sched_barrier(0);
+}
+// SC_TNW_IL: the k-step's 16 fragment reads (+ LN's 4 statistic reads) one at a time between
+// groups of 3 of the current stage's MFMAs, instead of all before the first MFMA
+template <int NR>
+__device__ __forceinline__ void interleave() {
+  if constexpr (SC_TNW_IL) {
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // DS read
+      __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);   // MFMA
+    }
+  }
+}
 struct Frag { i4v v[8]; };          // 8 fragments of one operand for one k-step
 }  // namespace tnw
 
@@ -1049,7 +1071,9 @@ __global__ void __launch_bounds__(256, 1) tnw32_kernel(TnArgs a, TnLn ln) {
   stat_acc(0, sv);
   // stage s is read after the barrier that retires it and multiplied one barrier later; at that
   // barrier every read of stage s - 1 is done, so its slot takes stage s - 1 + NS
-  for (int st = 0; st < nst; st += 2) {   // nst = K / 32 is even
+  // (the reads of the next stage and the MFMAs of the current one stay in one basic block, so
+  // that SC_TNW_IL can interleave them: the last pair is peeled instead of guarded)
+  for (int st = 0; st + 2 < nst; st += 2) {   // nst = K / 32 is even
     tnw::frag_wait();
     retire(st + 1);
     lds_barrier();
@@ -1057,17 +1081,29 @@ __global__ void __launch_bounds__(256, 1) tnw32_kernel(TnArgs a, TnLn ln) {
     read(st + 1, Y, Yw);
     stat_read(st + 1, sv);
     mfmas(X, Xw);
+    tnw::interleave<LN ? 20 : 16>();
     stat_acc(st + 1, sv);
     tnw::frag_wait();
-    if (st + 2 < nst) {
-      retire(st + 2);
-      lds_barrier();
-      if (st + 1 + NS < nst && !(SC_TN_ABL & 2)) dma(st + 1 + NS);
-      read(st + 2, X, Xw);
-      stat_read(st + 2, sv);
-    }
+    retire(st + 2);
+    lds_barrier();
+    if (st + 1 + NS < nst && !(SC_TN_ABL & 2)) dma(st + 1 + NS);
+    read(st + 2, X, Xw);
+    stat_read(st + 2, sv);
     mfmas(Y, Yw);
-    if (st + 2 < nst) stat_acc(st + 2, sv);
+    tnw::interleave<LN ? 20 : 16>();
+    stat_acc(st + 2, sv);
+  }
+  {   // the last pair of stages (nst - 2, nst - 1): nothing left to DMA
+    tnw::frag_wait();
+    retire(nst - 1);
+    lds_barrier();
+    read(nst - 1, Y, Yw);
+    stat_read(nst - 1, sv);
+    mfmas(X, Xw);
+    tnw::interleave<LN ? 20 : 16>();
+    stat_acc(nst - 1, sv);
+    tnw::frag_wait();
+    mfmas(Y, Yw);
   }
   if (SC_TN_ABL & 4) {
 #pragma unroll
