@@ -274,9 +274,10 @@ def _side_stream(dev):
     return s
 
 
-# SC_WGRAD128=0 (A/B only): layer 0's weight gradient back on the library GEMM (its 80 features
-# are otherwise zero-padded to the MFMA kernel's 128-column tile, round 6)
-USE_WGRAD128 = os.environ.get("SC_WGRAD128", "1") != "0"
+# SC_WGRAD128=1: layer 0's weight gradient on the MFMA kernel's 128-column tile over a
+# zero-padded copy of its 80 features (fp32 dW, 4.6e-7 of fp32 against the library's bf16 dW at
+# 2.6e-3).  Opt-in: same-box A/B 5.200-5.265 ms/step on vs 5.178-5.192 off (profiles/r6f_wgrad128_ab.md)
+USE_WGRAD128 = os.environ.get("SC_WGRAD128", "0") != "0"
 
 # SC_TN=0 routes the projection GEMMs back to the library (A/B timing in tools/ only)
 USE_TN = os.environ.get("SC_TN", "1") != "0"

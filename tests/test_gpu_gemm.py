@@ -277,13 +277,14 @@ def test_cell_side_stream_wgrad_bitwise(din, monkeypatch):
 
 
 def test_layer0_cell_weight_gradient_on_the_128_column_tile(monkeypatch):
-    """Layer 0 (Din = 80): LucyCellFn's weight gradient runs on the MFMA kernel's 128-column tile
+    """Layer 0 (Din = 80), SC_WGRAD128=1: LucyCellFn's weight gradient on the MFMA kernel's 128-column tile
     over the zero-padded bf16 copy of x and keeps dW's first 80 columns (round 6; the library's
     MT80x256 kernel ran at 12% MFMA).  Against fp32 torch on the dgates and x the kernel received:
     1e-5 of the largest |dW| (fp32 summation order).  The library path it replaces (wgrad_mfma
     forced off) rounds its split-K partials to bf16 and lands ~2.6e-3 away (measured); the bias
     gradient is bitwise the same either way (it does not touch the weight gradient)."""
     o = ops()
+    monkeypatch.setattr(o, "USE_WGRAD128", True)   # (opt-in: SC_WGRAD128=1)
     g = torch.Generator(device="cuda").manual_seed(5)
     B, T, D, din = 2, 1600, 512, 80   # B T = 3200 rows, a multiple of 64
     x = torch.randn(B, T, din, device="cuda", generator=g)
