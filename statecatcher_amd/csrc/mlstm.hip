@@ -34,7 +34,9 @@
 // SC_ML_ABL: timing ablations (tools/mlstm_abl.sh; results are garbage).  Forward walk: 1 no S
 // MFMAs, 2 no H MFMAs, 4 no state-update MFMAs, 8 no global stores, 16 no LDS fill.  Backward
 // walk: 32 no A/dA phase, 64 no dq phase, 128 no dk/dv phase, 256 no dC update, 512 no loads,
-// 1024 no dq role (its workgroups exit), 2048 no walk role.
+// 1024 no dq role (its workgroups exit), 2048 no walk role; per-operand loads of the backward
+// (both roles, for FETCH_SIZE differences): 4096 q, 8192 k, 16384 v, 32768 dh, 65536 h,
+// 131072 the dq role's state image.
 #ifndef SC_ML_ABL
 #define SC_ML_ABL 0
 #endif
@@ -851,8 +853,8 @@ __global__ void __launch_bounds__(512, 1) mlstm_bw_walk(MArgs a) {
 #pragma unroll
     for (int u = 0; u < UH; ++u) {
       if (!ML_ABL(512)) {
-        rd[u] = *(const u32x4*)(dh + (tid & 7) * 8 + 64 * u);
-        rh[u] = *(const u32x4*)(h + (tid & 7) * 8 + 64 * u);
+        if (!ML_ABL(32768)) rd[u] = *(const u32x4*)(dh + (tid & 7) * 8 + 64 * u);
+        if (!ML_ABL(65536)) rh[u] = *(const u32x4*)(h + (tid & 7) * 8 + 64 * u);
       }
     }
     m_t = a.mrow[ro];
@@ -871,14 +873,14 @@ __global__ void __launch_bounds__(512, 1) mlstm_bw_walk(MArgs a) {
     for (int u = 0; u < UQ; ++u) {
       const int e = tid + 512 * u, r = e / (DQ / 8), c = (e % (DQ / 8)) * 8;
       if (e < NQ8 && !ML_ABL(512)) {
-        rq[u] = *(const u32x4*)(Qg + (tb + r) * a.qt + c);
-        rk[u] = *(const u32x4*)(Kg + (tb + r) * a.qt + c);
+        if (!ML_ABL(4096)) rq[u] = *(const u32x4*)(Qg + (tb + r) * a.qt + c);
+        if (!ML_ABL(8192)) rk[u] = *(const u32x4*)(Kg + (tb + r) * a.qt + c);
       }
     }
 #pragma unroll
     for (int u = 0; u < UV; ++u) {
       const int e = tid + 512 * u, r = e / (DV / 8), c = (e % (DV / 8)) * 8;
-      if (e < NV8 && !ML_ABL(512)) rv[u] = *(const u32x4*)(Vg + (tb + r) * a.vt + c);
+      if (e < NV8 && !ML_ABL(512) && !ML_ABL(16384)) rv[u] = *(const u32x4*)(Vg + (tb + r) * a.vt + c);
     }
   };
   // gate quantities (every wave, lane = step) and the Q / K (/ Qr) / V fill; returns g = b_{L-1}
@@ -1032,7 +1034,7 @@ __global__ void __launch_bounds__(512, 1) mlstm_bw_walk(MArgs a) {
 #pragma unroll
       for (int u = 0; u < UC; ++u) {
         const int e = tid + 512 * u;
-        if (e < NC8 && !ML_ABL(512)) rc[u] = *(const u32x4*)(Ck + 8 * e);
+        if (e < NC8 && !ML_ABL(512) && !ML_ABL(131072)) rc[u] = *(const u32x4*)(Ck + 8 * e);
       }
       const float n_k = tid < DQ ? a.ns[((int64_t)bh * (a.nc + 1) + k) * DQ + tid] : 0.0f;
       load_qkv(k);
