@@ -36,7 +36,7 @@
 // walk: 32 no A/dA phase, 64 no dq phase, 128 no dk/dv phase, 256 no dC update, 512 no loads,
 // 1024 no dq role (its workgroups exit), 2048 no walk role; per-operand loads of the backward
 // (both roles, for FETCH_SIZE differences): 4096 q, 8192 k, 16384 v, 32768 dh, 65536 h,
-// 131072 the dq role's state image.
+// 131072 the dq role's state image; 262144 no dq / dk / dv stores.
 #ifndef SC_ML_ABL
 #define SC_ML_ABL 0
 #endif
@@ -1091,7 +1091,8 @@ __global__ void __launch_bounds__(512, 1) mlstm_bw_walk(MArgs a) {
           for (int r = 0; r < 4; ++r) {
             const int tt = 16 * tr + 4 * (lane >> 4) + r;
             const float v = d4[c][r] + rowf[tt] * (e4[c][r] + dden[tt] * nki);
-            dQg[(t0 + tt) * a.qt + i] = out16<DT, IO>(v * inv);
+            if (!ML_ABL(262144))
+              dQg[(t0 + tt) * a.qt + i] = out16<DT, IO>(v * inv);
             qd[r] = sum16(v * (float)Qs[tt * LQ + i]);
           }
           if ((lane & 15) == 0) {
@@ -1219,7 +1220,8 @@ __global__ void __launch_bounds__(512, 1) mlstm_bw_walk(MArgs a) {
           for (int r = 0; r < 4; ++r) {
             const int s = 16 * sr + 4 * (lane >> 4) + r;
             const float v = d4[c][r] + es[s] * (e4[c][r] + dni);
-            dKg[(t0 + s) * a.qt + i] = out16<DT, IO>(v * inv);
+            if (!ML_ABL(262144))
+              dKg[(t0 + s) * a.qt + i] = out16<DT, IO>(v * inv);
             kd[r] = sum16(v * (float)Ks[s * LQ + i]);
           }
           if ((lane & 15) == 0) {
@@ -1256,7 +1258,8 @@ __global__ void __launch_bounds__(512, 1) mlstm_bw_walk(MArgs a) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int s = 16 * sr + 4 * (lane >> 4) + r;
-            dVg[(t0 + s) * a.vt + j] = out16<DT, IO>((d4[c][r] + es[s] * e4[c][r]) * inv);
+            if (!ML_ABL(262144))
+              dVg[(t0 + s) * a.vt + j] = out16<DT, IO>((d4[c][r] + es[s] * e4[c][r]) * inv);
           }
         }
       }
