@@ -40,6 +40,9 @@
 #ifndef SC_ML_ABL
 #define SC_ML_ABL 0
 #endif
+#ifndef SC_ML_XCDH
+#define SC_ML_XCDH 1
+#endif
 #define ML_ABL(b) ((SC_ML_ABL & (b)) != 0)
 
 namespace sc {
@@ -828,7 +831,17 @@ __global__ void __launch_bounds__(512, 1) mlstm_bw_walk(MArgs a) {
   constexpr int UQ = (NQ8 + 511) / 512, UV = (NV8 + 511) / 512, UC = (NC8 + 511) / 512;
   constexpr int UH = DV / 64;   // dh / h pieces per thread (8 threads per row)
   const bool walk = (int)blockIdx.x < a.BH;
-  const int bh = walk ? blockIdx.x : blockIdx.x - a.BH;
+  // sequence of this workgroup.  SC_ML_XCDH: the NH heads of one batch row on one XCD (bids go
+  // round-robin over the 8 XCDs): in the xLSTM layer's fused gradient [B][T][N] the heads' dq /
+  // dk / dv segments of a time step share cache lines (192 / 384-byte segments at a 4,624-byte
+  // row pitch), and lines that heads on different XCDs write in parts reach HBM as partial lines
+  // the L2s must first read (90.9 MB of FETCH per launch at C4, r6m2).  Both roles keep sharing
+  // their XCD (workgroups i and BH + i, BH % 8 == 0).
+  int bh = walk ? blockIdx.x : blockIdx.x - a.BH;
+  if (SC_ML_XCDH && a.NH > 1 && a.BH % 8 == 0 && (a.BH / 8) % a.NH == 0) {
+    const int x = bh % 8, kk = bh / 8;
+    bh = (x + 8 * (kk / a.NH)) * a.NH + kk % a.NH;
+  }
   const T* Qg = (const T*)a.q + qrow(a, bh, 0);
   const T* Kg = (const T*)a.k + qrow(a, bh, 0);
   const T* Vg = (const T*)a.v + vrow(a, bh, 0);
