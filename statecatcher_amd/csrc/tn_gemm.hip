@@ -1074,9 +1074,28 @@ __global__ void __launch_bounds__(256, 1) tnw32_kernel(TnArgs a, TnLn ln) {
   stat_acc(0, sv);
   // stage s is read after the barrier that retires it and multiplied one barrier later; at that
   // barrier every read of stage s - 1 is done, so its slot takes stage s - 1 + NS
-  // (the reads of the next stage and the MFMAs of the current one stay in one basic block, so
-  // that SC_TNW_IL can interleave them: the last pair is peeled instead of guarded)
-  for (int st = 0; st + 2 < nst; st += 2) {   // nst = K / 32 is even
+  // LN: the reads of the next stage and the MFMAs of the current one stay in one basic block, so
+  // that SC_TNW_IL can interleave them: the last pair is peeled instead of guarded.  Plain: the
+  // guarded loop (the peeled form spills in the plain instances)
+  if constexpr (!LN) {
+    for (int st = 0; st < nst; st += 2) {
+      tnw::frag_wait();
+      retire(st + 1);
+      lds_barrier();
+      if (st + NS < nst && !(SC_TN_ABL & 2)) dma(st + NS);
+      read(st + 1, Y, Yw);
+      mfmas(X, Xw);
+      tnw::frag_wait();
+      if (st + 2 < nst) {
+        retire(st + 2);
+        lds_barrier();
+        if (st + 1 + NS < nst && !(SC_TN_ABL & 2)) dma(st + 1 + NS);
+        read(st + 2, X, Xw);
+      }
+      mfmas(Y, Yw);
+    }
+  }
+  for (int st = 0; LN && st + 2 < nst; st += 2) {   // nst = K / 32 is even
     tnw::frag_wait();
     retire(st + 1);
     lds_barrier();
@@ -1096,7 +1115,7 @@ __global__ void __launch_bounds__(256, 1) tnw32_kernel(TnArgs a, TnLn ln) {
     tnw::interleave<LN ? 20 : 16>();
     stat_acc(st + 2, sv);
   }
-  {   // the last pair of stages (nst - 2, nst - 1): nothing left to DMA
+  if constexpr (LN) {   // the last pair of stages (nst - 2, nst - 1): nothing left to DMA
     tnw::frag_wait();
     retire(nst - 1);
     lds_barrier();
