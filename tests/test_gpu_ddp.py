@@ -308,7 +308,7 @@ def test_two_ranks_bitwise_equal_to_split_batch_single_process(workload, tmp_pat
     assert any(not torch.equal(a, b) for a, b in zip(r0["params"], r0["init"]))
 
 
-@pytest.mark.parametrize("workload", ["c3", "c5"])
+@pytest.mark.parametrize("workload", ["c3", "c4", "c5"])
 def test_graph_replay_ddp_two_ranks_bitwise_equal_to_eager_ddp(workload, tmp_path):
     """Data-parallel training under HIP-graph replay (verdict r5 item 8): two rank processes on
     cuda:0 over gloo, each capturing its 4 segment positions (graphs.GraphedSegments on a trainer
